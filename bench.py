@@ -1,0 +1,251 @@
+"""Benchmark: depth maps/s of MVSNet.forward on the fused MI355X cost-volume path + warp-kernel HBM GB/s.
+
+Workload (BASELINE.json configs[1]): 3-view DTU geometry, 640x512 images (160x128 features), D=192,
+batch 4 per GPU, synthetic N(0,1) images already resident in HBM, real DTU scan-1 cameras
+(tests/golden/dtu_scan1_cameras.npz), d_min=425, d_int=1, D_SCALE=25, random-init weights of the
+reference architecture (tests/golden/weights.py formula), fp32, BN eval mode, inference (no_grad).
+
+A step = one full MVSNet.forward over one batch (feature encoder -> fused warp+variance HIP kernel ->
+3-D regulariser (MIOpen) -> HIP soft-argmin -> refinement).  value = depth maps/s over all ranks.
+
+Multi-GPU (torchrun, one process per GPU): --mode samples (default) shards SAMPLES across ranks --
+every rank runs its own batch, no collective in the data path, "scaling": "weak".  --mode dshard
+runs BASELINE configs[3]: D=256 planes split across ranks, each rank's fused kernel writes its
+D-slab, an RCCL all-gather reassembles the full cost volume, the sample's owner runs the regulariser.
+
+Also reported (one JSON line, rank 0):
+  roofline      the fused kernel (cost_volume_kernel): algorithmic bytes per launch
+                (4*B*V*C*h*w features read once + 4*B*C*D*h*w cost volume written once) / average
+                launch time measured with HIP events on the launch stream, vs 8 TB/s HBM peak;
+                traffic = PMC HBM bytes from profiles/ (rocprofv3 --pmc, FETCH_SIZE x2 on gfx950)
+  cpu_baseline  the oracle (oracle/mvs_oracle.py: the reference's op sequence in torch CPU,
+                per-plane warp loop with torch.cat growth) on ONE sample of the same workload
+  hot_path      cost volumes/s of the fused kernel alone
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for sub in ("deep-multiview-depth-estimation_amd", os.path.join("tests", "golden")):
+    sys.path.insert(0, os.path.join(REPO, sub))
+
+from cameras import camera_batch, depth_range  # noqa: E402
+from weights import deterministic_state_dict  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mode", choices=("samples", "dshard"), default="samples")
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--views", type=int, default=3)
+    ap.add_argument("--planes", type=int, default=None)
+    ap.add_argument("--height", type=int, default=512)
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-planes", type=int, default=None, help="planes for the CPU sample")
+    ap.add_argument("--kernel-only", action="store_true", help="skip the end-to-end forward")
+    return ap.parse_args()
+
+
+def init_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, torch.device("cuda", local)
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world, device):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
+def make_inputs(B, V, H, W, seed, device):
+    h, w = H // 4, W // 4
+    K, R, T = camera_batch(B, V, h, w, first_sample=seed)
+    d_min, d_int = depth_range(B)
+    g = torch.Generator(device="cpu").manual_seed(1000 + seed)
+    img = torch.randn(B * V, 3, H, W, generator=g).to(device)
+    return img, K.to(device), R.to(device), T.to(device), d_min.to(device), d_int.to(device)
+
+
+def build_model(D, H, W, device):
+    from mvs_amd.config import MVSConfig
+    from mvs_amd.model import MVSNet
+    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W))
+    net.load_state_dict(deterministic_state_dict(net.state_dict()))
+    return net.to(device).eval()
+
+
+def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None):
+    """Average fused-kernel launch time with HIP events on the launch stream."""
+    from mvs_amd import ops
+    d_count = D if d_count is None else d_count
+    K, R, T = camera_batch(B, V, h, w)
+    d_min, d_int = depth_range(B)
+    K, R, T, d_min, d_int = (x.to(device) for x in (K, R, T, d_min, d_int))
+    g = torch.Generator(device="cpu").manual_seed(7)
+    feat = torch.randn(B * V, C, h, w, generator=g).to(device)
+    with torch.no_grad():
+        for _ in range(3):
+            ops.cost_volume(feat, K, R, T, d_min, d_int, B, V, d_begin, d_count, 25.0)
+        stream = torch.cuda.current_stream(device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(iters):
+            ops.cost_volume(feat, K, R, T, d_min, d_int, B, V, d_begin, d_count, 25.0)
+        e1.record(stream)
+        torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    alg_bytes = 4.0 * B * V * C * h * w + 4.0 * B * C * d_count * h * w
+    return ms, alg_bytes
+
+
+def load_traffic(tag):
+    p = os.path.join(REPO, "profiles", "traffic_%s.json" % tag)
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
+def cpu_baseline(V, H, W, D):
+    """Oracle (reference op sequence, torch CPU) on ONE sample of the workload."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import mvs_oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    from mvs_amd.config import MVSConfig
+    from mvs_amd.model import MVSNet
+    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W), device=torch.device("cpu"))
+    net.load_state_dict(deterministic_state_dict(net.state_dict()))
+    net.eval()
+    img, K, R, T, d_min, d_int = make_inputs(1, V, H, W, 0, torch.device("cpu"))
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        mvs_oracle.mvsnet_forward(net, img, K, R, T, d_min, d_int, 1, V, D, (H // 4, W // 4),
+                                  concat_growth=True)
+        dt = time.perf_counter() - t0
+    return {"value": 1.0 / dt, "unit": "depth maps/s", "cores": threads, "kind": "port",
+            "sample": "1 sample (B=1, V=%d, %dx%d, D=%d) of the workload, full MVSNet.forward on "
+                      "the oracle (reference op sequence incl. per-plane warp loop with torch.cat "
+                      "growth), torch %s CPU, %d threads, %.1f s" % (V, W, H, D, torch.__version__,
+                                                                    threads, dt)}
+
+
+def main():
+    args = parse()
+    world, rank, device = init_dist(args)
+    V, H, W = args.views, args.height, args.width
+    h, w, C = H // 4, W // 4, 32
+    if args.mode == "samples":
+        B = args.batch or 4
+        D = args.planes or 192
+    else:
+        B = args.batch or 1
+        D = args.planes or 256
+        if D % world:
+            raise SystemExit("D=%d not divisible by world size %d" % (D, world))
+    torch.backends.cudnn.benchmark = True
+
+    result = {}
+    ms_step = None
+    if not args.kernel_only:
+        net = build_model(D, H, W, device)
+        inputs = make_inputs(B, V, H, W, rank, device)
+        if args.mode == "samples":
+            step = lambda: net(*inputs, B, V)
+        else:
+            from mvs_amd.depth_shards import DepthShardedMVSNet
+            sharded = DepthShardedMVSNet(net, world, rank)
+            step = lambda: sharded(*inputs, B, V)
+        with torch.no_grad():
+            for _ in range(args.warmup):
+                step()
+            barrier(world)
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            barrier(world)
+            dt = time.perf_counter() - t0
+        dt = max_over_ranks(dt, world, device)
+        ms_step = 1000.0 * dt / args.steps
+        maps = (B * world if args.mode == "samples" else B) * args.steps
+        result["value"] = maps / dt
+        del net
+
+    # fused kernel timing (this rank's share of planes in dshard mode)
+    d_count = D if args.mode == "samples" else D // world
+    k_ms, alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count)
+    k_ms = max_over_ranks(k_ms, world, device)
+    gbs = alg / (k_ms * 1e-3) / 1e9
+    tag = "b%dv%dd%dh%dw%d" % (B, V, d_count, h, w)
+    traffic = load_traffic(tag)
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    out = {
+        "metric": "depth maps/sec + warp-kernel HBM GB/s, 3-view 640x512 D=192, 1/2/4/8 GPU",
+        "value": result.get("value"),
+        "unit": "depth maps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak" if args.mode == "samples" else "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic N(0,1) images resident in HBM, real DTU scan-1 cameras, random-init weights",
+        "config": {"workload": "cfg%d: %d-view %dx%d D=%d batch=%d per %s" % (
+                       2 if args.mode == "samples" else 4, V, W, H, D, B,
+                       "GPU" if args.mode == "samples" else "job (D sharded)"),
+                   "global_batch": B * (world if args.mode == "samples" else 1),
+                   "views": V, "planes": D, "image_hw": [H, W], "feature_hw": [h, w],
+                   "parallelism": ("samples%d" % world) if args.mode == "samples" else ("dshard%d" % world)},
+        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": gbs / HBM_PEAK_GBS,
+                     "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
+                     "kernel": "cost_volume_kernel (+ plane_sampling_kernel)", "kernel_ms": k_ms,
+                     "alg_bytes_per_launch": alg},
+        "hot_path": {"cost_volumes_per_s": B / (k_ms * 1e-3), "kernel_ms": k_ms},
+    }
+    if not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(V, H, W, args.cpu_planes or D)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

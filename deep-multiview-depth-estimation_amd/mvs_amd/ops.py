@@ -1,0 +1,248 @@
+"""torch.library custom ops over the C ABI (namespace ``mvs``), with autograd and fake kernels.
+
+  mvs::cost_volume            fused warp + variance      (homography.py:6-92 + costvolume.py:3-16)
+  mvs::cost_volume_backward   d cv / d feat              (autograd of the above, train.py:103)
+  mvs::homography_warp        warp only                  (homography.py:6-92 warped volume)
+  mvs::assemble_cost_volume   variance of a warped volume (costvolume.py:3-16)
+  mvs::extract_depth_map      masked soft-argmin          (depthmap.py:4-22)
+
+Every op requires CUDA(HIP) tensors and raises otherwise: there is no CPU path in the product.
+Camera tensors (K, R, T, d_min, d_int) are moved to the feature device here, as the reference
+does with ``.to(DEVICE)`` (homography.py:25,43-58).
+"""
+import torch
+
+from . import _lib
+
+_F32 = torch.float32
+
+
+def _require_gpu(t, name):
+    if not t.is_cuda:
+        raise _lib.MVSLibraryError(
+            "%s must be a GPU (HIP) tensor: the MI355X cost-volume path has no CPU fallback" % name)
+
+
+def _cams(K, R, T, d_min, d_int, device, batch_size):
+    K = K.to(device=device, dtype=_F32).reshape(-1, 3, 3).contiguous()
+    R = R.to(device=device, dtype=_F32).reshape(-1, 3, 3).contiguous()
+    T = T.to(device=device, dtype=_F32).reshape(-1, 3).contiguous()
+    d_min = d_min.to(device=device, dtype=_F32).reshape(-1)
+    d_int = d_int.to(device=device, dtype=_F32).reshape(-1)
+    if d_min.numel() == 1:
+        d_min = d_min.expand(batch_size)
+    if d_int.numel() == 1:
+        d_int = d_int.expand(batch_size)
+    return K, R, T, d_min.contiguous(), d_int.contiguous()
+
+
+def _check_geometry(feat, K, batch_size, n_views):
+    if feat.dim() != 4:
+        raise ValueError("feature maps must be [B*V, C, h, w], got %s" % (tuple(feat.shape),))
+    n = batch_size * n_views
+    if feat.shape[0] != n:
+        raise ValueError("feature maps hold %d images, batch_size*n_views = %d" % (feat.shape[0], n))
+    if K.shape[0] != n:
+        raise ValueError("K holds %d cameras, batch_size*n_views = %d" % (K.shape[0], n))
+
+
+# ----------------------------------------------------------------------------------------------
+# mvs::cost_volume (+ backward)
+# ----------------------------------------------------------------------------------------------
+@torch.library.custom_op("mvs::cost_volume", mutates_args=())
+def cost_volume(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.Tensor,
+                d_min: torch.Tensor, d_int: torch.Tensor, batch_size: int, n_views: int,
+                d_begin: int, d_count: int, d_scale: float) -> tuple[torch.Tensor, torch.Tensor]:
+    """Fused warp + variance: returns (cv [B,C,d_count,h,w], sampling workspace [N*d_count*9])."""
+    _require_gpu(feat, "feature_maps")
+    lib = _lib.load()
+    feat = feat.to(_F32).contiguous()
+    K, R, T, d_min, d_int = _cams(K, R, T, d_min, d_int, feat.device, batch_size)
+    _check_geometry(feat, K, batch_size, n_views)
+    n, c, h, w = feat.shape
+    cv = torch.empty((batch_size, c, d_count, h, w), device=feat.device, dtype=_F32)
+    ws = torch.empty((n * d_count * 9,), device=feat.device, dtype=_F32)
+    st = lib.mvs_cost_volume_fwd(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T),
+                                 _lib.ptr(d_min), _lib.ptr(d_int), batch_size, n_views, c, h, w,
+                                 d_begin, d_count, float(d_scale), _lib.ptr(ws), _lib.ptr(cv),
+                                 _lib.stream_handle(feat.device))
+    _lib.check(st, "mvs_cost_volume_fwd")
+    return cv, ws
+
+
+@cost_volume.register_fake
+def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scale):
+    n, c, h, w = feat.shape
+    return (feat.new_empty((batch_size, c, d_count, h, w)), feat.new_empty((n * d_count * 9,)))
+
+
+@torch.library.custom_op("mvs::cost_volume_backward", mutates_args=())
+def cost_volume_backward(feat: torch.Tensor, sampling: torch.Tensor, grad_cv: torch.Tensor,
+                         batch_size: int, n_views: int, d_count: int) -> torch.Tensor:
+    _require_gpu(feat, "feature_maps")
+    lib = _lib.load()
+    feat = feat.to(_F32).contiguous()
+    grad_cv = grad_cv.to(_F32).contiguous()
+    n, c, h, w = feat.shape
+    grad_feat = torch.empty_like(feat)
+    st = lib.mvs_cost_volume_bwd(_lib.ptr(feat), _lib.ptr(sampling), _lib.ptr(grad_cv),
+                                 batch_size, n_views, c, h, w, d_count, _lib.ptr(grad_feat),
+                                 _lib.stream_handle(feat.device))
+    _lib.check(st, "mvs_cost_volume_bwd")
+    return grad_feat
+
+
+@cost_volume_backward.register_fake
+def _(feat, sampling, grad_cv, batch_size, n_views, d_count):
+    return torch.empty_like(feat)
+
+
+def _cv_setup(ctx, inputs, output):
+    feat, _, _, _, _, _, batch_size, n_views, _, d_count, _ = inputs
+    _, ws = output
+    ctx.save_for_backward(feat, ws)
+    ctx.dims = (batch_size, n_views, d_count)
+
+
+def _cv_backward(ctx, grad_cv, _grad_ws):
+    feat, ws = ctx.saved_tensors
+    batch_size, n_views, d_count = ctx.dims
+    grad_feat = None
+    if ctx.needs_input_grad[0] and grad_cv is not None:
+        grad_feat = cost_volume_backward(feat, ws, grad_cv, batch_size, n_views, d_count)
+    return grad_feat, None, None, None, None, None, None, None, None, None, None
+
+
+torch.library.register_autograd("mvs::cost_volume", _cv_backward, setup_context=_cv_setup)
+
+
+# ----------------------------------------------------------------------------------------------
+# mvs::homography_warp (materialised warped volume, API compatibility)
+# ----------------------------------------------------------------------------------------------
+@torch.library.custom_op("mvs::homography_warp", mutates_args=())
+def homography_warp(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.Tensor,
+                    d_min: torch.Tensor, d_int: torch.Tensor, batch_size: int, n_views: int,
+                    d_begin: int, d_count: int, d_scale: float) -> torch.Tensor:
+    """warped [B*V, C, d_count, h, w] (homography.py:6-92 output layout)."""
+    _require_gpu(feat, "feature_maps")
+    lib = _lib.load()
+    feat = feat.to(_F32).contiguous()
+    K, R, T, d_min, d_int = _cams(K, R, T, d_min, d_int, feat.device, batch_size)
+    _check_geometry(feat, K, batch_size, n_views)
+    n, c, h, w = feat.shape
+    warped = torch.empty((n, c, d_count, h, w), device=feat.device, dtype=_F32)
+    ws = torch.empty((n * d_count * 9,), device=feat.device, dtype=_F32)
+    st = lib.mvs_homography_warp_fwd(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T),
+                                     _lib.ptr(d_min), _lib.ptr(d_int), batch_size, n_views, c, h,
+                                     w, d_begin, d_count, float(d_scale), _lib.ptr(ws),
+                                     _lib.ptr(warped), _lib.stream_handle(feat.device))
+    _lib.check(st, "mvs_homography_warp_fwd")
+    return warped
+
+
+@homography_warp.register_fake
+def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scale):
+    n, c, h, w = feat.shape
+    return feat.new_empty((n, c, d_count, h, w))
+
+
+# ----------------------------------------------------------------------------------------------
+# mvs::assemble_cost_volume
+# ----------------------------------------------------------------------------------------------
+@torch.library.custom_op("mvs::assemble_cost_volume", mutates_args=())
+def assemble_cost_volume_op(warped: torch.Tensor, n_views: int) -> torch.Tensor:
+    _require_gpu(warped, "warped_feature_maps")
+    lib = _lib.load()
+    warped = warped.to(_F32).contiguous()
+    bn, c, d, h, w = warped.shape
+    if bn % n_views:
+        raise ValueError("%d warped images is not a multiple of n_views=%d" % (bn, n_views))
+    b = bn // n_views
+    cv = torch.empty((b, c, d, h, w), device=warped.device, dtype=_F32)
+    st = lib.mvs_assemble_cost_volume_fwd(_lib.ptr(warped), b, n_views, c, d, h, w, _lib.ptr(cv),
+                                          _lib.stream_handle(warped.device))
+    _lib.check(st, "mvs_assemble_cost_volume_fwd")
+    return cv
+
+
+@assemble_cost_volume_op.register_fake
+def _(warped, n_views):
+    bn, c, d, h, w = warped.shape
+    return warped.new_empty((bn // n_views, c, d, h, w))
+
+
+def _acv_setup(ctx, inputs, output):
+    warped, n_views = inputs
+    ctx.save_for_backward(warped)
+    ctx.n_views = n_views
+
+
+def _acv_backward(ctx, grad_cv):
+    # d cv / d x_v = 2 (x_v - mean) / V  (costvolume.py:14); plain torch on the device
+    (warped,) = ctx.saved_tensors
+    v = ctx.n_views
+    bn = warped.shape[0]
+    x = warped.reshape((bn // v, v) + tuple(warped.shape[1:]))
+    mean = x.mean(1, keepdim=True)
+    g = (2.0 / v) * (x - mean) * grad_cv.unsqueeze(1)
+    return g.reshape(warped.shape), None
+
+
+torch.library.register_autograd("mvs::assemble_cost_volume", _acv_backward, setup_context=_acv_setup)
+
+
+# ----------------------------------------------------------------------------------------------
+# mvs::extract_depth_map
+# ----------------------------------------------------------------------------------------------
+@torch.library.custom_op("mvs::extract_depth_map", mutates_args=())
+def extract_depth_map_op(prob_volume: torch.Tensor, d_batch: torch.Tensor, n_est: int) -> torch.Tensor:
+    _require_gpu(prob_volume, "prob_volume")
+    lib = _lib.load()
+    prob = prob_volume.to(_F32).contiguous()
+    if prob.dim() != 5 or prob.shape[1] != 1:
+        raise ValueError("prob_volume must be [B, 1, D, h, w], got %s" % (tuple(prob.shape),))
+    b, _, d, h, w = prob.shape
+    db = d_batch.to(device=prob.device, dtype=_F32).reshape(-1, d)
+    if db.shape[0] == 1 and b > 1:
+        db = db.expand(b, d)
+    db = db.contiguous()
+    depth = torch.empty((b, 1, h, w), device=prob.device, dtype=_F32)
+    st = lib.mvs_extract_depth_map_fwd(_lib.ptr(prob), _lib.ptr(db), b, d, h, w, int(n_est),
+                                       _lib.ptr(depth), _lib.stream_handle(prob.device))
+    _lib.check(st, "mvs_extract_depth_map_fwd")
+    return depth
+
+
+@extract_depth_map_op.register_fake
+def _(prob_volume, d_batch, n_est):
+    b, _, d, h, w = prob_volume.shape
+    return prob_volume.new_empty((b, 1, h, w))
+
+
+def _sam_setup(ctx, inputs, output):
+    prob, d_batch, n_est = inputs
+    ctx.save_for_backward(prob, d_batch, output)
+    ctx.n_est = n_est
+
+
+def _sam_backward(ctx, grad_depth):
+    # depth = sum_{r in S} d_r P_r / sum_{r in S} P_r  ->  d depth / d P_r = (d_r - depth) / den
+    # on S = {rank_j : j < n_est} (the mask is piecewise constant in P).  Plain torch on device.
+    prob, d_batch, depth = ctx.saved_tensors
+    b, _, d, h, w = prob.shape
+    n_est = min(ctx.n_est, d)
+    p = prob[:, 0]                                              # [B, D, h, w]
+    pj = p[:, :n_est].unsqueeze(2)                              # [B, E, 1, h, w]
+    idx = torch.arange(d, device=p.device)
+    before = (idx.view(1, 1, d, 1, 1) < torch.arange(n_est, device=p.device).view(1, n_est, 1, 1, 1))
+    rank = ((p.unsqueeze(1) > pj) | ((p.unsqueeze(1) == pj) & before)).sum(2)   # [B, E, h, w]
+    mask = torch.zeros_like(p).scatter_(1, rank, 1.0)
+    db = d_batch.to(p).reshape(-1, d)
+    if db.shape[0] == 1 and b > 1:
+        db = db.expand(b, d)
+    den = (p * mask).sum(1, keepdim=True)
+    g = mask * (db.view(b, d, 1, 1) - depth) / den * grad_depth
+    return g.unsqueeze(1), None, None
+
+
+torch.library.register_autograd("mvs::extract_depth_map", _sam_backward, setup_context=_sam_setup)

@@ -1,0 +1,117 @@
+/*
+ * mvs_cost_volume.h -- C ABI of the MI355X (gfx950) MVSNet cost-volume path.
+ *
+ * Drop-in boundary for bcollico/Deep-Multiview-Depth-Estimation's hot path (SURVEY.md §8 b).
+ * The reference boundary is three plain Python functions; each entry point below replaces one
+ * of them (or a fusion of them) and is bound from Python by ctypes in
+ * deep-multiview-depth-estimation_amd/mvs_amd/_lib.py (binding stub: INTEGRATION.md).
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a DEVICE pointer (HBM) except where noted; fp32 unless noted;
+ *   - tensors are dense row-major (NCHW / NCDHW) exactly as the reference lays them out;
+ *   - the callee allocates nothing: outputs and workspaces are caller-provided;
+ *   - no global mutable state: re-entrant per stream, graph-capturable (no sync, no malloc);
+ *   - `stream` is a hipStream_t (NULL = legacy default stream);
+ *   - return MVS_OK (0) or a negative MVS_ERR_* code; mvs_status_string() names it.
+ *
+ * Shapes: B batch, V views per sample (reference view first, included in the variance),
+ *         N = B*V images, C channels, h x w feature map, D planes in this call (a depth shard
+ *         [d_begin, d_begin + d_count) of the full hypothesis set), plane k has depth
+ *         d_min[i mod B] + d_scale * d_int[i mod B] * k for image i (homography.py:24-26 tiling).
+ */
+#ifndef MVS_COST_VOLUME_H
+#define MVS_COST_VOLUME_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MVS_ABI_VERSION 1
+
+#define MVS_OK 0
+#define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
+#define MVS_ERR_UNSUPPORTED_VIEWS (-2) /* n_views outside [1, MVS_MAX_VIEWS]               */
+#define MVS_ERR_TOO_LARGE (-3)         /* a tensor exceeds the kernel's 32-bit index space */
+#define MVS_ERR_HIP (-4)               /* a HIP launch/runtime error (see hipGetLastError)  */
+
+#define MVS_MAX_VIEWS 16
+
+/* ABI version of the loaded library (MVS_ABI_VERSION at build time). */
+int mvs_abi_version(void);
+
+/* Static string for a status code. */
+const char* mvs_status_string(int status);
+
+/* Bytes of the per-(image, plane) sampling workspace for n_images x d_count planes. */
+size_t mvs_sampling_workspace_bytes(int n_images, int d_count);
+
+/*
+ * Per-(image, plane) sampling matrices: the 3x3 map from kornia-normalised reference
+ * coordinates to normalised source coordinates, G = inv(Nrm H Nrm^-1) with
+ * H = K_i R_i (I - (C_i - C_r) n_r^T / d) R_r^T K_r^-1   (homography.py:40-75, kornia
+ * normalize_homography + inverse).  Computed in fp64, stored fp32 as sampling[N][d_count][9].
+ *   K, R: [N][3][3]; T: [N][3]; d_min, d_int: [B].
+ * Replaces homography.py:40-75 (the H_i tensor) + kornia's per-plane matrix setup.
+ */
+int mvs_plane_sampling(const float* K, const float* R, const float* T,
+                       const float* d_min, const float* d_int,
+                       int batch_size, int n_views, int h, int w,
+                       int d_begin, int d_count, float d_scale,
+                       float* sampling, void* stream);
+
+/*
+ * FUSED warp + variance: cv[B][C][d_count][h][w] from feat[N][C][h][w].
+ * Replaces homography.py:6-92 + costvolume.py:3-16 (model.py:177-181) in one pass; the
+ * warped N x C x D x h x w volume is never materialised.  `workspace` must hold
+ * mvs_sampling_workspace_bytes(N, d_count) bytes; on return it holds the sampling matrices
+ * (reused by mvs_cost_volume_bwd).
+ */
+int mvs_cost_volume_fwd(const float* feat, const float* K, const float* R, const float* T,
+                        const float* d_min, const float* d_int,
+                        int batch_size, int n_views, int channels, int h, int w,
+                        int d_begin, int d_count, float d_scale,
+                        float* workspace, float* cv_out, void* stream);
+
+/*
+ * Warp only (API-compatible homography_warping, homography.py:6-92):
+ * warped[N][C][d_count][h][w].  Same workspace contract as mvs_cost_volume_fwd.
+ */
+int mvs_homography_warp_fwd(const float* feat, const float* K, const float* R, const float* T,
+                            const float* d_min, const float* d_int,
+                            int batch_size, int n_views, int channels, int h, int w,
+                            int d_begin, int d_count, float d_scale,
+                            float* workspace, float* warped_out, void* stream);
+
+/*
+ * Variance over views of an already-warped volume (costvolume.py:3-16):
+ * warped[B*V][C][D][h][w] -> cv[B][C][D][h][w].
+ */
+int mvs_assemble_cost_volume_fwd(const float* warped, int batch_size, int n_views,
+                                 int channels, int d, int h, int w, float* cv_out, void* stream);
+
+/*
+ * Backward of the fused op w.r.t. the features (autograd of costvolume.py:14 + grid_sample,
+ * exercised by train.py:103).  grad_feat[N][C][h][w] is OVERWRITTEN (zeroed, then accumulated
+ * with float atomics -- summation order is not deterministic, like torch's grid_sample backward
+ * on GPU).  `sampling` is the workspace filled by the forward call with the same geometry.
+ */
+int mvs_cost_volume_bwd(const float* feat, const float* sampling, const float* grad_cv,
+                        int batch_size, int n_views, int channels, int h, int w, int d_count,
+                        float* grad_feat, void* stream);
+
+/*
+ * Soft-argmin with the reference's permutation-indexed mask (depthmap.py:4-22):
+ * depth[b][0][y][x] = sum_r d[b][r] P[b][0][r][y][x] m_r / sum_r P m_r, with
+ * m_r = (argsort_desc(P)[r] < n_est), ties broken by ascending plane index.
+ *   prob: [B][1][D][h][w]; d_batch: [B][D]; depth_out: [B][1][h][w].
+ */
+int mvs_extract_depth_map_fwd(const float* prob, const float* d_batch, int batch_size, int d,
+                              int h, int w, int n_est, float* depth_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MVS_COST_VOLUME_H */

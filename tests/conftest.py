@@ -1,0 +1,32 @@
+"""Shared pytest setup: import paths and the ``gpu`` marker.
+
+``-m "not gpu"`` runs here (no GPU): oracle vs golden vectors, host logic, library load/exports,
+gloo world_size-2 distributed logic.  ``-m gpu`` runs on an MI355X: parity of the HIP path
+(through the C ABI) against the oracle and the golden vectors.
+"""
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for sub in ("deep-multiview-depth-estimation_amd", "oracle", os.path.join("tests", "golden")):
+    p = os.path.join(REPO, sub)
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) -- parity of the HIP path")
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return GOLDEN
+
+
+def load_golden(name):
+    import numpy as np
+    return np.load(os.path.join(GOLDEN, name))
