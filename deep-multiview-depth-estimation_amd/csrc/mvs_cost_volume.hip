@@ -388,10 +388,11 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
     for (int v = 0; v < MAXV; ++v)
       if (v < V) {
         const float coef = k2 * (val[v] - mean);
-        float* plane = gb + ((size_t)v * C + c) * hw;
+        char* plane = reinterpret_cast<char*>(gb + ((size_t)v * C + c) * hw);
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-          if (tp[v].wt[t] != 0.0f) unsafeAtomicAdd(plane + tp[v].off[t], tp[v].wt[t] * coef);
+        for (int t = 0; t < 4; ++t)  // off[] are byte offsets
+          if (tp[v].wt[t] != 0.0f)
+            unsafeAtomicAdd(reinterpret_cast<float*>(plane + tp[v].off[t]), tp[v].wt[t] * coef);
       }
   }
 }

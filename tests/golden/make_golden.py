@@ -15,6 +15,7 @@ Outputs (small .npz, committed):
                              random, D == N_DEPTH_EST)
   cfg1_cv.npz                config-1 cost volume (B=1,V=3,C=32,128x160,D=48): 4096 seeded voxel
                              samples + sum, sum of squares, max
+  state_dict_keys.json       the reference MVSNet state_dict keys/shapes (D_NUM=20) and parameter count
   cfg1_e2e.npz               MVSNet.forward at config 1 (640x512 images, D=48) with the weights of
                              tests/golden/weights.py: initial/refined depth, BN eval mode and the
                              test.py:61 train-mode-under-no_grad mode
@@ -166,7 +167,18 @@ def case_cfg1_e2e():
     np.savez_compressed(os.path.join(HERE, "cfg1_e2e.npz"), **out)
 
 
-CASES = {"tiny_v3": lambda: case_tiny(3), "tiny_v5": lambda: case_tiny(5),
+def case_state_dict_keys():
+    import json
+    _import_reference(20, 128, 160)
+    import model as ref_model
+    net = ref_model.MVSNet()
+    keys = [[k, list(v.shape)] for k, v in net.state_dict().items()]
+    n_params = sum(p.numel() for p in net.parameters)
+    with open(os.path.join(HERE, "state_dict_keys.json"), "w") as f:
+        json.dump({"keys": keys, "n_params": n_params, "d_num": 20}, f, indent=0)
+
+
+CASES = {"keys": case_state_dict_keys, "tiny_v3": lambda: case_tiny(3), "tiny_v5": lambda: case_tiny(5),
          "softargmin": case_softargmin, "cfg1_cv": case_cfg1_cv, "cfg1_e2e": case_cfg1_e2e}
 
 

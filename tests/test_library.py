@@ -1,0 +1,74 @@
+"""CPU: the C-ABI library exists, loads, and exports every entry point include/*.h declares.
+
+No kernel is launched here (no GPU); only host-side functions that touch no device are called.
+"""
+import glob
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+
+def _declared():
+    names = []
+    for h in glob.glob(os.path.join(REPO, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names += re.findall(r"^\s*(?:const\s+)?[\w\*\s]+?\b(mvs_\w+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_the_abi():
+    names = _declared()
+    assert "mvs_cost_volume_fwd" in names and "mvs_cost_volume_bwd" in names
+    assert len(names) == 9, names
+
+
+def test_library_exports_every_declared_symbol():
+    from mvs_amd import _lib
+    lib = _lib.load()
+    for name in _declared():
+        assert hasattr(lib, name), name
+    assert set(_declared()) == set(_lib.SIGNATURES), "ctypes bindings out of sync with the header"
+
+
+def test_host_only_entry_points():
+    from mvs_amd import _lib
+    lib = _lib.load()
+    assert lib.mvs_abi_version() == _lib.ABI_VERSION == 1
+    assert lib.mvs_status_string(0) == b"ok"
+    assert lib.mvs_status_string(-2).startswith(b"n_views")
+    assert lib.mvs_sampling_workspace_bytes(12, 192) == 12 * 192 * 9 * 4
+    assert lib.mvs_sampling_workspace_bytes(0, 192) == 0
+
+
+def test_invalid_arguments_rejected_before_any_launch():
+    """Argument validation returns an error code without touching the device."""
+    import ctypes
+    from mvs_amd import _lib
+    lib = _lib.load()
+    null = ctypes.c_void_p(0)
+    fake = ctypes.c_void_p(0x1000)
+    # null pointers
+    assert lib.mvs_cost_volume_fwd(null, fake, fake, fake, fake, fake, 1, 3, 32, 128, 160, 0, 48,
+                                   25.0, fake, fake, null) == -1
+    # unsupported view count
+    assert lib.mvs_cost_volume_fwd(fake, fake, fake, fake, fake, fake, 1, 17, 32, 128, 160, 0, 48,
+                                   25.0, fake, fake, null) == -2
+    # degenerate image (kornia's (w-1) normalisation needs w, h >= 2)
+    assert lib.mvs_cost_volume_fwd(fake, fake, fake, fake, fake, fake, 1, 3, 32, 1, 160, 0, 48,
+                                   25.0, fake, fake, null) == -1
+    # per-image index space
+    assert lib.mvs_cost_volume_fwd(fake, fake, fake, fake, fake, fake, 1, 3, 70000, 128, 256, 0, 4,
+                                   25.0, fake, fake, null) == -3
+    assert lib.mvs_extract_depth_map_fwd(fake, fake, 1, 48, 8, 8, 0, fake, null) == -1
+
+
+def test_build_is_gfx950_in_tree():
+    from mvs_amd import _build
+    assert _build.ARCH == "gfx950" or os.environ.get("MVS_OFFLOAD_ARCH")
+    assert os.path.dirname(_build.OUTPUT).startswith(REPO)
+    data = open(_build.OUTPUT, "rb").read()
+    assert b"gfx950" in data
