@@ -29,6 +29,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/mvs_cost_volume.h"
 
 namespace {
@@ -139,19 +141,29 @@ struct Taps {
   float wt[4];      // bilinear weights (0 when out of bounds)
 };
 
+// Source sampling position (ix, iy) of normalised reference pixel (xn, yn) under sampling matrix G
+// (kornia transform_points + convert_points_from_homogeneous + grid_sample unnormalise).  Every
+// rounding step is explicit (__f*_rn), so all call sites -- every view, every kernel -- produce
+// bit-identical coordinates for identical inputs regardless of how the compiler contracts code.
+__device__ inline void sample_coord(const float* __restrict__ G, float xn, float yn, int h, int w,
+                                    float& ix, float& iy) {
+  float u = __fmaf_rn(G[1], yn, __fmaf_rn(G[0], xn, G[2]));
+  float v = __fmaf_rn(G[4], yn, __fmaf_rn(G[3], xn, G[5]));
+  const float s = __fmaf_rn(G[7], yn, __fmaf_rn(G[6], xn, G[8]));
+  if (fabsf(s) > 1e-8f) {  // kornia eps: scale = 1 / (s + eps) where |s| > eps, else 1
+    const float sc = __fdiv_rn(1.0f, __fadd_rn(s, 1e-8f));
+    u = __fmul_rn(u, sc);
+    v = __fmul_rn(v, sc);
+  }
+  // grid_sample(align_corners=False) unnormalise, as torch's CPU kernel: (g + 1) * (size / 2) - 0.5
+  ix = __fsub_rn(__fmul_rn(__fadd_rn(u, 1.0f), 0.5f * (float)w), 0.5f);
+  iy = __fsub_rn(__fmul_rn(__fadd_rn(v, 1.0f), 0.5f * (float)h), 0.5f);
+}
+
 __device__ inline void make_taps(const float* __restrict__ G, float xn, float yn, int h, int w,
                                  Taps& tp) {
-  float u = G[0] * xn + G[1] * yn + G[2];
-  float v = G[3] * xn + G[4] * yn + G[5];
-  const float s = G[6] * xn + G[7] * yn + G[8];
-  if (fabsf(s) > 1e-8f) {  // kornia convert_points_from_homogeneous, eps = 1e-8
-    const float sc = 1.0f / (s + 1e-8f);
-    u *= sc;
-    v *= sc;
-  }
-  // grid_sample unnormalise, align_corners=False: (g + 1) * size / 2 - 0.5
-  float ix = (u + 1.0f) * (0.5f * (float)w) - 0.5f;
-  float iy = (v + 1.0f) * (0.5f * (float)h) - 0.5f;
+  float ix, iy;
+  sample_coord(G, xn, yn, h, w, ix, iy);
   // far outside (or NaN): every tap invalid; keeps the int conversion in range
   if (!(ix > -2.0f && ix < (float)w + 1.0f && iy > -2.0f && iy < (float)h + 1.0f)) {
     ix = -4.0f;
@@ -223,11 +235,15 @@ __device__ inline WorkItem decode(int wk, int Dc, int tiles) {
 }
 
 // meshgrid of kornia (normalized_coordinates=True): (x / (w-1) - 0.5) * 2
+__device__ inline float norm_coord(uint32_t x, int size) {
+  return __fmul_rn(__fsub_rn(__fdiv_rn((float)x, (float)(size - 1)), 0.5f), 2.0f);
+}
+
 __device__ inline void pixel_coords(uint32_t p, int w, int h, float& xn, float& yn) {
   const uint32_t y = p / (uint32_t)w;
   const uint32_t x = p - y * (uint32_t)w;
-  xn = ((float)x / (float)(w - 1) - 0.5f) * 2.0f;
-  yn = ((float)y / (float)(h - 1) - 0.5f) * 2.0f;
+  xn = norm_coord(x, w);
+  yn = norm_coord(y, h);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -443,6 +459,374 @@ __global__ __launch_bounds__(kBlock) void soft_argmin_kernel(const float* __rest
 }
 
 // ------------------------------------------------------------------------------------------
+// v2 fused path: features packed channel-chunk-last, source footprints staged in LDS
+// ------------------------------------------------------------------------------------------
+// pack: feat[N][C][h][w] -> packed[N][NCH][h][w][CH], NCH = ceil(C / CH), zero-padded channels.
+template <int CH>
+__global__ __launch_bounds__(kBlock) void pack_features_kernel(const float* __restrict__ feat,
+                                                              float* __restrict__ packed, int N,
+                                                              int C, uint32_t hw) {
+  const int nch = (C + CH - 1) / CH;
+  const size_t n = (size_t)N * nch * hw;
+  for (size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (size_t)gridDim.x * kBlock) {
+    const size_t p = e % hw;
+    const size_t t = e / hw;
+    const int ch = (int)(t % nch);
+    const size_t i = t / nch;
+    float v[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int c = ch * CH + j;
+      v[j] = c < C ? feat[(i * C + c) * hw + p] : 0.0f;
+    }
+    float4* o = reinterpret_cast<float4*>(packed + e * CH);
+#pragma unroll
+    for (int q = 0; q < CH / 4; ++q) o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  }
+}
+
+#ifndef MVS_EXP_TW
+#define MVS_EXP_TW 16
+#endif
+constexpr int kTW = MVS_EXP_TW;        // tile width  (pixels)
+constexpr int kTH = 256 / kTW;         // tile height (pixels): 256 threads, one pixel each
+#ifndef MVS_EXP_LDS_KB
+#define MVS_EXP_LDS_KB 48
+#endif
+constexpr int kLdsBytes = MVS_EXP_LDS_KB * 1024;   // footprint staging budget per workgroup
+constexpr uint32_t kInvalidTap = 0xFFFFFFFFu;
+
+// Source coordinates of one (pixel, view, plane): kornia sampling law as make_taps, reduced to the
+// integer corner (x0, y0) and fractions; positions whose 4 taps all fall outside the image
+// (ix < -1, ix >= w, ...) are marked invalid (value exactly 0).
+__device__ inline void src_coords(const float* __restrict__ G, float xn, float yn, int h, int w,
+                                  bool active, uint32_t& pos, float& wx, float& wy) {
+  float ix, iy;
+  sample_coord(G, xn, yn, h, w, ix, iy);
+  const bool ok = active && ix >= -1.0f && ix < (float)w && iy >= -1.0f && iy < (float)h;
+  const float fx = floorf(ok ? ix : 0.0f), fy = floorf(ok ? iy : 0.0f);
+  wx = ok ? ix - fx : 0.0f;
+  wy = ok ? iy - fy : 0.0f;
+  // x0 in [-1, w-1], y0 in [-1, h-1]; stored +2 so both fields are positive 16-bit values
+  pos = ok ? ((uint32_t)((int)fy + 2) << 16) | (uint32_t)((int)fx + 2) : kInvalidTap;
+}
+
+__device__ inline int pos_x(uint32_t p) { return (int)(p & 0xFFFFu) - 2; }
+__device__ inline int pos_y(uint32_t p) { return (int)(p >> 16) - 2; }
+
+// Workgroup-wide min of NV ints (every thread gets the result, in SGPR-uniform form).
+template <int NV>
+__device__ inline void block_min(int (&v)[NV], int* scratch /* >= 4 * NV ints in LDS */) {
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    int x = v[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o));
+    v[k] = x;
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) scratch[wave * NV + k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    int x = scratch[k];
+#pragma unroll
+    for (int q = 1; q < kBlock / 64; ++q) x = min(x, scratch[q * NV + k]);
+    v[k] = __builtin_amdgcn_readfirstlane(x);
+  }
+  __syncthreads();
+}
+
+// Footprint of one source view in LDS: region rows [y0, y0+rh), cols [x0, x0+rw), preceded by a
+// zero prefix of rw + 2 pixels that invalid taps point at.  Offsets in bytes.
+struct Region {
+  int x0, y0, rw, rh;
+  int base;  // byte offset of the prefix in the staging buffer
+};
+
+// CH == 8: pixel p occupies 16-B slots 2p + p/8 and 2p + p/8 + 1 (a 16-B pad every 8 pixels), so
+// the 16 lanes of a ds_read_b128 group that read 16 consecutive pixels hit 16 distinct 4-bank groups.
+// CH == 4: one 16-B slot per pixel, consecutive pixels are conflict-free as they are.
+template <int CH>
+__device__ inline int slot_of(int p) {
+  return CH == 8 ? 2 * p + (p >> 3) : p;
+}
+
+template <int CH>
+__device__ inline int region_bytes(const Region& r) {
+  return r.rw > 0 ? (slot_of<CH>(r.rh * r.rw + r.rw + 2) + 2) * 16 : 0;
+}
+
+template <int CH>
+__device__ inline void stage_region(char* lds, const Region& r, const float* __restrict__ src,
+                                    int h, int w) {
+  // src = packed[i][chunk] plane: [h][w][CH]
+  constexpr int HALVES = CH / 4;
+  if (r.rw <= 0) return;
+  const int prefix = (r.rw + 2) * HALVES;
+  const int body = r.rh * r.rw * HALVES;
+  const float inv = 1.0f / (float)(r.rw * HALVES);
+  for (int q = threadIdx.x; q < prefix + body; q += kBlock) {
+    float4 val = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    int p, half;
+    if (q < prefix) {
+      p = q / HALVES;
+      half = q - p * HALVES;
+    } else {
+      const int e = q - prefix;
+      const int row = (int)(((float)e + 0.5f) * inv);
+      const int rem = e - row * r.rw * HALVES;
+      const int col = rem / HALVES;
+      half = rem - col * HALVES;
+      p = r.rw + 2 + row * r.rw + col;
+      const int gx = r.x0 + col, gy = r.y0 + row;
+      if (gx >= 0 && gx < w && gy >= 0 && gy < h)
+        val = *reinterpret_cast<const float4*>(src + ((size_t)gy * w + gx) * CH + half * 4);
+    }
+    *reinterpret_cast<float4*>(lds + r.base + (slot_of<CH>(p) + half) * 16) = val;
+  }
+}
+
+// Bilinear sample of CH channels of one staged view: taps p, p+1, p+rw, p+rw+1.
+template <int CH>
+__device__ inline void gather_lds(const char* lds, const Region& r, uint32_t pos, float wx, float wy,
+                                  float (&out)[CH]) {
+#pragma unroll
+  for (int j = 0; j < CH; ++j) out[j] = 0.0f;
+  // all four taps outside the image: exactly zero (the view's region may even be empty)
+  if (pos == kInvalidTap) return;
+  const int p = r.rw + 2 + (pos_y(pos) - r.y0) * r.rw + (pos_x(pos) - r.x0);
+  const float ex = 1.0f - wx, ny = 1.0f - wy;
+  const float wt[4] = {ny * ex, ny * wx, wy * ex, wy * wx};
+  const int tp[4] = {p, p + 1, p + r.rw, p + r.rw + 1};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const char* a0 = lds + r.base + slot_of<CH>(tp[t]) * 16;
+#pragma unroll
+    for (int q = 0; q < CH / 4; ++q) {
+      const float4 a = *reinterpret_cast<const float4*>(a0 + 16 * q);
+      out[4 * q + 0] += a.x * wt[t];
+      out[4 * q + 1] += a.y * wt[t];
+      out[4 * q + 2] += a.z * wt[t];
+      out[4 * q + 3] += a.w * wt[t];
+    }
+  }
+}
+
+// Bilinear sample of CH channels straight from the packed global plane (ref view, and planes whose
+// footprint does not fit the LDS budget).  Per-tap bounds checks; zero padding.
+template <int CH>
+__device__ inline void gather_global(const float* __restrict__ src, uint32_t pos, float wx, float wy,
+                                     int h, int w, float (&out)[CH]) {
+#pragma unroll
+  for (int j = 0; j < CH; ++j) out[j] = 0.0f;
+  if (pos == kInvalidTap) return;
+  const int x0 = pos_x(pos), y0 = pos_y(pos);
+  const float ex = 1.0f - wx, ny = 1.0f - wy;
+  const float wt[4] = {ny * ex, ny * wx, wy * ex, wy * wx};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int x = x0 + (t & 1), y = y0 + (t >> 1);
+    const bool ok = x >= 0 && x < w && y >= 0 && y < h;
+    const float* px = src + ((size_t)(ok ? y : 0) * w + (ok ? x : 0)) * CH;
+    const float wk = ok ? wt[t] : 0.0f;
+#pragma unroll
+    for (int q = 0; q < CH / 4; ++q) {
+      const float4 a = *reinterpret_cast<const float4*>(px + 4 * q);
+      out[4 * q + 0] += a.x * wk;
+      out[4 * q + 1] += a.y * wk;
+      out[4 * q + 2] += a.z * wk;
+      out[4 * q + 3] += a.w * wk;
+    }
+  }
+}
+
+// One workgroup: sample b, a 16x16 pixel tile, planes [k0, k0 + npl) (npl <= kPG).
+//   1. every thread computes the source corner/fractions of its pixel for every (plane, source
+//      view) into registers (the ref view's sampling is plane independent: P = I exactly);
+//   2. the union footprint of the whole plane group is reduced over the workgroup; if all source
+//      views fit the LDS budget the group is processed as ONE sub-range, else plane by plane
+//      (a plane that still does not fit gathers straight from global memory);
+//   3. per sub-range and per CH-channel chunk: stage the footprints, then every thread samples
+//      V views x CH channels per plane and writes CH cost-volume values (two-pass variance).
+// depth planes per workgroup: the per-(plane, source view) tap state lives in registers
+#ifndef MVS_EXP_PG
+#define MVS_EXP_PG 8
+#endif
+template <int V>
+constexpr int planes_per_group() { return V <= 3 ? MVS_EXP_PG : 4; }
+
+template <int V, int CH>
+__global__ __launch_bounds__(kBlock) void cost_volume_lds_kernel(
+    const float* __restrict__ packed, const float* __restrict__ sampling, float* __restrict__ cv,
+    int C, int h, int w, int Dc, int pg, int tiles_x, int tiles_y, int groups, int total) {
+  // pg (<= kPG) planes per workgroup, chosen by the host so that small problems still fill the chip
+  constexpr int NS = V - 1;
+  constexpr int kPG = planes_per_group<V>();
+  __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+  __shared__ int scratch[4 * 4 * (NS > 0 ? NS : 1)];
+
+  const int wk = xcd_work_id(blockIdx.x, total);
+  if (wk >= total) return;
+  const int g = wk % groups;
+  const int t = wk / groups;
+  const int tile = t % (tiles_x * tiles_y);
+  const int b = t / (tiles_x * tiles_y);
+  const int px = (tile % tiles_x) * kTW + (threadIdx.x % kTW);
+  const int py = (tile / tiles_x) * kTH + (threadIdx.x / kTW);
+  const bool active = px < w && py < h;
+  const int k0 = g * pg;
+  const int npl = min(pg, Dc - k0);
+  const uint32_t hw = (uint32_t)h * (uint32_t)w;
+  const int nch = (C + CH - 1) / CH;
+  const float xn = norm_coord(px, w);
+  const float yn = norm_coord(py, h);
+
+  // 1. sampling coordinates
+  uint32_t rpos;
+  float rwx, rwy;
+  src_coords(sampling + ((size_t)(b * V) * Dc + k0) * 9, xn, yn, h, w, active, rpos, rwx, rwy);
+  uint32_t pos[kPG][NS > 0 ? NS : 1];
+  float fwx[kPG][NS > 0 ? NS : 1], fwy[kPG][NS > 0 ? NS : 1];
+#pragma unroll
+  for (int pl = 0; pl < kPG; ++pl)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      pos[pl][s] = kInvalidTap;
+      fwx[pl][s] = fwy[pl][s] = 0.0f;
+      if (pl < npl)
+        src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + k0 + pl) * 9, xn, yn, h, w, active,
+                   pos[pl][s], fwx[pl][s], fwy[pl][s]);
+    }
+
+  // footprint of planes [lo, hi) per source view -> regions; returns true if all fit
+  auto plan = [&](int lo, int hi, Region (&reg)[NS > 0 ? NS : 1]) -> bool {
+    int bb[4 * (NS > 0 ? NS : 1)];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      int mnx = 1 << 30, mny = 1 << 30, mxx = 1 << 30, mxy = 1 << 30;  // mx* hold -max
+#pragma unroll
+      for (int pl = 0; pl < kPG; ++pl) {
+        const uint32_t p = pos[pl][s];
+        if (pl >= lo && pl < hi && p != kInvalidTap) {
+          mnx = min(mnx, pos_x(p));
+          mny = min(mny, pos_y(p));
+          mxx = min(mxx, -(pos_x(p) + 1));
+          mxy = min(mxy, -(pos_y(p) + 1));
+        }
+      }
+      bb[4 * s + 0] = mnx;
+      bb[4 * s + 1] = mny;
+      bb[4 * s + 2] = mxx;
+      bb[4 * s + 3] = mxy;
+    }
+    block_min<4 * (NS > 0 ? NS : 1)>(bb, scratch);
+    int off = 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      Region& r = reg[s];
+      r.x0 = bb[4 * s + 0];
+      r.y0 = bb[4 * s + 1];
+      const int x1 = -bb[4 * s + 2], y1 = -bb[4 * s + 3];
+      const bool empty = r.x0 > x1;
+      r.rw = empty ? 0 : x1 - r.x0 + 1;
+      r.rh = empty ? 0 : y1 - r.y0 + 1;
+      r.base = off;
+      off += region_bytes<CH>(r);
+    }
+    return off <= kLdsBytes;
+  };
+
+  const float inv_v = 1.0f / (float)V;
+  // process planes [lo, hi) with the given regions (staged) or from global memory
+  auto run = [&](int lo, int hi, const Region (&reg)[NS > 0 ? NS : 1], bool staged) {
+    for (int ch = 0; ch < nch; ++ch) {
+      const float* ref_src = packed + ((size_t)(b * V) * nch + ch) * hw * CH;
+      if (staged) {
+#if !defined(MVS_EXP_NO_STAGE)
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          stage_region<CH>(lds, reg[s], packed + ((size_t)(b * V + 1 + s) * nch + ch) * hw * CH, h, w);
+#endif
+        __syncthreads();
+      }
+      float x0v[CH];
+      gather_global<CH>(ref_src, rpos, rwx, rwy, h, w, x0v);
+#pragma unroll
+      for (int pl = 0; pl < kPG; ++pl) {
+        if (pl < lo || pl >= hi) continue;
+        float sum[CH], val[NS > 0 ? NS : 1][CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) sum[j] = x0v[j];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          // opaque copies: stop the compiler from hoisting per-(plane, view) tap addresses and
+          // weights out of the chunk loop (16 sets x 8 registers would not fit)
+          uint32_t tpos = pos[pl][s];
+          float twx = fwx[pl][s], twy = fwy[pl][s];
+          asm volatile("" : "+v"(tpos), "+v"(twx), "+v"(twy));
+#if defined(MVS_EXP_NO_GATHER)  // experiment: store path + staging only
+          for (int j = 0; j < CH; ++j) val[s][j] = twx * (float)j + twy;
+          if (false) {
+          } else if (false)
+#else
+          if (staged)
+#endif
+            gather_lds<CH>(lds, reg[s], tpos, twx, twy, val[s]);
+          else
+            gather_global<CH>(packed + ((size_t)(b * V + 1 + s) * nch + ch) * hw * CH, tpos, twx,
+                              twy, h, w, val[s]);
+#pragma unroll
+          for (int j = 0; j < CH; ++j) sum[j] += val[s][j];
+        }
+        if (active) {
+          float* ob = cv + ((size_t)b * C * Dc + (size_t)(k0 + pl)) * hw + (size_t)py * w + px;
+#pragma unroll
+          for (int j = 0; j < CH; ++j) {
+            const int c = ch * CH + j;
+            if (c < C) {
+              const float mean = sum[j] * inv_v;
+              float d = x0v[j] - mean;
+              float acc = d * d;
+#pragma unroll
+              for (int s = 0; s < NS; ++s) {
+                d = val[s][j] - mean;
+                acc += d * d;
+              }
+#if defined(MVS_EXP_NO_STORE)  // experiment: keep the compute, drop the traffic
+              if (acc != acc) ob[(size_t)c * Dc * hw] = acc * inv_v;
+#elif defined(MVS_EXP_PLAIN_STORE)
+              ob[(size_t)c * Dc * hw] = acc * inv_v;
+#else
+              __builtin_nontemporal_store(acc * inv_v, ob + (size_t)c * Dc * hw);
+#endif
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep each plane's LDS reads out of its neighbours'
+      }
+      if (staged) __syncthreads();
+    }
+  };
+
+  Region reg[NS > 0 ? NS : 1];
+  const bool whole = plan(0, npl, reg);   // whole plane group in one staging pass?
+  const int nsub = whole ? 1 : npl;
+  for (int sr = 0; sr < nsub; ++sr) {
+    const int lo = whole ? 0 : sr, hi = whole ? npl : sr + 1;
+#if defined(MVS_EXP_FORCE_GLOBAL)
+    const bool staged = whole ? false : (plan(lo, hi, reg) && false);
+#else
+    const bool staged = whole ? true : plan(lo, hi, reg);
+#endif
+    run(lo, hi, reg, staged);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
 inline int hip_status() {
@@ -480,6 +864,31 @@ void launch_fused(const Geometry& g, const float* feat, const float* smp, float*
                   hipStream_t s) {
   hipLaunchKernelGGL((cost_volume_kernel<MAXV, EXACT, 4>), xcd_grid(g.total), dim3(kBlock), 0, s,
                      feat, smp, cv, g.V, g.C, g.h, g.w, g.Dc, g.tiles, g.total);
+}
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+#ifndef MVS_EXP_CH3
+#define MVS_EXP_CH3 8
+#endif
+inline int packed_chunk(int n_views) { return n_views <= 3 ? MVS_EXP_CH3 : 4; }
+
+template <int V, int CH>
+void launch_lds(const Geometry& g, const float* feat, const float* smp, float* packed, float* cv,
+                hipStream_t s) {
+  const uint32_t hw = (uint32_t)g.h * (uint32_t)g.w;
+  const size_t n_pack = (size_t)g.B * V * ((g.C + CH - 1) / CH) * hw;
+  const unsigned pgrid = (unsigned)std::min<size_t>((n_pack + kBlock - 1) / kBlock, 4096);
+  hipLaunchKernelGGL((pack_features_kernel<CH>), dim3(pgrid), dim3(kBlock), 0, s, feat, packed,
+                     g.B * V, g.C, hw);
+  const int tiles_x = (g.w + kTW - 1) / kTW, tiles_y = (g.h + kTH - 1) / kTH;
+  // planes per workgroup: the register maximum, lowered until the grid has >= 4 workgroups per CU
+  int pg = planes_per_group<V>();
+  while (pg > 1 && (long)g.B * tiles_x * tiles_y * ((g.Dc + pg - 1) / pg) < 1024) pg >>= 1;
+  const int groups = (g.Dc + pg - 1) / pg;
+  const int total = g.B * tiles_x * tiles_y * groups;
+  hipLaunchKernelGGL((cost_volume_lds_kernel<V, CH>), xcd_grid(total), dim3(kBlock), 0, s, packed,
+                     smp, cv, g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total);
 }
 
 template <int MAXV, bool EXACT>
@@ -525,6 +934,16 @@ int mvs_plane_sampling(const float* K, const float* R, const float* T, const flo
   return hip_status();
 }
 
+size_t mvs_cost_volume_workspace_bytes(int batch_size, int n_views, int channels, int h, int w,
+                                       int d_count) {
+  if (batch_size <= 0 || n_views <= 0 || channels <= 0 || h <= 0 || w <= 0 || d_count <= 0) return 0;
+  const size_t n = (size_t)batch_size * n_views;
+  const size_t ch = packed_chunk(n_views);
+  const size_t nch = ((size_t)channels + ch - 1) / ch;
+  return align256(mvs_sampling_workspace_bytes((int)n, d_count)) +
+         n * nch * ch * (size_t)h * (size_t)w * sizeof(float);
+}
+
 int mvs_cost_volume_fwd(const float* feat, const float* K, const float* R, const float* T,
                         const float* d_min, const float* d_int, int batch_size, int n_views,
                         int channels, int h, int w, int d_begin, int d_count, float d_scale,
@@ -537,14 +956,26 @@ int mvs_cost_volume_fwd(const float* feat, const float* K, const float* R, const
                           d_scale, workspace, stream);
   if (st != MVS_OK) return st;
   hipStream_t s = (hipStream_t)stream;
+  if (n_views == 1) {  // variance of a single view is identically zero
+    if (hipMemsetAsync(cv_out, 0, (size_t)batch_size * channels * d_count * h * w * sizeof(float), s) !=
+        hipSuccess)
+      return MVS_ERR_HIP;
+    return hip_status();
+  }
+  if (n_views > 8) {  // generic path: direct gathers from the NCHW features
+    launch_fused<MVS_MAX_VIEWS, false>(g, feat, workspace, cv_out, s);
+    return hip_status();
+  }
+  float* packed = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) +
+                                           align256(mvs_sampling_workspace_bytes(g.B * g.V, g.Dc)));
   switch (n_views) {
-    case 1: launch_fused<1, true>(g, feat, workspace, cv_out, s); break;
-    case 2: launch_fused<2, true>(g, feat, workspace, cv_out, s); break;
-    case 3: launch_fused<3, true>(g, feat, workspace, cv_out, s); break;
-    case 4: launch_fused<4, true>(g, feat, workspace, cv_out, s); break;
-    case 5: launch_fused<5, true>(g, feat, workspace, cv_out, s); break;
-    case 6: case 7: case 8: launch_fused<8, false>(g, feat, workspace, cv_out, s); break;
-    default: launch_fused<MVS_MAX_VIEWS, false>(g, feat, workspace, cv_out, s); break;
+    case 2: launch_lds<2, MVS_EXP_CH3>(g, feat, workspace, packed, cv_out, s); break;
+    case 3: launch_lds<3, MVS_EXP_CH3>(g, feat, workspace, packed, cv_out, s); break;
+    case 4: launch_lds<4, 4>(g, feat, workspace, packed, cv_out, s); break;
+    case 5: launch_lds<5, 4>(g, feat, workspace, packed, cv_out, s); break;
+    case 6: launch_lds<6, 4>(g, feat, workspace, packed, cv_out, s); break;
+    case 7: launch_lds<7, 4>(g, feat, workspace, packed, cv_out, s); break;
+    default: launch_lds<8, 4>(g, feat, workspace, packed, cv_out, s); break;
   }
   return hip_status();
 }

@@ -16,7 +16,8 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmvs_cost_volume.so"
-LIB_PATH = os.path.join(_HERE, LIB_NAME)
+# MVS_LIB_PATH: load another build of the same ABI (A/B kernel experiments, tools/exp_*.sh)
+LIB_PATH = os.environ.get("MVS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
 ABI_VERSION = 1
 
 MVS_OK = 0
@@ -30,6 +31,8 @@ SIGNATURES = {
     "mvs_abi_version": (_c_int, []),
     "mvs_status_string": (ctypes.c_char_p, [_c_int]),
     "mvs_sampling_workspace_bytes": (ctypes.c_size_t, [_c_int, _c_int]),
+    "mvs_cost_volume_workspace_bytes": (ctypes.c_size_t, [_c_int, _c_int, _c_int, _c_int, _c_int,
+                                                           _c_int]),
     "mvs_plane_sampling": (_c_int, [_p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int,
                                     _c_int, _c_float, _p, _p]),
     "mvs_cost_volume_fwd": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,

@@ -53,7 +53,8 @@ def _check_geometry(feat, K, batch_size, n_views):
 def cost_volume(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.Tensor,
                 d_min: torch.Tensor, d_int: torch.Tensor, batch_size: int, n_views: int,
                 d_begin: int, d_count: int, d_scale: float) -> tuple[torch.Tensor, torch.Tensor]:
-    """Fused warp + variance: returns (cv [B,C,d_count,h,w], sampling workspace [N*d_count*9])."""
+    """Fused warp + variance: returns (cv [B,C,d_count,h,w], workspace).  The workspace starts
+    with the per-(image, plane) sampling matrices the backward reuses."""
     _require_gpu(feat, "feature_maps")
     lib = _lib.load()
     feat = feat.to(_F32).contiguous()
@@ -61,7 +62,8 @@ def cost_volume(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.T
     _check_geometry(feat, K, batch_size, n_views)
     n, c, h, w = feat.shape
     cv = torch.empty((batch_size, c, d_count, h, w), device=feat.device, dtype=_F32)
-    ws = torch.empty((n * d_count * 9,), device=feat.device, dtype=_F32)
+    ws_bytes = lib.mvs_cost_volume_workspace_bytes(batch_size, n_views, c, h, w, d_count)
+    ws = torch.empty((max(ws_bytes, 4) // 4,), device=feat.device, dtype=_F32)
     st = lib.mvs_cost_volume_fwd(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T),
                                  _lib.ptr(d_min), _lib.ptr(d_int), batch_size, n_views, c, h, w,
                                  d_begin, d_count, float(d_scale), _lib.ptr(ws), _lib.ptr(cv),
@@ -73,7 +75,9 @@ def cost_volume(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.T
 @cost_volume.register_fake
 def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scale):
     n, c, h, w = feat.shape
-    return (feat.new_empty((batch_size, c, d_count, h, w)), feat.new_empty((n * d_count * 9,)))
+    ch = 8 if n_views <= 3 else 4
+    ws = ((n * d_count * 9 * 4 + 255) // 256 * 256 + n * ((c + ch - 1) // ch) * ch * h * w * 4) // 4
+    return (feat.new_empty((batch_size, c, d_count, h, w)), feat.new_empty((ws,)))
 
 
 @torch.library.custom_op("mvs::cost_volume_backward", mutates_args=())

@@ -62,11 +62,19 @@ int mvs_plane_sampling(const float* K, const float* R, const float* T,
                        float* sampling, void* stream);
 
 /*
+ * Bytes of the workspace mvs_cost_volume_fwd needs: the sampling matrices (first
+ * mvs_sampling_workspace_bytes(N, d_count) bytes, rounded up to 256) followed by a copy of the
+ * features packed channel-chunk-last ([N][C/CH][h][w][CH], CH = 8 for n_views <= 3 else 4).
+ */
+size_t mvs_cost_volume_workspace_bytes(int batch_size, int n_views, int channels, int h, int w,
+                                       int d_count);
+
+/*
  * FUSED warp + variance: cv[B][C][d_count][h][w] from feat[N][C][h][w].
  * Replaces homography.py:6-92 + costvolume.py:3-16 (model.py:177-181) in one pass; the
  * warped N x C x D x h x w volume is never materialised.  `workspace` must hold
- * mvs_sampling_workspace_bytes(N, d_count) bytes; on return it holds the sampling matrices
- * (reused by mvs_cost_volume_bwd).
+ * mvs_cost_volume_workspace_bytes(...) bytes; on return its first part holds the sampling
+ * matrices (reused by mvs_cost_volume_bwd).
  */
 int mvs_cost_volume_fwd(const float* feat, const float* K, const float* R, const float* T,
                         const float* d_min, const float* d_int,
