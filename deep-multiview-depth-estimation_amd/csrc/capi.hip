@@ -1,0 +1,154 @@
+// capi.hip -- the C ABI declared in include/mvs_cost_volume.h (drop-in boundary, SURVEY.md §8 b).
+//
+// Validates arguments, lays out the caller-provided workspace and enqueues the launchers of the
+// other translation units on the caller's stream.  No allocation, no synchronisation, no global
+// mutable state: every entry point is re-entrant per stream and graph-capturable.
+#include "launchers.h"
+
+namespace {
+
+using mvs::Geometry;
+
+int check_geometry(int B, int V, int C, int h, int w, int d_count, Geometry& g) {
+  if (B <= 0 || C <= 0 || h < 2 || w < 2 || d_count <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if (V < 1 || V > MVS_MAX_VIEWS) return MVS_ERR_UNSUPPORTED_VIEWS;
+  const uint64_t hw = (uint64_t)h * (uint64_t)w;
+  // per-image plane offsets are 32-bit; work ids are 32-bit ints; packed corners are 16-bit
+  if ((uint64_t)C * hw >= (1ull << 31) || h > 32000 || w > 32000) return MVS_ERR_TOO_LARGE;
+  const uint64_t tiles = (hw + mvs::kBlock - 1) / mvs::kBlock;
+  const uint64_t total = (uint64_t)B * tiles * (uint64_t)d_count;
+  if (total >= (1ull << 31) - 8) return MVS_ERR_TOO_LARGE;
+  g.B = B;
+  g.V = V;
+  g.C = C;
+  g.h = h;
+  g.w = w;
+  g.Dc = d_count;
+  g.tiles = (int)tiles;
+  g.total = (int)total;
+  return MVS_OK;
+}
+
+bool cams_ok(const float* K, const float* R, const float* T, const float* d_min, const float* d_int) {
+  return K && R && T && d_min && d_int;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mvs_abi_version(void) { return MVS_ABI_VERSION; }
+
+const char* mvs_status_string(int status) {
+  switch (status) {
+    case MVS_OK: return "ok";
+    case MVS_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case MVS_ERR_UNSUPPORTED_VIEWS: return "n_views outside [1, MVS_MAX_VIEWS]";
+    case MVS_ERR_TOO_LARGE: return "tensor exceeds the kernel's 32-bit index space";
+    case MVS_ERR_HIP: return "HIP runtime error";
+    default: return "unknown status";
+  }
+}
+
+size_t mvs_sampling_workspace_bytes(int n_images, int d_count) {
+  if (n_images <= 0 || d_count <= 0) return 0;
+  return (size_t)n_images * (size_t)d_count * 9 * sizeof(float);
+}
+
+size_t mvs_cost_volume_workspace_bytes(int batch_size, int n_views, int channels, int h, int w,
+                                       int d_count) {
+  if (batch_size <= 0 || n_views <= 0 || channels <= 0 || h <= 0 || w <= 0 || d_count <= 0) return 0;
+  return mvs::align256(mvs_sampling_workspace_bytes(batch_size * n_views, d_count)) +
+         mvs::packed_bytes(batch_size, n_views, channels, h, w);
+}
+
+int mvs_plane_sampling(const float* K, const float* R, const float* T, const float* d_min,
+                       const float* d_int, int batch_size, int n_views, int h, int w, int d_begin,
+                       int d_count, float d_scale, float* sampling, void* stream) {
+  if (!cams_ok(K, R, T, d_min, d_int) || !sampling) return MVS_ERR_INVALID_ARGUMENT;
+  if (batch_size <= 0 || h < 2 || w < 2 || d_count <= 0 || d_begin < 0)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (n_views < 1 || n_views > MVS_MAX_VIEWS) return MVS_ERR_UNSUPPORTED_VIEWS;
+  mvs::launch_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
+                             d_scale, sampling, (hipStream_t)stream);
+  return mvs::hip_status();
+}
+
+int mvs_cost_volume_fwd(const float* feat, const float* K, const float* R, const float* T,
+                        const float* d_min, const float* d_int, int batch_size, int n_views,
+                        int channels, int h, int w, int d_begin, int d_count, float d_scale,
+                        float* workspace, float* cv_out, void* stream) {
+  if (!feat || !workspace || !cv_out) return MVS_ERR_INVALID_ARGUMENT;
+  Geometry g;
+  int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g);
+  if (st != MVS_OK) return st;
+  st = mvs_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
+                          d_scale, workspace, stream);
+  if (st != MVS_OK) return st;
+  hipStream_t s = (hipStream_t)stream;
+  if (n_views == 1) {  // the variance of a single view is identically zero
+    if (hipMemsetAsync(cv_out, 0, (size_t)batch_size * channels * d_count * h * w * sizeof(float), s) !=
+        hipSuccess)
+      return MVS_ERR_HIP;
+    return mvs::hip_status();
+  }
+  float* packed = reinterpret_cast<float*>(
+      reinterpret_cast<char*>(workspace) +
+      mvs::align256(mvs_sampling_workspace_bytes(batch_size * n_views, d_count)));
+  mvs::launch_cost_volume_fwd(g, feat, workspace, packed, cv_out, s);
+  return mvs::hip_status();
+}
+
+int mvs_homography_warp_fwd(const float* feat, const float* K, const float* R, const float* T,
+                            const float* d_min, const float* d_int, int batch_size, int n_views,
+                            int channels, int h, int w, int d_begin, int d_count, float d_scale,
+                            float* workspace, float* warped_out, void* stream) {
+  if (!feat || !workspace || !warped_out) return MVS_ERR_INVALID_ARGUMENT;
+  Geometry g;
+  int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g);
+  if (st != MVS_OK) return st;
+  st = mvs_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
+                          d_scale, workspace, stream);
+  if (st != MVS_OK) return st;
+  mvs::launch_warp(g, feat, workspace, warped_out, (hipStream_t)stream);
+  return mvs::hip_status();
+}
+
+int mvs_assemble_cost_volume_fwd(const float* warped, int batch_size, int n_views, int channels,
+                                 int d, int h, int w, float* cv_out, void* stream) {
+  if (!warped || !cv_out || batch_size <= 0 || channels <= 0 || d <= 0 || h <= 0 || w <= 0)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (n_views < 1) return MVS_ERR_UNSUPPORTED_VIEWS;
+  mvs::launch_variance(warped, batch_size, n_views, (size_t)channels * d * h * w, cv_out,
+                       (hipStream_t)stream);
+  return mvs::hip_status();
+}
+
+int mvs_cost_volume_bwd(const float* feat, const float* sampling, const float* grad_cv,
+                        int batch_size, int n_views, int channels, int h, int w, int d_count,
+                        float* grad_feat, void* stream) {
+  if (!feat || !sampling || !grad_cv || !grad_feat) return MVS_ERR_INVALID_ARGUMENT;
+  Geometry g;
+  const int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g);
+  if (st != MVS_OK) return st;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(grad_feat, 0, (size_t)batch_size * n_views * channels * h * w * sizeof(float),
+                     s) != hipSuccess)
+    return MVS_ERR_HIP;
+  mvs::launch_cost_volume_bwd(g, feat, sampling, grad_cv, grad_feat, s);
+  return mvs::hip_status();
+}
+
+int mvs_extract_depth_map_fwd(const float* prob, const float* d_batch, int batch_size, int d,
+                              int h, int w, int n_est, float* depth_out, void* stream) {
+  if (!prob || !d_batch || !depth_out || batch_size <= 0 || d <= 0 || h <= 0 || w <= 0)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (n_est < 1) return MVS_ERR_INVALID_ARGUMENT;
+  if (n_est > d) n_est = d;  // every plane index is < n_est: all planes kept
+  if (n_est > 16) return MVS_ERR_INVALID_ARGUMENT;
+  mvs::launch_soft_argmin(prob, d_batch, batch_size, d, (uint32_t)h * (uint32_t)w, n_est, depth_out,
+                          (hipStream_t)stream);
+  return mvs::hip_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,181 @@
+// common.h -- device/host helpers shared by the MVSNet cost-volume kernels (gfx950 / CDNA4).
+//
+// Sampling law (scripts/homography.py:83-90 -> kornia 0.6.3 warp_perspective ->
+// torch grid_sample(bilinear, zeros, align_corners=False)):
+//   xn = (x / (w-1) - 0.5) * 2                         kornia create_meshgrid (normalised)
+//   [u, v, s] = G [xn, yn, 1]                           G = inv(Nrm H Nrm^-1), per (image, plane)
+//   (u, v) *= 1 / (s + 1e-8)   where |s| > 1e-8          kornia convert_points_from_homogeneous
+//   ix = (u + 1) * (w / 2) - 0.5                         grid_sample unnormalise (align_corners=False)
+//   out = sum of the 4 bilinear taps, taps outside the image contribute 0
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/mvs_cost_volume.h"
+
+namespace mvs {
+
+constexpr int kBlock = 256;
+constexpr uint32_t kInvalidTap = 0xFFFFFFFFu;
+
+// ------------------------------------------------------------------------------------------
+// sampling coordinates.  Every rounding step is explicit (__f*_rn) so that every call site -- every
+// view, every kernel -- produces bit-identical coordinates for identical inputs, whatever the
+// compiler's contraction choices in the surrounding code.
+// ------------------------------------------------------------------------------------------
+__device__ inline float norm_coord(uint32_t x, int size) {
+  return __fmul_rn(__fsub_rn(__fdiv_rn((float)x, (float)(size - 1)), 0.5f), 2.0f);
+}
+
+__device__ inline void sample_coord(const float* __restrict__ G, float xn, float yn, int h, int w,
+                                    float& ix, float& iy) {
+  float u = __fmaf_rn(G[1], yn, __fmaf_rn(G[0], xn, G[2]));
+  float v = __fmaf_rn(G[4], yn, __fmaf_rn(G[3], xn, G[5]));
+  const float s = __fmaf_rn(G[7], yn, __fmaf_rn(G[6], xn, G[8]));
+  if (fabsf(s) > 1e-8f) {
+    const float sc = __fdiv_rn(1.0f, __fadd_rn(s, 1e-8f));
+    u = __fmul_rn(u, sc);
+    v = __fmul_rn(v, sc);
+  }
+  ix = __fsub_rn(__fmul_rn(__fadd_rn(u, 1.0f), 0.5f * (float)w), 0.5f);
+  iy = __fsub_rn(__fmul_rn(__fadd_rn(v, 1.0f), 0.5f * (float)h), 0.5f);
+}
+
+// Compact tap state: integer corner (x0, y0) packed as ((y0 + 2) << 16) | (x0 + 2) plus the two
+// fractions.  Positions whose 4 taps all fall outside the image (ix < -1, ix >= w, ...) are
+// kInvalidTap: their sample is exactly 0.  Valid corners satisfy x0 in [-1, w-1], y0 in [-1, h-1].
+__device__ inline void src_coords(const float* __restrict__ G, float xn, float yn, int h, int w,
+                                  bool active, uint32_t& pos, float& wx, float& wy) {
+  float ix, iy;
+  sample_coord(G, xn, yn, h, w, ix, iy);
+  const bool ok = active && ix >= -1.0f && ix < (float)w && iy >= -1.0f && iy < (float)h;
+  const float fx = floorf(ok ? ix : 0.0f), fy = floorf(ok ? iy : 0.0f);
+  wx = ok ? ix - fx : 0.0f;
+  wy = ok ? iy - fy : 0.0f;
+  pos = ok ? ((uint32_t)((int)fy + 2) << 16) | (uint32_t)((int)fx + 2) : kInvalidTap;
+}
+
+__device__ inline int pos_x(uint32_t p) { return (int)(p & 0xFFFFu) - 2; }
+__device__ inline int pos_y(uint32_t p) { return (int)(p >> 16) - 2; }
+
+// bilinear weights of the nw, ne, sw, se taps (torch CPU grid_sample: nw = (1-fy)(1-fx) ...)
+__device__ inline void tap_weights(float wx, float wy, float (&wt)[4]) {
+  const float ex = 1.0f - wx, ny = 1.0f - wy;
+  wt[0] = ny * ex;
+  wt[1] = ny * wx;
+  wt[2] = wy * ex;
+  wt[3] = wy * wx;
+}
+
+// ------------------------------------------------------------------------------------------
+// per-lane taps into an NCHW plane (generic / warp / backward kernels): byte offsets + weights,
+// out-of-image taps get weight 0 and offset 0
+// ------------------------------------------------------------------------------------------
+struct Taps {
+  uint32_t off[4];
+  float wt[4];
+};
+
+__device__ inline void make_taps(const float* __restrict__ G, float xn, float yn, int h, int w,
+                                 Taps& tp) {
+  float ix, iy;
+  sample_coord(G, xn, yn, h, w, ix, iy);
+  if (!(ix > -2.0f && ix < (float)w + 1.0f && iy > -2.0f && iy < (float)h + 1.0f)) {
+    ix = -4.0f;  // far outside or NaN: every tap invalid, int conversion stays in range
+    iy = -4.0f;
+  }
+  const float fx = floorf(ix), fy = floorf(iy);
+  const int x0 = (int)fx, y0 = (int)fy;
+  float wt[4];
+  tap_weights(ix - fx, iy - fy, wt);
+  const bool vx0 = x0 >= 0 && x0 < w, vx1 = x0 + 1 >= 0 && x0 + 1 < w;
+  const bool vy0 = y0 >= 0 && y0 < h, vy1 = y0 + 1 >= 0 && y0 + 1 < h;
+  const uint32_t base = (uint32_t)(y0 * w + x0) * 4u;
+  const bool ok[4] = {vx0 && vy0, vx1 && vy0, vx0 && vy1, vx1 && vy1};
+  const uint32_t off[4] = {base, base + 4u, base + 4u * (uint32_t)w, base + 4u * (uint32_t)w + 4u};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    tp.wt[t] = ok[t] ? wt[t] : 0.0f;
+    tp.off[t] = ok[t] ? off[t] : 0u;
+  }
+}
+
+__device__ inline float gather(const float* __restrict__ plane, const Taps& tp) {
+  const char* pb = reinterpret_cast<const char*>(plane);
+  auto ld = [&](int t) { return *reinterpret_cast<const float*>(pb + tp.off[t]); };
+  return ld(0) * tp.wt[0] + ld(1) * tp.wt[1] + ld(2) * tp.wt[2] + ld(3) * tp.wt[3];
+}
+
+// ------------------------------------------------------------------------------------------
+// buffer descriptors (cdna_hip_programming.md T8/T20): base/bytes must be workgroup-uniform
+// ------------------------------------------------------------------------------------------
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+__device__ inline Rsrc make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+
+__device__ inline float gather_buf(Rsrc rs, uint32_t soff, const Taps& tp) {
+  const float a = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, tp.off[0], soff, 0));
+  const float b = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, tp.off[1], soff, 0));
+  const float c = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, tp.off[2], soff, 0));
+  const float d = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, tp.off[3], soff, 0));
+  return a * tp.wt[0] + b * tp.wt[1] + c * tp.wt[2] + d * tp.wt[3];
+}
+
+__device__ inline void store_buf(Rsrc rs, uint32_t voff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, voff, 0, 0);
+}
+
+// ------------------------------------------------------------------------------------------
+// XCD-chunked work ids: workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
+// §Workgroup dispatch), so w = (L % 8) * ceil(T/8) + L / 8 hands each XCD a contiguous run of work
+// items -- neighbouring depth planes of one tile share source footprints through one 4 MiB L2.
+// Placement only changes speed, never results.
+// ------------------------------------------------------------------------------------------
+__device__ inline int xcd_work_id(int L, int total) {
+  const int q = (total + 7) >> 3;
+  return (L & 7) * q + (L >> 3);
+}
+
+inline dim3 xcd_grid(int total) { return dim3(8u * (unsigned)((total + 7) / 8)); }
+
+// flattened-pixel work item (generic / warp / backward kernels): 256 consecutive pixels of one
+// (sample, plane)
+struct WorkItem {
+  int b, kk, tile;
+};
+
+__device__ inline WorkItem decode_flat(int wk, int Dc, int tiles) {
+  WorkItem it;
+  it.kk = wk % Dc;
+  const int t = wk / Dc;
+  it.tile = t % tiles;
+  it.b = t / tiles;
+  return it;
+}
+
+__device__ inline void pixel_coords(uint32_t p, int w, int h, float& xn, float& yn) {
+  const uint32_t y = p / (uint32_t)w;
+  const uint32_t x = p - y * (uint32_t)w;
+  xn = norm_coord(x, w);
+  yn = norm_coord(y, h);
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+struct Geometry {
+  int B, V, C, h, w, Dc;
+  int tiles;  // flattened 256-pixel tiles per plane
+  int total;  // flattened work items (B * tiles * Dc)
+};
+
+inline int hip_status() { return hipGetLastError() == hipSuccess ? MVS_OK : MVS_ERR_HIP; }
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace mvs

@@ -1,0 +1,82 @@
+// cost_volume_bwd.hip -- gradient of the fused warp + variance w.r.t. the features.
+//
+// Autograd of costvolume.py:14 (d cv / d x_v = 2 (x_v - mean) / V) composed with the
+// grid_sample backward of homography.py:86 (each sample's gradient is scattered to its 4 bilinear
+// taps), as train.py:103 exercises it.  One thread per output pixel of one (sample, plane): the
+// samples are recomputed (no warped volume is stored) and scattered with float atomics into
+// grad_feat[N][C][h][w] -- like torch's grid_sample backward on GPU, the summation order is not
+// deterministic.
+#include "launchers.h"
+
+namespace mvs {
+namespace {
+
+// backward: g_x_v = 2 (x_v - mean) / V * g_cv, scattered to the 4 taps with bilinear weights
+template <int MAXV, bool EXACT>
+__global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
+    const float* __restrict__ feat, const float* __restrict__ sampling,
+    const float* __restrict__ grad_cv, float* __restrict__ grad_feat, int nv_rt, int C, int h,
+    int w, int Dc, int tiles, int total) {
+  const int wk = xcd_work_id(blockIdx.x, total);
+  if (wk >= total) return;
+  const int V = EXACT ? MAXV : nv_rt;
+  const WorkItem it = decode_flat(wk, Dc, tiles);
+  const uint32_t hw = (uint32_t)h * (uint32_t)w;
+  const uint32_t p = (uint32_t)it.tile * kBlock + threadIdx.x;
+  if (p >= hw) return;
+  float xn, yn;
+  pixel_coords(p, w, h, xn, yn);
+  Taps tp[MAXV];
+#pragma unroll
+  for (int v = 0; v < MAXV; ++v)
+    if (v < V) make_taps(sampling + ((size_t)(it.b * V + v) * Dc + it.kk) * 9, xn, yn, h, w, tp[v]);
+  const float* fb = feat + (size_t)it.b * V * C * hw;
+  float* gb = grad_feat + (size_t)it.b * V * C * hw;
+  const float* gcv = grad_cv + ((size_t)it.b * C * Dc + it.kk) * hw + p;
+  const float inv_v = 1.0f / (float)V;
+  for (int c = 0; c < C; ++c) {
+    const float g = gcv[(size_t)c * Dc * hw];
+    float val[MAXV];
+    float sum = 0.0f;
+#pragma unroll
+    for (int v = 0; v < MAXV; ++v)
+      if (v < V) {
+        val[v] = gather(fb + ((size_t)v * C + c) * hw, tp[v]);
+        sum += val[v];
+      }
+    const float mean = sum * inv_v;
+    const float k2 = 2.0f * inv_v * g;
+#pragma unroll
+    for (int v = 0; v < MAXV; ++v)
+      if (v < V) {
+        const float coef = k2 * (val[v] - mean);
+        char* plane = reinterpret_cast<char*>(gb + ((size_t)v * C + c) * hw);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)  // off[] are byte offsets
+          if (tp[v].wt[t] != 0.0f)
+            unsafeAtomicAdd(reinterpret_cast<float*>(plane + tp[v].off[t]), tp[v].wt[t] * coef);
+      }
+  }
+}
+
+template <int MAXV, bool EXACT>
+void launch_bwd(const Geometry& g, const float* feat, const float* smp, const float* gcv,
+                float* gf, hipStream_t s) {
+  hipLaunchKernelGGL((cost_volume_bwd_kernel<MAXV, EXACT>), xcd_grid(g.total), dim3(kBlock), 0, s,
+                     feat, smp, gcv, gf, g.V, g.C, g.h, g.w, g.Dc, g.tiles, g.total);
+}
+
+}  // namespace
+
+void launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* sampling,
+                            const float* grad_cv, float* grad_feat, hipStream_t s) {
+  switch (g.V) {
+    case 1: launch_bwd<1, true>(g, feat, sampling, grad_cv, grad_feat, s); break;
+    case 2: launch_bwd<2, true>(g, feat, sampling, grad_cv, grad_feat, s); break;
+    case 3: launch_bwd<3, true>(g, feat, sampling, grad_cv, grad_feat, s); break;
+    case 5: launch_bwd<5, true>(g, feat, sampling, grad_cv, grad_feat, s); break;
+    default: launch_bwd<MVS_MAX_VIEWS, false>(g, feat, sampling, grad_cv, grad_feat, s); break;
+  }
+}
+
+}  // namespace mvs

@@ -1,0 +1,36 @@
+// launchers.h -- host-side launchers, one per translation unit; the C ABI (capi.hip) calls these.
+// Arguments are validated by the caller; launchers only enqueue work on `s` and never allocate or
+// synchronise (graph-capturable).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+
+namespace mvs {
+
+// plane_sampling.hip: sampling[N][d_count][9] (fp64 geometry, stored fp32)
+void launch_plane_sampling(const float* K, const float* R, const float* T, const float* d_min,
+                           const float* d_int, int B, int V, int h, int w, int d_begin,
+                           int d_count, float d_scale, float* sampling, hipStream_t s);
+
+// cost_volume_fwd.hip: fused warp + variance.  `packed` is the workspace area after the sampling
+// matrices (packed_bytes()).
+size_t packed_bytes(int B, int V, int C, int h, int w);
+void launch_cost_volume_fwd(const Geometry& g, const float* feat, const float* sampling,
+                            float* packed, float* cv, hipStream_t s);
+
+// warp_variance.hip
+void launch_warp(const Geometry& g, const float* feat, const float* sampling, float* warped,
+                 hipStream_t s);
+void launch_variance(const float* warped, int B, int V, size_t M, float* cv, hipStream_t s);
+
+// cost_volume_bwd.hip (grad_feat must be zeroed)
+void launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* sampling,
+                            const float* grad_cv, float* grad_feat, hipStream_t s);
+
+// soft_argmin.hip
+void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, uint32_t hw,
+                        int n_est, float* depth, hipStream_t s);
+
+}  // namespace mvs

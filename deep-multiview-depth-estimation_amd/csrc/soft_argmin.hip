@@ -1,0 +1,71 @@
+// soft_argmin.hip -- depthmap.py:4-22 (extract_depth_map) with the reference's permutation-indexed
+// mask: plane r is kept when argsort_desc(P)[r] < n_est.  Instead of sorting D values per pixel,
+// the rank of each of the first n_est planes is counted in one pass over D (ties ordered by
+// ascending plane index, i.e. stable -- what torch's CPU sort does for D <= 16; above that torch's
+// order for exact ties is implementation-defined).  One thread per pixel; the D reads of a pixel
+// are coalesced across the wave (stride h*w).
+#include "launchers.h"
+
+namespace mvs {
+namespace {
+
+// depthmap.py:4-22.  rank_j = #{m : P_m > P_j} + #{m < j : P_m == P_j} is the sorted position of
+// plane j (descending, ties by ascending index); mask[r] = 1 exactly at r = rank_j, j < n_est.
+template <int MAXE>
+__global__ __launch_bounds__(kBlock) void soft_argmin_kernel(const float* __restrict__ prob,
+                                                             const float* __restrict__ d_batch,
+                                                             int B, int D, uint32_t hw, int n_est,
+                                                             float* __restrict__ depth) {
+  const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= (size_t)B * hw) return;
+  const size_t b = e / hw, p = e - b * hw;
+  const float* P = prob + b * D * hw + p;
+  const float* db = d_batch + b * D;
+  float pj[MAXE];
+  int rank[MAXE];
+#pragma unroll
+  for (int j = 0; j < MAXE; ++j) {
+    pj[j] = (j < n_est) ? P[(size_t)j * hw] : 0.0f;
+    rank[j] = 0;
+  }
+  for (int m = 0; m < D; ++m) {
+    const float pm = P[(size_t)m * hw];
+#pragma unroll
+    for (int j = 0; j < MAXE; ++j) rank[j] += (pm > pj[j]) || (pm == pj[j] && m < j);
+  }
+  // sum in ascending plane order, as the masked sum over dim 2 does
+#pragma unroll
+  for (int a = 1; a < MAXE; ++a)
+#pragma unroll
+    for (int c = a; c > 0; --c)
+      if (c < n_est && rank[c] < rank[c - 1]) {
+        const int t = rank[c];
+        rank[c] = rank[c - 1];
+        rank[c - 1] = t;
+      }
+  float num = 0.0f, den = 0.0f;
+#pragma unroll
+  for (int j = 0; j < MAXE; ++j)
+    if (j < n_est) {
+      const float pr = P[(size_t)rank[j] * hw];
+      num += db[rank[j]] * pr;
+      den += pr;
+    }
+  depth[e] = num / den;
+}
+
+}  // namespace
+
+void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, uint32_t hw,
+                        int n_est, float* depth, hipStream_t s) {
+  const size_t n = (size_t)B * hw;
+  const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+  if (n_est <= 8)
+    hipLaunchKernelGGL((soft_argmin_kernel<8>), grid, dim3(kBlock), 0, s, prob, d_batch, B, D, hw,
+                       n_est, depth);
+  else
+    hipLaunchKernelGGL((soft_argmin_kernel<16>), grid, dim3(kBlock), 0, s, prob, d_batch, B, D, hw,
+                       n_est, depth);
+}
+
+}  // namespace mvs

@@ -6,8 +6,13 @@ import subprocess
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-SOURCES = [os.path.join(PKG_ROOT, "csrc", "mvs_cost_volume.hip")]
-HEADERS = [os.path.join(REPO_ROOT, "include", "mvs_cost_volume.h")]
+CSRC = os.path.join(PKG_ROOT, "csrc")
+# one translation unit per kernel family + the C ABI (capi.hip); launchers.h declares the seams
+SOURCES = [os.path.join(CSRC, f) for f in ("capi.hip", "plane_sampling.hip", "cost_volume_fwd.hip",
+                                           "cost_volume_bwd.hip", "warp_variance.hip",
+                                           "soft_argmin.hip")]
+HEADERS = [os.path.join(REPO_ROOT, "include", "mvs_cost_volume.h"),
+           os.path.join(CSRC, "common.h"), os.path.join(CSRC, "launchers.h")]
 OUTPUT = os.path.join(_HERE, "libmvs_cost_volume.so")
 ARCH = os.environ.get("MVS_OFFLOAD_ARCH", "gfx950")
 
@@ -19,16 +24,17 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def build_library(force=False, verbose=False):
+def build_library(force=False, verbose=False, extra_flags=(), output=None):
     """Compile the HIP sources into OUTPUT unless it is newer than every source/header."""
-    if not force and os.path.exists(OUTPUT):
+    out = output or OUTPUT
+    if not force and not extra_flags and os.path.exists(out):
         newest = max(os.path.getmtime(p) for p in SOURCES + HEADERS)
-        if os.path.getmtime(OUTPUT) >= newest:
-            return OUTPUT
+        if os.path.getmtime(out) >= newest:
+            return out
     cmd = [hipcc(), "-O3", "-std=c++17", "--offload-arch=%s" % ARCH, "-fPIC", "-shared",
-           "-o", OUTPUT + ".tmp"] + SOURCES
+           "-parallel-jobs=%d" % min(8, os.cpu_count() or 1), "-o", out + ".tmp"] + list(extra_flags) + SOURCES
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
-    os.replace(OUTPUT + ".tmp", OUTPUT)
-    return OUTPUT
+    os.replace(out + ".tmp", out)
+    return out

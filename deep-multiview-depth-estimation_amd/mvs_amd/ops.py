@@ -75,8 +75,7 @@ def cost_volume(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.T
 @cost_volume.register_fake
 def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scale):
     n, c, h, w = feat.shape
-    ch = 8 if n_views <= 3 else 4
-    ws = ((n * d_count * 9 * 4 + 255) // 256 * 256 + n * ((c + ch - 1) // ch) * ch * h * w * 4) // 4
+    ws = ((n * d_count * 9 * 4 + 255) // 256 * 256 + n * ((c + 3) // 4) * 4 * h * w * 4) // 4
     return (feat.new_empty((batch_size, c, d_count, h, w)), feat.new_empty((ws,)))
 
 

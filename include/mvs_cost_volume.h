@@ -64,7 +64,7 @@ int mvs_plane_sampling(const float* K, const float* R, const float* T,
 /*
  * Bytes of the workspace mvs_cost_volume_fwd needs: the sampling matrices (first
  * mvs_sampling_workspace_bytes(N, d_count) bytes, rounded up to 256) followed by a copy of the
- * features packed channel-chunk-last ([N][C/CH][h][w][CH], CH = 8 for n_views <= 3 else 4).
+ * features packed channel-quad-last ([N][ceil(C/4)][h][w][4], zero-padded channels).
  */
 size_t mvs_cost_volume_workspace_bytes(int batch_size, int n_views, int channels, int h, int w,
                                        int d_count);
