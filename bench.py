@@ -28,11 +28,16 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 REPO = os.path.dirname(os.path.abspath(__file__))
+# MIOpen find results for the regulariser's convolutions ship with the repo (a text database of
+# chosen solvers, tools/miopen_db), so a fresh box skips most of the multi-minute search.  Must be
+# set before torch initialises MIOpen.
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(REPO, "tools", "miopen_db"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
 for sub in ("deep-multiview-depth-estimation_amd", os.path.join("tests", "golden")):
     sys.path.insert(0, os.path.join(REPO, sub))
 
@@ -57,6 +62,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-planes", type=int, default=None, help="planes for the CPU sample")
     ap.add_argument("--kernel-only", action="store_true", help="skip the end-to-end forward")
+    ap.add_argument("--conv-search", choices=("on", "off"), default="on",
+                    help="torch.backends.cudnn.benchmark (MIOpen find) for the regulariser convs")
     return ap.parse_args()
 
 
@@ -172,7 +179,7 @@ def main():
         D = args.planes or 256
         if D % world:
             raise SystemExit("D=%d not divisible by world size %d" % (D, world))
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = args.conv_search == "on"
 
     result = {}
     ms_step = None

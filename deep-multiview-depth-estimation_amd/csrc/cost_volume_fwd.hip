@@ -122,7 +122,10 @@ constexpr int kLdsSlots = 2560;           // 40 KB of float4 slots -> 4 workgrou
 constexpr int kPrefetch = 4;              // staging pieces per thread carried in registers
 
 template <int V>
-constexpr int group_planes() { return V <= 5 ? 4 : 2; }
+#ifndef MVS_EXP_PG
+#define MVS_EXP_PG 4
+#endif
+constexpr int group_planes() { return V <= 5 ? MVS_EXP_PG : 2; }
 
 // Footprint of one view in LDS: pixels [x0, x0+rw) x [y0, y0+rh), row-major from slot `base`.
 struct Region {
@@ -432,6 +435,86 @@ __global__ __launch_bounds__(kBlock) void cost_volume_tile_kernel(
   }
 }
 
+// Direct-gather variant: same tiling, tap state and stores as the LDS kernel, but every view is
+// sampled straight from the packed global features (one 16-B load per tap and 4-channel chunk);
+// no LDS, no barriers, so occupancy is set by registers alone.
+template <int V, int KPG>
+__global__ __launch_bounds__(kBlock) void cost_volume_direct_tile_kernel(
+    const float4* __restrict__ packed, const float* __restrict__ sampling, float* __restrict__ cv,
+    int C, int h, int w, int Dc, int pg, int tiles_x, int tiles_y, int groups, int total) {
+  constexpr int NS = V - 1;
+  const int wk = xcd_work_id(blockIdx.x, total);
+  if (wk >= total) return;
+  const int g = wk % groups;
+  const int t = wk / groups;
+  const int tile = t % (tiles_x * tiles_y);
+  const int b = t / (tiles_x * tiles_y);
+  const int px = (tile % tiles_x) * kTileW + (int)(threadIdx.x % kTileW);
+  const int py = (tile / tiles_x) * kTileH + (int)(threadIdx.x / kTileW);
+  const bool active = px < w && py < h;
+  if (!active) return;   // no barriers in this kernel
+  const int k0 = g * pg;
+  const int npl = min(pg, Dc - k0);
+  const uint32_t hw = (uint32_t)h * (uint32_t)w;
+  const int c4 = (C + 3) / 4;
+  const float xn = norm_coord(px, w);
+  const float yn = norm_coord(py, h);
+  uint32_t rpos;
+  float rwx, rwy;
+  src_coords(sampling + ((size_t)(b * V) * Dc + k0) * 9, xn, yn, h, w, true, rpos, rwx, rwy);
+  uint32_t pos[KPG][NS];
+  float fwx[KPG][NS], fwy[KPG][NS];
+#pragma unroll
+  for (int pl = 0; pl < KPG; ++pl)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      pos[pl][s] = kInvalidTap;
+      fwx[pl][s] = fwy[pl][s] = 0.0f;
+      if (pl < npl)
+        src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + k0 + pl) * 9, xn, yn, h, w, true,
+                   pos[pl][s], fwx[pl][s], fwy[pl][s]);
+    }
+  const float inv_v = 1.0f / (float)V;
+  float* obase = cv + ((size_t)b * C * Dc + (size_t)k0) * hw + (size_t)py * w + px;
+  for (int ch = 0; ch < c4; ++ch) {
+    const float4* src0 = packed + ((size_t)(b * V) * c4 + ch) * hw;
+    const float4 x0 = gather_glb4(src0, rpos, rwx, rwy, h, w);
+#pragma unroll
+    for (int pl = 0; pl < KPG; ++pl) {
+      if (pl >= npl) continue;
+      float4 xs[NS > 0 ? NS : 1];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        uint32_t tpos = pos[pl][s];
+        float twx = fwx[pl][s], twy = fwy[pl][s];
+        asm volatile("" : "+v"(tpos), "+v"(twx), "+v"(twy));
+        xs[s] = gather_glb4(packed + ((size_t)(b * V + 1 + s) * c4 + ch) * hw, tpos, twx, twy, h, w);
+      }
+      float* ob = obase + (size_t)pl * hw;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = ch * 4 + j;
+        if (c < C) {
+          const float a0 = (&x0.x)[j];
+          float sum = a0;
+#pragma unroll
+          for (int s = 0; s < NS; ++s) sum += (&xs[s].x)[j];
+          const float mean = sum * inv_v;
+          float d = a0 - mean;
+          float acc = d * d;
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            d = (&xs[s].x)[j] - mean;
+            acc += d * d;
+          }
+          __builtin_nontemporal_store(acc * inv_v, ob + (size_t)c * Dc * hw);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
 template <int V>
 void launch_tile(const Geometry& g, const float* feat, const float* smp, float* packed, float* cv,
                  hipStream_t s) {
@@ -446,9 +529,15 @@ void launch_tile(const Geometry& g, const float* feat, const float* smp, float* 
   while (pg > 1 && (long)g.B * tiles_x * tiles_y * ((g.Dc + pg - 1) / pg) < 2048) pg >>= 1;
   const int groups = (g.Dc + pg - 1) / pg;
   const int total = g.B * tiles_x * tiles_y * groups;
+#if !defined(MVS_FWD_LDS)
+  hipLaunchKernelGGL((cost_volume_direct_tile_kernel<V, group_planes<V>()>), xcd_grid(total),
+                     dim3(kBlock), 0, s, reinterpret_cast<const float4*>(packed), smp, cv, g.C, g.h,
+                     g.w, g.Dc, pg, tiles_x, tiles_y, groups, total);
+#else
   hipLaunchKernelGGL((cost_volume_tile_kernel<V, group_planes<V>()>), xcd_grid(total), dim3(kBlock), 0,
                      s, reinterpret_cast<const float4*>(packed), smp, cv, g.C, g.h, g.w, g.Dc, pg,
                      tiles_x, tiles_y, groups, total);
+#endif
 }
 
 template <int MAXV, bool EXACT>
