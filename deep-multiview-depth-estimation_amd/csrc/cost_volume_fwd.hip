@@ -125,7 +125,7 @@ template <int V>
 #ifndef MVS_EXP_PG
 #define MVS_EXP_PG 4
 #endif
-constexpr int group_planes() { return V <= 5 ? MVS_EXP_PG : 2; }
+constexpr int group_planes() { return V <= 3 ? MVS_EXP_PG : (V <= 5 ? 4 : 2); }
 
 // Footprint of one view in LDS: pixels [x0, x0+rw) x [y0, y0+rh), row-major from slot `base`.
 struct Region {
