@@ -241,7 +241,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": gbs / HBM_PEAK_GBS,
                      "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
-                     "kernel": "cost_volume_kernel (+ plane_sampling_kernel)", "kernel_ms": k_ms,
+                     "kernel": "cost_volume_direct_tile_kernel (+ pack4_kernel, plane_sampling_kernel)", "kernel_ms": k_ms,
                      "alg_bytes_per_launch": alg},
         "hot_path": {"cost_volumes_per_s": B / (k_ms * 1e-3), "kernel_ms": k_ms},
     }
