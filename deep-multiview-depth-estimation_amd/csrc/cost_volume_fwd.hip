@@ -91,87 +91,265 @@ __global__ __launch_bounds__(kBlock) void cost_volume_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
-// packing: feat[N][C][h][w] -> packed[N][C4][h][w] float4, C4 = ceil(C / 4), zero-padded channels
+// Padded channel-quad layout (workspace):
+//   packed[N][C4][h + 2][w + 2] float4, C4 = ceil(C / 4), channel 4q+j in component j (zero pad),
+//   pixel (x, y) at padded (x + 1, y + 1); columns 0, w + 1 and rows 0, h + 1 are zero.
+// Every tap corner the sampling law can produce (x0 in [-1, w-1], y0 in [-1, h-1]) then has its
+// four taps inside the padded plane, and out-of-image taps read zeros: the bilinear gather needs no
+// bounds test and no branch.  A sample whose corner lies outside that range (all four taps outside
+// the image, sample exactly 0) gets an out-of-range buffer offset: its loads return 0 without
+// touching memory (about half of all samples on DTU geometry at D=192).
+//   refs[B][C4][h][w] float4: the reference view resampled through its own (plane-independent)
+// sampling matrix -- identical arithmetic to an in-kernel gather, computed once per launch.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void pack4_kernel(const float* __restrict__ feat,
-                                                       float4* __restrict__ packed, int N, int C,
-                                                       uint32_t hw) {
+struct PadGeom {
+  int pitch;        // w + 2 slots per padded row
+  uint32_t plane;   // (h + 2) * pitch slots per padded plane
+};
+
+__host__ __device__ inline PadGeom pad_geom(int h, int w) {
+  PadGeom p;
+  p.pitch = w + 2;
+  p.plane = (uint32_t)(h + 2) * (uint32_t)(w + 2);
+  return p;
+}
+
+__global__ __launch_bounds__(kBlock) void pack_pad_kernel(const float* __restrict__ feat,
+                                                          float4* __restrict__ packed, int N, int C,
+                                                          int h, int w) {
   const int c4 = (C + 3) / 4;
-  const size_t n = (size_t)N * c4 * hw;
+  const PadGeom pg = pad_geom(h, w);
+  const uint32_t hw = (uint32_t)h * (uint32_t)w;
+  const size_t n = (size_t)N * c4 * pg.plane;
   for (size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (size_t)gridDim.x * kBlock) {
-    const size_t p = e % hw;
-    const size_t t = e / hw;
+    const uint32_t q = (uint32_t)(e % pg.plane);
+    const size_t t = e / pg.plane;
     const int ch = (int)(t % c4);
     const size_t i = t / c4;
-    float v[4];
+    const int y = (int)(q / (uint32_t)pg.pitch) - 1;
+    const int x = (int)(q % (uint32_t)pg.pitch) - 1;
+    float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (x >= 0 && x < w && y >= 0 && y < h) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = ch * 4 + j;
-      v[j] = c < C ? feat[(i * C + c) * hw + p] : 0.0f;
+      for (int j = 0; j < 4; ++j) {
+        const int c = ch * 4 + j;
+        if (c < C) v[j] = feat[(i * C + c) * hw + (size_t)y * w + x];
+      }
     }
     packed[e] = make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t kOobOffset = 0x80000000u;   // >= every descriptor's num_records
+
+// Tap state of one (pixel, plane, view): byte offset of the nw tap in the padded plane + fractions.
+__device__ inline uint32_t tap_offset(uint32_t pos, const PadGeom& pg) {
+  if (pos == kInvalidTap) return kOobOffset;
+  return ((uint32_t)(pos_y(pos) + 1) * (uint32_t)pg.pitch + (uint32_t)(pos_x(pos) + 1)) * 16u;
+}
+
+__device__ inline f4v ld4(Rsrc rs, uint32_t voff, int soff) {
+  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff, soff, 0));
+}
+
+// Bilinear sample of 4 channels: acc = 0, then fma(tap_t, weight_t, acc) over nw, ne, sw, se --
+// the order of every other gather in this library (zero taps add exactly nothing).  Packed fp32
+// FMAs (v_pk_fma_f32), elementwise identical to scalar fmaf.
+__device__ inline f4v bilerp(const f4v (&t)[4], float wx, float wy) {
+  // weights {nw, ne} = (1-wy) * {1-wx, wx}, {sw, se} = wy * {1-wx, wx}: tap_weights() in pairs
+  const f2v e = {1.0f - wx, wx};
+  const f2v w01 = f2v{1.0f - wy, 1.0f - wy} * e;
+  const f2v w23 = f2v{wy, wy} * e;
+  f2v lo = t[0].xy * w01.xx, hi = t[0].zw * w01.xx;   // fma(t, w, 0) == t * w
+  lo = __builtin_elementwise_fma(t[1].xy, w01.yy, lo);
+  hi = __builtin_elementwise_fma(t[1].zw, w01.yy, hi);
+  lo = __builtin_elementwise_fma(t[2].xy, w23.xx, lo);
+  hi = __builtin_elementwise_fma(t[2].zw, w23.xx, hi);
+  lo = __builtin_elementwise_fma(t[3].xy, w23.yy, lo);
+  hi = __builtin_elementwise_fma(t[3].zw, w23.yy, hi);
+  return f4v{lo.x, lo.y, hi.x, hi.y};
+}
+
+__device__ inline void load_taps(Rsrc rs, uint32_t voff, int soff, int row_bytes, f4v (&t)[4]) {
+  t[0] = ld4(rs, voff, soff);
+  t[1] = ld4(rs, voff + 16u, soff);
+  t[2] = ld4(rs, voff, soff + row_bytes);
+  t[3] = ld4(rs, voff + 16u, soff + row_bytes);
+}
+
+// costvolume.py:12-14: mean = sum / V, cv = sum (x - mean)^2 / V (two-pass), 4 channels at once;
+// every intermediate rounded as written (no contraction of the mean into the differences).
+template <int NS>
+__device__ inline f4v variance4(const f4v& x0, const f4v (&xs)[NS], const f4v& inv_v) {
+#pragma clang fp contract(off)
+  f4v sum = x0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) sum += xs[s];
+  const f4v nmean = -(sum * inv_v);   // x + (-mean) == x - mean exactly; keeps v_pk_add_f32
+  f4v d = x0 + nmean;
+  f4v acc = d * d;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    d = xs[s] + nmean;
+    acc = __builtin_elementwise_fma(d, d, acc);
+  }
+  return acc * inv_v;
+}
+
+// refs[b][ch][p] = bilinear sample of the reference image b*V through G(b*V, plane 0).
+__global__ __launch_bounds__(kBlock) void ref_resample_kernel(const float4* __restrict__ packed,
+                                                              const float* __restrict__ sampling,
+                                                              float4* __restrict__ refs, int B, int V,
+                                                              int C, int h, int w, int Dc) {
+  const int c4 = (C + 3) / 4;
+  const uint32_t hw = (uint32_t)h * (uint32_t)w;
+  const PadGeom pg = pad_geom(h, w);
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  const int ch = (int)blockIdx.y % c4;
+  const int b = (int)blockIdx.y / c4;
+  if (p >= hw) return;
+  const int y = (int)(p / (uint32_t)w), x = (int)(p % (uint32_t)w);
+  uint32_t pos;
+  float wx, wy;
+  src_coords(sampling + (size_t)(b * V) * Dc * 9, norm_coord(x, w), norm_coord(y, h), h, w, true, pos,
+             wx, wy);
+  const Rsrc rs = make_rsrc(packed + (size_t)(b * V) * c4 * pg.plane, (uint32_t)c4 * pg.plane * 16u);
+  f4v t[4];
+  load_taps(rs, tap_offset(pos, pg), (int)((uint32_t)ch * pg.plane * 16u), pg.pitch * 16, t);
+  const f4v r = bilerp(t, wx, wy);
+  refs[((size_t)b * c4 + ch) * hw + p] = make_float4(r.x, r.y, r.z, r.w);
+}
+
 // ------------------------------------------------------------------------------------------
-// tile kernel
+// Fused gather kernel (2 <= V <= 8).  A 256-thread workgroup owns a 32 x 8 pixel tile of one sample
+// and a group of up to KPG consecutive depth planes; one thread = one pixel.  Per thread, the tap
+// state of every (plane, source view) is computed once and kept in registers (3 VGPRs each); then
+// for every 4-channel chunk: one coalesced load of the resampled reference, and per plane 4
+// branch-free 16-byte buffer loads per source view, bilinear + two-pass variance in packed fp32,
+// four dword stores (32-pixel rows: 128-byte segments).
 // ------------------------------------------------------------------------------------------
 constexpr int kTileW = 32;
 constexpr int kTileH = kBlock / kTileW;   // 8
-constexpr int kLdsSlots = 2560;           // 40 KB of float4 slots -> 4 workgroups per CU
-constexpr int kPrefetch = 4;              // staging pieces per thread carried in registers
 
 template <int V>
-#ifndef MVS_EXP_PG
-#define MVS_EXP_PG 4
+constexpr int group_planes() {
+#ifdef MVS_EXP_PG
+  return MVS_EXP_PG;
+#else
+  return V <= 3 ? 8 : (V <= 5 ? 4 : 2);
 #endif
-constexpr int group_planes() { return V <= 3 ? MVS_EXP_PG : (V <= 5 ? 4 : 2); }
-
-// Footprint of one view in LDS: pixels [x0, x0+rw) x [y0, y0+rh), row-major from slot `base`.
-struct Region {
-  int x0, y0, rw, rh, base;
-};
-
-__device__ inline float4 f4zero() { return make_float4(0.0f, 0.0f, 0.0f, 0.0f); }
-
-__device__ inline void fma4(float4& acc, const float4& a, float w) {
-  acc.x = __fmaf_rn(a.x, w, acc.x);
-  acc.y = __fmaf_rn(a.y, w, acc.y);
-  acc.z = __fmaf_rn(a.z, w, acc.z);
-  acc.w = __fmaf_rn(a.w, w, acc.w);
 }
 
-// bilinear sample of 4 channels from a staged region
-__device__ inline float4 gather_lds4(const float4* lds, const Region& r, uint32_t pos, float wx,
-                                     float wy) {
-  float4 acc = f4zero();
-  if (pos == kInvalidTap) return acc;
-  const int p = r.base + (pos_y(pos) - r.y0) * r.rw + (pos_x(pos) - r.x0);
-  float wt[4];
-  tap_weights(wx, wy, wt);
-  fma4(acc, lds[p], wt[0]);
-  fma4(acc, lds[p + 1], wt[1]);
-  fma4(acc, lds[p + r.rw], wt[2]);
-  fma4(acc, lds[p + r.rw + 1], wt[3]);
-  return acc;
-}
+template <int V, int KPG>
+__global__ __launch_bounds__(kBlock) void cost_volume_gather_kernel(
+    const float4* __restrict__ packed, const float4* __restrict__ refs,
+    const float* __restrict__ sampling, float* __restrict__ cv, int C, int h, int w, int Dc, int pg_n,
+    int tiles_x, int tiles_y, int groups, int total) {
+  constexpr int NS = V - 1;
+  const int wk = xcd_work_id(blockIdx.x, total);
+  if (wk >= total) return;
+  const int g = wk % groups;
+  const int t = wk / groups;
+  const int tile = t % (tiles_x * tiles_y);
+  const int b = t / (tiles_x * tiles_y);
+  const int px = (tile % tiles_x) * kTileW + (int)(threadIdx.x % kTileW);
+  const int py = (tile / tiles_x) * kTileH + (int)(threadIdx.x / kTileW);
+  if (px >= w || py >= h) return;   // no barriers in this kernel
+  const int k0 = g * pg_n;
+  const int npl = min(pg_n, Dc - k0);
+  const uint32_t hw = (uint32_t)h * (uint32_t)w;
+  const int c4 = (C + 3) / 4;
+  const PadGeom pg = pad_geom(h, w);
+  const float xn = norm_coord(px, w);
+  const float yn = norm_coord(py, h);
 
-// bilinear sample of 4 channels straight from a packed global plane (fallback path)
-__device__ inline float4 gather_glb4(const float4* __restrict__ src, uint32_t pos, float wx, float wy,
-                                     int h, int w) {
-  float4 acc = f4zero();
-  if (pos == kInvalidTap) return acc;
-  const int x0 = pos_x(pos), y0 = pos_y(pos);
-  float wt[4];
-  tap_weights(wx, wy, wt);
+  uint32_t off[KPG][NS];
+  float fwx[KPG][NS], fwy[KPG][NS];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int x = x0 + (t & 1), y = y0 + (t >> 1);
-    const bool ok = x >= 0 && x < w && y >= 0 && y < h;
-    const float4 a = src[ok ? (size_t)y * w + x : 0];
-    fma4(acc, a, ok ? wt[t] : 0.0f);
+  for (int pl = 0; pl < KPG; ++pl)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      uint32_t pos = kInvalidTap;
+      fwx[pl][s] = fwy[pl][s] = 0.0f;
+      if (pl < npl)
+        src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + k0 + pl) * 9, xn, yn, h, w, true, pos,
+                   fwx[pl][s], fwy[pl][s]);
+      off[pl][s] = tap_offset(pos, pg);
+    }
+
+  Rsrc rs[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    rs[s] = make_rsrc(packed + (size_t)(b * V + 1 + s) * c4 * pg.plane, (uint32_t)c4 * pg.plane * 16u);
+  const int row_bytes = pg.pitch * 16;
+  const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
+  const uint32_t pix = (uint32_t)py * (uint32_t)w + (uint32_t)px;
+  const float4* rbase = refs + (size_t)b * c4 * hw + pix;
+  float* obase = cv + ((size_t)b * C * Dc + (size_t)k0) * hw + pix;
+  const size_t cstride = (size_t)Dc * hw;
+
+  for (int ch = 0; ch < c4; ++ch) {
+    const float4 r4 = rbase[(size_t)ch * hw];
+    const f4v x0 = {r4.x, r4.y, r4.z, r4.w};
+    const int soff = (int)((uint32_t)ch * pg.plane * 16u);
+#pragma unroll
+    for (int pl = 0; pl < KPG; ++pl) {
+      if (pl >= npl) break;
+      f4v xs[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+#ifdef MVS_EXP_BRANCH
+        f4v tp[4] = {};
+        if (off[pl][s] != kOobOffset) load_taps(rs[s], off[pl][s], soff, row_bytes, tp);
+#else
+        f4v tp[4];
+        load_taps(rs[s], off[pl][s], soff, row_bytes, tp);
+#endif
+        // opaque copies: the weights are rebuilt per chunk (3 VALU) instead of being held in 8
+        // VGPRs per (plane, view) across the chunk loop
+        float twx = fwx[pl][s], twy = fwy[pl][s];
+        asm volatile("" : "+v"(twx), "+v"(twy));
+        xs[s] = bilerp(tp, twx, twy);
+      }
+      const f4v acc = variance4<NS>(x0, xs, inv_v);
+      float* ob = obase + (size_t)pl * hw + (size_t)(ch * 4) * cstride;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (ch * 4 + j < C) {
+#ifdef MVS_EXP_NOSTORE
+          if (acc[j] == 12345.678f)
+#endif
+#ifdef MVS_EXP_NT
+          __builtin_nontemporal_store(acc[j], ob + (size_t)j * cstride);
+#else
+          ob[(size_t)j * cstride] = acc[j];
+#endif
+        }
+      }
+#ifndef MVS_EXP_NOSB
+      __builtin_amdgcn_sched_barrier(0);   // one plane's loads in flight per wave (VGPR budget)
+#endif
+    }
   }
-  return acc;
+}
+
+// ------------------------------------------------------------------------------------------
+// LDS-staged kernel (2 <= V <= 8), the default.  Same tiling, tap state and arithmetic as the gather
+// kernel above, but the source views are read from LDS: per 4-channel chunk the workgroup stages,
+// for every source view, the bounding box of all tap corners of its tile over its plane group
+// (the footprint, about 1.8 slots per pixel at P = 4 on DTU geometry) with one coalesced 16-byte
+// load per slot, and every bilinear tap is then a conflict-light ds_read_b128 (4 LDS cycles per
+// wave-instruction against about 12 texture-path cycles for a 16-byte global gather, measured
+// in tools/microbench/gather_patterns.hip).  Slots 0 and 1 hold zeros: a sample with every tap outside the
+// image reads them with weights (1, 0, 0, 0) and is exactly 0.  A workgroup whose footprint exceeds
+// the LDS budget falls back to the global gathers of the kernel above.
+// ------------------------------------------------------------------------------------------
+template <int V>
+constexpr int staged_slots() {
+  return V <= 3 ? 2050 : (V <= 5 ? 3074 : 4098);   // 32 / 48 / 64 KB: 4 / 3 / 2 workgroups per CU
 }
 
 // Workgroup-wide min of NV ints; every thread gets the result as a wave-uniform value.
@@ -197,53 +375,20 @@ __device__ inline void block_min(int (&v)[NV], int* scratch /* >= 4 * NV ints of
     for (int q = 1; q < kBlock / 64; ++q) x = min(x, scratch[q * NV + k]);
     v[k] = __builtin_amdgcn_readfirstlane(x);
   }
-  __syncthreads();
-}
-
-template <int V>
-struct Plan {
-  Region reg[V];
-  int cum[V + 1];    // prefix sums of region sizes (pieces = pixels)
-  float inv_rw[V];   // 1 / rw for the piece -> (row, col) split
-  bool fits;
-};
-
-// One staging piece = one pixel (float4) of one view's region.  Regions are selected with an
-// unrolled compare chain (static indices only: a runtime-indexed Region array would live in scratch).
-template <int V>
-__device__ inline int piece_slot(const Plan<V>& pl, int q, int& view, int& gx, int& gy) {
-  int v = 0, x0 = pl.reg[0].x0, y0 = pl.reg[0].y0, rw = pl.reg[0].rw, base = pl.reg[0].base, cum = 0;
-  float inv = pl.inv_rw[0];
-#pragma unroll
-  for (int k = 1; k < V; ++k)
-    if (q >= pl.cum[k]) {
-      v = k;
-      x0 = pl.reg[k].x0;
-      y0 = pl.reg[k].y0;
-      rw = pl.reg[k].rw;
-      base = pl.reg[k].base;
-      cum = pl.cum[k];
-      inv = pl.inv_rw[k];
-    }
-  view = v;
-  const int e = q - cum;
-  const int row = (int)(((float)e + 0.5f) * inv);
-  const int col = e - row * rw;
-  gx = x0 + col;
-  gy = y0 + row;
-  return base + e;
 }
 
 template <int V, int KPG>
-__global__ __launch_bounds__(kBlock) void cost_volume_tile_kernel(
-    const float4* __restrict__ packed, const float* __restrict__ sampling, float* __restrict__ cv,
-    int C, int h, int w, int Dc, int pg, int tiles_x, int tiles_y, int groups, int total) {
+__global__ __launch_bounds__(kBlock) void cost_volume_staged_kernel(
+    const float4* __restrict__ packed, const float4* __restrict__ refs,
+    const float* __restrict__ sampling, float* __restrict__ cv, int C, int h, int w, int Dc, int pg_n,
+    int tiles_x, int tiles_y, int groups, int total) {
   constexpr int NS = V - 1;
-  __shared__ float4 lds[kLdsSlots];
-  __shared__ int scratch[4 * 4 * V];
+  constexpr int SLOTS = staged_slots<V>();
+  __shared__ f4v lds[SLOTS];
+  __shared__ int scratch[4 * 4 * NS];
 
   const int wk = xcd_work_id(blockIdx.x, total);
-  if (wk >= total) return;
+  if (wk >= total) return;   // workgroup-uniform
   const int g = wk % groups;
   const int t = wk / groups;
   const int tile = t % (tiles_x * tiles_y);
@@ -251,17 +396,14 @@ __global__ __launch_bounds__(kBlock) void cost_volume_tile_kernel(
   const int px = (tile % tiles_x) * kTileW + (int)(threadIdx.x % kTileW);
   const int py = (tile / tiles_x) * kTileH + (int)(threadIdx.x / kTileW);
   const bool active = px < w && py < h;
-  const int k0 = g * pg;
-  const int npl = min(pg, Dc - k0);
+  const int k0 = g * pg_n;
+  const int npl = min(pg_n, Dc - k0);
   const uint32_t hw = (uint32_t)h * (uint32_t)w;
   const int c4 = (C + 3) / 4;
+  const PadGeom pg = pad_geom(h, w);
   const float xn = norm_coord(active ? px : 0, w);
   const float yn = norm_coord(active ? py : 0, h);
 
-  // tap state: view 0 (plane independent), then (plane, source view)
-  uint32_t rpos;
-  float rwx, rwy;
-  src_coords(sampling + ((size_t)(b * V) * Dc + k0) * 9, xn, yn, h, w, active, rpos, rwx, rwy);
   uint32_t pos[KPG][NS];
   float fwx[KPG][NS], fwy[KPG][NS];
 #pragma unroll
@@ -275,268 +417,189 @@ __global__ __launch_bounds__(kBlock) void cost_volume_tile_kernel(
                    pos[pl][s], fwx[pl][s], fwy[pl][s]);
     }
 
-  // footprints of planes [lo, hi): view 0 from rpos, source views from pos[lo..hi)
-  auto make_plan = [&](int lo, int hi, Plan<V>& P) {
-    int bb[4 * V];
+  // footprint of every source view: bounding box of the valid tap corners over the plane group
+  int bb[4 * NS];
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-      int mnx = 1 << 30, mny = 1 << 30, mxx = 1 << 30, mxy = 1 << 30;  // mx*: -(max + 1)
-      auto take = [&](uint32_t p) {
-        if (p != kInvalidTap) {
-          mnx = min(mnx, pos_x(p));
-          mny = min(mny, pos_y(p));
-          mxx = min(mxx, -(pos_x(p) + 1));
-          mxy = min(mxy, -(pos_y(p) + 1));
-        }
-      };
-      if (v == 0) {
-        take(rpos);
-      } else {
+  for (int s = 0; s < NS; ++s) {
+    int mnx = 1 << 30, mny = 1 << 30, mxx = 1 << 30, mxy = 1 << 30;   // mx*: -(max corner)
 #pragma unroll
-        for (int pl = 0; pl < KPG; ++pl)
-          if (pl >= lo && pl < hi) take(pos[pl][v - 1]);
-      }
-      bb[4 * v + 0] = mnx;
-      bb[4 * v + 1] = mny;
-      bb[4 * v + 2] = mxx;
-      bb[4 * v + 3] = mxy;
-    }
-    block_min<4 * V>(bb, scratch);
-    int off = 0;
-    P.cum[0] = 0;
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      Region& r = P.reg[v];
-      r.x0 = bb[4 * v + 0];
-      r.y0 = bb[4 * v + 1];
-      const int x1 = -bb[4 * v + 2], y1 = -bb[4 * v + 3];
-      const bool empty = r.x0 > x1;
-      r.rw = empty ? 0 : x1 - r.x0 + 1;
-      r.rh = empty ? 0 : y1 - r.y0 + 1;
-      r.base = off;
-      off += r.rw * r.rh;
-      P.cum[v + 1] = off;
-      P.inv_rw[v] = r.rw > 0 ? 1.0f / (float)r.rw : 0.0f;
-    }
-    P.fits = off <= kLdsSlots;
-  };
-
-  const float inv_v = 1.0f / (float)V;
-
-  // staging: pieces q = threadIdx.x + kBlock * j; the first kPrefetch per thread go through
-  // registers (issued early), the rest are copied synchronously
-  float4 pre[kPrefetch];
-  int pslot[kPrefetch];
-  auto src_of = [&](int v, int ch) {
-    return packed + ((size_t)(b * V + v) * c4 + ch) * hw;
-  };
-  auto prefetch = [&](const Plan<V>& P, int ch) {
-#pragma unroll
-    for (int j = 0; j < kPrefetch; ++j) {
-      const int q = (int)threadIdx.x + kBlock * j;
-      pslot[j] = -1;
-      pre[j] = f4zero();
-      if (q < P.cum[V]) {
-        int v, gx, gy;
-        pslot[j] = piece_slot<V>(P, q, v, gx, gy);
-        if (gx >= 0 && gx < w && gy >= 0 && gy < h) pre[j] = src_of(v, ch)[(size_t)gy * w + gx];
+    for (int pl = 0; pl < KPG; ++pl) {
+      const uint32_t p = pos[pl][s];
+      if (p != kInvalidTap) {
+        mnx = min(mnx, pos_x(p));
+        mny = min(mny, pos_y(p));
+        mxx = min(mxx, -pos_x(p));
+        mxy = min(mxy, -pos_y(p));
       }
     }
-  };
-  auto commit = [&](const Plan<V>& P, int ch) {
+    bb[4 * s + 0] = mnx;
+    bb[4 * s + 1] = mny;
+    bb[4 * s + 2] = mxx;
+    bb[4 * s + 3] = mxy;
+  }
+  block_min<4 * NS>(bb, scratch);
+  int rx0[NS], ry0[NS], rw[NS], cum[NS + 1];
+  cum[0] = 2;   // slots 0, 1: zeros
 #pragma unroll
-    for (int j = 0; j < kPrefetch; ++j)
-      if (pslot[j] >= 0) lds[pslot[j]] = pre[j];
-    for (int q = (int)threadIdx.x + kBlock * kPrefetch; q < P.cum[V]; q += kBlock) {
-      int v, gx, gy;
-      const int slot = piece_slot<V>(P, q, v, gx, gy);
-      lds[slot] = (gx >= 0 && gx < w && gy >= 0 && gy < h) ? src_of(v, ch)[(size_t)gy * w + gx]
-                                                           : f4zero();
-    }
-  };
+  for (int s = 0; s < NS; ++s) {
+    const bool empty = bb[4 * s] == (1 << 30);
+    rx0[s] = bb[4 * s];
+    ry0[s] = bb[4 * s + 1];
+    rw[s] = empty ? 0 : -bb[4 * s + 2] - rx0[s] + 2;   // taps x0 .. x0 + 1
+    const int rh = empty ? 0 : -bb[4 * s + 3] - ry0[s] + 2;
+    cum[s + 1] = cum[s] + rw[s] * rh;
+  }
 
-  // one plane's 4 channels: sample every view, two-pass variance, store
-  auto emit = [&](int pl, int ch, const float4& x0, const float4 (&xs)[NS > 0 ? NS : 1]) {
-    if (!active) return;
-    float* ob = cv + ((size_t)b * C * Dc + (size_t)(k0 + pl)) * hw + (size_t)py * w + px;
-    const float* xv0 = &x0.x;
+  const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
+  const uint32_t pix = (uint32_t)(active ? py : 0) * (uint32_t)w + (uint32_t)(active ? px : 0);
+  const float4* rbase = refs + (size_t)b * c4 * hw + pix;
+  float* obase = cv + ((size_t)b * C * Dc + (size_t)k0) * hw + pix;
+  const size_t cstride = (size_t)Dc * hw;
+
+  auto emit = [&](int pl, int ch, const f4v& x0, const f4v (&xs)[NS]) {
+    const f4v acc = variance4<NS>(x0, xs, inv_v);
+    float* ob = obase + (size_t)pl * hw + (size_t)(ch * 4) * cstride;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int c = ch * 4 + j;
-      if (c < C) {
-        float sum = xv0[j];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) sum += (&xs[s].x)[j];
-        const float mean = sum * inv_v;
-        float d = xv0[j] - mean;
-        float acc = d * d;
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          d = (&xs[s].x)[j] - mean;
-          acc += d * d;
-        }
-        __builtin_nontemporal_store(acc * inv_v, ob + (size_t)c * Dc * hw);
+      if (ch * 4 + j < C) {
+#ifdef MVS_EXP_PLAINST
+        ob[(size_t)j * cstride] = acc[j];
+#else
+        __builtin_nontemporal_store(acc[j], ob + (size_t)j * cstride);
+#endif
       }
     }
   };
 
-  Plan<V> P;
-  make_plan(0, npl, P);
-  const bool whole = P.fits;
-  const int nsub = whole ? 1 : npl;
-  for (int sr = 0; sr < nsub; ++sr) {
-    const int lo = whole ? 0 : sr, hi = whole ? npl : sr + 1;
-    if (!whole) make_plan(lo, hi, P);
-    if (P.fits) {
-      prefetch(P, 0);
-      for (int ch = 0; ch < c4; ++ch) {
-        __syncthreads();   // every wave is done reading the previous chunk
-        commit(P, ch);
-        __syncthreads();   // chunk ch is in LDS
-        if (ch + 1 < c4) prefetch(P, ch + 1);   // in flight during this chunk's stores
-        const float4 x0 = gather_lds4(lds, P.reg[0], rpos, rwx, rwy);
+  if (cum[NS] > SLOTS) {
+    // footprint beyond the LDS budget (extreme zoom / long epipolar sweep): global gathers
+    if (!active) return;   // no barriers below
+    Rsrc rs[NS];
 #pragma unroll
-        for (int pl = 0; pl < KPG; ++pl) {
-          if (pl < lo || pl >= hi) continue;
-          float4 xs[NS > 0 ? NS : 1];
-#pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            // opaque copies: keep per-(plane, view) address/weight math inside the chunk loop
-            uint32_t tpos = pos[pl][s];
-            float twx = fwx[pl][s], twy = fwy[pl][s];
-            asm volatile("" : "+v"(tpos), "+v"(twx), "+v"(twy));
-            xs[s] = gather_lds4(lds, P.reg[1 + s], tpos, twx, twy);
-          }
-          emit(pl, ch, x0, xs);
-          __builtin_amdgcn_sched_barrier(0);  // one plane's LDS reads in flight at a time
-        }
-      }
-      __syncthreads();   // LDS reused by the next sub-range's staging
-    } else {
-      // footprint too large even for one plane (extreme zoom): sample the packed global features.
-      // Rare, so kept register-light: runtime plane loop, taps recomputed from G.
-      for (int ch = 0; ch < c4; ++ch) {
-        const float4 x0 = gather_glb4(src_of(0, ch), rpos, rwx, rwy, h, w);
+    for (int s = 0; s < NS; ++s)
+      rs[s] = make_rsrc(packed + (size_t)(b * V + 1 + s) * c4 * pg.plane, (uint32_t)c4 * pg.plane * 16u);
+    for (int ch = 0; ch < c4; ++ch) {
+      const float4 r4 = rbase[(size_t)ch * hw];
+      const f4v x0 = {r4.x, r4.y, r4.z, r4.w};
+      const int soff = (int)((uint32_t)ch * pg.plane * 16u);
 #pragma unroll 1
-        for (int pl = lo; pl < hi; ++pl) {
-          float4 xs[NS > 0 ? NS : 1];
+      for (int pl = 0; pl < npl; ++pl) {
+        f4v xs[NS];
 #pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            uint32_t tpos;
-            float twx, twy;
-            src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + k0 + pl) * 9, xn, yn, h, w,
-                       active, tpos, twx, twy);
-            xs[s] = gather_glb4(src_of(1 + s, ch), tpos, twx, twy, h, w);
-          }
-          emit(pl, ch, x0, xs);
+        for (int s = 0; s < NS; ++s) {
+          uint32_t p = kInvalidTap;
+          float wx = 0.0f, wy = 0.0f;
+#pragma unroll
+          for (int q = 0; q < KPG; ++q)   // static register indexing
+            if (q == pl) {
+              p = pos[q][s];
+              wx = fwx[q][s];
+              wy = fwy[q][s];
+            }
+          f4v tp[4];
+          load_taps(rs[s], tap_offset(p, pg), soff, pg.pitch * 16, tp);
+          xs[s] = bilerp(tp, wx, wy);
         }
+        emit(pl, ch, x0, xs);
       }
     }
+    return;
   }
-}
 
-// Direct-gather variant: same tiling, tap state and stores as the LDS kernel, but every view is
-// sampled straight from the packed global features (one 16-B load per tap and 4-channel chunk);
-// no LDS, no barriers, so occupancy is set by registers alone.
-template <int V, int KPG>
-__global__ __launch_bounds__(kBlock) void cost_volume_direct_tile_kernel(
-    const float4* __restrict__ packed, const float* __restrict__ sampling, float* __restrict__ cv,
-    int C, int h, int w, int Dc, int pg, int tiles_x, int tiles_y, int groups, int total) {
-  constexpr int NS = V - 1;
-  const int wk = xcd_work_id(blockIdx.x, total);
-  if (wk >= total) return;
-  const int g = wk % groups;
-  const int t = wk / groups;
-  const int tile = t % (tiles_x * tiles_y);
-  const int b = t / (tiles_x * tiles_y);
-  const int px = (tile % tiles_x) * kTileW + (int)(threadIdx.x % kTileW);
-  const int py = (tile / tiles_x) * kTileH + (int)(threadIdx.x / kTileW);
-  const bool active = px < w && py < h;
-  if (!active) return;   // no barriers in this kernel
-  const int k0 = g * pg;
-  const int npl = min(pg, Dc - k0);
-  const uint32_t hw = (uint32_t)h * (uint32_t)w;
-  const int c4 = (C + 3) / 4;
-  const float xn = norm_coord(px, w);
-  const float yn = norm_coord(py, h);
-  uint32_t rpos;
-  float rwx, rwy;
-  src_coords(sampling + ((size_t)(b * V) * Dc + k0) * 9, xn, yn, h, w, true, rpos, rwx, rwy);
-  uint32_t pos[KPG][NS];
-  float fwx[KPG][NS], fwy[KPG][NS];
+  // LDS index of every (plane, view) nw tap; 0 (zero slots) for samples outside the image: its
+  // other taps (1, rw, rw + 1) are the second zero slot or staged data, all finite, weighted 0
+  uint32_t li[KPG][NS];
 #pragma unroll
   for (int pl = 0; pl < KPG; ++pl)
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      pos[pl][s] = kInvalidTap;
-      fwx[pl][s] = fwy[pl][s] = 0.0f;
-      if (pl < npl)
-        src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + k0 + pl) * 9, xn, yn, h, w, true,
-                   pos[pl][s], fwx[pl][s], fwy[pl][s]);
+      const uint32_t p = pos[pl][s];
+      li[pl][s] = p == kInvalidTap ? 0u
+                                   : (uint32_t)(cum[s] + (pos_y(p) - ry0[s]) * rw[s] + (pos_x(p) - rx0[s]));
     }
-  const float inv_v = 1.0f / (float)V;
-  float* obase = cv + ((size_t)b * C * Dc + (size_t)k0) * hw + (size_t)py * w + px;
+  float inv_rw[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) inv_rw[s] = rw[s] > 0 ? 1.0f / (float)rw[s] : 0.0f;
+  if (threadIdx.x < 2) lds[threadIdx.x] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+  const int n_pieces = cum[NS] - 2;
+
   for (int ch = 0; ch < c4; ++ch) {
-    const float4* src0 = packed + ((size_t)(b * V) * c4 + ch) * hw;
-    const float4 x0 = gather_glb4(src0, rpos, rwx, rwy, h, w);
+    __syncthreads();   // every wave is done reading the previous chunk
+    for (int q = (int)threadIdx.x; q < n_pieces; q += kBlock) {
+      // piece q -> (view, row, col) of the concatenated footprints
+      int s = 0;
+#pragma unroll
+      for (int k = 1; k < NS; ++k)
+        if (q + 2 >= cum[k]) s = k;
+      int c0 = cum[0], x0 = rx0[0], y0 = ry0[0], ww = rw[0];
+      float iw = inv_rw[0];
+#pragma unroll
+      for (int k = 1; k < NS; ++k)
+        if (s == k) {
+          c0 = cum[k];
+          x0 = rx0[k];
+          y0 = ry0[k];
+          ww = rw[k];
+          iw = inv_rw[k];
+        }
+      const int e = q + 2 - c0;
+      const int row = (int)(((float)e + 0.5f) * iw);
+      const int col = e - row * ww;
+      const float4 v = packed[((size_t)(b * V + 1 + s) * c4 + ch) * pg.plane +
+                              (size_t)(y0 + row + 1) * pg.pitch + (x0 + col + 1)];
+      lds[q + 2] = f4v{v.x, v.y, v.z, v.w};
+    }
+    __syncthreads();   // chunk ch is in LDS
+    if (!active) continue;
+    const float4 r4 = rbase[(size_t)ch * hw];
+    const f4v x0 = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
     for (int pl = 0; pl < KPG; ++pl) {
-      if (pl >= npl) continue;
-      float4 xs[NS > 0 ? NS : 1];
+      if (pl >= npl) break;
+      f4v xs[NS];
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        uint32_t tpos = pos[pl][s];
+        const uint32_t i0 = li[pl][s];
+        f4v tp[4];
+        tp[0] = lds[i0];
+        tp[1] = lds[i0 + 1];
+        tp[2] = lds[i0 + rw[s]];
+        tp[3] = lds[i0 + rw[s] + 1];
         float twx = fwx[pl][s], twy = fwy[pl][s];
-        asm volatile("" : "+v"(tpos), "+v"(twx), "+v"(twy));
-        xs[s] = gather_glb4(packed + ((size_t)(b * V + 1 + s) * c4 + ch) * hw, tpos, twx, twy, h, w);
+        asm volatile("" : "+v"(twx), "+v"(twy));
+        xs[s] = bilerp(tp, twx, twy);
       }
-      float* ob = obase + (size_t)pl * hw;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = ch * 4 + j;
-        if (c < C) {
-          const float a0 = (&x0.x)[j];
-          float sum = a0;
-#pragma unroll
-          for (int s = 0; s < NS; ++s) sum += (&xs[s].x)[j];
-          const float mean = sum * inv_v;
-          float d = a0 - mean;
-          float acc = d * d;
-#pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            d = (&xs[s].x)[j] - mean;
-            acc += d * d;
-          }
-          __builtin_nontemporal_store(acc * inv_v, ob + (size_t)c * Dc * hw);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
+      emit(pl, ch, x0, xs);
     }
   }
 }
 
 template <int V>
-void launch_tile(const Geometry& g, const float* feat, const float* smp, float* packed, float* cv,
-                 hipStream_t s) {
-  const uint32_t hw = (uint32_t)g.h * (uint32_t)g.w;
-  const size_t n_pack = (size_t)g.B * V * ((g.C + 3) / 4) * hw;
+void launch_gather(const Geometry& g, const float* feat, const float* smp, float* ws, float* cv,
+                   hipStream_t s) {
+  const int c4 = (g.C + 3) / 4;
+  const PadGeom pgeo = pad_geom(g.h, g.w);
+  float4* packed = reinterpret_cast<float4*>(ws);
+  float4* refs = packed + (size_t)g.B * V * c4 * pgeo.plane;
+  const size_t n_pack = (size_t)g.B * V * c4 * pgeo.plane;
   const size_t pblocks = (n_pack + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(pack4_kernel, dim3((unsigned)(pblocks < 4096 ? pblocks : 4096)), dim3(kBlock), 0,
-                     s, feat, reinterpret_cast<float4*>(packed), g.B * V, g.C, hw);
+  hipLaunchKernelGGL(pack_pad_kernel, dim3((unsigned)(pblocks < 8192 ? pblocks : 8192)), dim3(kBlock), 0,
+                     s, feat, packed, g.B * V, g.C, g.h, g.w);
+  const uint32_t hw = (uint32_t)g.h * (uint32_t)g.w;
+  hipLaunchKernelGGL(ref_resample_kernel, dim3((hw + kBlock - 1) / kBlock, (unsigned)(g.B * c4)),
+                     dim3(kBlock), 0, s, packed, smp, refs, g.B, V, g.C, g.h, g.w, g.Dc);
   const int tiles_x = (g.w + kTileW - 1) / kTileW, tiles_y = (g.h + kTileH - 1) / kTileH;
   // planes per workgroup: the register maximum, halved until the grid has >= 8 workgroups per CU
   int pg = group_planes<V>();
   while (pg > 1 && (long)g.B * tiles_x * tiles_y * ((g.Dc + pg - 1) / pg) < 2048) pg >>= 1;
   const int groups = (g.Dc + pg - 1) / pg;
   const int total = g.B * tiles_x * tiles_y * groups;
-#if !defined(MVS_FWD_LDS)
-  hipLaunchKernelGGL((cost_volume_direct_tile_kernel<V, group_planes<V>()>), xcd_grid(total),
-                     dim3(kBlock), 0, s, reinterpret_cast<const float4*>(packed), smp, cv, g.C, g.h,
-                     g.w, g.Dc, pg, tiles_x, tiles_y, groups, total);
+#ifdef MVS_EXP_GATHER
+  hipLaunchKernelGGL((cost_volume_gather_kernel<V, group_planes<V>()>), xcd_grid(total), dim3(kBlock), 0,
+                     s, packed, refs, smp, cv, g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total);
 #else
-  hipLaunchKernelGGL((cost_volume_tile_kernel<V, group_planes<V>()>), xcd_grid(total), dim3(kBlock), 0,
-                     s, reinterpret_cast<const float4*>(packed), smp, cv, g.C, g.h, g.w, g.Dc, pg,
-                     tiles_x, tiles_y, groups, total);
+  hipLaunchKernelGGL((cost_volume_staged_kernel<V, group_planes<V>()>), xcd_grid(total), dim3(kBlock), 0,
+                     s, packed, refs, smp, cv, g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total);
 #endif
 }
 
@@ -549,19 +612,22 @@ void launch_direct(const Geometry& g, const float* feat, const float* smp, float
 }  // namespace
 
 size_t packed_bytes(int B, int V, int C, int h, int w) {
-  return (size_t)B * V * ((C + 3) / 4) * (size_t)h * (size_t)w * sizeof(float4);
+  if (V < 2 || V > 8)  // generic kernel: reads the NCHW features directly
+    return 0;
+  const size_t c4 = (size_t)((C + 3) / 4);
+  return ((size_t)B * V * c4 * pad_geom(h, w).plane + (size_t)B * c4 * h * w) * sizeof(float4);
 }
 
 void launch_cost_volume_fwd(const Geometry& g, const float* feat, const float* sampling,
                             float* packed, float* cv, hipStream_t s) {
   switch (g.V) {
-    case 2: launch_tile<2>(g, feat, sampling, packed, cv, s); break;
-    case 3: launch_tile<3>(g, feat, sampling, packed, cv, s); break;
-    case 4: launch_tile<4>(g, feat, sampling, packed, cv, s); break;
-    case 5: launch_tile<5>(g, feat, sampling, packed, cv, s); break;
-    case 6: launch_tile<6>(g, feat, sampling, packed, cv, s); break;
-    case 7: launch_tile<7>(g, feat, sampling, packed, cv, s); break;
-    case 8: launch_tile<8>(g, feat, sampling, packed, cv, s); break;
+    case 2: launch_gather<2>(g, feat, sampling, packed, cv, s); break;
+    case 3: launch_gather<3>(g, feat, sampling, packed, cv, s); break;
+    case 4: launch_gather<4>(g, feat, sampling, packed, cv, s); break;
+    case 5: launch_gather<5>(g, feat, sampling, packed, cv, s); break;
+    case 6: launch_gather<6>(g, feat, sampling, packed, cv, s); break;
+    case 7: launch_gather<7>(g, feat, sampling, packed, cv, s); break;
+    case 8: launch_gather<8>(g, feat, sampling, packed, cv, s); break;
     default: launch_direct<MVS_MAX_VIEWS, false>(g, feat, sampling, cv, s); break;
   }
 }

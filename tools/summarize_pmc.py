@@ -14,7 +14,7 @@ from collections import defaultdict
 
 def main():
     root = sys.argv[1]
-    pat = sys.argv[2] if len(sys.argv) > 2 else "cost_volume_direct_tile_kernel"
+    pat = sys.argv[2] if len(sys.argv) > 2 else "cost_volume_gather_kernel"
     acc = defaultdict(list)
     for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
         rows = list(csv.DictReader(open(f)))
