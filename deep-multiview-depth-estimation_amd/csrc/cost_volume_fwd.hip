@@ -231,7 +231,10 @@ __global__ __launch_bounds__(kBlock) void ref_resample_kernel(const float4* __re
 // branch-free 16-byte buffer loads per source view, bilinear + two-pass variance in packed fp32,
 // four dword stores (32-pixel rows: 128-byte segments).
 // ------------------------------------------------------------------------------------------
-constexpr int kTileW = 32;
+#ifndef MVS_EXP_TW
+#define MVS_EXP_TW 32
+#endif
+constexpr int kTileW = MVS_EXP_TW;
 constexpr int kTileH = kBlock / kTileW;   // 8
 
 template <int V>
@@ -343,13 +346,13 @@ __global__ __launch_bounds__(kBlock) void cost_volume_gather_kernel(
 // (the footprint, about 1.8 slots per pixel at P = 4 on DTU geometry) with one coalesced 16-byte
 // load per slot, and every bilinear tap is then a conflict-light ds_read_b128 (4 LDS cycles per
 // wave-instruction against about 12 texture-path cycles for a 16-byte global gather, measured
-// in tools/microbench/gather_patterns.hip).  Slots 0 and 1 hold zeros: a sample with every tap outside the
-// image reads them with weights (1, 0, 0, 0) and is exactly 0.  A workgroup whose footprint exceeds
+// in tools/microbench/gather_patterns.hip).  A zero area at the front of LDS serves the samples
+// with every tap outside the image (exactly 0).  A workgroup whose footprint exceeds
 // the LDS budget falls back to the global gathers of the kernel above.
 // ------------------------------------------------------------------------------------------
 template <int V>
 constexpr int staged_slots() {
-  return V <= 3 ? 2050 : (V <= 5 ? 3074 : 4098);   // 32 / 48 / 64 KB: 4 / 3 / 2 workgroups per CU
+  return V <= 3 ? 2560 : (V <= 5 ? 3072 : 4096);   // 40 / 48 / 64 KB: 4 / 3 / 2 workgroups per CU
 }
 
 // Workgroup-wide min of NV ints; every thread gets the result as a wave-uniform value.
@@ -376,6 +379,19 @@ __device__ inline void block_min(int (&v)[NV], int* scratch /* >= 4 * NV ints of
     v[k] = __builtin_amdgcn_readfirstlane(x);
   }
 }
+
+// Cost-volume stores through a buffer descriptor per (channel, plane group): planes past the group's
+// end, channels past C and inactive lanes get out-of-range offsets and are dropped by the hardware,
+// so every wave issues the same, statically known number of stores per chunk (the waits for the
+// next chunk's staging loads then never wait for this chunk's stores).
+#ifndef MVS_EXP_AUX
+#define MVS_EXP_AUX 2   /* nt */
+#endif
+__device__ inline void store_cv(Rsrc rs, uint32_t voff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)voff, 0, MVS_EXP_AUX);
+}
+
+constexpr int kPrefetch = 4;   // staging pieces per thread carried in registers across a chunk
 
 template <int V, int KPG>
 __global__ __launch_bounds__(kBlock) void cost_volume_staged_kernel(
@@ -438,40 +454,57 @@ __global__ __launch_bounds__(kBlock) void cost_volume_staged_kernel(
     bb[4 * s + 3] = mxy;
   }
   block_min<4 * NS>(bb, scratch);
-  int rx0[NS], ry0[NS], rw[NS], cum[NS + 1];
-  cum[0] = 2;   // slots 0, 1: zeros
+  // LDS image: [zero area][view 1 footprint][view 2 footprint] ...; footprint rows are padded to a
+  // pitch rp = 16k slots, so a row change inside a 16-lane ds_read_b128 group shifts every address
+  // of that group by a multiple of the 16 four-bank groups: no bank conflict from row crossings.
+  // The zero area (max rp + 2 slots) holds the taps of samples outside the image.
+  int rx0[NS], ry0[NS], rw[NS], rp[NS], pcum[NS + 1], scum[NS + 1];
+  int zero_slots = 0;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const bool empty = bb[4 * s] == (1 << 30);
     rx0[s] = bb[4 * s];
     ry0[s] = bb[4 * s + 1];
     rw[s] = empty ? 0 : -bb[4 * s + 2] - rx0[s] + 2;   // taps x0 .. x0 + 1
-    const int rh = empty ? 0 : -bb[4 * s + 3] - ry0[s] + 2;
-    cum[s + 1] = cum[s] + rw[s] * rh;
+    rp[s] = (rw[s] + 15) & ~15;
+    zero_slots = max(zero_slots, rp[s] + 2);
+  }
+  zero_slots = (zero_slots + 15) & ~15;
+  pcum[0] = 0;
+  scum[0] = zero_slots;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int rh = rw[s] == 0 ? 0 : -bb[4 * s + 3] - ry0[s] + 2;
+    pcum[s + 1] = pcum[s] + rw[s] * rh;   // staging pieces (real pixels)
+    scum[s + 1] = scum[s] + rp[s] * rh;   // LDS slots (padded rows)
   }
 
   const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
   const uint32_t pix = (uint32_t)(active ? py : 0) * (uint32_t)w + (uint32_t)(active ? px : 0);
   const float4* rbase = refs + (size_t)b * c4 * hw + pix;
-  float* obase = cv + ((size_t)b * C * Dc + (size_t)k0) * hw + pix;
-  const size_t cstride = (size_t)Dc * hw;
+  // store byte offset of (plane 0, this pixel) inside a (channel, group) descriptor
+#ifdef MVS_EXP_NOSTORE
+  const uint32_t soff0 = kOobOffset;
+#else
+  const uint32_t soff0 = active ? pix * 4u : kOobOffset;
+#endif
+  const uint32_t grp_bytes = (uint32_t)npl * hw * 4u;
 
-  auto emit = [&](int pl, int ch, const f4v& x0, const f4v (&xs)[NS]) {
-    const f4v acc = variance4<NS>(x0, xs, inv_v);
-    float* ob = obase + (size_t)pl * hw + (size_t)(ch * 4) * cstride;
+  // store descriptors of chunk ch's four channels (planes k0 .. k0 + npl of this sample)
+  auto chunk_rsrc = [&](int ch, Rsrc (&rs)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (ch * 4 + j < C) {
-#ifdef MVS_EXP_PLAINST
-        ob[(size_t)j * cstride] = acc[j];
-#else
-        __builtin_nontemporal_store(acc[j], ob + (size_t)j * cstride);
-#endif
-      }
+      const int c = ch * 4 + j;
+      rs[j] = make_rsrc(cv + (((size_t)b * C + (c < C ? c : 0)) * Dc + k0) * hw, c < C ? grp_bytes : 0u);
     }
   };
+  auto emit = [&](int pl, const Rsrc (&rs)[4], const f4v& x0, const f4v (&xs)[NS]) {
+    const f4v acc = variance4<NS>(x0, xs, inv_v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) store_cv(rs[j], soff0 + (uint32_t)pl * hw * 4u, acc[j]);
+  };
 
-  if (cum[NS] > SLOTS) {
+  if (scum[NS] > SLOTS) {
     // footprint beyond the LDS budget (extreme zoom / long epipolar sweep): global gathers
     if (!active) return;   // no barriers below
     Rsrc rs[NS];
@@ -482,6 +515,8 @@ __global__ __launch_bounds__(kBlock) void cost_volume_staged_kernel(
       const float4 r4 = rbase[(size_t)ch * hw];
       const f4v x0 = {r4.x, r4.y, r4.z, r4.w};
       const int soff = (int)((uint32_t)ch * pg.plane * 16u);
+      Rsrc ors[4];
+      chunk_rsrc(ch, ors);
 #pragma unroll 1
       for (int pl = 0; pl < npl; ++pl) {
         f4v xs[NS];
@@ -500,14 +535,14 @@ __global__ __launch_bounds__(kBlock) void cost_volume_staged_kernel(
           load_taps(rs[s], tap_offset(p, pg), soff, pg.pitch * 16, tp);
           xs[s] = bilerp(tp, wx, wy);
         }
-        emit(pl, ch, x0, xs);
+        emit(pl, ors, x0, xs);
       }
     }
     return;
   }
 
-  // LDS index of every (plane, view) nw tap; 0 (zero slots) for samples outside the image: its
-  // other taps (1, rw, rw + 1) are the second zero slot or staged data, all finite, weighted 0
+  // LDS index of every (plane, view) nw tap; 0 (zero area) for samples outside the image: its
+  // other taps (1, rp, rp + 1) lie in the zero area too
   uint32_t li[KPG][NS];
 #pragma unroll
   for (int pl = 0; pl < KPG; ++pl)
@@ -515,47 +550,78 @@ __global__ __launch_bounds__(kBlock) void cost_volume_staged_kernel(
     for (int s = 0; s < NS; ++s) {
       const uint32_t p = pos[pl][s];
       li[pl][s] = p == kInvalidTap ? 0u
-                                   : (uint32_t)(cum[s] + (pos_y(p) - ry0[s]) * rw[s] + (pos_x(p) - rx0[s]));
+                                   : (uint32_t)(scum[s] + (pos_y(p) - ry0[s]) * rp[s] + (pos_x(p) - rx0[s]));
     }
   float inv_rw[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) inv_rw[s] = rw[s] > 0 ? 1.0f / (float)rw[s] : 0.0f;
-  if (threadIdx.x < 2) lds[threadIdx.x] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-  const int n_pieces = cum[NS] - 2;
+  for (int q = (int)threadIdx.x; q < zero_slots; q += kBlock) lds[q] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+  const int n_pieces = pcum[NS];
+
+  // staging piece q -> (LDS slot, element of the padded packed source planes of chunk 0)
+  auto piece = [&](int q, uint32_t& slot) -> uint32_t {   // element index relative to this sample
+    int s = 0;
+#pragma unroll
+    for (int k = 1; k < NS; ++k)
+      if (q >= pcum[k]) s = k;
+    int p0 = pcum[0], s0 = scum[0], x0 = rx0[0], y0 = ry0[0], ww = rw[0], pp = rp[0];
+    float iw = inv_rw[0];
+#pragma unroll
+    for (int k = 1; k < NS; ++k)
+      if (s == k) {
+        p0 = pcum[k];
+        s0 = scum[k];
+        x0 = rx0[k];
+        y0 = ry0[k];
+        ww = rw[k];
+        pp = rp[k];
+        iw = inv_rw[k];
+      }
+    const int e = q - p0;
+    const int row = (int)(((float)e + 0.5f) * iw);
+    const int col = e - row * ww;
+    slot = (uint32_t)(s0 + row * pp + col);
+    return (uint32_t)(1 + s) * (uint32_t)c4 * pg.plane + (uint32_t)((y0 + row + 1) * pg.pitch + (x0 + col + 1));
+  };
+  const float4* pbase = packed + (size_t)b * V * c4 * pg.plane;
+  uint32_t psrc[kPrefetch], pslot[kPrefetch];
+#pragma unroll
+  for (int j = 0; j < kPrefetch; ++j) {
+    const int q = (int)threadIdx.x + kBlock * j;
+    pslot[j] = 0;
+    psrc[j] = q < n_pieces ? piece(q, pslot[j]) : 0;
+  }
+  float4 pre[kPrefetch];
+  float4 rpre;
+  auto prefetch = [&](int ch) {   // chunk ch's first kBlock * kPrefetch pieces + reference -> registers
+    rpre = rbase[(size_t)ch * hw];
+#pragma unroll
+    for (int j = 0; j < kPrefetch; ++j)
+      pre[j] = pbase[psrc[j] + (uint32_t)ch * pg.plane];
+  };
+  prefetch(0);
 
   for (int ch = 0; ch < c4; ++ch) {
     __syncthreads();   // every wave is done reading the previous chunk
-    for (int q = (int)threadIdx.x; q < n_pieces; q += kBlock) {
-      // piece q -> (view, row, col) of the concatenated footprints
-      int s = 0;
 #pragma unroll
-      for (int k = 1; k < NS; ++k)
-        if (q + 2 >= cum[k]) s = k;
-      int c0 = cum[0], x0 = rx0[0], y0 = ry0[0], ww = rw[0];
-      float iw = inv_rw[0];
-#pragma unroll
-      for (int k = 1; k < NS; ++k)
-        if (s == k) {
-          c0 = cum[k];
-          x0 = rx0[k];
-          y0 = ry0[k];
-          ww = rw[k];
-          iw = inv_rw[k];
-        }
-      const int e = q + 2 - c0;
-      const int row = (int)(((float)e + 0.5f) * iw);
-      const int col = e - row * ww;
-      const float4 v = packed[((size_t)(b * V + 1 + s) * c4 + ch) * pg.plane +
-                              (size_t)(y0 + row + 1) * pg.pitch + (x0 + col + 1)];
-      lds[q + 2] = f4v{v.x, v.y, v.z, v.w};
+    for (int j = 0; j < kPrefetch; ++j) {
+      const int q = (int)threadIdx.x + kBlock * j;
+      if (q < n_pieces) lds[pslot[j]] = f4v{pre[j].x, pre[j].y, pre[j].z, pre[j].w};
     }
+#ifndef MVS_EXP_NOSTAGE
+    for (int q = (int)threadIdx.x + kBlock * kPrefetch; q < n_pieces; q += kBlock) {
+      uint32_t slot;
+      const float4 v = pbase[piece(q, slot) + (uint32_t)ch * pg.plane];
+      lds[slot] = f4v{v.x, v.y, v.z, v.w};
+    }
+#endif
+    const f4v x0 = {rpre.x, rpre.y, rpre.z, rpre.w};
     __syncthreads();   // chunk ch is in LDS
-    if (!active) continue;
-    const float4 r4 = rbase[(size_t)ch * hw];
-    const f4v x0 = {r4.x, r4.y, r4.z, r4.w};
+    if (ch + 1 < c4) prefetch(ch + 1);   // in flight during this chunk's stores
+    Rsrc ors[4];
+    chunk_rsrc(ch, ors);
 #pragma unroll
     for (int pl = 0; pl < KPG; ++pl) {
-      if (pl >= npl) break;
       f4v xs[NS];
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
@@ -563,13 +629,13 @@ __global__ __launch_bounds__(kBlock) void cost_volume_staged_kernel(
         f4v tp[4];
         tp[0] = lds[i0];
         tp[1] = lds[i0 + 1];
-        tp[2] = lds[i0 + rw[s]];
-        tp[3] = lds[i0 + rw[s] + 1];
+        tp[2] = lds[i0 + rp[s]];
+        tp[3] = lds[i0 + rp[s] + 1];
         float twx = fwx[pl][s], twy = fwy[pl][s];
         asm volatile("" : "+v"(twx), "+v"(twy));
         xs[s] = bilerp(tp, twx, twy);
       }
-      emit(pl, ch, x0, xs);
+      emit(pl, ors, x0, xs);
     }
   }
 }
