@@ -23,9 +23,11 @@ Also reported (one JSON line, rank 0):
   hot_path      cost volumes/s of the fused kernel alone
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -45,6 +47,27 @@ from cameras import camera_batch, depth_range  # noqa: E402
 from weights import deterministic_state_dict  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+_T0 = time.perf_counter()
+
+
+_PHASE = ["start"]
+
+
+def log(msg):
+    """Progress on stderr (stdout carries only the JSON line)."""
+    _PHASE[0] = msg
+    print("[bench %7.1fs] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
+
+
+def _heartbeat():
+    # a long phase (first MIOpen call, CPU baseline) still shows progress every 30 s
+    while True:
+        time.sleep(30.0)
+        print("[bench %7.1fs] ... %s" % (time.perf_counter() - _T0, _PHASE[0]), file=sys.stderr,
+              flush=True)
+
+
+threading.Thread(target=_heartbeat, daemon=True).start()
 
 
 def parse():
@@ -62,7 +85,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-planes", type=int, default=None, help="planes for the CPU sample")
     ap.add_argument("--kernel-only", action="store_true", help="skip the end-to-end forward")
-    ap.add_argument("--conv-search", choices=("on", "off"), default="on",
+    ap.add_argument("--conv-search", choices=("on", "off"), default="off",
                     help="torch.backends.cudnn.benchmark (MIOpen find) for the regulariser convs")
     return ap.parse_args()
 
@@ -110,28 +133,51 @@ def build_model(D, H, W, device):
 
 
 def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None):
-    """Average fused-kernel launch time with HIP events on the launch stream."""
-    from mvs_amd import ops
+    """Fused-kernel timing with HIP events on the launch stream, through the C ABI.
+
+    Returns (main_ms, op_ms, alg_bytes): main_ms = average duration of the main fused kernel
+    (events recorded by mvs_cost_volume_fwd_timed right around its launch), op_ms = average
+    duration of the whole op (sampling matrices + packing + reference resampling + main kernel)."""
+    from mvs_amd import _lib, ops
+    lib = _lib.load()
     d_count = D if d_count is None else d_count
     K, R, T = camera_batch(B, V, h, w)
     d_min, d_int = depth_range(B)
-    K, R, T, d_min, d_int = (x.to(device) for x in (K, R, T, d_min, d_int))
+    K, R, T, d_min, d_int = ops._cams(K, R, T, d_min, d_int, device, B)
     g = torch.Generator(device="cpu").manual_seed(7)
     feat = torch.randn(B * V, C, h, w, generator=g).to(device)
-    with torch.no_grad():
-        for _ in range(3):
-            ops.cost_volume(feat, K, R, T, d_min, d_int, B, V, d_begin, d_count, 25.0)
-        stream = torch.cuda.current_stream(device)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
+    cv = torch.empty((B, C, d_count, h, w), device=device)
+    ws = torch.empty((lib.mvs_cost_volume_workspace_bytes(B, V, C, h, w, d_count) + 3) // 4,
+                     device=device)
+    stream = torch.cuda.current_stream(device)
+    sp = _lib.stream_handle(device)
+
+    def launch(e0=None, e1=None):
+        st = lib.mvs_cost_volume_fwd_timed(
+            _lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T), _lib.ptr(d_min), _lib.ptr(d_int),
+            B, V, C, h, w, d_begin, d_count, 25.0, _lib.ptr(ws), _lib.ptr(cv), sp,
+            None if e0 is None else ctypes.c_void_p(e0.cuda_event),
+            None if e1 is None else ctypes.c_void_p(e1.cuda_event))
+        _lib.check(st, "mvs_cost_volume_fwd_timed")
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(iters)]
+    for e0, e1 in ev:   # materialise the HIP events (torch creates them on first record)
         e0.record(stream)
-        for _ in range(iters):
-            ops.cost_volume(feat, K, R, T, d_min, d_int, B, V, d_begin, d_count, 25.0)
         e1.record(stream)
-        torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / iters
+    op0, op1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        launch()
+    torch.cuda.synchronize()
+    op0.record(stream)
+    for e0, e1 in ev:
+        launch(e0, e1)
+    op1.record(stream)
+    torch.cuda.synchronize()
+    main_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / iters
+    op_ms = op0.elapsed_time(op1) / iters
     alg_bytes = 4.0 * B * V * C * h * w + 4.0 * B * C * d_count * h * w
-    return ms, alg_bytes
+    return main_ms, op_ms, alg_bytes
 
 
 def load_traffic(tag):
@@ -184,6 +230,7 @@ def main():
     result = {}
     ms_step = None
     if not args.kernel_only:
+        log("building model (D=%d, %dx%d)" % (D, H, W))
         net = build_model(D, H, W, device)
         inputs = make_inputs(B, V, H, W, rank, device)
         if args.mode == "samples":
@@ -193,14 +240,17 @@ def main():
             sharded = DepthShardedMVSNet(net, world, rank)
             step = lambda: sharded(*inputs, B, V)
         with torch.no_grad():
-            for _ in range(args.warmup):
+            for i in range(args.warmup):
                 step()
+                torch.cuda.synchronize()
+                log("warmup step %d/%d done" % (i + 1, args.warmup))
             barrier(world)
             t0 = time.perf_counter()
             for _ in range(args.steps):
                 step()
             barrier(world)
             dt = time.perf_counter() - t0
+        log("timed %d steps: %.2f ms/step" % (args.steps, 1000.0 * dt / args.steps))
         dt = max_over_ranks(dt, world, device)
         ms_step = 1000.0 * dt / args.steps
         maps = (B * world if args.mode == "samples" else B) * args.steps
@@ -209,8 +259,10 @@ def main():
 
     # fused kernel timing (this rank's share of planes in dshard mode)
     d_count = D if args.mode == "samples" else D // world
-    k_ms, alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count)
+    log("timing the fused kernel")
+    k_ms, op_ms, alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count)
     k_ms = max_over_ranks(k_ms, world, device)
+    op_ms = max_over_ranks(op_ms, world, device)
     gbs = alg / (k_ms * 1e-3) / 1e9
     tag = "b%dv%dd%dh%dw%d" % (B, V, d_count, h, w)
     traffic = load_traffic(tag)
@@ -241,11 +293,15 @@ def main():
         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": gbs / HBM_PEAK_GBS,
                      "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
-                     "kernel": "cost_volume_direct_tile_kernel (+ pack4_kernel, plane_sampling_kernel)", "kernel_ms": k_ms,
+                     "kernel": "cost_volume_staged_kernel", "kernel_ms": k_ms,
                      "alg_bytes_per_launch": alg},
-        "hot_path": {"cost_volumes_per_s": B / (k_ms * 1e-3), "kernel_ms": k_ms},
+        "hot_path": {"cost_volumes_per_s": B / (op_ms * 1e-3), "op_ms": op_ms,
+                     "op": "mvs_cost_volume_fwd: plane_sampling + pack_pad + ref_resample + "
+                           "cost_volume_staged kernels",
+                     "op_GBps": alg / (op_ms * 1e-3) / 1e9},
     }
     if not args.no_cpu_baseline and world == 1:
+        log("cpu baseline (oracle, one sample)")
         out["cpu_baseline"] = cpu_baseline(V, H, W, args.cpu_planes or D)
     else:
         out["cpu_baseline"] = None

@@ -74,10 +74,11 @@ int mvs_plane_sampling(const float* K, const float* R, const float* T, const flo
   return mvs::hip_status();
 }
 
-int mvs_cost_volume_fwd(const float* feat, const float* K, const float* R, const float* T,
+int mvs_cost_volume_fwd_timed(const float* feat, const float* K, const float* R, const float* T,
                         const float* d_min, const float* d_int, int batch_size, int n_views,
                         int channels, int h, int w, int d_begin, int d_count, float d_scale,
-                        float* workspace, float* cv_out, void* stream) {
+                        float* workspace, float* cv_out, void* stream,
+                              void* main_begin_event, void* main_end_event) {
   if (!feat || !workspace || !cv_out) return MVS_ERR_INVALID_ARGUMENT;
   Geometry g;
   int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g);
@@ -95,8 +96,18 @@ int mvs_cost_volume_fwd(const float* feat, const float* K, const float* R, const
   float* packed = reinterpret_cast<float*>(
       reinterpret_cast<char*>(workspace) +
       mvs::align256(mvs_sampling_workspace_bytes(batch_size * n_views, d_count)));
-  mvs::launch_cost_volume_fwd(g, feat, workspace, packed, cv_out, s);
+  mvs::launch_cost_volume_fwd(g, feat, workspace, packed, cv_out, s, (hipEvent_t)main_begin_event,
+                              (hipEvent_t)main_end_event);
   return mvs::hip_status();
+}
+
+int mvs_cost_volume_fwd(const float* feat, const float* K, const float* R, const float* T,
+                        const float* d_min, const float* d_int, int batch_size, int n_views,
+                        int channels, int h, int w, int d_begin, int d_count, float d_scale,
+                        float* workspace, float* cv_out, void* stream) {
+  return mvs_cost_volume_fwd_timed(feat, K, R, T, d_min, d_int, batch_size, n_views, channels, h, w,
+                                   d_begin, d_count, d_scale, workspace, cv_out, stream, nullptr,
+                                   nullptr);
 }
 
 int mvs_homography_warp_fwd(const float* feat, const float* K, const float* R, const float* T,
@@ -148,6 +159,27 @@ int mvs_extract_depth_map_fwd(const float* prob, const float* d_batch, int batch
   if (n_est > 16) return MVS_ERR_INVALID_ARGUMENT;
   mvs::launch_soft_argmin(prob, d_batch, batch_size, d, (uint32_t)h * (uint32_t)w, n_est, depth_out,
                           (hipStream_t)stream);
+  return mvs::hip_status();
+}
+
+int mvs_normalize_images(const unsigned char* rgb, int n_images, int h, int w, const float* mean,
+                         const float* std_dev, float* out, void* stream) {
+  if (!rgb || !out || !mean || !std_dev || n_images <= 0 || h <= 0 || w <= 0)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (((uintptr_t)rgb & 3u) || ((uintptr_t)out & 15u)) return MVS_ERR_INVALID_ARGUMENT;
+  const uint64_t hw = (uint64_t)h * (uint64_t)w;
+  if (hw >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
+  for (int c = 0; c < 3; ++c)
+    if (!(std_dev[c] != 0.0f)) return MVS_ERR_INVALID_ARGUMENT;
+  mvs::launch_normalize_images(rgb, n_images, (uint32_t)hw, mean, std_dev, out, (hipStream_t)stream);
+  return mvs::hip_status();
+}
+
+int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float* out, void* stream) {
+  if (!depth || !out) return MVS_ERR_INVALID_ARGUMENT;
+  if (((uintptr_t)depth & 15u) || ((uintptr_t)out & 15u)) return MVS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return MVS_OK;
+  mvs::launch_depth_threshold(depth, n, lo, hi, out, (hipStream_t)stream);
   return mvs::hip_status();
 }
 

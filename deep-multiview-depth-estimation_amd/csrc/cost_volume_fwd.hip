@@ -642,7 +642,7 @@ __global__ __launch_bounds__(kBlock) void cost_volume_staged_kernel(
 
 template <int V>
 void launch_gather(const Geometry& g, const float* feat, const float* smp, float* ws, float* cv,
-                   hipStream_t s) {
+                   hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int c4 = (g.C + 3) / 4;
   const PadGeom pgeo = pad_geom(g.h, g.w);
   float4* packed = reinterpret_cast<float4*>(ws);
@@ -660,6 +660,7 @@ void launch_gather(const Geometry& g, const float* feat, const float* smp, float
   while (pg > 1 && (long)g.B * tiles_x * tiles_y * ((g.Dc + pg - 1) / pg) < 2048) pg >>= 1;
   const int groups = (g.Dc + pg - 1) / pg;
   const int total = g.B * tiles_x * tiles_y * groups;
+  if (ev0) (void)hipEventRecord(ev0, s);
 #ifdef MVS_EXP_GATHER
   hipLaunchKernelGGL((cost_volume_gather_kernel<V, group_planes<V>()>), xcd_grid(total), dim3(kBlock), 0,
                      s, packed, refs, smp, cv, g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total);
@@ -667,12 +668,16 @@ void launch_gather(const Geometry& g, const float* feat, const float* smp, float
   hipLaunchKernelGGL((cost_volume_staged_kernel<V, group_planes<V>()>), xcd_grid(total), dim3(kBlock), 0,
                      s, packed, refs, smp, cv, g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total);
 #endif
+  if (ev1) (void)hipEventRecord(ev1, s);
 }
 
 template <int MAXV, bool EXACT>
-void launch_direct(const Geometry& g, const float* feat, const float* smp, float* cv, hipStream_t s) {
+void launch_direct(const Geometry& g, const float* feat, const float* smp, float* cv, hipStream_t s,
+                   hipEvent_t ev0, hipEvent_t ev1) {
+  if (ev0) (void)hipEventRecord(ev0, s);
   hipLaunchKernelGGL((cost_volume_kernel<MAXV, EXACT, 4>), xcd_grid(g.total), dim3(kBlock), 0, s,
                      feat, smp, cv, g.V, g.C, g.h, g.w, g.Dc, g.tiles, g.total);
+  if (ev1) (void)hipEventRecord(ev1, s);
 }
 
 }  // namespace
@@ -685,16 +690,17 @@ size_t packed_bytes(int B, int V, int C, int h, int w) {
 }
 
 void launch_cost_volume_fwd(const Geometry& g, const float* feat, const float* sampling,
-                            float* packed, float* cv, hipStream_t s) {
+                            float* packed, float* cv, hipStream_t s, hipEvent_t ev0,
+                            hipEvent_t ev1) {
   switch (g.V) {
-    case 2: launch_gather<2>(g, feat, sampling, packed, cv, s); break;
-    case 3: launch_gather<3>(g, feat, sampling, packed, cv, s); break;
-    case 4: launch_gather<4>(g, feat, sampling, packed, cv, s); break;
-    case 5: launch_gather<5>(g, feat, sampling, packed, cv, s); break;
-    case 6: launch_gather<6>(g, feat, sampling, packed, cv, s); break;
-    case 7: launch_gather<7>(g, feat, sampling, packed, cv, s); break;
-    case 8: launch_gather<8>(g, feat, sampling, packed, cv, s); break;
-    default: launch_direct<MVS_MAX_VIEWS, false>(g, feat, sampling, cv, s); break;
+    case 2: launch_gather<2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 3: launch_gather<3>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 4: launch_gather<4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 5: launch_gather<5>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 6: launch_gather<6>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 7: launch_gather<7>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 8: launch_gather<8>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    default: launch_direct<MVS_MAX_VIEWS, false>(g, feat, sampling, cv, s, ev0, ev1); break;
   }
 }
 

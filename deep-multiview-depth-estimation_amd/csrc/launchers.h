@@ -15,10 +15,12 @@ void launch_plane_sampling(const float* K, const float* R, const float* T, const
                            int d_count, float d_scale, float* sampling, hipStream_t s);
 
 // cost_volume_fwd.hip: fused warp + variance.  `packed` is the workspace area after the sampling
-// matrices (packed_bytes()).
+// matrices (packed_bytes()).  ev0/ev1 (optional) are recorded on `s` right before and after the
+// main fused kernel (its live timing, bench.py).
 size_t packed_bytes(int B, int V, int C, int h, int w);
 void launch_cost_volume_fwd(const Geometry& g, const float* feat, const float* sampling,
-                            float* packed, float* cv, hipStream_t s);
+                            float* packed, float* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
+                            hipEvent_t ev1 = nullptr);
 
 // warp_variance.hip
 void launch_warp(const Geometry& g, const float* feat, const float* sampling, float* warped,
@@ -32,5 +34,12 @@ void launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* s
 // soft_argmin.hip
 void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, uint32_t hw,
                         int n_est, float* depth, hipStream_t s);
+
+// dtu_input.hip: data.py:206-210 image normalisation (uint8 HWC -> fp32 NCHW), data.py:300-301
+// depth thresholds
+void launch_normalize_images(const uint8_t* rgb, int n, uint32_t hw, const float* mean3,
+                             const float* std3, float* out, hipStream_t s);
+void launch_depth_threshold(const float* depth, size_t n, float lo, float hi, float* out,
+                            hipStream_t s);
 
 }  // namespace mvs

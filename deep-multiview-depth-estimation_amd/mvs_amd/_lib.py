@@ -37,6 +37,8 @@ SIGNATURES = {
                                     _c_int, _c_float, _p, _p]),
     "mvs_cost_volume_fwd": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
                                      _c_int, _c_int, _c_int, _c_float, _p, _p, _p]),
+    "mvs_cost_volume_fwd_timed": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
+                                           _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p]),
     "mvs_homography_warp_fwd": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
                                          _c_int, _c_int, _c_int, _c_float, _p, _p, _p]),
     "mvs_assemble_cost_volume_fwd": (_c_int, [_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
@@ -45,6 +47,8 @@ SIGNATURES = {
                                      _p, _p]),
     "mvs_extract_depth_map_fwd": (_c_int, [_p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _p,
                                            _p]),
+    "mvs_normalize_images": (_c_int, [_p, _c_int, _c_int, _c_int, _p, _p, _p, _p]),
+    "mvs_depth_threshold": (_c_int, [_p, ctypes.c_size_t, _c_float, _c_float, _p, _p]),
 }
 
 

@@ -83,6 +83,19 @@ int mvs_cost_volume_fwd(const float* feat, const float* K, const float* R, const
                         float* workspace, float* cv_out, void* stream);
 
 /*
+ * mvs_cost_volume_fwd with live timing of its main fused kernel: main_begin_event and
+ * main_end_event (hipEvent_t, either may be NULL) are recorded on `stream` immediately before
+ * and after that kernel's launch (the sampling-matrix, packing and reference-resampling kernels
+ * run before main_begin_event).  Used by bench.py for the roofline's per-launch duration.
+ */
+int mvs_cost_volume_fwd_timed(const float* feat, const float* K, const float* R, const float* T,
+                              const float* d_min, const float* d_int,
+                              int batch_size, int n_views, int channels, int h, int w,
+                              int d_begin, int d_count, float d_scale,
+                              float* workspace, float* cv_out, void* stream,
+                              void* main_begin_event, void* main_end_event);
+
+/*
  * Warp only (API-compatible homography_warping, homography.py:6-92):
  * warped[N][C][d_count][h][w].  Same workspace contract as mvs_cost_volume_fwd.
  */
@@ -117,6 +130,27 @@ int mvs_cost_volume_bwd(const float* feat, const float* sampling, const float* g
  */
 int mvs_extract_depth_map_fwd(const float* prob, const float* d_batch, int batch_size, int d,
                               int h, int w, int n_est, float* depth_out, void* stream);
+
+/*
+ * DTU input transforms, the callers on the input side of the path.
+ *
+ * Image normalisation of data.py:206-210 (transforms.PILToTensor -> ConvertImageDtype(float) ->
+ * Normalize(mean, std), applied per image in DtuTrainDataset.__getitem__, data.py:286-291):
+ *   out[n][c][y][x] = (rgb[n][y][x][c] / 255 - mean[c]) / std_dev[c], fp32, rounded step by step
+ *   exactly as torch's CPU ops (bit-identical).
+ *   rgb: [n_images][h][w][3] uint8 (decoded pixels as PIL gives them), DEVICE, 4-byte aligned;
+ *   mean, std_dev: 3 floats each, HOST pointers (read at launch); out: [n_images][3][h][w] fp32,
+ *   DEVICE, 16-byte aligned.
+ */
+int mvs_normalize_images(const unsigned char* rgb, int n_images, int h, int w, const float* mean,
+                         const float* std_dev, float* out, void* stream);
+
+/*
+ * Ground-truth depth clamp of data.py:300-301 (cv2.threshold THRESH_TOZERO at lo = 0, then
+ * THRESH_TOZERO_INV at hi = 1000): v = x > lo ? x : 0; out = v > hi ? 0 : v.  n floats, DEVICE,
+ * 16-byte aligned; out may alias depth.
+ */
+int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float* out, void* stream);
 
 #ifdef __cplusplus
 }
