@@ -352,8 +352,17 @@ __global__ __launch_bounds__(kBlock) void cost_volume_gather_kernel(
 // ------------------------------------------------------------------------------------------
 template <int V>
 constexpr int staged_slots() {
+#ifdef MVS_EXP_SLOTS
+  return MVS_EXP_SLOTS;
+#else
   return V <= 3 ? 2560 : (V <= 5 ? 3072 : 4096);   // 40 / 48 / 64 KB: 4 / 3 / 2 workgroups per CU
+#endif
 }
+#ifdef MVS_EXP_WPE
+#define MVS_STAGED_ATTR __attribute__((amdgpu_waves_per_eu(MVS_EXP_WPE)))
+#else
+#define MVS_STAGED_ATTR
+#endif
 
 // Workgroup-wide min of NV ints; every thread gets the result as a wave-uniform value.
 template <int NV>
@@ -394,14 +403,17 @@ __device__ inline void store_cv(Rsrc rs, uint32_t voff, float v) {
 constexpr int kPrefetch = 4;   // staging pieces per thread carried in registers across a chunk
 
 template <int V, int KPG>
-__global__ __launch_bounds__(kBlock) void cost_volume_staged_kernel(
+__global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_kernel(
     const float4* __restrict__ packed, const float4* __restrict__ refs,
     const float* __restrict__ sampling, float* __restrict__ cv, int C, int h, int w, int Dc, int pg_n,
     int tiles_x, int tiles_y, int groups, int total) {
   constexpr int NS = V - 1;
   constexpr int SLOTS = staged_slots<V>();
   __shared__ f4v lds[SLOTS];
-  __shared__ int scratch[4 * 4 * NS];
+  // block_min's scratch lives in the last slots of the staging area: it is read before the first
+  // chunk's barrier, and staging writes only follow that barrier (the zero area is at the front).
+  // Keeping the whole workgroup at exactly SLOTS * 16 B (40 KB at V = 3) fits 4 workgroups per CU.
+  int* scratch = reinterpret_cast<int*>(&lds[SLOTS - (4 * 4 * NS + 3) / 4]);
 
   const int wk = xcd_work_id(blockIdx.x, total);
   if (wk >= total) return;   // workgroup-uniform
