@@ -173,6 +173,27 @@ __device__ inline f4v bilerp(const f4v (&t)[4], float wx, float wy) {
   return f4v{lo.x, lo.y, hi.x, hi.y};
 }
 
+// Experiment (MVS_EXP_VSUBW): bilerp() with 1 - wx and 1 - wy produced by volatile v_sub_f32 (the
+// instruction the compiler emits for `1.0f - w`, so the values are identical), which removes the
+// register copies of the opaque-copy barrier -- but the compiler then reserves a register next to
+// every wx / wy to pair them for v_pk_mul_f32 (+32 VGPRs at 8 planes).
+__device__ inline f4v bilerp_loop(const f4v (&t)[4], float wx, float wy) {
+  float omx, omy;
+  asm volatile("v_sub_f32 %0, 1.0, %1" : "=v"(omx) : "v"(wx));
+  asm volatile("v_sub_f32 %0, 1.0, %1" : "=v"(omy) : "v"(wy));
+  const f2v e = {omx, wx};
+  const f2v w01 = f2v{omy, omy} * e;
+  const f2v w23 = f2v{wy, wy} * e;
+  f2v lo = t[0].xy * w01.xx, hi = t[0].zw * w01.xx;
+  lo = __builtin_elementwise_fma(t[1].xy, w01.yy, lo);
+  hi = __builtin_elementwise_fma(t[1].zw, w01.yy, hi);
+  lo = __builtin_elementwise_fma(t[2].xy, w23.xx, lo);
+  hi = __builtin_elementwise_fma(t[2].zw, w23.xx, hi);
+  lo = __builtin_elementwise_fma(t[3].xy, w23.yy, lo);
+  hi = __builtin_elementwise_fma(t[3].zw, w23.yy, hi);
+  return f4v{lo.x, lo.y, hi.x, hi.y};
+}
+
 __device__ inline void load_taps(Rsrc rs, uint32_t voff, int soff, int row_bytes, f4v (&t)[4]) {
   t[0] = ld4(rs, voff, soff);
   t[1] = ld4(rs, voff + 16u, soff);
@@ -643,9 +664,13 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
         tp[1] = lds[i0 + 1];
         tp[2] = lds[i0 + rp[s]];
         tp[3] = lds[i0 + rp[s] + 1];
+#ifdef MVS_EXP_VSUBW   // 32 fewer VALU per chunk, but 200 VGPRs (2 waves per SIMD)
+        xs[s] = bilerp_loop(tp, fwx[pl][s], fwy[pl][s]);
+#else
         float twx = fwx[pl][s], twy = fwy[pl][s];
         asm volatile("" : "+v"(twx), "+v"(twy));
         xs[s] = bilerp(tp, twx, twy);
+#endif
       }
       emit(pl, ors, x0, xs);
     }
