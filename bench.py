@@ -132,12 +132,14 @@ def build_model(D, H, W, device):
     return net.to(device).eval()
 
 
-def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None):
+def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=False):
     """Fused-kernel timing with HIP events on the launch stream, through the C ABI.
 
     Returns (main_ms, op_ms, alg_bytes): main_ms = average duration of the main fused kernel
     (events recorded by mvs_cost_volume_fwd_timed right around its launch), op_ms = average
-    duration of the whole op (sampling matrices + packing + reference resampling + main kernel)."""
+    duration of the whole op (sampling matrices + packing + reference resampling + main kernel).
+    bf16=True times the opt-in bf16 cost volume (mvs_cost_volume_fwd_bf16): op-level only
+    (main_ms None), algorithmic bytes with a 2-byte cost volume."""
     from mvs_amd import _lib, ops
     lib = _lib.load()
     d_count = D if d_count is None else d_count
@@ -146,13 +148,20 @@ def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None):
     K, R, T, d_min, d_int = ops._cams(K, R, T, d_min, d_int, device, B)
     g = torch.Generator(device="cpu").manual_seed(7)
     feat = torch.randn(B * V, C, h, w, generator=g).to(device)
-    cv = torch.empty((B, C, d_count, h, w), device=device)
+    cv = torch.empty((B, C, d_count, h, w), device=device,
+                     dtype=torch.bfloat16 if bf16 else torch.float32)
     ws = torch.empty((lib.mvs_cost_volume_workspace_bytes(B, V, C, h, w, d_count) + 3) // 4,
                      device=device)
     stream = torch.cuda.current_stream(device)
     sp = _lib.stream_handle(device)
 
     def launch(e0=None, e1=None):
+        if bf16:
+            st = lib.mvs_cost_volume_fwd_bf16(
+                _lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T), _lib.ptr(d_min),
+                _lib.ptr(d_int), B, V, C, h, w, d_begin, d_count, 25.0, _lib.ptr(ws), _lib.ptr(cv), sp)
+            _lib.check(st, "mvs_cost_volume_fwd_bf16")
+            return
         st = lib.mvs_cost_volume_fwd_timed(
             _lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T), _lib.ptr(d_min), _lib.ptr(d_int),
             B, V, C, h, w, d_begin, d_count, 25.0, _lib.ptr(ws), _lib.ptr(cv), sp,
@@ -174,9 +183,9 @@ def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None):
         launch(e0, e1)
     op1.record(stream)
     torch.cuda.synchronize()
-    main_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / iters
+    main_ms = None if bf16 else sum(e0.elapsed_time(e1) for e0, e1 in ev) / iters
     op_ms = op0.elapsed_time(op1) / iters
-    alg_bytes = 4.0 * B * V * C * h * w + 4.0 * B * C * d_count * h * w
+    alg_bytes = 4.0 * B * V * C * h * w + (2.0 if bf16 else 4.0) * B * C * d_count * h * w
     return main_ms, op_ms, alg_bytes
 
 
@@ -300,6 +309,11 @@ def main():
                            "cost_volume_staged kernels",
                      "op_GBps": alg / (op_ms * 1e-3) / 1e9},
     }
+    # opt-in bf16 cost volume: informational, not the headline (reduced precision)
+    _, bf_op_ms, bf_alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count, bf16=True)
+    out["bf16_cv_opt_in"] = {"op_ms": bf_op_ms, "alg_bytes_per_launch": bf_alg,
+                             "op_GBps": bf_alg / (bf_op_ms * 1e-3) / 1e9,
+                             "cost_volumes_per_s": B / (bf_op_ms * 1e-3)}
     if not args.no_cpu_baseline and world == 1:
         log("cpu baseline (oracle, one sample)")
         out["cpu_baseline"] = cpu_baseline(V, H, W, args.cpu_planes or D)

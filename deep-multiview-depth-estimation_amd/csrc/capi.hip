@@ -33,6 +33,36 @@ bool cams_ok(const float* K, const float* R, const float* T, const float* d_min,
   return K && R && T && d_min && d_int;
 }
 
+// Fused warp + variance into an fp32 (es = 4) or bf16 (es = 2) cost volume.
+int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, const float* T,
+                         const float* d_min, const float* d_int, int batch_size, int n_views,
+                         int channels, int h, int w, int d_begin, int d_count, float d_scale,
+                         float* workspace, void* cv_out, int es, void* stream, void* ev0, void* ev1) {
+  if (!feat || !workspace || !cv_out) return MVS_ERR_INVALID_ARGUMENT;
+  Geometry g;
+  int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g);
+  if (st != MVS_OK) return st;
+  st = mvs_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
+                          d_scale, workspace, stream);
+  if (st != MVS_OK) return st;
+  hipStream_t s = (hipStream_t)stream;
+  if (n_views == 1) {  // the variance of a single view is identically zero (0 in fp32 and bf16)
+    if (hipMemsetAsync(cv_out, 0, (size_t)batch_size * channels * d_count * h * w * es, s) != hipSuccess)
+      return MVS_ERR_HIP;
+    return mvs::hip_status();
+  }
+  float* packed = reinterpret_cast<float*>(
+      reinterpret_cast<char*>(workspace) +
+      mvs::align256((size_t)batch_size * n_views * d_count * 9 * sizeof(float)));
+  if (es == 4)
+    mvs::launch_cost_volume_fwd(g, feat, workspace, packed, static_cast<float*>(cv_out), s,
+                                (hipEvent_t)ev0, (hipEvent_t)ev1);
+  else
+    mvs::launch_cost_volume_fwd_bf16(g, feat, workspace, packed, cv_out, s, (hipEvent_t)ev0,
+                                     (hipEvent_t)ev1);
+  return mvs::hip_status();
+}
+
 }  // namespace
 
 extern "C" {
@@ -75,39 +105,32 @@ int mvs_plane_sampling(const float* K, const float* R, const float* T, const flo
 }
 
 int mvs_cost_volume_fwd_timed(const float* feat, const float* K, const float* R, const float* T,
-                        const float* d_min, const float* d_int, int batch_size, int n_views,
-                        int channels, int h, int w, int d_begin, int d_count, float d_scale,
-                        float* workspace, float* cv_out, void* stream,
+                              const float* d_min, const float* d_int, int batch_size, int n_views,
+                              int channels, int h, int w, int d_begin, int d_count, float d_scale,
+                              float* workspace, float* cv_out, void* stream,
                               void* main_begin_event, void* main_end_event) {
-  if (!feat || !workspace || !cv_out) return MVS_ERR_INVALID_ARGUMENT;
-  Geometry g;
-  int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g);
-  if (st != MVS_OK) return st;
-  st = mvs_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
-                          d_scale, workspace, stream);
-  if (st != MVS_OK) return st;
-  hipStream_t s = (hipStream_t)stream;
-  if (n_views == 1) {  // the variance of a single view is identically zero
-    if (hipMemsetAsync(cv_out, 0, (size_t)batch_size * channels * d_count * h * w * sizeof(float), s) !=
-        hipSuccess)
-      return MVS_ERR_HIP;
-    return mvs::hip_status();
-  }
-  float* packed = reinterpret_cast<float*>(
-      reinterpret_cast<char*>(workspace) +
-      mvs::align256(mvs_sampling_workspace_bytes(batch_size * n_views, d_count)));
-  mvs::launch_cost_volume_fwd(g, feat, workspace, packed, cv_out, s, (hipEvent_t)main_begin_event,
-                              (hipEvent_t)main_end_event);
-  return mvs::hip_status();
+  return cost_volume_fwd_impl(feat, K, R, T, d_min, d_int, batch_size, n_views, channels, h, w,
+                              d_begin, d_count, d_scale, workspace, cv_out, 4, stream,
+                              main_begin_event, main_end_event);
 }
 
 int mvs_cost_volume_fwd(const float* feat, const float* K, const float* R, const float* T,
                         const float* d_min, const float* d_int, int batch_size, int n_views,
                         int channels, int h, int w, int d_begin, int d_count, float d_scale,
                         float* workspace, float* cv_out, void* stream) {
-  return mvs_cost_volume_fwd_timed(feat, K, R, T, d_min, d_int, batch_size, n_views, channels, h, w,
-                                   d_begin, d_count, d_scale, workspace, cv_out, stream, nullptr,
-                                   nullptr);
+  return cost_volume_fwd_impl(feat, K, R, T, d_min, d_int, batch_size, n_views, channels, h, w,
+                              d_begin, d_count, d_scale, workspace, cv_out, 4, stream, nullptr,
+                              nullptr);
+}
+
+int mvs_cost_volume_fwd_bf16(const float* feat, const float* K, const float* R, const float* T,
+                             const float* d_min, const float* d_int, int batch_size, int n_views,
+                             int channels, int h, int w, int d_begin, int d_count, float d_scale,
+                             float* workspace, void* cv_out, void* stream) {
+  if (n_views > 8) return MVS_ERR_UNSUPPORTED_VIEWS;
+  return cost_volume_fwd_impl(feat, K, R, T, d_min, d_int, batch_size, n_views, channels, h, w,
+                              d_begin, d_count, d_scale, workspace, cv_out, 2, stream, nullptr,
+                              nullptr);
 }
 
 int mvs_homography_warp_fwd(const float* feat, const float* K, const float* R, const float* T,

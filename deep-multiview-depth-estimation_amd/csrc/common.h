@@ -35,7 +35,11 @@ __device__ inline void sample_coord(const float* __restrict__ G, float xn, float
   float v = __fmaf_rn(G[4], yn, __fmaf_rn(G[3], xn, G[5]));
   const float s = __fmaf_rn(G[7], yn, __fmaf_rn(G[6], xn, G[8]));
   if (fabsf(s) > 1e-8f) {
+#ifdef MVS_FAST_RCP
+    const float sc = __builtin_amdgcn_rcpf(__fadd_rn(s, 1e-8f));   // 1 ulp, 1 instruction
+#else
     const float sc = __fdiv_rn(1.0f, __fadd_rn(s, 1e-8f));
+#endif
     u = __fmul_rn(u, sc);
     v = __fmul_rn(v, sc);
   }

@@ -258,6 +258,14 @@ __global__ __launch_bounds__(kBlock) void ref_resample_kernel(const float4* __re
 constexpr int kTileW = MVS_EXP_TW;
 constexpr int kTileH = kBlock / kTileW;   // 8
 
+// staged kernel: pixels per tile row.  64-px rows for bf16 (128-B store rows) measured slower
+// (0.669 ms against 0.557 ms at cfg 2: 160 = 2.5 x 64 leaves a sixth of the lanes idle and the
+// kernel is bound by its gather/compute side, not by the bf16 stores), so both use 32.
+template <int ES>
+constexpr int tile_w() {
+  return kTileW;
+}
+
 template <int V>
 constexpr int group_planes() {
 #ifdef MVS_EXP_PG
@@ -379,26 +387,34 @@ constexpr int staged_slots() {
   return V <= 3 ? 2560 : (V <= 5 ? 3072 : 4096);   // 40 / 48 / 64 KB: 4 / 3 / 2 workgroups per CU
 #endif
 }
-#ifdef MVS_EXP_WPE
-#define MVS_STAGED_ATTR __attribute__((amdgpu_waves_per_eu(MVS_EXP_WPE)))
-#else
-#define MVS_STAGED_ATTR
+// 3 waves per SIMD (at most 168 VGPRs): without the hint the V = 3 kernel lands at 169 VGPRs and 2
+// waves; with it, 153 VGPRs and no VGPR spill.
+#ifndef MVS_EXP_WPE
+#define MVS_EXP_WPE 3
 #endif
+#define MVS_STAGED_ATTR __attribute__((amdgpu_waves_per_eu(MVS_EXP_WPE)))
+
+// Wave-wide min on the DPP network (no LDS traffic): xor-1 and xor-2 quad permutes, half-row and
+// row mirrors (min over 16 lanes), then the row broadcasts of lanes 15 and 31; lane 63 ends with the
+// minimum of the wave.  Lanes of rows a broadcast does not write keep their value (old = x).
+__device__ inline int wave_min_to_lane63(int x) {
+  x = min(x, __builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  x = min(x, __builtin_amdgcn_update_dpp(x, x, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  x = min(x, __builtin_amdgcn_update_dpp(x, x, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  x = min(x, __builtin_amdgcn_update_dpp(x, x, 0x140, 0xF, 0xF, false));  // row_mirror
+  x = min(x, __builtin_amdgcn_update_dpp(x, x, 0x142, 0xA, 0xF, false));  // row_bcast15 -> rows 1, 3
+  x = min(x, __builtin_amdgcn_update_dpp(x, x, 0x143, 0xC, 0xF, false));  // row_bcast31 -> rows 2, 3
+  return x;
+}
 
 // Workgroup-wide min of NV ints; every thread gets the result as a wave-uniform value.
 template <int NV>
 __device__ inline void block_min(int (&v)[NV], int* scratch /* >= 4 * NV ints of LDS */) {
+  const int wave = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    int x = v[k];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o));
-    v[k] = x;
-  }
-  const int wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) scratch[wave * NV + k] = v[k];
+    const int m = __builtin_amdgcn_readlane(wave_min_to_lane63(v[k]), 63);
+    if ((threadIdx.x & 63) == 0) scratch[wave * NV + k] = m;
   }
   __syncthreads();
 #pragma unroll
@@ -421,12 +437,29 @@ __device__ inline void store_cv(Rsrc rs, uint32_t voff, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)voff, 0, MVS_EXP_AUX);
 }
 
+// bf16 output (opt-in): the fp32 variance rounded to nearest-even exactly as
+// torch's float -> bfloat16 conversion (c10::BFloat16 round_to_nearest_even; NaN -> 0x7FC0).
+__device__ inline uint32_t bf16_rne(float v) {
+  const uint32_t u = __float_as_uint(v);
+  if (v != v) return 0x7FC0u;
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+
+template <int ES>
+__device__ inline void store_out(Rsrc rs, uint32_t voff, float v) {
+  if constexpr (ES == 4) {
+    store_cv(rs, voff, v);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bf16_rne(v), rs, (int)voff, 0, MVS_EXP_AUX);
+  }
+}
+
 constexpr int kPrefetch = 4;   // staging pieces per thread carried in registers across a chunk
 
-template <int V, int KPG>
+template <int V, int KPG, int ES /* output element bytes: 4 fp32, 2 bf16 */>
 __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_kernel(
     const float4* __restrict__ packed, const float4* __restrict__ refs,
-    const float* __restrict__ sampling, float* __restrict__ cv, int C, int h, int w, int Dc, int pg_n,
+    const float* __restrict__ sampling, void* __restrict__ cv, int C, int h, int w, int Dc, int pg_n,
     int tiles_x, int tiles_y, int groups, int total) {
   constexpr int NS = V - 1;
   constexpr int SLOTS = staged_slots<V>();
@@ -442,8 +475,9 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   const int t = wk / groups;
   const int tile = t % (tiles_x * tiles_y);
   const int b = t / (tiles_x * tiles_y);
-  const int px = (tile % tiles_x) * kTileW + (int)(threadIdx.x % kTileW);
-  const int py = (tile / tiles_x) * kTileH + (int)(threadIdx.x / kTileW);
+  constexpr int TW = tile_w<ES>(), TH = kBlock / TW;
+  const int px = (tile % tiles_x) * TW + (int)(threadIdx.x % TW);
+  const int py = (tile / tiles_x) * TH + (int)(threadIdx.x / TW);
   const bool active = px < w && py < h;
   const int k0 = g * pg_n;
   const int npl = min(pg_n, Dc - k0);
@@ -459,11 +493,14 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   for (int pl = 0; pl < KPG; ++pl)
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      pos[pl][s] = kInvalidTap;
-      fwx[pl][s] = fwy[pl][s] = 0.0f;
-      if (pl < npl)
-        src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + k0 + pl) * 9, xn, yn, h, w, active,
-                   pos[pl][s], fwx[pl][s], fwy[pl][s]);
+      // planes past the group's end (last group only) compute a clamped plane, then drop it
+      const int kk = k0 + (pl < npl ? pl : npl - 1);
+      src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + kk) * 9, xn, yn, h, w, active,
+                 pos[pl][s], fwx[pl][s], fwy[pl][s]);
+      if (pl >= npl) {
+        pos[pl][s] = kInvalidTap;
+        fwx[pl][s] = fwy[pl][s] = 0.0f;
+      }
     }
 
   // footprint of every source view: bounding box of the valid tap corners over the plane group
@@ -472,14 +509,14 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   for (int s = 0; s < NS; ++s) {
     int mnx = 1 << 30, mny = 1 << 30, mxx = 1 << 30, mxy = 1 << 30;   // mx*: -(max corner)
 #pragma unroll
-    for (int pl = 0; pl < KPG; ++pl) {
+    for (int pl = 0; pl < KPG; ++pl) {   // branch-free: invalid taps contribute 1 << 30
       const uint32_t p = pos[pl][s];
-      if (p != kInvalidTap) {
-        mnx = min(mnx, pos_x(p));
-        mny = min(mny, pos_y(p));
-        mxx = min(mxx, -pos_x(p));
-        mxy = min(mxy, -pos_y(p));
-      }
+      const bool ok = p != kInvalidTap;
+      const int x = pos_x(p), y = pos_y(p);
+      mnx = min(mnx, ok ? x : 1 << 30);
+      mny = min(mny, ok ? y : 1 << 30);
+      mxx = min(mxx, ok ? -x : 1 << 30);
+      mxy = min(mxy, ok ? -y : 1 << 30);
     }
     bb[4 * s + 0] = mnx;
     bb[4 * s + 1] = mny;
@@ -519,22 +556,23 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
 #ifdef MVS_EXP_NOSTORE
   const uint32_t soff0 = kOobOffset;
 #else
-  const uint32_t soff0 = active ? pix * 4u : kOobOffset;
+  const uint32_t soff0 = active ? pix * (uint32_t)ES : kOobOffset;
 #endif
-  const uint32_t grp_bytes = (uint32_t)npl * hw * 4u;
+  const uint32_t grp_bytes = (uint32_t)npl * hw * (uint32_t)ES;
 
   // store descriptors of chunk ch's four channels (planes k0 .. k0 + npl of this sample)
   auto chunk_rsrc = [&](int ch, Rsrc (&rs)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int c = ch * 4 + j;
-      rs[j] = make_rsrc(cv + (((size_t)b * C + (c < C ? c : 0)) * Dc + k0) * hw, c < C ? grp_bytes : 0u);
+      rs[j] = make_rsrc(static_cast<char*>(cv) + (((size_t)b * C + (c < C ? c : 0)) * Dc + k0) * hw * ES,
+                        c < C ? grp_bytes : 0u);
     }
   };
   auto emit = [&](int pl, const Rsrc (&rs)[4], const f4v& x0, const f4v (&xs)[NS]) {
     const f4v acc = variance4<NS>(x0, xs, inv_v);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) store_cv(rs[j], soff0 + (uint32_t)pl * hw * 4u, acc[j]);
+    for (int j = 0; j < 4; ++j) store_out<ES>(rs[j], soff0 + (uint32_t)pl * hw * (uint32_t)ES, acc[j]);
   };
 
   if (scum[NS] > SLOTS) {
@@ -677,8 +715,8 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   }
 }
 
-template <int V>
-void launch_gather(const Geometry& g, const float* feat, const float* smp, float* ws, float* cv,
+template <int V, int ES>
+void launch_gather(const Geometry& g, const float* feat, const float* smp, float* ws, void* cv,
                    hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int c4 = (g.C + 3) / 4;
   const PadGeom pgeo = pad_geom(g.h, g.w);
@@ -691,7 +729,13 @@ void launch_gather(const Geometry& g, const float* feat, const float* smp, float
   const uint32_t hw = (uint32_t)g.h * (uint32_t)g.w;
   hipLaunchKernelGGL(ref_resample_kernel, dim3((hw + kBlock - 1) / kBlock, (unsigned)(g.B * c4)),
                      dim3(kBlock), 0, s, packed, smp, refs, g.B, V, g.C, g.h, g.w, g.Dc);
-  const int tiles_x = (g.w + kTileW - 1) / kTileW, tiles_y = (g.h + kTileH - 1) / kTileH;
+#ifdef MVS_EXP_GATHER
+  constexpr int TW = kTileW;
+#else
+  constexpr int TW = tile_w<ES>();
+#endif
+  constexpr int TH = kBlock / TW;
+  const int tiles_x = (g.w + TW - 1) / TW, tiles_y = (g.h + TH - 1) / TH;
   // planes per workgroup: the register maximum, halved until the grid has >= 8 workgroups per CU
   int pg = group_planes<V>();
   while (pg > 1 && (long)g.B * tiles_x * tiles_y * ((g.Dc + pg - 1) / pg) < 2048) pg >>= 1;
@@ -699,11 +743,13 @@ void launch_gather(const Geometry& g, const float* feat, const float* smp, float
   const int total = g.B * tiles_x * tiles_y * groups;
   if (ev0) (void)hipEventRecord(ev0, s);
 #ifdef MVS_EXP_GATHER
-  hipLaunchKernelGGL((cost_volume_gather_kernel<V, group_planes<V>()>), xcd_grid(total), dim3(kBlock), 0,
-                     s, packed, refs, smp, cv, g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total);
+  if constexpr (ES == 4)
+    hipLaunchKernelGGL((cost_volume_gather_kernel<V, group_planes<V>()>), xcd_grid(total), dim3(kBlock),
+                       0, s, packed, refs, smp, static_cast<float*>(cv), g.C, g.h, g.w, g.Dc, pg, tiles_x,
+                       tiles_y, groups, total);
 #else
-  hipLaunchKernelGGL((cost_volume_staged_kernel<V, group_planes<V>()>), xcd_grid(total), dim3(kBlock), 0,
-                     s, packed, refs, smp, cv, g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total);
+  hipLaunchKernelGGL((cost_volume_staged_kernel<V, group_planes<V>(), ES>), xcd_grid(total), dim3(kBlock),
+                     0, s, packed, refs, smp, cv, g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total);
 #endif
   if (ev1) (void)hipEventRecord(ev1, s);
 }
@@ -726,17 +772,32 @@ size_t packed_bytes(int B, int V, int C, int h, int w) {
   return ((size_t)B * V * c4 * pad_geom(h, w).plane + (size_t)B * c4 * h * w) * sizeof(float4);
 }
 
+void launch_cost_volume_fwd_bf16(const Geometry& g, const float* feat, const float* sampling,
+                                 float* packed, void* cv, hipStream_t s, hipEvent_t ev0,
+                                 hipEvent_t ev1) {
+  switch (g.V) {
+    case 2: launch_gather<2, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 3: launch_gather<3, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 4: launch_gather<4, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 5: launch_gather<5, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 6: launch_gather<6, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 7: launch_gather<7, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 8: launch_gather<8, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    default: break;   // rejected by the C ABI (2 <= V <= 8 only)
+  }
+}
+
 void launch_cost_volume_fwd(const Geometry& g, const float* feat, const float* sampling,
                             float* packed, float* cv, hipStream_t s, hipEvent_t ev0,
                             hipEvent_t ev1) {
   switch (g.V) {
-    case 2: launch_gather<2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 3: launch_gather<3>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 4: launch_gather<4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 5: launch_gather<5>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 6: launch_gather<6>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 7: launch_gather<7>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 8: launch_gather<8>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 2: launch_gather<2, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 3: launch_gather<3, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 4: launch_gather<4, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 5: launch_gather<5, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 6: launch_gather<6, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 7: launch_gather<7, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 8: launch_gather<8, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
     default: launch_direct<MVS_MAX_VIEWS, false>(g, feat, sampling, cv, s, ev0, ev1); break;
   }
 }

@@ -21,6 +21,10 @@ size_t packed_bytes(int B, int V, int C, int h, int w);
 void launch_cost_volume_fwd(const Geometry& g, const float* feat, const float* sampling,
                             float* packed, float* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
                             hipEvent_t ev1 = nullptr);
+// same, bf16 cost volume (uint16 storage, RNE), 2 <= V <= 8
+void launch_cost_volume_fwd_bf16(const Geometry& g, const float* feat, const float* sampling,
+                                 float* packed, void* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
+                                 hipEvent_t ev1 = nullptr);
 
 // warp_variance.hip
 void launch_warp(const Geometry& g, const float* feat, const float* sampling, float* warped,

@@ -39,6 +39,8 @@ SIGNATURES = {
                                      _c_int, _c_int, _c_int, _c_float, _p, _p, _p]),
     "mvs_cost_volume_fwd_timed": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
                                            _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p]),
+    "mvs_cost_volume_fwd_bf16": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
+                                          _c_int, _c_int, _c_int, _c_float, _p, _p, _p]),
     "mvs_homography_warp_fwd": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
                                          _c_int, _c_int, _c_int, _c_float, _p, _p, _p]),
     "mvs_assemble_cost_volume_fwd": (_c_int, [_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,

@@ -8,6 +8,8 @@ assemble_cost_volume) with ONE fused HIP kernel (``mvs::cost_volume``): every vi
 the two-pass variance is accumulated in registers, so the B*V x C x D x h x w warped volume is never
 written; ``d_begin``/``d_count`` select a depth shard for the multi-GPU path.
 """
+import torch
+
 from . import ops
 from .config import D_NUM, D_SCALE
 from .homography import depth_hypotheses, reference_indices
@@ -19,15 +21,23 @@ def assemble_cost_volume(warped_feature_maps, n_views: int):
 
 def warp_and_assemble_cost_volume(K_batch, R_batch, T_batch, d_min, d_int, feature_maps,
                                   batch_size, n_views, d_num=D_NUM, d_scale=D_SCALE,
-                                  d_begin=0, d_count=None):
-    """-> (cv [B, C, d_count, h, w], d_batch_0 [B, d_num, 1, 1], ref_idx_0 [B] CPU int64)."""
+                                  d_begin=0, d_count=None, cv_dtype=torch.float32):
+    """-> (cv [B, C, d_count, h, w], d_batch_0 [B, d_num, 1, 1], ref_idx_0 [B] CPU int64).
+
+    ``cv_dtype=torch.bfloat16`` (opt-in) returns the fp32 variance rounded to
+    bf16 in the kernel's store (half the write); the default fp32 is the reference's."""
     if d_count is None:
         d_count = d_num - d_begin
     if d_begin < 0 or d_count <= 0 or d_begin + d_count > d_num:
         raise ValueError("depth shard [%d, %d) outside [0, %d)" % (d_begin, d_begin + d_count, d_num))
     device = feature_maps.device
     d_batch_0 = depth_hypotheses(d_min, d_int, d_num, d_scale).to(device)
-    cv, _ = ops.cost_volume(feature_maps, K_batch, R_batch, T_batch, d_min, d_int,
-                            int(batch_size), int(n_views), int(d_begin), int(d_count),
-                            float(d_scale))
+    if cv_dtype == torch.float32:
+        op = ops.cost_volume
+    elif cv_dtype == torch.bfloat16:
+        op = ops.cost_volume_bf16
+    else:
+        raise ValueError("cv_dtype must be torch.float32 or torch.bfloat16, got %s" % (cv_dtype,))
+    cv, _ = op(feature_maps, K_batch, R_batch, T_batch, d_min, d_int, int(batch_size), int(n_views),
+               int(d_begin), int(d_count), float(d_scale))
     return cv, d_batch_0, reference_indices(batch_size, n_views)

@@ -135,10 +135,16 @@ class MVSNet(nn.Module):
         c = self.cfg
         device = nn_input.device
         feature_maps = self.feature_encoder(nn_input)
+        bf16 = c.cv_dtype == "bfloat16"
         cost_volume, d_batch, ref_views = warp_and_assemble_cost_volume(
             K_batch, R_batch, T_batch, d_min, d_int, feature_maps, batch_size, n_views,
-            d_num=c.d_num, d_scale=c.d_scale)
-        prob_volume = self.cost_volume_reg(cost_volume)
+            d_num=c.d_num, d_scale=c.d_scale,
+            cv_dtype=torch.bfloat16 if bf16 else torch.float32)
+        if bf16:   # opt-in: regulariser under bf16 autocast, fp32 probabilities
+            with torch.autocast(device.type, dtype=torch.bfloat16):
+                prob_volume = self.cost_volume_reg(cost_volume).float()
+        else:
+            prob_volume = self.cost_volume_reg(cost_volume)
         initial_depth_map = extract_depth_map(prob_volume, d_batch, c.n_depth_est)
         return initial_depth_map, self.refine(nn_input, initial_depth_map, d_min, d_int, ref_views)
 

@@ -1,6 +1,7 @@
 """torch.library custom ops over the C ABI (namespace ``mvs``), with autograd and fake kernels.
 
   mvs::cost_volume            fused warp + variance      (homography.py:6-92 + costvolume.py:3-16)
+  mvs::cost_volume_bf16       same, bf16 cost volume     (opt-in)
   mvs::cost_volume_backward   d cv / d feat              (autograd of the above, train.py:103)
   mvs::homography_warp        warp only                  (homography.py:6-92 warped volume)
   mvs::assemble_cost_volume   variance of a warped volume (costvolume.py:3-16)
@@ -72,11 +73,46 @@ def cost_volume(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.T
     return cv, ws
 
 
+def _ws_floats(batch_size, n_views, c, h, w, d_count):
+    """Workspace size in floats, from the library's own size function (host-only, no GPU)."""
+    return max(_lib.load().mvs_cost_volume_workspace_bytes(batch_size, n_views, c, h, w, d_count), 4) // 4
+
+
 @cost_volume.register_fake
 def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scale):
     n, c, h, w = feat.shape
-    ws = ((n * d_count * 9 * 4 + 255) // 256 * 256 + n * ((c + 3) // 4) * 4 * h * w * 4) // 4
-    return (feat.new_empty((batch_size, c, d_count, h, w)), feat.new_empty((ws,)))
+    return (feat.new_empty((batch_size, c, d_count, h, w)),
+            feat.new_empty((_ws_floats(batch_size, n_views, c, h, w, d_count),)))
+
+
+@torch.library.custom_op("mvs::cost_volume_bf16", mutates_args=())
+def cost_volume_bf16(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.Tensor,
+                     d_min: torch.Tensor, d_int: torch.Tensor, batch_size: int, n_views: int,
+                     d_begin: int, d_count: int, d_scale: float) -> tuple[torch.Tensor, torch.Tensor]:
+    """mvs::cost_volume with a bf16 cost volume (SURVEY.md §8 f3, opt-in): the fp32 variance
+    rounded to nearest-even in the kernel's store, half the HBM write."""
+    _require_gpu(feat, "feature_maps")
+    lib = _lib.load()
+    feat = feat.to(_F32).contiguous()
+    K, R, T, d_min, d_int = _cams(K, R, T, d_min, d_int, feat.device, batch_size)
+    _check_geometry(feat, K, batch_size, n_views)
+    n, c, h, w = feat.shape
+    cv = torch.empty((batch_size, c, d_count, h, w), device=feat.device, dtype=torch.bfloat16)
+    ws = torch.empty((_ws_floats(batch_size, n_views, c, h, w, d_count),), device=feat.device,
+                     dtype=_F32)
+    st = lib.mvs_cost_volume_fwd_bf16(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T),
+                                      _lib.ptr(d_min), _lib.ptr(d_int), batch_size, n_views, c, h, w,
+                                      d_begin, d_count, float(d_scale), _lib.ptr(ws), _lib.ptr(cv),
+                                      _lib.stream_handle(feat.device))
+    _lib.check(st, "mvs_cost_volume_fwd_bf16")
+    return cv, ws
+
+
+@cost_volume_bf16.register_fake
+def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scale):
+    n, c, h, w = feat.shape
+    return (feat.new_empty((batch_size, c, d_count, h, w), dtype=torch.bfloat16),
+            feat.new_empty((_ws_floats(batch_size, n_views, c, h, w, d_count),)))
 
 
 @torch.library.custom_op("mvs::cost_volume_backward", mutates_args=())
@@ -117,6 +153,9 @@ def _cv_backward(ctx, grad_cv, _grad_ws):
 
 
 torch.library.register_autograd("mvs::cost_volume", _cv_backward, setup_context=_cv_setup)
+# bf16 cost volume: the rounding is passed straight through (d round(x) / dx := 1); the fp32
+# gradient kernel is reused on the upcast bf16 gradient
+torch.library.register_autograd("mvs::cost_volume_bf16", _cv_backward, setup_context=_cv_setup)
 
 
 # ----------------------------------------------------------------------------------------------

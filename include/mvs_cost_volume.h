@@ -96,6 +96,19 @@ int mvs_cost_volume_fwd_timed(const float* feat, const float* K, const float* R,
                               void* main_begin_event, void* main_end_event);
 
 /*
+ * mvs_cost_volume_fwd with a bf16 cost volume (reduced-precision cv, opt-in;
+ * halves the kernel's dominant write).  cv_out is [B][C][d_count][h][w] bf16 (uint16 storage):
+ * the fp32 variance of mvs_cost_volume_fwd rounded to nearest-even, bit-identical to
+ * torch's .to(torch.bfloat16) of that fp32 result.  2 <= n_views <= 8 (else
+ * MVS_ERR_UNSUPPORTED_VIEWS) or n_views == 1 (zeros).  Same workspace contract.
+ */
+int mvs_cost_volume_fwd_bf16(const float* feat, const float* K, const float* R, const float* T,
+                             const float* d_min, const float* d_int,
+                             int batch_size, int n_views, int channels, int h, int w,
+                             int d_begin, int d_count, float d_scale,
+                             float* workspace, void* cv_out, void* stream);
+
+/*
  * Warp only (API-compatible homography_warping, homography.py:6-92):
  * warped[N][C][d_count][h][w].  Same workspace contract as mvs_cost_volume_fwd.
  */
