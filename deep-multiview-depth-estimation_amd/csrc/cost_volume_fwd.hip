@@ -575,7 +575,8 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
     for (int j = 0; j < 4; ++j) store_out<ES>(rs[j], soff0 + (uint32_t)pl * hw * (uint32_t)ES, acc[j]);
   };
 
-  if (scum[NS] > SLOTS) {
+  // the last slot is the dummy target of prefetch registers that carry no piece (kDummy below)
+  if (scum[NS] > SLOTS - 1) {
     // footprint beyond the LDS budget (extreme zoom / long epipolar sweep): global gathers
     if (!active) return;   // no barriers below
     Rsrc rs[NS];
@@ -659,7 +660,7 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
 #pragma unroll
   for (int j = 0; j < kPrefetch; ++j) {
     const int q = (int)threadIdx.x + kBlock * j;
-    pslot[j] = 0;
+    pslot[j] = SLOTS - 1;   // dummy slot: never read
     psrc[j] = q < n_pieces ? piece(q, pslot[j]) : 0;
   }
   float4 pre[kPrefetch];
@@ -672,13 +673,19 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   };
   prefetch(0);
 
-  for (int ch = 0; ch < c4; ++ch) {
-    __syncthreads();   // every wave is done reading the previous chunk
+  // Staging of chunk ch from the prefetch registers (and the pieces beyond them) into LDS.  It runs
+  // right after the previous chunk's stores, and consumes only loads issued BEFORE those stores:
+  // vmcnt retires in issue order, so its waits are counted (vmcnt(36) ...) and never wait for the
+  // stores.  (With the staging at the top of the loop, the loop-header merge of the first
+  // iteration's counts made every wait there drain all of the previous chunk's stores.)
+  f4v x0;
+  auto stage = [&](int ch) {
+    x0 = f4v{rpre.x, rpre.y, rpre.z, rpre.w};
+    // branch-free: registers without a piece go to the dummy slot, so every wait here is executed
+    // by the whole wave and stays counted (a skipped conditional wait would leave the loads
+    // formally pending at the loop head and force a full vmcnt drain there)
 #pragma unroll
-    for (int j = 0; j < kPrefetch; ++j) {
-      const int q = (int)threadIdx.x + kBlock * j;
-      if (q < n_pieces) lds[pslot[j]] = f4v{pre[j].x, pre[j].y, pre[j].z, pre[j].w};
-    }
+    for (int j = 0; j < kPrefetch; ++j) lds[pslot[j]] = f4v{pre[j].x, pre[j].y, pre[j].z, pre[j].w};
 #ifndef MVS_EXP_NOSTAGE
     for (int q = (int)threadIdx.x + kBlock * kPrefetch; q < n_pieces; q += kBlock) {
       uint32_t slot;
@@ -686,8 +693,12 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
       lds[slot] = f4v{v.x, v.y, v.z, v.w};
     }
 #endif
-    const f4v x0 = {rpre.x, rpre.y, rpre.z, rpre.w};
+  };
+  stage(0);
+
+  for (int ch = 0; ch < c4; ++ch) {
     __syncthreads();   // chunk ch is in LDS
+    const f4v xr = x0;
     if (ch + 1 < c4) prefetch(ch + 1);   // in flight during this chunk's stores
     Rsrc ors[4];
     chunk_rsrc(ch, ors);
@@ -710,7 +721,11 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
         xs[s] = bilerp(tp, twx, twy);
 #endif
       }
-      emit(pl, ors, x0, xs);
+      emit(pl, ors, xr, xs);
+    }
+    if (ch + 1 < c4) {
+      __syncthreads();   // every wave is done reading chunk ch
+      stage(ch + 1);
     }
   }
 }
