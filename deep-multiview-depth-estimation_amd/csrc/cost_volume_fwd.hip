@@ -730,6 +730,23 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   }
 }
 
+// The staged kernel instantiated with KPG = pg: its per-plane tap state, staging and store loop are
+// unrolled over KPG planes, so a group narrower than the template (small plane shards, where pg is
+// halved to fill the chip) would still compute and drop KPG - pg planes.
+template <int V, int KPG, int ES>
+void launch_staged(int pg, dim3 grid, hipStream_t s, const float4* packed, const float4* refs,
+                   const float* smp, void* cv, const Geometry& g, int tiles_x, int tiles_y, int groups,
+                   int total) {
+  if constexpr (KPG > 1) {
+    if (pg < KPG) {
+      launch_staged<V, KPG / 2, ES>(pg, grid, s, packed, refs, smp, cv, g, tiles_x, tiles_y, groups, total);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((cost_volume_staged_kernel<V, KPG, ES>), grid, dim3(kBlock), 0, s, packed, refs, smp, cv,
+                     g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total);
+}
+
 template <int V, int ES>
 void launch_gather(const Geometry& g, const float* feat, const float* smp, float* ws, void* cv,
                    hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
@@ -751,9 +768,13 @@ void launch_gather(const Geometry& g, const float* feat, const float* smp, float
 #endif
   constexpr int TH = kBlock / TW;
   const int tiles_x = (g.w + TW - 1) / TW, tiles_y = (g.h + TH - 1) / TH;
-  // planes per workgroup: the register maximum, halved until the grid has >= 8 workgroups per CU
+  // planes per workgroup: the register maximum, halved until the grid has >= 4 workgroups per CU
+  // (cfg 4, 32-plane shards: 0.128 ms with the 8-plane template at pg = 1, 0.044 ms at pg = 2)
+#ifndef MVS_EXP_MINWG
+#define MVS_EXP_MINWG 1024
+#endif
   int pg = group_planes<V>();
-  while (pg > 1 && (long)g.B * tiles_x * tiles_y * ((g.Dc + pg - 1) / pg) < 2048) pg >>= 1;
+  while (pg > 1 && (long)g.B * tiles_x * tiles_y * ((g.Dc + pg - 1) / pg) < MVS_EXP_MINWG) pg >>= 1;
   const int groups = (g.Dc + pg - 1) / pg;
   const int total = g.B * tiles_x * tiles_y * groups;
   if (ev0) (void)hipEventRecord(ev0, s);
@@ -763,8 +784,8 @@ void launch_gather(const Geometry& g, const float* feat, const float* smp, float
                        0, s, packed, refs, smp, static_cast<float*>(cv), g.C, g.h, g.w, g.Dc, pg, tiles_x,
                        tiles_y, groups, total);
 #else
-  hipLaunchKernelGGL((cost_volume_staged_kernel<V, group_planes<V>(), ES>), xcd_grid(total), dim3(kBlock),
-                     0, s, packed, refs, smp, cv, g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total);
+  launch_staged<V, group_planes<V>(), ES>(pg, xcd_grid(total), s, packed, refs, smp, cv, g, tiles_x, tiles_y,
+                                         groups, total);
 #endif
   if (ev1) (void)hipEventRecord(ev1, s);
 }

@@ -63,6 +63,7 @@ def test_bf16_backward_is_straight_through():
     assert (grads[0] - grads[1]).abs().max().item() <= 1e-5 * max(scale, 1.0)
 
 
+@pytest.mark.timeout(400)   # first bf16 Conv3d use compiles MIOpen kernels on a fresh box (~2 min)
 def test_bf16_mvsnet_runs_close_to_fp32():
     """End to end with the opt-in: bf16 cv + bf16-autocast regulariser.  No parity claim against
     the reference (reduced precision by design); bounded against the fp32 model: median relative
@@ -70,7 +71,7 @@ def test_bf16_mvsnet_runs_close_to_fp32():
     from weights import deterministic_state_dict
     from mvs_amd.config import MVSConfig
     from mvs_amd.model import MVSNet
-    B, V, D, H, W = 1, 3, 48, 512, 640
+    B, V, D, H, W = 1, 3, 24, 256, 320
     K, R, T = camera_batch(B, V, H // 4, W // 4)
     d_min, d_int = depth_range(B)
     img = torch.randn(B * V, 3, H, W, generator=torch.Generator().manual_seed(5)).to(DEV)
