@@ -194,6 +194,29 @@ __device__ inline f4v bilerp_loop(const f4v (&t)[4], float wx, float wy) {
   return f4v{lo.x, lo.y, hi.x, hi.y};
 }
 
+// bilerp() with the weights rebuilt from a packed {wx, wy} register pair in 4 VALU: two v_pk_fma_f32
+// give e = {1 - wx, wx} and f = {1 - wy, wy} (fma(w, -1, 1) == 1 - w and fma(w, 1, 0) == w exactly, so
+// the weights are bit-identical to tap_weights()), then w01 = f.xx * e and w23 = f.yy * e.  The fmas
+// are volatile asm, so the compiler cannot hoist the weights out of the channel loop (which would
+// hold 4 VGPRs per (plane, view) instead of 2), and no opaque register copy is needed (the plain
+// bilerp() path pays 2 v_mov_b32 + 2 v_sub_f32 per (plane, view) per chunk for the same effect).
+__device__ inline f4v bilerp_pk(const f4v (&t)[4], f2v wxy, f2v cneg /* {-1, 1} */, f2v c10 /* {1, 0} */) {
+  f2v e, f;
+  asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(e) : "v"(wxy), "v"(cneg), "v"(c10));
+  asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,1]"
+               : "=v"(f) : "v"(wxy), "v"(cneg), "v"(c10));
+  const f2v w01 = f.xx * e;
+  const f2v w23 = f.yy * e;
+  f2v lo = t[0].xy * w01.xx, hi = t[0].zw * w01.xx;
+  lo = __builtin_elementwise_fma(t[1].xy, w01.yy, lo);
+  hi = __builtin_elementwise_fma(t[1].zw, w01.yy, hi);
+  lo = __builtin_elementwise_fma(t[2].xy, w23.xx, lo);
+  hi = __builtin_elementwise_fma(t[2].zw, w23.xx, hi);
+  lo = __builtin_elementwise_fma(t[3].xy, w23.yy, lo);
+  hi = __builtin_elementwise_fma(t[3].zw, w23.yy, hi);
+  return f4v{lo.x, lo.y, hi.x, hi.y};
+}
+
 __device__ inline void load_taps(Rsrc rs, uint32_t voff, int soff, int row_bytes, f4v (&t)[4]) {
   t[0] = ld4(rs, voff, soff);
   t[1] = ld4(rs, voff + 16u, soff);
@@ -540,14 +563,35 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
     zero_slots = max(zero_slots, rp[s] + 2);
   }
   zero_slots = (zero_slots + 15) & ~15;
-  pcum[0] = 0;
-  scum[0] = zero_slots;
+  int rh[NS];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int rh = rw[s] == 0 ? 0 : -bb[4 * s + 3] - ry0[s] + 2;
-    pcum[s + 1] = pcum[s] + rw[s] * rh;   // staging pieces (real pixels)
-    scum[s + 1] = scum[s] + rp[s] * rh;   // LDS slots (padded rows)
+  for (int s = 0; s < NS; ++s) rh[s] = rw[s] == 0 ? 0 : -bb[4 * s + 3] - ry0[s] + 2;
+  auto layout = [&]() {
+    pcum[0] = 0;
+    scum[0] = zero_slots;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      pcum[s + 1] = pcum[s] + rw[s] * rh[s];   // staging pieces (real pixels)
+      scum[s + 1] = scum[s] + rp[s] * rh[s];   // LDS slots (padded rows)
+    }
+  };
+  layout();
+#ifndef MVS_EXP_NOPADRETRY
+  // Over budget with 16-slot row pitches: retry with unpadded rows (pitch = width).  Row crossings
+  // inside a 16-lane ds_read_b128 group may then conflict, but the workgroup stays on LDS instead of
+  // the global-gather path (unpadded, 97.1 % of V = 5 footprints fit instead of 92.3 %,
+  // tools/footprint_stats.py).
+  if (scum[NS] > SLOTS - 1) {
+    zero_slots = 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      rp[s] = rw[s];
+      zero_slots = max(zero_slots, rp[s] + 2);
+    }
+    zero_slots = (zero_slots + 15) & ~15;
+    layout();
   }
+#endif
 
   const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
   const uint32_t pix = (uint32_t)(active ? py : 0) * (uint32_t)w + (uint32_t)(active ? px : 0);
@@ -579,6 +623,9 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   if (scum[NS] > SLOTS - 1) {
     // footprint beyond the LDS budget (extreme zoom / long epipolar sweep): global gathers
     if (!active) return;   // no barriers below
+#ifdef MVS_EXP_NOFALLBACK
+    return;
+#endif
     Rsrc rs[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s)
@@ -696,6 +743,7 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   };
   stage(0);
 
+  const f2v cneg = {-1.0f, 1.0f}, c10 = {1.0f, 0.0f};
   for (int ch = 0; ch < c4; ++ch) {
     __syncthreads();   // chunk ch is in LDS
     const f4v xr = x0;
@@ -715,6 +763,8 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
         tp[3] = lds[i0 + rp[s] + 1];
 #ifdef MVS_EXP_VSUBW   // 32 fewer VALU per chunk, but 200 VGPRs (2 waves per SIMD)
         xs[s] = bilerp_loop(tp, fwx[pl][s], fwy[pl][s]);
+#elif defined(MVS_EXP_PKW)
+        xs[s] = bilerp_pk(tp, f2v{fwx[pl][s], fwy[pl][s]}, cneg, c10);
 #else
         float twx = fwx[pl][s], twy = fwy[pl][s];
         asm volatile("" : "+v"(twx), "+v"(twy));

@@ -66,7 +66,7 @@ def main():
                         xx, yy = x0[s][sl[1:]][m], y0[s][sl[1:]][m]
                         rw = xx.max() - xx.min() + 2
                         rh = yy.max() - yy.min() + 2
-                        rp = (rw + 15) & ~15
+                        rp = rw if os.environ.get("NOPAD") else (rw + 15) & ~15
                         zero = max(zero, rp + 2)
                         total += rp * rh
                     total += (zero + 15) & ~15

@@ -66,6 +66,44 @@ __global__ void k_flat256pg(float* o, int total) {
       }
 }
 
+// (f) 32x8 tile, 8 planes: after a 4x4 quad transpose each lane owns 4 consecutive pixels of ONE
+// channel -> one float4 store per (plane, 4-channel chunk) instead of four dword stores
+template <bool NT>
+__global__ void k_tile32q(float* o, int total) {
+  int wk = xcd(blockIdx.x, total); if (wk >= total) return;
+  int tx = W / 32, ty = H / 8, groups = D / 8;
+  int g = wk % groups; int t = wk / groups; int tile = t % (tx * ty); int b = t / (tx * ty);
+  int lane = threadIdx.x;
+  int j = lane & 3;                       // channel within the chunk
+  int q = lane >> 2;                      // quad id: 64 quads = 8 per row x 8 rows
+  int px = (tile % tx) * 32 + (q & 7) * 4, py = (tile / tx) * 8 + (q >> 3);
+  for (int ch = 0; ch < C / 4; ++ch)
+    for (int pl = 0; pl < 8; ++pl) {
+      float* dst = o + (((size_t)b * C + ch * 4 + j) * D + g * 8 + pl) * HW + py * W + px;
+      f4 v = {(float)j, 1, 2, 3};
+      if (NT) __builtin_nontemporal_store(v, (f4*)dst); else *(f4*)dst = v;
+    }
+}
+// (g) 64x4 tile, 8 planes, dword per lane, 4 channels per chunk (rows of 256 B)
+template <bool NT>
+__global__ void k_tile64(float* o, int total) {
+  int wk = xcd(blockIdx.x, total); if (wk >= total) return;
+  int tx = W / 32, ty = H / 4, groups = D / 8;   // W = 160 = 2.5 x 64: half-used tiles at the edge
+  int g = wk % groups; int t = wk / groups; int tile = t % (tx * ty); int b = t / (tx * ty);
+  (void)tile; (void)b; (void)g;
+  int px = (tile % tx) * 32 + (int)(threadIdx.x % 64) / 2 * 0 + (int)(threadIdx.x % 32);
+  int py = (tile / tx) * 4 + (int)(threadIdx.x / 64);
+  // 32x4 per 128 threads: each tile is covered twice over two 8-plane halves to keep 256 threads
+  int half = (threadIdx.x / 32) & 1;
+  py = (tile / tx) * 4 + (int)(threadIdx.x / 64);
+  for (int ch = 0; ch < C / 4; ++ch)
+    for (int pl = 0; pl < 4; ++pl)
+      for (int jj = 0; jj < 4; ++jj) {
+        float* dst = o + (((size_t)b * C + ch * 4 + jj) * D + g * 8 + half * 4 + pl) * HW + py * W + px;
+        if (NT) __builtin_nontemporal_store((float)jj, dst); else *dst = (float)jj;
+      }
+}
+
 template <typename F>
 void timeit(const char* name, F launch, size_t bytes) {
   hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
@@ -99,6 +137,11 @@ int main() {
   timeit("flat256 pg8 nt", [&] { k_flat256pg<8, true><<<g(tf), 256>>>(o, tf); }, bytes);
   int tf2 = B * (HW / 256) * (D / 2);
   timeit("flat256 pg2 nt", [&] { k_flat256pg<2, true><<<g(tf2), 256>>>(o, tf2); }, bytes);
+  timeit("tile32 pg8 plain", [&] { k_tile<32, 8, false><<<g(t32), 256>>>(o, t32); }, bytes);
+  timeit("tile32 quad-f4 nt", [&] { k_tile32q<true><<<g(t32), 256>>>(o, t32); }, bytes);
+  timeit("tile32 quad-f4 plain", [&] { k_tile32q<false><<<g(t32), 256>>>(o, t32); }, bytes);
+  int t64 = B * (W / 32) * (H / 4) * (D / 8);
+  timeit("tile32x4 halves nt", [&] { k_tile64<true><<<g(t64), 256>>>(o, t64); }, bytes);
   hipFree(o);
   return 0;
 }
