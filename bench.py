@@ -264,6 +264,24 @@ def main():
         ms_step = 1000.0 * dt / args.steps
         maps = (B * world if args.mode == "samples" else B) * args.steps
         result["value"] = maps / dt
+        # the same step with the regulariser over the WHOLE volume (CostVolumeReg.forward_full,
+        # the reference's op sequence) instead of its eval-mode live regions: reported beside
+        # value so the gain of the live-region evaluation is visible
+        net.cost_volume_reg.live_region = False
+        full_steps = max(1, min(args.steps, 5))
+        with torch.no_grad():
+            step()
+            barrier(world)
+            t0 = time.perf_counter()
+            for _ in range(full_steps):
+                step()
+            barrier(world)
+            dtf = time.perf_counter() - t0
+        dtf = max_over_ranks(dtf, world, device)
+        result["full"] = {"ms_per_step": 1000.0 * dtf / full_steps,
+                          "value": (B * world if args.mode == "samples" else B) * full_steps / dtf,
+                          "steps": full_steps}
+        log("full-volume regulariser: %.2f ms/step" % result["full"]["ms_per_step"])
         del net
 
     # fused kernel timing (this rank's share of planes in dshard mode)
@@ -309,6 +327,11 @@ def main():
                            "cost_volume_staged kernels",
                      "op_GBps": alg / (op_ms * 1e-3) / 1e9},
     }
+    if "full" in result:
+        out["full_volume_regulariser"] = dict(result["full"], unit="depth maps/s", note=(
+            "same step with CostVolumeReg.forward_full (every voxel of every level, as "
+            "model.py:100-126 computes it); value uses forward_live (eval BN: only the regions "
+            "whose values reach the output; same sums, fp32 summation order may differ)"))
     # opt-in bf16 cost volume: informational, not the headline (reduced precision)
     _, bf_op_ms, bf_alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count, bf16=True)
     out["bf16_cv_opt_in"] = {"op_ms": bf_op_ms, "alg_bytes_per_launch": bf_alg,

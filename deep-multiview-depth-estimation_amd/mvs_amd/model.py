@@ -86,8 +86,57 @@ class CostVolumeReg(nn.Module):
         self.BN_2 = nn.BatchNorm3d(f4, eps=1e-5, momentum=0.1, device=device)
         self.BN_3 = nn.BatchNorm3d(f8, eps=1e-5, momentum=0.1, device=device)
         self.Norm = nn.Softmax(2)
+        self.pad, self.outpad = tuple(pad), tuple(outpad)
+        # eval-mode live-region evaluation (see forward_live); False = always the full-volume path
+        self.live_region = True
 
     def forward(self, cv):
+        if self.live_region and not self._bn_uses_batch_stats():
+            return self.forward_live(cv)
+        return self.forward_full(cv)
+
+    def _bn_uses_batch_stats(self):
+        return any(bn.training or bn.running_mean is None
+                   for bn in (self.BN_0, self.BN_1, self.BN_2, self.BN_3))
+
+    def forward_live(self, cv):
+        """Eval-mode regulariser evaluated only where its values reach the output.
+
+        The stride-2 convs pad every dim by n//2 + 1 (config.py:20), so output j of conv_k_0 reads
+        inputs 2j-P .. 2j-P+2 and is exactly 0 outside the middle half of each dim; the stride-2
+        transposed convs likewise only READ the middle half of their input (an input i lands on
+        outputs 2i-P .. 2i-P+2, off the [0, n) output range elsewhere).  Tracing the U-Net back
+        from the full-size output: deconv_1_0 needs its input on B (middle half), deconv_2_0 needs
+        its input on C2 (the middle of B), deconv_3_0 on C3 -- so level k's convs are evaluated on
+        its region only (+1 halo for the 3x3x3 stride-1 conv), with exact zero padding at the
+        tensor's borders.  Every output element is the same sum of the same products as in
+        forward_full (only structurally-zero products and discarded outputs are skipped); sums may
+        be ordered differently by MIOpen's kernels for the smaller shapes (fp32 rounding level).
+        Eval-mode BatchNorm is elementwise, so it commutes with the restriction; train-mode BN
+        (batch statistics over the whole volume, test.py:61) uses forward_full.
+        """
+        act = lambda bn, y: self.ReLU(bn(y))
+        n = tuple(cv.shape[2:])
+        full = tuple((0, d - 1) for d in n)
+        B = _tconv_input_region(full, n, self.pad)
+        C2 = _tconv_input_region(B, n, self.pad)
+        C3 = _tconv_input_region(C2, n, self.pad)
+        y0 = act(self.BN_0, self.conv_0_0(cv))
+        # level 1 on B, level 2 on C2, level 3 on C3 (regions carry their origin in the volume)
+        lv = []
+        for conv_a, conv_b, bn, reg in ((self.conv_1_0, self.conv_1_1, self.BN_1, B),
+                                        (self.conv_2_0, self.conv_2_1, self.BN_2, C2),
+                                        (self.conv_3_0, self.conv_3_1, self.BN_3, C3)):
+            halo = _grow(reg, n, 1)
+            y = act(bn, _conv_s2_region(cv, conv_a.weight, halo, self.pad))
+            lv.append(act(bn, _conv_s1_region(y, halo, conv_b.weight, reg, n)))
+        y1, y2, y3 = lv
+        y3 = act(self.BN_2, _tconv_region(y3, C3, self.deconv_3_0.weight, C2, self.pad))
+        y2 = act(self.BN_1, _tconv_region(y3 + y2, C2, self.deconv_2_0.weight, B, self.pad))
+        y1 = act(self.BN_0, _tconv_region(y2 + y1, B, self.deconv_1_0.weight, full, self.pad))
+        return self.Norm(self.conv_out(y1 + y0))
+
+    def forward_full(self, cv):
         act = lambda bn, y: self.ReLU(bn(y))
         # the BN modules are shared between levels exactly as in model.py:101-121
         y0 = act(self.BN_0, self.conv_0_0(cv))
@@ -101,6 +150,63 @@ class CostVolumeReg(nn.Module):
         y2 = act(self.BN_1, self.deconv_2_0(y3 + y2))
         y1 = act(self.BN_0, self.deconv_1_0(y2 + y1))
         return self.Norm(self.conv_out(y1 + y0))
+
+
+# ---- live-region helpers (CostVolumeReg.forward_live).  A region is a tuple of inclusive
+# (lo, hi) index ranges over (D, H, W); a region tensor holds the volume's values on it.
+def _grow(reg, n, k):
+    return tuple((max(lo - k, 0), min(hi + k, d - 1)) for (lo, hi), d in zip(reg, n))
+
+
+def _tconv_input_region(out_reg, n, pad):
+    """Inputs of a stride-2, kernel-3, padding-P transposed conv that reach outputs out_reg:
+    input i lands on outputs 2i - P + t, t = 0..2."""
+    return tuple((max(-((-(lo + p - 2)) // 2), 0), min((hi + p) // 2, d - 1))
+                 for (lo, hi), d, p in zip(out_reg, n, pad))
+
+
+def _crop_pad(x, x_reg, want, n):
+    """Values of the region tensor x (on x_reg) over the index box `want` (may leave the volume:
+    zeros there, i.e. the conv's zero padding).  `want` inside the volume must lie in x_reg."""
+    sl, pads = [], []
+    for (xlo, xhi), (lo, hi), d in zip(x_reg, want, n):
+        a, b = max(lo, 0), min(hi, d - 1)
+        assert xlo <= a and b <= xhi, "region tensor does not cover the requested box"
+        sl.append(slice(a - xlo, b - xlo + 1))
+        pads.append((a - lo, hi - b))
+    y = x[:, :, sl[0], sl[1], sl[2]]
+    flat = [v for pr in reversed(pads) for v in pr]   # F.pad order: W, H, D
+    return F.pad(y, flat) if any(flat) else y
+
+
+def _conv_s2_region(x, weight, out_reg, pad):
+    """conv3d(x, weight, stride 2, padding pad) on the output box out_reg (x: full volume)."""
+    n = tuple(x.shape[2:])
+    full = tuple((0, d - 1) for d in n)
+    want = tuple((2 * lo - p, 2 * hi - p + 2) for (lo, hi), p in zip(out_reg, pad))
+    return F.conv3d(_crop_pad(x, full, want, n), weight, stride=2)
+
+
+def _conv_s1_region(x, x_reg, weight, out_reg, n):
+    """conv3d(., weight, stride 1, padding 1) on out_reg, from the region tensor x on x_reg."""
+    want = tuple((lo - 1, hi + 1) for lo, hi in out_reg)
+    return F.conv3d(_crop_pad(x, x_reg, want, n), weight)
+
+
+def _tconv_region(x, x_reg, weight, out_reg, pad):
+    """conv_transpose3d(., weight, stride 2, padding pad) on out_reg, from the region tensor x on
+    x_reg (which must hold every input that reaches out_reg: _tconv_input_region)."""
+    y = F.conv_transpose3d(x, weight, stride=2)   # output q <-> volume index 2 * xlo + q - P
+    sl, pads = [], []
+    for (xlo, _), (lo, hi), p, m in zip(x_reg, out_reg, pad, y.shape[2:]):
+        o0 = 2 * xlo - p
+        a, b = lo - o0, hi - o0
+        assert a >= 0, "transposed-conv input region starts after the output box"
+        sl.append(slice(a, min(b, m - 1) + 1))
+        pads.append((0, max(b - (m - 1), 0)))   # outputs past the last input's reach are 0
+    y = y[:, :, sl[0], sl[1], sl[2]]
+    flat = [v for pr in reversed(pads) for v in pr]
+    return F.pad(y, flat) if any(flat) else y
 
 
 class DepthRefinement(nn.Module):

@@ -120,7 +120,10 @@ def mvsnet_forward(model, nn_input, K_batch, R_batch, T_batch, d_min, d_int, bat
                                                     batch_size, n_views, d_num, d_scale,
                                                     concat_growth=concat_growth)
     cv = assemble_cost_volume(warped, n_views)
-    prob = model.cost_volume_reg(cv)
+    reg = model.cost_volume_reg
+    # the reference's op sequence (model.py:100-126) over the whole volume: the build's
+    # eval-mode live-region shortcut (CostVolumeReg.forward_live) is not the oracle
+    prob = reg.forward_full(cv) if hasattr(reg, "forward_full") else reg(cv)
     initial = extract_depth_map(prob, d_batch)
     d_trans = d_min
     d_span = d_int.mul(d_num).mul(d_scale)

@@ -1,0 +1,73 @@
+"""CPU: the eval-mode live-region regulariser (CostVolumeReg.forward_live) against the full-volume
+op sequence of the reference (model.py:100-126, CostVolumeReg.forward_full).
+
+Both evaluate the same sums of the same products for every output element (forward_live skips only
+structurally-zero products of the n//2+1 padding and outputs no later layer reads); they differ by
+fp32 summation order only.  Shapes cover even/odd/degenerate extents of D, H and W."""
+import pytest
+import torch
+
+from mvs_amd.config import pad_outpad
+from mvs_amd.model import CostVolumeReg
+
+
+def _reg(D, h, w, seed=0):
+    torch.manual_seed(seed)
+    pad, outpad = pad_outpad(D, h, w)
+    m = CostVolumeReg(pad=pad, outpad=outpad)
+    for mod in m.modules():   # non-trivial eval statistics: BN(0) != 0 outside the live regions
+        if isinstance(mod, torch.nn.BatchNorm3d):
+            mod.running_mean.uniform_(-0.5, 0.5)
+            mod.running_var.uniform_(0.5, 2.0)
+            mod.weight.data.uniform_(0.5, 1.5)
+            mod.bias.data.uniform_(-0.5, 0.5)
+    return m
+
+
+@pytest.mark.parametrize("shape", [(8, 12, 16), (7, 9, 11), (20, 32, 40), (5, 6, 6), (2, 3, 4),
+                                   (1, 2, 3), (3, 1, 5), (48, 32, 40), (13, 10, 17)])
+def test_live_region_equals_full_volume(shape):
+    D, h, w = shape
+    m = _reg(D, h, w).eval()
+    cv = torch.rand(2, 32, D, h, w, generator=torch.Generator().manual_seed(D * 1000 + h))
+    with torch.no_grad():
+        full = m.forward_full(cv)
+        live = m(cv)
+    assert live.shape == full.shape == (2, 1, D, h, w)
+    torch.testing.assert_close(live, full, rtol=1e-5, atol=1e-7)
+
+
+def test_train_mode_bn_uses_full_volume():
+    """Train-mode BN normalises with statistics of the whole volume (test.py:61 runs the model in
+    train mode under no_grad), so the restriction does not apply: forward == forward_full."""
+    m = _reg(8, 12, 16).train()
+    cv = torch.rand(1, 32, 8, 12, 16)
+    with torch.no_grad():
+        a = m(cv)
+        m2 = _reg(8, 12, 16).train()
+        b = m2.forward_full(cv)
+    assert torch.equal(a, b)
+
+
+def test_live_region_disabled_flag():
+    m = _reg(8, 12, 16).eval()
+    m.live_region = False
+    cv = torch.rand(1, 32, 8, 12, 16)
+    with torch.no_grad():
+        assert torch.equal(m(cv), m.forward_full(cv))
+
+
+def test_live_region_gradients_match():
+    """Autograd through forward_live (eval BN, e.g. fine-tuning with frozen statistics) gives the
+    gradients of the full path w.r.t. the cost volume and the conv weights."""
+    m = _reg(6, 8, 10).eval()
+    cv = torch.rand(1, 32, 6, 8, 10)
+    g = torch.rand(1, 1, 6, 8, 10)
+    grads = []
+    for fn in (m.forward_full, m.forward_live):
+        x = cv.clone().requires_grad_(True)
+        m.zero_grad()
+        (fn(x) * g).sum().backward()
+        grads.append((x.grad.clone(), m.conv_3_1.weight.grad.clone(), m.deconv_1_0.weight.grad.clone()))
+    for a, b in zip(*grads):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-8)
