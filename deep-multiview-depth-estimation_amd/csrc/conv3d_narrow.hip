@@ -1,0 +1,136 @@
+// conv3d_narrow.hip -- 3x3x3, stride-1, padding-1, bias-free Conv3d with few output channels
+// (COUT = 1 or 8), for the regulariser's full-resolution layers that MIOpen runs far below the
+// chip's fp32 rate: conv_0_0 (32 -> 8, model.py:77) and conv_out (8 -> 1, model.py:96).
+//
+// out[b][co][d][y][x] = sum_{c, kd, ky, kx} W[co][c][kd][ky][kx] * in[b][c][d+kd-1][y+ky-1][x+kx-1]
+// (zero outside the volume), accumulated in fp32 in the order c, kd, ky, kx with one fma per term.
+//
+// A 256-thread workgroup owns a 32 x 8 (x, y) tile and DT consecutive depths of one sample; one
+// thread = one (x, y) column of DT output voxels x COUT channels, held in registers.  Per input
+// channel the workgroup stages the (DT + 2) x 10 x 34 halo block in LDS (zero-filled outside the
+// volume) plus that channel's COUT x 27 weights, then every thread reads the 9 taps of each staged
+// plane once (54 VGPRs) and applies them to the output depths they reach (plane p feeds depth
+// p - kd).  Weights are read as broadcast float4 LDS loads (scalar loads of a channel's 216
+// weights spilled 630 SGPRs).  The staging of channel c + 1 is loaded into registers before
+// channel c is computed.  Compute-bound: COUT * 27 fmas per staged input element.
+#include "launchers.h"
+
+namespace mvs {
+namespace {
+
+constexpr int kTX = 32, kTY = 8, kDT = 4;
+constexpr int kPX = kTX + 2, kPY = kTY + 2, kPD = kDT + 2;
+constexpr int kPlane = kPX * kPY;          // 340
+constexpr int kStage = kPD * kPlane;       // 3400 floats per input channel
+constexpr int kPer = (kStage + kBlock - 1) / kBlock;   // 8 staging elements per thread
+constexpr int kWPad = 12;                  // one (co, kd) row of 9 weights, padded to 3 float4
+
+template <int COUT>
+__global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(const float* __restrict__ in,
+                                                                  const float* __restrict__ wt,
+                                                                  float* __restrict__ out, int Cin,
+                                                                  int D, int H, int W, int tiles_x,
+                                                                  int tiles_y, int dgroups) {
+  __shared__ float lds[kStage];
+  __shared__ __attribute__((aligned(16))) float wl[COUT * 3 * kWPad];   // W[co][c][kd][.] of channel c
+  int t = blockIdx.x;
+  const int tx0 = (t % tiles_x) * kTX;
+  t /= tiles_x;
+  const int ty0 = (t % tiles_y) * kTY;
+  t /= tiles_y;
+  const int d0 = (t % dgroups) * kDT;
+  const int b = t / dgroups;
+  const size_t plane = (size_t)H * W;
+  const size_t vol = (size_t)D * plane;
+  const float* ib = in + (size_t)b * Cin * vol;
+
+  // staging map: element e of the halo block -> (global offset inside one channel, valid)
+  int goff[kPer];
+  bool gok[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int e = (int)threadIdx.x + j * kBlock;
+    const int pd = e / kPlane, r = e % kPlane;
+    const int py = r / kPX, px = r % kPX;
+    const int gz = d0 + pd - 1, gy = ty0 + py - 1, gx = tx0 + px - 1;
+    gok[j] = e < kStage && gz >= 0 && gz < D && gy >= 0 && gy < H && gx >= 0 && gx < W;
+    goff[j] = gok[j] ? (int)((size_t)gz * plane + (size_t)gy * W + gx) : 0;
+  }
+  float pre[kPer];
+  auto fetch = [&](int c) {
+    const float* src = ib + (size_t)c * vol;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) pre[j] = gok[j] ? src[goff[j]] : 0.0f;
+  };
+  fetch(0);
+
+  const int lx = (int)threadIdx.x % kTX, ly = (int)threadIdx.x / kTX;
+  float acc[kDT][COUT];
+#pragma unroll
+  for (int d = 0; d < kDT; ++d)
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) acc[d][co] = 0.0f;
+
+  for (int c = 0; c < Cin; ++c) {
+    __syncthreads();   // previous channel's reads are done
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int e = (int)threadIdx.x + j * kBlock;
+      if (e < kStage) lds[e] = pre[j];
+    }
+    for (int i = (int)threadIdx.x; i < COUT * 3 * kWPad; i += kBlock) {   // weights, rows padded to 12
+      const int co = i / (3 * kWPad), r = i % (3 * kWPad);
+      const int kd = r / kWPad, k = r % kWPad;
+      wl[i] = k < 9 ? wt[((size_t)co * Cin + c) * 27 + kd * 9 + k] : 0.0f;
+    }
+    __syncthreads();
+    if (c + 1 < Cin) fetch(c + 1);   // in flight during this channel's arithmetic
+    // the 9 taps of every staged plane, read once
+    float tap[kPD][9];
+#pragma unroll
+    for (int p = 0; p < kPD; ++p)
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) tap[p][ky * 3 + kx] = lds[p * kPlane + (ly + ky) * kPX + lx + kx];
+#pragma unroll
+    for (int kd = 0; kd < 3; ++kd)
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) {
+        // workgroup-uniform weights: broadcast LDS reads (one address for all lanes)
+        const float4* wr = reinterpret_cast<const float4*>(wl + (co * 3 + kd) * kWPad);
+        const float4 w0 = wr[0], w1 = wr[1], w2 = wr[2];
+        const float w[9] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x};
+#pragma unroll
+        for (int d = 0; d < kDT; ++d)   // output depth d reads plane d + kd through kernel depth kd
+#pragma unroll
+          for (int k = 0; k < 9; ++k) acc[d][co] = fmaf(tap[d + kd][k], w[k], acc[d][co]);
+      }
+  }
+
+  const int gx = tx0 + lx, gy = ty0 + ly;
+  if (gx >= W || gy >= H) return;
+  float* ob = out + (size_t)b * COUT * vol + (size_t)gy * W + gx;
+#pragma unroll
+  for (int d = 0; d < kDT; ++d) {
+    if (d0 + d >= D) break;
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) ob[(size_t)co * vol + (size_t)(d0 + d) * plane] = acc[d][co];
+  }
+}
+
+}  // namespace
+
+void launch_conv3d_k3_narrow(const float* in, const float* weight, float* out, int B, int Cin,
+                             int Cout, int D, int H, int W, hipStream_t s) {
+  const int tiles_x = (W + kTX - 1) / kTX, tiles_y = (H + kTY - 1) / kTY, dgroups = (D + kDT - 1) / kDT;
+  const dim3 grid((unsigned)((size_t)B * dgroups * tiles_y * tiles_x));
+  if (Cout == 8)
+    hipLaunchKernelGGL(conv3d_k3_narrow_kernel<8>, grid, dim3(kBlock), 0, s, in, weight, out, Cin, D, H,
+                       W, tiles_x, tiles_y, dgroups);
+  else
+    hipLaunchKernelGGL(conv3d_k3_narrow_kernel<1>, grid, dim3(kBlock), 0, s, in, weight, out, Cin, D, H,
+                       W, tiles_x, tiles_y, dgroups);
+}
+
+}  // namespace mvs

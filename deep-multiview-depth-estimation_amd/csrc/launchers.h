@@ -39,6 +39,10 @@ void launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* s
 void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, uint32_t hw,
                         int n_est, float* depth, hipStream_t s);
 
+// conv3d_narrow.hip: 3x3x3 stride-1 padding-1 bias-free Conv3d, NCDHW fp32, Cout in {1, 8}
+void launch_conv3d_k3_narrow(const float* in, const float* weight, float* out, int B, int Cin,
+                             int Cout, int D, int H, int W, hipStream_t s);
+
 // dtu_input.hip: data.py:206-210 image normalisation (uint8 HWC -> fp32 NCHW), data.py:300-301
 // depth thresholds
 void launch_normalize_images(const uint8_t* rgb, int n, uint32_t hw, const float* mean3,

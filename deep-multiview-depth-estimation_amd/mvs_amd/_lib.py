@@ -51,6 +51,7 @@ SIGNATURES = {
                                            _p]),
     "mvs_normalize_images": (_c_int, [_p, _c_int, _c_int, _c_int, _p, _p, _p, _p]),
     "mvs_depth_threshold": (_c_int, [_p, ctypes.c_size_t, _c_float, _c_float, _p, _p]),
+    "mvs_conv3d_k3_fwd": (_c_int, [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _p]),
 }
 
 

@@ -121,7 +121,7 @@ class CostVolumeReg(nn.Module):
         B = _tconv_input_region(full, n, self.pad)
         C2 = _tconv_input_region(B, n, self.pad)
         C3 = _tconv_input_region(C2, n, self.pad)
-        y0 = act(self.BN_0, self.conv_0_0(cv))
+        y0 = act(self.BN_0, _narrow_conv(self.conv_0_0, cv))
         # level 1 on B, level 2 on C2, level 3 on C3 (regions carry their origin in the volume)
         lv = []
         for conv_a, conv_b, bn, reg in ((self.conv_1_0, self.conv_1_1, self.BN_1, B),
@@ -134,7 +134,7 @@ class CostVolumeReg(nn.Module):
         y3 = act(self.BN_2, _tconv_region(y3, C3, self.deconv_3_0.weight, C2, self.pad))
         y2 = act(self.BN_1, _tconv_region(y3 + y2, C2, self.deconv_2_0.weight, B, self.pad))
         y1 = act(self.BN_0, _tconv_region(y2 + y1, B, self.deconv_1_0.weight, full, self.pad))
-        return self.Norm(self.conv_out(y1 + y0))
+        return self.Norm(_narrow_conv(self.conv_out, y1 + y0))
 
     def forward_full(self, cv):
         act = lambda bn, y: self.ReLU(bn(y))
@@ -150,6 +150,17 @@ class CostVolumeReg(nn.Module):
         y2 = act(self.BN_1, self.deconv_2_0(y3 + y2))
         y1 = act(self.BN_0, self.deconv_1_0(y2 + y1))
         return self.Norm(self.conv_out(y1 + y0))
+
+
+def _narrow_conv(conv, x):
+    """conv_0_0 (32 -> 8) / conv_out (8 -> 1) at full resolution: on a HIP device, in fp32 and
+    without autograd, the hand-written kernel (mvs::conv3d_k3, csrc/conv3d_narrow.hip: MIOpen
+    runs these narrow full-volume layers at a few TFLOP/s); otherwise the module itself."""
+    if (x.is_cuda and x.dtype == torch.float32 and not torch.is_grad_enabled()
+            and not torch.is_autocast_enabled()):
+        from .ops import conv3d_k3
+        return conv3d_k3(x, conv.weight)
+    return conv(x)
 
 
 # ---- live-region helpers (CostVolumeReg.forward_live).  A region is a tuple of inclusive

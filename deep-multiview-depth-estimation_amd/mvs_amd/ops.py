@@ -288,3 +288,32 @@ def _sam_backward(ctx, grad_depth):
 
 
 torch.library.register_autograd("mvs::extract_depth_map", _sam_backward, setup_context=_sam_setup)
+
+
+# ----------------------------------------------------------------------------------------------
+# mvs::conv3d_k3 -- CostVolumeReg.conv_0_0 (32 -> 8) / conv_out (8 -> 1), model.py:77,96
+# ----------------------------------------------------------------------------------------------
+@torch.library.custom_op("mvs::conv3d_k3", mutates_args=())
+def conv3d_k3(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """nn.Conv3d(c_in, c_out, 3, stride=1, padding=1, bias=False) forward, c_out in {1, 8}, fp32
+    NCDHW, on the HIP kernel (csrc/conv3d_narrow.hip).  Inference only (no autograd formula):
+    CostVolumeReg uses it on the eval-mode, no-grad path."""
+    _require_gpu(x, "x")
+    lib = _lib.load()
+    if x.dim() != 5 or weight.dim() != 5 or tuple(weight.shape[2:]) != (3, 3, 3) or weight.shape[1] != x.shape[1]:
+        raise ValueError("x [B, Cin, D, H, W] and weight [Cout, Cin, 3, 3, 3] expected, got %s / %s"
+                         % (tuple(x.shape), tuple(weight.shape)))
+    x = x.to(_F32).contiguous()
+    w = weight.to(device=x.device, dtype=_F32).contiguous()
+    b, cin, d, h, wd = x.shape
+    cout = w.shape[0]
+    y = torch.empty((b, cout, d, h, wd), device=x.device, dtype=_F32)
+    st = lib.mvs_conv3d_k3_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), b, cin, cout, d, h, wd,
+                               _lib.stream_handle(x.device))
+    _lib.check(st, "mvs_conv3d_k3_fwd")
+    return y
+
+
+@conv3d_k3.register_fake
+def _(x, weight):
+    return x.new_empty((x.shape[0], weight.shape[0]) + tuple(x.shape[2:]))

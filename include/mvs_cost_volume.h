@@ -165,6 +165,15 @@ int mvs_normalize_images(const unsigned char* rgb, int n_images, int h, int w, c
  */
 int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float* out, void* stream);
 
+/* Regulariser layers conv_0_0 (32 -> 8) and conv_out (8 -> 1) of CostVolumeReg (model.py:77,96 /
+ * forward at model.py:101,123): nn.Conv3d(c_in, c_out, 3, stride=1, padding=1, bias=False) over
+ * x[batch][c_in][d][h][w] fp32 with weight[c_out][c_in][3][3][3], into y[batch][c_out][d][h][w].
+ * c_out must be 1 or 8 (MVS_ERR_INVALID_ARGUMENT otherwise); d*h*w < 2^31.  Replaces the MIOpen
+ * convolution behind torch.nn.Conv3d.forward for these two layers in eval-mode inference; same
+ * products per output as the reference layer, fp32 summation order differs. */
+int mvs_conv3d_k3_fwd(const float* x, const float* weight, float* y, int batch, int c_in, int c_out,
+                      int d, int h, int w, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -344,3 +344,48 @@ def test_depth_sharded_single_rank_equals_model():
         owned, ini_s, ref_s = DepthShardedMVSNet(net, 1, 0)(img, K, R, T, d_min, d_int, 2, 3)
     assert owned == [0, 1]
     assert torch.equal(ini, ini_s) and torch.equal(ref, ref_s)
+
+
+@pytest.mark.parametrize("shape", [(2, 32, 8, 12, 20, 40), (1, 8, 1, 5, 9, 33), (1, 32, 8, 7, 8, 32),
+                                   (2, 8, 1, 16, 24, 70)])
+def test_narrow_conv3d_matches_torch(shape):
+    """mvs::conv3d_k3 (csrc/conv3d_narrow.hip, CostVolumeReg.conv_0_0 / conv_out) against the torch
+    fp32 Conv3d on the same device, and against float64 on the CPU: ragged x/y tiles, D not a
+    multiple of the 4-depth groups, both channel counts."""
+    from mvs_amd.ops import conv3d_k3
+    b, cin, cout, d, h, w = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(b, cin, d, h, w, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, 3, generator=g) * 0.1
+    ref64 = torch.nn.functional.conv3d(x.double(), wt.double(), padding=1)
+    with torch.no_grad():
+        y = conv3d_k3(x.to(DEV), wt.to(DEV)).cpu()
+        yt = torch.nn.functional.conv3d(x.to(DEV), wt.to(DEV), padding=1).cpu()
+    scale = ref64.abs().max().item()
+    err = (y.double() - ref64).abs().max().item()
+    err_t = (yt.double() - ref64).abs().max().item()
+    assert err <= 1e-5 * scale, (err, scale)
+    assert err <= 4 * err_t + 1e-6 * scale, (err, err_t)   # no worse than MIOpen's own fp32 sums
+
+
+def test_live_regulariser_gpu_matches_full_volume():
+    """Eval-mode CostVolumeReg on the GPU: live-region path (region convs + HIP conv_0_0/conv_out)
+    against the full-volume MIOpen path at a cfg-1-like shape."""
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import CostVolumeReg
+    D, h, w = 48, 32, 40
+    pad, outpad = pad_outpad(D, h, w)
+    torch.manual_seed(0)
+    m = CostVolumeReg(pad=pad, outpad=outpad)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.BatchNorm3d):
+            mod.running_mean.uniform_(-0.5, 0.5)
+            mod.running_var.uniform_(0.5, 2.0)
+            mod.weight.data.uniform_(0.5, 1.5)
+            mod.bias.data.uniform_(-0.5, 0.5)
+    m = m.to(DEV).eval()
+    cv = torch.rand(2, 32, D, h, w, generator=torch.Generator().manual_seed(1)).to(DEV)
+    with torch.no_grad():
+        live = m(cv)
+        full = m.forward_full(cv)
+    torch.testing.assert_close(live, full, rtol=1e-4, atol=1e-7)
