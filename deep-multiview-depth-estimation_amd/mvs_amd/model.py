@@ -191,11 +191,29 @@ def _crop_pad(x, x_reg, want, n):
 
 
 def _conv_s2_region(x, weight, out_reg, pad):
-    """conv3d(x, weight, stride 2, padding pad) on the output box out_reg (x: full volume)."""
+    """conv3d(x, weight, stride 2, padding pad) on the output box out_reg (x: full volume).
+
+    Output j reads inputs 2j - P .. 2j - P + 2.  The input box of out_reg usually leaves the volume
+    by different amounts on the two sides (n even); instead of materialising an asymmetrically
+    padded copy, the conv runs on the in-volume crop with a symmetric padding p >= both overhangs,
+    p of the left overhang's parity (so the stride-2 grid stays aligned), and the wanted outputs
+    are sliced out: every kept output reads exactly its own window."""
     n = tuple(x.shape[2:])
-    full = tuple((0, d - 1) for d in n)
-    want = tuple((2 * lo - p, 2 * hi - p + 2) for (lo, hi), p in zip(out_reg, pad))
-    return F.conv3d(_crop_pad(x, full, want, n), weight, stride=2)
+    sl, pads, offs = [], [], []
+    for (lo, hi), p, d in zip(out_reg, pad, n):
+        a, b = 2 * lo - p, 2 * hi - p + 2
+        ca, cb = max(a, 0), min(b, d - 1)
+        assert ca <= cb, "output box reads no input"
+        lp, rp = ca - a, b - cb
+        ps = max(lp, rp)
+        ps += (ps - lp) % 2
+        sl.append(slice(ca, cb + 1))
+        pads.append(ps)
+        offs.append((ps - lp) // 2)
+    y = F.conv3d(x[:, :, sl[0], sl[1], sl[2]], weight, stride=2, padding=tuple(pads))
+    cnt = [hi - lo + 1 for lo, hi in out_reg]
+    assert all(o + c <= m for o, c, m in zip(offs, cnt, y.shape[2:]))
+    return y[:, :, offs[0]:offs[0] + cnt[0], offs[1]:offs[1] + cnt[1], offs[2]:offs[2] + cnt[2]]
 
 
 def _conv_s1_region(x, x_reg, weight, out_reg, n):

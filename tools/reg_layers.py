@@ -8,8 +8,9 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "deep-multiview-depth-estimation_amd"))
+import bench  # noqa: E402,F401  (MIOPEN_USER_DB_PATH -> tools/miopen_db)
 import torch  # noqa: E402
-import torch.nn.functional as F  # noqa: E402
+import torch.nn.functional as F  # noqa: E402,F401
 from mvs_amd import model as M  # noqa: E402
 from mvs_amd.config import pad_outpad  # noqa: E402
 
@@ -40,7 +41,10 @@ def main():
     C3 = M._tconv_input_region(C2, n, pad)
     print("regions", Bq, C2, C3, flush=True)
     with torch.no_grad():
-        y0 = timed("conv_0_0 full", lambda: reg.conv_0_0(cv))
+        y0 = timed("conv_0_0 full (MIOpen)", lambda: reg.conv_0_0(cv))
+        from mvs_amd.ops import conv3d_k3
+        y0h = timed("conv_0_0 full (HIP conv3d_k3)", lambda: conv3d_k3(cv, reg.conv_0_0.weight))
+        print("  max |HIP - MIOpen| %.3g (max %.3g)" % ((y0h - y0).abs().max().item(), y0.abs().max().item()))
         timed("bn+relu y0", lambda: reg.ReLU(reg.BN_0(y0)))
         ys = []
         for k, (ca, cb, bn, r) in enumerate(((reg.conv_1_0, reg.conv_1_1, reg.BN_1, Bq),
@@ -55,15 +59,10 @@ def main():
         y2 = timed("deconv_2_0", lambda: M._tconv_region(y3 + y2, C2, reg.deconv_2_0.weight, Bq, pad))
         y1 = timed("deconv_1_0 (full output)", lambda: M._tconv_region(y2 + y1, Bq, reg.deconv_1_0.weight, full, pad))
         z = timed("add y1+y0", lambda: y1 + y0)
-        o = timed("conv_out full", lambda: reg.conv_out(z))
+        o = timed("conv_out full (MIOpen)", lambda: reg.conv_out(z))
+        timed("conv_out full (HIP conv3d_k3)", lambda: conv3d_k3(z, reg.conv_out.weight))
         timed("softmax", lambda: reg.Norm(o))
         timed("whole forward_live", lambda: reg(cv))
-        cvl = cv.contiguous(memory_format=torch.channels_last_3d)
-        c00 = torch.nn.Conv3d(32, 8, 3, padding=1, bias=False).to(dev).to(memory_format=torch.channels_last_3d)
-        timed("conv_0_0 channels_last", lambda: c00(cvl))
-        torch.backends.cudnn.benchmark = True
-        timed("conv_0_0 full (find)", lambda: reg.conv_0_0(cv))
-        timed("conv_out full (find)", lambda: reg.conv_out(z))
 
 
 if __name__ == "__main__":
