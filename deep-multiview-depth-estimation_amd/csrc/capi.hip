@@ -217,4 +217,18 @@ int mvs_conv3d_k3_fwd(const float* x, const float* weight, float* y, int batch, 
   return mvs::hip_status();
 }
 
+int mvs_deconv3d_k3s2_fwd(const float* x, int batch, int c_in, int c_out, int rd, int rh, int rw,
+                          int x0d, int x0h, int x0w, const float* weight, int d, int h, int w,
+                          int pd, int ph, int pw, const float* bn_scale, const float* bn_shift,
+                          const float* bn_mean, const float* residual, float* y, void* stream) {
+  if (!x || !weight || !y || batch <= 0 || c_in <= 0 || c_in > 64 || c_out != 8) return MVS_ERR_INVALID_ARGUMENT;
+  if (rd <= 0 || rh <= 0 || rw <= 0 || d <= 0 || h <= 0 || w <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if (x0d < 0 || x0h < 0 || x0w < 0 || pd < 0 || ph < 0 || pw < 0) return MVS_ERR_INVALID_ARGUMENT;
+  if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
+    return MVS_ERR_INVALID_ARGUMENT;
+  mvs::launch_deconv3d_k3s2(x, batch, c_in, rd, rh, rw, x0d, x0h, x0w, weight, d, h, w, pd, ph, pw, bn_scale,
+                            bn_shift, bn_mean, residual, y, (hipStream_t)stream);
+  return mvs::hip_status();
+}
+
 }  // extern "C"

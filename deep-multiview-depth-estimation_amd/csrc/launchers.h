@@ -43,6 +43,13 @@ void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, u
 void launch_conv3d_k3_narrow(const float* in, const float* weight, float* out, int B, int Cin,
                              int Cout, int D, int H, int W, hipStream_t s);
 
+// deconv3d_region.hip: stride-2 kernel-3 ConvTranspose3d (Cout 8) from a region tensor to the full
+// volume, optional fused BN(eval)+ReLU and residual add
+void launch_deconv3d_k3s2(const float* x, int B, int Cin, int rd, int rh, int rw, int x0d, int x0h,
+                          int x0w, const float* weight, int D, int H, int W, int pd, int ph, int pw,
+                          const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                          const float* residual, float* y, hipStream_t s);
+
 // dtu_input.hip: data.py:206-210 image normalisation (uint8 HWC -> fp32 NCHW), data.py:300-301
 // depth thresholds
 void launch_normalize_images(const uint8_t* rgb, int n, uint32_t hw, const float* mean3,

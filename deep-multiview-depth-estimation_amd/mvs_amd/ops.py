@@ -317,3 +317,39 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
 @conv3d_k3.register_fake
 def _(x, weight):
     return x.new_empty((x.shape[0], weight.shape[0]) + tuple(x.shape[2:]))
+
+
+
+# ----------------------------------------------------------------------------------------------
+# mvs::deconv3d_k3s2 -- CostVolumeReg.deconv_1_0 + BN_0 + ReLU + `+ y0` (model.py:121-123)
+# ----------------------------------------------------------------------------------------------
+@torch.library.custom_op("mvs::deconv3d_k3s2", mutates_args=())
+def deconv3d_k3s2(x: torch.Tensor, origin: list[int], weight: torch.Tensor, out_dims: list[int],
+                  pad: list[int], bn_scale: torch.Tensor, bn_shift: torch.Tensor,
+                  bn_mean: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:
+    """ConvTranspose3d(c_in, 8, 3, stride 2, padding pad) of the region tensor x (input region
+    starting at `origin`) into the full volume out_dims, then max((y - mean) * scale + shift, 0)
+    + residual (csrc/deconv3d_region.hip).  Inference only."""
+    _require_gpu(x, "x")
+    lib = _lib.load()
+    x = x.to(_F32).contiguous()
+    b, cin, rd, rh, rw = x.shape
+    w = weight.to(device=x.device, dtype=_F32).contiguous()
+    if tuple(w.shape) != (cin, 8, 3, 3, 3):
+        raise ValueError("weight [c_in, 8, 3, 3, 3] expected, got %s" % (tuple(w.shape),))
+    d, h, wd = out_dims
+    f = lambda t: t.to(device=x.device, dtype=_F32).contiguous()
+    sc, sh, mu, res = f(bn_scale), f(bn_shift), f(bn_mean), f(residual)
+    if tuple(res.shape) != (b, 8, d, h, wd):
+        raise ValueError("residual must be [B, 8, D, H, W]")
+    y = torch.empty((b, 8, d, h, wd), device=x.device, dtype=_F32)
+    st = lib.mvs_deconv3d_k3s2_fwd(_lib.ptr(x), b, cin, 8, rd, rh, rw, *origin, _lib.ptr(w), d, h, wd,
+                                   *pad, _lib.ptr(sc), _lib.ptr(sh), _lib.ptr(mu), _lib.ptr(res),
+                                   _lib.ptr(y), _lib.stream_handle(x.device))
+    _lib.check(st, "mvs_deconv3d_k3s2_fwd")
+    return y
+
+
+@deconv3d_k3s2.register_fake
+def _(x, origin, weight, out_dims, pad, bn_scale, bn_shift, bn_mean, residual):
+    return x.new_empty((x.shape[0], 8) + tuple(out_dims))

@@ -174,6 +174,19 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
 int mvs_conv3d_k3_fwd(const float* x, const float* weight, float* y, int batch, int c_in, int c_out,
                       int d, int h, int w, void* stream);
 
+/* Regulariser layer deconv_1_0 (model.py:87, forward at model.py:121): nn.ConvTranspose3d(c_in, 8,
+ * 3, stride=2, padding=(pd, ph, pw), output_padding, bias=False) into the full volume
+ * y[batch][8][d][h][w], from a REGION input x[batch][c_in][rd][rh][rw] holding the input on
+ * [x0, x0 + r) per dim (it must hold every input that reaches [0, n): CostVolumeReg.forward_live).
+ * weight[c_in][8][3][3][3] (ConvTranspose layout), c_in <= 64.  Optional epilogue (all three
+ * BN pointers or none; residual nullable): y = max((y - bn_mean) * bn_scale + bn_shift, 0)
+ * + residual, i.e. model.py:121-123's ReLU(BN_0(.)) and `+ y0` (eval BN: bn_scale =
+ * gamma / sqrt(var + eps), bn_shift = beta).  Eval-mode inference only. */
+int mvs_deconv3d_k3s2_fwd(const float* x, int batch, int c_in, int c_out, int rd, int rh, int rw,
+                          int x0d, int x0h, int x0w, const float* weight, int d, int h, int w,
+                          int pd, int ph, int pw, const float* bn_scale, const float* bn_shift,
+                          const float* bn_mean, const float* residual, float* y, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
