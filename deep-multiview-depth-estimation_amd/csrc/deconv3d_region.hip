@@ -6,86 +6,162 @@
 // so output o gathers the inputs i = (o + P - k) / 2 with o + P - k even: 1 or 2 taps per dim.
 // x is a REGION tensor: it holds the input only on [x0, x0 + r) per dim -- every input that
 // reaches an output in [0, n) (CostVolumeReg.forward_live); inputs outside it reach no output.
-// Epilogue (optional): z = max((y - mean) * rsqrt(var + eps) * gamma + beta, 0) + residual.
+// Epilogue (optional): z = max((y - mean) * scale + shift, 0) + residual (scale = gamma /
+// sqrt(var + eps), shift = beta: eval BN).
 //
-// One thread = one output voxel (x fastest: coalesced stores per channel plane) x COUT channels
-// in registers; weights in LDS.  HBM-bound: the full-size output (+ residual read) dominates.
+// One thread = one 2 x 2 x 2 block of output voxels (o = 2m + s, s = 0, 1 per dim) x 8 channels.
+// Per dim the block reads the two inputs L = x[m + q + c - 1], U = x[m + q + c] (P = 2q + c) and
+//   c = 1:  out(s=0) = L * W1,            out(s=1) = U * W0 + L * W2
+//   c = 0:  out(s=0) = U * W0 + L * W2,   out(s=1) = U * W1
+// -- the tensor product over the 3 dims is the block's 27 (input, tap) pairs, so a thread does
+// exactly the transposed conv's work, no lane diverges, and neighbouring lanes store adjacent
+// float2 pairs.  Weights of one input channel (8 x 27, padded to 28) are broadcast LDS reads.
+// HBM-bound: the full-size output (+ residual read) dominates.
 #include "launchers.h"
 
 namespace mvs {
 namespace {
 
 constexpr int kCout = 8;
+constexpr int kWRow = 28;   // 27 taps padded to 7 float4
 
-struct Taps1 {
-  int n;        // 1 or 2 valid taps
-  int i[2];     // input index inside the region
-  int k[2];     // kernel index
+// per dim: (input slot 0 = L, 1 = U, kernel tap k) pairs feeding output s
+template <int C>
+struct Stencil {
+  // n[s]: number of terms for output s; in[s][t], k[s][t]
+  static constexpr int n0 = C ? 1 : 2, n1 = C ? 2 : 1;
+  static constexpr int in0[2] = {C ? 0 : 1, 0};
+  static constexpr int k0[2] = {C ? 1 : 0, 2};
+  static constexpr int in1[2] = {C ? 1 : 1, 0};
+  static constexpr int k1[2] = {C ? 0 : 1, 2};
 };
 
-__device__ inline Taps1 taps1(int o, int p, int x0, int r) {
-  Taps1 t;
-  t.n = 0;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int q = o + p - k;
-    if (q & 1) continue;
-    const int i = (q >> 1) - x0;
-    if (i < 0 || i >= r) continue;
-    t.i[t.n] = i;
-    t.k[t.n] = k;
-    ++t.n;
-  }
-  return t;
-}
-
+template <int CD, int CH, int CW>
 __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
     const float* __restrict__ x, const float* __restrict__ wt, int Cin, int rd, int rh, int rw,
-    int x0d, int x0h, int x0w, int D, int H, int W, int pd, int ph, int pw,
+    int x0d, int x0h, int x0w, int D, int H, int W, int qd, int qh, int qw,
     const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
     const float* __restrict__ mean, const float* __restrict__ residual, float* __restrict__ y,
-    size_t total) {
-  extern __shared__ float wl[];   // W[ci][co][27]
-  const int nw = Cin * kCout * 27;
-  for (int e = (int)threadIdx.x; e < nw; e += kBlock) wl[e] = wt[e];
+    int md_n, int mh_n, int mw_n, size_t total) {
+  extern __shared__ float4 wl4[];   // [ci][co][7] float4 = W[ci][co][27] padded
+  float* wl = reinterpret_cast<float*>(wl4);
+  const int nw = Cin * kCout * kWRow;
+  for (int e = (int)threadIdx.x; e < nw; e += kBlock) {
+    const int k = e % kWRow, cc = e / kWRow;
+    wl[e] = k < 27 ? wt[(size_t)cc * 27 + k] : 0.0f;
+  }
   __syncthreads();
   const size_t gid = (size_t)blockIdx.x * kBlock + threadIdx.x;
   if (gid >= total) return;
-  const int ow = (int)(gid % W);
-  size_t t = gid / W;
-  const int oh = (int)(t % H);
-  t /= H;
-  const int od = (int)(t % D);
-  const int b = (int)(t / D);
-  const Taps1 td = taps1(od, pd, x0d, rd), th = taps1(oh, ph, x0h, rh), tw = taps1(ow, pw, x0w, rw);
+  const int mw = (int)(gid % mw_n);
+  size_t t = gid / mw_n;
+  const int mh = (int)(t % mh_n);
+  t /= mh_n;
+  const int md = (int)(t % md_n);
+  const int b = (int)(t / md_n);
+  // region-relative indices of L (slot 0) and U (slot 1) per dim, and their validity
+  const int ld = md + qd + CD - 1 - x0d, lh = mh + qh + CH - 1 - x0h, lw = mw + qw + CW - 1 - x0w;
+  bool okd[2], okh[2], okw[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    okd[j] = ld + j >= 0 && ld + j < rd;
+    okh[j] = lh + j >= 0 && lh + j < rh;
+    okw[j] = lw + j >= 0 && lw + j < rw;
+  }
   const size_t rvol = (size_t)rd * rh * rw;
   const float* xb = x + (size_t)b * Cin * rvol;
-  float acc[kCout];
+  float acc[2][2][2][kCout];
 #pragma unroll
-  for (int co = 0; co < kCout; ++co) acc[co] = 0.0f;
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int co = 0; co < kCout; ++co) acc[a][c][e][co] = 0.0f;
+  using SD = Stencil<CD>;
+  using SH = Stencil<CH>;
+  using SW = Stencil<CW>;
   for (int ci = 0; ci < Cin; ++ci) {
     const float* xc = xb + (size_t)ci * rvol;
-    const float* wc = wl + ci * kCout * 27;
-    for (int a = 0; a < td.n; ++a)
-      for (int c = 0; c < th.n; ++c)
-        for (int e = 0; e < tw.n; ++e) {
-          const float v = xc[((size_t)td.i[a] * rh + th.i[c]) * rw + tw.i[e]];
-          const int k = td.k[a] * 9 + th.k[c] * 3 + tw.k[e];
+    float v[2][2][2];
 #pragma unroll
-          for (int co = 0; co < kCout; ++co) acc[co] = fmaf(v, wc[co * 27 + k], acc[co]);
-        }
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          v[a][c][e] = (okd[a] && okh[c] && okw[e]) ? xc[((size_t)(ld + a) * rh + (lh + c)) * rw + (lw + e)] : 0.0f;
+#pragma unroll
+    for (int co = 0; co < kCout; ++co) {
+      const float4* wr = wl4 + (ci * kCout + co) * (kWRow / 4);
+      float w[kWRow];
+#pragma unroll
+      for (int q = 0; q < kWRow / 4; ++q) {
+        const float4 f = wr[q];
+        w[4 * q] = f.x; w[4 * q + 1] = f.y; w[4 * q + 2] = f.z; w[4 * q + 3] = f.w;
+      }
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd)
+#pragma unroll
+        for (int td = 0; td < (sd ? SD::n1 : SD::n0); ++td)
+#pragma unroll
+          for (int sh = 0; sh < 2; ++sh)
+#pragma unroll
+            for (int th = 0; th < (sh ? SH::n1 : SH::n0); ++th)
+#pragma unroll
+              for (int sw = 0; sw < 2; ++sw)
+#pragma unroll
+                for (int tw = 0; tw < (sw ? SW::n1 : SW::n0); ++tw) {
+                  const int id = sd ? SD::in1[td] : SD::in0[td], kd = sd ? SD::k1[td] : SD::k0[td];
+                  const int ih = sh ? SH::in1[th] : SH::in0[th], kh = sh ? SH::k1[th] : SH::k0[th];
+                  const int iw = sw ? SW::in1[tw] : SW::in0[tw], kw = sw ? SW::k1[tw] : SW::k0[tw];
+                  acc[sd][sh][sw][co] = fmaf(v[id][ih][iw], w[kd * 9 + kh * 3 + kw], acc[sd][sh][sw][co]);
+                }
+    }
   }
   const size_t plane = (size_t)D * H * W;
-  const size_t pos = ((size_t)od * H + oh) * W + ow;
-  float* yb = y + (size_t)b * kCout * plane + pos;
-  const float* rb = residual ? residual + (size_t)b * kCout * plane + pos : nullptr;
+  const int od0 = 2 * md, oh0 = 2 * mh, ow0 = 2 * mw;
+  const bool w2 = ow0 + 1 < W;
+  float* yb = y + (size_t)b * kCout * plane;
+  const float* rb = residual ? residual + (size_t)b * kCout * plane : nullptr;
 #pragma unroll
   for (int co = 0; co < kCout; ++co) {
-    float v = acc[co];
-    if (bn_scale) v = fmaxf((v - mean[co]) * bn_scale[co] + bn_shift[co], 0.0f);
-    if (rb) v += rb[(size_t)co * plane];
-    yb[(size_t)co * plane] = v;
+    const float m = bn_scale ? mean[co] : 0.0f, sc = bn_scale ? bn_scale[co] : 0.0f,
+                sh = bn_scale ? bn_shift[co] : 0.0f;
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int od = od0 + sd, oh = oh0 + s2;
+        if (od >= D || oh >= H) continue;
+        const size_t off = (size_t)co * plane + ((size_t)od * H + oh) * W + ow0;
+        float o[2];
+#pragma unroll
+        for (int sw = 0; sw < 2; ++sw) {
+          float v = acc[sd][s2][sw][co];
+          if (bn_scale) v = fmaxf((v - m) * sc + sh, 0.0f);
+          o[sw] = v;
+        }
+        if (w2 && !(off & 1)) {   // 8-byte aligned pair
+          float2 r = rb ? *reinterpret_cast<const float2*>(rb + off) : make_float2(0.0f, 0.0f);
+          *reinterpret_cast<float2*>(yb + off) = make_float2(o[0] + r.x, o[1] + r.y);
+        } else {
+          yb[off] = o[0] + (rb ? rb[off] : 0.0f);
+          if (w2) yb[off + 1] = o[1] + (rb ? rb[off + 1] : 0.0f);
+        }
+      }
   }
+}
+
+template <int CD, int CH, int CW>
+void launch_cls(dim3 grid, size_t lds, hipStream_t s, const float* x, const float* weight, int Cin,
+                int rd, int rh, int rw, int x0d, int x0h, int x0w, int D, int H, int W, int pd, int ph,
+                int pw, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                const float* residual, float* y, int md_n, int mh_n, int mw_n, size_t total) {
+  hipLaunchKernelGGL((deconv3d_k3s2_kernel<CD, CH, CW>), grid, dim3(kBlock), lds, s, x, weight, Cin, rd, rh,
+                     rw, x0d, x0h, x0w, D, H, W, pd >> 1, ph >> 1, pw >> 1, bn_scale, bn_shift, bn_mean,
+                     residual, y, md_n, mh_n, mw_n, total);
 }
 
 }  // namespace
@@ -94,12 +170,22 @@ void launch_deconv3d_k3s2(const float* x, int B, int Cin, int rd, int rh, int rw
                           int x0w, const float* weight, int D, int H, int W, int pd, int ph, int pw,
                           const float* bn_scale, const float* bn_shift, const float* bn_mean,
                           const float* residual, float* y, hipStream_t s) {
-  const size_t total = (size_t)B * D * H * W;
-  const size_t blocks = (total + kBlock - 1) / kBlock;
-  const size_t lds = (size_t)Cin * kCout * 27 * sizeof(float);
-  hipLaunchKernelGGL(deconv3d_k3s2_kernel, dim3((unsigned)blocks), dim3(kBlock), lds, s, x, weight, Cin,
-                     rd, rh, rw, x0d, x0h, x0w, D, H, W, pd, ph, pw, bn_scale, bn_shift, bn_mean, residual,
-                     y, total);
+  const int md_n = (D + 1) / 2, mh_n = (H + 1) / 2, mw_n = (W + 1) / 2;
+  const size_t total = (size_t)B * md_n * mh_n * mw_n;
+  const dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
+  const size_t lds = (size_t)Cin * kCout * kWRow * sizeof(float);
+  const int cls = (pd & 1) * 4 + (ph & 1) * 2 + (pw & 1);
+#define MVS_DECONV_CASE(c)                                                                         \
+  case c:                                                                                          \
+    launch_cls<(c >> 2) & 1, (c >> 1) & 1, c & 1>(grid, lds, s, x, weight, Cin, rd, rh, rw, x0d, x0h, \
+                                                  x0w, D, H, W, pd, ph, pw, bn_scale, bn_shift,     \
+                                                  bn_mean, residual, y, md_n, mh_n, mw_n, total);   \
+    break;
+  switch (cls) {
+    MVS_DECONV_CASE(0) MVS_DECONV_CASE(1) MVS_DECONV_CASE(2) MVS_DECONV_CASE(3)
+    MVS_DECONV_CASE(4) MVS_DECONV_CASE(5) MVS_DECONV_CASE(6) MVS_DECONV_CASE(7)
+  }
+#undef MVS_DECONV_CASE
 }
 
 }  // namespace mvs

@@ -133,8 +133,16 @@ class CostVolumeReg(nn.Module):
         y1, y2, y3 = lv
         y3 = act(self.BN_2, _tconv_region(y3, C3, self.deconv_3_0.weight, C2, self.pad))
         y2 = act(self.BN_1, _tconv_region(y3 + y2, C2, self.deconv_2_0.weight, B, self.pad))
-        y1 = act(self.BN_0, _tconv_region(y2 + y1, B, self.deconv_1_0.weight, full, self.pad))
-        return self.Norm(_narrow_conv(self.conv_out, y1 + y0))
+        if _hip_inference(cv):
+            # deconv_1_0 -> BN_0 -> ReLU -> + y0 in one HIP kernel (csrc/deconv3d_region.hip)
+            from .ops import deconv3d_k3s2
+            bn = self.BN_0
+            scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+            z = deconv3d_k3s2(y2 + y1, [lo for lo, _ in B], self.deconv_1_0.weight, list(n),
+                              list(self.pad), scale, bn.bias, bn.running_mean, y0)
+        else:
+            z = act(self.BN_0, _tconv_region(y2 + y1, B, self.deconv_1_0.weight, full, self.pad)) + y0
+        return self.Norm(_narrow_conv(self.conv_out, z))
 
     def forward_full(self, cv):
         act = lambda bn, y: self.ReLU(bn(y))
@@ -152,12 +160,18 @@ class CostVolumeReg(nn.Module):
         return self.Norm(self.conv_out(y1 + y0))
 
 
+def _hip_inference(x):
+    """fp32 inference on a HIP device (no autograd, no autocast): the regulariser's hand-written
+    full-resolution layers apply."""
+    return (x.is_cuda and x.dtype == torch.float32 and not torch.is_grad_enabled()
+            and not torch.is_autocast_enabled())
+
+
 def _narrow_conv(conv, x):
     """conv_0_0 (32 -> 8) / conv_out (8 -> 1) at full resolution: on a HIP device, in fp32 and
     without autograd, the hand-written kernel (mvs::conv3d_k3, csrc/conv3d_narrow.hip: MIOpen
     runs these narrow full-volume layers at a few TFLOP/s); otherwise the module itself."""
-    if (x.is_cuda and x.dtype == torch.float32 and not torch.is_grad_enabled()
-            and not torch.is_autocast_enabled()):
+    if _hip_inference(x):
         from .ops import conv3d_k3
         return conv3d_k3(x, conv.weight)
     return conv(x)

@@ -389,3 +389,35 @@ def test_live_regulariser_gpu_matches_full_volume():
         live = m(cv)
         full = m.forward_full(cv)
     torch.testing.assert_close(live, full, rtol=1e-4, atol=1e-7)
+
+
+def test_region_deconv_fused_epilogue_matches_torch():
+    """mvs::deconv3d_k3s2 (csrc/deconv3d_region.hip): deconv_1_0 from its live input region into the
+    full volume, with BN_0(eval) + ReLU + `+ y0` fused, against the torch ops on the same device
+    (full-size transposed conv of the zero-extended input, then BN, ReLU, add)."""
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _tconv_input_region
+    from mvs_amd.ops import deconv3d_k3s2
+    for (D, h, w) in ((48, 32, 40), (13, 10, 17)):
+        pad, outpad = pad_outpad(D, h, w)
+        n = (D, h, w)
+        reg = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
+        g = torch.Generator().manual_seed(D)
+        x_full = torch.zeros(2, 16, D, h, w)
+        sl = tuple(slice(lo, hi + 1) for lo, hi in reg)
+        x_full[:, :, sl[0], sl[1], sl[2]] = torch.randn(2, 16, *[hi - lo + 1 for lo, hi in reg], generator=g)
+        wt = torch.randn(16, 8, 3, 3, 3, generator=g) * 0.1
+        mean, var = torch.randn(8, generator=g) * 0.1, torch.rand(8, generator=g) + 0.5
+        gamma, beta = torch.rand(8, generator=g) + 0.5, torch.randn(8, generator=g) * 0.1
+        y0 = torch.randn(2, 8, D, h, w, generator=g)
+        dev = lambda t: t.to(DEV)
+        with torch.no_grad():
+            ref = torch.nn.functional.conv_transpose3d(dev(x_full), dev(wt), stride=2, padding=pad,
+                                                       output_padding=outpad)
+            ref = torch.relu((ref - dev(mean).view(1, 8, 1, 1, 1)) / torch.sqrt(dev(var) + 1e-5).view(1, 8, 1, 1, 1)
+                             * dev(gamma).view(1, 8, 1, 1, 1) + dev(beta).view(1, 8, 1, 1, 1)) + dev(y0)
+            x_reg = dev(x_full[:, :, sl[0], sl[1], sl[2]])
+            out = deconv3d_k3s2(x_reg, [lo for lo, _ in reg], dev(wt), list(n), list(pad),
+                                dev(gamma / torch.sqrt(var + 1e-5)), dev(beta), dev(mean), dev(y0))
+        assert out.shape == ref.shape
+        torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
