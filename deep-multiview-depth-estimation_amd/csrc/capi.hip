@@ -207,13 +207,17 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
 }
 
 int mvs_conv3d_k3_fwd(const float* x, const float* weight, float* y, int batch, int c_in, int c_out,
-                      int d, int h, int w, void* stream) {
+                      int d, int h, int w, const float* bn_scale, const float* bn_shift,
+                      const float* bn_mean, void* stream) {
   if (!x || !weight || !y || batch <= 0 || c_in <= 0 || d <= 0 || h <= 0 || w <= 0)
     return MVS_ERR_INVALID_ARGUMENT;
   if (c_out != 1 && c_out != 8) return MVS_ERR_INVALID_ARGUMENT;
+  if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
+    return MVS_ERR_INVALID_ARGUMENT;
   // staging offsets inside one channel volume are 32-bit
   if ((uint64_t)d * (uint64_t)h * (uint64_t)w >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
-  mvs::launch_conv3d_k3_narrow(x, weight, y, batch, c_in, c_out, d, h, w, (hipStream_t)stream);
+  mvs::launch_conv3d_k3_narrow(x, weight, y, batch, c_in, c_out, d, h, w, bn_scale, bn_shift, bn_mean,
+                               (hipStream_t)stream);
   return mvs::hip_status();
 }
 

@@ -5,8 +5,8 @@
 // out[b][co][d][y][x] = sum_{c, kd, ky, kx} W[co][c][kd][ky][kx] * in[b][c][d+kd-1][y+ky-1][x+kx-1]
 // (zero outside the volume), accumulated in fp32 in the order c, kd, ky, kx with one fma per term.
 //
-// A 256-thread workgroup owns a 32 x 8 (x, y) tile and DT consecutive depths of one sample; one
-// thread = one (x, y) column of DT output voxels x COUT channels, held in registers.  Per input
+// A 256-thread workgroup owns a 32 x 8 NR (x, y) tile and DT consecutive depths of one sample; one
+// thread = NR (x, y) columns of DT output voxels x COUT channels, held in registers.  Per input
 // channel the workgroup stages the (DT + 2) x 10 x 34 halo block in LDS (zero-filled outside the
 // volume) plus that channel's COUT x 27 weights, then every thread reads the 9 taps of each staged
 // plane once (54 VGPRs) and applies them to the output depths they reach (plane p feeds depth
@@ -18,19 +18,22 @@
 namespace mvs {
 namespace {
 
-constexpr int kTX = 32, kTY = 8, kDT = 4;
-constexpr int kPX = kTX + 2, kPY = kTY + 2, kPD = kDT + 2;
-constexpr int kPlane = kPX * kPY;          // 340
-constexpr int kStage = kPD * kPlane;       // 3400 floats per input channel
-constexpr int kPer = (kStage + kBlock - 1) / kBlock;   // 8 staging elements per thread
+constexpr int kTX = 32, kDT = 4;
 constexpr int kWPad = 12;                  // one (co, kd) row of 9 weights, padded to 3 float4
 
-template <int COUT>
-__global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(const float* __restrict__ in,
-                                                                  const float* __restrict__ wt,
-                                                                  float* __restrict__ out, int Cin,
-                                                                  int D, int H, int W, int tiles_x,
-                                                                  int tiles_y, int dgroups) {
+// NR output rows per thread: the workgroup tile is 32 x (8 NR); a thread reads (NR + 2) x 3 taps
+// per staged plane and applies each (co, kd) weight row to NR x DT outputs, so the broadcast weight
+// reads (the LDS-bound part at NR = 1) are amortised over NR times the fmas.
+template <int COUT, int NR>
+__global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
+    const float* __restrict__ in, const float* __restrict__ wt, float* __restrict__ out, int Cin,
+    int D, int H, int W, int tiles_x, int tiles_y, int dgroups, const float* __restrict__ bn_scale,
+    const float* __restrict__ bn_shift, const float* __restrict__ bn_mean) {
+  constexpr int kTY = 8 * NR;
+  constexpr int kPX = kTX + 2, kPY = kTY + 2, kPD = kDT + 2;
+  constexpr int kPlane = kPX * kPY;
+  constexpr int kStage = kPD * kPlane;                      // floats per input channel
+  constexpr int kPer = (kStage + kBlock - 1) / kBlock;      // staging elements per thread
   __shared__ float lds[kStage];
   __shared__ __attribute__((aligned(16))) float wl[COUT * 3 * kWPad];   // W[co][c][kd][.] of channel c
   int t = blockIdx.x;
@@ -64,12 +67,14 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(const float* _
   };
   fetch(0);
 
-  const int lx = (int)threadIdx.x % kTX, ly = (int)threadIdx.x / kTX;
-  float acc[kDT][COUT];
+  const int lx = (int)threadIdx.x % kTX, ly = ((int)threadIdx.x / kTX) * NR;
+  float acc[kDT][NR][COUT];
 #pragma unroll
   for (int d = 0; d < kDT; ++d)
 #pragma unroll
-    for (int co = 0; co < COUT; ++co) acc[d][co] = 0.0f;
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) acc[d][r][co] = 0.0f;
 
   for (int c = 0; c < Cin; ++c) {
     __syncthreads();   // previous channel's reads are done
@@ -85,14 +90,14 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(const float* _
     }
     __syncthreads();
     if (c + 1 < Cin) fetch(c + 1);   // in flight during this channel's arithmetic
-    // the 9 taps of every staged plane, read once
-    float tap[kPD][9];
+    // the (NR + 2) x 3 taps of every staged plane, read once
+    float tap[kPD][NR + 2][3];
 #pragma unroll
     for (int p = 0; p < kPD; ++p)
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
+      for (int ry = 0; ry < NR + 2; ++ry)
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) tap[p][ky * 3 + kx] = lds[p * kPlane + (ly + ky) * kPX + lx + kx];
+        for (int kx = 0; kx < 3; ++kx) tap[p][ry][kx] = lds[p * kPlane + (ly + ry) * kPX + lx + kx];
 #pragma unroll
     for (int kd = 0; kd < 3; ++kd)
 #pragma unroll
@@ -104,33 +109,57 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(const float* _
 #pragma unroll
         for (int d = 0; d < kDT; ++d)   // output depth d reads plane d + kd through kernel depth kd
 #pragma unroll
-          for (int k = 0; k < 9; ++k) acc[d][co] = fmaf(tap[d + kd][k], w[k], acc[d][co]);
+          for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+              for (int kx = 0; kx < 3; ++kx)
+                acc[d][r][co] = fmaf(tap[d + kd][r + ky][kx], w[ky * 3 + kx], acc[d][r][co]);
       }
   }
 
-  const int gx = tx0 + lx, gy = ty0 + ly;
-  if (gx >= W || gy >= H) return;
-  float* ob = out + (size_t)b * COUT * vol + (size_t)gy * W + gx;
+  const int gx = tx0 + lx;
+  if (gx >= W) return;
 #pragma unroll
-  for (int d = 0; d < kDT; ++d) {
-    if (d0 + d >= D) break;
+  for (int r = 0; r < NR; ++r) {
+    const int gy = ty0 + ly + r;
+    if (gy >= H) break;
+    float* ob = out + (size_t)b * COUT * vol + (size_t)gy * W + gx;
 #pragma unroll
-    for (int co = 0; co < COUT; ++co) ob[(size_t)co * vol + (size_t)(d0 + d) * plane] = acc[d][co];
+    for (int d = 0; d < kDT; ++d) {
+      if (d0 + d >= D) break;
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) {
+        float v = acc[d][r][co];
+        if (bn_scale) v = fmaxf((v - bn_mean[co]) * bn_scale[co] + bn_shift[co], 0.0f);
+        ob[(size_t)co * vol + (size_t)(d0 + d) * plane] = v;
+      }
+    }
   }
+}
+
+template <int COUT, int NR>
+void launch_narrow(const float* in, const float* weight, float* out, int B, int Cin, int D, int H, int W,
+                   const float* bn_scale, const float* bn_shift, const float* bn_mean, hipStream_t s) {
+  const int tiles_x = (W + kTX - 1) / kTX, tiles_y = (H + 8 * NR - 1) / (8 * NR), dgroups = (D + kDT - 1) / kDT;
+  const dim3 grid((unsigned)((size_t)B * dgroups * tiles_y * tiles_x));
+  hipLaunchKernelGGL((conv3d_k3_narrow_kernel<COUT, NR>), grid, dim3(kBlock), 0, s, in, weight, out, Cin, D,
+                     H, W, tiles_x, tiles_y, dgroups, bn_scale, bn_shift, bn_mean);
 }
 
 }  // namespace
 
+#ifndef MVS_EXP_CONV_NR
+#define MVS_EXP_CONV_NR 1   /* 2 rows per thread: 256 VGPRs, 1 wave per SIMD, 4.17 vs 3.95 ms at cfg 2 */
+#endif
+
 void launch_conv3d_k3_narrow(const float* in, const float* weight, float* out, int B, int Cin,
-                             int Cout, int D, int H, int W, hipStream_t s) {
-  const int tiles_x = (W + kTX - 1) / kTX, tiles_y = (H + kTY - 1) / kTY, dgroups = (D + kDT - 1) / kDT;
-  const dim3 grid((unsigned)((size_t)B * dgroups * tiles_y * tiles_x));
+                             int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
+                             const float* bn_mean, hipStream_t s) {
   if (Cout == 8)
-    hipLaunchKernelGGL(conv3d_k3_narrow_kernel<8>, grid, dim3(kBlock), 0, s, in, weight, out, Cin, D, H,
-                       W, tiles_x, tiles_y, dgroups);
+    launch_narrow<8, MVS_EXP_CONV_NR>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
   else
-    hipLaunchKernelGGL(conv3d_k3_narrow_kernel<1>, grid, dim3(kBlock), 0, s, in, weight, out, Cin, D, H,
-                       W, tiles_x, tiles_y, dgroups);
+    launch_narrow<1, 1>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
 }
 
 }  // namespace mvs

@@ -40,8 +40,10 @@ void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, u
                         int n_est, float* depth, hipStream_t s);
 
 // conv3d_narrow.hip: 3x3x3 stride-1 padding-1 bias-free Conv3d, NCDHW fp32, Cout in {1, 8}
+// (optional epilogue: max((v - bn_mean) * bn_scale + bn_shift, 0), all three or none)
 void launch_conv3d_k3_narrow(const float* in, const float* weight, float* out, int B, int Cin,
-                             int Cout, int D, int H, int W, hipStream_t s);
+                             int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
+                             const float* bn_mean, hipStream_t s);
 
 // deconv3d_region.hip: stride-2 kernel-3 ConvTranspose3d (Cout 8) from a region tensor to the full
 // volume, optional fused BN(eval)+ReLU and residual add

@@ -51,7 +51,8 @@ SIGNATURES = {
                                            _p]),
     "mvs_normalize_images": (_c_int, [_p, _c_int, _c_int, _c_int, _p, _p, _p, _p]),
     "mvs_depth_threshold": (_c_int, [_p, ctypes.c_size_t, _c_float, _c_float, _p, _p]),
-    "mvs_conv3d_k3_fwd": (_c_int, [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _p]),
+    "mvs_conv3d_k3_fwd": (_c_int, [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _p, _p, _p,
+                                   _p]),
     "mvs_deconv3d_k3s2_fwd": (_c_int, [_p] + [_c_int] * 9 + [_p] + [_c_int] * 6 + [_p] * 6),
 }
 

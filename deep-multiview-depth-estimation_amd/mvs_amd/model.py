@@ -121,7 +121,13 @@ class CostVolumeReg(nn.Module):
         B = _tconv_input_region(full, n, self.pad)
         C2 = _tconv_input_region(B, n, self.pad)
         C3 = _tconv_input_region(C2, n, self.pad)
-        y0 = act(self.BN_0, _narrow_conv(self.conv_0_0, cv))
+        if _hip_inference(cv):   # conv_0_0 -> BN_0 -> ReLU in one HIP kernel
+            from .ops import conv3d_k3
+            bn = self.BN_0
+            y0 = conv3d_k3(cv, self.conv_0_0.weight, bn.weight / torch.sqrt(bn.running_var + bn.eps),
+                           bn.bias, bn.running_mean)
+        else:
+            y0 = act(self.BN_0, self.conv_0_0(cv))
         # level 1 on B, level 2 on C2, level 3 on C3 (regions carry their origin in the volume)
         lv = []
         for conv_a, conv_b, bn, reg in ((self.conv_1_0, self.conv_1_1, self.BN_1, B),

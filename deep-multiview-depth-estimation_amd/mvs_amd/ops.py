@@ -11,6 +11,8 @@ Every op requires CUDA(HIP) tensors and raises otherwise: there is no CPU path i
 Camera tensors (K, R, T, d_min, d_int) are moved to the feature device here, as the reference
 does with ``.to(DEVICE)`` (homography.py:25,43-58).
 """
+from typing import Optional
+
 import torch
 
 from . import _lib
@@ -294,10 +296,12 @@ torch.library.register_autograd("mvs::extract_depth_map", _sam_backward, setup_c
 # mvs::conv3d_k3 -- CostVolumeReg.conv_0_0 (32 -> 8) / conv_out (8 -> 1), model.py:77,96
 # ----------------------------------------------------------------------------------------------
 @torch.library.custom_op("mvs::conv3d_k3", mutates_args=())
-def conv3d_k3(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Tensor] = None,
+              bn_shift: Optional[torch.Tensor] = None, bn_mean: Optional[torch.Tensor] = None) -> torch.Tensor:
     """nn.Conv3d(c_in, c_out, 3, stride=1, padding=1, bias=False) forward, c_out in {1, 8}, fp32
-    NCDHW, on the HIP kernel (csrc/conv3d_narrow.hip).  Inference only (no autograd formula):
-    CostVolumeReg uses it on the eval-mode, no-grad path."""
+    NCDHW, on the HIP kernel (csrc/conv3d_narrow.hip); with bn_* given, max((y - mean) * scale +
+    shift, 0) is fused (eval BN + ReLU).  Inference only (no autograd formula): CostVolumeReg
+    uses it on the eval-mode, no-grad path."""
     _require_gpu(x, "x")
     lib = _lib.load()
     if x.dim() != 5 or weight.dim() != 5 or tuple(weight.shape[2:]) != (3, 3, 3) or weight.shape[1] != x.shape[1]:
@@ -307,17 +311,20 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     w = weight.to(device=x.device, dtype=_F32).contiguous()
     b, cin, d, h, wd = x.shape
     cout = w.shape[0]
+    bn = [t if t is None else t.to(device=x.device, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
+    if any(t is None for t in bn) and not all(t is None for t in bn):
+        raise ValueError("bn_scale, bn_shift and bn_mean go together")
+    bp = [None if t is None else _lib.ptr(t) for t in bn]
     y = torch.empty((b, cout, d, h, wd), device=x.device, dtype=_F32)
-    st = lib.mvs_conv3d_k3_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), b, cin, cout, d, h, wd,
+    st = lib.mvs_conv3d_k3_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), b, cin, cout, d, h, wd, *bp,
                                _lib.stream_handle(x.device))
     _lib.check(st, "mvs_conv3d_k3_fwd")
     return y
 
 
 @conv3d_k3.register_fake
-def _(x, weight):
+def _(x, weight, bn_scale=None, bn_shift=None, bn_mean=None):
     return x.new_empty((x.shape[0], weight.shape[0]) + tuple(x.shape[2:]))
-
 
 
 # ----------------------------------------------------------------------------------------------

@@ -168,11 +168,14 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
 /* Regulariser layers conv_0_0 (32 -> 8) and conv_out (8 -> 1) of CostVolumeReg (model.py:77,96 /
  * forward at model.py:101,123): nn.Conv3d(c_in, c_out, 3, stride=1, padding=1, bias=False) over
  * x[batch][c_in][d][h][w] fp32 with weight[c_out][c_in][3][3][3], into y[batch][c_out][d][h][w].
- * c_out must be 1 or 8 (MVS_ERR_INVALID_ARGUMENT otherwise); d*h*w < 2^31.  Replaces the MIOpen
- * convolution behind torch.nn.Conv3d.forward for these two layers in eval-mode inference; same
- * products per output as the reference layer, fp32 summation order differs. */
+ * c_out must be 1 or 8 (MVS_ERR_INVALID_ARGUMENT otherwise); d*h*w < 2^31.  Optional epilogue
+ * (all three BN pointers, c_out floats each, or none): y = max((y - bn_mean) * bn_scale + bn_shift,
+ * 0), the eval BN + ReLU that follows conv_0_0 (model.py:101; bn_scale = gamma / sqrt(var + eps),
+ * bn_shift = beta).  Replaces the MIOpen convolution behind torch.nn.Conv3d.forward for these two
+ * layers in eval-mode inference; same products per output, fp32 summation order differs. */
 int mvs_conv3d_k3_fwd(const float* x, const float* weight, float* y, int batch, int c_in, int c_out,
-                      int d, int h, int w, void* stream);
+                      int d, int h, int w, const float* bn_scale, const float* bn_shift,
+                      const float* bn_mean, void* stream);
 
 /* Regulariser layer deconv_1_0 (model.py:87, forward at model.py:121): nn.ConvTranspose3d(c_in, 8,
  * 3, stride=2, padding=(pd, ph, pw), output_padding, bias=False) into the full volume
