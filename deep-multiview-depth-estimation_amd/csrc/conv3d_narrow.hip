@@ -24,8 +24,13 @@ constexpr int kWPad = 12;                  // one (co, kd) row of 9 weights, pad
 // NR output rows per thread: the workgroup tile is 32 x (8 NR); a thread reads (NR + 2) x 3 taps
 // per staged plane and applies each (co, kd) weight row to NR x DT outputs, so the broadcast weight
 // reads (the LDS-bound part at NR = 1) are amortised over NR times the fmas.
+#ifdef MVS_EXP_CONV_WPE
+#define MVS_CONV_ATTR __attribute__((amdgpu_waves_per_eu(MVS_EXP_CONV_WPE)))
+#else
+#define MVS_CONV_ATTR
+#endif
 template <int COUT, int NR>
-__global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
+__global__ __launch_bounds__(kBlock) MVS_CONV_ATTR void conv3d_k3_narrow_kernel(
     const float* __restrict__ in, const float* __restrict__ wt, float* __restrict__ out, int Cin,
     int D, int H, int W, int tiles_x, int tiles_y, int dgroups, const float* __restrict__ bn_scale,
     const float* __restrict__ bn_shift, const float* __restrict__ bn_mean) {

@@ -59,6 +59,99 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
   }
 }
 
+// Grouped form (V = 2..8, the default): one thread per pixel of one (sample, group of PG planes).
+// The reference view's sampling is plane independent (C_i = C_r gives P = I exactly; the forward
+// resamples it once per launch), so its gradient coefficients are summed over the group's planes
+// in registers and scattered once per group: PG times fewer reference-view atomics, and PG times
+// less same-address contention (all planes of a pixel hit the same 4 reference taps).  Channels
+// run in chunks of CC so the per-channel reference values and sums stay in registers.
+constexpr int kBwdPG = 8, kBwdCC = 8;
+
+template <int V>
+__global__ __launch_bounds__(kBlock) void cost_volume_bwd_grouped_kernel(
+    const float* __restrict__ feat, const float* __restrict__ sampling,
+    const float* __restrict__ grad_cv, float* __restrict__ grad_feat, int C, int h, int w, int Dc,
+    int tiles, int groups, int total) {
+  const int wk = xcd_work_id(blockIdx.x, total);
+  if (wk >= total) return;
+  const int grp = wk % groups;
+  const int t = wk / groups;
+  const int tile = t % tiles;
+  const int b = t / tiles;
+  const uint32_t hw = (uint32_t)h * (uint32_t)w;
+  const uint32_t p = (uint32_t)tile * kBlock + threadIdx.x;
+  if (p >= hw) return;
+  const int k0 = grp * kBwdPG;
+  const int npl = min(kBwdPG, Dc - k0);
+  float xn, yn;
+  pixel_coords(p, w, h, xn, yn);
+  Taps tref;
+  make_taps(sampling + ((size_t)(b * V) * Dc + k0) * 9, xn, yn, h, w, tref);
+  const float* fb = feat + (size_t)b * V * C * hw;
+  float* gb = grad_feat + (size_t)b * V * C * hw;
+  const float* gcv = grad_cv + (size_t)b * C * Dc * hw + p;
+  const float inv_v = 1.0f / (float)V;
+  for (int c0 = 0; c0 < C; c0 += kBwdCC) {
+    float rval[kBwdCC], racc[kBwdCC];
+#pragma unroll
+    for (int cc = 0; cc < kBwdCC; ++cc) {
+      racc[cc] = 0.0f;
+      rval[cc] = c0 + cc < C ? gather(fb + (size_t)(c0 + cc) * hw, tref) : 0.0f;
+    }
+    for (int kk = 0; kk < npl; ++kk) {
+      const int k = k0 + kk;
+      Taps tp[V - 1];
+#pragma unroll
+      for (int v = 1; v < V; ++v)
+        make_taps(sampling + ((size_t)(b * V + v) * Dc + k) * 9, xn, yn, h, w, tp[v - 1]);
+#pragma unroll
+      for (int cc = 0; cc < kBwdCC; ++cc) {
+        const int c = c0 + cc;
+        if (c >= C) break;
+        const float g = gcv[((size_t)c * Dc + k) * hw];
+        float val[V];
+        val[0] = rval[cc];
+        float sum = val[0];
+#pragma unroll
+        for (int v = 1; v < V; ++v) {
+          val[v] = gather(fb + ((size_t)v * C + c) * hw, tp[v - 1]);
+          sum += val[v];
+        }
+        const float mean = sum * inv_v;
+        const float k2 = 2.0f * inv_v * g;
+        racc[cc] += k2 * (val[0] - mean);
+#pragma unroll
+        for (int v = 1; v < V; ++v) {
+          const float coef = k2 * (val[v] - mean);
+          char* plane = reinterpret_cast<char*>(gb + ((size_t)v * C + c) * hw);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (tp[v - 1].wt[q] != 0.0f)
+              unsafeAtomicAdd(reinterpret_cast<float*>(plane + tp[v - 1].off[q]), tp[v - 1].wt[q] * coef);
+        }
+      }
+    }
+#pragma unroll
+    for (int cc = 0; cc < kBwdCC; ++cc) {
+      if (c0 + cc >= C) break;
+      char* plane = reinterpret_cast<char*>(gb + (size_t)(c0 + cc) * hw);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (tref.wt[q] != 0.0f)
+          unsafeAtomicAdd(reinterpret_cast<float*>(plane + tref.off[q]), tref.wt[q] * racc[cc]);
+    }
+  }
+}
+
+template <int V>
+void launch_bwd_grouped(const Geometry& g, const float* feat, const float* smp, const float* gcv,
+                        float* gf, hipStream_t s) {
+  const int groups = (g.Dc + kBwdPG - 1) / kBwdPG;
+  const int total = g.B * g.tiles * groups;
+  hipLaunchKernelGGL((cost_volume_bwd_grouped_kernel<V>), xcd_grid(total), dim3(kBlock), 0, s, feat, smp,
+                     gcv, gf, g.C, g.h, g.w, g.Dc, g.tiles, groups, total);
+}
+
 template <int MAXV, bool EXACT>
 void launch_bwd(const Geometry& g, const float* feat, const float* smp, const float* gcv,
                 float* gf, hipStream_t s) {
@@ -72,9 +165,19 @@ void launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* s
                             const float* grad_cv, float* grad_feat, hipStream_t s) {
   switch (g.V) {
     case 1: launch_bwd<1, true>(g, feat, sampling, grad_cv, grad_feat, s); break;
+#ifdef MVS_EXP_BWD_FLAT
     case 2: launch_bwd<2, true>(g, feat, sampling, grad_cv, grad_feat, s); break;
     case 3: launch_bwd<3, true>(g, feat, sampling, grad_cv, grad_feat, s); break;
     case 5: launch_bwd<5, true>(g, feat, sampling, grad_cv, grad_feat, s); break;
+#else
+    case 2: launch_bwd_grouped<2>(g, feat, sampling, grad_cv, grad_feat, s); break;
+    case 3: launch_bwd_grouped<3>(g, feat, sampling, grad_cv, grad_feat, s); break;
+    case 4: launch_bwd_grouped<4>(g, feat, sampling, grad_cv, grad_feat, s); break;
+    case 5: launch_bwd_grouped<5>(g, feat, sampling, grad_cv, grad_feat, s); break;
+    case 6: launch_bwd_grouped<6>(g, feat, sampling, grad_cv, grad_feat, s); break;
+    case 7: launch_bwd_grouped<7>(g, feat, sampling, grad_cv, grad_feat, s); break;
+    case 8: launch_bwd_grouped<8>(g, feat, sampling, grad_cv, grad_feat, s); break;
+#endif
     default: launch_bwd<MVS_MAX_VIEWS, false>(g, feat, sampling, grad_cv, grad_feat, s); break;
   }
 }
