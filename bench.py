@@ -189,6 +189,35 @@ def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=F
     return main_ms, op_ms, alg_bytes
 
 
+def time_backward(B, V, C, h, w, D, device, iters=5):
+    """Fused cost-volume op forward and backward (mvs::cost_volume_backward) through autograd,
+    HIP events on the current stream; ms per call."""
+    from mvs_amd import warp_and_assemble_cost_volume
+    K, R, T = camera_batch(B, V, h, w)
+    d_min, d_int = depth_range(B)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    feat = torch.randn(B * V, C, h, w, generator=g).to(device).requires_grad_(True)
+    gcv = torch.randn(B, C, D, h, w, generator=g).to(device)
+    fwd = lambda: warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feat, B, V, d_num=D)[0]
+    fwd().backward(gcv)
+    torch.cuda.synchronize()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    tf = tb = 0.0
+    for _ in range(iters):
+        feat.grad = None
+        e[0].record()
+        cv = fwd()
+        e[1].record()
+        cv.backward(gcv)
+        e[2].record()
+        torch.cuda.synchronize()
+        tf += e[0].elapsed_time(e[1])
+        tb += e[1].elapsed_time(e[2])
+    del cv, gcv, feat
+    return {"fwd_ms": tf / iters, "bwd_ms": tb / iters,
+            "kernel": "cost_volume_bwd_lds_kernel (LDS footprint accumulation + float atomics)"}
+
+
 def load_traffic(tag):
     p = os.path.join(REPO, "profiles", "traffic_%s.json" % tag)
     if os.path.exists(p):
@@ -332,6 +361,8 @@ def main():
             "same step with CostVolumeReg.forward_full (every voxel of every level, as "
             "model.py:100-126 computes it); value uses forward_live (eval BN: only the regions "
             "whose values reach the output; same sums, fp32 summation order may differ)"))
+    # backward of the fused op (train.py:103): informational, through autograd
+    out["cost_volume_backward"] = time_backward(B, V, C, h, w, d_count, device)
     # opt-in bf16 cost volume: informational, not the headline (reduced precision)
     _, bf_op_ms, bf_alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count, bf16=True)
     out["bf16_cv_opt_in"] = {"op_ms": bf_op_ms, "alg_bytes_per_launch": bf_alg,
