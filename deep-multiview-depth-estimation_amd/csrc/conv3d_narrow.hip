@@ -10,8 +10,7 @@
 // channel the workgroup stages the (DT + 2) x 10 x 34 halo block in LDS (zero-filled outside the
 // volume) plus that channel's COUT x 27 weights, then every thread reads the 9 taps of each staged
 // plane once (54 VGPRs) and applies them to the output depths they reach (plane p feeds depth
-// p - kd).  Weights are read as broadcast float4 LDS loads (scalar loads of a channel's 216
-// weights spilled 630 SGPRs).  The staging of channel c + 1 is loaded into registers before
+// p - kd).  Weights are workgroup-uniform scalar loads, 9 at a time (SGPR operands of the fmas).  The staging of channel c + 1 is loaded into registers before
 // channel c is computed.  Compute-bound: COUT * 27 fmas per staged input element.
 #include "launchers.h"
 
@@ -88,11 +87,13 @@ __global__ __launch_bounds__(kBlock) MVS_CONV_ATTR void conv3d_k3_narrow_kernel(
       const int e = (int)threadIdx.x + j * kBlock;
       if (e < kStage) lds[e] = pre[j];
     }
+#ifdef MVS_EXP_CONV_LDSW
     for (int i = (int)threadIdx.x; i < COUT * 3 * kWPad; i += kBlock) {   // weights, rows padded to 12
       const int co = i / (3 * kWPad), r = i % (3 * kWPad);
       const int kd = r / kWPad, k = r % kWPad;
       wl[i] = k < 9 ? wt[((size_t)co * Cin + c) * 27 + kd * 9 + k] : 0.0f;
     }
+#endif
     __syncthreads();
     if (c + 1 < Cin) fetch(c + 1);   // in flight during this channel's arithmetic
     // the (NR + 2) x 3 taps of every staged plane, read once
@@ -107,10 +108,21 @@ __global__ __launch_bounds__(kBlock) MVS_CONV_ATTR void conv3d_k3_narrow_kernel(
     for (int kd = 0; kd < 3; ++kd)
 #pragma unroll
       for (int co = 0; co < COUT; ++co) {
+#ifndef MVS_EXP_CONV_LDSW
+        // weights as scalar loads (SGPR operands of the fmas), at most 9 live at a time: the
+        // memory clobber keeps the compiler from hoisting all 216 of a channel (630 SGPR spills);
+        // 3.53 ms at cfg 2 against 3.92 ms with broadcast LDS reads (-DMVS_EXP_CONV_LDSW)
+        asm volatile("" ::: "memory");
+        const float* wg = wt + ((size_t)co * Cin + c) * 27 + kd * 9;
+        float w[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) w[k] = wg[k];
+#else
         // workgroup-uniform weights: broadcast LDS reads (one address for all lanes)
         const float4* wr = reinterpret_cast<const float4*>(wl + (co * 3 + kd) * kWPad);
         const float4 w0 = wr[0], w1 = wr[1], w2 = wr[2];
         const float w[9] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x};
+#endif
 #pragma unroll
         for (int d = 0; d < kDT; ++d)   // output depth d reads plane d + kd through kernel depth kd
 #pragma unroll
