@@ -215,7 +215,7 @@ def time_backward(B, V, C, h, w, D, device, iters=5):
         tb += e[1].elapsed_time(e[2])
     del cv, gcv, feat
     return {"fwd_ms": tf / iters, "bwd_ms": tb / iters,
-            "kernel": "cost_volume_bwd_lds_kernel (LDS footprint accumulation + float atomics)"}
+            "kernel": "cost_volume_bwd_kernel (recompute + 64-bit fixed-point LDS footprint accumulation, deterministic)"}
 
 
 def load_traffic(tag):
@@ -226,28 +226,87 @@ def load_traffic(tag):
     return None
 
 
+def host_cpus():
+    """CPUs this process may use: its affinity set, capped by a cgroup-v2 CPU quota (a GPU box
+    shows the whole machine in os.cpu_count() but grants one GPU's share), plus lscpu facts."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    info = {"os_cpu_count": os.cpu_count(), "affinity": n, "cgroup_quota": quota}
+    try:
+        import subprocess
+        txt = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in txt.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core"):
+                info[k.strip()] = v.strip()
+    except (OSError, ValueError):
+        pass
+    return min(n, quota) if quota else n, info
+
+
+def _median(fn, reps=3, warmup=True):
+    import statistics
+    if warmup:
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts)
+
+
 def cpu_baseline(V, H, W, D):
-    """Oracle (reference op sequence, torch CPU) on ONE sample of the workload."""
+    """The oracle (oracle/mvs_oracle.py: the reference's op sequence in torch CPU, per-plane warp
+    loop with torch.cat growth; within 6 % of the imported reference at config 1 in the survey
+    container, profiles/cpu_calibration_r02.json) on the host cores available to this job,
+    BASELINE.md's CPU-baseline plan on bounded samples:
+      value  cfg 2 (D=192, 640x512, V=3) full MVSNet.forward of ONE sample, median of 3 (the
+             config-1 runs before it warm every op up);
+      legs   config 1 (D=48) full forward, one warm-up + median of 3; cfg 2 warp + variance only
+             (homography_warping + assemble_cost_volume), one sample, median of 3.
+    cfg 5 is skipped (the reference's O(D^2) torch.cat makes it ~1.5 TB of copies per sample)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import mvs_oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads, info = host_cpus()
     torch.set_num_threads(threads)
     from mvs_amd.config import MVSConfig
     from mvs_amd.model import MVSNet
-    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W), device=torch.device("cpu"))
-    net.load_state_dict(deterministic_state_dict(net.state_dict()))
-    net.eval()
-    img, K, R, T, d_min, d_int = make_inputs(1, V, H, W, 0, torch.device("cpu"))
+    out = {}
     with torch.no_grad():
-        t0 = time.perf_counter()
-        mvs_oracle.mvsnet_forward(net, img, K, R, T, d_min, d_int, 1, V, D, (H // 4, W // 4),
-                                  concat_growth=True)
-        dt = time.perf_counter() - t0
+        for tag, d in (("cfg1", 48), ("cfg2", D)):
+            net = MVSNet(MVSConfig(d_num=d, in_h=H, in_w=W), device=torch.device("cpu"))
+            net.load_state_dict(deterministic_state_dict(net.state_dict()))
+            net.eval()
+            img, K, R, T, d_min, d_int = make_inputs(1, V, H, W, 0, torch.device("cpu"))
+            log("cpu baseline: %s full forward (D=%d, %d threads)" % (tag, d, threads))
+            out[tag + "_forward_s"] = _median(lambda: mvs_oracle.mvsnet_forward(
+                net, img, K, R, T, d_min, d_int, 1, V, d, (H // 4, W // 4), concat_growth=True),
+                warmup=(tag == "cfg1"))
+            if tag == "cfg2":
+                feats = net.feature_encoder(img)
+                log("cpu baseline: cfg2 warp + variance")
+                out["cfg2_warp_variance_s"] = _median(lambda: mvs_oracle.assemble_cost_volume(
+                    mvs_oracle.homography_warping(K, R, T, d_min, d_int, feats, 1, V, d,
+                                                  concat_growth=True)[0], V), warmup=False)
+    dt = out["cfg2_forward_s"]
     return {"value": 1.0 / dt, "unit": "depth maps/s", "cores": threads, "kind": "port",
-            "sample": "1 sample (B=1, V=%d, %dx%d, D=%d) of the workload, full MVSNet.forward on "
-                      "the oracle (reference op sequence incl. per-plane warp loop with torch.cat "
-                      "growth), torch %s CPU, %d threads, %.1f s" % (V, W, H, D, torch.__version__,
-                                                                    threads, dt)}
+            "sample": "1 sample (B=1, V=%d, %dx%d, D=%d) of the workload, full MVSNet.forward on the "
+                      "oracle (reference op sequence incl. per-plane warp loop with torch.cat growth), "
+                      "median of 3, torch %s CPU, %d threads: %.1f s" % (V, W, H, D, torch.__version__,
+                                                                        threads, dt),
+            "legs": {"cfg1_forward_s": out["cfg1_forward_s"],
+                     "cfg1_depth_maps_per_s": 1.0 / out["cfg1_forward_s"],
+                     "cfg2_forward_s": dt,
+                     "cfg2_warp_variance_s": out["cfg2_warp_variance_s"],
+                     "cfg2_warp_variance_cost_volumes_per_s": 1.0 / out["cfg2_warp_variance_s"]},
+            "host": info, "calibration": "profiles/cpu_calibration_r02.json"}
 
 
 def main():

@@ -15,6 +15,11 @@ int check_geometry(int B, int V, int C, int h, int w, int d_count, Geometry& g) 
   const uint64_t hw = (uint64_t)h * (uint64_t)w;
   // per-image plane offsets are 32-bit; work ids are 32-bit ints; packed corners are 16-bit
   if ((uint64_t)C * hw >= (1ull << 31) || h > 32000 || w > 32000) return MVS_ERR_TOO_LARGE;
+  // the packed kernels build 32-bit buffer descriptors and offsets: a sample's padded channel-quad
+  // images (V * ceil(C/4) * (h+2) * (w+2) float4, byte offsets held in ints) and a plane group's
+  // cost-volume run (8 planes * hw * 4 B)
+  const uint64_t padded = (uint64_t)V * (uint64_t)((C + 3) / 4) * (uint64_t)(h + 2) * (uint64_t)(w + 2) * 16u;
+  if ((V >= 2 && V <= 8 && padded >= (1ull << 31)) || 8ull * hw * 4ull >= (1ull << 32)) return MVS_ERR_TOO_LARGE;
   const uint64_t tiles = (hw + mvs::kBlock - 1) / mvs::kBlock;
   const uint64_t total = (uint64_t)B * tiles * (uint64_t)d_count;
   if (total >= (1ull << 31) - 8) return MVS_ERR_TOO_LARGE;
@@ -158,19 +163,22 @@ int mvs_assemble_cost_volume_fwd(const float* warped, int batch_size, int n_view
   return mvs::hip_status();
 }
 
-int mvs_cost_volume_bwd(const float* feat, const float* sampling, const float* grad_cv,
+size_t mvs_cost_volume_bwd_workspace_bytes(int batch_size, int n_views, int channels, int h, int w,
+                                           int d_count) {
+  if (batch_size <= 0 || n_views <= 0 || channels <= 0 || h <= 0 || w <= 0 || d_count <= 0) return 0;
+  return mvs::cost_volume_bwd_workspace_bytes(batch_size, n_views, channels, h, w, d_count);
+}
+
+int mvs_cost_volume_bwd(const float* feat, const float* workspace, const float* grad_cv,
                         int batch_size, int n_views, int channels, int h, int w, int d_count,
-                        float* grad_feat, void* stream) {
-  if (!feat || !sampling || !grad_cv || !grad_feat) return MVS_ERR_INVALID_ARGUMENT;
+                        void* bwd_workspace, float* grad_feat, void* stream) {
+  if (!feat || !workspace || !grad_cv || !grad_feat || (n_views > 1 && !bwd_workspace))
+    return MVS_ERR_INVALID_ARGUMENT;
   Geometry g;
   const int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g);
   if (st != MVS_OK) return st;
-  hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(grad_feat, 0, (size_t)batch_size * n_views * channels * h * w * sizeof(float),
-                     s) != hipSuccess)
-    return MVS_ERR_HIP;
-  mvs::launch_cost_volume_bwd(g, feat, sampling, grad_cv, grad_feat, s);
-  return mvs::hip_status();
+  return mvs::launch_cost_volume_bwd(g, feat, workspace, grad_cv, bwd_workspace, grad_feat,
+                                     (hipStream_t)stream);
 }
 
 int mvs_extract_depth_map_fwd(const float* prob, const float* d_batch, int batch_size, int d,

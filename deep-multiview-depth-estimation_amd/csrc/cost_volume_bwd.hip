@@ -1,390 +1,495 @@
 // cost_volume_bwd.hip -- gradient of the fused warp + variance w.r.t. the features.
 //
-// Autograd of costvolume.py:14 (d cv / d x_v = 2 (x_v - mean) / V) composed with the
-// grid_sample backward of homography.py:86 (each sample's gradient is scattered to its 4 bilinear
-// taps), as train.py:103 exercises it.  One thread per output pixel of one (sample, plane): the
-// samples are recomputed (no warped volume is stored) and scattered with float atomics into
-// grad_feat[N][C][h][w] -- like torch's grid_sample backward on GPU, the summation order is not
-// deterministic.
+// Autograd of costvolume.py:14 (d cv / d x_v = 2 (x_v - mean) / V) composed with the grid_sample
+// backward of homography.py:86 (each sample's gradient is scattered to its 4 bilinear taps), as
+// train.py:103 exercises it.  No warped volume is stored: the samples are recomputed from the
+// forward's packed features (packed.h), exactly as the forward computed them.
+//
+// Accumulation is in 64-bit FIXED POINT: every contribution v is added as llrint(v * 2^S), with
+// one shift S per launch derived on the device from max|grad_cv| and max|feat| so that no gradient
+// element can exceed 2^62 (bound: d_count * h * w contributions of at most 4 max|g| max|feat| / V
+// each).  Integer addition is associative, so the result is bit-identical whatever the order in
+// which workgroups and lanes add -- the backward is deterministic -- and integer LDS atomics run
+// at ~25x the rate of fp32 ones on gfx950 (tools/microbench/atomic_patterns.hip: ds_add_u64 5.1 T
+// lanes/s, ds_add_f32 0.20 T).  Resolution: 2^-S = d_count*h*w*4*max|g|*max|feat|/V * 2^-61, i.e.
+// about 1e-12 of the largest possible contribution at BASELINE cfg 2.
+//
+// Kernels (V = 2..8 views):
+//   abs_max_kernel        max|grad_cv|, max|feat| (device scalars, order-independent atomicMax)
+//   cost_volume_bwd_kernel  a 256-thread workgroup owns a 32 x 8 pixel tile of one sample, a
+//                         group of 32 planes and one 4-channel chunk.  Per plane, every thread
+//                         recomputes its pixel's samples of all views (packed float4 gathers),
+//                         forms the per-view coefficients 2/V g (x_v - mean), keeps the reference
+//                         view's sum over planes in registers (its taps do not depend on the
+//                         plane), and adds each source view's 4 tap contributions into an LDS
+//                         image of the tile's footprint (ds_add_u64).  Footprints come from the
+//                         tile's 4 corners per (plane, view) (a homography maps the tile to a
+//                         convex quad); consecutive planes share one LDS image while the union
+//                         fits the budget, which is then flushed with one 64-bit global atomic
+//                         per slot and channel.  Taps outside the image box (rounding) or a plane
+//                         whose footprint alone exceeds the budget go straight to global atomics.
+//   ref_scatter_kernel    sums the reference view's per-group partials in a fixed order and
+//                         scatters them to its (plane-independent) taps
+//   fixed_to_float_kernel grad_feat = acc * 2^-S
+// More than 8 views: one thread per (sample, plane, pixel) with NCHW gathers and global atomics.
 #include "launchers.h"
+#include "packed.h"
 
 namespace mvs {
 namespace {
 
-// backward: g_x_v = 2 (x_v - mean) / V * g_cv, scattered to the 4 taps with bilinear weights
-template <int MAXV, bool EXACT>
+constexpr int kBwdTW = 32, kBwdTH = 8;
+constexpr int kBwdKPG = 32;              // planes per workgroup
+constexpr int kBwdSlots = 1536;          // LDS accumulator slots (x 4 channels x 8 B = 48 KB)
+typedef unsigned long long u64;
+
+// ---- fixed point ------------------------------------------------------------------------------
+struct Fixed {
+  float to_fixed;    // 2^S
+  double to_float;   // 2^-S
+};
+
+__device__ inline Fixed fixed_scale(const unsigned* __restrict__ mx, int V, int Dc, uint32_t hw) {
+  const double gmax = (double)__uint_as_float(mx[0]), fmax = (double)__uint_as_float(mx[1]);
+  // |2/V g (x - mean)| <= 4 gmax fmax / V per contribution; a gradient element collects at most
+  // Dc * hw of them (tap weights of one sample sum to 1); x2 margin for fp32 rounding
+  const double bound = 8.0 * gmax * fmax / (double)V * (double)Dc * (double)hw;
+  int S = 0;
+  if (bound > 0.0 && bound < 1e300) {
+    int e;
+    frexp(bound, &e);   // bound < 2^e
+    S = 61 - e;
+  }
+  S = S < -100 ? -100 : (S > 120 ? 120 : S);
+  Fixed f;
+  f.to_fixed = ldexpf(1.0f, S);
+  f.to_float = ldexp(1.0, -S);
+  return f;
+}
+
+__device__ inline u64 to_fixed(float v, float sc) { return (u64)(long long)__builtin_rintf(v * sc); }
+
+__device__ inline void gadd(u64* p, u64 v) { atomicAdd(p, v); }
+
+// ---- max|x| pre-pass ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void abs_max_kernel(const float* __restrict__ a, size_t n,
+                                                         unsigned* __restrict__ out) {
+  float m = 0.0f;
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  if (((uintptr_t)a & 15u) == 0) {
+    const float4* a4 = reinterpret_cast<const float4*>(a);
+    const size_t n4 = n / 4;
+    for (size_t j = i; j < n4; j += stride) {
+      const float4 v = a4[j];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    i += n4 * 4;
+  }
+  for (; i < n; i += stride) m = fmaxf(m, fabsf(a[i]));
+  // NaN compares false in fmaxf's favour of the other operand; a non-finite maximum is kept as is
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));   // m >= 0: uint order = float order
+}
+
+// ---- per-(plane, view) footprint boxes -----------------------------------------------------------
+// Box of the in-image taps of a tile for one (plane, view), from the tile's 4 corner pixels: with
+// the homogeneous coordinate s of one sign and |s| > 1e-8 at the corners (s is affine in the pixel,
+// so then everywhere in the tile) the tile maps to a convex quad whose bounding box is the corners'
+// bounding box; one slot of margin each side absorbs fp32 rounding.  Otherwise: the whole image.
+struct Box {
+  int x0, y0, x1, y1;   // inclusive, clipped to the image; x1 < x0 = empty
+};
+
+__device__ inline int box_area(const Box& b) {
+  return (b.x1 < b.x0 || b.y1 < b.y0) ? 0 : (b.x1 - b.x0 + 1) * (b.y1 - b.y0 + 1);
+}
+
+__device__ inline Box box_union(const Box& a, const Box& b) {
+  if (a.x1 < a.x0 || a.y1 < a.y0) return b;
+  if (b.x1 < b.x0 || b.y1 < b.y0) return a;
+  return Box{min(a.x0, b.x0), min(a.y0, b.y0), max(a.x1, b.x1), max(a.y1, b.y1)};
+}
+
+__device__ Box tile_box(const float* __restrict__ G, int px0, int py0, int px1, int py1, int h, int w) {
+  float mnx = 1e30f, mny = 1e30f, mxx = -1e30f, mxy = -1e30f;
+  bool pos = false, neg = false, bad = false;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float xn = norm_coord((c & 1) ? px1 : px0, w), yn = norm_coord((c & 2) ? py1 : py0, h);
+    float u = __fmaf_rn(G[1], yn, __fmaf_rn(G[0], xn, G[2]));
+    float v = __fmaf_rn(G[4], yn, __fmaf_rn(G[3], xn, G[5]));
+    const float s = __fmaf_rn(G[7], yn, __fmaf_rn(G[6], xn, G[8]));
+    if (!(fabsf(s) > 1e-8f)) bad = true;
+    pos |= s > 0.0f;
+    neg |= s < 0.0f;
+    const float sc = __fdiv_rn(1.0f, __fadd_rn(s, 1e-8f));
+    u = __fmul_rn(u, sc);
+    v = __fmul_rn(v, sc);
+    const float ix = __fsub_rn(__fmul_rn(__fadd_rn(u, 1.0f), 0.5f * (float)w), 0.5f);
+    const float iy = __fsub_rn(__fmul_rn(__fadd_rn(v, 1.0f), 0.5f * (float)h), 0.5f);
+    if (!(fabsf(ix) < 1e7f && fabsf(iy) < 1e7f)) bad = true;   // also NaN
+    mnx = fminf(mnx, ix);
+    mny = fminf(mny, iy);
+    mxx = fmaxf(mxx, ix);
+    mxy = fmaxf(mxy, iy);
+  }
+  if (bad || (pos && neg)) return Box{0, 0, w - 1, h - 1};
+  Box b;
+  b.x0 = max((int)floorf(mnx) - 1, 0);
+  b.y0 = max((int)floorf(mny) - 1, 0);
+  b.x1 = min((int)floorf(mxx) + 2, w - 1);
+  b.y1 = min((int)floorf(mxy) + 2, h - 1);
+  return b;
+}
+
+// ---- main kernel (2 <= V <= 8) -----------------------------------------------------------------
+template <int V>
 __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
+    const float4* __restrict__ packed, const float4* __restrict__ refs,
+    const float* __restrict__ sampling, const float* __restrict__ grad_cv, u64* __restrict__ acc,
+    float4* __restrict__ ref_part, const unsigned* __restrict__ mx, int B, int C, int h, int w,
+    int Dc, int tiles_x, int tiles_y, int groups, int total) {
+  constexpr int NS = V - 1;
+  __shared__ u64 lds[4 * kBwdSlots];
+  __shared__ Box boxes[kBwdKPG][NS];
+
+  const int wk = xcd_work_id(blockIdx.x, total);
+  if (wk >= total) return;   // workgroup-uniform
+  const int c4 = (C + 3) / 4;
+  const int grp = wk % groups;
+  int t = wk / groups;
+  const int tile = t % (tiles_x * tiles_y);
+  t /= tiles_x * tiles_y;
+  const int ch = t % c4;
+  const int b = t / c4;
+  const int tx0 = (tile % tiles_x) * kBwdTW, ty0 = (tile / tiles_x) * kBwdTH;
+  const int px = tx0 + (int)(threadIdx.x % kBwdTW), py = ty0 + (int)(threadIdx.x / kBwdTW);
+  const bool active = px < w && py < h;
+  const int k0 = grp * kBwdKPG;
+  const int npl = min(kBwdKPG, Dc - k0);
+  const uint32_t hw = (uint32_t)h * (uint32_t)w;
+  const PadGeom pg = pad_geom(h, w);
+  const Fixed fx = fixed_scale(mx, V, Dc, hw);
+
+  // footprint box of every (plane, view): one (plane, view) per thread
+  if ((int)threadIdx.x < npl * NS) {
+    const int pl = (int)threadIdx.x / NS, s = (int)threadIdx.x % NS;
+    boxes[pl][s] = tile_box(sampling + ((size_t)(b * V + 1 + s) * Dc + k0 + pl) * 9, tx0, ty0,
+                            min(tx0 + kBwdTW, w) - 1, min(ty0 + kBwdTH, h) - 1, h, w);
+  }
+
+  const float xn = norm_coord(active ? px : 0, w), yn = norm_coord(active ? py : 0, h);
+  const uint32_t pix = (uint32_t)(active ? py : 0) * (uint32_t)w + (uint32_t)(active ? px : 0);
+  const float4 r4 = refs[((size_t)b * c4 + ch) * hw + pix];
+  const f4v x0 = {r4.x, r4.y, r4.z, r4.w};
+  const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
+  const f4v two_inv_v = inv_v + inv_v;
+  Rsrc rs[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    rs[s] = make_rsrc(packed + (size_t)(b * V + 1 + s) * c4 * pg.plane, (uint32_t)c4 * pg.plane * 16u);
+  const int soff = (int)((uint32_t)ch * pg.plane * 16u);
+  const int row_bytes = pg.pitch * 16;
+  // grad_cv of channel 4 ch + j, plane k0 + pl at this pixel: gcv + j * cstride + pl * hw
+  const size_t cstride = (size_t)Dc * hw;
+  const float* gcv = grad_cv + (((size_t)b * C + (size_t)ch * 4) * Dc + k0) * hw + pix;
+  int nch = C - ch * 4;
+  nch = nch > 4 ? 4 : nch;
+  // accumulator planes of this chunk: acc + ((n * C + 4 ch + j) * hw) for image n
+  auto acc_at = [&](int n, int j, int yy, int xx) -> u64* {
+    return acc + ((size_t)n * C + (size_t)ch * 4 + j) * hw + (size_t)yy * w + xx;
+  };
+  f4v racc = {0.0f, 0.0f, 0.0f, 0.0f};
+  __syncthreads();   // boxes
+
+  for (int kp = 0; kp < npl;) {
+    // ---- plan a pass: consecutive planes whose union footprint fits the LDS budget ----
+    Box ub[NS];
+    int area = 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      ub[s] = boxes[kp][s];
+      area += box_area(ub[s]);
+    }
+    int ke = kp + 1;
+    if (area <= kBwdSlots) {
+      for (; ke < npl; ++ke) {
+        Box nb[NS];
+        int na = 0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          nb[s] = box_union(ub[s], boxes[ke][s]);
+          na += box_area(nb[s]);
+        }
+        if (na > kBwdSlots) break;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) ub[s] = nb[s];
+        area = na;
+      }
+    }
+    const bool use_lds = area <= kBwdSlots;
+    const int T = use_lds ? area : 0;   // slots per channel plane of the LDS image
+    int base[NS], bw[NS];
+    {
+      int o = 0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        base[s] = o;
+        bw[s] = ub[s].x1 - ub[s].x0 + 1;
+        o += box_area(ub[s]);
+      }
+    }
+    if (use_lds) {
+      for (int q = (int)threadIdx.x; q < 4 * T; q += kBlock) lds[q] = 0ull;
+      __syncthreads();
+    }
+
+    // ---- the pass's planes ----
+    if (active) {
+      for (int pl = kp; pl < ke; ++pl) {
+        const int kk = k0 + pl;
+        f4v g = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j < nch) g[j] = gcv[(size_t)j * cstride + (size_t)pl * hw];
+        uint32_t pos[NS];
+        float wx[NS], wy[NS];
+        f4v xs[NS];
+        f4v sum = x0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + kk) * 9, xn, yn, h, w, true, pos[s],
+                     wx[s], wy[s]);
+          f4v tp[4];
+          load_taps(rs[s], tap_offset(pos[s], pg), soff, row_bytes, tp);
+          xs[s] = bilerp(tp, wx[s], wy[s]);
+          sum += xs[s];
+        }
+        const f4v nmean = -(sum * inv_v);
+        const f4v k2 = two_inv_v * g;
+        racc += k2 * (x0 + nmean);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          if (pos[s] == kInvalidTap) continue;
+          const f4v cs = k2 * (xs[s] + nmean);
+          const float ex = 1.0f - wx[s], ny = 1.0f - wy[s];
+          const float wt[4] = {ny * ex, ny * wx[s], wy[s] * ex, wy[s] * wx[s]};
+          const int cx = pos_x(pos[s]), cy = pos_y(pos[s]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int xx = cx + (q & 1), yy = cy + (q >> 1);
+            if (xx < 0 || xx >= w || yy < 0 || yy >= h) continue;   // zero padding: no gradient
+            const bool in_box = use_lds && xx >= ub[s].x0 && xx <= ub[s].x1 && yy >= ub[s].y0 && yy <= ub[s].y1;
+            const int slot = base[s] + (yy - ub[s].y0) * bw[s] + (xx - ub[s].x0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              if (j >= nch) break;
+              const u64 v = to_fixed(wt[q] * cs[j], fx.to_fixed);
+              if (in_box) atomicAdd(&lds[j * T + slot], v);
+              else gadd(acc_at(b * V + 1 + s, j, yy, xx), v);
+            }
+          }
+        }
+      }
+    }
+
+    // ---- flush the pass's LDS image: one global atomic per nonzero (slot, channel) ----
+    if (use_lds) {
+      __syncthreads();
+      for (int e = (int)threadIdx.x; e < T; e += kBlock) {
+        int s = 0;
+#pragma unroll
+        for (int q = 1; q < NS; ++q)
+          if (e >= base[q]) s = q;
+        int o = 0, ww = 1, bx = 0, by = 0;
+#pragma unroll
+        for (int q = 0; q < NS; ++q)
+          if (q == s) {
+            o = base[q];
+            ww = bw[q];
+            bx = ub[q].x0;
+            by = ub[q].y0;
+          }
+        const int r = (e - o) / ww, c = (e - o) - r * ww;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (j >= nch) break;
+          const u64 v = lds[j * T + e];
+          if (v) gadd(acc_at(b * V + 1 + s, j, by + r, bx + c), v);
+        }
+      }
+      __syncthreads();   // the next pass re-zeroes the image
+    }
+    kp = ke;
+  }
+  if (active) ref_part[(((size_t)grp * B + b) * c4 + ch) * hw + pix] = make_float4(racc.x, racc.y, racc.z, racc.w);
+}
+
+// Reference view: S = sum over plane groups of the partials (fixed order), scattered to the
+// reference view's plane-independent taps (its sampling matrix, plane 0 of the shard).
+__global__ __launch_bounds__(kBlock) void ref_scatter_kernel(const float4* __restrict__ ref_part,
+                                                            const float* __restrict__ sampling,
+                                                            u64* __restrict__ acc,
+                                                            const unsigned* __restrict__ mx, int B,
+                                                            int V, int C, int h, int w, int Dc,
+                                                            int groups) {
+  const uint32_t hw = (uint32_t)h * (uint32_t)w;
+  const int c4 = (C + 3) / 4;
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  const int ch = (int)blockIdx.y % c4;
+  const int b = (int)blockIdx.y / c4;
+  if (p >= hw) return;
+  const Fixed fx = fixed_scale(mx, V, Dc, hw);
+  f4v S = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int g = 0; g < groups; ++g) {
+    const float4 v = ref_part[(((size_t)g * B + b) * c4 + ch) * hw + p];
+    S += f4v{v.x, v.y, v.z, v.w};
+  }
+  const int y = (int)(p / (uint32_t)w), x = (int)(p % (uint32_t)w);
+  uint32_t pos;
+  float wx, wy;
+  src_coords(sampling + (size_t)(b * V) * Dc * 9, norm_coord(x, w), norm_coord(y, h), h, w, true, pos,
+             wx, wy);
+  if (pos == kInvalidTap) return;
+  const float ex = 1.0f - wx, ny = 1.0f - wy;
+  const float wt[4] = {ny * ex, ny * wx, wy * ex, wy * wx};
+  const int cx = pos_x(pos), cy = pos_y(pos);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int xx = cx + (q & 1), yy = cy + (q >> 1);
+    if (xx < 0 || xx >= w || yy < 0 || yy >= h) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = ch * 4 + j;
+      if (c >= C) break;
+      gadd(acc + ((size_t)(b * V) * C + c) * hw + (size_t)yy * w + xx, to_fixed(wt[q] * S[j], fx.to_fixed));
+    }
+  }
+}
+
+// More than 8 views (no packed workspace): one thread per (sample, plane, pixel), NCHW gathers,
+// every view's taps straight to the global accumulators.
+__global__ __launch_bounds__(kBlock) void cost_volume_bwd_generic_kernel(
     const float* __restrict__ feat, const float* __restrict__ sampling,
-    const float* __restrict__ grad_cv, float* __restrict__ grad_feat, int nv_rt, int C, int h,
-    int w, int Dc, int tiles, int total) {
+    const float* __restrict__ grad_cv, u64* __restrict__ acc, const unsigned* __restrict__ mx,
+    int V, int C, int h, int w, int Dc, int tiles, int total) {
   const int wk = xcd_work_id(blockIdx.x, total);
   if (wk >= total) return;
-  const int V = EXACT ? MAXV : nv_rt;
   const WorkItem it = decode_flat(wk, Dc, tiles);
   const uint32_t hw = (uint32_t)h * (uint32_t)w;
   const uint32_t p = (uint32_t)it.tile * kBlock + threadIdx.x;
   if (p >= hw) return;
+  const Fixed fx = fixed_scale(mx, V, Dc, hw);
   float xn, yn;
   pixel_coords(p, w, h, xn, yn);
-  Taps tp[MAXV];
-#pragma unroll
-  for (int v = 0; v < MAXV; ++v)
-    if (v < V) make_taps(sampling + ((size_t)(it.b * V + v) * Dc + it.kk) * 9, xn, yn, h, w, tp[v]);
+  Taps tp[MVS_MAX_VIEWS];
+  for (int v = 0; v < V; ++v) make_taps(sampling + ((size_t)(it.b * V + v) * Dc + it.kk) * 9, xn, yn, h, w, tp[v]);
   const float* fb = feat + (size_t)it.b * V * C * hw;
-  float* gb = grad_feat + (size_t)it.b * V * C * hw;
-  const float* gcv = grad_cv + ((size_t)it.b * C * Dc + it.kk) * hw + p;
   const float inv_v = 1.0f / (float)V;
   for (int c = 0; c < C; ++c) {
-    const float g = gcv[(size_t)c * Dc * hw];
-    float val[MAXV];
+    const float g = grad_cv[(((size_t)it.b * C + c) * Dc + it.kk) * hw + p];
+    float val[MVS_MAX_VIEWS];
     float sum = 0.0f;
-#pragma unroll
-    for (int v = 0; v < MAXV; ++v)
-      if (v < V) {
-        val[v] = gather(fb + ((size_t)v * C + c) * hw, tp[v]);
-        sum += val[v];
-      }
-    const float mean = sum * inv_v;
-    const float k2 = 2.0f * inv_v * g;
-#pragma unroll
-    for (int v = 0; v < MAXV; ++v)
-      if (v < V) {
-        const float coef = k2 * (val[v] - mean);
-        char* plane = reinterpret_cast<char*>(gb + ((size_t)v * C + c) * hw);
-#pragma unroll
-        for (int t = 0; t < 4; ++t)  // off[] are byte offsets
-          if (tp[v].wt[t] != 0.0f)
-            unsafeAtomicAdd(reinterpret_cast<float*>(plane + tp[v].off[t]), tp[v].wt[t] * coef);
-      }
-  }
-}
-
-// Grouped form (V = 2..8, the default): one thread per pixel of one (sample, group of PG planes).
-// The reference view's sampling is plane independent (C_i = C_r gives P = I exactly; the forward
-// resamples it once per launch), so its gradient coefficients are summed over the group's planes
-// in registers and scattered once per group: PG times fewer reference-view atomics, and PG times
-// less same-address contention (all planes of a pixel hit the same 4 reference taps).  Channels
-// run in chunks of CC so the per-channel reference values and sums stay in registers.
-constexpr int kBwdPG = 8, kBwdCC = 8;
-
-template <int V>
-__global__ __launch_bounds__(kBlock) void cost_volume_bwd_grouped_kernel(
-    const float* __restrict__ feat, const float* __restrict__ sampling,
-    const float* __restrict__ grad_cv, float* __restrict__ grad_feat, int C, int h, int w, int Dc,
-    int tiles, int groups, int total) {
-  const int wk = xcd_work_id(blockIdx.x, total);
-  if (wk >= total) return;
-  const int grp = wk % groups;
-  const int t = wk / groups;
-  const int tile = t % tiles;
-  const int b = t / tiles;
-  const uint32_t hw = (uint32_t)h * (uint32_t)w;
-  const uint32_t p = (uint32_t)tile * kBlock + threadIdx.x;
-  if (p >= hw) return;
-  const int k0 = grp * kBwdPG;
-  const int npl = min(kBwdPG, Dc - k0);
-  float xn, yn;
-  pixel_coords(p, w, h, xn, yn);
-  Taps tref;
-  make_taps(sampling + ((size_t)(b * V) * Dc + k0) * 9, xn, yn, h, w, tref);
-  const float* fb = feat + (size_t)b * V * C * hw;
-  float* gb = grad_feat + (size_t)b * V * C * hw;
-  const float* gcv = grad_cv + (size_t)b * C * Dc * hw + p;
-  const float inv_v = 1.0f / (float)V;
-  for (int c0 = 0; c0 < C; c0 += kBwdCC) {
-    float rval[kBwdCC], racc[kBwdCC];
-#pragma unroll
-    for (int cc = 0; cc < kBwdCC; ++cc) {
-      racc[cc] = 0.0f;
-      rval[cc] = c0 + cc < C ? gather(fb + (size_t)(c0 + cc) * hw, tref) : 0.0f;
+    for (int v = 0; v < V; ++v) {
+      val[v] = gather(fb + ((size_t)v * C + c) * hw, tp[v]);
+      sum += val[v];
     }
-    for (int kk = 0; kk < npl; ++kk) {
-      const int k = k0 + kk;
-      Taps tp[V - 1];
-#pragma unroll
-      for (int v = 1; v < V; ++v)
-        make_taps(sampling + ((size_t)(b * V + v) * Dc + k) * 9, xn, yn, h, w, tp[v - 1]);
-#pragma unroll
-      for (int cc = 0; cc < kBwdCC; ++cc) {
-        const int c = c0 + cc;
-        if (c >= C) break;
-        const float g = gcv[((size_t)c * Dc + k) * hw];
-        float val[V];
-        val[0] = rval[cc];
-        float sum = val[0];
-#pragma unroll
-        for (int v = 1; v < V; ++v) {
-          val[v] = gather(fb + ((size_t)v * C + c) * hw, tp[v - 1]);
-          sum += val[v];
-        }
-        const float mean = sum * inv_v;
-        const float k2 = 2.0f * inv_v * g;
-        racc[cc] += k2 * (val[0] - mean);
-#pragma unroll
-        for (int v = 1; v < V; ++v) {
-          const float coef = k2 * (val[v] - mean);
-          char* plane = reinterpret_cast<char*>(gb + ((size_t)v * C + c) * hw);
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (tp[v - 1].wt[q] != 0.0f)
-              unsafeAtomicAdd(reinterpret_cast<float*>(plane + tp[v - 1].off[q]), tp[v - 1].wt[q] * coef);
-        }
-      }
-    }
-#pragma unroll
-    for (int cc = 0; cc < kBwdCC; ++cc) {
-      if (c0 + cc >= C) break;
-      char* plane = reinterpret_cast<char*>(gb + (size_t)(c0 + cc) * hw);
+    const float nmean = -(sum * inv_v);
+    const float k2 = (inv_v + inv_v) * g;
+    for (int v = 0; v < V; ++v) {
+      const float coef = k2 * (val[v] + nmean);
+      u64* plane = acc + ((size_t)(it.b * V + v) * C + c) * hw;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (tref.wt[q] != 0.0f)
-          unsafeAtomicAdd(reinterpret_cast<float*>(plane + tref.off[q]), tref.wt[q] * racc[cc]);
+        if (tp[v].wt[q] != 0.0f) gadd(plane + tp[v].off[q] / 4u, to_fixed(tp[v].wt[q] * coef, fx.to_fixed));
     }
   }
 }
 
-// LDS-accumulated form (V = 2..8, the default): a workgroup owns a 32 x 8 pixel tile of one sample
-// and a group of 8 planes, like the forward's staged kernel.  Per channel, every source view's
-// gradient taps land in an LDS image of that view's footprint over the group (bounding box of the
-// tile's tap corners, ds_add_f32), which is then flushed with one global atomic per nonzero slot
-// (instead of 4 per (pixel, plane)); the reference view is summed over the group's planes in
-// registers as in the grouped form.  A tile whose footprints exceed the LDS budget scatters
-// straight to global memory.
-constexpr int kBwdTW = 32, kBwdTH = 8, kBwdSlots = 8192;   // 32 KB of fp32 accumulators
-
-template <int V>
-__global__ __launch_bounds__(kBlock) void cost_volume_bwd_lds_kernel(
-    const float* __restrict__ feat, const float* __restrict__ sampling,
-    const float* __restrict__ grad_cv, float* __restrict__ grad_feat, int C, int h, int w, int Dc,
-    int tiles_x, int tiles_y, int groups, int total) {
-  constexpr int NS = V - 1;
-  __shared__ float acc_l[kBwdSlots];
-  __shared__ int bb[4 * NS];
-  const int wk = xcd_work_id(blockIdx.x, total);
-  if (wk >= total) return;   // workgroup-uniform
-  const int grp = wk % groups;
-  const int t = wk / groups;
-  const int tile = t % (tiles_x * tiles_y);
-  const int b = t / (tiles_x * tiles_y);
-  const int px = (tile % tiles_x) * kBwdTW + (int)(threadIdx.x % kBwdTW);
-  const int py = (tile / tiles_x) * kBwdTH + (int)(threadIdx.x / kBwdTW);
-  const bool active = px < w && py < h;
-  const int k0 = grp * kBwdPG;
-  const int npl = min(kBwdPG, Dc - k0);
-  const uint32_t hw = (uint32_t)h * (uint32_t)w;
-  const float xn = norm_coord(active ? px : 0, w), yn = norm_coord(active ? py : 0, h);
-
-  uint32_t pos[kBwdPG][NS];
-  float fwx[kBwdPG][NS], fwy[kBwdPG][NS];
-#pragma unroll
-  for (int pl = 0; pl < kBwdPG; ++pl)
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int kk = k0 + (pl < npl ? pl : npl - 1);
-      src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + kk) * 9, xn, yn, h, w, active, pos[pl][s],
-                 fwx[pl][s], fwy[pl][s]);
-      if (pl >= npl) pos[pl][s] = kInvalidTap;
-    }
-  if (threadIdx.x < 4 * NS) bb[threadIdx.x] = 1 << 30;
-  __syncthreads();
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    int mnx = 1 << 30, mny = 1 << 30, mxx = 1 << 30, mxy = 1 << 30;   // mx*: -(max corner)
-#pragma unroll
-    for (int pl = 0; pl < kBwdPG; ++pl) {
-      const uint32_t p = pos[pl][s];
-      if (p == kInvalidTap) continue;
-      mnx = min(mnx, pos_x(p));
-      mny = min(mny, pos_y(p));
-      mxx = min(mxx, -pos_x(p));
-      mxy = min(mxy, -pos_y(p));
-    }
-    if (mnx != (1 << 30)) {
-      atomicMin(&bb[4 * s], mnx);
-      atomicMin(&bb[4 * s + 1], mny);
-      atomicMin(&bb[4 * s + 2], mxx);
-      atomicMin(&bb[4 * s + 3], mxy);
-    }
-  }
-  __syncthreads();
-  int rx0[NS], ry0[NS], rw[NS], rh[NS], base[NS + 1];
-  base[0] = 0;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const bool empty = bb[4 * s] == (1 << 30);
-    rx0[s] = empty ? 0 : bb[4 * s];
-    ry0[s] = empty ? 0 : bb[4 * s + 1];
-    rw[s] = empty ? 0 : -bb[4 * s + 2] - rx0[s] + 2;   // taps x0 .. x0 + 1
-    rh[s] = empty ? 0 : -bb[4 * s + 3] - ry0[s] + 2;
-    base[s + 1] = base[s] + rw[s] * rh[s];
-  }
-  const int nslots = base[NS];
-  const bool use_lds = nslots <= kBwdSlots;
-
-  Taps tref;
-  make_taps(sampling + ((size_t)(b * V) * Dc + k0) * 9, xn, yn, h, w, tref);
-  const float* fb = feat + (size_t)b * V * C * hw;
-  float* gb = grad_feat + (size_t)b * V * C * hw;
-  const uint32_t pix = (uint32_t)(active ? py : 0) * (uint32_t)w + (uint32_t)(active ? px : 0);
-  const float* gcv = grad_cv + (size_t)b * C * Dc * hw + pix;
-  const float inv_v = 1.0f / (float)V;
-
-  for (int c = 0; c < C; ++c) {
-    if (use_lds) {
-      __syncthreads();   // the previous channel's flush has read every slot
-      for (int q = (int)threadIdx.x; q < nslots; q += kBlock) acc_l[q] = 0.0f;
-      __syncthreads();
-    }
-    if (active) {
-      const float rv = gather(fb + (size_t)c * hw, tref);
-      float racc = 0.0f;
-      for (int pl = 0; pl < npl; ++pl) {
-        const float g = gcv[((size_t)c * Dc + k0 + pl) * hw];
-        float val[V], wt[NS][4];
-        val[0] = rv;
-        float sum = rv;
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          float x = 0.0f;
-          uint32_t p = kInvalidTap;
-          float wx = 0.0f, wy = 0.0f;
-#pragma unroll
-          for (int q = 0; q < kBwdPG; ++q)   // static register indexing
-            if (q == pl) {
-              p = pos[q][s];
-              wx = fwx[q][s];
-              wy = fwy[q][s];
-            }
-          tap_weights(wx, wy, wt[s]);
-          if (p != kInvalidTap) {
-            const int x0 = pos_x(p), y0 = pos_y(p);
-            const float* fp = fb + ((size_t)(1 + s) * C + c) * hw;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const int xx = x0 + (q & 1), yy = y0 + (q >> 1);
-              if (xx >= 0 && xx < w && yy >= 0 && yy < h) x += fp[(size_t)yy * w + xx] * wt[s][q];
-              else wt[s][q] = 0.0f;
-            }
-          } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) wt[s][q] = 0.0f;
-          }
-          val[1 + s] = x;
-          sum += x;
-        }
-        const float mean = sum * inv_v;
-        const float k2 = 2.0f * inv_v * g;
-        racc += k2 * (val[0] - mean);
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          const float coef = k2 * (val[1 + s] - mean);
-          uint32_t p = kInvalidTap;
-#pragma unroll
-          for (int q = 0; q < kBwdPG; ++q)
-            if (q == pl) p = pos[q][s];
-          if (p == kInvalidTap) continue;
-          const int x0 = pos_x(p), y0 = pos_y(p);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (wt[s][q] == 0.0f) continue;
-            const int xx = x0 + (q & 1), yy = y0 + (q >> 1);
-            if (use_lds) {
-              const int slot = base[s] + (yy - ry0[s]) * rw[s] + (xx - rx0[s]);
-              atomicAdd(&acc_l[slot], wt[s][q] * coef);
-            } else {
-              unsafeAtomicAdd(gb + ((size_t)(1 + s) * C + c) * hw + (size_t)yy * w + xx, wt[s][q] * coef);
-            }
-          }
-        }
-      }
-      char* rplane = reinterpret_cast<char*>(gb + (size_t)c * hw);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (tref.wt[q] != 0.0f)
-          unsafeAtomicAdd(reinterpret_cast<float*>(rplane + tref.off[q]), tref.wt[q] * racc);
-    }
-    if (use_lds) {
-      __syncthreads();   // every tap of this channel is in LDS
-      for (int q = (int)threadIdx.x; q < nslots; q += kBlock) {
-        const float v = acc_l[q];
-        if (v == 0.0f) continue;
-        int s = 0;
-#pragma unroll
-        for (int k = 1; k < NS; ++k)
-          if (q >= base[k]) s = k;
-        int ww = rw[0], xo = rx0[0], yo = ry0[0], bs = base[0];
-#pragma unroll
-        for (int k = 1; k < NS; ++k)
-          if (s == k) {
-            ww = rw[k];
-            xo = rx0[k];
-            yo = ry0[k];
-            bs = base[k];
-          }
-        const int e = q - bs;
-        const int yy = yo + e / ww, xx = xo + e % ww;
-        if (xx >= 0 && xx < w && yy >= 0 && yy < h)   // always: only in-image taps were added
-          unsafeAtomicAdd(gb + ((size_t)(1 + s) * C + c) * hw + (size_t)yy * w + xx, v);
-      }
-    }
-  }
+__global__ __launch_bounds__(kBlock) void fixed_to_float_kernel(const u64* __restrict__ acc, size_t n,
+                                                               const unsigned* __restrict__ mx, int V,
+                                                               int Dc, uint32_t hw, float* __restrict__ out) {
+  const Fixed fx = fixed_scale(mx, V, Dc, hw);
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock)
+    out[i] = (float)((double)(long long)acc[i] * fx.to_float);
 }
 
 template <int V>
-void launch_bwd_lds(const Geometry& g, const float* feat, const float* smp, const float* gcv, float* gf,
-                    hipStream_t s) {
+void launch_main(const Geometry& g, const float4* packed, const float4* refs, const float* smp,
+                 const float* gcv, u64* acc, float4* ref_part, const unsigned* mx, hipStream_t s) {
   const int tiles_x = (g.w + kBwdTW - 1) / kBwdTW, tiles_y = (g.h + kBwdTH - 1) / kBwdTH;
-  const int groups = (g.Dc + kBwdPG - 1) / kBwdPG;
-  const int total = g.B * tiles_x * tiles_y * groups;
-  hipLaunchKernelGGL((cost_volume_bwd_lds_kernel<V>), xcd_grid(total), dim3(kBlock), 0, s, feat, smp, gcv,
-                     gf, g.C, g.h, g.w, g.Dc, tiles_x, tiles_y, groups, total);
+  const int groups = (g.Dc + kBwdKPG - 1) / kBwdKPG;
+  const int c4 = (g.C + 3) / 4;
+  const int total = g.B * c4 * tiles_x * tiles_y * groups;
+  hipLaunchKernelGGL((cost_volume_bwd_kernel<V>), xcd_grid(total), dim3(kBlock), 0, s, packed, refs, smp,
+                     gcv, acc, ref_part, mx, g.B, g.C, g.h, g.w, g.Dc, tiles_x, tiles_y, groups, total);
 }
 
-template <int V>
-void launch_bwd_grouped(const Geometry& g, const float* feat, const float* smp, const float* gcv,
-                        float* gf, hipStream_t s) {
-  const int groups = (g.Dc + kBwdPG - 1) / kBwdPG;
-  const int total = g.B * g.tiles * groups;
-  hipLaunchKernelGGL((cost_volume_bwd_grouped_kernel<V>), xcd_grid(total), dim3(kBlock), 0, s, feat, smp,
-                     gcv, gf, g.C, g.h, g.w, g.Dc, g.tiles, groups, total);
-}
+// backward workspace: [acc u64 N*C*hw][ref partials groups*B*C4*hw float4][2 uints max]
+struct BwdLayout {
+  size_t acc, ref_part, mx, total;
+};
 
-template <int MAXV, bool EXACT>
-void launch_bwd(const Geometry& g, const float* feat, const float* smp, const float* gcv,
-                float* gf, hipStream_t s) {
-  hipLaunchKernelGGL((cost_volume_bwd_kernel<MAXV, EXACT>), xcd_grid(g.total), dim3(kBlock), 0, s,
-                     feat, smp, gcv, gf, g.V, g.C, g.h, g.w, g.Dc, g.tiles, g.total);
+BwdLayout bwd_layout(int B, int V, int C, int h, int w, int Dc) {
+  BwdLayout L;
+  const size_t hw = (size_t)h * w;
+  const size_t groups = (size_t)(Dc + kBwdKPG - 1) / kBwdKPG;
+  L.acc = 0;
+  L.ref_part = align256((size_t)B * V * C * hw * 8);
+  L.mx = L.ref_part + (V >= 2 && V <= 8 ? align256(groups * B * ((C + 3) / 4) * hw * 16) : 0);
+  L.total = L.mx + 256;
+  return L;
 }
 
 }  // namespace
 
-void launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* sampling,
-                            const float* grad_cv, float* grad_feat, hipStream_t s) {
-  switch (g.V) {
-    case 1: launch_bwd<1, true>(g, feat, sampling, grad_cv, grad_feat, s); break;
-#ifdef MVS_EXP_BWD_FLAT
-    case 2: launch_bwd<2, true>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 3: launch_bwd<3, true>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 5: launch_bwd<5, true>(g, feat, sampling, grad_cv, grad_feat, s); break;
-#elif defined(MVS_EXP_BWD_GROUPED)
-    case 2: launch_bwd_grouped<2>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 3: launch_bwd_grouped<3>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 4: launch_bwd_grouped<4>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 5: launch_bwd_grouped<5>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 6: launch_bwd_grouped<6>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 7: launch_bwd_grouped<7>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 8: launch_bwd_grouped<8>(g, feat, sampling, grad_cv, grad_feat, s); break;
-#else
-    case 2: launch_bwd_lds<2>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 3: launch_bwd_lds<3>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 4: launch_bwd_lds<4>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 5: launch_bwd_lds<5>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 6: launch_bwd_lds<6>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 7: launch_bwd_lds<7>(g, feat, sampling, grad_cv, grad_feat, s); break;
-    case 8: launch_bwd_lds<8>(g, feat, sampling, grad_cv, grad_feat, s); break;
-#endif
-    default: launch_bwd<MVS_MAX_VIEWS, false>(g, feat, sampling, grad_cv, grad_feat, s); break;
+size_t cost_volume_bwd_workspace_bytes(int B, int V, int C, int h, int w, int Dc) {
+  return bwd_layout(B, V, C, h, w, Dc).total;
+}
+
+int launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* fwd_ws,
+                           const float* grad_cv, void* bwd_ws, float* grad_feat, hipStream_t s) {
+  const size_t n_feat = (size_t)g.B * g.V * g.C * g.h * g.w;
+  if (g.V == 1)   // the variance of one view is identically 0: so is its gradient
+    return hipMemsetAsync(grad_feat, 0, n_feat * sizeof(float), s) == hipSuccess ? MVS_OK : MVS_ERR_HIP;
+  const BwdLayout L = bwd_layout(g.B, g.V, g.C, g.h, g.w, g.Dc);
+  char* ws = static_cast<char*>(bwd_ws);
+  u64* acc = reinterpret_cast<u64*>(ws + L.acc);
+  float4* ref_part = reinterpret_cast<float4*>(ws + L.ref_part);
+  unsigned* mx = reinterpret_cast<unsigned*>(ws + L.mx);
+  if (hipMemsetAsync(acc, 0, n_feat * 8, s) != hipSuccess) return MVS_ERR_HIP;
+  if (hipMemsetAsync(mx, 0, 8, s) != hipSuccess) return MVS_ERR_HIP;
+  const size_t n_gcv = (size_t)g.B * g.C * g.Dc * g.h * g.w;
+  hipLaunchKernelGGL(abs_max_kernel, dim3(2048), dim3(kBlock), 0, s, grad_cv, n_gcv, mx);
+  hipLaunchKernelGGL(abs_max_kernel, dim3(256), dim3(kBlock), 0, s, feat, n_feat, mx + 1);
+  const float* smp = fwd_ws;
+  if (g.V <= 8) {
+    const float4* packed = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(fwd_ws) +
+                                                           sampling_bytes_aligned(g.B * g.V, g.Dc));
+    const int c4 = (g.C + 3) / 4;
+    const float4* refs = packed + (size_t)g.B * g.V * c4 * pad_geom(g.h, g.w).plane;
+    switch (g.V) {
+      case 2: launch_main<2>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
+      case 3: launch_main<3>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
+      case 4: launch_main<4>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
+      case 5: launch_main<5>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
+      case 6: launch_main<6>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
+      case 7: launch_main<7>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
+      default: launch_main<8>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
+    }
+    const uint32_t hw = (uint32_t)g.h * (uint32_t)g.w;
+    const int groups = (g.Dc + kBwdKPG - 1) / kBwdKPG;
+    hipLaunchKernelGGL(ref_scatter_kernel, dim3((hw + kBlock - 1) / kBlock, (unsigned)(g.B * c4)), dim3(kBlock),
+                       0, s, ref_part, smp, acc, mx, g.B, g.V, g.C, g.h, g.w, g.Dc, groups);
+  } else {
+    hipLaunchKernelGGL(cost_volume_bwd_generic_kernel, xcd_grid(g.total), dim3(kBlock), 0, s, feat, smp, grad_cv,
+                       acc, mx, g.V, g.C, g.h, g.w, g.Dc, g.tiles, g.total);
   }
+  const size_t blocks = (n_feat + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(fixed_to_float_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(kBlock), 0, s,
+                     acc, n_feat, mx, g.V, g.Dc, (uint32_t)((size_t)g.h * g.w), grad_feat);
+  return hip_status();
 }
 
 }  // namespace mvs

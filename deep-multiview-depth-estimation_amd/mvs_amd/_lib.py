@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmvs_cost_volume.so"
 # MVS_LIB_PATH: load another build of the same ABI (A/B kernel experiments, tools/exp_*.sh)
 LIB_PATH = os.environ.get("MVS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 MVS_OK = 0
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported n_views", -3: "too large",
@@ -45,8 +45,10 @@ SIGNATURES = {
                                          _c_int, _c_int, _c_int, _c_float, _p, _p, _p]),
     "mvs_assemble_cost_volume_fwd": (_c_int, [_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                                               _p, _p]),
+    "mvs_cost_volume_bwd_workspace_bytes": (ctypes.c_size_t, [_c_int, _c_int, _c_int, _c_int,
+                                                              _c_int, _c_int]),
     "mvs_cost_volume_bwd": (_c_int, [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
-                                     _p, _p]),
+                                     _p, _p, _p]),
     "mvs_extract_depth_map_fwd": (_c_int, [_p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _p,
                                            _p]),
     "mvs_normalize_images": (_c_int, [_p, _c_int, _c_int, _c_int, _p, _p, _p, _p]),

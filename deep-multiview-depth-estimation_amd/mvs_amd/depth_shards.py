@@ -3,19 +3,28 @@
 The fused warp+variance is independent per (sample, plane, pixel), so rank r of P computes planes
 [r*D/P, (r+1)*D/P) with no communication (the kernel's ``d_begin``/``d_count``), from replicated
 features and cameras.  The 3-D regulariser is NOT D-local (stride-2 convs with padding D/2+1 remap
-planes non-locally, softmax and the soft-argmin span all D; SURVEY.md §8 e), so the parity-preserving
-exchange is an all-gather of the cost-volume D-slabs (RCCL over xGMI when the process group is
-``nccl``), after which the rank that owns a sample (b mod P) runs the regulariser and soft-argmin.
+planes non-locally, softmax and the soft-argmin span all D; SURVEY.md §8 e), so each sample's
+full-D cost volume is assembled on the ONE rank that owns it (sample b -> rank b mod P), which then
+runs the regulariser, soft-argmin and refinement for it:
+
+  * owner-targeted exchange (``exchange_to_owners``): every rank sends its slab of sample b only
+    to b's owner -- a gather to the owner when B < P (cfg 4: B = 1, only rank 0 receives), an
+    all-to-all by sample when B >= P; nothing goes to ranks that would discard it;
+  * the owner receives straight into the final [B_own, C, D, h, w] layout: for every (sample,
+    channel) a source rank's slab is one contiguous block of D/P planes of the destination, so
+    each block is its own point-to-point receive (one grouped ``batch_isend_irecv``, RCCL over
+    xGMI when the process group is ``nccl``); only the rank's own slab is copied locally.
+
+Eval-mode inference only: BatchNorm in train mode would normalise with the statistics of the
+owned samples instead of the whole batch (model.py:184), and the point-to-point exchange carries
+no gradient -- ``DepthShardedMVSNet.forward`` raises in either case.
 
 Reference: there is no multi-GPU path in the reference (single device, ``config.py:24``); this
-module reproduces ``model.py:168-207`` exactly for every owned sample (BN eval mode).
+module reproduces ``model.py:168-207`` for every owned sample.
 """
 import torch
 import torch.distributed as dist
 import torch.nn as nn
-
-from .costvolume import warp_and_assemble_cost_volume
-from .depthmap import extract_depth_map
 
 
 def plane_shard(d_num, world, rank):
@@ -31,51 +40,119 @@ def owned_samples(batch_size, world, rank):
     return [b for b in range(batch_size) if b % world == rank]
 
 
+def exchange_to_owners(slab, world, rank, group=None):
+    """Owner-targeted exchange of cost-volume D-slabs.
+
+    ``slab`` is this rank's [B, C, Dl, h, w] (planes [rank*Dl, (rank+1)*Dl) of every sample).
+    Returns the full-D volume [len(owned_samples), C, world*Dl, h, w] of the samples this rank
+    owns (an empty tensor when it owns none).  Every rank must call it (collective)."""
+    slab = slab.contiguous()
+    b_all, c, dl, h, w = slab.shape
+    mine = owned_samples(b_all, world, rank)
+    out = slab.new_empty((len(mine), c, world * dl, h, w))
+    for i, b in enumerate(mine):   # own planes: the one local copy
+        out[i, :, rank * dl:(rank + 1) * dl].copy_(slab[b])
+    if world == 1:
+        return out
+    ops = []
+    for b in range(b_all):
+        owner = b % world
+        if owner != rank:
+            ops += [dist.P2POp(dist.isend, slab[b, ch], owner, group) for ch in range(c)]
+        else:
+            i = mine.index(b)
+            for src in range(world):
+                if src != rank:
+                    ops += [dist.P2POp(dist.irecv, out[i, ch, src * dl:(src + 1) * dl], src, group)
+                            for ch in range(c)]
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return out
+
+
 def gather_depth_slabs(slab, world, group=None):
-    """All-gather [B, C, Dl, h, w] slabs (rank order = plane order) into [B, C, world*Dl, h, w]."""
+    """All-gather [B, C, Dl, h, w] slabs (rank order = plane order) into [B, C, world*Dl, h, w] on
+    every rank (every rank then holds every sample: use exchange_to_owners when only the owner
+    needs a sample's volume)."""
     if world == 1:
         return slab
     slab = slab.contiguous()
-    backend = dist.get_backend(group)
-    if backend == "nccl":
-        buf = torch.empty((world,) + tuple(slab.shape), dtype=slab.dtype, device=slab.device)
-        dist.all_gather_into_tensor(buf, slab, group=group)
-    else:
-        parts = [torch.empty_like(slab) for _ in range(world)]
-        dist.all_gather(parts, slab, group=group)
-        buf = torch.stack(parts)
     b, c, dl, h, w = slab.shape
-    return buf.permute(1, 2, 0, 3, 4, 5).reshape(b, c, world * dl, h, w)
+    out = slab.new_empty((b, c, world * dl, h, w))
+    ops = []
+    rank = dist.get_rank(group)
+    out[:, :, rank * dl:(rank + 1) * dl].copy_(slab)
+    for peer in range(world):
+        if peer == rank:
+            continue
+        for bb in range(b):
+            for ch in range(c):
+                ops.append(dist.P2POp(dist.isend, slab[bb, ch], peer, group))
+                ops.append(dist.P2POp(dist.irecv, out[bb, ch, peer * dl:(peer + 1) * dl], peer, group))
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
+    return out
+
+
+class _HipOps:
+    """The product path: fused HIP cost volume slab + HIP soft-argmin."""
+
+    @staticmethod
+    def cost_volume_slab(K, R, T, d_min, d_int, feats, batch_size, n_views, d_num, d_scale, d_begin,
+                         d_count):
+        from .costvolume import warp_and_assemble_cost_volume
+        return warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, batch_size, n_views,
+                                             d_num=d_num, d_scale=d_scale, d_begin=d_begin,
+                                             d_count=d_count)
+
+    @staticmethod
+    def extract_depth_map(prob, d_batch, n_est):
+        from .depthmap import extract_depth_map
+        return extract_depth_map(prob, d_batch, n_est)
 
 
 class DepthShardedMVSNet(nn.Module):
-    """Wraps an ``MVSNet``: sharded cost volume + all-gather + owner-computes regulariser.
+    """Wraps an ``MVSNet``: D-sharded cost volume + owner-targeted exchange + owner-computes
+    regulariser.
 
     ``forward`` returns ``(samples, initial, refined)``: the indices of the samples this rank owns
-    and their depth maps ([len(samples), 1, h, w] each; empty when the rank owns none)."""
+    and their depth maps ([len(samples), 1, h, w] each; ``None`` when the rank owns none).
+    ``ops`` supplies the slab producer and the soft-argmin (default: the HIP kernels)."""
 
-    def __init__(self, net, world, rank, group=None):
+    def __init__(self, net, world, rank, group=None, ops=None):
         super().__init__()
         self.net = net
         self.world = world
         self.rank = rank
         self.group = group
+        self.ops = ops or _HipOps
+
+    def _check_mode(self):
+        if torch.is_grad_enabled():
+            raise RuntimeError("DepthShardedMVSNet is inference-only: the point-to-point exchange "
+                               "carries no gradient (run under torch.no_grad())")
+        bns = [m for m in self.net.modules() if isinstance(m, nn.modules.batchnorm._BatchNorm)]
+        if any(m.training for m in bns):
+            raise RuntimeError("DepthShardedMVSNet needs BatchNorm in eval mode: train-mode batch "
+                               "statistics would cover only this rank's samples (model.py:184)")
 
     def forward(self, nn_input, K_batch, R_batch, T_batch, d_min, d_int, batch_size, n_views):
+        self._check_mode()
         c = self.net.cfg
         d_begin, d_count = plane_shard(c.d_num, self.world, self.rank)
         feats = self.net.feature_encoder(nn_input)
-        slab, d_batch, ref_views = warp_and_assemble_cost_volume(
-            K_batch, R_batch, T_batch, d_min, d_int, feats, batch_size, n_views,
-            d_num=c.d_num, d_scale=c.d_scale, d_begin=d_begin, d_count=d_count)
-        cv = gather_depth_slabs(slab, self.world, self.group)
+        slab, d_batch, ref_views = self.ops.cost_volume_slab(
+            K_batch, R_batch, T_batch, d_min, d_int, feats, batch_size, n_views, c.d_num, c.d_scale,
+            d_begin, d_count)
+        cv = exchange_to_owners(slab, self.world, self.rank, self.group)
         mine = owned_samples(batch_size, self.world, self.rank)
         if not mine:
             return mine, None, None
         idx = torch.tensor(mine, device=cv.device)
-        prob = self.net.cost_volume_reg(cv.index_select(0, idx))
-        d_sel = d_batch.index_select(0, idx)
-        initial = extract_depth_map(prob, d_sel, c.n_depth_est)
+        prob = self.net.cost_volume_reg(cv)
+        d_sel = d_batch.to(cv.device).index_select(0, idx)
+        initial = self.ops.extract_depth_map(prob, d_sel, c.n_depth_est)
         dm = d_min.reshape(-1, 1, 1, 1).expand(batch_size, 1, 1, 1).to(cv.device).index_select(0, idx)
         di = d_int.reshape(-1, 1, 1, 1).expand(batch_size, 1, 1, 1).to(cv.device).index_select(0, idx)
         refined = self.net.refine(nn_input, initial, dm, di, ref_views[mine])

@@ -91,9 +91,17 @@ class CostVolumeReg(nn.Module):
         self.live_region = True
 
     def forward(self, cv):
-        if self.live_region and not self._bn_uses_batch_stats():
+        if self.live_region and not self._bn_uses_batch_stats() and self._live_geometry_ok(cv):
             return self.forward_live(cv)
         return self.forward_full(cv)
+
+    def _live_geometry_ok(self, cv):
+        """forward_live relies on every U-Net level having the cost volume's extent n, which holds
+        when the module's padding is the one config.py:20-21 derives from n.  A module built for
+        another D or resolution takes forward_full, which (like the reference) then fails with the
+        shape mismatch at the level sums instead of returning wrongly indexed levels."""
+        from .config import pad_outpad
+        return (self.pad, self.outpad) == pad_outpad(*cv.shape[2:])
 
     def _bn_uses_batch_stats(self):
         return any(bn.training or bn.running_mean is None

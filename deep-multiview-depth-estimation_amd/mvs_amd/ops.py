@@ -118,23 +118,27 @@ def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scal
 
 
 @torch.library.custom_op("mvs::cost_volume_backward", mutates_args=())
-def cost_volume_backward(feat: torch.Tensor, sampling: torch.Tensor, grad_cv: torch.Tensor,
+def cost_volume_backward(feat: torch.Tensor, workspace: torch.Tensor, grad_cv: torch.Tensor,
                          batch_size: int, n_views: int, d_count: int) -> torch.Tensor:
+    """d <cv, grad_cv> / d feat (deterministic: 64-bit fixed-point accumulation in the kernel).
+    ``workspace`` is the forward's (sampling matrices, packed features, resampled references)."""
     _require_gpu(feat, "feature_maps")
     lib = _lib.load()
     feat = feat.to(_F32).contiguous()
     grad_cv = grad_cv.to(_F32).contiguous()
     n, c, h, w = feat.shape
     grad_feat = torch.empty_like(feat)
-    st = lib.mvs_cost_volume_bwd(_lib.ptr(feat), _lib.ptr(sampling), _lib.ptr(grad_cv),
-                                 batch_size, n_views, c, h, w, d_count, _lib.ptr(grad_feat),
-                                 _lib.stream_handle(feat.device))
+    nb = lib.mvs_cost_volume_bwd_workspace_bytes(batch_size, n_views, c, h, w, d_count)
+    bws = torch.empty((max(nb, 8) + 7) // 8, device=feat.device, dtype=torch.int64)
+    st = lib.mvs_cost_volume_bwd(_lib.ptr(feat), _lib.ptr(workspace), _lib.ptr(grad_cv),
+                                 batch_size, n_views, c, h, w, d_count, _lib.ptr(bws),
+                                 _lib.ptr(grad_feat), _lib.stream_handle(feat.device))
     _lib.check(st, "mvs_cost_volume_bwd")
     return grad_feat
 
 
 @cost_volume_backward.register_fake
-def _(feat, sampling, grad_cv, batch_size, n_views, d_count):
+def _(feat, workspace, grad_cv, batch_size, n_views, d_count):
     return torch.empty_like(feat)
 
 

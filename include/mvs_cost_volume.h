@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 1
+#define MVS_ABI_VERSION 2
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -125,15 +125,25 @@ int mvs_homography_warp_fwd(const float* feat, const float* K, const float* R, c
 int mvs_assemble_cost_volume_fwd(const float* warped, int batch_size, int n_views,
                                  int channels, int d, int h, int w, float* cv_out, void* stream);
 
+/* Bytes of the workspace mvs_cost_volume_bwd needs (64-bit accumulators for every feature element,
+ * the reference view's per-plane-group partial sums, two scalars). */
+size_t mvs_cost_volume_bwd_workspace_bytes(int batch_size, int n_views, int channels, int h, int w,
+                                           int d_count);
+
 /*
  * Backward of the fused op w.r.t. the features (autograd of costvolume.py:14 + grid_sample,
- * exercised by train.py:103).  grad_feat[N][C][h][w] is OVERWRITTEN (zeroed, then accumulated
- * with float atomics -- summation order is not deterministic, like torch's grid_sample backward
- * on GPU).  `sampling` is the workspace filled by the forward call with the same geometry.
+ * exercised by train.py:103): grad_feat[N][C][h][w] is OVERWRITTEN with d<cv, grad_cv>/d feat.
+ * `workspace` is the forward call's workspace (same geometry, not modified since): its sampling
+ * matrices, packed features and resampled reference views are reused.  `bwd_workspace` holds
+ * mvs_cost_volume_bwd_workspace_bytes(...) bytes.
+ * DETERMINISTIC: contributions are accumulated in 64-bit fixed point (integer adds are
+ * associative), so the result is bit-identical across runs whatever the scheduling; resolution
+ * 2^-61 * d_count*h*w*8*max|grad_cv|*max|feat|/n_views (about 1e-12 of the largest possible
+ * contribution at BASELINE cfg 2).  Non-finite inputs give unspecified results.
  */
-int mvs_cost_volume_bwd(const float* feat, const float* sampling, const float* grad_cv,
+int mvs_cost_volume_bwd(const float* feat, const float* workspace, const float* grad_cv,
                         int batch_size, int n_views, int channels, int h, int w, int d_count,
-                        float* grad_feat, void* stream);
+                        void* bwd_workspace, float* grad_feat, void* stream);
 
 /*
  * Soft-argmin with the reference's permutation-indexed mask (depthmap.py:4-22):

@@ -195,3 +195,50 @@ def cost_volume_fp64(feat, K, R, T, d_min, d_int, batch_size, n_views, d_num, d_
             x = np.stack(vals)
             cv[b, :, kk] = ((x - x.mean(0)) ** 2).mean(0)
     return cv
+
+
+def cost_volume_torch64(feat, K, R, T, d_min, d_int, batch_size, n_views, d_num, d_scale=D_SCALE,
+                        d_begin=0, d_count=None):
+    """The float64 law of ``cost_volume_fp64`` in torch (differentiable w.r.t. ``feat``): the
+    gradient oracle for the backward, free of the reference's fp32 homography noise.  Sampling at
+    ix = xs*w/(w-1) - 0.5 (xs = dehom(H^-1 [x,y,1])) through grid_sample(bilinear, zeros,
+    align_corners=False) with the normalised coordinate (2 ix + 1) / w - 1."""
+    feat = torch.as_tensor(feat).double()
+    K = np.asarray(K, np.float64)
+    R = np.asarray(R, np.float64)
+    T = np.asarray(T, np.float64).reshape(-1, 3, 1)
+    d_min = np.asarray(d_min, np.float64).reshape(-1)
+    d_int = np.asarray(d_int, np.float64).reshape(-1)
+    n, c, h, w = feat.shape
+    if d_count is None:
+        d_count = d_num - d_begin
+    ys, xs = np.meshgrid(np.arange(h, dtype=np.float64), np.arange(w, dtype=np.float64), indexing="ij")
+    pix = np.stack([xs.ravel(), ys.ravel(), np.ones(h * w)])
+    out = []
+    for b in range(batch_size):
+        r = b * n_views
+        C_r = -R[r].T @ T[r]
+        n_r = R[r][:, 2:3].T
+        grids = []
+        for v in range(n_views):
+            i = b * n_views + v
+            C_i = -R[i].T @ T[i]
+            gv = []
+            for kk in range(d_count):
+                d = d_min[i % batch_size] + d_scale * d_int[i % batch_size] * (d_begin + kk)
+                H = K[i] @ R[i] @ (np.eye(3) - (C_i - C_r) @ n_r / d) @ R[r].T @ np.linalg.inv(K[r])
+                src = np.linalg.inv(H) @ pix
+                s = src[2]
+                good = np.abs(s) > 1e-8
+                sx = np.where(good, src[0] / np.where(good, s, 1.0), src[0])
+                sy = np.where(good, src[1] / np.where(good, s, 1.0), src[1])
+                ix = sx * w / (w - 1) - 0.5
+                iy = sy * h / (h - 1) - 0.5
+                gv.append(np.stack([(2 * ix + 1) / w - 1, (2 * iy + 1) / h - 1], -1).reshape(h, w, 2))
+            grids.append(torch.from_numpy(np.stack(gv)))          # [D, h, w, 2]
+        x = torch.stack([F.grid_sample(feat[b * n_views + v].unsqueeze(0).expand(d_count, c, h, w),
+                                       grids[v], mode="bilinear", padding_mode="zeros",
+                                       align_corners=False) for v in range(n_views)])   # [V, D, C, h, w]
+        mean = x.mean(0, keepdim=True)
+        out.append(((x - mean) ** 2).mean(0).permute(1, 0, 2, 3))   # [C, D, h, w]
+    return torch.stack(out)

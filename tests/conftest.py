@@ -16,6 +16,9 @@ for sub in ("deep-multiview-depth-estimation_amd", "oracle", os.path.join("tests
         sys.path.insert(0, p)
 
 GOLDEN = os.path.join(REPO, "tests", "golden")
+# MIOpen's find results for the regulariser's convolutions ship with the repo (tools/miopen_db,
+# as bench.py uses them): without them the first full-volume cfg-2 convolutions search for minutes
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(REPO, "tools", "miopen_db"))
 
 
 def pytest_configure(config):

@@ -1,9 +1,13 @@
-"""CPU, gloo, world_size 2: the multi-GPU exchange logic of mvs_amd.depth_shards.
+"""CPU, gloo, world_size 2: the multi-GPU path of mvs_amd.depth_shards.
 
-Each rank computes its D-slab of the cost volume (here with the oracle, on the CPU -- the HIP
-kernel computes the same slab on the GPU via d_begin/d_count, see test_gpu_parity
-test_depth_shards_concatenate_to_full_volume), then gather_depth_slabs reassembles the volume;
-it must equal the single-process volume bit for bit, on every rank.
+* ``exchange_to_owners`` / ``gather_depth_slabs``: each rank computes its D-slab of the cost
+  volume (here with the oracle, on the CPU -- the HIP kernel computes the same slab on the GPU via
+  d_begin/d_count, see test_gpu_parity test_depth_shards_concatenate_to_full_volume); the owner of
+  each sample must end with exactly the single-process volume of that sample, bit for bit.
+* ``DepthShardedMVSNet.forward`` end to end with the oracle injected as the slab producer and
+  soft-argmin (``ops=``) and the regulariser/refinement on the CPU: every rank's owned depth maps
+  must equal the single-process model's (model.py:168-207 via oracle.mvsnet_forward); B=3 (rank 0
+  owns samples 0 and 2, rank 1 owns sample 1) and B=1 (cfg 4's shape: rank 1 owns nothing).
 """
 import os
 import socket
@@ -24,17 +28,21 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+def _setup(rank, world, port):
     import sys
     for sub in ("deep-multiview-depth-estimation_amd", "oracle", os.path.join("tests", "golden")):
         sys.path.insert(0, os.path.join(REPO, sub))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+
+
+def _exchange_worker(rank, world, port, q):
+    _setup(rank, world, port)
     try:
-        torch.set_num_threads(2)
         import mvs_oracle
         from cameras import camera_batch, depth_range, features
-        from mvs_amd.depth_shards import gather_depth_slabs, owned_samples, plane_shard
+        from mvs_amd.depth_shards import exchange_to_owners, gather_depth_slabs, owned_samples, plane_shard
         B, V, C, h, w, D = 3, 3, 4, 10, 14, 8
         K, R, T = camera_batch(B, V, h, w)
         d_min, d_int = depth_range(B, d_int=40.0, distinct=True)
@@ -44,25 +52,101 @@ def _worker(rank, world, port, q):
         full = mvs_oracle.assemble_cost_volume(warped, V)
         begin, count = plane_shard(D, world, rank)
         slab = full[:, :, begin:begin + count].clone()
-        got = gather_depth_slabs(slab, world)
-        ok = torch.equal(got, full)
         mine = owned_samples(B, world, rank)
-        q.put((rank, ok, mine))
+        own = exchange_to_owners(slab, world, rank)
+        ok_owner = tuple(own.shape) == (len(mine), C, D, h, w) and torch.equal(own, full[mine])
+        ok_all = torch.equal(gather_depth_slabs(slab, world), full)
+        q.put((rank, ok_owner, ok_all, mine))
     finally:
         dist.destroy_process_group()
 
 
-def test_gather_depth_slabs_world2():
-    world = 2
+class _OracleOps:
+    """The oracle as DepthShardedMVSNet's slab producer and soft-argmin (CPU)."""
+
+    @staticmethod
+    def cost_volume_slab(K, R, T, d_min, d_int, feats, batch_size, n_views, d_num, d_scale, d_begin,
+                         d_count):
+        import mvs_oracle
+        warped, d_batch, ref_views = mvs_oracle.homography_warping(
+            K, R, T, d_min, d_int, feats, batch_size, n_views, d_num, d_scale, concat_growth=False)
+        cv = mvs_oracle.assemble_cost_volume(warped, n_views)
+        return cv[:, :, d_begin:d_begin + d_count].contiguous(), d_batch, ref_views
+
+    @staticmethod
+    def extract_depth_map(prob, d_batch, n_est):
+        import mvs_oracle
+        return mvs_oracle.extract_depth_map(prob, d_batch, n_est)
+
+
+def _model_worker(rank, world, port, B, q):
+    _setup(rank, world, port)
+    try:
+        import mvs_oracle
+        from cameras import camera_batch, depth_range
+        from weights import deterministic_state_dict
+        from mvs_amd.config import MVSConfig
+        from mvs_amd.depth_shards import DepthShardedMVSNet
+        from mvs_amd.model import MVSNet
+        V, D, H, W = 3, 8, 64, 80
+        net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W), device=torch.device("cpu"))
+        net.load_state_dict(deterministic_state_dict(net.state_dict()))
+        net.eval()
+        net.cost_volume_reg.live_region = False   # the oracle's op sequence (forward_full) on both sides
+        K, R, T = camera_batch(B, V, H // 4, W // 4)
+        d_min, d_int = depth_range(B, d_int=6.0, distinct=True)
+        img = torch.randn(B * V, 3, H, W, generator=torch.Generator().manual_seed(11))
+        sharded = DepthShardedMVSNet(net, world, rank, ops=_OracleOps)
+        with torch.no_grad():
+            ini1, ref1, _ = mvs_oracle.mvsnet_forward(net, img, K, R, T, d_min, d_int, B, V, D,
+                                                      (H // 4, W // 4))
+            mine, ini, ref = sharded(img, K, R, T, d_min, d_int, B, V)
+        ok = True
+        if mine:
+            ok = (torch.allclose(ini, ini1[mine], rtol=1e-6, atol=0)
+                  and torch.allclose(ref, ref1[mine], rtol=1e-5, atol=1e-3))
+        else:
+            ok = ini is None and ref is None
+        # inference-only: autograd enabled or train-mode BN must raise, not silently diverge
+        raised = 0
+        try:
+            sharded(img, K, R, T, d_min, d_int, B, V)
+        except RuntimeError:
+            raised += 1
+        net.train()
+        try:
+            with torch.no_grad():
+                sharded(img, K, R, T, d_min, d_int, B, V)
+        except RuntimeError:
+            raised += 1
+        q.put((rank, ok, mine, raised))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(target, world, *args):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=300) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert [r[1] for r in res] == [True, True]
-    assert res[0][2] == [0, 2] and res[1][2] == [1]
+    return res
+
+
+def test_exchange_to_owners_world2():
+    res = _run(_exchange_worker, 2)
+    assert [(r[1], r[2]) for r in res] == [(True, True), (True, True)]
+    assert res[0][3] == [0, 2] and res[1][3] == [1]
+
+
+@pytest.mark.parametrize("B", [3, 1])
+def test_depth_sharded_model_world2(B):
+    res = _run(_model_worker, 2, B)
+    assert all(r[1] for r in res), res
+    assert res[0][2] == ([0, 2] if B == 3 else [0]) and res[1][2] == ([1] if B == 3 else [])
+    assert all(r[3] == 2 for r in res), res

@@ -109,11 +109,12 @@ def test_cfg1_cost_volume_golden_samples():
 
 
 def test_fused_matches_oracle_distinct_depths_and_views():
-    """Oracle (reference op sequence) on the CPU vs the HIP path: B=3, distinct d_min/d_int."""
+    """Oracle (reference op sequence) on the CPU vs the HIP path: B=3, distinct d_min/d_int; V=9
+    and V=16 run the generic kernel (more views than the staged kernel's 8)."""
     import mvs_oracle
     from cameras import camera_batch, depth_range, features
     from mvs_amd import warp_and_assemble_cost_volume
-    for nv in (2, 3, 4, 6):
+    for nv in (2, 3, 4, 6, 9, 16):
         B, C, h, w, D = 3, 12, 20, 36, 7
         K, R, T = camera_batch(B, nv, h, w, first_sample=5)
         d_min, d_int = depth_range(B, d_int=30.0, distinct=True)
@@ -155,13 +156,15 @@ def test_full_size_properties():
     Ks, Rs, Ts = K[0::V].repeat_interleave(V, 0), R[0::V].repeat_interleave(V, 0), T[0::V].repeat_interleave(V, 0)
     cvz, _, _ = warp_and_assemble_cost_volume(Ks, Rs, Ts, d_min, d_int, same, B, V, d_num=8)
     assert cvz.abs().max().item() <= 1e-10
-    # spot-check 8 planes of the big volume against the float64 law
+    # spot-check 8 planes of every sample of the big volume against the float64 law
     import mvs_oracle
-    ks = [0, 1, 17, 63, 100, 150, 190, 191]
-    for k in ks[:3]:
-        ref = mvs_oracle.cost_volume_fp64(feat[:V].cpu().numpy(), K[:V], R[:V], T[:V], d_min[:1],
-                                          d_int[:1], 1, V, D, d_begin=k, d_count=1)
-        _close(cv1[:1, :, k:k + 1], ref, atol=1e-3, rtol=1e-3, l2=1e-4)
+    fn = feat.cpu().numpy()
+    for b in range(B):
+        sl = slice(b * V, (b + 1) * V)
+        for k in (0, 1, 17, 63, 100, 150, 190, 191):
+            ref = mvs_oracle.cost_volume_fp64(fn[sl], K[sl], R[sl], T[sl], d_min[b:b + 1],
+                                              d_int[b:b + 1], 1, V, D, d_begin=k, d_count=1)
+            _close(cv1[b:b + 1, :, k:k + 1], ref, atol=1e-3, rtol=1e-3, l2=1e-4)
 
 
 def test_single_view_is_zero():
@@ -174,23 +177,114 @@ def test_single_view_is_zero():
     assert cv.abs().max().item() == 0.0
 
 
-def test_backward_matches_autograd_of_oracle():
+def _oracle_grad(K, R, T, d_min, d_int, feat, g, B, nv, D, d_begin=0, d_count=None):
+    """Autograd of the oracle's reference op sequence (fp32, the reference's own numerics)."""
     import mvs_oracle
-    from cameras import camera_batch, depth_range, features
+    fc = feat.clone().requires_grad_(True)
+    wr, _, _ = mvs_oracle.homography_warping(K, R, T, d_min, d_int, fc, B, nv, D, concat_growth=False)
+    d_count = D - d_begin if d_count is None else d_count
+    mvs_oracle.assemble_cost_volume(wr, nv)[:, :, d_begin:d_begin + d_count].backward(g)
+    return fc.grad
+
+
+def _law_grad(K, R, T, d_min, d_int, feat, g, B, nv, D, d_begin=0, d_count=None):
+    """Autograd of the float64 law (oracle/mvs_oracle.py::cost_volume_torch64)."""
+    import mvs_oracle
+    f = feat.double().clone().requires_grad_(True)
+    mvs_oracle.cost_volume_torch64(f, K, R, T, d_min, d_int, B, nv, D, d_begin=d_begin,
+                                   d_count=d_count).backward(g.double())
+    return f.grad
+
+
+def _gpu_grad(K, R, T, d_min, d_int, feat, g, B, nv, D, **kw):
     from mvs_amd import warp_and_assemble_cost_volume
-    for nv in (3, 5):
-        B, C, h, w, D = 2, 6, 18, 24, 5
-        K, R, T = camera_batch(B, nv, h, w)
-        d_min, d_int = depth_range(B, d_int=30.0, distinct=True)
-        feat = features(B * nv, C, h, w, seed=21)
-        g = torch.from_numpy(np.random.default_rng(22).standard_normal((B, C, D, h, w), dtype=np.float32))
-        fg = feat.to(DEV).requires_grad_(True)
-        cv, _, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, fg, B, nv, d_num=D)
-        cv.backward(g.to(DEV))
-        fc = feat.clone().requires_grad_(True)
-        wr, _, _ = mvs_oracle.homography_warping(K, R, T, d_min, d_int, fc, B, nv, D, concat_growth=False)
-        mvs_oracle.assemble_cost_volume(wr, nv).backward(g)
-        _close(fg.grad, fc.grad, atol=5e-4, rtol=5e-4, l2=5e-5)
+    fg = feat.to(DEV).requires_grad_(True)
+    cv, _, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, fg, B, nv, d_num=D, **kw)
+    cv.backward(g.to(DEV))
+    return fg.grad
+
+
+def _check_grad(args, d_begin=0, d_count=None):
+    """The HIP gradient against the float64 law's gradient: relative L2 <= 3e-5 and no larger than
+    the reference fp32 gradient's (measured at config 1: 1.5e-5 against 6.3e-5), and no element
+    further from it than the reference's own fp32 gradient is (x 1.5, + 1e-5 of the largest
+    element).  The reference builds its homographies in fp32 (homography.py:40-75); its sampling
+    coordinates carry ~1e-3 px of error at 160 px, which moves gradient mass between neighbouring
+    taps (the tent function), so the fp32 reference itself is ~1e-2 relative from the law on
+    single elements at config-1 size."""
+    K, R, T, d_min, d_int, feat, g, B, nv, D = args
+    kw = {} if d_count is None else {"d_begin": d_begin, "d_count": d_count}
+    gpu = _gpu_grad(K, R, T, d_min, d_int, feat, g, B, nv, D, **kw).double().cpu()
+    ref = _oracle_grad(K, R, T, d_min, d_int, feat, g, B, nv, D, d_begin, d_count).double()
+    law = _law_grad(K, R, T, d_min, d_int, feat, g, B, nv, D, d_begin, d_count)
+    scale = law.abs().max().item()
+    e_gpu = (gpu - law).abs().max().item()
+    e_ref = (ref - law).abs().max().item()
+    rel = ((gpu - law).norm() / law.norm()).item()
+    rel_ref = ((ref - law).norm() / law.norm()).item()
+    assert rel <= 3e-5 and rel <= rel_ref, "relative L2 %g vs float64 law (reference fp32: %g)" % (rel, rel_ref)
+    assert e_gpu <= 1.5 * e_ref + 1e-5 * scale, (e_gpu, e_ref, scale)
+
+
+@pytest.mark.parametrize("nv", [2, 3, 5, 9])
+def test_backward_matches_autograd_of_oracle(nv):
+    """mvs::cost_volume_backward against torch autograd through the oracle's reference op
+    sequence (grid_sample backward + variance backward), distinct depths per sample; V=9 runs the
+    generic (> 8 views) kernel."""
+    from cameras import camera_batch, depth_range, features
+    B, C, h, w, D = 2, 6, 18, 24, 5
+    K, R, T = camera_batch(B, nv, h, w)
+    d_min, d_int = depth_range(B, d_int=30.0, distinct=True)
+    feat = features(B * nv, C, h, w, seed=21)
+    g = torch.from_numpy(np.random.default_rng(22).standard_normal((B, C, D, h, w), dtype=np.float32))
+    _close(_gpu_grad(K, R, T, d_min, d_int, feat, g, B, nv, D),
+           _oracle_grad(K, R, T, d_min, d_int, feat, g, B, nv, D), atol=5e-4, rtol=5e-4, l2=5e-5)
+    _check_grad((K, R, T, d_min, d_int, feat, g, B, nv, D))
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 32, 128, 160, 48), (2, 5, 8, 64, 80, 40), (1, 3, 7, 37, 53, 70)])
+def test_backward_config_sizes(shape):
+    """Backward at config-1 size (B=1, V=3, C=32, 128x160, D=48: 2 plane groups of 32), V=5, and a
+    ragged geometry (C not a multiple of 4, tiles cut by the image border, a partial plane group)
+    against the float64 law's gradient and the oracle's fp32 autograd (_check_grad)."""
+    from cameras import camera_batch, depth_range, features
+    B, nv, C, h, w, D = shape
+    K, R, T = camera_batch(B, nv, h, w)
+    d_min, d_int = depth_range(B)
+    feat = features(B * nv, C, h, w, seed=sum(shape))
+    g = torch.from_numpy(np.random.default_rng(7).standard_normal((B, C, D, h, w), dtype=np.float32))
+    _check_grad((K, R, T, d_min, d_int, feat, g, B, nv, D))
+
+
+def test_backward_over_budget_footprints_and_shards():
+    """A zoomed-out source camera (footprints of one plane beyond the LDS budget: taps go straight
+    to the global accumulators) and a depth shard (d_begin > 0)."""
+    from cameras import camera_batch, depth_range, features
+    B, nv, C, h, w, D = 2, 3, 8, 128, 160, 16
+    K, R, T = camera_batch(B, nv, h, w)
+    K[2::3, :2, :] *= 0.2
+    d_min, d_int = depth_range(B, d_int=4.0)
+    feat = features(B * nv, C, h, w, seed=8)
+    g = torch.from_numpy(np.random.default_rng(9).standard_normal((B, C, D, h, w), dtype=np.float32))
+    _check_grad((K, R, T, d_min, d_int, feat, g, B, nv, D))
+    _check_grad((K, R, T, d_min, d_int, feat, g[:, :, 8:].contiguous(), B, nv, D), d_begin=8, d_count=8)
+
+
+def test_backward_is_deterministic_at_cfg2():
+    """BASELINE cfg 2 (B=4, V=3, C=32, 128x160, D=192): two backward runs are bit-identical (64-bit
+    fixed-point accumulation), and the gradient of sum(cv * g) is linear in g."""
+    from cameras import camera_batch, depth_range, features
+    B, nv, C, h, w, D = 4, 3, 32, 128, 160, 192
+    K, R, T = camera_batch(B, nv, h, w)
+    d_min, d_int = depth_range(B)
+    feat = features(B * nv, C, h, w, seed=12)
+    g = torch.randn(B, C, D, h, w, generator=torch.Generator().manual_seed(13)).to(DEV)
+    a = _gpu_grad(K, R, T, d_min, d_int, feat, g, B, nv, D)
+    b = _gpu_grad(K, R, T, d_min, d_int, feat, g, B, nv, D)
+    assert torch.equal(a, b)
+    assert torch.isfinite(a).all() and a.abs().max() > 0
+    c = _gpu_grad(K, R, T, d_min, d_int, feat, 2.0 * g, B, nv, D)
+    torch.testing.assert_close(c, 2.0 * a, rtol=1e-5, atol=1e-6)
 
 
 def test_soft_argmin_matches_golden():

@@ -23,7 +23,7 @@ def _declared():
 def test_header_declares_the_abi():
     names = _declared()
     assert "mvs_cost_volume_fwd" in names and "mvs_cost_volume_bwd" in names
-    assert len(names) == 16, names
+    assert len(names) == 17, names
 
 
 def test_library_exports_every_declared_symbol():
@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from mvs_amd import _lib
     lib = _lib.load()
-    assert lib.mvs_abi_version() == _lib.ABI_VERSION == 1
+    assert lib.mvs_abi_version() == _lib.ABI_VERSION == 2
     assert lib.mvs_status_string(0) == b"ok"
     assert lib.mvs_status_string(-2).startswith(b"n_views")
     assert lib.mvs_sampling_workspace_bytes(12, 192) == 12 * 192 * 9 * 4
@@ -63,7 +63,20 @@ def test_invalid_arguments_rejected_before_any_launch():
     # per-image index space
     assert lib.mvs_cost_volume_fwd(fake, fake, fake, fake, fake, fake, 1, 3, 70000, 128, 256, 0, 4,
                                    25.0, fake, fake, null) == -3
+    # 32-bit buffer descriptors of the packed kernels: C=4 with hw = 2^28 passes the per-image
+    # element bound (C*hw < 2^31) but not the descriptor byte counts
+    assert lib.mvs_cost_volume_fwd(fake, fake, fake, fake, fake, fake, 1, 3, 4, 16384, 16384, 0, 4,
+                                   25.0, fake, fake, null) == -3
+    # 8 views of 32 channels at 2048x2048 features: 8 * 8 * 2050 * 2050 * 16 B > 2^31
+    assert lib.mvs_cost_volume_fwd(fake, fake, fake, fake, fake, fake, 1, 8, 32, 2048, 2048, 0, 4,
+                                   25.0, fake, fake, null) == -3
     assert lib.mvs_extract_depth_map_fwd(fake, fake, 1, 48, 8, 8, 0, fake, null) == -1
+    # backward: missing backward workspace (needed for n_views > 1), bad geometry
+    assert lib.mvs_cost_volume_bwd(fake, fake, fake, 1, 3, 32, 128, 160, 48, null, fake, null) == -1
+    assert lib.mvs_cost_volume_bwd(fake, fake, fake, 1, 17, 32, 128, 160, 48, fake, fake, null) == -2
+    assert lib.mvs_cost_volume_bwd_workspace_bytes(1, 3, 32, 128, 160, 0) == 0
+    # 64-bit accumulators for every feature element + reference-view partials + scalars
+    assert lib.mvs_cost_volume_bwd_workspace_bytes(4, 3, 32, 128, 160, 192) >= 12 * 32 * 128 * 160 * 8
 
 
 def test_build_is_gfx950_in_tree():

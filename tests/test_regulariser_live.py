@@ -71,3 +71,13 @@ def test_live_region_gradients_match():
         grads.append((x.grad.clone(), m.conv_3_1.weight.grad.clone(), m.deconv_1_0.weight.grad.clone()))
     for a, b in zip(*grads):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-8)
+
+
+def test_live_region_needs_matching_geometry():
+    """A regulariser built for one geometry and run on another takes forward_full, which raises
+    the reference's shape mismatch instead of returning wrongly indexed live regions."""
+    m = _reg(8, 12, 16).eval()
+    cv = torch.rand(1, 32, 10, 12, 16)
+    assert not m._live_geometry_ok(cv)
+    with torch.no_grad(), pytest.raises(RuntimeError):
+        m(cv)

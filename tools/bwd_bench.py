@@ -1,7 +1,7 @@
-"""Time the fused cost-volume op's backward (mvs::cost_volume_backward: recompute + atomic scatter
+"""Time the fused cost-volume op's backward (mvs::cost_volume_backward: recompute + fixed-point scatter
 into grad_feat) beside its forward, through torch autograd, at BASELINE configs.
 
-Usage: python tools/bwd_bench.py [cfg ...]   (cfg in 1, 2; default both)
+Usage: python tools/bwd_bench.py [cfg ...]   (cfg in 1, 2, 3; default all)
 """
 import json
 import os
@@ -14,7 +14,7 @@ import torch  # noqa: E402
 from cameras import camera_batch, depth_range  # noqa: E402
 from mvs_amd import warp_and_assemble_cost_volume  # noqa: E402
 
-CFGS = {"1": (1, 3, 128, 160, 48), "2": (4, 3, 128, 160, 192)}
+CFGS = {"1": (1, 3, 128, 160, 48), "2": (4, 3, 128, 160, 192), "3": (8, 5, 128, 160, 192)}
 
 
 def main():
