@@ -190,32 +190,53 @@ def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=F
 
 
 def time_backward(B, V, C, h, w, D, device, iters=5):
-    """Fused cost-volume op forward and backward (mvs::cost_volume_backward) through autograd,
-    HIP events on the current stream; ms per call."""
-    from mvs_amd import warp_and_assemble_cost_volume
+    """The fused op's backward (mvs::cost_volume_backward, SURVEY.md §8 f1), called directly after
+    one forward, HIP events on the current stream: ms per call in the default mode (fp64 on-chip
+    partial sums, fp32 global atomics) and the deterministic mode (64-bit fixed point)."""
+    from mvs_amd import ops
     K, R, T = camera_batch(B, V, h, w)
     d_min, d_int = depth_range(B)
     g = torch.Generator(device="cpu").manual_seed(3)
-    feat = torch.randn(B * V, C, h, w, generator=g).to(device).requires_grad_(True)
+    feat = torch.randn(B * V, C, h, w, generator=g).to(device)
     gcv = torch.randn(B, C, D, h, w, generator=g).to(device)
-    fwd = lambda: warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feat, B, V, d_num=D)[0]
-    fwd().backward(gcv)
-    torch.cuda.synchronize()
-    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    tf = tb = 0.0
-    for _ in range(iters):
-        feat.grad = None
-        e[0].record()
-        cv = fwd()
-        e[1].record()
-        cv.backward(gcv)
-        e[2].record()
+    _, ws = ops.cost_volume(feat, K, R, T, d_min, d_int, B, V, 0, D, 25.0)
+    out = {}
+    for det in (False, True):
+        ops.cost_volume_backward(feat, ws, gcv, B, V, D, det)
         torch.cuda.synchronize()
-        tf += e[0].elapsed_time(e[1])
-        tb += e[1].elapsed_time(e[2])
-    del cv, gcv, feat
-    return {"fwd_ms": tf / iters, "bwd_ms": tb / iters,
-            "kernel": "cost_volume_bwd_kernel (recompute + 64-bit fixed-point LDS footprint accumulation, deterministic)"}
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            ops.cost_volume_backward(feat, ws, gcv, B, V, D, det)
+        e1.record()
+        torch.cuda.synchronize()
+        out["deterministic_ms" if det else "bwd_ms"] = e0.elapsed_time(e1) / iters
+    # 2 GB of grad_cv read once + features read + gradient written: the HBM floor of the op
+    alg = 4.0 * B * C * D * h * w + 8.0 * B * V * C * h * w
+    out.update({"alg_bytes": alg, "hbm_floor_ms": alg / (HBM_PEAK_GBS * 1e9) * 1e3,
+                "kernel": "cost_volume_bwd_kernel (recompute + LDS footprint accumulation: fp64 "
+                          "default / 64-bit fixed point deterministic) + ref_scatter_kernel"})
+    del feat, gcv, ws
+    return out
+
+
+KERNEL_CFGS = {   # BASELINE.json configs[2..4]: (B, V, h, w, D, d_count)
+    "cfg3": (8, 5, 128, 160, 192, 192),
+    "cfg4_shard": (1, 3, 128, 160, 256, 32),
+    "cfg5": (1, 3, 296, 400, 256, 256),
+}
+
+
+def kernel_configs(device, iters):
+    """Main fused kernel at the other BASELINE configs (live HIP events, as the roofline)."""
+    out = {}
+    for name, (B, V, h, w, D, dc) in KERNEL_CFGS.items():
+        k_ms, op_ms, alg = time_kernel(B, V, 32, h, w, D, device, iters, D - dc, dc)
+        gbs = alg / (k_ms * 1e-3) / 1e9
+        out[name] = {"B": B, "V": V, "feature_hw": [h, w], "planes": dc, "kernel_ms": k_ms, "op_ms": op_ms,
+                     "alg_bytes": alg, "GBps": gbs, "frac": gbs / HBM_PEAK_GBS}
+        torch.cuda.empty_cache()
+    return out
 
 
 def load_traffic(tag):
@@ -370,6 +391,25 @@ def main():
                           "value": (B * world if args.mode == "samples" else B) * full_steps / dtf,
                           "steps": full_steps}
         log("full-volume regulariser: %.2f ms/step" % result["full"]["ms_per_step"])
+        # test.py:53,61: the reference's test driver runs the model in TRAIN mode under no_grad
+        # (BatchNorm normalises with batch statistics over the whole volume, so the eval-mode
+        # live-region shortcut does not apply): timed as its own field
+        if args.mode == "samples":
+            net.cost_volume_reg.live_region = True
+            net.train()
+            train_steps = max(1, min(args.steps, 3))
+            with torch.no_grad():
+                step()
+                barrier(world)
+                t0 = time.perf_counter()
+                for _ in range(train_steps):
+                    step()
+                barrier(world)
+                dtt = time.perf_counter() - t0
+            dtt = max_over_ranks(dtt, world, device)
+            result["train_bn"] = {"ms_per_step": 1000.0 * dtt / train_steps,
+                                  "value": B * world * train_steps / dtt, "steps": train_steps}
+            log("train-mode BN step (test.py:61): %.2f ms/step" % result["train_bn"]["ms_per_step"])
         del net
 
     # fused kernel timing (this rank's share of planes in dshard mode)
@@ -398,8 +438,11 @@ def main():
         "scaling": "weak" if args.mode == "samples" else "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic N(0,1) images resident in HBM, real DTU scan-1 cameras, random-init weights",
-        "config": {"workload": "cfg%d: %d-view %dx%d D=%d batch=%d per %s" % (
+        "data": "synthetic N(0,1) images resident in HBM, real DTU scan-1 cameras, random-init "
+                "weights; BN eval mode, live-region regulariser (train-mode BN as in test.py:61: "
+                "field train_bn)",
+        "config": {"workload": "cfg%d: %d-view %dx%d D=%d batch=%d per %s, BN eval, live-region "
+                               "regulariser" % (
                        2 if args.mode == "samples" else 4, V, W, H, D, B,
                        "GPU" if args.mode == "samples" else "job (D sharded)"),
                    "global_batch": B * (world if args.mode == "samples" else 1),
@@ -418,10 +461,19 @@ def main():
     if "full" in result:
         out["full_volume_regulariser"] = dict(result["full"], unit="depth maps/s", note=(
             "same step with CostVolumeReg.forward_full (every voxel of every level, as "
-            "model.py:100-126 computes it); value uses forward_live (eval BN: only the regions "
-            "whose values reach the output; same sums, fp32 summation order may differ)"))
-    # backward of the fused op (train.py:103): informational, through autograd
+            "model.py:100-126 computes it: MIOpen, HIP conv_0_0/conv_out); value uses forward_live "
+            "(eval BN: only the regions whose values reach the output; same sums, fp32 summation "
+            "order may differ)"))
+    if "train_bn" in result:
+        out["train_bn"] = dict(result["train_bn"], unit="depth maps/s", note=(
+            "test.py:53,61 mode: model.train() under no_grad, BatchNorm batch statistics over the "
+            "whole volume (forward_full)"))
+    # backward of the fused op (train.py:103): informational
+    log("timing the backward")
     out["cost_volume_backward"] = time_backward(B, V, C, h, w, d_count, device)
+    if args.mode == "samples":
+        log("timing the fused kernel at cfg 3/4/5")
+        out["kernel_configs"] = kernel_configs(device, max(5, args.kernel_iters // 2))
     # opt-in bf16 cost volume: informational, not the headline (reduced precision)
     _, bf_op_ms, bf_alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count, bf16=True)
     out["bf16_cv_opt_in"] = {"op_ms": bf_op_ms, "alg_bytes_per_launch": bf_alg,

@@ -171,14 +171,15 @@ size_t mvs_cost_volume_bwd_workspace_bytes(int batch_size, int n_views, int chan
 
 int mvs_cost_volume_bwd(const float* feat, const float* workspace, const float* grad_cv,
                         int batch_size, int n_views, int channels, int h, int w, int d_count,
-                        void* bwd_workspace, float* grad_feat, void* stream) {
+                        int flags, void* bwd_workspace, float* grad_feat, void* stream) {
   if (!feat || !workspace || !grad_cv || !grad_feat || (n_views > 1 && !bwd_workspace))
     return MVS_ERR_INVALID_ARGUMENT;
+  if (flags & ~MVS_BWD_DETERMINISTIC) return MVS_ERR_INVALID_ARGUMENT;
   Geometry g;
   const int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g);
   if (st != MVS_OK) return st;
   return mvs::launch_cost_volume_bwd(g, feat, workspace, grad_cv, bwd_workspace, grad_feat,
-                                     (hipStream_t)stream);
+                                     (flags & MVS_BWD_DETERMINISTIC) != 0, (hipStream_t)stream);
 }
 
 int mvs_extract_depth_map_fwd(const float* prob, const float* d_batch, int batch_size, int d,

@@ -117,6 +117,19 @@ __device__ inline float gather(const float* __restrict__ plane, const Taps& tp) 
 // ------------------------------------------------------------------------------------------
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 
+// Workgroup-uniform values the compiler cannot prove uniform (derived from LDS loads, or computed
+// in VALU): readfirstlane moves them to SGPRs, so descriptors built from them need no waterfall
+// loop and branches on them are scalar.
+__device__ inline int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+template <typename T>
+__device__ inline T* uniform_ptr(T* p) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
+
 __device__ inline Rsrc make_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
                                            0x00020000);

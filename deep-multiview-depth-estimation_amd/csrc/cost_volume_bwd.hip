@@ -5,32 +5,37 @@
 // train.py:103 exercises it.  No warped volume is stored: the samples are recomputed from the
 // forward's packed features (packed.h), exactly as the forward computed them.
 //
-// Accumulation is in 64-bit FIXED POINT: every contribution v is added as llrint(v * 2^S), with
-// one shift S per launch derived on the device from max|grad_cv| and max|feat| so that no gradient
-// element can exceed 2^62 (bound: d_count * h * w contributions of at most 4 max|g| max|feat| / V
-// each).  Integer addition is associative, so the result is bit-identical whatever the order in
-// which workgroups and lanes add -- the backward is deterministic -- and integer LDS atomics run
-// at ~25x the rate of fp32 ones on gfx950 (tools/microbench/atomic_patterns.hip: ds_add_u64 5.1 T
-// lanes/s, ds_add_f32 0.20 T).  Resolution: 2^-S = d_count*h*w*4*max|g|*max|feat|/V * 2^-61, i.e.
-// about 1e-12 of the largest possible contribution at BASELINE cfg 2.
+// LDS accumulation never uses fp32 atomics: on gfx950 ds_add_f32 runs at 0.20 T lanes/s against
+// 4.3 T for ds_add_f64 and 5.1 T for ds_add_u64 (tools/microbench/atomic_patterns.hip).  Two modes:
+//   default        footprint images in fp64 LDS (each contribution an fp32 product widened once),
+//                  flushed with fp32 global atomics (summation order varies, like torch's
+//                  grid_sample backward on GPU);
+//   deterministic  (MVS_BWD_DETERMINISTIC; torch.use_deterministic_algorithms) 64-bit FIXED POINT
+//                  everywhere: every contribution v is added as llrint(v * 2^S), with one shift S
+//                  per launch derived on the device from max|grad_cv| and max|feat| so that no
+//                  gradient element can exceed 2^62 (bound: d_count * h * w contributions of at most
+//                  4 max|g| max|feat| / V each).  Integer addition is associative, so the result is
+//                  bit-identical whatever the order in which workgroups and lanes add.  Resolution:
+//                  2^-S = d_count*h*w*8*max|g|*max|feat|/V * 2^-61, about 1e-12 of the largest
+//                  possible contribution at BASELINE cfg 2.
 //
 // Kernels (V = 2..8 views):
-//   abs_max_kernel        max|grad_cv|, max|feat| (device scalars, order-independent atomicMax)
+//   abs_max_kernel        (deterministic) max|grad_cv|, max|feat| (device scalars, atomicMax)
 //   cost_volume_bwd_kernel  a 256-thread workgroup owns a 32 x 8 pixel tile of one sample, a
 //                         group of 32 planes and one 4-channel chunk.  Per plane, every thread
 //                         recomputes its pixel's samples of all views (packed float4 gathers),
 //                         forms the per-view coefficients 2/V g (x_v - mean), keeps the reference
 //                         view's sum over planes in registers (its taps do not depend on the
 //                         plane), and adds each source view's 4 tap contributions into an LDS
-//                         image of the tile's footprint (ds_add_u64).  Footprints come from the
+//                         image of the tile's footprint (ds_add_f64 / ds_add_u64).  Footprints: the
 //                         tile's 4 corners per (plane, view) (a homography maps the tile to a
 //                         convex quad); consecutive planes share one LDS image while the union
-//                         fits the budget, which is then flushed with one 64-bit global atomic
+//                         fits the budget, which is then flushed with one global atomic
 //                         per slot and channel.  Taps outside the image box (rounding) or a plane
 //                         whose footprint alone exceeds the budget go straight to global atomics.
 //   ref_scatter_kernel    sums the reference view's per-group partials in a fixed order and
 //                         scatters them to its (plane-independent) taps
-//   fixed_to_float_kernel grad_feat = acc * 2^-S
+//   fixed_to_float_kernel (deterministic) grad_feat = acc * 2^-S
 // More than 8 views: one thread per (sample, plane, pixel) with NCHW gathers and global atomics.
 #include "launchers.h"
 #include "packed.h"
@@ -96,7 +101,8 @@ __global__ __launch_bounds__(kBlock) void abs_max_kernel(const float* __restrict
 // Box of the in-image taps of a tile for one (plane, view), from the tile's 4 corner pixels: with
 // the homogeneous coordinate s of one sign and |s| > 1e-8 at the corners (s is affine in the pixel,
 // so then everywhere in the tile) the tile maps to a convex quad whose bounding box is the corners'
-// bounding box; one slot of margin each side absorbs fp32 rounding.  Otherwise: the whole image.
+// bounding box (taps x0 .. x0 + 1).  A tap that fp32 rounding of an interior pixel puts just
+// outside goes straight to the global accumulators.  Otherwise (pole in the tile): the whole image.
 struct Box {
   int x0, y0, x1, y1;   // inclusive, clipped to the image; x1 < x0 = empty
 };
@@ -136,22 +142,39 @@ __device__ Box tile_box(const float* __restrict__ G, int px0, int py0, int px1, 
   }
   if (bad || (pos && neg)) return Box{0, 0, w - 1, h - 1};
   Box b;
-  b.x0 = max((int)floorf(mnx) - 1, 0);
-  b.y0 = max((int)floorf(mny) - 1, 0);
-  b.x1 = min((int)floorf(mxx) + 2, w - 1);
-  b.y1 = min((int)floorf(mxy) + 2, h - 1);
+  b.x0 = max((int)floorf(mnx), 0);
+  b.y0 = max((int)floorf(mny), 0);
+  b.x1 = min((int)floorf(mxx) + 1, w - 1);
+  b.y1 = min((int)floorf(mxy) + 1, h - 1);
   return b;
 }
 
 // ---- main kernel (2 <= V <= 8) -----------------------------------------------------------------
-template <int V>
+// DET = false (default): the LDS footprint images accumulate in fp64 (ds_add_f64, ~4.3 T lanes/s;
+// each contribution is an exact fp32 product widened once) and are flushed to grad_feat with fp32
+// global atomics.  DET = true: 64-bit fixed point in LDS and in the global accumulators (see top).
+template <bool DET>
+struct Acc;
+template <>
+struct Acc<false> {
+  typedef double lds_t;
+  __device__ static lds_t conv(float v, float) { return (double)v; }
+};
+template <>
+struct Acc<true> {
+  typedef u64 lds_t;
+  __device__ static lds_t conv(float v, float sc) { return to_fixed(v, sc); }
+};
+
+template <int V, bool DET>
 __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
     const float4* __restrict__ packed, const float4* __restrict__ refs,
     const float* __restrict__ sampling, const float* __restrict__ grad_cv, u64* __restrict__ acc,
-    float4* __restrict__ ref_part, const unsigned* __restrict__ mx, int B, int C, int h, int w,
-    int Dc, int tiles_x, int tiles_y, int groups, int total) {
+    float* __restrict__ grad_feat, float4* __restrict__ ref_part, const unsigned* __restrict__ mx, int B,
+    int C, int h, int w, int Dc, int tiles_x, int tiles_y, int groups, int total) {
   constexpr int NS = V - 1;
-  __shared__ u64 lds[4 * kBwdSlots];
+  typedef typename Acc<DET>::lds_t lds_t;
+  __shared__ lds_t lds[4 * kBwdSlots];
   __shared__ Box boxes[kBwdKPG][NS];
 
   const int wk = xcd_work_id(blockIdx.x, total);
@@ -170,7 +193,7 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
   const int npl = min(kBwdKPG, Dc - k0);
   const uint32_t hw = (uint32_t)h * (uint32_t)w;
   const PadGeom pg = pad_geom(h, w);
-  const Fixed fx = fixed_scale(mx, V, Dc, hw);
+  const float sc = DET ? fixed_scale(mx, V, Dc, hw).to_fixed : 1.0f;
 
   // footprint box of every (plane, view): one (plane, view) per thread
   if ((int)threadIdx.x < npl * NS) {
@@ -185,31 +208,50 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
   const f4v x0 = {r4.x, r4.y, r4.z, r4.w};
   const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
   const f4v two_inv_v = inv_v + inv_v;
-  Rsrc rs[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s)
-    rs[s] = make_rsrc(packed + (size_t)(b * V + 1 + s) * c4 * pg.plane, (uint32_t)c4 * pg.plane * 16u);
   const int soff = (int)((uint32_t)ch * pg.plane * 16u);
   const int row_bytes = pg.pitch * 16;
   // grad_cv of channel 4 ch + j, plane k0 + pl at this pixel: gcv + j * cstride + pl * hw
   const size_t cstride = (size_t)Dc * hw;
   const float* gcv = grad_cv + (((size_t)b * C + (size_t)ch * 4) * Dc + k0) * hw + pix;
-  int nch = C - ch * 4;
-  nch = nch > 4 ? 4 : nch;
-  // accumulator planes of this chunk: acc + ((n * C + 4 ch + j) * hw) for image n
-  auto acc_at = [&](int n, int j, int yy, int xx) -> u64* {
-    return acc + ((size_t)n * C + (size_t)ch * 4 + j) * hw + (size_t)yy * w + xx;
+  const int nch = min(C - ch * 4, 4);
+  // per-image planes of this chunk's channels (global accumulators / gradient)
+  auto gidx = [&](int n, int j, int yy, int xx) -> size_t {
+    return ((size_t)n * C + (size_t)ch * 4 + j) * hw + (size_t)yy * w + xx;
+  };
+  auto gadd_out = [&](int n, int j, int yy, int xx, lds_t v) {
+    if constexpr (DET) gadd(acc + gidx(n, j, yy, xx), v);
+    else unsafeAtomicAdd(grad_feat + gidx(n, j, yy, xx), (float)v);
   };
   f4v racc = {0.0f, 0.0f, 0.0f, 0.0f};
   __syncthreads();   // boxes
 
+  // view subsets: consecutive source views whose largest single-plane footprints fit the budget
+  // together (all views at once unless the views are many or the footprints large); every subset
+  // recomputes the samples, the reference view's sum is kept in the first subset's passes only
+  int amax[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    int m = 0;
+    for (int pl = 0; pl < npl; ++pl) m = max(m, box_area(boxes[pl][s]));
+    amax[s] = uniform(m);
+  }
+  for (int s0 = 0; s0 < NS;) {
+    int s1 = s0 + 1, sub_area = amax[s0];
+#pragma unroll
+    for (int s = 1; s < NS; ++s)
+      if (s == s1 && s1 < NS && sub_area + amax[s] <= kBwdSlots) {
+        sub_area += amax[s];
+        ++s1;
+      }
   for (int kp = 0; kp < npl;) {
-    // ---- plan a pass: consecutive planes whose union footprint fits the LDS budget ----
+    // ---- plan a pass: consecutive planes whose union footprint fits the LDS budget (uniform) ----
     Box ub[NS];
     int area = 0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      ub[s] = boxes[kp][s];
+      const Box bx = boxes[kp][s];
+      ub[s] = (s >= s0 && s < s1) ? Box{uniform(bx.x0), uniform(bx.y0), uniform(bx.x1), uniform(bx.y1)}
+                                  : Box{0, 0, -1, -1};
       area += box_area(ub[s]);
     }
     int ke = kp + 1;
@@ -219,7 +261,10 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
         int na = 0;
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-          nb[s] = box_union(ub[s], boxes[ke][s]);
+          const Box bx = boxes[ke][s];
+          nb[s] = (s >= s0 && s < s1)
+                      ? box_union(ub[s], Box{uniform(bx.x0), uniform(bx.y0), uniform(bx.x1), uniform(bx.y1)})
+                      : ub[s];
           na += box_area(nb[s]);
         }
         if (na > kBwdSlots) break;
@@ -241,54 +286,56 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
       }
     }
     if (use_lds) {
-      for (int q = (int)threadIdx.x; q < 4 * T; q += kBlock) lds[q] = 0ull;
+      for (int q = (int)threadIdx.x; q < 4 * T; q += kBlock) lds[q] = (lds_t)0;
       __syncthreads();
     }
 
-    // ---- the pass's planes ----
-    if (active) {
-      for (int pl = kp; pl < ke; ++pl) {
-        const int kk = k0 + pl;
-        f4v g = {0.0f, 0.0f, 0.0f, 0.0f};
+    // ---- the pass's planes (every lane runs them; inactive lanes have g = 0 and no taps) ----
+    for (int pl = kp; pl < ke; ++pl) {
+      const int kk = k0 + pl;
+      f4v g = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (active) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (j < nch) g[j] = gcv[(size_t)j * cstride + (size_t)pl * hw];
-        uint32_t pos[NS];
-        float wx[NS], wy[NS];
-        f4v xs[NS];
-        f4v sum = x0;
+      }
+      uint32_t pos[NS];
+      float wx[NS], wy[NS];
+      f4v xs[NS];
+      f4v sum = x0;
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + kk) * 9, xn, yn, h, w, true, pos[s],
-                     wx[s], wy[s]);
-          f4v tp[4];
-          load_taps(rs[s], tap_offset(pos[s], pg), soff, row_bytes, tp);
-          xs[s] = bilerp(tp, wx[s], wy[s]);
-          sum += xs[s];
-        }
-        const f4v nmean = -(sum * inv_v);
-        const f4v k2 = two_inv_v * g;
-        racc += k2 * (x0 + nmean);
+      for (int s = 0; s < NS; ++s) {
+        src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + kk) * 9, xn, yn, h, w, active, pos[s],
+                   wx[s], wy[s]);
+        const Rsrc rs = make_rsrc(uniform_ptr(packed + (size_t)(b * V + 1 + s) * c4 * pg.plane),
+                                  (uint32_t)c4 * pg.plane * 16u);
+        f4v tp[4];
+        load_taps(rs, tap_offset(pos[s], pg), soff, row_bytes, tp);
+        xs[s] = bilerp(tp, wx[s], wy[s]);
+        sum += xs[s];
+      }
+      const f4v nmean = -(sum * inv_v);
+      const f4v k2 = two_inv_v * g;
+      if (s0 == 0) racc += k2 * (x0 + nmean);
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          if (pos[s] == kInvalidTap) continue;
-          const f4v cs = k2 * (xs[s] + nmean);
-          const float ex = 1.0f - wx[s], ny = 1.0f - wy[s];
-          const float wt[4] = {ny * ex, ny * wx[s], wy[s] * ex, wy[s] * wx[s]};
-          const int cx = pos_x(pos[s]), cy = pos_y(pos[s]);
+      for (int s = 0; s < NS; ++s) {
+        if (s < s0 || s >= s1 || pos[s] == kInvalidTap) continue;
+        const f4v cs = k2 * (xs[s] + nmean);
+        const float ex = 1.0f - wx[s], ny = 1.0f - wy[s];
+        const float wt[4] = {ny * ex, ny * wx[s], wy[s] * ex, wy[s] * wx[s]};
+        const int cx = pos_x(pos[s]), cy = pos_y(pos[s]);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int xx = cx + (q & 1), yy = cy + (q >> 1);
-            if (xx < 0 || xx >= w || yy < 0 || yy >= h) continue;   // zero padding: no gradient
-            const bool in_box = use_lds && xx >= ub[s].x0 && xx <= ub[s].x1 && yy >= ub[s].y0 && yy <= ub[s].y1;
-            const int slot = base[s] + (yy - ub[s].y0) * bw[s] + (xx - ub[s].x0);
+        for (int q = 0; q < 4; ++q) {
+          const int xx = cx + (q & 1), yy = cy + (q >> 1);
+          if (xx < 0 || xx >= w || yy < 0 || yy >= h) continue;   // zero padding: no gradient
+          const bool in_box = use_lds && xx >= ub[s].x0 && xx <= ub[s].x1 && yy >= ub[s].y0 && yy <= ub[s].y1;
+          const int slot = base[s] + (yy - ub[s].y0) * bw[s] + (xx - ub[s].x0);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              if (j >= nch) break;
-              const u64 v = to_fixed(wt[q] * cs[j], fx.to_fixed);
-              if (in_box) atomicAdd(&lds[j * T + slot], v);
-              else gadd(acc_at(b * V + 1 + s, j, yy, xx), v);
-            }
+          for (int j = 0; j < 4; ++j) {
+            if (j >= nch) break;
+            const lds_t v = Acc<DET>::conv(wt[q] * cs[j], sc);
+            if (in_box) atomicAdd(&lds[j * T + slot], v);
+            else gadd_out(b * V + 1 + s, j, yy, xx, v);
           }
         }
       }
@@ -315,22 +362,25 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (j >= nch) break;
-          const u64 v = lds[j * T + e];
-          if (v) gadd(acc_at(b * V + 1 + s, j, by + r, bx + c), v);
+          const lds_t v = lds[j * T + e];
+          if (v != (lds_t)0) gadd_out(b * V + 1 + s, j, by + r, bx + c, v);
         }
       }
       __syncthreads();   // the next pass re-zeroes the image
     }
     kp = ke;
   }
+    s0 = s1;
+  }
   if (active) ref_part[(((size_t)grp * B + b) * c4 + ch) * hw + pix] = make_float4(racc.x, racc.y, racc.z, racc.w);
 }
 
 // Reference view: S = sum over plane groups of the partials (fixed order), scattered to the
 // reference view's plane-independent taps (its sampling matrix, plane 0 of the shard).
+template <bool DET>
 __global__ __launch_bounds__(kBlock) void ref_scatter_kernel(const float4* __restrict__ ref_part,
                                                             const float* __restrict__ sampling,
-                                                            u64* __restrict__ acc,
+                                                            u64* __restrict__ acc, float* __restrict__ grad_feat,
                                                             const unsigned* __restrict__ mx, int B,
                                                             int V, int C, int h, int w, int Dc,
                                                             int groups) {
@@ -340,7 +390,7 @@ __global__ __launch_bounds__(kBlock) void ref_scatter_kernel(const float4* __res
   const int ch = (int)blockIdx.y % c4;
   const int b = (int)blockIdx.y / c4;
   if (p >= hw) return;
-  const Fixed fx = fixed_scale(mx, V, Dc, hw);
+  const float sc = DET ? fixed_scale(mx, V, Dc, hw).to_fixed : 1.0f;
   f4v S = {0.0f, 0.0f, 0.0f, 0.0f};
   for (int g = 0; g < groups; ++g) {
     const float4 v = ref_part[(((size_t)g * B + b) * c4 + ch) * hw + p];
@@ -363,24 +413,27 @@ __global__ __launch_bounds__(kBlock) void ref_scatter_kernel(const float4* __res
     for (int j = 0; j < 4; ++j) {
       const int c = ch * 4 + j;
       if (c >= C) break;
-      gadd(acc + ((size_t)(b * V) * C + c) * hw + (size_t)yy * w + xx, to_fixed(wt[q] * S[j], fx.to_fixed));
+      const size_t o = ((size_t)(b * V) * C + c) * hw + (size_t)yy * w + xx;
+      if constexpr (DET) gadd(acc + o, to_fixed(wt[q] * S[j], sc));
+      else unsafeAtomicAdd(grad_feat + o, wt[q] * S[j]);
     }
   }
 }
 
 // More than 8 views (no packed workspace): one thread per (sample, plane, pixel), NCHW gathers,
 // every view's taps straight to the global accumulators.
+template <bool DET>
 __global__ __launch_bounds__(kBlock) void cost_volume_bwd_generic_kernel(
     const float* __restrict__ feat, const float* __restrict__ sampling,
-    const float* __restrict__ grad_cv, u64* __restrict__ acc, const unsigned* __restrict__ mx,
-    int V, int C, int h, int w, int Dc, int tiles, int total) {
+    const float* __restrict__ grad_cv, u64* __restrict__ acc, float* __restrict__ grad_feat,
+    const unsigned* __restrict__ mx, int V, int C, int h, int w, int Dc, int tiles, int total) {
   const int wk = xcd_work_id(blockIdx.x, total);
   if (wk >= total) return;
   const WorkItem it = decode_flat(wk, Dc, tiles);
   const uint32_t hw = (uint32_t)h * (uint32_t)w;
   const uint32_t p = (uint32_t)it.tile * kBlock + threadIdx.x;
   if (p >= hw) return;
-  const Fixed fx = fixed_scale(mx, V, Dc, hw);
+  const float sc = DET ? fixed_scale(mx, V, Dc, hw).to_fixed : 1.0f;
   float xn, yn;
   pixel_coords(p, w, h, xn, yn);
   Taps tp[MVS_MAX_VIEWS];
@@ -399,10 +452,14 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_generic_kernel(
     const float k2 = (inv_v + inv_v) * g;
     for (int v = 0; v < V; ++v) {
       const float coef = k2 * (val[v] + nmean);
-      u64* plane = acc + ((size_t)(it.b * V + v) * C + c) * hw;
+      const size_t plane = ((size_t)(it.b * V + v) * C + c) * hw;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (tp[v].wt[q] != 0.0f) gadd(plane + tp[v].off[q] / 4u, to_fixed(tp[v].wt[q] * coef, fx.to_fixed));
+      for (int q = 0; q < 4; ++q) {
+        if (tp[v].wt[q] == 0.0f) continue;
+        const size_t o = plane + tp[v].off[q] / 4u;
+        if constexpr (DET) gadd(acc + o, to_fixed(tp[v].wt[q] * coef, sc));
+        else unsafeAtomicAdd(grad_feat + o, tp[v].wt[q] * coef);
+      }
     }
   }
 }
@@ -415,18 +472,35 @@ __global__ __launch_bounds__(kBlock) void fixed_to_float_kernel(const u64* __res
     out[i] = (float)((double)(long long)acc[i] * fx.to_float);
 }
 
-template <int V>
+template <int V, bool DET>
 void launch_main(const Geometry& g, const float4* packed, const float4* refs, const float* smp,
-                 const float* gcv, u64* acc, float4* ref_part, const unsigned* mx, hipStream_t s) {
+                 const float* gcv, u64* acc, float* grad_feat, float4* ref_part, const unsigned* mx,
+                 hipStream_t s) {
   const int tiles_x = (g.w + kBwdTW - 1) / kBwdTW, tiles_y = (g.h + kBwdTH - 1) / kBwdTH;
   const int groups = (g.Dc + kBwdKPG - 1) / kBwdKPG;
   const int c4 = (g.C + 3) / 4;
   const int total = g.B * c4 * tiles_x * tiles_y * groups;
-  hipLaunchKernelGGL((cost_volume_bwd_kernel<V>), xcd_grid(total), dim3(kBlock), 0, s, packed, refs, smp,
-                     gcv, acc, ref_part, mx, g.B, g.C, g.h, g.w, g.Dc, tiles_x, tiles_y, groups, total);
+  hipLaunchKernelGGL((cost_volume_bwd_kernel<V, DET>), xcd_grid(total), dim3(kBlock), 0, s, packed, refs, smp,
+                     gcv, acc, grad_feat, ref_part, mx, g.B, g.C, g.h, g.w, g.Dc, tiles_x, tiles_y, groups, total);
 }
 
-// backward workspace: [acc u64 N*C*hw][ref partials groups*B*C4*hw float4][2 uints max]
+template <bool DET>
+void launch_views(const Geometry& g, const float4* packed, const float4* refs, const float* smp,
+                  const float* gcv, u64* acc, float* grad_feat, float4* ref_part, const unsigned* mx,
+                  hipStream_t s) {
+  switch (g.V) {
+    case 2: launch_main<2, DET>(g, packed, refs, smp, gcv, acc, grad_feat, ref_part, mx, s); break;
+    case 3: launch_main<3, DET>(g, packed, refs, smp, gcv, acc, grad_feat, ref_part, mx, s); break;
+    case 4: launch_main<4, DET>(g, packed, refs, smp, gcv, acc, grad_feat, ref_part, mx, s); break;
+    case 5: launch_main<5, DET>(g, packed, refs, smp, gcv, acc, grad_feat, ref_part, mx, s); break;
+    case 6: launch_main<6, DET>(g, packed, refs, smp, gcv, acc, grad_feat, ref_part, mx, s); break;
+    case 7: launch_main<7, DET>(g, packed, refs, smp, gcv, acc, grad_feat, ref_part, mx, s); break;
+    default: launch_main<8, DET>(g, packed, refs, smp, gcv, acc, grad_feat, ref_part, mx, s); break;
+  }
+}
+
+// backward workspace: [acc u64 N*C*hw (deterministic mode)][ref partials groups*B*C4*hw float4]
+// [2 uints max]
 struct BwdLayout {
   size_t acc, ref_part, mx, total;
 };
@@ -449,46 +523,53 @@ size_t cost_volume_bwd_workspace_bytes(int B, int V, int C, int h, int w, int Dc
 }
 
 int launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* fwd_ws,
-                           const float* grad_cv, void* bwd_ws, float* grad_feat, hipStream_t s) {
+                           const float* grad_cv, void* bwd_ws, float* grad_feat, bool deterministic,
+                           hipStream_t s) {
   const size_t n_feat = (size_t)g.B * g.V * g.C * g.h * g.w;
-  if (g.V == 1)   // the variance of one view is identically 0: so is its gradient
-    return hipMemsetAsync(grad_feat, 0, n_feat * sizeof(float), s) == hipSuccess ? MVS_OK : MVS_ERR_HIP;
+  if (!deterministic || g.V == 1)   // V == 1: the variance of one view is identically 0, so is its gradient
+    if (hipMemsetAsync(grad_feat, 0, n_feat * sizeof(float), s) != hipSuccess) return MVS_ERR_HIP;
+  if (g.V == 1) return MVS_OK;
   const BwdLayout L = bwd_layout(g.B, g.V, g.C, g.h, g.w, g.Dc);
   char* ws = static_cast<char*>(bwd_ws);
   u64* acc = reinterpret_cast<u64*>(ws + L.acc);
   float4* ref_part = reinterpret_cast<float4*>(ws + L.ref_part);
   unsigned* mx = reinterpret_cast<unsigned*>(ws + L.mx);
-  if (hipMemsetAsync(acc, 0, n_feat * 8, s) != hipSuccess) return MVS_ERR_HIP;
-  if (hipMemsetAsync(mx, 0, 8, s) != hipSuccess) return MVS_ERR_HIP;
-  const size_t n_gcv = (size_t)g.B * g.C * g.Dc * g.h * g.w;
-  hipLaunchKernelGGL(abs_max_kernel, dim3(2048), dim3(kBlock), 0, s, grad_cv, n_gcv, mx);
-  hipLaunchKernelGGL(abs_max_kernel, dim3(256), dim3(kBlock), 0, s, feat, n_feat, mx + 1);
+  if (deterministic) {
+    if (hipMemsetAsync(acc, 0, n_feat * 8, s) != hipSuccess) return MVS_ERR_HIP;
+    if (hipMemsetAsync(mx, 0, 8, s) != hipSuccess) return MVS_ERR_HIP;
+    const size_t n_gcv = (size_t)g.B * g.C * g.Dc * g.h * g.w;
+    hipLaunchKernelGGL(abs_max_kernel, dim3(2048), dim3(kBlock), 0, s, grad_cv, n_gcv, mx);
+    hipLaunchKernelGGL(abs_max_kernel, dim3(256), dim3(kBlock), 0, s, feat, n_feat, mx + 1);
+  }
   const float* smp = fwd_ws;
   if (g.V <= 8) {
     const float4* packed = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(fwd_ws) +
                                                            sampling_bytes_aligned(g.B * g.V, g.Dc));
     const int c4 = (g.C + 3) / 4;
     const float4* refs = packed + (size_t)g.B * g.V * c4 * pad_geom(g.h, g.w).plane;
-    switch (g.V) {
-      case 2: launch_main<2>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
-      case 3: launch_main<3>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
-      case 4: launch_main<4>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
-      case 5: launch_main<5>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
-      case 6: launch_main<6>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
-      case 7: launch_main<7>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
-      default: launch_main<8>(g, packed, refs, smp, grad_cv, acc, ref_part, mx, s); break;
-    }
+    if (deterministic) launch_views<true>(g, packed, refs, smp, grad_cv, acc, grad_feat, ref_part, mx, s);
+    else launch_views<false>(g, packed, refs, smp, grad_cv, acc, grad_feat, ref_part, mx, s);
     const uint32_t hw = (uint32_t)g.h * (uint32_t)g.w;
     const int groups = (g.Dc + kBwdKPG - 1) / kBwdKPG;
-    hipLaunchKernelGGL(ref_scatter_kernel, dim3((hw + kBlock - 1) / kBlock, (unsigned)(g.B * c4)), dim3(kBlock),
-                       0, s, ref_part, smp, acc, mx, g.B, g.V, g.C, g.h, g.w, g.Dc, groups);
+    const dim3 grid((hw + kBlock - 1) / kBlock, (unsigned)(g.B * c4));
+    if (deterministic)
+      hipLaunchKernelGGL(ref_scatter_kernel<true>, grid, dim3(kBlock), 0, s, ref_part, smp, acc, grad_feat, mx,
+                         g.B, g.V, g.C, g.h, g.w, g.Dc, groups);
+    else
+      hipLaunchKernelGGL(ref_scatter_kernel<false>, grid, dim3(kBlock), 0, s, ref_part, smp, acc, grad_feat, mx,
+                         g.B, g.V, g.C, g.h, g.w, g.Dc, groups);
+  } else if (deterministic) {
+    hipLaunchKernelGGL(cost_volume_bwd_generic_kernel<true>, xcd_grid(g.total), dim3(kBlock), 0, s, feat, smp,
+                       grad_cv, acc, grad_feat, mx, g.V, g.C, g.h, g.w, g.Dc, g.tiles, g.total);
   } else {
-    hipLaunchKernelGGL(cost_volume_bwd_generic_kernel, xcd_grid(g.total), dim3(kBlock), 0, s, feat, smp, grad_cv,
-                       acc, mx, g.V, g.C, g.h, g.w, g.Dc, g.tiles, g.total);
+    hipLaunchKernelGGL(cost_volume_bwd_generic_kernel<false>, xcd_grid(g.total), dim3(kBlock), 0, s, feat, smp,
+                       grad_cv, acc, grad_feat, mx, g.V, g.C, g.h, g.w, g.Dc, g.tiles, g.total);
   }
-  const size_t blocks = (n_feat + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(fixed_to_float_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(kBlock), 0, s,
-                     acc, n_feat, mx, g.V, g.Dc, (uint32_t)((size_t)g.h * g.w), grad_feat);
+  if (deterministic) {
+    const size_t blocks = (n_feat + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(fixed_to_float_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(kBlock), 0,
+                       s, acc, n_feat, mx, g.V, g.Dc, (uint32_t)((size_t)g.h * g.w), grad_feat);
+  }
   return hip_status();
 }
 

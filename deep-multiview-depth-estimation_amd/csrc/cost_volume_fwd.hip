@@ -22,6 +22,7 @@
 //     plane; a plane that still does not fit samples straight from the packed global features.
 // Workgroup ids are remapped so each XCD walks consecutive (tile, plane group) items.
 #include "launchers.h"
+#include "packed.h"
 
 namespace mvs {
 namespace {
@@ -90,29 +91,7 @@ __global__ __launch_bounds__(kBlock) void cost_volume_kernel(
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// Padded channel-quad layout (workspace):
-//   packed[N][C4][h + 2][w + 2] float4, C4 = ceil(C / 4), channel 4q+j in component j (zero pad),
-//   pixel (x, y) at padded (x + 1, y + 1); columns 0, w + 1 and rows 0, h + 1 are zero.
-// Every tap corner the sampling law can produce (x0 in [-1, w-1], y0 in [-1, h-1]) then has its
-// four taps inside the padded plane, and out-of-image taps read zeros: the bilinear gather needs no
-// bounds test and no branch.  A sample whose corner lies outside that range (all four taps outside
-// the image, sample exactly 0) gets an out-of-range buffer offset: its loads return 0 without
-// touching memory (about half of all samples on DTU geometry at D=192).
-//   refs[B][C4][h][w] float4: the reference view resampled through its own (plane-independent)
-// sampling matrix -- identical arithmetic to an in-kernel gather, computed once per launch.
-// ------------------------------------------------------------------------------------------
-struct PadGeom {
-  int pitch;        // w + 2 slots per padded row
-  uint32_t plane;   // (h + 2) * pitch slots per padded plane
-};
-
-__host__ __device__ inline PadGeom pad_geom(int h, int w) {
-  PadGeom p;
-  p.pitch = w + 2;
-  p.plane = (uint32_t)(h + 2) * (uint32_t)(w + 2);
-  return p;
-}
+// Padded channel-quad layout of the workspace: packed.h.
 
 __global__ __launch_bounds__(kBlock) void pack_pad_kernel(const float* __restrict__ feat,
                                                           float4* __restrict__ packed, int N, int C,
@@ -138,90 +117,6 @@ __global__ __launch_bounds__(kBlock) void pack_pad_kernel(const float* __restric
     }
     packed[e] = make_float4(v[0], v[1], v[2], v[3]);
   }
-}
-
-typedef float f2v __attribute__((ext_vector_type(2)));
-typedef float f4v __attribute__((ext_vector_type(4)));
-
-constexpr uint32_t kOobOffset = 0x80000000u;   // >= every descriptor's num_records
-
-// Tap state of one (pixel, plane, view): byte offset of the nw tap in the padded plane + fractions.
-__device__ inline uint32_t tap_offset(uint32_t pos, const PadGeom& pg) {
-  if (pos == kInvalidTap) return kOobOffset;
-  return ((uint32_t)(pos_y(pos) + 1) * (uint32_t)pg.pitch + (uint32_t)(pos_x(pos) + 1)) * 16u;
-}
-
-__device__ inline f4v ld4(Rsrc rs, uint32_t voff, int soff) {
-  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff, soff, 0));
-}
-
-// Bilinear sample of 4 channels: acc = 0, then fma(tap_t, weight_t, acc) over nw, ne, sw, se --
-// the order of every other gather in this library (zero taps add exactly nothing).  Packed fp32
-// FMAs (v_pk_fma_f32), elementwise identical to scalar fmaf.
-__device__ inline f4v bilerp(const f4v (&t)[4], float wx, float wy) {
-  // weights {nw, ne} = (1-wy) * {1-wx, wx}, {sw, se} = wy * {1-wx, wx}: tap_weights() in pairs
-  const f2v e = {1.0f - wx, wx};
-  const f2v w01 = f2v{1.0f - wy, 1.0f - wy} * e;
-  const f2v w23 = f2v{wy, wy} * e;
-  f2v lo = t[0].xy * w01.xx, hi = t[0].zw * w01.xx;   // fma(t, w, 0) == t * w
-  lo = __builtin_elementwise_fma(t[1].xy, w01.yy, lo);
-  hi = __builtin_elementwise_fma(t[1].zw, w01.yy, hi);
-  lo = __builtin_elementwise_fma(t[2].xy, w23.xx, lo);
-  hi = __builtin_elementwise_fma(t[2].zw, w23.xx, hi);
-  lo = __builtin_elementwise_fma(t[3].xy, w23.yy, lo);
-  hi = __builtin_elementwise_fma(t[3].zw, w23.yy, hi);
-  return f4v{lo.x, lo.y, hi.x, hi.y};
-}
-
-// Experiment (MVS_EXP_VSUBW): bilerp() with 1 - wx and 1 - wy produced by volatile v_sub_f32 (the
-// instruction the compiler emits for `1.0f - w`, so the values are identical), which removes the
-// register copies of the opaque-copy barrier -- but the compiler then reserves a register next to
-// every wx / wy to pair them for v_pk_mul_f32 (+32 VGPRs at 8 planes).
-__device__ inline f4v bilerp_loop(const f4v (&t)[4], float wx, float wy) {
-  float omx, omy;
-  asm volatile("v_sub_f32 %0, 1.0, %1" : "=v"(omx) : "v"(wx));
-  asm volatile("v_sub_f32 %0, 1.0, %1" : "=v"(omy) : "v"(wy));
-  const f2v e = {omx, wx};
-  const f2v w01 = f2v{omy, omy} * e;
-  const f2v w23 = f2v{wy, wy} * e;
-  f2v lo = t[0].xy * w01.xx, hi = t[0].zw * w01.xx;
-  lo = __builtin_elementwise_fma(t[1].xy, w01.yy, lo);
-  hi = __builtin_elementwise_fma(t[1].zw, w01.yy, hi);
-  lo = __builtin_elementwise_fma(t[2].xy, w23.xx, lo);
-  hi = __builtin_elementwise_fma(t[2].zw, w23.xx, hi);
-  lo = __builtin_elementwise_fma(t[3].xy, w23.yy, lo);
-  hi = __builtin_elementwise_fma(t[3].zw, w23.yy, hi);
-  return f4v{lo.x, lo.y, hi.x, hi.y};
-}
-
-// bilerp() with the weights rebuilt from a packed {wx, wy} register pair in 4 VALU: two v_pk_fma_f32
-// give e = {1 - wx, wx} and f = {1 - wy, wy} (fma(w, -1, 1) == 1 - w and fma(w, 1, 0) == w exactly, so
-// the weights are bit-identical to tap_weights()), then w01 = f.xx * e and w23 = f.yy * e.  The fmas
-// are volatile asm, so the compiler cannot hoist the weights out of the channel loop (which would
-// hold 4 VGPRs per (plane, view) instead of 2), and no opaque register copy is needed (the plain
-// bilerp() path pays 2 v_mov_b32 + 2 v_sub_f32 per (plane, view) per chunk for the same effect).
-__device__ inline f4v bilerp_pk(const f4v (&t)[4], f2v wxy, f2v cneg /* {-1, 1} */, f2v c10 /* {1, 0} */) {
-  f2v e, f;
-  asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(e) : "v"(wxy), "v"(cneg), "v"(c10));
-  asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,1]"
-               : "=v"(f) : "v"(wxy), "v"(cneg), "v"(c10));
-  const f2v w01 = f.xx * e;
-  const f2v w23 = f.yy * e;
-  f2v lo = t[0].xy * w01.xx, hi = t[0].zw * w01.xx;
-  lo = __builtin_elementwise_fma(t[1].xy, w01.yy, lo);
-  hi = __builtin_elementwise_fma(t[1].zw, w01.yy, hi);
-  lo = __builtin_elementwise_fma(t[2].xy, w23.xx, lo);
-  hi = __builtin_elementwise_fma(t[2].zw, w23.xx, hi);
-  lo = __builtin_elementwise_fma(t[3].xy, w23.yy, lo);
-  hi = __builtin_elementwise_fma(t[3].zw, w23.yy, hi);
-  return f4v{lo.x, lo.y, hi.x, hi.y};
-}
-
-__device__ inline void load_taps(Rsrc rs, uint32_t voff, int soff, int row_bytes, f4v (&t)[4]) {
-  t[0] = ld4(rs, voff, soff);
-  t[1] = ld4(rs, voff + 16u, soff);
-  t[2] = ld4(rs, voff, soff + row_bytes);
-  t[3] = ld4(rs, voff + 16u, soff + row_bytes);
 }
 
 // costvolume.py:12-14: mean = sum / V, cv = sum (x - mean)^2 / V (two-pass), 4 channels at once;
@@ -267,155 +162,35 @@ __global__ __launch_bounds__(kBlock) void ref_resample_kernel(const float4* __re
   refs[((size_t)b * c4 + ch) * hw + p] = make_float4(r.x, r.y, r.z, r.w);
 }
 
-// ------------------------------------------------------------------------------------------
-// Fused gather kernel (2 <= V <= 8).  A 256-thread workgroup owns a 32 x 8 pixel tile of one sample
-// and a group of up to KPG consecutive depth planes; one thread = one pixel.  Per thread, the tap
-// state of every (plane, source view) is computed once and kept in registers (3 VGPRs each); then
-// for every 4-channel chunk: one coalesced load of the resampled reference, and per plane 4
-// branch-free 16-byte buffer loads per source view, bilinear + two-pass variance in packed fp32,
-// four dword stores (32-pixel rows: 128-byte segments).
-// ------------------------------------------------------------------------------------------
-#ifndef MVS_EXP_TW
-#define MVS_EXP_TW 32
-#endif
-constexpr int kTileW = MVS_EXP_TW;
+constexpr int kTileW = 32;                // pixels per tile row: every cost-volume store is a 128-B row
 constexpr int kTileH = kBlock / kTileW;   // 8
 
-// staged kernel: pixels per tile row.  64-px rows for bf16 (128-B store rows) measured slower
-// (0.669 ms against 0.557 ms at cfg 2: 160 = 2.5 x 64 leaves a sixth of the lanes idle and the
-// kernel is bound by its gather/compute side, not by the bf16 stores), so both use 32.
-template <int ES>
-constexpr int tile_w() {
-  return kTileW;
-}
-
+// planes per workgroup: the tap state of every (plane, source view) lives in registers
 template <int V>
 constexpr int group_planes() {
-#ifdef MVS_EXP_PG
-  return MVS_EXP_PG;
-#else
   return V <= 3 ? 8 : (V <= 5 ? 4 : 2);
-#endif
-}
-
-template <int V, int KPG>
-__global__ __launch_bounds__(kBlock) void cost_volume_gather_kernel(
-    const float4* __restrict__ packed, const float4* __restrict__ refs,
-    const float* __restrict__ sampling, float* __restrict__ cv, int C, int h, int w, int Dc, int pg_n,
-    int tiles_x, int tiles_y, int groups, int total) {
-  constexpr int NS = V - 1;
-  const int wk = xcd_work_id(blockIdx.x, total);
-  if (wk >= total) return;
-  const int g = wk % groups;
-  const int t = wk / groups;
-  const int tile = t % (tiles_x * tiles_y);
-  const int b = t / (tiles_x * tiles_y);
-  const int px = (tile % tiles_x) * kTileW + (int)(threadIdx.x % kTileW);
-  const int py = (tile / tiles_x) * kTileH + (int)(threadIdx.x / kTileW);
-  if (px >= w || py >= h) return;   // no barriers in this kernel
-  const int k0 = g * pg_n;
-  const int npl = min(pg_n, Dc - k0);
-  const uint32_t hw = (uint32_t)h * (uint32_t)w;
-  const int c4 = (C + 3) / 4;
-  const PadGeom pg = pad_geom(h, w);
-  const float xn = norm_coord(px, w);
-  const float yn = norm_coord(py, h);
-
-  uint32_t off[KPG][NS];
-  float fwx[KPG][NS], fwy[KPG][NS];
-#pragma unroll
-  for (int pl = 0; pl < KPG; ++pl)
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      uint32_t pos = kInvalidTap;
-      fwx[pl][s] = fwy[pl][s] = 0.0f;
-      if (pl < npl)
-        src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + k0 + pl) * 9, xn, yn, h, w, true, pos,
-                   fwx[pl][s], fwy[pl][s]);
-      off[pl][s] = tap_offset(pos, pg);
-    }
-
-  Rsrc rs[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s)
-    rs[s] = make_rsrc(packed + (size_t)(b * V + 1 + s) * c4 * pg.plane, (uint32_t)c4 * pg.plane * 16u);
-  const int row_bytes = pg.pitch * 16;
-  const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
-  const uint32_t pix = (uint32_t)py * (uint32_t)w + (uint32_t)px;
-  const float4* rbase = refs + (size_t)b * c4 * hw + pix;
-  float* obase = cv + ((size_t)b * C * Dc + (size_t)k0) * hw + pix;
-  const size_t cstride = (size_t)Dc * hw;
-
-  for (int ch = 0; ch < c4; ++ch) {
-    const float4 r4 = rbase[(size_t)ch * hw];
-    const f4v x0 = {r4.x, r4.y, r4.z, r4.w};
-    const int soff = (int)((uint32_t)ch * pg.plane * 16u);
-#pragma unroll
-    for (int pl = 0; pl < KPG; ++pl) {
-      if (pl >= npl) break;
-      f4v xs[NS];
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-#ifdef MVS_EXP_BRANCH
-        f4v tp[4] = {};
-        if (off[pl][s] != kOobOffset) load_taps(rs[s], off[pl][s], soff, row_bytes, tp);
-#else
-        f4v tp[4];
-        load_taps(rs[s], off[pl][s], soff, row_bytes, tp);
-#endif
-        // opaque copies: the weights are rebuilt per chunk (3 VALU) instead of being held in 8
-        // VGPRs per (plane, view) across the chunk loop
-        float twx = fwx[pl][s], twy = fwy[pl][s];
-        asm volatile("" : "+v"(twx), "+v"(twy));
-        xs[s] = bilerp(tp, twx, twy);
-      }
-      const f4v acc = variance4<NS>(x0, xs, inv_v);
-      float* ob = obase + (size_t)pl * hw + (size_t)(ch * 4) * cstride;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (ch * 4 + j < C) {
-#ifdef MVS_EXP_NOSTORE
-          if (acc[j] == 12345.678f)
-#endif
-#ifdef MVS_EXP_NT
-          __builtin_nontemporal_store(acc[j], ob + (size_t)j * cstride);
-#else
-          ob[(size_t)j * cstride] = acc[j];
-#endif
-        }
-      }
-#ifndef MVS_EXP_NOSB
-      __builtin_amdgcn_sched_barrier(0);   // one plane's loads in flight per wave (VGPR budget)
-#endif
-    }
-  }
 }
 
 // ------------------------------------------------------------------------------------------
-// LDS-staged kernel (2 <= V <= 8), the default.  Same tiling, tap state and arithmetic as the gather
-// kernel above, but the source views are read from LDS: per 4-channel chunk the workgroup stages,
+// LDS-staged kernel (2 <= V <= 8).  A 256-thread workgroup owns a 32 x 8 pixel tile of one sample
+// and a group of up to KPG consecutive depth planes; one thread = one pixel.  Per thread, the tap
+// state of every (plane, source view) is computed once and kept in registers (3 VGPRs each).  The
+// source views are read from LDS: per 4-channel chunk the workgroup stages,
 // for every source view, the bounding box of all tap corners of its tile over its plane group
 // (the footprint, about 1.8 slots per pixel at P = 4 on DTU geometry) with one coalesced 16-byte
 // load per slot, and every bilinear tap is then a conflict-light ds_read_b128 (4 LDS cycles per
 // wave-instruction against about 12 texture-path cycles for a 16-byte global gather, measured
 // in tools/microbench/gather_patterns.hip).  A zero area at the front of LDS serves the samples
-// with every tap outside the image (exactly 0).  A workgroup whose footprint exceeds
-// the LDS budget falls back to the global gathers of the kernel above.
+// with every tap outside the image (exactly 0).  A workgroup whose footprint exceeds the LDS
+// budget samples the packed features straight from global memory (16-byte buffer gathers).
 // ------------------------------------------------------------------------------------------
 template <int V>
 constexpr int staged_slots() {
-#ifdef MVS_EXP_SLOTS
-  return MVS_EXP_SLOTS;
-#else
   return V <= 3 ? 2560 : (V <= 5 ? 3072 : 4096);   // 40 / 48 / 64 KB: 4 / 3 / 2 workgroups per CU
-#endif
 }
 // 3 waves per SIMD (at most 168 VGPRs): without the hint the V = 3 kernel lands at 169 VGPRs and 2
 // waves; with it, 153 VGPRs and no VGPR spill.
-#ifndef MVS_EXP_WPE
-#define MVS_EXP_WPE 3
-#endif
-#define MVS_STAGED_ATTR __attribute__((amdgpu_waves_per_eu(MVS_EXP_WPE)))
+#define MVS_STAGED_ATTR __attribute__((amdgpu_waves_per_eu(3)))
 
 // Wave-wide min on the DPP network (no LDS traffic): xor-1 and xor-2 quad permutes, half-row and
 // row mirrors (min over 16 lanes), then the row broadcasts of lanes 15 and 31; lane 63 ends with the
@@ -453,11 +228,9 @@ __device__ inline void block_min(int (&v)[NV], int* scratch /* >= 4 * NV ints of
 // end, channels past C and inactive lanes get out-of-range offsets and are dropped by the hardware,
 // so every wave issues the same, statically known number of stores per chunk (the waits for the
 // next chunk's staging loads then never wait for this chunk's stores).
-#ifndef MVS_EXP_AUX
-#define MVS_EXP_AUX 2   /* nt */
-#endif
+constexpr int kStoreAux = 2;   // nt: 0.52 ms at cfg 2 against 0.66 ms with the default policy
 __device__ inline void store_cv(Rsrc rs, uint32_t voff, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)voff, 0, MVS_EXP_AUX);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)voff, 0, kStoreAux);
 }
 
 // bf16 output (opt-in): the fp32 variance rounded to nearest-even exactly as
@@ -473,7 +246,7 @@ __device__ inline void store_out(Rsrc rs, uint32_t voff, float v) {
   if constexpr (ES == 4) {
     store_cv(rs, voff, v);
   } else {
-    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bf16_rne(v), rs, (int)voff, 0, MVS_EXP_AUX);
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)bf16_rne(v), rs, (int)voff, 0, kStoreAux);
   }
 }
 
@@ -498,7 +271,7 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   const int t = wk / groups;
   const int tile = t % (tiles_x * tiles_y);
   const int b = t / (tiles_x * tiles_y);
-  constexpr int TW = tile_w<ES>(), TH = kBlock / TW;
+  constexpr int TW = kTileW, TH = kTileH;
   const int px = (tile % tiles_x) * TW + (int)(threadIdx.x % TW);
   const int py = (tile / tiles_x) * TH + (int)(threadIdx.x / TW);
   const bool active = px < w && py < h;
@@ -576,7 +349,6 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
     }
   };
   layout();
-#ifndef MVS_EXP_NOPADRETRY
   // Over budget with 16-slot row pitches: retry with unpadded rows (pitch = width).  Row crossings
   // inside a 16-lane ds_read_b128 group may then conflict, but the workgroup stays on LDS instead of
   // the global-gather path (unpadded, 97.1 % of V = 5 footprints fit instead of 92.3 %,
@@ -591,17 +363,12 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
     zero_slots = (zero_slots + 15) & ~15;
     layout();
   }
-#endif
 
   const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
   const uint32_t pix = (uint32_t)(active ? py : 0) * (uint32_t)w + (uint32_t)(active ? px : 0);
   const float4* rbase = refs + (size_t)b * c4 * hw + pix;
   // store byte offset of (plane 0, this pixel) inside a (channel, group) descriptor
-#ifdef MVS_EXP_NOSTORE
-  const uint32_t soff0 = kOobOffset;
-#else
   const uint32_t soff0 = active ? pix * (uint32_t)ES : kOobOffset;
-#endif
   const uint32_t grp_bytes = (uint32_t)npl * hw * (uint32_t)ES;
 
   // store descriptors of chunk ch's four channels (planes k0 .. k0 + npl of this sample)
@@ -623,9 +390,6 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   if (scum[NS] > SLOTS - 1) {
     // footprint beyond the LDS budget (extreme zoom / long epipolar sweep): global gathers
     if (!active) return;   // no barriers below
-#ifdef MVS_EXP_NOFALLBACK
-    return;
-#endif
     Rsrc rs[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s)
@@ -733,17 +497,14 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
     // formally pending at the loop head and force a full vmcnt drain there)
 #pragma unroll
     for (int j = 0; j < kPrefetch; ++j) lds[pslot[j]] = f4v{pre[j].x, pre[j].y, pre[j].z, pre[j].w};
-#ifndef MVS_EXP_NOSTAGE
     for (int q = (int)threadIdx.x + kBlock * kPrefetch; q < n_pieces; q += kBlock) {
       uint32_t slot;
       const float4 v = pbase[piece(q, slot) + (uint32_t)ch * pg.plane];
       lds[slot] = f4v{v.x, v.y, v.z, v.w};
     }
-#endif
   };
   stage(0);
 
-  const f2v cneg = {-1.0f, 1.0f}, c10 = {1.0f, 0.0f};
   for (int ch = 0; ch < c4; ++ch) {
     __syncthreads();   // chunk ch is in LDS
     const f4v xr = x0;
@@ -761,15 +522,11 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
         tp[1] = lds[i0 + 1];
         tp[2] = lds[i0 + rp[s]];
         tp[3] = lds[i0 + rp[s] + 1];
-#ifdef MVS_EXP_VSUBW   // 32 fewer VALU per chunk, but 200 VGPRs (2 waves per SIMD)
-        xs[s] = bilerp_loop(tp, fwx[pl][s], fwy[pl][s]);
-#elif defined(MVS_EXP_PKW)
-        xs[s] = bilerp_pk(tp, f2v{fwx[pl][s], fwy[pl][s]}, cneg, c10);
-#else
+        // opaque copies: the weights are rebuilt per chunk (3 VALU) instead of being held in 8
+        // VGPRs per (plane, view) across the chunk loop
         float twx = fwx[pl][s], twy = fwy[pl][s];
         asm volatile("" : "+v"(twx), "+v"(twy));
         xs[s] = bilerp(tp, twx, twy);
-#endif
       }
       emit(pl, ors, xr, xs);
     }
@@ -811,32 +568,18 @@ void launch_gather(const Geometry& g, const float* feat, const float* smp, float
   const uint32_t hw = (uint32_t)g.h * (uint32_t)g.w;
   hipLaunchKernelGGL(ref_resample_kernel, dim3((hw + kBlock - 1) / kBlock, (unsigned)(g.B * c4)),
                      dim3(kBlock), 0, s, packed, smp, refs, g.B, V, g.C, g.h, g.w, g.Dc);
-#ifdef MVS_EXP_GATHER
-  constexpr int TW = kTileW;
-#else
-  constexpr int TW = tile_w<ES>();
-#endif
-  constexpr int TH = kBlock / TW;
+  constexpr int TW = kTileW, TH = kTileH;
   const int tiles_x = (g.w + TW - 1) / TW, tiles_y = (g.h + TH - 1) / TH;
   // planes per workgroup: the register maximum, halved until the grid has >= 4 workgroups per CU
   // (cfg 4, 32-plane shards: 0.128 ms with the 8-plane template at pg = 1, 0.044 ms at pg = 2)
-#ifndef MVS_EXP_MINWG
-#define MVS_EXP_MINWG 1024
-#endif
+  constexpr long kMinWorkgroups = 1024;
   int pg = group_planes<V>();
-  while (pg > 1 && (long)g.B * tiles_x * tiles_y * ((g.Dc + pg - 1) / pg) < MVS_EXP_MINWG) pg >>= 1;
+  while (pg > 1 && (long)g.B * tiles_x * tiles_y * ((g.Dc + pg - 1) / pg) < kMinWorkgroups) pg >>= 1;
   const int groups = (g.Dc + pg - 1) / pg;
   const int total = g.B * tiles_x * tiles_y * groups;
   if (ev0) (void)hipEventRecord(ev0, s);
-#ifdef MVS_EXP_GATHER
-  if constexpr (ES == 4)
-    hipLaunchKernelGGL((cost_volume_gather_kernel<V, group_planes<V>()>), xcd_grid(total), dim3(kBlock),
-                       0, s, packed, refs, smp, static_cast<float*>(cv), g.C, g.h, g.w, g.Dc, pg, tiles_x,
-                       tiles_y, groups, total);
-#else
   launch_staged<V, group_planes<V>(), ES>(pg, xcd_grid(total), s, packed, refs, smp, cv, g, tiles_x, tiles_y,
                                          groups, total);
-#endif
   if (ev1) (void)hipEventRecord(ev1, s);
 }
 

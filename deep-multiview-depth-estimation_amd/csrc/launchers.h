@@ -33,10 +33,11 @@ void launch_variance(const float* warped, int B, int V, size_t M, float* cv, hip
 
 // cost_volume_bwd.hip: grad_feat (overwritten) from grad_cv, the forward's workspace (sampling
 // matrices + packed features + resampled reference views) and a backward workspace of
-// cost_volume_bwd_workspace_bytes(); deterministic (64-bit fixed-point accumulation)
+// cost_volume_bwd_workspace_bytes(); deterministic = 64-bit fixed-point accumulation throughout
 size_t cost_volume_bwd_workspace_bytes(int B, int V, int C, int h, int w, int Dc);
 int launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* fwd_ws,
-                           const float* grad_cv, void* bwd_ws, float* grad_feat, hipStream_t s);
+                           const float* grad_cv, void* bwd_ws, float* grad_feat, bool deterministic,
+                           hipStream_t s);
 
 // soft_argmin.hip
 void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, uint32_t hw,

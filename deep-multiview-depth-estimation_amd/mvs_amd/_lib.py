@@ -21,6 +21,7 @@ LIB_PATH = os.environ.get("MVS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
 ABI_VERSION = 2
 
 MVS_OK = 0
+MVS_BWD_DETERMINISTIC = 1
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported n_views", -3: "too large",
           -4: "HIP runtime error"}
 
@@ -48,7 +49,7 @@ SIGNATURES = {
     "mvs_cost_volume_bwd_workspace_bytes": (ctypes.c_size_t, [_c_int, _c_int, _c_int, _c_int,
                                                               _c_int, _c_int]),
     "mvs_cost_volume_bwd": (_c_int, [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
-                                     _p, _p, _p]),
+                                     _c_int, _p, _p, _p]),
     "mvs_extract_depth_map_fwd": (_c_int, [_p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _p,
                                            _p]),
     "mvs_normalize_images": (_c_int, [_p, _c_int, _c_int, _c_int, _p, _p, _p, _p]),

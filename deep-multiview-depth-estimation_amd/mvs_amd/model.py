@@ -160,8 +160,10 @@ class CostVolumeReg(nn.Module):
 
     def forward_full(self, cv):
         act = lambda bn, y: self.ReLU(bn(y))
-        # the BN modules are shared between levels exactly as in model.py:101-121
-        y0 = act(self.BN_0, self.conv_0_0(cv))
+        # the BN modules are shared between levels exactly as in model.py:101-121; the two narrow
+        # full-resolution layers run on the HIP kernel in no-grad fp32 inference (_narrow_conv),
+        # e.g. test.py:61's train-mode BatchNorm under no_grad
+        y0 = act(self.BN_0, _narrow_conv(self.conv_0_0, cv))
         y1 = act(self.BN_1, self.conv_1_0(cv))
         y2 = act(self.BN_2, self.conv_2_0(cv))
         y3 = act(self.BN_3, self.conv_3_0(cv))
@@ -171,7 +173,7 @@ class CostVolumeReg(nn.Module):
         y3 = act(self.BN_2, self.deconv_3_0(y3))
         y2 = act(self.BN_1, self.deconv_2_0(y3 + y2))
         y1 = act(self.BN_0, self.deconv_1_0(y2 + y1))
-        return self.Norm(self.conv_out(y1 + y0))
+        return self.Norm(_narrow_conv(self.conv_out, y1 + y0))
 
 
 def _hip_inference(x):

@@ -119,9 +119,11 @@ def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scal
 
 @torch.library.custom_op("mvs::cost_volume_backward", mutates_args=())
 def cost_volume_backward(feat: torch.Tensor, workspace: torch.Tensor, grad_cv: torch.Tensor,
-                         batch_size: int, n_views: int, d_count: int) -> torch.Tensor:
-    """d <cv, grad_cv> / d feat (deterministic: 64-bit fixed-point accumulation in the kernel).
-    ``workspace`` is the forward's (sampling matrices, packed features, resampled references)."""
+                         batch_size: int, n_views: int, d_count: int,
+                         deterministic: bool = False) -> torch.Tensor:
+    """d <cv, grad_cv> / d feat.  ``workspace`` is the forward's (sampling matrices, packed
+    features, resampled references).  ``deterministic``: 64-bit fixed-point accumulation,
+    bit-identical across runs (autograd passes torch.are_deterministic_algorithms_enabled())."""
     _require_gpu(feat, "feature_maps")
     lib = _lib.load()
     feat = feat.to(_F32).contiguous()
@@ -131,14 +133,15 @@ def cost_volume_backward(feat: torch.Tensor, workspace: torch.Tensor, grad_cv: t
     nb = lib.mvs_cost_volume_bwd_workspace_bytes(batch_size, n_views, c, h, w, d_count)
     bws = torch.empty((max(nb, 8) + 7) // 8, device=feat.device, dtype=torch.int64)
     st = lib.mvs_cost_volume_bwd(_lib.ptr(feat), _lib.ptr(workspace), _lib.ptr(grad_cv),
-                                 batch_size, n_views, c, h, w, d_count, _lib.ptr(bws),
+                                 batch_size, n_views, c, h, w, d_count,
+                                 _lib.MVS_BWD_DETERMINISTIC if deterministic else 0, _lib.ptr(bws),
                                  _lib.ptr(grad_feat), _lib.stream_handle(feat.device))
     _lib.check(st, "mvs_cost_volume_bwd")
     return grad_feat
 
 
 @cost_volume_backward.register_fake
-def _(feat, workspace, grad_cv, batch_size, n_views, d_count):
+def _(feat, workspace, grad_cv, batch_size, n_views, d_count, deterministic=False):
     return torch.empty_like(feat)
 
 
@@ -154,7 +157,8 @@ def _cv_backward(ctx, grad_cv, _grad_ws):
     batch_size, n_views, d_count = ctx.dims
     grad_feat = None
     if ctx.needs_input_grad[0] and grad_cv is not None:
-        grad_feat = cost_volume_backward(feat, ws, grad_cv, batch_size, n_views, d_count)
+        grad_feat = cost_volume_backward(feat, ws, grad_cv, batch_size, n_views, d_count,
+                                         torch.are_deterministic_algorithms_enabled())
     return grad_feat, None, None, None, None, None, None, None, None, None, None
 
 
@@ -312,9 +316,10 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Te
         raise ValueError("x [B, Cin, D, H, W] and weight [Cout, Cin, 3, 3, 3] expected, got %s / %s"
                          % (tuple(x.shape), tuple(weight.shape)))
     x = x.to(_F32).contiguous()
-    w = weight.to(device=x.device, dtype=_F32).contiguous()
+    cout = weight.shape[0]
+    # the kernel reads weight[c_in][3][3][3][c_out] (pairs of output channels per 8-byte load)
+    w = weight.to(device=x.device, dtype=_F32).permute(1, 2, 3, 4, 0).contiguous()
     b, cin, d, h, wd = x.shape
-    cout = w.shape[0]
     bn = [t if t is None else t.to(device=x.device, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
     if any(t is None for t in bn) and not all(t is None for t in bn):
         raise ValueError("bn_scale, bn_shift and bn_mean go together")

@@ -130,20 +130,27 @@ int mvs_assemble_cost_volume_fwd(const float* warped, int batch_size, int n_view
 size_t mvs_cost_volume_bwd_workspace_bytes(int batch_size, int n_views, int channels, int h, int w,
                                            int d_count);
 
+/* mvs_cost_volume_bwd flags */
+#define MVS_BWD_DETERMINISTIC 1
+
 /*
  * Backward of the fused op w.r.t. the features (autograd of costvolume.py:14 + grid_sample,
  * exercised by train.py:103): grad_feat[N][C][h][w] is OVERWRITTEN with d<cv, grad_cv>/d feat.
  * `workspace` is the forward call's workspace (same geometry, not modified since): its sampling
  * matrices, packed features and resampled reference views are reused.  `bwd_workspace` holds
  * mvs_cost_volume_bwd_workspace_bytes(...) bytes.
- * DETERMINISTIC: contributions are accumulated in 64-bit fixed point (integer adds are
- * associative), so the result is bit-identical across runs whatever the scheduling; resolution
- * 2^-61 * d_count*h*w*8*max|grad_cv|*max|feat|/n_views (about 1e-12 of the largest possible
- * contribution at BASELINE cfg 2).  Non-finite inputs give unspecified results.
+ * flags = 0: per-tile partial sums are accumulated in fp64 on chip and added to grad_feat with
+ *   fp32 atomics -- the summation order (and so the last bits) may vary between runs, like
+ *   torch's grid_sample backward on GPU.
+ * flags = MVS_BWD_DETERMINISTIC: 64-bit fixed point throughout (integer adds are associative),
+ *   so the result is bit-identical across runs whatever the scheduling; resolution
+ *   2^-61 * d_count*h*w*8*max|grad_cv|*max|feat|/n_views (about 1e-12 of the largest possible
+ *   contribution at BASELINE cfg 2); one extra pass reads grad_cv for its maximum.
+ * Non-finite inputs give unspecified results in deterministic mode.
  */
 int mvs_cost_volume_bwd(const float* feat, const float* workspace, const float* grad_cv,
                         int batch_size, int n_views, int channels, int h, int w, int d_count,
-                        void* bwd_workspace, float* grad_feat, void* stream);
+                        int flags, void* bwd_workspace, float* grad_feat, void* stream);
 
 /*
  * Soft-argmin with the reference's permutation-indexed mask (depthmap.py:4-22):
@@ -177,7 +184,9 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
 
 /* Regulariser layers conv_0_0 (32 -> 8) and conv_out (8 -> 1) of CostVolumeReg (model.py:77,96 /
  * forward at model.py:101,123): nn.Conv3d(c_in, c_out, 3, stride=1, padding=1, bias=False) over
- * x[batch][c_in][d][h][w] fp32 with weight[c_out][c_in][3][3][3], into y[batch][c_out][d][h][w].
+ * x[batch][c_in][d][h][w] fp32 into y[batch][c_out][d][h][w], with the weight TRANSPOSED to
+ * weight[c_in][3][3][3][c_out] (nn.Conv3d's weight.permute(1, 2, 3, 4, 0): pairs of output channels
+ * are adjacent, one 8-byte scalar load feeds a packed fp32 FMA).
  * c_out must be 1 or 8 (MVS_ERR_INVALID_ARGUMENT otherwise); d*h*w < 2^31.  Optional epilogue
  * (all three BN pointers, c_out floats each, or none): y = max((y - bn_mean) * bn_scale + bn_shift,
  * 0), the eval BN + ReLU that follows conv_0_0 (model.py:101; bn_scale = gamma / sqrt(var + eps),

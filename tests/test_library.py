@@ -72,8 +72,9 @@ def test_invalid_arguments_rejected_before_any_launch():
                                    25.0, fake, fake, null) == -3
     assert lib.mvs_extract_depth_map_fwd(fake, fake, 1, 48, 8, 8, 0, fake, null) == -1
     # backward: missing backward workspace (needed for n_views > 1), bad geometry
-    assert lib.mvs_cost_volume_bwd(fake, fake, fake, 1, 3, 32, 128, 160, 48, null, fake, null) == -1
-    assert lib.mvs_cost_volume_bwd(fake, fake, fake, 1, 17, 32, 128, 160, 48, fake, fake, null) == -2
+    assert lib.mvs_cost_volume_bwd(fake, fake, fake, 1, 3, 32, 128, 160, 48, 0, null, fake, null) == -1
+    assert lib.mvs_cost_volume_bwd(fake, fake, fake, 1, 17, 32, 128, 160, 48, 0, fake, fake, null) == -2
+    assert lib.mvs_cost_volume_bwd(fake, fake, fake, 1, 3, 32, 128, 160, 48, 2, fake, fake, null) == -1
     assert lib.mvs_cost_volume_bwd_workspace_bytes(1, 3, 32, 128, 160, 0) == 0
     # 64-bit accumulators for every feature element + reference-view partials + scalars
     assert lib.mvs_cost_volume_bwd_workspace_bytes(4, 3, 32, 128, 160, 192) >= 12 * 32 * 128 * 160 * 8

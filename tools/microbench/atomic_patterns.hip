@@ -24,6 +24,7 @@ __global__ void k_global(T* t, uint32_t rows) {
     const uint32_t row = hash(wave * kIters + i) % rows;
     T* p = t + (size_t)row * 64 + lane;
     if constexpr (sizeof(T) == 4) unsafeAtomicAdd(p, (T)1.0f);
+    else if constexpr (__is_same(T, double)) unsafeAtomicAdd(p, 1.0);
     else atomicAdd((unsigned long long*)p, 1ull);
   }
 }
@@ -35,7 +36,10 @@ __global__ void k_lds(T* out) {
   __syncthreads();
   for (int i = 0; i < 1024; ++i) {
     const int a = (threadIdx.x + i * 256) & 8191;
-    if constexpr (sizeof(T) == 4) atomicAdd(&s[a], 1.0f);
+    if constexpr (__is_same(T, float)) atomicAdd(&s[a], 1.0f);
+    else if constexpr (__is_same(T, unsigned)) atomicAdd(&s[a], 1u);
+    else if constexpr (__is_same(T, int)) s[a] = i;   // plain ds_write baseline
+    else if constexpr (__is_same(T, double)) unsafeAtomicAdd(&s[a], 1.0);
     else atomicAdd((unsigned long long*)&s[a], 1ull);
   }
   __syncthreads();
@@ -76,5 +80,13 @@ int main() {
   printf("(c) LDS f32 atomic add: %.3f ms for %.0f M lanes = %.1f G/s\n", ms, nl / 1e6, nl / ms / 1e6);
   ms = time_ms([&] { k_lds<unsigned long long><<<2048, 256>>>(ti); });
   printf("(d) LDS u64 atomic add: %.3f ms for %.0f M lanes = %.1f G/s\n", ms, nl / 1e6, nl / ms / 1e6);
+  ms = time_ms([&] { k_lds<unsigned><<<2048, 256>>>((unsigned*)ti); });
+  printf("(e) LDS u32 atomic add: %.3f ms for %.0f M lanes = %.1f G/s\n", ms, nl / 1e6, nl / ms / 1e6);
+  ms = time_ms([&] { k_lds<int><<<2048, 256>>>((int*)ti); });
+  printf("(f) LDS plain b32 write: %.3f ms for %.0f M lanes = %.1f G/s\n", ms, nl / 1e6, nl / ms / 1e6);
+  ms = time_ms([&] { k_lds<double><<<2048, 256>>>((double*)ti); });
+  printf("(g) LDS f64 atomic add: %.3f ms for %.0f M lanes = %.1f G/s\n", ms, nl / 1e6, nl / ms / 1e6);
+  ms = time_ms([&] { k_global<double><<<blocks, 256>>>((double*)ti, (uint32_t)(kTarget / 64)); });
+  printf("(h) global f64 atomic add: %.3f ms for %.0f M lanes = %.1f G/s\n", ms, n / 1e6, n / ms / 1e6);
   return 0;
 }
