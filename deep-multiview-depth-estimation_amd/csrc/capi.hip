@@ -52,7 +52,8 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
   if (st != MVS_OK) return st;
   hipStream_t s = (hipStream_t)stream;
   if (n_views == 1) {  // the variance of a single view is identically zero (0 in fp32 and bf16)
-    if (hipMemsetAsync(cv_out, 0, (size_t)batch_size * channels * d_count * h * w * es, s) != hipSuccess)
+    const size_t ch = es == 16 ? (size_t)((channels + 3) / 4) : (size_t)channels;
+    if (hipMemsetAsync(cv_out, 0, (size_t)batch_size * ch * d_count * h * w * es, s) != hipSuccess)
       return MVS_ERR_HIP;
     return mvs::hip_status();
   }
@@ -62,6 +63,9 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
   if (es == 4)
     mvs::launch_cost_volume_fwd(g, feat, workspace, packed, static_cast<float*>(cv_out), s,
                                 (hipEvent_t)ev0, (hipEvent_t)ev1);
+  else if (es == 16)
+    mvs::launch_cost_volume_fwd_c4(g, feat, workspace, packed, static_cast<float*>(cv_out), s,
+                                   (hipEvent_t)ev0, (hipEvent_t)ev1);
   else
     mvs::launch_cost_volume_fwd_bf16(g, feat, workspace, packed, cv_out, s, (hipEvent_t)ev0,
                                      (hipEvent_t)ev1);
@@ -136,6 +140,18 @@ int mvs_cost_volume_fwd_bf16(const float* feat, const float* K, const float* R, 
   return cost_volume_fwd_impl(feat, K, R, T, d_min, d_int, batch_size, n_views, channels, h, w,
                               d_begin, d_count, d_scale, workspace, cv_out, 2, stream, nullptr,
                               nullptr);
+}
+
+int mvs_cost_volume_fwd_c4(const float* feat, const float* K, const float* R, const float* T,
+                           const float* d_min, const float* d_int, int batch_size, int n_views,
+                           int channels, int h, int w, int d_begin, int d_count, float d_scale,
+                           float* workspace, float* cv_out, void* stream, void* main_begin_event,
+                           void* main_end_event) {
+  if (n_views > 8) return MVS_ERR_UNSUPPORTED_VIEWS;
+  if ((uintptr_t)cv_out & 15u) return MVS_ERR_INVALID_ARGUMENT;
+  return cost_volume_fwd_impl(feat, K, R, T, d_min, d_int, batch_size, n_views, channels, h, w,
+                              d_begin, d_count, d_scale, workspace, cv_out, 16, stream,
+                              main_begin_event, main_end_event);
 }
 
 int mvs_homography_warp_fwd(const float* feat, const float* K, const float* R, const float* T,
@@ -215,32 +231,75 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
   return mvs::hip_status();
 }
 
-int mvs_conv3d_k3_fwd(const float* x, const float* weight, float* y, int batch, int c_in, int c_out,
-                      int d, int h, int w, const float* bn_scale, const float* bn_shift,
+int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, int batch, int c_in,
+                      int c_out, int d, int h, int w, const float* bn_scale, const float* bn_shift,
                       const float* bn_mean, void* stream) {
   if (!x || !weight || !y || batch <= 0 || c_in <= 0 || d <= 0 || h <= 0 || w <= 0)
     return MVS_ERR_INVALID_ARGUMENT;
   if (c_out != 1 && c_out != 8) return MVS_ERR_INVALID_ARGUMENT;
+  if (flags & ~MVS_CONV_IN_C4) return MVS_ERR_INVALID_ARGUMENT;
+  if ((flags & MVS_CONV_IN_C4) && (c_in % 4 || ((uintptr_t)x & 15u))) return MVS_ERR_INVALID_ARGUMENT;
   if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
     return MVS_ERR_INVALID_ARGUMENT;
   // staging offsets inside one channel volume are 32-bit
   if ((uint64_t)d * (uint64_t)h * (uint64_t)w >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
-  mvs::launch_conv3d_k3_narrow(x, weight, y, batch, c_in, c_out, d, h, w, bn_scale, bn_shift, bn_mean,
+  mvs::launch_conv3d_k3_narrow(x, (flags & MVS_CONV_IN_C4) != 0, weight, y, batch, c_in, c_out, d, h, w,
+                               bn_scale, bn_shift, bn_mean,
                                (hipStream_t)stream);
   return mvs::hip_status();
 }
 
-int mvs_deconv3d_k3s2_fwd(const float* x, int batch, int c_in, int c_out, int rd, int rh, int rw,
-                          int x0d, int x0h, int x0w, const float* weight, int d, int h, int w,
-                          int pd, int ph, int pw, const float* bn_scale, const float* bn_shift,
-                          const float* bn_mean, const float* residual, float* y, void* stream) {
+int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch, int c_in, int c_out,
+                          int rd, int rh, int rw, int x0d, int x0h, int x0w, const float* weight, int d,
+                          int h, int w, int pd, int ph, int pw, const float* bn_scale,
+                          const float* bn_shift, const float* bn_mean, const float* residual, float* y,
+                          void* stream) {
   if (!x || !weight || !y || batch <= 0 || c_in <= 0 || c_in > 64 || c_out != 8) return MVS_ERR_INVALID_ARGUMENT;
+  if (flags & ~MVS_LAYOUT_CHANNELS_LAST) return MVS_ERR_INVALID_ARGUMENT;
+  if ((flags & MVS_LAYOUT_CHANNELS_LAST) && (c_in % 4 || ((uintptr_t)x & 15u) || ((uintptr_t)x2 & 15u)))
+    return MVS_ERR_INVALID_ARGUMENT;   // 16-byte channel-quad loads
   if (rd <= 0 || rh <= 0 || rw <= 0 || d <= 0 || h <= 0 || w <= 0) return MVS_ERR_INVALID_ARGUMENT;
   if (x0d < 0 || x0h < 0 || x0w < 0 || pd < 0 || ph < 0 || pw < 0) return MVS_ERR_INVALID_ARGUMENT;
   if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
     return MVS_ERR_INVALID_ARGUMENT;
-  mvs::launch_deconv3d_k3s2(x, batch, c_in, rd, rh, rw, x0d, x0h, x0w, weight, d, h, w, pd, ph, pw, bn_scale,
-                            bn_shift, bn_mean, residual, y, (hipStream_t)stream);
+  mvs::launch_deconv3d_k3s2(x, x2, (flags & MVS_LAYOUT_CHANNELS_LAST) != 0, batch, c_in, rd, rh, rw, x0d, x0h,
+                            x0w, weight, d, h, w, pd, ph, pw, bn_scale, bn_shift, bn_mean, residual, y,
+                            (hipStream_t)stream);
+  return mvs::hip_status();
+}
+
+int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, const float* weight, float* y,
+                          int batch, int c_in, int c_out, const int* dims, const int* out_origin,
+                          const int* out_size, const int* in_origin, const int* in_size,
+                          const int* pad, const float* bn_scale, const float* bn_shift,
+                          const float* bn_mean, void* stream) {
+  if (!x || !weight || !y || !dims || !out_origin || !out_size || batch <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if (mode < MVS_CONV_S1 || mode > MVS_CONV_T2 || (flags & ~(MVS_CONV_OUT_NCDHW | MVS_CONV_IN_C4)))
+    return MVS_ERR_INVALID_ARGUMENT;
+  if ((flags & MVS_CONV_IN_C4) && (mode != MVS_CONV_S2 || c_in % 4)) return MVS_ERR_INVALID_ARGUMENT;
+  if (mode != MVS_CONV_S2 && (!in_origin || !in_size)) return MVS_ERR_INVALID_ARGUMENT;
+  if (mode != MVS_CONV_S1 && !pad) return MVS_ERR_INVALID_ARGUMENT;
+  if (((uintptr_t)x | (uintptr_t)x2 | (uintptr_t)weight) & 15u) return MVS_ERR_INVALID_ARGUMENT;   // 16-byte loads
+  if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
+    return MVS_ERR_INVALID_ARGUMENT;
+  uint64_t ovox = (uint64_t)batch, ivox = (uint64_t)batch, nvox = (uint64_t)batch * c_in;
+  for (int k = 0; k < 3; ++k) {
+    if (dims[k] <= 0 || out_size[k] <= 0 || out_origin[k] < 0 || out_origin[k] + out_size[k] > dims[k])
+      return MVS_ERR_INVALID_ARGUMENT;
+    if (mode != MVS_CONV_S2 &&
+        (in_size[k] <= 0 || in_origin[k] < 0 || in_origin[k] + in_size[k] > dims[k]))
+      return MVS_ERR_INVALID_ARGUMENT;
+    ovox *= (uint64_t)out_size[k];
+    ivox *= (uint64_t)(mode == MVS_CONV_S2 ? dims[k] : in_size[k]);
+    nvox *= (uint64_t)dims[k];
+  }
+  // 32-bit row indices; element offsets are 64-bit
+  if (ovox >= (1ull << 31) || ivox * (uint64_t)c_in >= (1ull << 62) || nvox >= (1ull << 62)) return MVS_ERR_TOO_LARGE;
+  const int st = mvs::launch_conv3d_region(mode, (flags & MVS_CONV_OUT_NCDHW) != 0, (flags & MVS_CONV_IN_C4) != 0,
+                                           x, x2, weight, y, batch, c_in, c_out, dims, out_origin, out_size,
+                                           in_origin, in_size, pad, bn_scale, bn_shift, bn_mean,
+                                           (hipStream_t)stream);
+  if (st != MVS_OK) return st;
   return mvs::hip_status();
 }
 

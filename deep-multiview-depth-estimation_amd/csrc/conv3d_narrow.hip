@@ -10,7 +10,8 @@
 // stages the (DT + 2) x 10 x 34 halo block in LDS (zero-filled outside the volume), and every
 // thread reads the 9 taps of each staged plane once (54 VGPRs) and applies them to the output
 // depths they reach (plane p feeds depth p - kd).  The staging of channel c + 1 is loaded into
-// registers before channel c is computed.
+// registers before channel c is computed.  Input NCDHW, or channel-quad (C4, the fused kernel's
+// NC4DHW4 output): then a pass stages 4 channels with one 16-byte load per element into 4 LDS planes.
 //   COUT = 8: output channels in pairs on the packed fp32 FMA (v_pk_fma_f32: the tap broadcast to
 //   both halves, the two channels' weights as one 64-bit scalar operand), 2 FMAs per lane-
 //   instruction -- the weights arrive pre-transposed as wt[c][kd][ky][kx][co] (ops.py), so each
@@ -23,7 +24,7 @@ namespace {
 
 constexpr int kTX = 32, kTY = 8, kDT = 4;
 
-template <int COUT>
+template <int COUT, bool C4>
 __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
     const float* __restrict__ in, const float* __restrict__ wt, float* __restrict__ out, int Cin,
     int D, int H, int W, int tiles_x, int tiles_y, int dgroups, const float* __restrict__ bn_scale,
@@ -33,7 +34,8 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   constexpr int kStage = kPD * kPlane;                      // floats per input channel
   constexpr int kPer = (kStage + kBlock - 1) / kBlock;      // staging elements per thread
   constexpr int NP = COUT / 2;                              // channel pairs (COUT = 8)
-  __shared__ float lds[kStage];
+  constexpr int NQ = C4 ? 4 : 1;                            // channels staged per pass
+  __shared__ float lds[NQ * kStage];
   int t = blockIdx.x;
   const int tx0 = (t % tiles_x) * kTX;
   t /= tiles_x;
@@ -43,7 +45,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   const int b = t / dgroups;
   const size_t plane = (size_t)H * W;
   const size_t vol = (size_t)D * plane;
-  const float* ib = in + (size_t)b * Cin * vol;
+  const float* ib = in + (size_t)b * Cin * vol;   // (channel-quad layout: the same element count)
 
   // staging map: element e of the halo block -> (global offset inside one channel, valid)
   int goff[kPer];
@@ -57,11 +59,24 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
     gok[j] = e < kStage && gz >= 0 && gz < D && gy >= 0 && gy < H && gx >= 0 && gx < W;
     goff[j] = gok[j] ? (int)((size_t)gz * plane + (size_t)gy * W + gx) : 0;
   }
-  float pre[kPer];
-  auto fetch = [&](int c) {
-    const float* src = ib + (size_t)c * vol;
+  // one pass = one input channel (NCDHW) or one channel quad (C4: 16-byte loads, 4 LDS planes)
+  float pre[kPer][NQ];
+  auto fetch = [&](int q) {
+    if constexpr (C4) {
+      const float4* src = reinterpret_cast<const float4*>(ib) + (size_t)q * vol;
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) pre[j] = gok[j] ? src[goff[j]] : 0.0f;
+      for (int j = 0; j < kPer; ++j) {
+        const float4 v = gok[j] ? src[goff[j]] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        pre[j][0] = v.x;
+        pre[j][1] = v.y;
+        pre[j][2] = v.z;
+        pre[j][3] = v.w;
+      }
+    } else {
+      const float* src = ib + (size_t)q * vol;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) pre[j][0] = gok[j] ? src[goff[j]] : 0.0f;
+    }
   };
   fetch(0);
 
@@ -75,57 +90,65 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
     for (int q = 0; q < (NP > 0 ? NP : 1); ++q) acc2[d][q] = f2v{0.0f, 0.0f};
   }
 
-  for (int c = 0; c < Cin; ++c) {
-    __syncthreads();   // previous channel's reads are done
+  const int passes = C4 ? Cin / 4 : Cin;
+  for (int q = 0; q < passes; ++q) {
+    __syncthreads();   // the previous pass's reads are done
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int e = (int)threadIdx.x + j * kBlock;
-      if (e < kStage) lds[e] = pre[j];
+      if (e < kStage)
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) lds[u * kStage + e] = pre[j][u];
     }
     __syncthreads();
-    if (c + 1 < Cin) fetch(c + 1);   // in flight during this channel's arithmetic
-    // the 3 x 3 taps of every staged plane, read once
-    float tap[kPD][3][3];
+    if (q + 1 < passes) fetch(q + 1);   // in flight during this pass's arithmetic
+#pragma unroll 1
+    for (int u = 0; u < NQ; ++u) {
+      const int c = q * NQ + u;
+      const float* lc = lds + u * kStage;
+      // the 3 x 3 taps of every staged plane, read once
+      float tap[kPD][3][3];
 #pragma unroll
-    for (int p = 0; p < kPD; ++p)
+      for (int p = 0; p < kPD; ++p)
 #pragma unroll
-      for (int ry = 0; ry < 3; ++ry)
+        for (int ry = 0; ry < 3; ++ry)
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) tap[p][ry][kx] = lds[p * kPlane + (ly + ry) * kPX + lx + kx];
+          for (int kx = 0; kx < 3; ++kx) tap[p][ry][kx] = lc[p * kPlane + (ly + ry) * kPX + lx + kx];
 #pragma unroll
-    for (int kd = 0; kd < 3; ++kd) {
-      if constexpr (COUT == 8) {
+      for (int kd = 0; kd < 3; ++kd) {
+        if constexpr (COUT == 8) {
 #pragma unroll
-        for (int q = 0; q < NP; ++q) {
-          // weight pairs (co = 2q, 2q + 1) of the 9 (ky, kx) taps: workgroup-uniform scalar loads;
-          // the memory clobber keeps the compiler from hoisting a whole channel's 216 weights
+          for (int qq = 0; qq < NP; ++qq) {
+            // weight pairs (co = 2qq, 2qq + 1) of the 9 (ky, kx) taps: workgroup-uniform scalar
+            // loads; the memory clobber keeps the compiler from hoisting a whole channel's weights
+            asm volatile("" ::: "memory");
+            const f2v* wg = reinterpret_cast<const f2v*>(wt + ((size_t)(c * 3 + kd) * 9) * 8) + qq;
+            f2v wp[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) wp[k] = wg[k * 4];
+#pragma unroll
+            for (int d = 0; d < kDT; ++d)   // output depth d reads plane d + kd through kernel depth kd
+#pragma unroll
+              for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                  const float tv = tap[d + kd][ky][kx];
+                  acc2[d][qq] = __builtin_elementwise_fma(f2v{tv, tv}, wp[ky * 3 + kx], acc2[d][qq]);
+                }
+          }
+        } else {
           asm volatile("" ::: "memory");
-          const f2v* wg = reinterpret_cast<const f2v*>(wt + ((size_t)(c * 3 + kd) * 9) * 8) + q;
-          f2v wp[9];
+          const float* wg = wt + ((size_t)c * 3 + kd) * 9;
+          float w9[9];
 #pragma unroll
-          for (int k = 0; k < 9; ++k) wp[k] = wg[k * 4];
+          for (int k = 0; k < 9; ++k) w9[k] = wg[k];
 #pragma unroll
-          for (int d = 0; d < kDT; ++d)   // output depth d reads plane d + kd through kernel depth kd
+          for (int d = 0; d < kDT; ++d)
 #pragma unroll
             for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-              for (int kx = 0; kx < 3; ++kx) {
-                const float tv = tap[d + kd][ky][kx];
-                acc2[d][q] = __builtin_elementwise_fma(f2v{tv, tv}, wp[ky * 3 + kx], acc2[d][q]);
-              }
+              for (int kx = 0; kx < 3; ++kx) acc1[d] = fmaf(tap[d + kd][ky][kx], w9[ky * 3 + kx], acc1[d]);
         }
-      } else {
-        asm volatile("" ::: "memory");
-        const float* wg = wt + ((size_t)c * 3 + kd) * 9;
-        float w9[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) w9[k] = wg[k];
-#pragma unroll
-        for (int d = 0; d < kDT; ++d)
-#pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-            for (int kx = 0; kx < 3; ++kx) acc1[d] = fmaf(tap[d + kd][ky][kx], w9[ky * 3 + kx], acc1[d]);
       }
     }
   }
@@ -145,24 +168,28 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   }
 }
 
-template <int COUT>
+template <int COUT, bool C4>
 void launch_narrow(const float* in, const float* weight, float* out, int B, int Cin, int D, int H, int W,
                    const float* bn_scale, const float* bn_shift, const float* bn_mean, hipStream_t s) {
   const int tiles_x = (W + kTX - 1) / kTX, tiles_y = (H + kTY - 1) / kTY, dgroups = (D + kDT - 1) / kDT;
   const dim3 grid((unsigned)((size_t)B * dgroups * tiles_y * tiles_x));
-  hipLaunchKernelGGL((conv3d_k3_narrow_kernel<COUT>), grid, dim3(kBlock), 0, s, in, weight, out, Cin, D, H, W,
+  hipLaunchKernelGGL((conv3d_k3_narrow_kernel<COUT, C4>), grid, dim3(kBlock), 0, s, in, weight, out, Cin, D, H, W,
                      tiles_x, tiles_y, dgroups, bn_scale, bn_shift, bn_mean);
 }
 
 }  // namespace
 
-void launch_conv3d_k3_narrow(const float* in, const float* weight, float* out, int B, int Cin,
+void launch_conv3d_k3_narrow(const float* in, bool in_c4, const float* weight, float* out, int B, int Cin,
                              int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
                              const float* bn_mean, hipStream_t s) {
-  if (Cout == 8)
-    launch_narrow<8>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
+  if (Cout == 8 && in_c4)
+    launch_narrow<8, true>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
+  else if (Cout == 8)
+    launch_narrow<8, false>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
+  else if (in_c4)
+    launch_narrow<1, true>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
   else
-    launch_narrow<1>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
+    launch_narrow<1, false>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
 }
 
 }  // namespace mvs

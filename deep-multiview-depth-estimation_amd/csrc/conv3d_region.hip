@@ -1,0 +1,270 @@
+// conv3d_region.hip -- the regulariser's region convolutions (CostVolumeReg, model.py:76-95, forward
+// at model.py:101-121) as implicit GEMMs on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: exact
+// fp32, one rounding per product, the f32 VALU's peak rate without its operand traffic), with the
+// eval-mode BatchNorm + ReLU that follows every one of them fused into the epilogue.
+//
+// forward_live evaluates the U-Net level k only on its live region.  The region
+// tensors live channels-last, x[b][z][y][x][c] (NDHWC, the GEMM's K = channel axis contiguous),
+// with their box origin (o0) in the volume; three forms:
+//   S1  conv_k_1:     3x3x3, stride 1, padding 1 (zero outside the VOLUME), region -> region
+//   S2  conv_k_0:     3x3x3, stride 2, padding P (config.py:20), the full cost volume (NCDHW, or
+//                     the fused kernel's channel-quad NC4DHW4: 4 channels per 16-byte load) ->
+//                     region: output o reads inputs 2 o - P + t, t = 0..2, per dim
+//   T2  deconv_k_0:   ConvTranspose3d 3x3x3, stride 2, padding P, region -> region: output o
+//                     gathers inputs i = (o + P - t) / 2 for t of o + P's parity (1 or 2 taps per
+//                     dim); outputs are processed by parity class (8 launches' worth of grid.y), so
+//                     every voxel of a 16-voxel MFMA row block has the same taps; the input may be
+//                     the sum of two region tensors (model.py:119-121's `y3 + y2`, `y2 + y1`).
+// GEMM per sample: rows = output voxels of the region (flattened z, y, x; parity class for T2),
+// columns = output channels, K = (tap, input channel).  A wave owns 2 x 16 rows and every column
+// block (CO / 16); per (tap, 16-channel block) each lane loads 4 consecutive channels of its row's
+// input voxel (channels-last: one 16-byte load; S2 reads the NCDHW volume per channel) and of its
+// column's weights, which feed 4 MFMAs (K-step s takes component s).  Weights arrive as
+// w[tap][co][ci] (ops.py transposes nn.Conv3d / nn.ConvTranspose3d's layouts).  Products are summed
+// per tap over channels in a fixed order -- MIOpen's kernels sum in other orders; same products,
+// fp32 rounding-level differences.
+#include "launchers.h"
+
+namespace mvs {
+namespace {
+
+typedef float f4v_t __attribute__((ext_vector_type(4)));
+
+constexpr int kRows = 32;   // output voxels per wave (2 MFMA row blocks)
+
+template <int MODE>
+struct ConvMode {};
+constexpr int kS1 = 0, kS2 = 1, kT2 = 2;
+
+struct Geo {
+  int n[3];     // volume dims (D, H, W)
+  int o0[3];    // output region origin
+  int on[3];    // output region size
+  int i0[3];    // input region origin (S1, T2)
+  int in[3];    // input region size (S1, T2)
+  int pad[3];   // P (S2, T2)
+  int out_cf;   // 1: output region tensor channels-first y[b][co][z][y][x] (else channels-last)
+  int in_c4;    // S2: the volume is channel-quad x[b][C/4][D][H][W][4] (else NCDHW)
+};
+
+// T2 parity class: per dim, outputs o with (o + P) % 2 == par; first such o in the region and count
+__device__ inline void class_dim(int o0, int on, int p, int par, int& first, int& cnt) {
+  first = o0 + (((o0 + p) & 1) != par ? 1 : 0);
+  cnt = first < o0 + on ? (o0 + on - 1 - first) / 2 + 1 : 0;
+}
+
+__device__ inline void store_out(float* __restrict__ y, const Geo& g, int b, int co, int vz, int vy, int vx,
+                                 int CO, float v) {
+  const size_t vox = ((size_t)vz * g.on[1] + vy) * g.on[2] + vx;
+  const size_t rvol = (size_t)g.on[0] * g.on[1] * g.on[2];
+  if (g.out_cf) y[((size_t)b * CO + co) * rvol + vox] = v;
+  else y[((size_t)b * rvol + vox) * CO + co] = v;
+}
+
+template <int MODE, int CI, int CO>
+__global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
+    const float* __restrict__ x, const float* __restrict__ x2, const float* __restrict__ w,
+    float* __restrict__ y, const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
+    const float* __restrict__ bn_mean, Geo g) {
+  constexpr int NB = CO / 16;          // column blocks
+  static_assert(CI % 16 == 0 && CO % 16 == 0, "channel counts in multiples of 16");
+  const int lane = (int)threadIdx.x & 63;
+  const int m = lane & 15, kq = lane >> 4;   // MFMA row / K index of this lane's A value
+  const int b = (int)blockIdx.z;
+
+  // ---- rows of this wave: parity class (T2) or the whole region ----
+  int cf[3], cn[3], par[3] = {0, 0, 0};
+  if constexpr (MODE == kT2) {
+    const int cls = (int)blockIdx.y;
+    par[0] = (cls >> 2) & 1;
+    par[1] = (cls >> 1) & 1;
+    par[2] = cls & 1;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) class_dim(g.o0[d], g.on[d], g.pad[d], par[d], cf[d], cn[d]);
+  } else {
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      cf[d] = g.o0[d];
+      cn[d] = g.on[d];
+    }
+  }
+  const int rows = cn[0] * cn[1] * cn[2];
+  const int step = MODE == kT2 ? 2 : 1;
+  const int row0 = ((int)blockIdx.x * (kBlock / 64) + ((int)threadIdx.x >> 6)) * kRows;
+  if (row0 >= rows) return;   // wave-uniform; no barriers in this kernel
+
+  // per row block: this lane's output voxel (volume coords), validity
+  int oz[2], oy[2], ox[2];
+  bool rok[2];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    const int r = row0 + rb * 16 + m;
+    rok[rb] = r < rows;
+    const int rr = rok[rb] ? r : 0;
+    const int jx = rr % cn[2], t = rr / cn[2];
+    const int jy = t % cn[1], jz = t / cn[1];
+    oz[rb] = cf[0] + step * jz;
+    oy[rb] = cf[1] + step * jy;
+    ox[rb] = cf[2] + step * jx;
+  }
+
+  f4v_t acc[2][NB];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = f4v_t{0.0f, 0.0f, 0.0f, 0.0f};
+
+  // ---- K loop: taps by rows (tz, ty); per row and 16-channel block the A values of its (up to)
+  // three x taps and both row blocks and the matching weights are loaded together, then fed to
+  // the MFMAs (3x the loads in flight of a tap-at-a-time loop) ----
+  const size_t nvol = (size_t)g.n[0] * g.n[1] * g.n[2];                  // S2 channel plane
+  for (int tz = 0; tz < 3; ++tz) {
+    if (MODE == kT2 && ((tz & 1) != par[0])) continue;   // t of o + P's parity only
+    for (int ty = 0; ty < 3; ++ty) {
+      if (MODE == kT2 && ((ty & 1) != par[1])) continue;
+      // input element offset of this lane's row (channel 0) per (x tap, row block), -1 = zero
+      long long off[3][2];
+#pragma unroll
+      for (int tx = 0; tx < 3; ++tx)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          int iz, iy, ix;
+          bool ok = rok[rb] && !(MODE == kT2 && ((tx & 1) != par[2]));
+          if constexpr (MODE == kS1) {
+            iz = oz[rb] + tz - 1;
+            iy = oy[rb] + ty - 1;
+            ix = ox[rb] + tx - 1;
+          } else if constexpr (MODE == kS2) {
+            iz = 2 * oz[rb] - g.pad[0] + tz;
+            iy = 2 * oy[rb] - g.pad[1] + ty;
+            ix = 2 * ox[rb] - g.pad[2] + tx;
+          } else {
+            iz = (oz[rb] + g.pad[0] - tz) >> 1;
+            iy = (oy[rb] + g.pad[1] - ty) >> 1;
+            ix = (ox[rb] + g.pad[2] - tx) >> 1;
+          }
+          ok = ok && iz >= 0 && iz < g.n[0] && iy >= 0 && iy < g.n[1] && ix >= 0 && ix < g.n[2];
+          if constexpr (MODE == kS2) {
+            off[tx][rb] = ok ? (long long)(((size_t)iz * g.n[1] + iy) * g.n[2] + ix) : -1;   // voxel
+          } else {
+            const int rz = iz - g.i0[0], ry = iy - g.i0[1], rx = ix - g.i0[2];
+            ok = ok && rz >= 0 && rz < g.in[0] && ry >= 0 && ry < g.in[1] && rx >= 0 && rx < g.in[2];
+            off[tx][rb] = ok ? (long long)((((size_t)b * g.in[0] + rz) * g.in[1] + ry) * g.in[2] + rx) * CI : -1;
+          }
+        }
+      // K = each tap's CI channels in blocks of 16: in K-step s of block cb, lane (m, kq) supplies
+      // channel cb * 16 + 4 kq + s -- one 16-byte load per lane (4 consecutive channels of its row's
+      // voxel, channels-last; of its column's weight row, w[tap][co][ci]) feeds 4 MFMAs
+#pragma unroll
+      for (int cb = 0; cb < CI / 16; ++cb) {
+        const int c4 = cb * 16 + kq * 4;
+        f4v_t a[3][2], bw[3][NB];
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) {
+          if (MODE == kT2 && ((tx & 1) != par[2])) continue;
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            f4v_t v = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (off[tx][rb] >= 0) {
+              if constexpr (MODE == kS2) {
+                if (g.in_c4) {   // the quad (c4 / 4) of the voxel: one 16-byte load
+                  v = *reinterpret_cast<const f4v_t*>(x + (((size_t)b * (CI / 4) + c4 / 4) * nvol + off[tx][rb]) * 4);
+                } else {
+#pragma unroll
+                  for (int s = 0; s < 4; ++s) v[s] = x[((size_t)b * CI + c4 + s) * nvol + off[tx][rb]];
+                }
+              } else {
+                v = *reinterpret_cast<const f4v_t*>(x + off[tx][rb] + c4);
+                if (x2) v += *reinterpret_cast<const f4v_t*>(x2 + off[tx][rb] + c4);
+              }
+            }
+            a[tx][rb] = v;
+          }
+          const float* wt = w + (size_t)((tz * 3 + ty) * 3 + tx) * CO * CI;
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+            bw[tx][nb] = *reinterpret_cast<const f4v_t*>(wt + (size_t)(nb * 16 + m) * CI + c4);
+        }
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) {
+          if (MODE == kT2 && ((tx & 1) != par[2])) continue;
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+              for (int nb = 0; nb < NB; ++nb)
+                acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[tx][rb][s], bw[tx][nb][s], acc[rb][nb], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: eval BN + ReLU, NDHWC store.  acc[rb][nb][r] = (row (lane>>4)*4 + r, col lane&15)
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const int co = nb * 16 + m;
+    const float sc = bn_scale ? bn_scale[co] : 1.0f, sh = bn_scale ? bn_shift[co] : 0.0f,
+                mu = bn_scale ? bn_mean[co] : 0.0f;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + rb * 16 + kq * 4 + r;
+        if (row >= rows) continue;
+        const int jx = row % cn[2], t = row / cn[2];
+        const int jy = t % cn[1], jz = t / cn[1];
+        const int vz = cf[0] + step * jz - g.o0[0], vy = cf[1] + step * jy - g.o0[1],
+                  vx = cf[2] + step * jx - g.o0[2];
+        float v = acc[rb][nb][r];
+        if (bn_scale) v = fmaxf((v - mu) * sc + sh, 0.0f);
+        store_out(y, g, b, co, vz, vy, vx, CO, v);
+      }
+  }
+}
+
+template <int MODE, int CI, int CO>
+void launch_mode(const float* x, const float* x2, const float* w, float* y, const float* sc, const float* sh,
+                 const float* mu, int B, const Geo& g, hipStream_t s) {
+  const int classes = MODE == kT2 ? 8 : 1;
+  // rows of the largest class (T2) or of the region
+  const int rz = MODE == kT2 ? (g.on[0] + 1) / 2 : g.on[0], ry = MODE == kT2 ? (g.on[1] + 1) / 2 : g.on[1],
+            rx = MODE == kT2 ? (g.on[2] + 1) / 2 : g.on[2];
+  const int rows = rz * ry * rx;
+  const int per_block = (kBlock / 64) * kRows;
+  const dim3 grid((unsigned)((rows + per_block - 1) / per_block), (unsigned)classes, (unsigned)B);
+  hipLaunchKernelGGL((conv3d_region_kernel<MODE, CI, CO>), grid, dim3(kBlock), 0, s, x, x2, w, y, sc, sh, mu, g);
+}
+
+}  // namespace
+
+int launch_conv3d_region(int mode, bool out_cf, bool in_c4, const float* x, const float* x2, const float* w,
+                         float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on, const int* i0,
+                         const int* in, const int* pad, const float* bn_scale, const float* bn_shift,
+                         const float* bn_mean, hipStream_t s) {
+  Geo g;
+  g.out_cf = out_cf ? 1 : 0;
+  g.in_c4 = in_c4 ? 1 : 0;
+  for (int d = 0; d < 3; ++d) {
+    g.n[d] = n[d];
+    g.o0[d] = o0[d];
+    g.on[d] = on[d];
+    g.i0[d] = i0 ? i0[d] : 0;
+    g.in[d] = in ? in[d] : n[d];
+    g.pad[d] = pad ? pad[d] : 1;
+  }
+#define MVS_REGION_CASE(MD, A, C)                                                       \
+  if (mode == MD && CI == A && CO == C) {                                               \
+    launch_mode<MD, A, C>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s);           \
+    return MVS_OK;                                                                      \
+  }
+  // S2: conv_1_0 / conv_2_0 / conv_3_0 (32 -> 16 / 32 / 64); S1: conv_k_1; T2: deconv_3_0 (64 -> 32),
+  // deconv_2_0 (32 -> 16)
+  MVS_REGION_CASE(kS2, 32, 16) MVS_REGION_CASE(kS2, 32, 32) MVS_REGION_CASE(kS2, 32, 64)
+  MVS_REGION_CASE(kS1, 16, 16) MVS_REGION_CASE(kS1, 32, 32) MVS_REGION_CASE(kS1, 64, 64)
+  MVS_REGION_CASE(kT2, 64, 32) MVS_REGION_CASE(kT2, 32, 16)
+#undef MVS_REGION_CASE
+  return MVS_ERR_INVALID_ARGUMENT;
+}
+
+}  // namespace mvs

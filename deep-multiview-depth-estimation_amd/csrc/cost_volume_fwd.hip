@@ -250,6 +250,14 @@ __device__ inline void store_out(Rsrc rs, uint32_t voff, float v) {
   }
 }
 
+// Output element bytes / layout of the staged kernel:
+//   ES = 4   fp32 cv[B][C][D][h][w] (the reference layout)
+//   ES = 2   bf16, same layout (SURVEY.md §8 f3 opt-in)
+//   ES = 16  fp32 channel-quad cv[B][C/4][D][h][w][4] ("NC4DHW4"): each (pixel, plane, chunk) is one
+//            16-byte store, a wave's 64 pixels one contiguous 1 KB run; the regulariser's HIP layers
+//            read 4 channels of a voxel per load from it (MVSNet.forward's inference path)
+constexpr int kQuad = 16;
+
 constexpr int kPrefetch = 4;   // staging pieces per thread carried in registers across a chunk
 
 template <int V, int KPG, int ES /* output element bytes: 4 fp32, 2 bf16 */>
@@ -371,19 +379,29 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   const uint32_t soff0 = active ? pix * (uint32_t)ES : kOobOffset;
   const uint32_t grp_bytes = (uint32_t)npl * hw * (uint32_t)ES;
 
-  // store descriptors of chunk ch's four channels (planes k0 .. k0 + npl of this sample)
+  // store descriptors of chunk ch's four channels (planes k0 .. k0 + npl of this sample); the
+  // channel-quad layout has one descriptor for the chunk's quad plane
   auto chunk_rsrc = [&](int ch, Rsrc (&rs)[4]) {
+    if constexpr (ES == kQuad) {
+      rs[0] = make_rsrc(static_cast<char*>(cv) + (((size_t)b * c4 + ch) * Dc + k0) * hw * kQuad, grp_bytes);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = ch * 4 + j;
-      rs[j] = make_rsrc(static_cast<char*>(cv) + (((size_t)b * C + (c < C ? c : 0)) * Dc + k0) * hw * ES,
-                        c < C ? grp_bytes : 0u);
+      for (int j = 0; j < 4; ++j) {
+        const int c = ch * 4 + j;
+        rs[j] = make_rsrc(static_cast<char*>(cv) + (((size_t)b * C + (c < C ? c : 0)) * Dc + k0) * hw * ES,
+                          c < C ? grp_bytes : 0u);
+      }
     }
   };
   auto emit = [&](int pl, const Rsrc (&rs)[4], const f4v& x0, const f4v (&xs)[NS]) {
     const f4v acc = variance4<NS>(x0, xs, inv_v);
+    if constexpr (ES == kQuad) {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc),
+                                             rs[0], (int)(soff0 + (uint32_t)pl * hw * (uint32_t)kQuad), 0, kStoreAux);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) store_out<ES>(rs[j], soff0 + (uint32_t)pl * hw * (uint32_t)ES, acc[j]);
+      for (int j = 0; j < 4; ++j) store_out<ES>(rs[j], soff0 + (uint32_t)pl * hw * (uint32_t)ES, acc[j]);
+    }
   };
 
   // the last slot is the dummy target of prefetch registers that carry no piece (kDummy below)
@@ -612,6 +630,20 @@ void launch_cost_volume_fwd_bf16(const Geometry& g, const float* feat, const flo
     case 6: launch_gather<6, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
     case 7: launch_gather<7, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
     case 8: launch_gather<8, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    default: break;   // rejected by the C ABI (2 <= V <= 8 only)
+  }
+}
+
+void launch_cost_volume_fwd_c4(const Geometry& g, const float* feat, const float* sampling,
+                               float* packed, float* cv, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  switch (g.V) {
+    case 2: launch_gather<2, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 3: launch_gather<3, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 4: launch_gather<4, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 5: launch_gather<5, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 6: launch_gather<6, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 7: launch_gather<7, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 8: launch_gather<8, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
     default: break;   // rejected by the C ABI (2 <= V <= 8 only)
   }
 }

@@ -6,6 +6,8 @@
 // so output o gathers the inputs i = (o + P - k) / 2 with o + P - k even: 1 or 2 taps per dim.
 // x is a REGION tensor: it holds the input only on [x0, x0 + r) per dim -- every input that
 // reaches an output in [0, n) (CostVolumeReg.forward_live); inputs outside it reach no output.
+// It is NCDHW or channels-last (the MFMA region convs' layout, conv3d_region.hip), optionally the
+// sum of two region tensors (model.py:121's `y2 + y1`, added on load).
 // Epilogue (optional): z = max((y - mean) * scale + shift, 0) + residual (scale = gamma /
 // sqrt(var + eps), shift = beta: eval BN).
 //
@@ -36,9 +38,10 @@ struct Stencil {
   static constexpr int k1[2] = {C ? 0 : 1, 2};
 };
 
-template <int CD, int CH, int CW>
+template <int CD, int CH, int CW, bool CL>
 __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
-    const float* __restrict__ x, const float* __restrict__ wt, int Cin, int rd, int rh, int rw,
+    const float* __restrict__ x, const float* __restrict__ x2, const float* __restrict__ wt, int Cin, int rd,
+    int rh, int rw,
     int x0d, int x0h, int x0w, int D, int H, int W, int qd, int qh, int qw,
     const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
     const float* __restrict__ mean, const float* __restrict__ residual, float* __restrict__ y,
@@ -70,6 +73,10 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
   }
   const size_t rvol = (size_t)rd * rh * rw;
   const float* xb = x + (size_t)b * Cin * rvol;
+  const float* xb2 = x2 ? x2 + (size_t)b * Cin * rvol : nullptr;
+  using SD = Stencil<CD>;
+  using SH = Stencil<CH>;
+  using SW = Stencil<CW>;
   float acc[2][2][2][kCout];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -79,19 +86,8 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
       for (int e = 0; e < 2; ++e)
 #pragma unroll
         for (int co = 0; co < kCout; ++co) acc[a][c][e][co] = 0.0f;
-  using SD = Stencil<CD>;
-  using SH = Stencil<CH>;
-  using SW = Stencil<CW>;
-  for (int ci = 0; ci < Cin; ++ci) {
-    const float* xc = xb + (size_t)ci * rvol;
-    float v[2][2][2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-          v[a][c][e] = (okd[a] && okh[c] && okw[e]) ? xc[((size_t)(ld + a) * rh + (lh + c)) * rw + (lw + e)] : 0.0f;
+  // one input channel's 8 voxel values v -> the 27 (input, tap) products of the 2x2x2 block
+  auto channel = [&](int ci, const float (&v)[2][2][2]) {
 #pragma unroll
     for (int co = 0; co < kCout; ++co) {
       const float4* wr = wl4 + (ci * kCout + co) * (kWRow / 4);
@@ -118,6 +114,58 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
                   const int iw = sw ? SW::in1[tw] : SW::in0[tw], kw = sw ? SW::k1[tw] : SW::k0[tw];
                   acc[sd][sh][sw][co] = fmaf(v[id][ih][iw], w[kd * 9 + kh * 3 + kw], acc[sd][sh][sw][co]);
                 }
+    }
+  };
+  if constexpr (CL) {
+    // channels-last: 4 channels of each of the 8 input voxels per 16-byte load (Cin % 4 == 0)
+    for (int c0 = 0; c0 < Cin; c0 += 4) {
+      float4 q[2][2][2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const size_t o = (((size_t)(ld + a) * rh + (lh + c)) * rw + (lw + e)) * Cin + c0;
+            float4 t = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (okd[a] && okh[c] && okw[e]) {
+              t = *reinterpret_cast<const float4*>(xb + o);
+              if (xb2) {
+                const float4 u = *reinterpret_cast<const float4*>(xb2 + o);
+                t = make_float4(t.x + u.x, t.y + u.y, t.z + u.z, t.w + u.w);
+              }
+            }
+            q[a][c][e] = t;
+          }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v[2][2][2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const float4 t = q[a][c][e];
+              v[a][c][e] = j == 0 ? t.x : (j == 1 ? t.y : (j == 2 ? t.z : t.w));
+            }
+        channel(c0 + j, v);
+      }
+    }
+  } else {
+    for (int ci = 0; ci < Cin; ++ci) {
+      float v[2][2][2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const size_t o = (size_t)ci * rvol + (((size_t)(ld + a) * rh + (lh + c)) * rw + (lw + e));
+            const bool ok = okd[a] && okh[c] && okw[e];
+            v[a][c][e] = ok ? (xb2 ? xb[o] + xb2[o] : xb[o]) : 0.0f;
+          }
+      channel(ci, v);
     }
   }
   const size_t plane = (size_t)D * H * W;
@@ -155,21 +203,27 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
 }
 
 template <int CD, int CH, int CW>
-void launch_cls(dim3 grid, size_t lds, hipStream_t s, const float* x, const float* weight, int Cin,
-                int rd, int rh, int rw, int x0d, int x0h, int x0w, int D, int H, int W, int pd, int ph,
-                int pw, const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                const float* residual, float* y, int md_n, int mh_n, int mw_n, size_t total) {
-  hipLaunchKernelGGL((deconv3d_k3s2_kernel<CD, CH, CW>), grid, dim3(kBlock), lds, s, x, weight, Cin, rd, rh,
-                     rw, x0d, x0h, x0w, D, H, W, pd >> 1, ph >> 1, pw >> 1, bn_scale, bn_shift, bn_mean,
-                     residual, y, md_n, mh_n, mw_n, total);
+void launch_cls(dim3 grid, size_t lds, hipStream_t s, const float* x, const float* x2, bool cl,
+                const float* weight, int Cin, int rd, int rh, int rw, int x0d, int x0h, int x0w, int D, int H,
+                int W, int pd, int ph, int pw, const float* bn_scale, const float* bn_shift,
+                const float* bn_mean, const float* residual, float* y, int md_n, int mh_n, int mw_n,
+                size_t total) {
+  if (cl)
+    hipLaunchKernelGGL((deconv3d_k3s2_kernel<CD, CH, CW, true>), grid, dim3(kBlock), lds, s, x, x2, weight, Cin,
+                       rd, rh, rw, x0d, x0h, x0w, D, H, W, pd >> 1, ph >> 1, pw >> 1, bn_scale, bn_shift,
+                       bn_mean, residual, y, md_n, mh_n, mw_n, total);
+  else
+    hipLaunchKernelGGL((deconv3d_k3s2_kernel<CD, CH, CW, false>), grid, dim3(kBlock), lds, s, x, x2, weight, Cin,
+                       rd, rh, rw, x0d, x0h, x0w, D, H, W, pd >> 1, ph >> 1, pw >> 1, bn_scale, bn_shift,
+                       bn_mean, residual, y, md_n, mh_n, mw_n, total);
 }
 
 }  // namespace
 
-void launch_deconv3d_k3s2(const float* x, int B, int Cin, int rd, int rh, int rw, int x0d, int x0h,
-                          int x0w, const float* weight, int D, int H, int W, int pd, int ph, int pw,
-                          const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                          const float* residual, float* y, hipStream_t s) {
+void launch_deconv3d_k3s2(const float* x, const float* x2, bool channels_last, int B, int Cin, int rd,
+                          int rh, int rw, int x0d, int x0h, int x0w, const float* weight, int D, int H,
+                          int W, int pd, int ph, int pw, const float* bn_scale, const float* bn_shift,
+                          const float* bn_mean, const float* residual, float* y, hipStream_t s) {
   const int md_n = (D + 1) / 2, mh_n = (H + 1) / 2, mw_n = (W + 1) / 2;
   const size_t total = (size_t)B * md_n * mh_n * mw_n;
   const dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
@@ -177,7 +231,7 @@ void launch_deconv3d_k3s2(const float* x, int B, int Cin, int rd, int rh, int rw
   const int cls = (pd & 1) * 4 + (ph & 1) * 2 + (pw & 1);
 #define MVS_DECONV_CASE(c)                                                                         \
   case c:                                                                                          \
-    launch_cls<(c >> 2) & 1, (c >> 1) & 1, c & 1>(grid, lds, s, x, weight, Cin, rd, rh, rw, x0d, x0h, \
+    launch_cls<(c >> 2) & 1, (c >> 1) & 1, c & 1>(grid, lds, s, x, x2, channels_last, weight, Cin, rd, rh, rw, x0d, x0h, \
                                                   x0w, D, H, W, pd, ph, pw, bn_scale, bn_shift,     \
                                                   bn_mean, residual, y, md_n, mh_n, mw_n, total);   \
     break;

@@ -21,6 +21,10 @@ size_t packed_bytes(int B, int V, int C, int h, int w);
 void launch_cost_volume_fwd(const Geometry& g, const float* feat, const float* sampling,
                             float* packed, float* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
                             hipEvent_t ev1 = nullptr);
+// same, channel-quad layout cv[B][C/4][Dc][h][w][4] fp32, 2 <= V <= 8
+void launch_cost_volume_fwd_c4(const Geometry& g, const float* feat, const float* sampling,
+                               float* packed, float* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
+                               hipEvent_t ev1 = nullptr);
 // same, bf16 cost volume (uint16 storage, RNE), 2 <= V <= 8
 void launch_cost_volume_fwd_bf16(const Geometry& g, const float* feat, const float* sampling,
                                  float* packed, void* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
@@ -44,17 +48,29 @@ void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, u
                         int n_est, float* depth, hipStream_t s);
 
 // conv3d_narrow.hip: 3x3x3 stride-1 padding-1 bias-free Conv3d, NCDHW fp32, Cout in {1, 8}
-// (optional epilogue: max((v - bn_mean) * bn_scale + bn_shift, 0), all three or none)
-void launch_conv3d_k3_narrow(const float* in, const float* weight, float* out, int B, int Cin,
+// (optional epilogue: max((v - bn_mean) * bn_scale + bn_shift, 0), all three or none); in_c4: the
+// input is channel-quad in[B][Cin/4][D][H][W][4]
+void launch_conv3d_k3_narrow(const float* in, bool in_c4, const float* weight, float* out, int B, int Cin,
                              int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
                              const float* bn_mean, hipStream_t s);
 
 // deconv3d_region.hip: stride-2 kernel-3 ConvTranspose3d (Cout 8) from a region tensor to the full
 // volume, optional fused BN(eval)+ReLU and residual add
-void launch_deconv3d_k3s2(const float* x, int B, int Cin, int rd, int rh, int rw, int x0d, int x0h,
-                          int x0w, const float* weight, int D, int H, int W, int pd, int ph, int pw,
-                          const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                          const float* residual, float* y, hipStream_t s);
+// (channels_last: x and x2 are [B][rd][rh][rw][Cin]; x2 (nullable) is added to x)
+void launch_deconv3d_k3s2(const float* x, const float* x2, bool channels_last, int B, int Cin, int rd,
+                          int rh, int rw, int x0d, int x0h, int x0w, const float* weight, int D, int H,
+                          int W, int pd, int ph, int pw, const float* bn_scale, const float* bn_shift,
+                          const float* bn_mean, const float* residual, float* y, hipStream_t s);
+
+// conv3d_region.hip: region convolutions of the regulariser on the fp32 MFMA (mode 0 = stride 1,
+// 1 = stride 2 from the full NCDHW volume, 2 = transposed stride 2), channels-last region tensors,
+// optional fused eval BN + ReLU, output channels-last or (out_cf) channels-first;
+// MVS_ERR_INVALID_ARGUMENT for an unsupported (mode, CI, CO)
+int launch_conv3d_region(int mode, bool out_cf, bool in_c4, const float* x, const float* x2, const float* w,
+                         float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on, const int* i0,
+                         const int* in,
+                         const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                         hipStream_t s);
 
 // dtu_input.hip: data.py:206-210 image normalisation (uint8 HWC -> fp32 NCHW), data.py:300-301
 // depth thresholds

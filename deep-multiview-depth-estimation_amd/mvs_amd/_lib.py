@@ -22,6 +22,10 @@ ABI_VERSION = 2
 
 MVS_OK = 0
 MVS_BWD_DETERMINISTIC = 1
+MVS_LAYOUT_CHANNELS_LAST = 1
+MVS_CONV_S1, MVS_CONV_S2, MVS_CONV_T2 = 0, 1, 2
+MVS_CONV_OUT_NCDHW = 1
+MVS_CONV_IN_C4 = 2
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported n_views", -3: "too large",
           -4: "HIP runtime error"}
 
@@ -40,6 +44,8 @@ SIGNATURES = {
                                      _c_int, _c_int, _c_int, _c_float, _p, _p, _p]),
     "mvs_cost_volume_fwd_timed": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
                                            _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p]),
+    "mvs_cost_volume_fwd_c4": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
+                                        _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p]),
     "mvs_cost_volume_fwd_bf16": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
                                           _c_int, _c_int, _c_int, _c_float, _p, _p, _p]),
     "mvs_homography_warp_fwd": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
@@ -54,9 +60,9 @@ SIGNATURES = {
                                            _p]),
     "mvs_normalize_images": (_c_int, [_p, _c_int, _c_int, _c_int, _p, _p, _p, _p]),
     "mvs_depth_threshold": (_c_int, [_p, ctypes.c_size_t, _c_float, _c_float, _p, _p]),
-    "mvs_conv3d_k3_fwd": (_c_int, [_p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _p, _p, _p,
-                                   _p]),
-    "mvs_deconv3d_k3s2_fwd": (_c_int, [_p] + [_c_int] * 9 + [_p] + [_c_int] * 6 + [_p] * 6),
+    "mvs_conv3d_k3_fwd": (_c_int, [_p, _c_int, _p, _p] + [_c_int] * 6 + [_p] * 4),
+    "mvs_deconv3d_k3s2_fwd": (_c_int, [_p, _p] + [_c_int] * 10 + [_p] + [_c_int] * 6 + [_p] * 6),
+    "mvs_conv3d_region_fwd": (_c_int, [_c_int, _c_int, _p, _p, _p, _p, _c_int, _c_int, _c_int] + [_p] * 10),
 }
 
 

@@ -21,17 +21,25 @@ def assemble_cost_volume(warped_feature_maps, n_views: int):
 
 def warp_and_assemble_cost_volume(K_batch, R_batch, T_batch, d_min, d_int, feature_maps,
                                   batch_size, n_views, d_num=D_NUM, d_scale=D_SCALE,
-                                  d_begin=0, d_count=None, cv_dtype=torch.float32):
+                                  d_begin=0, d_count=None, cv_dtype=torch.float32, channel_quads=False):
     """-> (cv [B, C, d_count, h, w], d_batch_0 [B, d_num, 1, 1], ref_idx_0 [B] CPU int64).
 
     ``cv_dtype=torch.bfloat16`` (opt-in) returns the fp32 variance rounded to
-    bf16 in the kernel's store (half the write); the default fp32 is the reference's."""
+    bf16 in the kernel's store (half the write); the default fp32 is the reference's.
+    ``channel_quads=True`` (fp32 inference) returns the same values in the channel-quad layout
+    [B, C/4, d_count, h, w, 4] that CostVolumeReg's HIP path reads 16 bytes at a time."""
     if d_count is None:
         d_count = d_num - d_begin
     if d_begin < 0 or d_count <= 0 or d_begin + d_count > d_num:
         raise ValueError("depth shard [%d, %d) outside [0, %d)" % (d_begin, d_begin + d_count, d_num))
     device = feature_maps.device
     d_batch_0 = depth_hypotheses(d_min, d_int, d_num, d_scale).to(device)
+    if channel_quads:
+        if cv_dtype != torch.float32:
+            raise ValueError("the channel-quad cost volume is fp32")
+        cv = ops.cost_volume_c4(feature_maps, K_batch, R_batch, T_batch, d_min, d_int, int(batch_size),
+                                int(n_views), int(d_begin), int(d_count), float(d_scale))
+        return cv, d_batch_0, reference_indices(batch_size, n_views)
     if cv_dtype == torch.float32:
         op = ops.cost_volume
     elif cv_dtype == torch.bfloat16:

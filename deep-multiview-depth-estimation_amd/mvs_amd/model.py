@@ -91,17 +91,28 @@ class CostVolumeReg(nn.Module):
         self.live_region = True
 
     def forward(self, cv):
-        if self.live_region and not self._bn_uses_batch_stats() and self._live_geometry_ok(cv):
+        """cv [B, C, D, H, W], or the channel-quad [B, C/4, D, H, W, 4] of ops.cost_volume_c4 (HIP
+        inference feed, MVSNet.forward); the latter is read in place by the HIP live path and
+        re-laid to NCDHW for any other path."""
+        if cv.dim() == 6:
+            if self.live_ok(cv.shape[2:5]) and _hip_inference(cv):
+                return self.forward_live(cv)
+            cv = cv.permute(0, 1, 5, 2, 3, 4).reshape((cv.shape[0], 4 * cv.shape[1]) + tuple(cv.shape[2:5]))
+        if self.live_ok(cv.shape[2:]):
             return self.forward_live(cv)
         return self.forward_full(cv)
 
-    def _live_geometry_ok(self, cv):
+    def live_ok(self, n):
+        """forward_live applies (eval BN, live_region on, the module's padding derived from n)."""
+        return self.live_region and not self._bn_uses_batch_stats() and self._live_geometry_ok(n)
+
+    def _live_geometry_ok(self, n):
         """forward_live relies on every U-Net level having the cost volume's extent n, which holds
         when the module's padding is the one config.py:20-21 derives from n.  A module built for
         another D or resolution takes forward_full, which (like the reference) then fails with the
         shape mismatch at the level sums instead of returning wrongly indexed levels."""
         from .config import pad_outpad
-        return (self.pad, self.outpad) == pad_outpad(*cv.shape[2:])
+        return (self.pad, self.outpad) == pad_outpad(*n)
 
     def _bn_uses_batch_stats(self):
         return any(bn.training or bn.running_mean is None
@@ -124,18 +135,16 @@ class CostVolumeReg(nn.Module):
         (batch statistics over the whole volume, test.py:61) uses forward_full.
         """
         act = lambda bn, y: self.ReLU(bn(y))
-        n = tuple(cv.shape[2:])
+        c4 = cv.dim() == 6          # channel-quad cost volume (HIP path only, see forward)
+        n = tuple(cv.shape[2:5])
         full = tuple((0, d - 1) for d in n)
         B = _tconv_input_region(full, n, self.pad)
         C2 = _tconv_input_region(B, n, self.pad)
         C3 = _tconv_input_region(C2, n, self.pad)
-        if _hip_inference(cv):   # conv_0_0 -> BN_0 -> ReLU in one HIP kernel
-            from .ops import conv3d_k3
-            bn = self.BN_0
-            y0 = conv3d_k3(cv, self.conv_0_0.weight, bn.weight / torch.sqrt(bn.running_var + bn.eps),
-                           bn.bias, bn.running_mean)
-        else:
-            y0 = act(self.BN_0, self.conv_0_0(cv))
+        if _hip_inference(cv):
+            return self._forward_live_hip(cv, n, B, C2, C3, c4)
+        # torch layers (CPU, autograd): the same regions through PyTorch's convolutions
+        y0 = act(self.BN_0, self.conv_0_0(cv))
         # level 1 on B, level 2 on C2, level 3 on C3 (regions carry their origin in the volume)
         lv = []
         for conv_a, conv_b, bn, reg in ((self.conv_1_0, self.conv_1_1, self.BN_1, B),
@@ -147,16 +156,41 @@ class CostVolumeReg(nn.Module):
         y1, y2, y3 = lv
         y3 = act(self.BN_2, _tconv_region(y3, C3, self.deconv_3_0.weight, C2, self.pad))
         y2 = act(self.BN_1, _tconv_region(y3 + y2, C2, self.deconv_2_0.weight, B, self.pad))
-        if _hip_inference(cv):
-            # deconv_1_0 -> BN_0 -> ReLU -> + y0 in one HIP kernel (csrc/deconv3d_region.hip)
-            from .ops import deconv3d_k3s2
-            bn = self.BN_0
-            scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
-            z = deconv3d_k3s2(y2 + y1, [lo for lo, _ in B], self.deconv_1_0.weight, list(n),
-                              list(self.pad), scale, bn.bias, bn.running_mean, y0)
-        else:
-            z = act(self.BN_0, _tconv_region(y2 + y1, B, self.deconv_1_0.weight, full, self.pad)) + y0
-        return self.Norm(_narrow_conv(self.conv_out, z))
+        z = act(self.BN_0, _tconv_region(y2 + y1, B, self.deconv_1_0.weight, full, self.pad)) + y0
+        return self.Norm(self.conv_out(z))
+
+    def _forward_live_hip(self, cv, n, B, C2, C3, c4=False):
+        """forward_live on the HIP kernels: conv_0_0 (csrc/conv3d_narrow.hip), every region conv
+        and transposed conv on the fp32 MFMA with channels-last region tensors and the eval BN +
+        ReLU fused (csrc/conv3d_region.hip), deconv_1_0 + BN_0 + ReLU + `+ y0` and the `y2 + y1`
+        sum in one kernel (csrc/deconv3d_region.hip), conv_out (conv3d_narrow.hip).  ``c4``: cv is
+        the channel-quad volume, read by conv_0_0 and the three stride-2 convs with 16-byte loads."""
+        from .ops import CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_region, deconv3d_k3s2, region_weight
+        org = lambda reg: [lo for lo, _ in reg]
+        size = lambda reg: [hi - lo + 1 for lo, hi in reg]
+        dims, pad = list(n), list(self.pad)
+
+        def bn_eval(bn):
+            return bn.weight / torch.sqrt(bn.running_var + bn.eps), bn.bias, bn.running_mean
+
+        y0 = conv3d_k3(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), in_c4=c4)
+        lv = []
+        for conv_a, conv_b, bn, reg in ((self.conv_1_0, self.conv_1_1, self.BN_1, B),
+                                        (self.conv_2_0, self.conv_2_1, self.BN_2, C2),
+                                        (self.conv_3_0, self.conv_3_1, self.BN_3, C3)):
+            halo = _grow(reg, n, 1)
+            ya = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(halo), size(halo), None,
+                               None, pad, *bn_eval(bn), in_c4=c4)
+            # level 1's output only feeds deconv_1_0's input sum: channels-first for its loads
+            lv.append(conv3d_region(ya, None, region_weight(conv_b), CONV_S1, dims, org(reg), size(reg),
+                                    org(halo), size(halo), None, *bn_eval(bn), out_ncdhw=reg is B))
+        y1, y2, y3 = lv
+        y3 = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, org(C2), size(C2), org(C3),
+                           size(C3), pad, *bn_eval(self.BN_2))
+        y2 = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, org(B), size(B), org(C2),
+                           size(C2), pad, *bn_eval(self.BN_1), out_ncdhw=True)
+        z = deconv3d_k3s2(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0, x2=y1)
+        return self.Norm(conv3d_k3(z, self.conv_out.weight))
 
     def forward_full(self, cv):
         act = lambda bn, y: self.ReLU(bn(y))
@@ -301,10 +335,16 @@ class MVSNet(nn.Module):
         device = nn_input.device
         feature_maps = self.feature_encoder(nn_input)
         bf16 = c.cv_dtype == "bfloat16"
+        reg = self.cost_volume_reg
+        # fp32 HIP inference on the live path: the cost volume goes straight to the regulariser's
+        # kernels in the channel-quad layout (ops.cost_volume_c4, the fused kernel's 16-byte store)
+        quads = (not bf16 and _hip_inference(feature_maps) and 2 <= n_views <= 8
+                 and feature_maps.shape[1] % 4 == 0
+                 and reg.live_ok((c.d_num,) + tuple(feature_maps.shape[2:])))
         cost_volume, d_batch, ref_views = warp_and_assemble_cost_volume(
             K_batch, R_batch, T_batch, d_min, d_int, feature_maps, batch_size, n_views,
             d_num=c.d_num, d_scale=c.d_scale,
-            cv_dtype=torch.bfloat16 if bf16 else torch.float32)
+            cv_dtype=torch.bfloat16 if bf16 else torch.float32, channel_quads=quads)
         if bf16:   # opt-in: regulariser under bf16 autocast, fp32 probabilities
             with torch.autocast(device.type, dtype=torch.bfloat16):
                 prob_volume = self.cost_volume_reg(cost_volume).float()

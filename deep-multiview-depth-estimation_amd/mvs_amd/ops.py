@@ -2,6 +2,7 @@
 
   mvs::cost_volume            fused warp + variance      (homography.py:6-92 + costvolume.py:3-16)
   mvs::cost_volume_bf16       same, bf16 cost volume     (SURVEY.md §8 f3, opt-in)
+  mvs::cost_volume_c4         same, channel-quad layout  (inference feed of the HIP regulariser)
   mvs::cost_volume_backward   d cv / d feat              (autograd of the above, train.py:103)
   mvs::homography_warp        warp only                  (homography.py:6-92 warped volume)
   mvs::assemble_cost_volume   variance of a warped volume (costvolume.py:3-16)
@@ -11,6 +12,7 @@ Every op requires CUDA(HIP) tensors and raises otherwise: there is no CPU path i
 Camera tensors (K, R, T, d_min, d_int) are moved to the feature device here, as the reference
 does with ``.to(DEVICE)`` (homography.py:25,43-58).
 """
+import ctypes
 from typing import Optional
 
 import torch
@@ -115,6 +117,38 @@ def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scal
     n, c, h, w = feat.shape
     return (feat.new_empty((batch_size, c, d_count, h, w), dtype=torch.bfloat16),
             feat.new_empty((_ws_floats(batch_size, n_views, c, h, w, d_count),)))
+
+
+@torch.library.custom_op("mvs::cost_volume_c4", mutates_args=())
+def cost_volume_c4(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.Tensor,
+                   d_min: torch.Tensor, d_int: torch.Tensor, batch_size: int, n_views: int,
+                   d_begin: int, d_count: int, d_scale: float) -> torch.Tensor:
+    """mvs::cost_volume in the channel-quad layout cv[B][C/4][d_count][h][w][4] (the same values:
+    cv_c4[b, q, d, y, x, j] == cv[b, 4q + j, d, y, x]), what conv3d_k3 / conv3d_region (CONV_S2)
+    read with in_c4=True.  Inference only (no autograd formula), 2 <= n_views <= 8, C % 4 == 0."""
+    _require_gpu(feat, "feature_maps")
+    lib = _lib.load()
+    feat = feat.to(_F32).contiguous()
+    K, R, T, d_min, d_int = _cams(K, R, T, d_min, d_int, feat.device, batch_size)
+    _check_geometry(feat, K, batch_size, n_views)
+    n, c, h, w = feat.shape
+    if c % 4:
+        raise ValueError("the channel-quad cost volume needs C % 4 == 0, got C=%d" % c)
+    cv = torch.empty((batch_size, c // 4, d_count, h, w, 4), device=feat.device, dtype=_F32)
+    ws = torch.empty((_ws_floats(batch_size, n_views, c, h, w, d_count),), device=feat.device,
+                     dtype=_F32)
+    st = lib.mvs_cost_volume_fwd_c4(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T),
+                                    _lib.ptr(d_min), _lib.ptr(d_int), batch_size, n_views, c, h, w,
+                                    d_begin, d_count, float(d_scale), _lib.ptr(ws), _lib.ptr(cv),
+                                    _lib.stream_handle(feat.device), None, None)
+    _lib.check(st, "mvs_cost_volume_fwd_c4")
+    return cv
+
+
+@cost_volume_c4.register_fake
+def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scale):
+    n, c, h, w = feat.shape
+    return feat.new_empty((batch_size, c // 4, d_count, h, w, 4))
 
 
 @torch.library.custom_op("mvs::cost_volume_backward", mutates_args=())
@@ -305,35 +339,44 @@ torch.library.register_autograd("mvs::extract_depth_map", _sam_backward, setup_c
 # ----------------------------------------------------------------------------------------------
 @torch.library.custom_op("mvs::conv3d_k3", mutates_args=())
 def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Tensor] = None,
-              bn_shift: Optional[torch.Tensor] = None, bn_mean: Optional[torch.Tensor] = None) -> torch.Tensor:
+              bn_shift: Optional[torch.Tensor] = None, bn_mean: Optional[torch.Tensor] = None,
+              in_c4: bool = False) -> torch.Tensor:
     """nn.Conv3d(c_in, c_out, 3, stride=1, padding=1, bias=False) forward, c_out in {1, 8}, fp32
     NCDHW, on the HIP kernel (csrc/conv3d_narrow.hip); with bn_* given, max((y - mean) * scale +
-    shift, 0) is fused (eval BN + ReLU).  Inference only (no autograd formula): CostVolumeReg
-    uses it on the eval-mode, no-grad path."""
+    shift, 0) is fused (eval BN + ReLU).  ``in_c4``: x is the channel-quad [B, Cin/4, D, H, W, 4]
+    of cost_volume_c4.  Inference only (no autograd formula): CostVolumeReg uses it on the
+    eval-mode, no-grad path."""
     _require_gpu(x, "x")
     lib = _lib.load()
-    if x.dim() != 5 or weight.dim() != 5 or tuple(weight.shape[2:]) != (3, 3, 3) or weight.shape[1] != x.shape[1]:
-        raise ValueError("x [B, Cin, D, H, W] and weight [Cout, Cin, 3, 3, 3] expected, got %s / %s"
-                         % (tuple(x.shape), tuple(weight.shape)))
+    if in_c4:
+        if x.dim() != 6 or x.shape[-1] != 4:
+            raise ValueError("in_c4: x [B, Cin/4, D, H, W, 4] expected, got %s" % (tuple(x.shape),))
+        b, c4, d, h, wd, _ = x.shape
+        cin = 4 * c4
+    else:
+        if x.dim() != 5:
+            raise ValueError("x [B, Cin, D, H, W] expected, got %s" % (tuple(x.shape),))
+        b, cin, d, h, wd = x.shape
+    if weight.dim() != 5 or tuple(weight.shape[2:]) != (3, 3, 3) or weight.shape[1] != cin:
+        raise ValueError("weight [Cout, %d, 3, 3, 3] expected, got %s" % (cin, tuple(weight.shape)))
     x = x.to(_F32).contiguous()
     cout = weight.shape[0]
     # the kernel reads weight[c_in][3][3][3][c_out] (pairs of output channels per 8-byte load)
     w = weight.to(device=x.device, dtype=_F32).permute(1, 2, 3, 4, 0).contiguous()
-    b, cin, d, h, wd = x.shape
     bn = [t if t is None else t.to(device=x.device, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
     if any(t is None for t in bn) and not all(t is None for t in bn):
         raise ValueError("bn_scale, bn_shift and bn_mean go together")
     bp = [None if t is None else _lib.ptr(t) for t in bn]
     y = torch.empty((b, cout, d, h, wd), device=x.device, dtype=_F32)
-    st = lib.mvs_conv3d_k3_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), b, cin, cout, d, h, wd, *bp,
-                               _lib.stream_handle(x.device))
+    st = lib.mvs_conv3d_k3_fwd(_lib.ptr(x), _lib.MVS_CONV_IN_C4 if in_c4 else 0, _lib.ptr(w), _lib.ptr(y),
+                               b, cin, cout, d, h, wd, *bp, _lib.stream_handle(x.device))
     _lib.check(st, "mvs_conv3d_k3_fwd")
     return y
 
 
 @conv3d_k3.register_fake
-def _(x, weight, bn_scale=None, bn_shift=None, bn_mean=None):
-    return x.new_empty((x.shape[0], weight.shape[0]) + tuple(x.shape[2:]))
+def _(x, weight, bn_scale=None, bn_shift=None, bn_mean=None, in_c4=False):
+    return x.new_empty((x.shape[0], weight.shape[0]) + tuple(x.shape[2:5]))
 
 
 # ----------------------------------------------------------------------------------------------
@@ -342,14 +385,23 @@ def _(x, weight, bn_scale=None, bn_shift=None, bn_mean=None):
 @torch.library.custom_op("mvs::deconv3d_k3s2", mutates_args=())
 def deconv3d_k3s2(x: torch.Tensor, origin: list[int], weight: torch.Tensor, out_dims: list[int],
                   pad: list[int], bn_scale: torch.Tensor, bn_shift: torch.Tensor,
-                  bn_mean: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:
-    """ConvTranspose3d(c_in, 8, 3, stride 2, padding pad) of the region tensor x (input region
-    starting at `origin`) into the full volume out_dims, then max((y - mean) * scale + shift, 0)
-    + residual (csrc/deconv3d_region.hip).  Inference only."""
+                  bn_mean: torch.Tensor, residual: torch.Tensor, x2: Optional[torch.Tensor] = None,
+                  channels_last: bool = False) -> torch.Tensor:
+    """ConvTranspose3d(c_in, 8, 3, stride 2, padding pad) of the region tensor x (+ x2) (input region
+    starting at `origin`; [B, c_in, r...] or, channels_last, [B, r..., c_in]) into the full volume
+    out_dims, then max((y - mean) * scale + shift, 0) + residual (csrc/deconv3d_region.hip).
+    Inference only."""
     _require_gpu(x, "x")
     lib = _lib.load()
     x = x.to(_F32).contiguous()
-    b, cin, rd, rh, rw = x.shape
+    if channels_last:
+        b, rd, rh, rw, cin = x.shape
+    else:
+        b, cin, rd, rh, rw = x.shape
+    if x2 is not None:
+        x2 = x2.to(_F32).contiguous()
+        if x2.shape != x.shape:
+            raise ValueError("x2 must have x's shape")
     w = weight.to(device=x.device, dtype=_F32).contiguous()
     if tuple(w.shape) != (cin, 8, 3, 3, 3):
         raise ValueError("weight [c_in, 8, 3, 3, 3] expected, got %s" % (tuple(w.shape),))
@@ -359,13 +411,77 @@ def deconv3d_k3s2(x: torch.Tensor, origin: list[int], weight: torch.Tensor, out_
     if tuple(res.shape) != (b, 8, d, h, wd):
         raise ValueError("residual must be [B, 8, D, H, W]")
     y = torch.empty((b, 8, d, h, wd), device=x.device, dtype=_F32)
-    st = lib.mvs_deconv3d_k3s2_fwd(_lib.ptr(x), b, cin, 8, rd, rh, rw, *origin, _lib.ptr(w), d, h, wd,
-                                   *pad, _lib.ptr(sc), _lib.ptr(sh), _lib.ptr(mu), _lib.ptr(res),
-                                   _lib.ptr(y), _lib.stream_handle(x.device))
+    st = lib.mvs_deconv3d_k3s2_fwd(_lib.ptr(x), None if x2 is None else _lib.ptr(x2),
+                                   _lib.MVS_LAYOUT_CHANNELS_LAST if channels_last else 0, b, cin, 8, rd, rh,
+                                   rw, *origin, _lib.ptr(w), d, h, wd, *pad, _lib.ptr(sc), _lib.ptr(sh),
+                                   _lib.ptr(mu), _lib.ptr(res), _lib.ptr(y), _lib.stream_handle(x.device))
     _lib.check(st, "mvs_deconv3d_k3s2_fwd")
     return y
 
 
 @deconv3d_k3s2.register_fake
-def _(x, origin, weight, out_dims, pad, bn_scale, bn_shift, bn_mean, residual):
+def _(x, origin, weight, out_dims, pad, bn_scale, bn_shift, bn_mean, residual, x2=None, channels_last=False):
     return x.new_empty((x.shape[0], 8) + tuple(out_dims))
+
+
+# ----------------------------------------------------------------------------------------------
+# mvs::conv3d_region -- the regulariser's region convolutions on the fp32 MFMA (model.py:101-121)
+# ----------------------------------------------------------------------------------------------
+CONV_S1, CONV_S2, CONV_T2 = _lib.MVS_CONV_S1, _lib.MVS_CONV_S2, _lib.MVS_CONV_T2
+
+
+def region_weight(module):
+    """weight[27][c_out][c_in] of an nn.Conv3d / nn.ConvTranspose3d (mvs_conv3d_region_fwd layout)."""
+    w = module.weight
+    if isinstance(module, torch.nn.ConvTranspose3d):
+        return w.permute(2, 3, 4, 1, 0).reshape(27, w.shape[1], w.shape[0]).contiguous()
+    return w.permute(2, 3, 4, 0, 1).reshape(27, w.shape[0], w.shape[1]).contiguous()
+
+
+def _ints3(v):
+    return (ctypes.c_int * 3)(*[int(a) for a in v])
+
+
+@torch.library.custom_op("mvs::conv3d_region", mutates_args=())
+def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Tensor, mode: int,
+                  dims: list[int], out_origin: list[int], out_size: list[int],
+                  in_origin: Optional[list[int]], in_size: Optional[list[int]], pad: Optional[list[int]],
+                  bn_scale: Optional[torch.Tensor] = None, bn_shift: Optional[torch.Tensor] = None,
+                  bn_mean: Optional[torch.Tensor] = None, out_ncdhw: bool = False,
+                  in_c4: bool = False) -> torch.Tensor:
+    """Region convolution (mvs_conv3d_region_fwd): mode CONV_S2 reads the full NCDHW volume x
+    (in_c4: the channel-quad [B, C/4, D, H, W, 4] of cost_volume_c4),
+    CONV_S1 / CONV_T2 a channels-last region tensor x (+ x2) on in_origin + [0, in_size); returns the
+    channels-last region tensor [B, *out_size, c_out] ([B, c_out, *out_size] with out_ncdhw), eval
+    BN + ReLU fused when bn_* are given.  ``weight`` is region_weight(module).  Inference only."""
+    _require_gpu(x, "x")
+    lib = _lib.load()
+    x = x.to(_F32).contiguous()
+    if x2 is not None:
+        x2 = x2.to(_F32).contiguous()
+    w = weight.to(device=x.device, dtype=_F32).contiguous()
+    _, cout, cin = w.shape
+    b = x.shape[0]
+    bn = [t if t is None else t.to(device=x.device, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
+    if any(t is None for t in bn) and not all(t is None for t in bn):
+        raise ValueError("bn_scale, bn_shift and bn_mean go together")
+    shape = (b, cout) + tuple(out_size) if out_ncdhw else (b,) + tuple(out_size) + (cout,)
+    y = torch.empty(shape, device=x.device, dtype=_F32)
+    flags = (_lib.MVS_CONV_OUT_NCDHW if out_ncdhw else 0) | (_lib.MVS_CONV_IN_C4 if in_c4 else 0)
+    st = lib.mvs_conv3d_region_fwd(int(mode), flags, _lib.ptr(x), None if x2 is None else _lib.ptr(x2), _lib.ptr(w),
+                                   _lib.ptr(y), b, cin, cout, _ints3(dims), _ints3(out_origin), _ints3(out_size),
+                                   None if in_origin is None else _ints3(in_origin),
+                                   None if in_size is None else _ints3(in_size),
+                                   None if pad is None else _ints3(pad),
+                                   *[None if t is None else _lib.ptr(t) for t in bn],
+                                   _lib.stream_handle(x.device))
+    _lib.check(st, "mvs_conv3d_region_fwd")
+    return y
+
+
+@conv3d_region.register_fake
+def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, bn_scale=None, bn_shift=None,
+      bn_mean=None, out_ncdhw=False, in_c4=False):
+    if out_ncdhw:
+        return x.new_empty((x.shape[0], weight.shape[1]) + tuple(out_size))
+    return x.new_empty((x.shape[0],) + tuple(out_size) + (weight.shape[1],))

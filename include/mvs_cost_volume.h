@@ -109,6 +109,21 @@ int mvs_cost_volume_fwd_bf16(const float* feat, const float* K, const float* R, 
                              float* workspace, void* cv_out, void* stream);
 
 /*
+ * mvs_cost_volume_fwd writing the channel-quad layout cv_out[B][ceil(C/4)][d_count][h][w][4] (fp32,
+ * channel 4q + j in component j, padded channels 0; 16-byte aligned): the same values, one 16-byte
+ * store per (pixel, plane, 4 channels).  The layout MVSNet.forward's inference path hands to the
+ * regulariser's HIP layers (mvs_conv3d_k3_fwd / mvs_conv3d_region_fwd with c4 input), which read 4
+ * channels of a voxel per load.  Events as mvs_cost_volume_fwd_timed (either may be NULL).
+ * 2 <= n_views <= 8 (else MVS_ERR_UNSUPPORTED_VIEWS) or n_views == 1 (zeros).
+ */
+int mvs_cost_volume_fwd_c4(const float* feat, const float* K, const float* R, const float* T,
+                           const float* d_min, const float* d_int,
+                           int batch_size, int n_views, int channels, int h, int w,
+                           int d_begin, int d_count, float d_scale,
+                           float* workspace, float* cv_out, void* stream,
+                           void* main_begin_event, void* main_end_event);
+
+/*
  * Warp only (API-compatible homography_warping, homography.py:6-92):
  * warped[N][C][d_count][h][w].  Same workspace contract as mvs_cost_volume_fwd.
  */
@@ -182,9 +197,14 @@ int mvs_normalize_images(const unsigned char* rgb, int n_images, int h, int w, c
  */
 int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float* out, void* stream);
 
+/* input-layout flag of mvs_conv3d_k3_fwd / mvs_conv3d_region_fwd (MVS_CONV_S2): the volume is
+ * channel-quad x[batch][c_in/4][D][H][W][4], the layout of mvs_cost_volume_fwd_c4 */
+#define MVS_CONV_IN_C4 2
+
 /* Regulariser layers conv_0_0 (32 -> 8) and conv_out (8 -> 1) of CostVolumeReg (model.py:77,96 /
  * forward at model.py:101,123): nn.Conv3d(c_in, c_out, 3, stride=1, padding=1, bias=False) over
- * x[batch][c_in][d][h][w] fp32 into y[batch][c_out][d][h][w], with the weight TRANSPOSED to
+ * x[batch][c_in][d][h][w] fp32 (flags = MVS_CONV_IN_C4: the channel-quad x[batch][c_in/4][d][h][w][4]
+ * of mvs_cost_volume_fwd_c4, 16-byte aligned) into y[batch][c_out][d][h][w], with the weight TRANSPOSED to
  * weight[c_in][3][3][3][c_out] (nn.Conv3d's weight.permute(1, 2, 3, 4, 0): pairs of output channels
  * are adjacent, one 8-byte scalar load feeds a packed fp32 FMA).
  * c_out must be 1 or 8 (MVS_ERR_INVALID_ARGUMENT otherwise); d*h*w < 2^31.  Optional epilogue
@@ -192,22 +212,59 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
  * 0), the eval BN + ReLU that follows conv_0_0 (model.py:101; bn_scale = gamma / sqrt(var + eps),
  * bn_shift = beta).  Replaces the MIOpen convolution behind torch.nn.Conv3d.forward for these two
  * layers in eval-mode inference; same products per output, fp32 summation order differs. */
-int mvs_conv3d_k3_fwd(const float* x, const float* weight, float* y, int batch, int c_in, int c_out,
-                      int d, int h, int w, const float* bn_scale, const float* bn_shift,
+int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, int batch, int c_in,
+                      int c_out, int d, int h, int w, const float* bn_scale, const float* bn_shift,
                       const float* bn_mean, void* stream);
+
+/* layout flag of mvs_deconv3d_k3s2_fwd: the region input is channels-last x[batch][rd][rh][rw][c_in] */
+#define MVS_LAYOUT_CHANNELS_LAST 1
 
 /* Regulariser layer deconv_1_0 (model.py:87, forward at model.py:121): nn.ConvTranspose3d(c_in, 8,
  * 3, stride=2, padding=(pd, ph, pw), output_padding, bias=False) into the full volume
- * y[batch][8][d][h][w], from a REGION input x[batch][c_in][rd][rh][rw] holding the input on
- * [x0, x0 + r) per dim (it must hold every input that reaches [0, n): CostVolumeReg.forward_live).
- * weight[c_in][8][3][3][3] (ConvTranspose layout), c_in <= 64.  Optional epilogue (all three
- * BN pointers or none; residual nullable): y = max((y - bn_mean) * bn_scale + bn_shift, 0)
- * + residual, i.e. model.py:121-123's ReLU(BN_0(.)) and `+ y0` (eval BN: bn_scale =
- * gamma / sqrt(var + eps), bn_shift = beta).  Eval-mode inference only. */
-int mvs_deconv3d_k3s2_fwd(const float* x, int batch, int c_in, int c_out, int rd, int rh, int rw,
-                          int x0d, int x0h, int x0w, const float* weight, int d, int h, int w,
-                          int pd, int ph, int pw, const float* bn_scale, const float* bn_shift,
-                          const float* bn_mean, const float* residual, float* y, void* stream);
+ * y[batch][8][d][h][w], from a REGION input holding the input on [x0, x0 + r) per dim (it must hold
+ * every input that reaches [0, n): CostVolumeReg.forward_live): x[batch][c_in][rd][rh][rw], or
+ * channels-last x[batch][rd][rh][rw][c_in] with flags = MVS_LAYOUT_CHANNELS_LAST; x2 (nullable, same
+ * layout) is added to x on load (model.py:121's `y2 + y1`).  weight[c_in][8][3][3][3]
+ * (ConvTranspose layout), c_in <= 64.  Optional epilogue (all three BN pointers or none; residual
+ * nullable): y = max((y - bn_mean) * bn_scale + bn_shift, 0) + residual, i.e. model.py:121-123's
+ * ReLU(BN_0(.)) and `+ y0` (eval BN: bn_scale = gamma / sqrt(var + eps), bn_shift = beta).
+ * Eval-mode inference only. */
+int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch, int c_in, int c_out,
+                          int rd, int rh, int rw, int x0d, int x0h, int x0w, const float* weight, int d,
+                          int h, int w, int pd, int ph, int pw, const float* bn_scale,
+                          const float* bn_shift, const float* bn_mean, const float* residual, float* y,
+                          void* stream);
+
+/* mvs_conv3d_region_fwd modes */
+#define MVS_CONV_S1 0   /* Conv3d 3x3x3, stride 1, padding 1: region -> region                     */
+#define MVS_CONV_S2 1   /* Conv3d 3x3x3, stride 2, padding pad: full NCDHW volume -> region         */
+#define MVS_CONV_T2 2   /* ConvTranspose3d 3x3x3, stride 2, padding pad: region (+ x2) -> region   */
+/* mvs_conv3d_region_fwd flags */
+#define MVS_CONV_OUT_NCDHW 1   /* output region tensor channels-first y[batch][c_out][size...]   */
+/* (and MVS_CONV_IN_C4, above: an MVS_CONV_S2 input volume in the channel-quad layout) */
+
+/* The regulariser's region convolutions (CostVolumeReg, model.py:76-95, forward at model.py:101-121,
+ * evaluated on their live regions: DESIGN.md §5a) on the fp32 matrix cores, with the following eval
+ * BatchNorm + ReLU fused (all three BN pointers, c_out floats each, or none):
+ *   y = max((conv(x) - bn_mean) * bn_scale + bn_shift, 0).
+ * The volume is dims[3] = (D, H, W); the output is the channels-last region tensor
+ * y[batch][out_size[0]][out_size[1]][out_size[2]][c_out] holding voxels out_origin + [0, out_size)
+ * (flags = MVS_CONV_OUT_NCDHW: channels-first y[batch][c_out][out_size...]).
+ * Input: MVS_CONV_S2 the full cost volume x[batch][c_in][D][H][W] (reads 2 o - pad + t, zero outside
+ * the volume); MVS_CONV_S1 / MVS_CONV_T2 a channels-last region tensor
+ * x[batch][in_size...][c_in] on in_origin + [0, in_size) (S1: o + t - 1; T2: i = (o + pad - t) / 2 for
+ * t of o + pad's parity; voxels outside the volume or the input region read zero), plus x2 (same
+ * geometry, nullable) added on load.  Weights transposed to weight[27][c_out][c_in] (tap =
+ * (kd * 3 + kh) * 3 + kw): nn.Conv3d's weight.permute(2, 3, 4, 0, 1), nn.ConvTranspose3d's
+ * weight.permute(2, 3, 4, 1, 0).  Supported (mode, c_in, c_out): S2 (32, 16|32|64), S1 (16, 16),
+ * (32, 32), (64, 64), T2 (64, 32), (32, 16); else MVS_ERR_INVALID_ARGUMENT.  dims, origins, sizes and
+ * pad are HOST pointers to 3 ints.  Eval-mode inference only; products summed in the order (tap,
+ * c_in) -- MIOpen sums them in other orders (fp32 rounding-level differences). */
+int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, const float* weight, float* y,
+                          int batch, int c_in, int c_out, const int* dims, const int* out_origin,
+                          const int* out_size, const int* in_origin, const int* in_size,
+                          const int* pad, const float* bn_scale, const float* bn_shift,
+                          const float* bn_mean, void* stream);
 
 #ifdef __cplusplus
 }

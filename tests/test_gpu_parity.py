@@ -529,3 +529,205 @@ def test_region_deconv_fused_epilogue_matches_torch():
                                 dev(gamma / torch.sqrt(var + 1e-5)), dev(beta), dev(mean), dev(y0))
         assert out.shape == ref.shape
         torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+
+
+def _bn_params(c, g):
+    mean, var = torch.randn(c, generator=g) * 0.1, torch.rand(c, generator=g) + 0.5
+    gamma, beta = torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1
+    return gamma / torch.sqrt(var + 1e-5), beta, mean
+
+
+def _bn_relu(y, sc, sh, mu):
+    v = lambda t: t.view(1, -1, 1, 1, 1).to(y)
+    return torch.relu((y - v(mu)) * v(sc) + v(sh))
+
+
+@pytest.mark.parametrize("mode,cin,cout,ncdhw", [(1, 32, 16, False), (1, 32, 32, False), (1, 32, 64, False),
+                                                 (0, 16, 16, False), (0, 32, 32, False), (0, 64, 64, False),
+                                                 (2, 64, 32, False), (2, 32, 16, False), (0, 16, 16, True),
+                                                 (2, 32, 16, True)])
+def test_region_conv_matches_torch(mode, cin, cout, ncdhw):
+    """mvs::conv3d_region (csrc/conv3d_region.hip, the regulariser's region convs on the fp32 MFMA)
+    at the live regions forward_live uses (cfg-1-like volume 24 x 20 x 26 -- odd and even dims,
+    both parities of P; the S2 tile is cut by the region border in every dim), channels-last and
+    channels-first outputs, against torch's conv on the zero-extended tensors in float64 (CPU) and in
+    fp32 on the same device: max error <= 1e-5 of the output scale and <= 4x MIOpen's own."""
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _grow, _tconv_input_region
+    from mvs_amd.ops import conv3d_region
+    import torch.nn.functional as F
+    n = (24, 20, 26)
+    pad, outpad = pad_outpad(*n)
+    full = tuple((0, d - 1) for d in n)
+    Bx = _tconv_input_region(full, n, pad)
+    C2 = _tconv_input_region(Bx, n, pad)
+    g = torch.Generator().manual_seed(mode * 100 + cin + cout)
+    sc, sh, mu = _bn_params(cout, g)
+    org = lambda r: [lo for lo, _ in r]
+    size = lambda r: [hi - lo + 1 for lo, hi in r]
+    sl = lambda r: (slice(None), slice(None)) + tuple(slice(lo, hi + 1) for lo, hi in r)
+    cl = lambda t: t.permute(0, 2, 3, 4, 1).contiguous()
+
+    def zero_ext(reg, c):
+        t = torch.zeros(2, c, *n)
+        t[sl(reg)] = torch.randn(2, c, *size(reg), generator=g)
+        return t
+
+    if mode == 1:      # S2: conv_k_0 from the full cost volume onto halo(B)
+        out_reg = _grow(Bx, n, 1)
+        x = torch.randn(2, cin, *n, generator=g)
+        wt = torch.randn(cout, cin, 3, 3, 3, generator=g) * 0.1
+        f = lambda xx, ww: F.conv3d(xx, ww, stride=2, padding=pad)
+        args = lambda xd: (xd, None, None, None)
+        in_reg = None
+    elif mode == 0:    # S1: conv_k_1 on B from halo(B)
+        out_reg, in_reg = Bx, _grow(Bx, n, 1)
+        x = zero_ext(in_reg, cin)
+        wt = torch.randn(cout, cin, 3, 3, 3, generator=g) * 0.1
+        f = lambda xx, ww: F.conv3d(xx, ww, padding=1)
+    else:              # T2: deconv from C2 (+ addend) onto B
+        out_reg, in_reg = Bx, C2
+        x, x2 = zero_ext(in_reg, cin), zero_ext(in_reg, cin)
+        wt = torch.randn(cin, cout, 3, 3, 3, generator=g) * 0.1
+        f = lambda xx, ww: F.conv_transpose3d(xx, ww, stride=2, padding=pad, output_padding=outpad)
+    xin = x + x2 if mode == 2 else x
+    ref64 = _bn_relu(f(xin.double(), wt.double()), sc.double(), sh.double(), mu.double())[sl(out_reg)]
+    with torch.no_grad():
+        reft = _bn_relu(f(xin.to(DEV), wt.to(DEV)), sc, sh, mu)[sl(out_reg)].cpu()
+        conv = torch.nn.ConvTranspose3d(cin, cout, 3) if mode == 2 else torch.nn.Conv3d(cin, cout, 3)
+        conv.weight.data = wt
+        from mvs_amd.ops import region_weight
+        w27 = region_weight(conv).to(DEV)
+        if mode == 1:
+            y = conv3d_region(x.to(DEV), None, w27, mode, list(n), org(out_reg), size(out_reg), None, None,
+                              list(pad), sc.to(DEV), sh.to(DEV), mu.to(DEV), out_ncdhw=ncdhw)
+        else:
+            xr = cl(x[sl(in_reg)]).to(DEV)
+            x2r = cl(x2[sl(in_reg)]).to(DEV) if mode == 2 else None
+            y = conv3d_region(xr, x2r, w27, mode, list(n), org(out_reg), size(out_reg), org(in_reg),
+                              size(in_reg), list(pad), sc.to(DEV), sh.to(DEV), mu.to(DEV), out_ncdhw=ncdhw)
+    y = (y if ncdhw else y.permute(0, 4, 1, 2, 3)).cpu()
+    assert y.shape == ref64.shape, (y.shape, ref64.shape)
+    scale = ref64.abs().max().item()
+    err = (y.double() - ref64).abs().max().item()
+    err_t = (reft.double() - ref64).abs().max().item()
+    assert err <= 1e-5 * scale, (err, scale)
+    assert err <= 4 * err_t + 1e-6 * scale, (err, err_t)
+
+
+def test_region_deconv_channels_last_with_addend():
+    """deconv_1_0's HIP kernel reading the channels-last region sum y2 + y1 (model.py:121) equals
+    its NCDHW form on the pre-added input (same arithmetic: the sum is formed on load)."""
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _tconv_input_region
+    from mvs_amd.ops import deconv3d_k3s2
+    n = (13, 10, 17)
+    pad, _ = pad_outpad(*n)
+    reg = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
+    g = torch.Generator().manual_seed(5)
+    r = [hi - lo + 1 for lo, hi in reg]
+    a, b = torch.randn(2, 16, *r, generator=g).to(DEV), torch.randn(2, 16, *r, generator=g).to(DEV)
+    wt = (torch.randn(16, 8, 3, 3, 3, generator=g) * 0.1).to(DEV)
+    sc, sh, mu = (t.to(DEV) for t in _bn_params(8, g))
+    y0 = torch.randn(2, 8, *n, generator=g).to(DEV)
+    with torch.no_grad():
+        ref = deconv3d_k3s2(a + b, [lo for lo, _ in reg], wt, list(n), list(pad), sc, sh, mu, y0)
+        got = deconv3d_k3s2(a.permute(0, 2, 3, 4, 1).contiguous(), [lo for lo, _ in reg], wt, list(n), list(pad),
+                            sc, sh, mu, y0, x2=b.permute(0, 2, 3, 4, 1).contiguous(), channels_last=True)
+    assert torch.equal(got, ref)
+
+
+def _to_c4(x):
+    """[B, C, D, H, W] -> channel-quad [B, C/4, D, H, W, 4]."""
+    b, c = x.shape[:2]
+    return x.reshape((b, c // 4, 4) + tuple(x.shape[2:])).permute(0, 1, 3, 4, 5, 2).contiguous()
+
+
+@pytest.mark.parametrize("nv,shape", [(3, (2, 32, 24, 64, 80)), (2, (1, 8, 7, 37, 53)), (5, (1, 16, 9, 20, 36)),
+                                      (8, (1, 4, 3, 16, 16))])
+def test_channel_quad_cost_volume_is_the_same_values(nv, shape):
+    """mvs::cost_volume_c4 (the fused kernel's 16-byte channel-quad store) holds exactly the values
+    of mvs::cost_volume: bit-equal after the layout permutation, also for a depth shard."""
+    from cameras import camera_batch, depth_range, features
+    from mvs_amd import ops
+    B, C, D, h, w = shape
+    K, R, T = camera_batch(B, nv, h, w)
+    d_min, d_int = depth_range(B, d_int=6.0, distinct=True)
+    feat = features(B * nv, C, h, w, seed=C + D).to(DEV)
+    for d_begin, d_count in ((0, D), (D // 3, D - D // 3)):
+        ref, _ = ops.cost_volume(feat, K, R, T, d_min, d_int, B, nv, d_begin, d_count, 25.0)
+        c4 = ops.cost_volume_c4(feat, K, R, T, d_min, d_int, B, nv, d_begin, d_count, 25.0)
+        assert c4.shape == (B, C // 4, d_count, h, w, 4)
+        assert torch.equal(c4, _to_c4(ref))
+
+
+@pytest.mark.parametrize("shape", [(2, 32, 8, 12, 20, 40), (1, 32, 1, 7, 8, 32), (1, 8, 1, 5, 9, 33)])
+def test_narrow_conv3d_channel_quad_input_is_bit_equal(shape):
+    """conv3d_k3 reading the channel-quad volume sums the same products in the same order as the
+    NCDHW kernel: bit-equal outputs (with and without the fused eval BN + ReLU)."""
+    from mvs_amd.ops import conv3d_k3
+    b, cin, cout, d, h, w = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(b, cin, d, h, w, generator=g).to(DEV)
+    wt = (torch.randn(cout, cin, 3, 3, 3, generator=g) * 0.1).to(DEV)
+    bn = [t.to(DEV) for t in _bn_params(cout, g)]
+    with torch.no_grad():
+        for p in ([None, None, None], bn):
+            assert torch.equal(conv3d_k3(_to_c4(x), wt, *p, in_c4=True), conv3d_k3(x, wt, *p))
+
+
+@pytest.mark.parametrize("cout", [16, 32, 64])
+def test_region_conv_s2_channel_quad_input_is_bit_equal(cout):
+    """conv3d_region (CONV_S2) reading the channel-quad cost volume equals the NCDHW read bit for
+    bit (the kernel feeds the MFMA the same 4 channels either way)."""
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _grow, _tconv_input_region
+    from mvs_amd.ops import CONV_S2, conv3d_region
+    n = (24, 20, 26)
+    pad, _ = pad_outpad(*n)
+    Bx = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
+    out_reg = _grow(Bx, n, 1)
+    g = torch.Generator().manual_seed(cout)
+    x = torch.randn(2, 32, *n, generator=g).to(DEV)
+    conv = torch.nn.Conv3d(32, cout, 3)
+    from mvs_amd.ops import region_weight
+    w27 = region_weight(conv).detach().to(DEV)
+    sc, sh, mu = [t.to(DEV) for t in _bn_params(cout, g)]
+    args = (list(n), [lo for lo, _ in out_reg], [hi - lo + 1 for lo, hi in out_reg], None, None, list(pad),
+            sc, sh, mu)
+    with torch.no_grad():
+        ref = conv3d_region(x, None, w27, CONV_S2, *args)
+        y = conv3d_region(_to_c4(x), None, w27, CONV_S2, *args, in_c4=True)
+    assert torch.equal(y, ref)
+
+
+def test_mvsnet_channel_quad_feed_equals_ncdhw_feed():
+    """MVSNet.forward's HIP inference feed (channel-quad cost volume into the live regulariser)
+    against the same network fed the NCDHW volume: identical depth maps."""
+    from cameras import camera_batch, depth_range
+    from mvs_amd.config import MVSConfig
+    from mvs_amd.model import MVSNet
+    import mvs_amd.costvolume as cvmod
+    B, V, D, H, W = 1, 3, 32, 128, 160
+    torch.manual_seed(0)
+    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W)).to(DEV).eval()
+    K, R, T = camera_batch(B, V, H // 4, W // 4)
+    d_min, d_int = depth_range(B, d_int=10.0)
+    img = torch.rand(B * V, 3, H, W, generator=torch.Generator().manual_seed(3)).to(DEV)
+    calls = []
+    orig = cvmod.warp_and_assemble_cost_volume
+
+    def spy(*a, **kw):
+        calls.append(kw.get("channel_quads", False))
+        return orig(*a, **kw)
+    import mvs_amd.model as model_mod
+    with torch.no_grad():
+        model_mod.warp_and_assemble_cost_volume = spy
+        try:
+            d4, r4 = net(img, K, R, T, d_min, d_int, B, V)
+            model_mod.warp_and_assemble_cost_volume = lambda *a, **kw: orig(*a, **dict(kw, channel_quads=False))
+            d5, r5 = net(img, K, R, T, d_min, d_int, B, V)
+        finally:
+            model_mod.warp_and_assemble_cost_volume = orig
+    assert calls == [True]
+    assert torch.equal(d4, d5) and torch.equal(r4, r5)

@@ -78,6 +78,6 @@ def test_live_region_needs_matching_geometry():
     the reference's shape mismatch instead of returning wrongly indexed live regions."""
     m = _reg(8, 12, 16).eval()
     cv = torch.rand(1, 32, 10, 12, 16)
-    assert not m._live_geometry_ok(cv)
+    assert not m._live_geometry_ok(cv.shape[2:])
     with torch.no_grad(), pytest.raises(RuntimeError):
         m(cv)
