@@ -132,14 +132,16 @@ def build_model(D, H, W, device):
     return net.to(device).eval()
 
 
-def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=False):
+def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=False, quads=False):
     """Fused-kernel timing with HIP events on the launch stream, through the C ABI.
 
     Returns (main_ms, op_ms, alg_bytes): main_ms = average duration of the main fused kernel
     (events recorded by mvs_cost_volume_fwd_timed right around its launch), op_ms = average
     duration of the whole op (sampling matrices + packing + reference resampling + main kernel).
-    bf16=True times the opt-in bf16 cost volume (mvs_cost_volume_fwd_bf16): op-level only
-    (main_ms None), algorithmic bytes with a 2-byte cost volume."""
+    quads=True times the channel-quad variant (mvs_cost_volume_fwd_c4, what MVSNet.forward's
+    inference step runs; same bytes).  bf16=True times the opt-in bf16 cost volume
+    (mvs_cost_volume_fwd_bf16): op-level only (main_ms None), algorithmic bytes with a 2-byte
+    cost volume."""
     from mvs_amd import _lib, ops
     lib = _lib.load()
     d_count = D if d_count is None else d_count
@@ -162,12 +164,13 @@ def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=F
                 _lib.ptr(d_int), B, V, C, h, w, d_begin, d_count, 25.0, _lib.ptr(ws), _lib.ptr(cv), sp)
             _lib.check(st, "mvs_cost_volume_fwd_bf16")
             return
-        st = lib.mvs_cost_volume_fwd_timed(
+        fn = lib.mvs_cost_volume_fwd_c4 if quads else lib.mvs_cost_volume_fwd_timed
+        st = fn(
             _lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T), _lib.ptr(d_min), _lib.ptr(d_int),
             B, V, C, h, w, d_begin, d_count, 25.0, _lib.ptr(ws), _lib.ptr(cv), sp,
             None if e0 is None else ctypes.c_void_p(e0.cuda_event),
             None if e1 is None else ctypes.c_void_p(e1.cuda_event))
-        _lib.check(st, "mvs_cost_volume_fwd_timed")
+        _lib.check(st, "mvs_cost_volume_fwd_c4" if quads else "mvs_cost_volume_fwd_timed")
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(iters)]
@@ -228,13 +231,17 @@ KERNEL_CFGS = {   # BASELINE.json configs[2..4]: (B, V, h, w, D, d_count)
 
 
 def kernel_configs(device, iters):
-    """Main fused kernel at the other BASELINE configs (live HIP events, as the roofline)."""
+    """Main fused kernel at the other BASELINE configs (live HIP events, as the roofline): the
+    channel-quad store of the inference step, NCDHW for the depth shard (the layout the owner
+    exchange moves)."""
     out = {}
     for name, (B, V, h, w, D, dc) in KERNEL_CFGS.items():
-        k_ms, op_ms, alg = time_kernel(B, V, 32, h, w, D, device, iters, D - dc, dc)
+        quads = dc == D
+        k_ms, op_ms, alg = time_kernel(B, V, 32, h, w, D, device, iters, D - dc, dc, quads=quads)
         gbs = alg / (k_ms * 1e-3) / 1e9
         out[name] = {"B": B, "V": V, "feature_hw": [h, w], "planes": dc, "kernel_ms": k_ms, "op_ms": op_ms,
-                     "alg_bytes": alg, "GBps": gbs, "frac": gbs / HBM_PEAK_GBS}
+                     "alg_bytes": alg, "GBps": gbs, "frac": gbs / HBM_PEAK_GBS,
+                     "store": "channel-quad" if quads else "NCDHW"}
         torch.cuda.empty_cache()
     return out
 
@@ -357,17 +364,33 @@ def main():
             from mvs_amd.depth_shards import DepthShardedMVSNet
             sharded = DepthShardedMVSNet(net, world, rank)
             step = lambda: sharded(*inputs, B, V)
+        # the main fused kernel's launches inside the timed steps, bracketed by HIP events on its
+        # launch stream (ops.KERNEL_EVENT_HOOK -> mvs_cost_volume_fwd_c4's event arguments)
+        from mvs_amd import ops as mvs_ops
+        step_events = []
+        stream = torch.cuda.current_stream(device)
+
+        def hook():
+            pair = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for e in pair:   # materialise the HIP event (torch creates it on first record)
+                e.record(stream)
+            step_events.append(pair)
+            return pair
         with torch.no_grad():
             for i in range(args.warmup):
                 step()
                 torch.cuda.synchronize()
                 log("warmup step %d/%d done" % (i + 1, args.warmup))
             barrier(world)
+            mvs_ops.KERNEL_EVENT_HOOK = hook if args.mode == "samples" else None
             t0 = time.perf_counter()
             for _ in range(args.steps):
                 step()
             barrier(world)
             dt = time.perf_counter() - t0
+            mvs_ops.KERNEL_EVENT_HOOK = None
+        if step_events:
+            result["step_kernel_ms"] = sum(a.elapsed_time(b) for a, b in step_events) / len(step_events)
         log("timed %d steps: %.2f ms/step" % (args.steps, 1000.0 * dt / args.steps))
         dt = max_over_ranks(dt, world, device)
         ms_step = 1000.0 * dt / args.steps
@@ -415,9 +438,19 @@ def main():
     # fused kernel timing (this rank's share of planes in dshard mode)
     d_count = D if args.mode == "samples" else D // world
     log("timing the fused kernel")
-    k_ms, op_ms, alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count)
+    # samples mode: the channel-quad store the eval step feeds the regulariser with; dshard mode:
+    # the NCDHW slabs the owner exchange moves
+    quads = args.mode == "samples"
+    k_ms, op_ms, alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count, quads=quads)
     k_ms = max_over_ranks(k_ms, world, device)
     op_ms = max_over_ranks(op_ms, world, device)
+    nc_ms, nc_op_ms, _ = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count)
+    nc_ms = max_over_ranks(nc_ms, world, device)
+    # roofline duration: the kernel's launches inside the timed steps when the step runs it
+    # (samples mode); the isolated back-to-back launches otherwise (dshard: NCDHW slabs)
+    iso_ms = k_ms
+    if "step_kernel_ms" in result:
+        k_ms = max_over_ranks(result["step_kernel_ms"], world, device)
     gbs = alg / (k_ms * 1e-3) / 1e9
     tag = "b%dv%dd%dh%dw%d" % (B, V, d_count, h, w)
     traffic = load_traffic(tag)
@@ -451,11 +484,17 @@ def main():
         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": gbs / HBM_PEAK_GBS,
                      "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
-                     "kernel": "cost_volume_staged_kernel", "kernel_ms": k_ms,
-                     "alg_bytes_per_launch": alg},
+                     "kernel": "cost_volume_staged_kernel<V=%d, planes=8, %s>" % (
+                         V, "channel-quad store" if quads else "NCDHW store"), "kernel_ms": k_ms,
+                     "alg_bytes_per_launch": alg,
+                     "timing": ("HIP events around each launch inside the %d timed steps" % args.steps
+                                if "step_kernel_ms" in result else "HIP events, isolated launches"),
+                     "isolated_kernel_ms": iso_ms,
+                     "ncdhw_store": {"kernel_ms": nc_ms, "op_ms": nc_op_ms,
+                                     "frac": alg / (nc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}},
         "hot_path": {"cost_volumes_per_s": B / (op_ms * 1e-3), "op_ms": op_ms,
-                     "op": "mvs_cost_volume_fwd: plane_sampling + pack_pad + ref_resample + "
-                           "cost_volume_staged kernels",
+                     "op": "mvs_cost_volume_fwd%s: plane_sampling + pack_pad + ref_resample + "
+                           "cost_volume_staged kernels" % ("_c4" if quads else ""),
                      "op_GBps": alg / (op_ms * 1e-3) / 1e9},
     }
     if "full" in result:

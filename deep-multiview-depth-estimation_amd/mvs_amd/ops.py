@@ -119,6 +119,12 @@ def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scal
             feat.new_empty((_ws_floats(batch_size, n_views, c, h, w, d_count),)))
 
 
+# Live timing of the main fused kernel inside a real step (bench.py): when set, a callable returning a
+# (begin, end) pair of torch.cuda.Event for each cost_volume_c4 call; the C ABI records them on the
+# launch stream right around the main kernel (mvs_cost_volume_fwd_c4's event arguments).
+KERNEL_EVENT_HOOK = None
+
+
 @torch.library.custom_op("mvs::cost_volume_c4", mutates_args=())
 def cost_volume_c4(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.Tensor,
                    d_min: torch.Tensor, d_int: torch.Tensor, batch_size: int, n_views: int,
@@ -137,10 +143,13 @@ def cost_volume_c4(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torc
     cv = torch.empty((batch_size, c // 4, d_count, h, w, 4), device=feat.device, dtype=_F32)
     ws = torch.empty((_ws_floats(batch_size, n_views, c, h, w, d_count),), device=feat.device,
                      dtype=_F32)
+    evs = (None, None)
+    if KERNEL_EVENT_HOOK is not None:
+        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK())
     st = lib.mvs_cost_volume_fwd_c4(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T),
                                     _lib.ptr(d_min), _lib.ptr(d_int), batch_size, n_views, c, h, w,
                                     d_begin, d_count, float(d_scale), _lib.ptr(ws), _lib.ptr(cv),
-                                    _lib.stream_handle(feat.device), None, None)
+                                    _lib.stream_handle(feat.device), *evs)
     _lib.check(st, "mvs_cost_volume_fwd_c4")
     return cv
 

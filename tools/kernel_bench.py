@@ -26,13 +26,14 @@ def main():
         B, V, h, w, D, dc = CFGS[name]
         C = int(os.environ.get("MVS_BENCH_C", "32"))   # channel-count sweeps (set-up vs per-chunk cost)
         bf16 = os.environ.get("MVS_BENCH_BF16") == "1"
-        ms, op_ms, alg = bench.time_kernel(B, V, C, h, w, D, dev, 20, 0, dc, bf16=bf16)
+        quads = os.environ.get("MVS_BENCH_C4") == "1"   # channel-quad store (inference feed)
+        ms, op_ms, alg = bench.time_kernel(B, V, C, h, w, D, dev, 20, 0, dc, bf16=bf16, quads=quads)
         ms = op_ms if ms is None else ms
         gbs = alg / (ms * 1e-3) / 1e9
         print(json.dumps({"cfg": name, "C": C, "B": B, "V": V, "hw": [h, w], "D": dc, "ms": round(ms, 4),
                           "op_ms": round(op_ms, 4),
                           "alg_GB": round(alg / 1e9, 4), "GBps": round(gbs, 1),
-                          "frac_8TBps": round(gbs / 8000.0, 4)}), flush=True)
+                          "frac_8TBps": round(gbs / 8000.0, 4), "c4": quads}), flush=True)
 
 
 if __name__ == "__main__":
