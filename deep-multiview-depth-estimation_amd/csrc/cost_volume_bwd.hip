@@ -45,7 +45,13 @@ namespace {
 
 constexpr int kBwdTW = 32, kBwdTH = 8;
 constexpr int kBwdKPG = 32;              // planes per workgroup
-constexpr int kBwdSlots = 1536;          // LDS accumulator slots (x 4 channels x 8 B = 48 KB)
+// LDS accumulator slots (x 4 channels x 8 B): 36 KB at V <= 3 (4 workgroups per CU: the loop is
+// latency-bound and occupancy pays more than fewer flushes, cfg 2 3.40 -> 3.12 ms), 48 KB above
+// (more views need the room: V = 5 15.5 -> 13.7 ms at 48 KB)
+template <int V>
+constexpr int bwd_slots() {
+  return V <= 3 ? 1152 : 1536;
+}
 typedef unsigned long long u64;
 
 // ---- fixed point ------------------------------------------------------------------------------
@@ -174,6 +180,7 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
     int C, int h, int w, int Dc, int tiles_x, int tiles_y, int groups, int total) {
   constexpr int NS = V - 1;
   typedef typename Acc<DET>::lds_t lds_t;
+  constexpr int kBwdSlots = bwd_slots<V>();
   __shared__ lds_t lds[4 * kBwdSlots];
   __shared__ Box boxes[kBwdKPG][NS];
 
@@ -291,22 +298,30 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
     }
 
     // ---- the pass's planes (every lane runs them; inactive lanes have g = 0 and no taps) ----
-    for (int pl = kp; pl < ke; ++pl) {
-      const int kk = k0 + pl;
+    // grad_cv of the chunk's 4 channels at this pixel, one plane ahead (the HBM read of the loop)
+    auto load_g = [&](int pl) {
       f4v g = {0.0f, 0.0f, 0.0f, 0.0f};
       if (active) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (j < nch) g[j] = gcv[(size_t)j * cstride + (size_t)pl * hw];
       }
+      return g;
+    };
+    f4v g_next = load_g(kp);
+    for (int pl = kp; pl < ke; ++pl) {
+      const int kk = k0 + pl;
+      const f4v g = g_next;
+      g_next = load_g(min(pl + 1, ke - 1));
       uint32_t pos[NS];
       float wx[NS], wy[NS];
       f4v xs[NS];
       f4v sum = x0;
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + kk) * 9, xn, yn, h, w, active, pos[s],
-                   wx[s], wy[s]);
+        // the sampling matrix is workgroup-uniform: scalar loads
+        src_coords(uniform_ptr(sampling + ((size_t)(b * V + 1 + s) * Dc + kk) * 9), xn, yn, h, w, active,
+                   pos[s], wx[s], wy[s]);
         const Rsrc rs = make_rsrc(uniform_ptr(packed + (size_t)(b * V + 1 + s) * c4 * pg.plane),
                                   (uint32_t)c4 * pg.plane * 16u);
         f4v tp[4];
