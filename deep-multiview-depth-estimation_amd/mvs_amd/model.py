@@ -97,10 +97,22 @@ class CostVolumeReg(nn.Module):
         if cv.dim() == 6:
             if self.live_ok(cv.shape[2:5]) and _hip_inference(cv):
                 return self.forward_live(cv)
+            if self.live_train_ok(cv.shape[2:5]) and _hip_inference(cv):
+                return self.forward_live_train(cv)
             cv = cv.permute(0, 1, 5, 2, 3, 4).reshape((cv.shape[0], 4 * cv.shape[1]) + tuple(cv.shape[2:5]))
         if self.live_ok(cv.shape[2:]):
             return self.forward_live(cv)
+        if self.live_train_ok(cv.shape[2:]):
+            return self.forward_live_train(cv)
         return self.forward_full(cv)
+
+    def live_train_ok(self, n):
+        """forward_live_train applies: every BN in train mode with running statistics (test.py:61's
+        `model.train()` under `torch.no_grad()`), no autograd, the module's padding derived from n."""
+        bns = (self.BN_0, self.BN_1, self.BN_2, self.BN_3)
+        return (self.live_region and not torch.is_grad_enabled() and self._live_geometry_ok(n)
+                and all(bn.training and bn.track_running_stats and bn.running_mean is not None
+                        and bn.affine for bn in bns))
 
     def live_ok(self, n):
         """forward_live applies (eval BN, live_region on, the module's padding derived from n)."""
@@ -192,6 +204,104 @@ class CostVolumeReg(nn.Module):
         z = deconv3d_k3s2(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0, x2=y1)
         return self.Norm(conv3d_k3(z, self.conv_out.weight))
 
+    def forward_live_train(self, cv):
+        """Train-mode-BatchNorm regulariser (test.py:53,61: `model.train()` under `no_grad`)
+        evaluated on live regions, exactly.
+
+        With batch statistics every BN normalises by the mean / variance over the WHOLE volume, so
+        the full-size tensors matter through their sums -- but most of them are structurally
+        constant (the eval-mode argument of forward_live, carried through BN):
+          * conv_k_0 (stride 2, padding n//2+1) is exactly 0 outside its middle-half region M, so
+            its BN statistics are the region's sums over the full element count, and
+            relu(BN(conv_k_0)) is the per-channel constant a_k = relu(BN(0)) outside M;
+          * conv_k_1 (3x3x3, padding 1) of that field is, outside M grown by 1 (R1), a constant per
+            channel and volume-border class (which of its taps fall inside the volume): 27 classes
+            with known voxel counts, so its statistics are the R1 region's sums plus
+            count x value (and count x value^2) per class;
+          * the stride-2 transposed convs read only the middle half M of their input (forward_live),
+            so deconv_3_0 / deconv_2_0 / deconv_1_0 are computed from the M-region tensors; their
+            statistics need the full output, computed here in full (it is not constant).
+        Every BatchNorm updates its running statistics once per use, in the reference's order
+        (BN_0, BN_1, BN_2, BN_3, BN_1, BN_2, BN_3, BN_2, BN_1, BN_0), as forward_full does."""
+        act = lambda y, bn: self.ReLU(_apply_bn(y, *bn))
+        n = tuple(cv.shape[2:5])
+        full = tuple((0, d - 1) for d in n)
+        M = _tconv_input_region(full, n, self.pad)
+        R1, R2 = _grow(M, n, 1), _grow(M, n, 2)
+        bsz = cv.shape[0]
+        count = bsz * n[0] * n[1] * n[2]
+        if _hip_inference(cv):
+            return self._forward_live_train_hip(cv, n, full, M, R1, R2, count)
+        y0 = _narrow_conv(self.conv_0_0, cv)
+        y0 = act(y0, _bn_train(self.BN_0, *_sums(y0), count))
+        stage = []
+        for conv_a, bn in ((self.conv_1_0, self.BN_1), (self.conv_2_0, self.BN_2), (self.conv_3_0, self.BN_3)):
+            z = _conv_s2_region(cv, conv_a.weight, R2, self.pad)    # exactly 0 outside M
+            p = _bn_train(bn, *_sums(z), count)
+            stage.append((act(z, p), _bn_constant(p)))              # relu(BN(0)) outside M
+        lv = []
+        for (y, a), conv_b, bn in zip(stage, (self.conv_1_1, self.conv_2_1, self.conv_3_1),
+                                      (self.BN_1, self.BN_2, self.BN_3)):
+            z = _conv_s1_region(y, R2, conv_b.weight, R1, n)
+            s1, s2 = _sums(z)
+            c1, c2 = _border_class_sums(conv_b.weight, a, R1, n, bsz)
+            p = _bn_train(bn, s1 + c1, s2 + c2, count)
+            lv.append(_crop_pad(act(z, p), R1, M, n))
+        y1, y2, y3 = lv
+        z = _tconv_region(y3, M, self.deconv_3_0.weight, full, self.pad)
+        y3 = _crop_pad(act(z, _bn_train(self.BN_2, *_sums(z), count)), full, M, n)
+        z = _tconv_region(y3 + y2, M, self.deconv_2_0.weight, full, self.pad)
+        y2 = _crop_pad(act(z, _bn_train(self.BN_1, *_sums(z), count)), full, M, n)
+        z = _tconv_region(y2 + y1, M, self.deconv_1_0.weight, full, self.pad)
+        z = act(z, _bn_train(self.BN_0, *_sums(z), count)) + y0
+        return self.Norm(_narrow_conv(self.conv_out, z))
+
+    def _forward_live_train_hip(self, cv, n, full, M, R1, R2, count):
+        """forward_live_train on the HIP kernels: raw (BN-free) region convs on the fp32 MFMA
+        (conv3d_region.hip), conv_0_0 / conv_out (conv3d_narrow.hip), deconv_1_0
+        (deconv3d_region.hip); batch statistics as float64 sums of the raw outputs; BN + ReLU
+        applied in place to the region tensors (channels-last).  The transposed convs run over
+        the full output volume (their statistics) and keep the M-region part.  ``cv`` may be the
+        channel-quad volume (conv_0_0 and the stride-2 convs read it with 16-byte loads)."""
+        from .ops import CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_region, deconv3d_k3s2, region_weight
+        c4 = cv.dim() == 6
+        org = lambda reg: [lo for lo, _ in reg]
+        size = lambda reg: [hi - lo + 1 for lo, hi in reg]
+        dims, pad, bsz = list(n), list(self.pad), cv.shape[0]
+        y0 = conv3d_k3(cv, self.conv_0_0.weight, in_c4=c4)
+        p0 = _bn_train(self.BN_0, *_sums(y0), count)
+        stage = []
+        for conv_a, bn in ((self.conv_1_0, self.BN_1), (self.conv_2_0, self.BN_2), (self.conv_3_0, self.BN_3)):
+            z = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(R2), size(R2), None, None,
+                              pad, in_c4=c4)
+            p = _bn_train(bn, *_sums(z, -1), count)
+            stage.append((_bn_relu_(z, p, -1), _bn_constant(p)))
+        lv = []
+        for (y, a), conv_b, bn in zip(stage, (self.conv_1_1, self.conv_2_1, self.conv_3_1),
+                                      (self.BN_1, self.BN_2, self.BN_3)):
+            z = conv3d_region(y, None, region_weight(conv_b), CONV_S1, dims, org(R1), size(R1), org(R2),
+                              size(R2), None)
+            s1, s2 = _sums(z, -1)
+            c1, c2 = _border_class_sums(conv_b.weight, a, R1, n, bsz)
+            p = _bn_train(bn, s1 + c1, s2 + c2, count)
+            lv.append(_bn_relu_(_crop_cl(z, R1, M), p, -1))
+        y1, y2, y3 = lv
+        z = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
+                          size(M), pad)
+        p = _bn_train(self.BN_2, *_sums(z, -1), count)
+        y3 = _bn_relu_(_crop_cl(z, full, M), p, -1)
+        del z
+        z = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
+                          size(M), pad)
+        p = _bn_train(self.BN_1, *_sums(z, -1), count)
+        y2 = _bn_relu_(_crop_cl(z, full, M), p, -1)
+        del z
+        z = deconv3d_k3s2(y2, org(M), self.deconv_1_0.weight, dims, pad, None, None, None, None, x2=y1,
+                          channels_last=True)
+        p = _bn_train(self.BN_0, *_sums(z), count)
+        z = _bn_relu_(z, p, 1).add_(_bn_relu_(y0, p0, 1))
+        return self.Norm(conv3d_k3(z, self.conv_out.weight))
+
     def forward_full(self, cv):
         act = lambda bn, y: self.ReLU(bn(y))
         # the BN modules are shared between levels exactly as in model.py:101-121; the two narrow
@@ -225,6 +335,86 @@ def _narrow_conv(conv, x):
         from .ops import conv3d_k3
         return conv3d_k3(x, conv.weight)
     return conv(x)
+
+
+# ---- train-mode BatchNorm from sums (CostVolumeReg.forward_live_train) ----------------------
+def _sums(y, cdim=1):
+    """Per-channel sum and sum of squares of y (channels on dim cdim) in float64."""
+    red = [d for d in range(y.dim()) if d != cdim % y.dim()]
+    return y.sum(red, dtype=torch.float64), (y * y).sum(red, dtype=torch.float64)
+
+
+def _bn_relu_(y, p, cdim):
+    """In place: y = relu((y - mean) * scale + shift), channels on dim cdim (region tensors are
+    channels-last: cdim = -1)."""
+    scale, shift, mean = p
+    shape = [1] * y.dim()
+    shape[cdim] = -1
+    v = lambda t: t.view(shape)
+    return y.sub_(v(mean)).mul_(v(scale)).add_(v(shift)).clamp_min_(0.0)
+
+
+def _crop_cl(x, x_reg, want):
+    """The box `want` (inside x_reg) of a channels-last region tensor x [B, d, h, w, C], contiguous."""
+    sl = [slice(lo - xlo, hi - xlo + 1) for (xlo, _), (lo, hi) in zip(x_reg, want)]
+    return x[:, sl[0], sl[1], sl[2], :].contiguous()
+
+
+def _bn_train(bn, s1, s2, count):
+    """Batch statistics of a train-mode BatchNorm from per-channel sums over `count` elements:
+    returns (scale, shift, mean) with BN(x) = (x - mean) * scale + shift (biased variance), and
+    updates bn's running statistics the way torch's batch_norm does (unbiased variance, momentum,
+    num_batches_tracked)."""
+    mean = s1 / count
+    var = (s2 / count - mean * mean).clamp_min(0.0)
+    with torch.no_grad():
+        bn.num_batches_tracked.add_(1)
+        m = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
+        bn.running_mean.mul_(1.0 - m).add_(mean.to(bn.running_mean), alpha=m)
+        bn.running_var.mul_(1.0 - m).add_((var * (count / max(count - 1, 1))).to(bn.running_var), alpha=m)
+    scale = bn.weight / torch.sqrt(var.float() + bn.eps)
+    return scale, bn.bias, mean.float()
+
+
+def _apply_bn(y, scale, shift, mean):
+    v = lambda t: t.view((1, -1) + (1,) * (y.dim() - 2))
+    return (y - v(mean)) * v(scale) + v(shift)
+
+
+def _bn_constant(p):
+    """relu(BN(0)) per channel: the value of a BN + ReLU output where its input is exactly 0."""
+    scale, shift, mean = p
+    return torch.relu(-mean * scale + shift)
+
+
+def _border_classes(d, lo, hi):
+    """One dim of size d under a 3-tap, stride-1, padding-1 conv: (taps inside the volume, voxels
+    of the class, of them inside [lo, hi]) for the border / interior index classes."""
+    spans = [(0, 0, (1,))] if d == 1 else (
+        [(0, 0, (1, 2)), (d - 1, d - 1, (0, 1))] + ([(1, d - 2, (0, 1, 2))] if d > 2 else []))
+    return [(taps, b - a + 1, max(0, min(b, hi) - max(a, lo) + 1)) for a, b, taps in spans]
+
+
+def _border_class_sums(weight, a, reg, n, bsz):
+    """Sums (value, value^2) per output channel of conv3d(field, weight, padding 1) over the
+    voxels OUTSIDE reg, where the input field is the per-channel constant a everywhere the
+    window of such a voxel reaches (in-volume taps only).  The output there depends only on the
+    voxel's border class: sum_ci a[ci] * sum_(in-volume taps) weight[co, ci, tap]."""
+    w = weight.double()
+    a = a.double()
+    s1 = torch.zeros(w.shape[0], dtype=torch.float64, device=w.device)
+    s2 = torch.zeros_like(s1)
+    per_dim = [_border_classes(d, lo, hi) for d, (lo, hi) in zip(n, reg)]
+    for td, nd, id_ in per_dim[0]:
+        for th, nh, ih in per_dim[1]:
+            for tw, nw, iw in per_dim[2]:
+                cnt = bsz * (nd * nh * nw - id_ * ih * iw)
+                if cnt == 0:
+                    continue
+                u = w[:, :, list(td)][:, :, :, list(th)][:, :, :, :, list(tw)].sum((2, 3, 4)) @ a
+                s1 += cnt * u
+                s2 += cnt * u * u
+    return s1, s2
 
 
 # ---- live-region helpers (CostVolumeReg.forward_live).  A region is a tuple of inclusive
@@ -340,7 +530,8 @@ class MVSNet(nn.Module):
         # kernels in the channel-quad layout (ops.cost_volume_c4, the fused kernel's 16-byte store)
         quads = (not bf16 and _hip_inference(feature_maps) and 2 <= n_views <= 8
                  and feature_maps.shape[1] % 4 == 0
-                 and reg.live_ok((c.d_num,) + tuple(feature_maps.shape[2:])))
+                 and (reg.live_ok((c.d_num,) + tuple(feature_maps.shape[2:]))
+                      or reg.live_train_ok((c.d_num,) + tuple(feature_maps.shape[2:]))))
         cost_volume, d_batch, ref_views = warp_and_assemble_cost_volume(
             K_batch, R_batch, T_batch, d_min, d_int, feature_maps, batch_size, n_views,
             d_num=c.d_num, d_scale=c.d_scale,

@@ -393,13 +393,13 @@ def _(x, weight, bn_scale=None, bn_shift=None, bn_mean=None, in_c4=False):
 # ----------------------------------------------------------------------------------------------
 @torch.library.custom_op("mvs::deconv3d_k3s2", mutates_args=())
 def deconv3d_k3s2(x: torch.Tensor, origin: list[int], weight: torch.Tensor, out_dims: list[int],
-                  pad: list[int], bn_scale: torch.Tensor, bn_shift: torch.Tensor,
-                  bn_mean: torch.Tensor, residual: torch.Tensor, x2: Optional[torch.Tensor] = None,
-                  channels_last: bool = False) -> torch.Tensor:
+                  pad: list[int], bn_scale: Optional[torch.Tensor], bn_shift: Optional[torch.Tensor],
+                  bn_mean: Optional[torch.Tensor], residual: Optional[torch.Tensor],
+                  x2: Optional[torch.Tensor] = None, channels_last: bool = False) -> torch.Tensor:
     """ConvTranspose3d(c_in, 8, 3, stride 2, padding pad) of the region tensor x (+ x2) (input region
     starting at `origin`; [B, c_in, r...] or, channels_last, [B, r..., c_in]) into the full volume
-    out_dims, then max((y - mean) * scale + shift, 0) + residual (csrc/deconv3d_region.hip).
-    Inference only."""
+    out_dims, then max((y - mean) * scale + shift, 0) + residual (csrc/deconv3d_region.hip); without
+    bn_* the raw transposed conv (+ residual if given).  Inference only."""
     _require_gpu(x, "x")
     lib = _lib.load()
     x = x.to(_F32).contiguous()
@@ -415,15 +415,18 @@ def deconv3d_k3s2(x: torch.Tensor, origin: list[int], weight: torch.Tensor, out_
     if tuple(w.shape) != (cin, 8, 3, 3, 3):
         raise ValueError("weight [c_in, 8, 3, 3, 3] expected, got %s" % (tuple(w.shape),))
     d, h, wd = out_dims
-    f = lambda t: t.to(device=x.device, dtype=_F32).contiguous()
+    f = lambda t: None if t is None else t.to(device=x.device, dtype=_F32).contiguous()
     sc, sh, mu, res = f(bn_scale), f(bn_shift), f(bn_mean), f(residual)
-    if tuple(res.shape) != (b, 8, d, h, wd):
+    if (sc is None) != (sh is None) or (sc is None) != (mu is None):
+        raise ValueError("bn_scale, bn_shift and bn_mean go together")
+    if res is not None and tuple(res.shape) != (b, 8, d, h, wd):
         raise ValueError("residual must be [B, 8, D, H, W]")
     y = torch.empty((b, 8, d, h, wd), device=x.device, dtype=_F32)
-    st = lib.mvs_deconv3d_k3s2_fwd(_lib.ptr(x), None if x2 is None else _lib.ptr(x2),
+    pt = lambda t: None if t is None else _lib.ptr(t)
+    st = lib.mvs_deconv3d_k3s2_fwd(_lib.ptr(x), pt(x2),
                                    _lib.MVS_LAYOUT_CHANNELS_LAST if channels_last else 0, b, cin, 8, rd, rh,
-                                   rw, *origin, _lib.ptr(w), d, h, wd, *pad, _lib.ptr(sc), _lib.ptr(sh),
-                                   _lib.ptr(mu), _lib.ptr(res), _lib.ptr(y), _lib.stream_handle(x.device))
+                                   rw, *origin, _lib.ptr(w), d, h, wd, *pad, pt(sc), pt(sh), pt(mu), pt(res),
+                                   _lib.ptr(y), _lib.stream_handle(x.device))
     _lib.check(st, "mvs_deconv3d_k3s2_fwd")
     return y
 

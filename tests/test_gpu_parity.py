@@ -499,6 +499,37 @@ def test_live_regulariser_gpu_matches_full_volume():
     torch.testing.assert_close(live, full, rtol=1e-4, atol=1e-7)
 
 
+def test_train_mode_live_regulariser_gpu_matches_full_volume():
+    """Train-mode BN (test.py:61) on the GPU: forward_live_train (region convs + batch statistics
+    from region sums and border-class constants) against forward_full, probabilities and running
+    statistics, at a cfg-1-like shape."""
+    import copy
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import CostVolumeReg
+    D, h, w = 48, 32, 40
+    pad, outpad = pad_outpad(D, h, w)
+    torch.manual_seed(0)
+    m = CostVolumeReg(pad=pad, outpad=outpad)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.BatchNorm3d):
+            mod.running_mean.uniform_(-0.5, 0.5)
+            mod.running_var.uniform_(0.5, 2.0)
+            mod.weight.data.uniform_(0.5, 1.5)
+            mod.bias.data.uniform_(-0.5, 0.5)
+    m1 = m.to(DEV).train()
+    m2 = copy.deepcopy(m1)
+    cv = torch.rand(2, 32, D, h, w, generator=torch.Generator().manual_seed(1)).to(DEV)
+    with torch.no_grad():
+        assert m1.live_train_ok(cv.shape[2:])
+        live = m1(cv)
+        full = m2.forward_full(cv)
+    torch.testing.assert_close(live, full, rtol=1e-4, atol=1e-6)
+    s1, s2 = m1.state_dict(), m2.state_dict()
+    for k in s2:
+        if "BN_" in k:
+            torch.testing.assert_close(s1[k], s2[k], rtol=1e-5, atol=1e-6, msg=k)
+
+
 def test_region_deconv_fused_epilogue_matches_torch():
     """mvs::deconv3d_k3s2 (csrc/deconv3d_region.hip): deconv_1_0 from its live input region into the
     full volume, with BN_0(eval) + ReLU + `+ y0` fused, against the torch ops on the same device

@@ -37,15 +37,41 @@ def test_live_region_equals_full_volume(shape):
     torch.testing.assert_close(live, full, rtol=1e-5, atol=1e-7)
 
 
-def test_train_mode_bn_uses_full_volume():
-    """Train-mode BN normalises with statistics of the whole volume (test.py:61 runs the model in
-    train mode under no_grad), so the restriction does not apply: forward == forward_full."""
-    m = _reg(8, 12, 16).train()
-    cv = torch.rand(1, 32, 8, 12, 16)
+def _bn_state(m):
+    return {k: v.clone() for k, v in m.state_dict().items() if "BN_" in k}
+
+
+@pytest.mark.parametrize("shape", [(8, 12, 16), (7, 9, 11), (20, 32, 40), (5, 6, 6), (2, 3, 4),
+                                   (1, 2, 3), (3, 1, 5), (13, 10, 17)])
+def test_train_mode_bn_live_equals_full_volume(shape):
+    """Train-mode BN (test.py:61: model.train() under no_grad) normalises with batch statistics of
+    the whole volume.  forward_live_train forms them from the live regions plus the structurally
+    constant parts (zeros of conv_k_0, the 27 border classes of conv_k_1 of a constant field) and
+    must give forward_full's probabilities AND running statistics (each BN updated once per use,
+    in the reference's order)."""
+    D, h, w = shape
+    m1 = _reg(D, h, w, seed=3).train()
+    m2 = _reg(D, h, w, seed=3).train()
+    cv = torch.rand(2, 32, D, h, w, generator=torch.Generator().manual_seed(7 * D + w))
     with torch.no_grad():
-        a = m(cv)
-        m2 = _reg(8, 12, 16).train()
-        b = m2.forward_full(cv)
+        assert m1.live_train_ok(cv.shape[2:])
+        live = m1(cv)
+        full = m2.forward_full(cv)
+    assert live.shape == full.shape == (2, 1, D, h, w)
+    torch.testing.assert_close(live, full, rtol=1e-4, atol=1e-6)
+    s1, s2 = _bn_state(m1), _bn_state(m2)
+    for k in s2:
+        torch.testing.assert_close(s1[k], s2[k], rtol=1e-5, atol=1e-6, msg=k)
+
+
+def test_train_mode_bn_with_grad_uses_full_volume():
+    """Autograd in train mode (train.py) keeps the reference op sequence (forward_full)."""
+    m = _reg(8, 12, 16).train()
+    cv = torch.rand(1, 32, 8, 12, 16, requires_grad=True)
+    assert not m.live_train_ok(cv.shape[2:]) or not torch.is_grad_enabled()
+    a = m(cv)
+    m2 = _reg(8, 12, 16).train()
+    b = m2.forward_full(cv)
     assert torch.equal(a, b)
 
 
