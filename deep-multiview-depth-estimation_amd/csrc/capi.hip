@@ -303,4 +303,36 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
   return mvs::hip_status();
 }
 
+
+static bool channel_layout_ok(int layout, int channels, const void* a, const void* b, const void* c) {
+  if (layout & ~MVS_LAYOUT_CHANNELS_LAST) return false;
+  if (!(layout & MVS_LAYOUT_CHANNELS_LAST)) return true;
+  const int c4 = channels / 4;
+  if (channels % 4 || c4 > 64 || (c4 & (c4 - 1))) return false;   // quads per voxel: a power of two
+  return ((((uintptr_t)a) | ((uintptr_t)b) | ((uintptr_t)c)) & 15u) == 0;
+}
+
+int mvs_channel_stats(const float* x, int layout, int batch, int channels, long long voxels, double* stats,
+                      void* stream) {
+  if (!x || !stats || batch <= 0 || channels <= 0 || voxels <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if (!channel_layout_ok(layout, channels, x, nullptr, nullptr)) return MVS_ERR_INVALID_ARGUMENT;
+  if ((uint64_t)batch * channels > 65535u && !(layout & MVS_LAYOUT_CHANNELS_LAST)) return MVS_ERR_TOO_LARGE;
+  mvs::launch_channel_stats(x, (layout & MVS_LAYOUT_CHANNELS_LAST) != 0, batch, channels, (size_t)voxels, stats,
+                            (hipStream_t)stream);
+  return mvs::hip_status();
+}
+
+int mvs_bn_relu(const float* x, int layout, int batch, int channels, long long voxels, const float* scale,
+                const float* shift, const float* mean, const float* r, const float* r_scale,
+                const float* r_shift, const float* r_mean, float* y, void* stream) {
+  if (!x || !y || !scale || !shift || !mean || batch <= 0 || channels <= 0 || voxels <= 0)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (r && (!r_scale || !r_shift || !r_mean)) return MVS_ERR_INVALID_ARGUMENT;
+  if (!channel_layout_ok(layout, channels, x, r, y)) return MVS_ERR_INVALID_ARGUMENT;
+  if ((uint64_t)batch * channels > 65535u && !(layout & MVS_LAYOUT_CHANNELS_LAST)) return MVS_ERR_TOO_LARGE;
+  mvs::launch_bn_relu(x, (layout & MVS_LAYOUT_CHANNELS_LAST) != 0, batch, channels, (size_t)voxels, scale, shift,
+                      mean, r, r_scale, r_shift, r_mean, y, (hipStream_t)stream);
+  return mvs::hip_status();
+}
+
 }  // extern "C"

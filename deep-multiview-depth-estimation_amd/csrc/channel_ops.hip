@@ -1,0 +1,204 @@
+// channel_ops.hip -- the train-mode BatchNorm pieces of the regulariser (model.py:101-121 with every
+// BatchNorm3d in training mode, test.py:53,61): per-channel batch sums of a tensor, and the
+// normalisation + ReLU (+ a second normalised, rectified tensor added: model.py:121-123's
+// `relu(BN_0(deconv_1_0)) + y0`, with y0 = relu(BN_0(conv_0_0)) kept un-normalised until then).
+//
+// Layouts: channels-last region tensors x[b][voxel][c] (CostVolumeReg.forward_live_train's conv
+// outputs) or NCDHW x[b][c][voxel].  Both kernels stream the tensor once with 16-byte accesses; they
+// are HBM-bound (sums: 4 B read per element; normalisation: 4 B read + 4 B written, + 4 B read for
+// the addend).
+//
+// Sums: float64 per thread, reduced across the wave's lanes of equal channel, then added into
+// stats[slot][0 / 1][c] (sum / sum of squares) with slot = workgroup % MVS_STATS_SLOTS, so the fp64
+// global atomics of different workgroups spread over 64 copies; the caller adds the copies.
+#include "launchers.h"
+#include "packed.h"
+
+namespace mvs {
+namespace {
+
+constexpr int kStatSlots = 64;   // == MVS_STATS_SLOTS
+
+// channels-last: float4 j holds channels 4 (j % C4) .. + 3; the grid stride is a multiple of C4
+// (C4 divides kBlock), so a thread's quad never changes
+__global__ __launch_bounds__(kBlock) void channel_stats_cl_kernel(const float4* __restrict__ x, size_t n4, int C4,
+                                                                  double* __restrict__ stats) {
+  double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  for (size_t j = (size_t)blockIdx.x * kBlock + threadIdx.x; j < n4; j += stride) {
+    const float4 v = x[j];
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      s[k] += (double)e[k];
+      q[k] += (double)e[k] * (double)e[k];
+    }
+  }
+  // lanes l and l ^ o (o >= C4) hold the same quad
+  for (int o = 32; o >= C4; o >>= 1)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      s[k] += __shfl_xor(s[k], o);
+      q[k] += __shfl_xor(q[k], o);
+    }
+  const int lane = (int)threadIdx.x & 63;
+  if (lane < C4) {
+    const int C = 4 * C4;
+    double* st = stats + (size_t)(blockIdx.x % kStatSlots) * 2 * C;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      atomicAdd(st + 4 * lane + k, s[k]);
+      atomicAdd(st + C + 4 * lane + k, q[k]);
+    }
+  }
+}
+
+// NCDHW: one (sample, channel) plane per blockIdx.y; float4 accesses when the plane is a multiple of 4
+__global__ __launch_bounds__(kBlock) void channel_stats_cf_kernel(const float* __restrict__ x, size_t plane, int C,
+                                                                  double* __restrict__ stats) {
+  const int c = (int)blockIdx.y % C;
+  const float* p = x + (size_t)blockIdx.y * plane;
+  double s = 0.0, q = 0.0;
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  if ((plane & 3) == 0) {
+    const float4* p4 = reinterpret_cast<const float4*>(p);
+    for (size_t j = (size_t)blockIdx.x * kBlock + threadIdx.x; j < plane / 4; j += stride) {
+      const float4 v = p4[j];
+      s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+      q += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    }
+  } else {
+    for (size_t j = (size_t)blockIdx.x * kBlock + threadIdx.x; j < plane; j += stride) {
+      const double v = p[j];
+      s += v;
+      q += v * v;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o);
+    q += __shfl_xor(q, o);
+  }
+  if (((int)threadIdx.x & 63) == 0) {
+    double* st = stats + (size_t)((blockIdx.x + blockIdx.y) % kStatSlots) * 2 * C;
+    atomicAdd(st + c, s);
+    atomicAdd(st + C + c, q);
+  }
+}
+
+__device__ inline float bn_relu(float v, float sc, float sh, float mu) { return fmaxf((v - mu) * sc + sh, 0.0f); }
+
+// y = relu((x - mean) * scale + shift) [+ relu((r - rmean) * rscale + rshift)], channels-last
+__global__ __launch_bounds__(kBlock) void bn_relu_cl_kernel(const float4* __restrict__ x, size_t n4, int C4,
+                                                            const float* __restrict__ sc, const float* __restrict__ sh,
+                                                            const float* __restrict__ mu, const float4* __restrict__ r,
+                                                            const float* __restrict__ rsc, const float* __restrict__ rsh,
+                                                            const float* __restrict__ rmu, float4* __restrict__ y) {
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  const size_t j0 = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  const int c = 4 * (int)(j0 % (size_t)C4);   // constant per thread (C4 divides the stride)
+  float a[4], b[4], m[4], ra[4] = {0, 0, 0, 0}, rb[4] = {0, 0, 0, 0}, rm[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    a[k] = sc[c + k];
+    b[k] = sh[c + k];
+    m[k] = mu[c + k];
+    if (r) {
+      ra[k] = rsc[c + k];
+      rb[k] = rsh[c + k];
+      rm[k] = rmu[c + k];
+    }
+  }
+  for (size_t j = j0; j < n4; j += stride) {
+    const float4 v = x[j];
+    float4 o = make_float4(bn_relu(v.x, a[0], b[0], m[0]), bn_relu(v.y, a[1], b[1], m[1]),
+                           bn_relu(v.z, a[2], b[2], m[2]), bn_relu(v.w, a[3], b[3], m[3]));
+    if (r) {
+      const float4 u = r[j];
+      o.x += bn_relu(u.x, ra[0], rb[0], rm[0]);
+      o.y += bn_relu(u.y, ra[1], rb[1], rm[1]);
+      o.z += bn_relu(u.z, ra[2], rb[2], rm[2]);
+      o.w += bn_relu(u.w, ra[3], rb[3], rm[3]);
+    }
+    y[j] = o;
+  }
+}
+
+// NCDHW: one (sample, channel) plane per blockIdx.y
+__global__ __launch_bounds__(kBlock) void bn_relu_cf_kernel(const float* __restrict__ x, size_t plane, int C,
+                                                            const float* __restrict__ sc, const float* __restrict__ sh,
+                                                            const float* __restrict__ mu, const float* __restrict__ r,
+                                                            const float* __restrict__ rsc, const float* __restrict__ rsh,
+                                                            const float* __restrict__ rmu, float* __restrict__ y) {
+  const int c = (int)blockIdx.y % C;
+  const size_t base = (size_t)blockIdx.y * plane;
+  const float a = sc[c], b = sh[c], m = mu[c];
+  const float ra = r ? rsc[c] : 0.0f, rb = r ? rsh[c] : 0.0f, rm = r ? rmu[c] : 0.0f;
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  if ((plane & 3) == 0) {
+    const float4* x4 = reinterpret_cast<const float4*>(x + base);
+    const float4* r4 = r ? reinterpret_cast<const float4*>(r + base) : nullptr;
+    float4* y4 = reinterpret_cast<float4*>(y + base);
+    for (size_t j = (size_t)blockIdx.x * kBlock + threadIdx.x; j < plane / 4; j += stride) {
+      const float4 v = x4[j];
+      float4 o = make_float4(bn_relu(v.x, a, b, m), bn_relu(v.y, a, b, m), bn_relu(v.z, a, b, m),
+                             bn_relu(v.w, a, b, m));
+      if (r4) {
+        const float4 u = r4[j];
+        o.x += bn_relu(u.x, ra, rb, rm);
+        o.y += bn_relu(u.y, ra, rb, rm);
+        o.z += bn_relu(u.z, ra, rb, rm);
+        o.w += bn_relu(u.w, ra, rb, rm);
+      }
+      y4[j] = o;
+    }
+  } else {
+    for (size_t j = (size_t)blockIdx.x * kBlock + threadIdx.x; j < plane; j += stride) {
+      float o = bn_relu(x[base + j], a, b, m);
+      if (r) o += bn_relu(r[base + j], ra, rb, rm);
+      y[base + j] = o;
+    }
+  }
+}
+
+unsigned grid_cl(size_t n4) {
+  const size_t blocks = (n4 + kBlock - 1) / kBlock;
+  return (unsigned)(blocks < 4096 ? blocks : 4096);
+}
+
+unsigned grid_cf(size_t plane, size_t planes) {
+  // about 2048 workgroups in total, at least one per plane
+  size_t per = (2048 + planes - 1) / planes;
+  const size_t need = (plane / 4 + kBlock - 1) / kBlock;
+  if (per > need) per = need;
+  return (unsigned)(per > 0 ? per : 1);
+}
+
+}  // namespace
+
+void launch_channel_stats(const float* x, bool channels_last, int B, int C, size_t voxels, double* stats,
+                          hipStream_t s) {
+  if (channels_last) {
+    const size_t n4 = (size_t)B * voxels * (size_t)C / 4;
+    hipLaunchKernelGGL(channel_stats_cl_kernel, dim3(grid_cl(n4)), dim3(kBlock), 0, s,
+                       reinterpret_cast<const float4*>(x), n4, C / 4, stats);
+  } else {
+    hipLaunchKernelGGL(channel_stats_cf_kernel, dim3(grid_cf(voxels, (size_t)B * C), (unsigned)(B * C)),
+                       dim3(kBlock), 0, s, x, voxels, C, stats);
+  }
+}
+
+void launch_bn_relu(const float* x, bool channels_last, int B, int C, size_t voxels, const float* sc,
+                    const float* sh, const float* mu, const float* r, const float* rsc, const float* rsh,
+                    const float* rmu, float* y, hipStream_t s) {
+  if (channels_last) {
+    const size_t n4 = (size_t)B * voxels * (size_t)C / 4;
+    hipLaunchKernelGGL(bn_relu_cl_kernel, dim3(grid_cl(n4)), dim3(kBlock), 0, s, reinterpret_cast<const float4*>(x),
+                       n4, C / 4, sc, sh, mu, reinterpret_cast<const float4*>(r), rsc, rsh, rmu,
+                       reinterpret_cast<float4*>(y));
+  } else {
+    hipLaunchKernelGGL(bn_relu_cf_kernel, dim3(grid_cf(voxels, (size_t)B * C), (unsigned)(B * C)), dim3(kBlock), 0,
+                       s, x, voxels, C, sc, sh, mu, r, rsc, rsh, rmu, y);
+  }
+}
+
+}  // namespace mvs

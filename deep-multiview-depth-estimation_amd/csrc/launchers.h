@@ -72,6 +72,14 @@ int launch_conv3d_region(int mode, bool out_cf, bool in_c4, const float* x, cons
                          const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                          hipStream_t s);
 
+// channel_ops.hip: train-mode BatchNorm pieces -- per-channel float64 sums into
+// stats[slot][2][C] (64 slots) and y = relu(BN(x)) [+ relu(BN'(r))], channels-last or NCDHW
+void launch_channel_stats(const float* x, bool channels_last, int B, int C, size_t voxels, double* stats,
+                          hipStream_t s);
+void launch_bn_relu(const float* x, bool channels_last, int B, int C, size_t voxels, const float* sc,
+                    const float* sh, const float* mu, const float* r, const float* rsc, const float* rsh,
+                    const float* rmu, float* y, hipStream_t s);
+
 // dtu_input.hip: data.py:206-210 image normalisation (uint8 HWC -> fp32 NCHW), data.py:300-301
 // depth thresholds
 void launch_normalize_images(const uint8_t* rgb, int n, uint32_t hw, const float* mean3,

@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmvs_cost_volume.so"
 # MVS_LIB_PATH: load another build of the same ABI (A/B kernel experiments, tools/exp_*.sh)
 LIB_PATH = os.environ.get("MVS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 MVS_OK = 0
 MVS_BWD_DETERMINISTIC = 1
@@ -26,6 +26,7 @@ MVS_LAYOUT_CHANNELS_LAST = 1
 MVS_CONV_S1, MVS_CONV_S2, MVS_CONV_T2 = 0, 1, 2
 MVS_CONV_OUT_NCDHW = 1
 MVS_CONV_IN_C4 = 2
+MVS_STATS_SLOTS = 64
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported n_views", -3: "too large",
           -4: "HIP runtime error"}
 
@@ -63,6 +64,8 @@ SIGNATURES = {
     "mvs_conv3d_k3_fwd": (_c_int, [_p, _c_int, _p, _p] + [_c_int] * 6 + [_p] * 4),
     "mvs_deconv3d_k3s2_fwd": (_c_int, [_p, _p] + [_c_int] * 10 + [_p] + [_c_int] * 6 + [_p] * 6),
     "mvs_conv3d_region_fwd": (_c_int, [_c_int, _c_int, _p, _p, _p, _p, _c_int, _c_int, _c_int] + [_p] * 10),
+    "mvs_channel_stats": (_c_int, [_p, _c_int, _c_int, _c_int, ctypes.c_longlong, _p, _p]),
+    "mvs_bn_relu": (_c_int, [_p, _c_int, _c_int, _c_int, ctypes.c_longlong] + [_p] * 9),
 }
 
 

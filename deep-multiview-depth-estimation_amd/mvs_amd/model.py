@@ -263,43 +263,44 @@ class CostVolumeReg(nn.Module):
         applied in place to the region tensors (channels-last).  The transposed convs run over
         the full output volume (their statistics) and keep the M-region part.  ``cv`` may be the
         channel-quad volume (conv_0_0 and the stride-2 convs read it with 16-byte loads)."""
-        from .ops import CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_region, deconv3d_k3s2, region_weight
+        from .ops import (CONV_S1, CONV_S2, CONV_T2, bn_relu_, channel_stats, conv3d_k3, conv3d_region,
+                          deconv3d_k3s2, region_weight)
         c4 = cv.dim() == 6
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad, bsz = list(n), list(self.pad), cv.shape[0]
         y0 = conv3d_k3(cv, self.conv_0_0.weight, in_c4=c4)
-        p0 = _bn_train(self.BN_0, *_sums(y0), count)
+        p0 = _bn_train(self.BN_0, *channel_stats(y0, False), count)
         stage = []
         for conv_a, bn in ((self.conv_1_0, self.BN_1), (self.conv_2_0, self.BN_2), (self.conv_3_0, self.BN_3)):
             z = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(R2), size(R2), None, None,
                               pad, in_c4=c4)
-            p = _bn_train(bn, *_sums(z, -1), count)
-            stage.append((_bn_relu_(z, p, -1), _bn_constant(p)))
+            p = _bn_train(bn, *channel_stats(z, True), count)
+            stage.append((bn_relu_(z, True, *p), _bn_constant(p)))
         lv = []
         for (y, a), conv_b, bn in zip(stage, (self.conv_1_1, self.conv_2_1, self.conv_3_1),
                                       (self.BN_1, self.BN_2, self.BN_3)):
             z = conv3d_region(y, None, region_weight(conv_b), CONV_S1, dims, org(R1), size(R1), org(R2),
                               size(R2), None)
-            s1, s2 = _sums(z, -1)
+            s1, s2 = channel_stats(z, True)
             c1, c2 = _border_class_sums(conv_b.weight, a, R1, n, bsz)
             p = _bn_train(bn, s1 + c1, s2 + c2, count)
-            lv.append(_bn_relu_(_crop_cl(z, R1, M), p, -1))
+            lv.append(bn_relu_(_crop_cl(z, R1, M), True, *p))
         y1, y2, y3 = lv
         z = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
                           size(M), pad)
-        p = _bn_train(self.BN_2, *_sums(z, -1), count)
-        y3 = _bn_relu_(_crop_cl(z, full, M), p, -1)
+        p = _bn_train(self.BN_2, *channel_stats(z, True), count)
+        y3 = bn_relu_(_crop_cl(z, full, M), True, *p)
         del z
         z = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
                           size(M), pad)
-        p = _bn_train(self.BN_1, *_sums(z, -1), count)
-        y2 = _bn_relu_(_crop_cl(z, full, M), p, -1)
+        p = _bn_train(self.BN_1, *channel_stats(z, True), count)
+        y2 = bn_relu_(_crop_cl(z, full, M), True, *p)
         del z
         z = deconv3d_k3s2(y2, org(M), self.deconv_1_0.weight, dims, pad, None, None, None, None, x2=y1,
                           channels_last=True)
-        p = _bn_train(self.BN_0, *_sums(z), count)
-        z = _bn_relu_(z, p, 1).add_(_bn_relu_(y0, p0, 1))
+        p = _bn_train(self.BN_0, *channel_stats(z, False), count)
+        z = bn_relu_(z, False, *p, r=y0, r_bn=p0)   # relu(BN_0(deconv_1_0)) + relu(BN_0'(conv_0_0))
         return self.Norm(conv3d_k3(z, self.conv_out.weight))
 
     def forward_full(self, cv):

@@ -497,3 +497,47 @@ def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, 
     if out_ncdhw:
         return x.new_empty((x.shape[0], weight.shape[1]) + tuple(out_size))
     return x.new_empty((x.shape[0],) + tuple(out_size) + (weight.shape[1],))
+
+
+# ----------------------------------------------------------------------------------------------
+# train-mode BatchNorm pieces of the regulariser (csrc/channel_ops.hip; forward_live_train)
+# ----------------------------------------------------------------------------------------------
+def channel_stats(x: torch.Tensor, channels_last: bool):
+    """Per-channel (sum, sum of squares) of x in float64 [C] each: channels on the last dim
+    (channels_last) or on dim 1 (NCDHW).  Inference only."""
+    _require_gpu(x, "x")
+    lib = _lib.load()
+    x = x.to(_F32).contiguous()
+    c = x.shape[-1] if channels_last else x.shape[1]
+    vox = x.numel() // (x.shape[0] * c)
+    st = torch.zeros((_lib.MVS_STATS_SLOTS, 2, c), device=x.device, dtype=torch.float64)
+    rc = lib.mvs_channel_stats(_lib.ptr(x), _lib.MVS_LAYOUT_CHANNELS_LAST if channels_last else 0, x.shape[0], c,
+                               vox, _lib.ptr(st), _lib.stream_handle(x.device))
+    _lib.check(rc, "mvs_channel_stats")
+    s = st.sum(0)
+    return s[0], s[1]
+
+
+def bn_relu_(x: torch.Tensor, channels_last: bool, scale, shift, mean, r=None, r_bn=None) -> torch.Tensor:
+    """In place: x = relu((x - mean) * scale + shift) [+ relu(BN_r(r))], channels on the last dim
+    (channels_last) or dim 1; r_bn = (scale, shift, mean) of r.  x must be contiguous fp32."""
+    _require_gpu(x, "x")
+    lib = _lib.load()
+    if not x.is_contiguous() or x.dtype != _F32:
+        raise ValueError("bn_relu_ works in place on a contiguous fp32 tensor")
+    c = x.shape[-1] if channels_last else x.shape[1]
+    vox = x.numel() // (x.shape[0] * c)
+    f = lambda t: t.to(device=x.device, dtype=_F32).contiguous()
+    sc, sh, mu = f(scale), f(shift), f(mean)
+    rr = rs = None
+    if r is not None:
+        rr = f(r)
+        if rr.shape != x.shape:
+            raise ValueError("r must have x's shape")
+        rs = [f(t) for t in r_bn]
+    pt = lambda t: None if t is None else _lib.ptr(t)
+    rc = lib.mvs_bn_relu(_lib.ptr(x), _lib.MVS_LAYOUT_CHANNELS_LAST if channels_last else 0, x.shape[0], c, vox,
+                         pt(sc), pt(sh), pt(mu), pt(rr), *(pt(t) for t in (rs or (None, None, None))), _lib.ptr(x),
+                         _lib.stream_handle(x.device))
+    _lib.check(rc, "mvs_bn_relu")
+    return x

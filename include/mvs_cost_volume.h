@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 2
+#define MVS_ABI_VERSION 3
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -265,6 +265,26 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
                           const int* out_size, const int* in_origin, const int* in_size,
                           const int* pad, const float* bn_scale, const float* bn_shift,
                           const float* bn_mean, void* stream);
+
+/* ---- train-mode BatchNorm of the regulariser (model.py:101-121 with every BatchNorm3d in training
+ * mode: test.py:53,61 runs `model.train()` under no_grad; CostVolumeReg.forward_live_train) ---- */
+#define MVS_STATS_SLOTS 64
+
+/* Per-channel batch sums of x: stats[slot][0][c] += sum of x over channel c, stats[slot][1][c] +=
+ * sum of x^2, in float64, over MVS_STATS_SLOTS slots (the caller zeroes stats, then adds the slots):
+ * the inputs of BatchNorm3d's batch mean and biased variance.  layout: MVS_LAYOUT_CHANNELS_LAST
+ * (x[batch][voxels][channels], channels / 4 a power of two <= 64, 16-byte aligned) or 0 (NCDHW
+ * x[batch][channels][voxels]). */
+int mvs_channel_stats(const float* x, int layout, int batch, int channels, long long voxels, double* stats,
+                      void* stream);
+
+/* y = max((x - mean) * scale + shift, 0) per channel (BatchNorm3d with the batch statistics:
+ * scale = gamma / sqrt(var + eps), shift = beta; then ReLU), and, when r is given,
+ * + max((r - r_mean) * r_scale + r_shift, 0) (model.py:121-123: relu(BN_0(deconv_1_0)) + y0).
+ * Layouts as mvs_channel_stats; y may alias x. */
+int mvs_bn_relu(const float* x, int layout, int batch, int channels, long long voxels, const float* scale,
+                const float* shift, const float* mean, const float* r, const float* r_scale,
+                const float* r_shift, const float* r_mean, float* y, void* stream);
 
 #ifdef __cplusplus
 }

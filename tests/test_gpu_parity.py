@@ -762,3 +762,32 @@ def test_mvsnet_channel_quad_feed_equals_ncdhw_feed():
             model_mod.warp_and_assemble_cost_volume = orig
     assert calls == [True]
     assert torch.equal(d4, d5) and torch.equal(r4, r5)
+
+
+@pytest.mark.parametrize("channels_last,C,shape", [(True, 16, (2, 5, 7, 9)), (True, 64, (1, 6, 6, 10)),
+                                                   (False, 8, (2, 6, 10, 12)), (False, 8, (1, 3, 5, 7))])
+def test_channel_stats_and_bn_relu_match_torch(channels_last, C, shape):
+    """csrc/channel_ops.hip (train-mode BN pieces of forward_live_train): float64 per-channel sums
+    and relu(BN(x)) [+ relu(BN'(r))] against torch on the same device; channels-last and NCDHW,
+    planes not a multiple of 4."""
+    from mvs_amd.ops import bn_relu_, channel_stats
+    g = torch.Generator().manual_seed(C + sum(shape))
+    b = shape[0]
+    full = (b,) + shape[1:] + (C,) if channels_last else (b, C) + shape[1:]
+    x = (torch.randn(full, generator=g) * 2 + 0.5).to(DEV)
+    r = torch.randn(full, generator=g).to(DEV)
+    cdim = -1 if channels_last else 1
+    red = [d for d in range(x.dim()) if d != cdim % x.dim()]
+    s1, s2 = channel_stats(x, channels_last)
+    torch.testing.assert_close(s1, x.double().sum(red), rtol=1e-12, atol=1e-9)
+    torch.testing.assert_close(s2, (x.double() ** 2).sum(red), rtol=1e-12, atol=1e-9)
+    p = [torch.rand(C, generator=g).to(DEV) + 0.5, torch.randn(C, generator=g).to(DEV), torch.randn(C, generator=g).to(DEV)]
+    q = [torch.rand(C, generator=g).to(DEV) + 0.5, torch.randn(C, generator=g).to(DEV), torch.randn(C, generator=g).to(DEV)]
+    shp = [1] * x.dim()
+    shp[cdim] = C
+    v = lambda t: t.view(shp)
+    ref = torch.relu((x - v(p[2])) * v(p[0]) + v(p[1])) + torch.relu((r - v(q[2])) * v(q[0]) + v(q[1]))
+    out = bn_relu_(x.clone(), channels_last, *p, r=r, r_bn=q)
+    torch.testing.assert_close(out, ref, rtol=1e-6, atol=1e-6)
+    ref1 = torch.relu((x - v(p[2])) * v(p[0]) + v(p[1]))
+    torch.testing.assert_close(bn_relu_(x.clone(), channels_last, *p), ref1, rtol=1e-6, atol=1e-6)

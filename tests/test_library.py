@@ -23,7 +23,7 @@ def _declared():
 def test_header_declares_the_abi():
     names = _declared()
     assert "mvs_cost_volume_fwd" in names and "mvs_cost_volume_bwd" in names
-    assert len(names) == 19, names
+    assert len(names) == 21, names
 
 
 def test_library_exports_every_declared_symbol():
@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from mvs_amd import _lib
     lib = _lib.load()
-    assert lib.mvs_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.mvs_abi_version() == _lib.ABI_VERSION == 3
     assert lib.mvs_status_string(0) == b"ok"
     assert lib.mvs_status_string(-2).startswith(b"n_views")
     assert lib.mvs_sampling_workspace_bytes(12, 192) == 12 * 192 * 9 * 4
@@ -78,6 +78,13 @@ def test_invalid_arguments_rejected_before_any_launch():
     assert lib.mvs_cost_volume_bwd_workspace_bytes(1, 3, 32, 128, 160, 0) == 0
     # 64-bit accumulators for every feature element + reference-view partials + scalars
     assert lib.mvs_cost_volume_bwd_workspace_bytes(4, 3, 32, 128, 160, 192) >= 12 * 32 * 128 * 160 * 8
+    # train-mode BN pieces: channels-last needs 4 | C with C / 4 a power of two, and 16-B alignment
+    assert lib.mvs_channel_stats(fake, 1, 2, 24, 100, fake, null) == -1
+    assert lib.mvs_channel_stats(ctypes.c_void_p(20), 1, 2, 16, 100, fake, null) == -1
+    assert lib.mvs_channel_stats(fake, 2, 2, 16, 100, fake, null) == -1
+    assert lib.mvs_channel_stats(fake, 0, 2, 16, 0, fake, null) == -1
+    assert lib.mvs_bn_relu(fake, 0, 2, 16, 100, fake, fake, None, None, None, None, None, fake, null) == -1
+    assert lib.mvs_bn_relu(fake, 0, 2, 16, 100, fake, fake, fake, fake, None, fake, fake, fake, null) == -1
 
 
 def test_build_is_gfx950_in_tree():
