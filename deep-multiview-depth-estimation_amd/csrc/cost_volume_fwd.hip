@@ -258,7 +258,12 @@ __device__ inline void store_out(Rsrc rs, uint32_t voff, float v) {
 //            read 4 channels of a voxel per load from it (MVSNet.forward's inference path)
 constexpr int kQuad = 16;
 
-constexpr int kPrefetch = 4;   // staging pieces per thread carried in registers across a chunk
+// staging pieces per thread carried in registers across a chunk: 4 covers the V = 3 footprints
+// (about 3.5 pieces per thread and chunk at cfg 2); 4 views of 4-plane groups average 6 (cfg 3)
+template <int V>
+constexpr int prefetch_pieces() {
+  return V <= 3 ? 4 : 8;
+}
 
 template <int V, int KPG, int ES /* output element bytes: 4 fp32, 2 bf16 */>
 __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_kernel(
@@ -485,6 +490,7 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
     return (uint32_t)(1 + s) * (uint32_t)c4 * pg.plane + (uint32_t)((y0 + row + 1) * pg.pitch + (x0 + col + 1));
   };
   const float4* pbase = packed + (size_t)b * V * c4 * pg.plane;
+  constexpr int kPrefetch = prefetch_pieces<V>();
   uint32_t psrc[kPrefetch], pslot[kPrefetch];
 #pragma unroll
   for (int j = 0; j < kPrefetch; ++j) {
@@ -515,10 +521,29 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
     // formally pending at the loop head and force a full vmcnt drain there)
 #pragma unroll
     for (int j = 0; j < kPrefetch; ++j) lds[pslot[j]] = f4v{pre[j].x, pre[j].y, pre[j].z, pre[j].w};
-    for (int q = (int)threadIdx.x + kBlock * kPrefetch; q < n_pieces; q += kBlock) {
-      uint32_t slot;
-      const float4 v = pbase[piece(q, slot) + (uint32_t)ch * pg.plane];
-      lds[slot] = f4v{v.x, v.y, v.z, v.w};
+    // pieces beyond the prefetch registers (rare at V <= 3): one at a time there; with more views
+    // four loads in flight per round (a load-store loop waits for every load; cfg 3 1.92 -> 1.85
+    // ms), rounds past the end targeting the dummy slot
+    if constexpr (V <= 3) {
+      for (int q = (int)threadIdx.x + kBlock * kPrefetch; q < n_pieces; q += kBlock) {
+        uint32_t slot;
+        const float4 v = pbase[piece(q, slot) + (uint32_t)ch * pg.plane];
+        lds[slot] = f4v{v.x, v.y, v.z, v.w};
+      }
+      return;
+    }
+    for (int q0 = (int)threadIdx.x + kBlock * kPrefetch; q0 < n_pieces; q0 += 4 * kBlock) {
+      uint32_t slot[4];
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = q0 + u * kBlock;
+        slot[u] = SLOTS - 1;
+        const uint32_t src = q < n_pieces ? piece(q, slot[u]) : 0u;
+        v[u] = pbase[src + (uint32_t)ch * pg.plane];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) lds[slot[u]] = f4v{v[u].x, v[u].y, v[u].z, v[u].w};
     }
   };
   stage(0);
