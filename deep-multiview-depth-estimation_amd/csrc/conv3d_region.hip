@@ -30,7 +30,7 @@ namespace {
 
 typedef float f4v_t __attribute__((ext_vector_type(4)));
 
-constexpr int kRows = 32;   // output voxels per wave (2 MFMA row blocks)
+// output voxels per wave: RB MFMA row blocks of 16 (template; 2 by default)
 
 template <int MODE>
 struct ConvMode {};
@@ -61,7 +61,7 @@ __device__ inline void store_out(float* __restrict__ y, const Geo& g, int b, int
   else y[((size_t)b * rvol + vox) * CO + co] = v;
 }
 
-template <int MODE, int CI, int CO>
+template <int MODE, int CI, int CO, int RB>
 __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
     const float* __restrict__ x, const float* __restrict__ x2, const float* __restrict__ w,
     float* __restrict__ y, const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
@@ -90,14 +90,15 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
   }
   const int rows = cn[0] * cn[1] * cn[2];
   const int step = MODE == kT2 ? 2 : 1;
+  constexpr int kRows = 16 * RB;
   const int row0 = ((int)blockIdx.x * (kBlock / 64) + ((int)threadIdx.x >> 6)) * kRows;
   if (row0 >= rows) return;   // wave-uniform; no barriers in this kernel
 
   // per row block: this lane's output voxel (volume coords), validity
-  int oz[2], oy[2], ox[2];
-  bool rok[2];
+  int oz[RB], oy[RB], ox[RB];
+  bool rok[RB];
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
+  for (int rb = 0; rb < RB; ++rb) {
     const int r = row0 + rb * 16 + m;
     rok[rb] = r < rows;
     const int rr = rok[rb] ? r : 0;
@@ -108,9 +109,9 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
     ox[rb] = cf[2] + step * jx;
   }
 
-  f4v_t acc[2][NB];
+  f4v_t acc[RB][NB];
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+  for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = f4v_t{0.0f, 0.0f, 0.0f, 0.0f};
 
@@ -123,11 +124,11 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
     for (int ty = 0; ty < 3; ++ty) {
       if (MODE == kT2 && ((ty & 1) != par[1])) continue;
       // input element offset of this lane's row (channel 0) per (x tap, row block), -1 = zero
-      long long off[3][2];
+      long long off[3][RB];
 #pragma unroll
       for (int tx = 0; tx < 3; ++tx)
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
+        for (int rb = 0; rb < RB; ++rb) {
           int iz, iy, ix;
           bool ok = rok[rb] && !(MODE == kT2 && ((tx & 1) != par[2]));
           if constexpr (MODE == kS1) {
@@ -158,12 +159,12 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
 #pragma unroll
       for (int cb = 0; cb < CI / 16; ++cb) {
         const int c4 = cb * 16 + kq * 4;
-        f4v_t a[3][2], bw[3][NB];
+        f4v_t a[3][RB], bw[3][NB];
 #pragma unroll
         for (int tx = 0; tx < 3; ++tx) {
           if (MODE == kT2 && ((tx & 1) != par[2])) continue;
 #pragma unroll
-          for (int rb = 0; rb < 2; ++rb) {
+          for (int rb = 0; rb < RB; ++rb) {
             f4v_t v = {0.0f, 0.0f, 0.0f, 0.0f};
             if (off[tx][rb] >= 0) {
               if constexpr (MODE == kS2) {
@@ -191,7 +192,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
 #pragma unroll
           for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int rb = 0; rb < 2; ++rb)
+            for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
               for (int nb = 0; nb < NB; ++nb)
                 acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[tx][rb][s], bw[tx][nb][s], acc[rb][nb], 0, 0, 0);
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
     const float sc = bn_scale ? bn_scale[co] : 1.0f, sh = bn_scale ? bn_shift[co] : 0.0f,
                 mu = bn_scale ? bn_mean[co] : 0.0f;
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+    for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = row0 + rb * 16 + kq * 4 + r;
@@ -223,7 +224,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
   }
 }
 
-template <int MODE, int CI, int CO>
+template <int MODE, int CI, int CO, int RB>
 void launch_mode(const float* x, const float* x2, const float* w, float* y, const float* sc, const float* sh,
                  const float* mu, int B, const Geo& g, hipStream_t s) {
   const int classes = MODE == kT2 ? 8 : 1;
@@ -231,9 +232,9 @@ void launch_mode(const float* x, const float* x2, const float* w, float* y, cons
   const int rz = MODE == kT2 ? (g.on[0] + 1) / 2 : g.on[0], ry = MODE == kT2 ? (g.on[1] + 1) / 2 : g.on[1],
             rx = MODE == kT2 ? (g.on[2] + 1) / 2 : g.on[2];
   const int rows = rz * ry * rx;
-  const int per_block = (kBlock / 64) * kRows;
+  const int per_block = (kBlock / 64) * 16 * RB;
   const dim3 grid((unsigned)((rows + per_block - 1) / per_block), (unsigned)classes, (unsigned)B);
-  hipLaunchKernelGGL((conv3d_region_kernel<MODE, CI, CO>), grid, dim3(kBlock), 0, s, x, x2, w, y, sc, sh, mu, g);
+  hipLaunchKernelGGL((conv3d_region_kernel<MODE, CI, CO, RB>), grid, dim3(kBlock), 0, s, x, x2, w, y, sc, sh, mu, g);
 }
 
 }  // namespace
@@ -253,9 +254,10 @@ int launch_conv3d_region(int mode, bool out_cf, bool in_c4, const float* x, cons
     g.in[d] = in ? in[d] : n[d];
     g.pad[d] = pad ? pad[d] : 1;
   }
+// two row blocks per wave (one and four measured slower on the cfg-2 eval and train-mode steps)
 #define MVS_REGION_CASE(MD, A, C)                                                       \
   if (mode == MD && CI == A && CO == C) {                                               \
-    launch_mode<MD, A, C>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s);           \
+    launch_mode<MD, A, C, 2>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s);        \
     return MVS_OK;                                                                      \
   }
   // S2: conv_1_0 / conv_2_0 / conv_3_0 (32 -> 16 / 32 / 64); S1: conv_k_1; T2: deconv_3_0 (64 -> 32),

@@ -17,7 +17,8 @@
 //   c = 0:  out(s=0) = U * W0 + L * W2,   out(s=1) = U * W1
 // -- the tensor product over the 3 dims is the block's 27 (input, tap) pairs, so a thread does
 // exactly the transposed conv's work, no lane diverges, and neighbouring lanes store adjacent
-// float2 pairs.  Weights of one input channel (8 x 27, padded to 28) are broadcast LDS reads.
+// float2 pairs.  Weights: workgroup-uniform scalar loads feeding the fmas' SGPR operand (NCDHW
+// input), broadcast LDS reads of the staged 8 x 27 (padded to 28) per channel (channels-last).
 // HBM-bound: the full-size output (+ residual read) dominates.
 #include "launchers.h"
 
@@ -46,14 +47,16 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
     const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
     const float* __restrict__ mean, const float* __restrict__ residual, float* __restrict__ y,
     int md_n, int mh_n, int mw_n, size_t total) {
-  extern __shared__ float4 wl4[];   // [ci][co][7] float4 = W[ci][co][27] padded
-  float* wl = reinterpret_cast<float*>(wl4);
-  const int nw = Cin * kCout * kWRow;
-  for (int e = (int)threadIdx.x; e < nw; e += kBlock) {
-    const int k = e % kWRow, cc = e / kWRow;
-    wl[e] = k < 27 ? wt[(size_t)cc * 27 + k] : 0.0f;
+  extern __shared__ float4 wl4[];   // CL: [ci][co][7] float4 = W[ci][co][27] padded
+  if constexpr (CL) {
+    float* wl = reinterpret_cast<float*>(wl4);
+    const int nw = Cin * kCout * kWRow;
+    for (int e = (int)threadIdx.x; e < nw; e += kBlock) {
+      const int k = e % kWRow, cc = e / kWRow;
+      wl[e] = k < 27 ? wt[(size_t)cc * 27 + k] : 0.0f;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const size_t gid = (size_t)blockIdx.x * kBlock + threadIdx.x;
   if (gid >= total) return;
   const int mw = (int)(gid % mw_n);
@@ -90,12 +93,21 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
   auto channel = [&](int ci, const float (&v)[2][2][2]) {
 #pragma unroll
     for (int co = 0; co < kCout; ++co) {
-      const float4* wr = wl4 + (ci * kCout + co) * (kWRow / 4);
       float w[kWRow];
+      if constexpr (CL) {   // broadcast LDS reads (4 channels per round keep SGPRs busy)
+        const float4* wr = wl4 + (ci * kCout + co) * (kWRow / 4);
 #pragma unroll
-      for (int q = 0; q < kWRow / 4; ++q) {
-        const float4 f = wr[q];
-        w[4 * q] = f.x; w[4 * q + 1] = f.y; w[4 * q + 2] = f.z; w[4 * q + 3] = f.w;
+        for (int q = 0; q < kWRow / 4; ++q) {
+          const float4 f = wr[q];
+          w[4 * q] = f.x; w[4 * q + 1] = f.y; w[4 * q + 2] = f.z; w[4 * q + 3] = f.w;
+        }
+      } else {
+        // workgroup-uniform scalar loads, the fmas' SGPR operand; the memory clobber keeps the
+        // compiler from hoisting every channel's weights at once
+        asm volatile("" ::: "memory");
+        const float* wr = wt + ((size_t)ci * kCout + co) * 27;
+#pragma unroll
+        for (int q = 0; q < 27; ++q) w[q] = wr[q];
       }
 #pragma unroll
       for (int sd = 0; sd < 2; ++sd)
@@ -137,7 +149,9 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
             }
             q[a][c][e] = t;
           }
-#pragma unroll
+      // one channel of the quad at a time (unrolled, the four channels' weight reads would be
+      // hoisted together: 504 VGPRs); the component is picked by selects
+#pragma unroll 1
       for (int j = 0; j < 4; ++j) {
         float v[2][2][2];
 #pragma unroll
@@ -227,7 +241,7 @@ void launch_deconv3d_k3s2(const float* x, const float* x2, bool channels_last, i
   const int md_n = (D + 1) / 2, mh_n = (H + 1) / 2, mw_n = (W + 1) / 2;
   const size_t total = (size_t)B * md_n * mh_n * mw_n;
   const dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
-  const size_t lds = (size_t)Cin * kCout * kWRow * sizeof(float);
+  const size_t lds = channels_last ? (size_t)Cin * kCout * kWRow * sizeof(float) : 0;
   const int cls = (pd & 1) * 4 + (ph & 1) * 2 + (pw & 1);
 #define MVS_DECONV_CASE(c)                                                                         \
   case c:                                                                                          \

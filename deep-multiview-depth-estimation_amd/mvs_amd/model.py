@@ -280,12 +280,14 @@ class CostVolumeReg(nn.Module):
         lv = []
         for (y, a), conv_b, bn in zip(stage, (self.conv_1_1, self.conv_2_1, self.conv_3_1),
                                       (self.BN_1, self.BN_2, self.BN_3)):
+            # level 1 only feeds deconv_1_0's input sum: channels-first for its loads
+            cf = bn is self.BN_1
             z = conv3d_region(y, None, region_weight(conv_b), CONV_S1, dims, org(R1), size(R1), org(R2),
-                              size(R2), None)
-            s1, s2 = channel_stats(z, True)
+                              size(R2), None, out_ncdhw=cf)
+            s1, s2 = channel_stats(z, not cf)
             c1, c2 = _border_class_sums(conv_b.weight, a, R1, n, bsz)
             p = _bn_train(bn, s1 + c1, s2 + c2, count)
-            lv.append(bn_relu_(_crop_cl(z, R1, M), True, *p))
+            lv.append(bn_relu_((_crop_cf if cf else _crop_cl)(z, R1, M), not cf, *p))
         y1, y2, y3 = lv
         z = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
                           size(M), pad)
@@ -293,12 +295,11 @@ class CostVolumeReg(nn.Module):
         y3 = bn_relu_(_crop_cl(z, full, M), True, *p)
         del z
         z = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
-                          size(M), pad)
-        p = _bn_train(self.BN_1, *channel_stats(z, True), count)
-        y2 = bn_relu_(_crop_cl(z, full, M), True, *p)
+                          size(M), pad, out_ncdhw=True)
+        p = _bn_train(self.BN_1, *channel_stats(z, False), count)
+        y2 = bn_relu_(_crop_cf(z, full, M), False, *p)
         del z
-        z = deconv3d_k3s2(y2, org(M), self.deconv_1_0.weight, dims, pad, None, None, None, None, x2=y1,
-                          channels_last=True)
+        z = deconv3d_k3s2(y2, org(M), self.deconv_1_0.weight, dims, pad, None, None, None, None, x2=y1)
         p = _bn_train(self.BN_0, *channel_stats(z, False), count)
         z = bn_relu_(z, False, *p, r=y0, r_bn=p0)   # relu(BN_0(deconv_1_0)) + relu(BN_0'(conv_0_0))
         return self.Norm(conv3d_k3(z, self.conv_out.weight))
@@ -355,6 +356,12 @@ def _bn_relu_(y, p, cdim):
     return y.sub_(v(mean)).mul_(v(scale)).add_(v(shift)).clamp_min_(0.0)
 
 
+def _crop_cf(x, x_reg, want):
+    """The box `want` (inside x_reg) of a channels-first region tensor x [B, C, d, h, w], contiguous."""
+    sl = [slice(lo - xlo, hi - xlo + 1) for (xlo, _), (lo, hi) in zip(x_reg, want)]
+    return x[:, :, sl[0], sl[1], sl[2]].contiguous()
+
+
 def _crop_cl(x, x_reg, want):
     """The box `want` (inside x_reg) of a channels-last region tensor x [B, d, h, w, C], contiguous."""
     sl = [slice(lo - xlo, hi - xlo + 1) for (xlo, _), (lo, hi) in zip(x_reg, want)]
@@ -400,22 +407,24 @@ def _border_class_sums(weight, a, reg, n, bsz):
     """Sums (value, value^2) per output channel of conv3d(field, weight, padding 1) over the
     voxels OUTSIDE reg, where the input field is the per-channel constant a everywhere the
     window of such a voxel reaches (in-volume taps only).  The output there depends only on the
-    voxel's border class: sum_ci a[ci] * sum_(in-volume taps) weight[co, ci, tap]."""
+    voxel's border class: sum_ci a[ci] * sum_(in-volume taps) weight[co, ci, tap].  All classes
+    at once (a few device ops, no per-class launches)."""
     w = weight.double()
-    a = a.double()
-    s1 = torch.zeros(w.shape[0], dtype=torch.float64, device=w.device)
-    s2 = torch.zeros_like(s1)
     per_dim = [_border_classes(d, lo, hi) for d, (lo, hi) in zip(n, reg)]
-    for td, nd, id_ in per_dim[0]:
-        for th, nh, ih in per_dim[1]:
-            for tw, nw, iw in per_dim[2]:
-                cnt = bsz * (nd * nh * nw - id_ * ih * iw)
-                if cnt == 0:
-                    continue
-                u = w[:, :, list(td)][:, :, :, list(th)][:, :, :, :, list(tw)].sum((2, 3, 4)) @ a
-                s1 += cnt * u
-                s2 += cnt * u * u
-    return s1, s2
+    masks, cnt, inside = [], [], []
+    for classes in per_dim:
+        masks.append(torch.tensor([[1.0 if k in taps else 0.0 for k in range(3)] for taps, _, _ in classes],
+                                  dtype=torch.float64, device=w.device))
+        cnt.append(torch.tensor([c for _, c, _ in classes], dtype=torch.float64, device=w.device))
+        inside.append(torch.tensor([i for _, _, i in classes], dtype=torch.float64, device=w.device))
+    # the constant field's response summed over each class's in-volume taps
+    wa = torch.einsum("oiabc,i->oabc", w, a.double())    # the field's response per tap
+    u = torch.einsum("oabc,zc->oabz", wa, masks[2])
+    u = torch.einsum("oabz,yb->oayz", u, masks[1])
+    u = torch.einsum("oayz,xa->oxyz", u, masks[0])
+    outer = lambda v: v[0].view(-1, 1, 1) * v[1].view(1, -1, 1) * v[2].view(1, 1, -1)
+    count = bsz * (outer(cnt) - outer(inside))            # voxels of each class outside reg
+    return (u * count).sum((1, 2, 3)), (u * u * count).sum((1, 2, 3))
 
 
 # ---- live-region helpers (CostVolumeReg.forward_live).  A region is a tuple of inclusive
