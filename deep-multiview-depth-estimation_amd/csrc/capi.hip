@@ -293,8 +293,14 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
     ivox *= (uint64_t)(mode == MVS_CONV_S2 ? dims[k] : in_size[k]);
     nvox *= (uint64_t)dims[k];
   }
-  // 32-bit row indices; element offsets are 64-bit
-  if (ovox >= (1ull << 31) || ivox * (uint64_t)c_in >= (1ull << 62) || nvox >= (1ull << 62)) return MVS_ERR_TOO_LARGE;
+  // 32-bit row indices; per sample, 32-bit buffer descriptors over the input (S2: the 16 channel planes
+  // or 4 channel quads of one 16-channel block, 64 B per voxel; S1 / T2: the region tensor)
+  uint64_t svox = 1;
+  for (int k = 0; k < 3; ++k) svox *= (uint64_t)(mode == MVS_CONV_S2 ? dims[k] : in_size[k]);
+  const uint64_t desc_bytes = mode == MVS_CONV_S2 ? svox * 64u : svox * (uint64_t)c_in * 4u;
+  if (ovox >= (1ull << 31) || desc_bytes >= 0xFFFFFFC0ull || ivox * (uint64_t)c_in >= (1ull << 62) ||
+      nvox >= (1ull << 62))
+    return MVS_ERR_TOO_LARGE;
   const int st = mvs::launch_conv3d_region(mode, (flags & MVS_CONV_OUT_NCDHW) != 0, (flags & MVS_CONV_IN_C4) != 0,
                                            x, x2, weight, y, batch, c_in, c_out, dims, out_origin, out_size,
                                            in_origin, in_size, pad, bn_scale, bn_shift, bn_mean,

@@ -24,11 +24,15 @@
 // per tap over channels in a fixed order -- MIOpen's kernels sum in other orders; same products,
 // fp32 rounding-level differences.
 #include "launchers.h"
+#include "packed.h"
 
 namespace mvs {
 namespace {
 
-typedef float f4v_t __attribute__((ext_vector_type(4)));
+typedef f4v f4v_t;
+// out-of-range buffer offset for taps without input (the loads return 0); every descriptor built
+// here covers less than 2^32 - 64 bytes (mvs_conv3d_region_fwd checks)
+constexpr uint32_t kOob = 0xFFFFFFC0u;
 
 // output voxels per wave: RB MFMA row blocks of 16 (template; 2 by default)
 
@@ -94,19 +98,39 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
   const int row0 = ((int)blockIdx.x * (kBlock / 64) + ((int)threadIdx.x >> 6)) * kRows;
   if (row0 >= rows) return;   // wave-uniform; no barriers in this kernel
 
-  // per row block: this lane's output voxel (volume coords), validity
-  int oz[RB], oy[RB], ox[RB];
-  bool rok[RB];
+  // per row block: this lane's input base voxel in the addressed space (the volume for S2, the
+  // input region for S1 / T2) and, per dim and tap, whether the tap's input exists; input voxel of
+  // tap t = base + delta(t) per dim with delta = t (S1, S2) or -(t >> 1) (T2, taps of the class's
+  // parity: t = par, par + 2)
+  int lim[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) lim[d] = MODE == kS2 ? g.n[d] : g.in[d];
+  int lin[RB];            // linear index of the base voxel (may be negative; masked)
+  unsigned vm[RB][3];     // per dim: bit t = tap t's input exists
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     const int r = row0 + rb * 16 + m;
-    rok[rb] = r < rows;
-    const int rr = rok[rb] ? r : 0;
+    const bool ok = r < rows;
+    const int rr = ok ? r : 0;
     const int jx = rr % cn[2], t = rr / cn[2];
     const int jy = t % cn[1], jz = t / cn[1];
-    oz[rb] = cf[0] + step * jz;
-    oy[rb] = cf[1] + step * jy;
-    ox[rb] = cf[2] + step * jx;
+    const int o[3] = {cf[0] + step * jz, cf[1] + step * jy, cf[2] + step * jx};
+    int bs[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      if constexpr (MODE == kS1) bs[d] = o[d] - 1 - g.i0[d];
+      else if constexpr (MODE == kS2) bs[d] = 2 * o[d] - g.pad[d];
+      else bs[d] = ((o[d] + g.pad[d] - par[d]) >> 1) - g.i0[d];
+      unsigned mk = 0;
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt) {
+        const int dl = MODE == kT2 ? -(tt >> 1) : tt;
+        const bool in = ok && bs[d] + dl >= 0 && bs[d] + dl < lim[d] && !(MODE == kT2 && ((tt & 1) != par[d]));
+        mk |= in ? (1u << tt) : 0u;
+      }
+      vm[rb][d] = mk;
+    }
+    lin[rb] = (bs[0] * lim[1] + bs[1]) * lim[2] + bs[2];
   }
 
   f4v_t acc[RB][NB];
@@ -115,43 +139,29 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = f4v_t{0.0f, 0.0f, 0.0f, 0.0f};
 
+  // buffer descriptors (workgroup-uniform bases; out-of-range offsets read 0): S2 the sample's
+  // volume (channel-quad: quads cb*4 .. cb*4+3 per channel block; NCDHW: 16 channel planes per
+  // block), S1 / T2 the sample's region tensor (and addend)
+  const size_t nvol = (size_t)g.n[0] * g.n[1] * g.n[2];
+  const size_t rvol = (size_t)g.in[0] * g.in[1] * g.in[2];
+  const int sy = lim[2], sz = lim[1] * lim[2];
   // ---- K loop: taps by rows (tz, ty); per row and 16-channel block the A values of its (up to)
-  // three x taps and both row blocks and the matching weights are loaded together, then fed to
+  // three x taps and every row block and the matching weights are loaded together, then fed to
   // the MFMAs (3x the loads in flight of a tap-at-a-time loop) ----
-  const size_t nvol = (size_t)g.n[0] * g.n[1] * g.n[2];                  // S2 channel plane
   for (int tz = 0; tz < 3; ++tz) {
     if (MODE == kT2 && ((tz & 1) != par[0])) continue;   // t of o + P's parity only
     for (int ty = 0; ty < 3; ++ty) {
       if (MODE == kT2 && ((ty & 1) != par[1])) continue;
-      // input element offset of this lane's row (channel 0) per (x tap, row block), -1 = zero
-      long long off[3][RB];
+      const int dz = MODE == kT2 ? -(tz >> 1) : tz, dy = MODE == kT2 ? -(ty >> 1) : ty;
+      // input voxel of this lane's row per (x tap, row block); kOob = no input (reads 0)
+      uint32_t vox[3][RB];
 #pragma unroll
       for (int tx = 0; tx < 3; ++tx)
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
-          int iz, iy, ix;
-          bool ok = rok[rb] && !(MODE == kT2 && ((tx & 1) != par[2]));
-          if constexpr (MODE == kS1) {
-            iz = oz[rb] + tz - 1;
-            iy = oy[rb] + ty - 1;
-            ix = ox[rb] + tx - 1;
-          } else if constexpr (MODE == kS2) {
-            iz = 2 * oz[rb] - g.pad[0] + tz;
-            iy = 2 * oy[rb] - g.pad[1] + ty;
-            ix = 2 * ox[rb] - g.pad[2] + tx;
-          } else {
-            iz = (oz[rb] + g.pad[0] - tz) >> 1;
-            iy = (oy[rb] + g.pad[1] - ty) >> 1;
-            ix = (ox[rb] + g.pad[2] - tx) >> 1;
-          }
-          ok = ok && iz >= 0 && iz < g.n[0] && iy >= 0 && iy < g.n[1] && ix >= 0 && ix < g.n[2];
-          if constexpr (MODE == kS2) {
-            off[tx][rb] = ok ? (long long)(((size_t)iz * g.n[1] + iy) * g.n[2] + ix) : -1;   // voxel
-          } else {
-            const int rz = iz - g.i0[0], ry = iy - g.i0[1], rx = ix - g.i0[2];
-            ok = ok && rz >= 0 && rz < g.in[0] && ry >= 0 && ry < g.in[1] && rx >= 0 && rx < g.in[2];
-            off[tx][rb] = ok ? (long long)((((size_t)b * g.in[0] + rz) * g.in[1] + ry) * g.in[2] + rx) * CI : -1;
-          }
+          const int dx = MODE == kT2 ? -(tx >> 1) : tx;
+          const bool ok = ((vm[rb][0] >> tz) & (vm[rb][1] >> ty) & (vm[rb][2] >> tx) & 1u) != 0;
+          vox[tx][rb] = ok ? (uint32_t)(lin[rb] + dz * sz + dy * sy + dx) : kOob;
         }
       // K = each tap's CI channels in blocks of 16: in K-step s of block cb, lane (m, kq) supplies
       // channel cb * 16 + 4 kq + s -- one 16-byte load per lane (4 consecutive channels of its row's
@@ -159,25 +169,35 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
 #pragma unroll
       for (int cb = 0; cb < CI / 16; ++cb) {
         const int c4 = cb * 16 + kq * 4;
+        Rsrc rs, rs2;
+        if constexpr (MODE == kS2) {
+          rs = g.in_c4 ? make_rsrc(x + ((size_t)b * (CI / 4) + cb * 4) * nvol * 4, (uint32_t)(nvol * 64))
+                       : make_rsrc(x + ((size_t)b * CI + cb * 16) * nvol, (uint32_t)(nvol * 64));
+        } else {
+          rs = make_rsrc(x + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
+          if (x2) rs2 = make_rsrc(x2 + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
+        }
         f4v_t a[3][RB], bw[3][NB];
 #pragma unroll
         for (int tx = 0; tx < 3; ++tx) {
           if (MODE == kT2 && ((tx & 1) != par[2])) continue;
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb) {
-            f4v_t v = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (off[tx][rb] >= 0) {
-              if constexpr (MODE == kS2) {
-                if (g.in_c4) {   // the quad (c4 / 4) of the voxel: one 16-byte load
-                  v = *reinterpret_cast<const f4v_t*>(x + (((size_t)b * (CI / 4) + c4 / 4) * nvol + off[tx][rb]) * 4);
-                } else {
-#pragma unroll
-                  for (int s = 0; s < 4; ++s) v[s] = x[((size_t)b * CI + c4 + s) * nvol + off[tx][rb]];
-                }
+            const uint32_t vx = vox[tx][rb];
+            f4v_t v;
+            if constexpr (MODE == kS2) {
+              if (g.in_c4) {   // the quad (c4 / 4) of the voxel: one 16-byte load
+                v = ld4(rs, vx == kOob ? kOob : ((uint32_t)kq * (uint32_t)nvol + vx) * 16u, 0);
               } else {
-                v = *reinterpret_cast<const f4v_t*>(x + off[tx][rb] + c4);
-                if (x2) v += *reinterpret_cast<const f4v_t*>(x2 + off[tx][rb] + c4);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                      rs, (int)(vx == kOob ? kOob : ((uint32_t)(kq * 4 + q) * (uint32_t)nvol + vx) * 4u), 0, 0));
               }
+            } else {
+              const uint32_t eo = vx == kOob ? kOob : (vx * (uint32_t)CI + (uint32_t)c4) * 4u;
+              v = ld4(rs, eo, 0);
+              if (x2) v += ld4(rs2, eo, 0);
             }
             a[tx][rb] = v;
           }
