@@ -42,6 +42,42 @@ def _conv_bn_relu_stack(spec, device):
     return nn.Sequential(*layers)
 
 
+def _run_stack(seq, x):
+    """A conv -> BatchNorm -> ReLU stack (encoder / refinement).  In fp32 no-grad inference on the
+    GPU every BatchNorm + ReLU pair is one in-place HIP pass (csrc/channel_ops.hip): eval BN from
+    the running statistics; train-mode BN (test.py:61) from one-pass float64 batch sums, with the
+    running statistics updated as torch does.  Elsewhere the modules themselves."""
+    if not _hip_inference(x):
+        return seq(x)
+    from .ops import bn_relu_, channel_stats
+    layers = list(seq)
+    i = 0
+    while i < len(layers):
+        layer = layers[i]
+        if (i + 2 < len(layers) and isinstance(layers[i + 1], nn.BatchNorm2d)
+                and isinstance(layers[i + 2], nn.ReLU)):
+            y = layer(x).contiguous()
+            bn = layers[i + 1]
+            if bn.running_mean is None or not bn.affine:   # no running statistics: the module
+                return _run_tail(layers[i:], x)
+            if bn.training:
+                p = _bn_train(bn, *channel_stats(y, False), y.numel() // y.shape[1])
+            else:
+                p = (bn.weight / torch.sqrt(bn.running_var + bn.eps), bn.bias, bn.running_mean)
+            x = bn_relu_(y, False, *p)
+            i += 3
+        else:
+            x = layer(x)
+            i += 1
+    return x
+
+
+def _run_tail(layers, x):
+    for layer in layers:
+        x = layer(x)
+    return x
+
+
 class FeatureEncoder(nn.Module):
     """model.py:22-65 -- images [N,3,H,W] -> features [N,32,H/4,W/4]."""
 
@@ -52,7 +88,7 @@ class FeatureEncoder(nn.Module):
         self.model = _conv_bn_relu_stack(_ENCODER, device)
 
     def forward(self, x):
-        return self.model(x)
+        return _run_stack(self.model, x)
 
 
 class CostVolumeReg(nn.Module):
@@ -512,7 +548,7 @@ class DepthRefinement(nn.Module):
         self.model = _conv_bn_relu_stack(_REFINE, device)
 
     def forward(self, depth_and_input):
-        return self.model(depth_and_input) + depth_and_input[:, 0].unsqueeze(1)
+        return _run_stack(self.model, depth_and_input) + depth_and_input[:, 0].unsqueeze(1)
 
 
 class MVSNet(nn.Module):

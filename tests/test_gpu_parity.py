@@ -791,3 +791,30 @@ def test_channel_stats_and_bn_relu_match_torch(channels_last, C, shape):
     torch.testing.assert_close(out, ref, rtol=1e-6, atol=1e-6)
     ref1 = torch.relu((x - v(p[2])) * v(p[0]) + v(p[1]))
     torch.testing.assert_close(bn_relu_(x.clone(), channels_last, *p), ref1, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_encoder_fused_bn_relu_matches_modules(train):
+    """FeatureEncoder / DepthRefinement on the HIP inference path (every BatchNorm + ReLU one
+    channel_ops pass; train mode: batch statistics from float64 sums and the running-statistic
+    update) against the nn.Sequential itself on the same device."""
+    import copy
+    from mvs_amd.model import DepthRefinement, FeatureEncoder
+    torch.manual_seed(0)
+    for net, shape in ((FeatureEncoder(), (3, 3, 96, 128)), (DepthRefinement(), (2, 4, 40, 48))):
+        for mod in net.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.running_mean.uniform_(-0.5, 0.5)
+                mod.running_var.uniform_(0.5, 2.0)
+                mod.weight.data.uniform_(0.5, 1.5)
+                mod.bias.data.uniform_(-0.5, 0.5)
+        a = net.to(DEV).train(train)
+        b = copy.deepcopy(a)
+        x = torch.randn(shape, generator=torch.Generator().manual_seed(5)).to(DEV)
+        with torch.no_grad():
+            ya = a(x)
+            yb = b.model(x) + (x[:, 0].unsqueeze(1) if isinstance(b, DepthRefinement) else 0)
+        torch.testing.assert_close(ya, yb, rtol=1e-4, atol=1e-5)
+        sa, sb = a.state_dict(), b.state_dict()
+        for k in sb:
+            torch.testing.assert_close(sa[k], sb[k], rtol=1e-5, atol=1e-6, msg=k)
