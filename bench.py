@@ -506,7 +506,8 @@ def main():
     if "train_bn" in result:
         out["train_bn"] = dict(result["train_bn"], unit="depth maps/s", note=(
             "test.py:53,61 mode: model.train() under no_grad, BatchNorm batch statistics over the "
-            "whole volume (forward_full)"))
+            "whole volume and running-statistic updates, exact on live regions "
+            "(CostVolumeReg.forward_live_train, DESIGN.md 5b)"))
     # backward of the fused op (train.py:103): informational
     log("timing the backward")
     out["cost_volume_backward"] = time_backward(B, V, C, h, w, d_count, device)
