@@ -310,6 +310,13 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
 }
 
 
+int mvs_softmax_depth_fwd(const float* x, int batch, int d_count, int h, int w, float* y, void* stream) {
+  if (!x || !y || batch <= 0 || d_count <= 0 || h <= 0 || w <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if ((uint64_t)h * (uint64_t)w >= (1ull << 32) || (uint64_t)batch * h * w >= (1ull << 37)) return MVS_ERR_TOO_LARGE;
+  mvs::launch_softmax_depth(x, batch, d_count, (uint32_t)((uint64_t)h * w), y, (hipStream_t)stream);
+  return mvs::hip_status();
+}
+
 static bool channel_layout_ok(int layout, int channels, const void* a, const void* b, const void* c) {
   if (layout & ~MVS_LAYOUT_CHANNELS_LAST) return false;
   if (!(layout & MVS_LAYOUT_CHANNELS_LAST)) return true;

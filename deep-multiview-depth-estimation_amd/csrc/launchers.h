@@ -43,7 +43,8 @@ int launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* fw
                            const float* grad_cv, void* bwd_ws, float* grad_feat, bool deterministic,
                            hipStream_t s);
 
-// soft_argmin.hip
+// soft_argmin.hip (+ the regulariser's softmax over depth, model.py:97)
+void launch_softmax_depth(const float* x, int B, int D, uint32_t hw, float* y, hipStream_t s);
 void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, uint32_t hw,
                         int n_est, float* depth, hipStream_t s);
 

@@ -68,4 +68,56 @@ void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, u
                        n_est, depth);
 }
 
+namespace {
+
+// model.py:97 (CostVolumeReg.Norm = nn.Softmax(2)) over the depth planes of the regulariser's
+// [B][1][D][h][w] output: per pixel m = max_d x, y_d = exp(x_d - m) / sum_d exp(x_d - m) -- the
+// operation order of torch's softmax (max, then the sum of exp(x - max), then a division).  One
+// thread per pixel, D reads coalesced across the wave (stride h*w), 64-thread workgroups so the
+// pixels of a small batch spread over every CU.
+__global__ __launch_bounds__(64) void softmax_depth_kernel(const float* __restrict__ x, int B, int D, uint32_t hw,
+                                                           float* __restrict__ y) {
+  const size_t e = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (e >= (size_t)B * hw) return;
+  const size_t b = e / hw, p = e - b * hw;
+  const float* xp = x + b * D * hw + p;
+  float* yp = y + b * D * hw + p;
+  // 8 planes' loads in flight per round (the loop is latency-bound otherwise); the sum keeps the
+  // sequential plane order
+  float m = -INFINITY;
+  int d = 0;
+  for (; d + 8 <= D; d += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = xp[(size_t)(d + k) * hw];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = fmaxf(m, v[k]);
+  }
+  for (; d < D; ++d) m = fmaxf(m, xp[(size_t)d * hw]);
+  float s = 0.0f;
+  for (d = 0; d + 8 <= D; d += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = xp[(size_t)(d + k) * hw];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += expf(v[k] - m);
+  }
+  for (; d < D; ++d) s += expf(xp[(size_t)d * hw] - m);
+  for (d = 0; d + 8 <= D; d += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = xp[(size_t)(d + k) * hw];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) yp[(size_t)(d + k) * hw] = expf(v[k] - m) / s;
+  }
+  for (; d < D; ++d) yp[(size_t)d * hw] = expf(xp[(size_t)d * hw] - m) / s;
+}
+
+}  // namespace
+
+void launch_softmax_depth(const float* x, int B, int D, uint32_t hw, float* y, hipStream_t s) {
+  const size_t n = (size_t)B * hw;
+  hipLaunchKernelGGL(softmax_depth_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, x, B, D, hw, y);
+}
+
 }  // namespace mvs

@@ -213,7 +213,8 @@ class CostVolumeReg(nn.Module):
         ReLU fused (csrc/conv3d_region.hip), deconv_1_0 + BN_0 + ReLU + `+ y0` and the `y2 + y1`
         sum in one kernel (csrc/deconv3d_region.hip), conv_out (conv3d_narrow.hip).  ``c4``: cv is
         the channel-quad volume, read by conv_0_0 and the three stride-2 convs with 16-byte loads."""
-        from .ops import CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_region, deconv3d_k3s2, region_weight
+        from .ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_region, deconv3d_k3s2, region_weight,
+                          softmax_depth)
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad = list(n), list(self.pad)
@@ -238,7 +239,7 @@ class CostVolumeReg(nn.Module):
         y2 = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, org(B), size(B), org(C2),
                            size(C2), pad, *bn_eval(self.BN_1), out_ncdhw=True)
         z = deconv3d_k3s2(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0, x2=y1)
-        return self.Norm(conv3d_k3(z, self.conv_out.weight))
+        return softmax_depth(conv3d_k3(z, self.conv_out.weight))
 
     def forward_live_train(self, cv):
         """Train-mode-BatchNorm regulariser (test.py:53,61: `model.train()` under `no_grad`)
@@ -300,7 +301,7 @@ class CostVolumeReg(nn.Module):
         the full output volume (their statistics) and keep the M-region part.  ``cv`` may be the
         channel-quad volume (conv_0_0 and the stride-2 convs read it with 16-byte loads)."""
         from .ops import (CONV_S1, CONV_S2, CONV_T2, bn_relu_, channel_stats, conv3d_k3, conv3d_region,
-                          deconv3d_k3s2, region_weight)
+                          deconv3d_k3s2, region_weight, softmax_depth)
         c4 = cv.dim() == 6
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
@@ -338,7 +339,7 @@ class CostVolumeReg(nn.Module):
         z = deconv3d_k3s2(y2, org(M), self.deconv_1_0.weight, dims, pad, None, None, None, None, x2=y1)
         p = _bn_train(self.BN_0, *channel_stats(z, False), count)
         z = bn_relu_(z, False, *p, r=y0, r_bn=p0)   # relu(BN_0(deconv_1_0)) + relu(BN_0'(conv_0_0))
-        return self.Norm(conv3d_k3(z, self.conv_out.weight))
+        return softmax_depth(conv3d_k3(z, self.conv_out.weight))
 
     def forward_full(self, cv):
         act = lambda bn, y: self.ReLU(bn(y))

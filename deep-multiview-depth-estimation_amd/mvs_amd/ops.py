@@ -541,3 +541,18 @@ def bn_relu_(x: torch.Tensor, channels_last: bool, scale, shift, mean, r=None, r
                          _lib.stream_handle(x.device))
     _lib.check(rc, "mvs_bn_relu")
     return x
+
+
+def softmax_depth(x: torch.Tensor) -> torch.Tensor:
+    """nn.Softmax(2) of the regulariser's [B, 1, D, h, w] output (model.py:97) on the HIP kernel.
+    Inference only."""
+    _require_gpu(x, "x")
+    lib = _lib.load()
+    if x.dim() != 5 or x.shape[1] != 1:
+        raise ValueError("softmax_depth expects [B, 1, D, h, w], got %s" % (tuple(x.shape),))
+    x = x.to(_F32).contiguous()
+    y = torch.empty_like(x)
+    b, _, d, h, w = x.shape
+    rc = lib.mvs_softmax_depth_fwd(_lib.ptr(x), b, d, h, w, _lib.ptr(y), _lib.stream_handle(x.device))
+    _lib.check(rc, "mvs_softmax_depth_fwd")
+    return y

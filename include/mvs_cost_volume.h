@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 3
+#define MVS_ABI_VERSION 4
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -265,6 +265,11 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
                           const int* out_size, const int* in_origin, const int* in_size,
                           const int* pad, const float* bn_scale, const float* bn_shift,
                           const float* bn_mean, void* stream);
+
+/* Softmax over the depth planes of the regulariser's output (CostVolumeReg.Norm = nn.Softmax(2),
+ * model.py:97 / :125): y[b][0][d][p] = exp(x - max_d x) / sum_d exp(x - max_d x) per pixel p, in
+ * torch's operation order; x, y [batch][1][d_count][h][w] fp32 (y may alias x). */
+int mvs_softmax_depth_fwd(const float* x, int batch, int d_count, int h, int w, float* y, void* stream);
 
 /* ---- train-mode BatchNorm of the regulariser (model.py:101-121 with every BatchNorm3d in training
  * mode: test.py:53,61 runs `model.train()` under no_grad; CostVolumeReg.forward_live_train) ---- */

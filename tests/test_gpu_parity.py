@@ -818,3 +818,12 @@ def test_encoder_fused_bn_relu_matches_modules(train):
         sa, sb = a.state_dict(), b.state_dict()
         for k in sb:
             torch.testing.assert_close(sa[k], sb[k], rtol=1e-5, atol=1e-6, msg=k)
+
+
+@pytest.mark.parametrize("shape", [(2, 1, 48, 32, 40), (1, 1, 7, 5, 9)])
+def test_softmax_depth_matches_torch(shape):
+    """mvs_softmax_depth_fwd (CostVolumeReg.Norm = nn.Softmax(2), model.py:97) against torch's
+    softmax on the same device."""
+    from mvs_amd.ops import softmax_depth
+    x = (torch.randn(shape, generator=torch.Generator().manual_seed(shape[2])) * 4).to(DEV)
+    torch.testing.assert_close(softmax_depth(x), torch.softmax(x, 2), rtol=2e-6, atol=1e-7)
