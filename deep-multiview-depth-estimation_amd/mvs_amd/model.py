@@ -222,7 +222,14 @@ class CostVolumeReg(nn.Module):
         def bn_eval(bn):
             return bn.weight / torch.sqrt(bn.running_var + bn.eps), bn.bias, bn.running_mean
 
-        y0 = conv3d_k3(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), in_c4=c4)
+        # conv_0_0 (VALU-bound) runs on a side stream, concurrently with the region chain (MFMA /
+        # memory-bound) that does not need it until deconv_1_0
+        main = torch.cuda.current_stream(cv.device)
+        side = _side_stream(cv.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            y0 = conv3d_k3(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), in_c4=c4)
+        cv.record_stream(side)
         lv = []
         for conv_a, conv_b, bn, reg in ((self.conv_1_0, self.conv_1_1, self.BN_1, B),
                                         (self.conv_2_0, self.conv_2_1, self.BN_2, C2),
@@ -238,6 +245,8 @@ class CostVolumeReg(nn.Module):
                            size(C3), pad, *bn_eval(self.BN_2))
         y2 = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, org(B), size(B), org(C2),
                            size(C2), pad, *bn_eval(self.BN_1), out_ncdhw=True)
+        main.wait_stream(side)
+        y0.record_stream(main)
         z = deconv3d_k3s2(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0, x2=y1)
         return softmax_depth(conv3d_k3(z, self.conv_out.weight))
 
@@ -306,8 +315,14 @@ class CostVolumeReg(nn.Module):
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad, bsz = list(n), list(self.pad), cv.shape[0]
-        y0 = conv3d_k3(cv, self.conv_0_0.weight, in_c4=c4)
-        p0 = _bn_train(self.BN_0, *channel_stats(y0, False), count)
+        # conv_0_0 and its batch statistics on a side stream, concurrently with the region chain
+        main = torch.cuda.current_stream(cv.device)
+        side = _side_stream(cv.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            y0 = conv3d_k3(cv, self.conv_0_0.weight, in_c4=c4)
+            p0 = _bn_train(self.BN_0, *channel_stats(y0, False), count)
+        cv.record_stream(side)
         stage = []
         for conv_a, bn in ((self.conv_1_0, self.BN_1), (self.conv_2_0, self.BN_2), (self.conv_3_0, self.BN_3)):
             z = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(R2), size(R2), None, None,
@@ -337,6 +352,9 @@ class CostVolumeReg(nn.Module):
         y2 = bn_relu_(_crop_cf(z, full, M), False, *p)
         del z
         z = deconv3d_k3s2(y2, org(M), self.deconv_1_0.weight, dims, pad, None, None, None, None, x2=y1)
+        main.wait_stream(side)
+        for t in (y0,) + tuple(p0):
+            t.record_stream(main)
         p = _bn_train(self.BN_0, *channel_stats(z, False), count)
         z = bn_relu_(z, False, *p, r=y0, r_bn=p0)   # relu(BN_0(deconv_1_0)) + relu(BN_0'(conv_0_0))
         return softmax_depth(conv3d_k3(z, self.conv_out.weight))
@@ -357,6 +375,17 @@ class CostVolumeReg(nn.Module):
         y2 = act(self.BN_1, self.deconv_2_0(y3 + y2))
         y1 = act(self.BN_0, self.deconv_1_0(y2 + y1))
         return self.Norm(_narrow_conv(self.conv_out, y1 + y0))
+
+
+_SIDE_STREAMS = {}
+
+
+def _side_stream(device):
+    """A second HIP stream per device for independent work of the inference step."""
+    key = torch.device(device).index
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = torch.cuda.Stream(device)
+    return _SIDE_STREAMS[key]
 
 
 def _hip_inference(x):
