@@ -194,6 +194,9 @@ int mvs_cost_volume_bwd(const float* feat, const float* workspace, const float* 
   Geometry g;
   const int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g);
   if (st != MVS_OK) return st;
+  // the packed backward reads grad_cv through a 32-bit descriptor over one 4-channel chunk
+  if (n_views >= 2 && n_views <= 8 && 16ull * (uint64_t)d_count * (uint64_t)h * (uint64_t)w >= (1ull << 31))
+    return MVS_ERR_TOO_LARGE;
   return mvs::launch_cost_volume_bwd(g, feat, workspace, grad_cv, bwd_workspace, grad_feat,
                                      (flags & MVS_BWD_DETERMINISTIC) != 0, (hipStream_t)stream);
 }

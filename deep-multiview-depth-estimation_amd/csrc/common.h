@@ -34,15 +34,11 @@ __device__ inline void sample_coord(const float* __restrict__ G, float xn, float
   float u = __fmaf_rn(G[1], yn, __fmaf_rn(G[0], xn, G[2]));
   float v = __fmaf_rn(G[4], yn, __fmaf_rn(G[3], xn, G[5]));
   const float s = __fmaf_rn(G[7], yn, __fmaf_rn(G[6], xn, G[8]));
-  if (fabsf(s) > 1e-8f) {
-#ifdef MVS_FAST_RCP
-    const float sc = __builtin_amdgcn_rcpf(__fadd_rn(s, 1e-8f));   // 1 ulp, 1 instruction
-#else
-    const float sc = __fdiv_rn(1.0f, __fadd_rn(s, 1e-8f));
-#endif
-    u = __fmul_rn(u, sc);
-    v = __fmul_rn(v, sc);
-  }
+  // selects, not a branch: the division runs on every lane and |s| <= 1e-8 keeps (u, v)
+  const bool div = fabsf(s) > 1e-8f;
+  const float sc = __fdiv_rn(1.0f, __fadd_rn(s, 1e-8f));
+  u = div ? __fmul_rn(u, sc) : u;
+  v = div ? __fmul_rn(v, sc) : v;
   ix = __fsub_rn(__fmul_rn(__fadd_rn(u, 1.0f), 0.5f * (float)w), 0.5f);
   iy = __fsub_rn(__fmul_rn(__fadd_rn(v, 1.0f), 0.5f * (float)h), 0.5f);
 }
@@ -128,6 +124,17 @@ __device__ inline T* uniform_ptr(T* p) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
   return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
+
+// A workgroup-uniform 3x3 sampling matrix through the constant address space: the loads become
+// s_load (scalar cache, lgkmcnt only).  Read through a generic pointer they are flat loads, which
+// count in vmcnt too, and every wait for them would also drain the wave's outstanding vector loads.
+typedef __attribute__((address_space(4))) const float const_float;
+
+__device__ inline void load_matrix_uniform(const float* p, float (&G)[9]) {
+  const const_float* c = (const const_float*)uniform_ptr(p);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) G[i] = c[i];
 }
 
 __device__ inline Rsrc make_rsrc(const void* base, uint32_t bytes) {

@@ -45,12 +45,18 @@ namespace {
 
 constexpr int kBwdTW = 32, kBwdTH = 8;
 constexpr int kBwdKPG = 32;              // planes per workgroup
-// LDS accumulator slots (x 4 channels x 8 B): 36 KB at V <= 3 (4 workgroups per CU: the loop is
-// latency-bound and occupancy pays more than fewer flushes, cfg 2 3.40 -> 3.12 ms), 48 KB above
-// (more views need the room: V = 5 15.5 -> 13.7 ms at 48 KB)
+// LDS accumulator image: slot-major, one slot = the 4 channels of one footprint pixel at a stride of
+// kSlotWords = 5 8-byte words: consecutive slots then fall on distinct bank pairs of a 16-lane
+// ds_add group (a stride of 4 words is a 4-way conflict: cfg 2 3.30 against 2.57 ms), and a tap's
+// 4 channels are immediate offsets of one address.  48 KB per workgroup (1228 slots, 3 workgroups
+// per CU): at V = 3 a single plane's footprint (both source views) fits, so no plane takes the
+// global-atomic path, and a 32-plane group needs 2.2 passes on average (tools/bwd_plan.py); 36 KB
+// at 4 workgroups per CU measured the same at cfg 2 and slower at cfg 1 and 3, 30 KB at 5 waves per
+// SIMD 1.6x slower (5 % of the planes overflow to global atomics).
+constexpr int kSlotWords = 5;
 template <int V>
 constexpr int bwd_slots() {
-  return V <= 3 ? 1152 : 1536;
+  return 49152 / (8 * kSlotWords);
 }
 typedef unsigned long long u64;
 
@@ -104,11 +110,14 @@ __global__ __launch_bounds__(kBlock) void abs_max_kernel(const float* __restrict
 }
 
 // ---- per-(plane, view) footprint boxes -----------------------------------------------------------
-// Box of the in-image taps of a tile for one (plane, view), from the tile's 4 corner pixels: with
-// the homogeneous coordinate s of one sign and |s| > 1e-8 at the corners (s is affine in the pixel,
-// so then everywhere in the tile) the tile maps to a convex quad whose bounding box is the corners'
-// bounding box (taps x0 .. x0 + 1).  A tap that fp32 rounding of an interior pixel puts just
-// outside goes straight to the global accumulators.  Otherwise (pole in the tile): the whole image.
+// Box of the taps of a tile for one (plane, view), from the tile's 4 corner pixels: with the
+// homogeneous coordinate s of one sign and |s| > 1e-8 at the corners (s is affine in the pixel, so
+// then everywhere in the tile) the tile maps to a convex quad whose bounding box is the corners'
+// bounding box (taps x0 .. x0 + 1).  Boxes are clipped to the image plus its one-pixel zero border
+// ([-1, w] x [-1, h], where every tap of a valid sample lies): border slots collect the taps the
+// zero padding drops, and are never flushed, so the accumulation needs no per-tap bounds test.  A
+// sample whose taps fp32 rounding of an interior pixel puts just outside goes straight to the
+// global accumulators.  Otherwise (pole in the tile): the whole bordered image.
 struct Box {
   int x0, y0, x1, y1;   // inclusive, clipped to the image; x1 < x0 = empty
 };
@@ -146,12 +155,12 @@ __device__ Box tile_box(const float* __restrict__ G, int px0, int py0, int px1, 
     mxx = fmaxf(mxx, ix);
     mxy = fmaxf(mxy, iy);
   }
-  if (bad || (pos && neg)) return Box{0, 0, w - 1, h - 1};
+  if (bad || (pos && neg)) return Box{-1, -1, w, h};
   Box b;
-  b.x0 = max((int)floorf(mnx), 0);
-  b.y0 = max((int)floorf(mny), 0);
-  b.x1 = min((int)floorf(mxx) + 1, w - 1);
-  b.y1 = min((int)floorf(mxy) + 1, h - 1);
+  b.x0 = max((int)floorf(mnx), -1);
+  b.y0 = max((int)floorf(mny), -1);
+  b.x1 = min((int)floorf(mxx) + 1, w);
+  b.y1 = min((int)floorf(mxy) + 1, h);
   return b;
 }
 
@@ -181,7 +190,7 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
   constexpr int NS = V - 1;
   typedef typename Acc<DET>::lds_t lds_t;
   constexpr int kBwdSlots = bwd_slots<V>();
-  __shared__ lds_t lds[4 * kBwdSlots];
+  __shared__ lds_t lds[kSlotWords * kBwdSlots];
   __shared__ Box boxes[kBwdKPG][NS];
 
   const int wk = xcd_work_id(blockIdx.x, total);
@@ -217,10 +226,11 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
   const f4v two_inv_v = inv_v + inv_v;
   const int soff = (int)((uint32_t)ch * pg.plane * 16u);
   const int row_bytes = pg.pitch * 16;
-  // grad_cv of channel 4 ch + j, plane k0 + pl at this pixel: gcv + j * cstride + pl * hw
-  const size_t cstride = (size_t)Dc * hw;
-  const float* gcv = grad_cv + (((size_t)b * C + (size_t)ch * 4) * Dc + k0) * hw + pix;
+  // grad_cv of channel 4 ch + j, plane k0 + pl at this pixel: byte j * cst_bytes + (pl * hw + pix) * 4
   const int nch = min(C - ch * 4, 4);
+  const uint32_t cst_bytes = (uint32_t)Dc * hw * 4u;   // < 2^29 (mvs_cost_volume_bwd checks 16 Dc hw)
+  const Rsrc grs = make_rsrc(uniform_ptr(grad_cv + (((size_t)b * C + (size_t)ch * 4) * Dc + k0) * hw),
+                             (uint32_t)uniform((int)((uint32_t)(nch - 1) * cst_bytes + (uint32_t)(Dc - k0) * hw * 4u)));
   // per-image planes of this chunk's channels (global accumulators / gradient)
   auto gidx = [&](int n, int j, int yy, int xx) -> size_t {
     return ((size_t)n * C + (size_t)ch * 4 + j) * hw + (size_t)yy * w + xx;
@@ -229,6 +239,14 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
     if constexpr (DET) gadd(acc + gidx(n, j, yy, xx), v);
     else unsafeAtomicAdd(grad_feat + gidx(n, j, yy, xx), (float)v);
   };
+  // per source view: sampling matrices of the group's planes, packed-feature descriptor (uniform)
+  const float* smat[NS];
+  Rsrc prs[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    smat[s] = uniform_ptr(sampling + ((size_t)(b * V + 1 + s) * Dc + k0) * 9);
+    prs[s] = make_rsrc(uniform_ptr(packed + (size_t)(b * V + 1 + s) * c4 * pg.plane), (uint32_t)c4 * pg.plane * 16u);
+  }
   f4v racc = {0.0f, 0.0f, 0.0f, 0.0f};
   __syncthreads();   // boxes
 
@@ -281,7 +299,7 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
       }
     }
     const bool use_lds = area <= kBwdSlots;
-    const int T = use_lds ? area : 0;   // slots per channel plane of the LDS image
+    const int T = use_lds ? area : 0;   // slots of the LDS image
     int base[NS], bw[NS];
     {
       int o = 0;
@@ -293,40 +311,45 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
       }
     }
     if (use_lds) {
-      for (int q = (int)threadIdx.x; q < 4 * T; q += kBlock) lds[q] = (lds_t)0;
+      for (int q = (int)threadIdx.x; q < kSlotWords * T; q += kBlock) lds[q] = (lds_t)0;
       __syncthreads();
     }
 
     // ---- the pass's planes (every lane runs them; inactive lanes have g = 0 and no taps) ----
     // grad_cv of the chunk's 4 channels at this pixel, one plane ahead (the HBM read of the loop)
+    // (buffer loads, no branches or selects: channels >= C lie past the descriptor's range and read
+    // 0; inactive lanes read pixel 0 and have no taps.  Every plane issues the same 4 loads, so the
+    // waits on them are counted exactly)
     auto load_g = [&](int pl) {
-      f4v g = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (active) {
+      f4v g;
+      const uint32_t o = ((uint32_t)pl * hw + pix) * 4u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (j < nch) g[j] = gcv[(size_t)j * cstride + (size_t)pl * hw];
-      }
+      for (int j = 0; j < 4; ++j)
+        g[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, o + (uint32_t)j * cst_bytes, 0, 0));
       return g;
     };
+    // grad_cv one plane ahead, issued after the plane's tap gathers (vmcnt retires loads in issue
+    // order: waiting for the gathers then leaves the next plane's grad_cv loads in flight)
     f4v g_next = load_g(kp);
     for (int pl = kp; pl < ke; ++pl) {
-      const int kk = k0 + pl;
       const f4v g = g_next;
-      g_next = load_g(min(pl + 1, ke - 1));
       uint32_t pos[NS];
       float wx[NS], wy[NS];
+      f4v tp[NS][4];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        // the sampling matrix is workgroup-uniform: scalar loads (load_matrix_uniform)
+        float G[9];
+        load_matrix_uniform(smat[s] + pl * 9, G);
+        src_coords(G, xn, yn, h, w, active, pos[s], wx[s], wy[s]);
+        load_taps(prs[s], tap_offset(pos[s], pg), soff, row_bytes, tp[s]);
+      }
+      g_next = load_g(min(pl + 1, ke - 1));
       f4v xs[NS];
       f4v sum = x0;
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        // the sampling matrix is workgroup-uniform: scalar loads
-        src_coords(uniform_ptr(sampling + ((size_t)(b * V + 1 + s) * Dc + kk) * 9), xn, yn, h, w, active,
-                   pos[s], wx[s], wy[s]);
-        const Rsrc rs = make_rsrc(uniform_ptr(packed + (size_t)(b * V + 1 + s) * c4 * pg.plane),
-                                  (uint32_t)c4 * pg.plane * 16u);
-        f4v tp[4];
-        load_taps(rs, tap_offset(pos[s], pg), soff, row_bytes, tp);
-        xs[s] = bilerp(tp, wx[s], wy[s]);
+        xs[s] = bilerp(tp[s], wx[s], wy[s]);
         sum += xs[s];
       }
       const f4v nmean = -(sum * inv_v);
@@ -334,23 +357,35 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
       if (s0 == 0) racc += k2 * (x0 + nmean);
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        if (s < s0 || s >= s1 || pos[s] == kInvalidTap) continue;
+        if (s < s0 || s >= s1) continue;   // uniform
         const f4v cs = k2 * (xs[s] + nmean);
         const float ex = 1.0f - wx[s], ny = 1.0f - wy[s];
         const float wt[4] = {ny * ex, ny * wx[s], wy[s] * ex, wy[s] * wx[s]};
         const int cx = pos_x(pos[s]), cy = pos_y(pos[s]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int xx = cx + (q & 1), yy = cy + (q >> 1);
-          if (xx < 0 || xx >= w || yy < 0 || yy >= h) continue;   // zero padding: no gradient
-          const bool in_box = use_lds && xx >= ub[s].x0 && xx <= ub[s].x1 && yy >= ub[s].y0 && yy <= ub[s].y1;
-          const int slot = base[s] + (yy - ub[s].y0) * bw[s] + (xx - ub[s].x0);
+        const bool valid = pos[s] != kInvalidTap;
+        const bool inb = use_lds && valid && cx >= ub[s].x0 && cx < ub[s].x1 && cy >= ub[s].y0 && cy < ub[s].y1;
+        // all 4 taps inside the pass's box: 16 LDS adds at immediate offsets of two addresses
+        if (inb) {
+          lds_t* a0 = lds + (base[s] + (cy - ub[s].y0) * bw[s] + (cx - ub[s].x0)) * kSlotWords;
+          lds_t* a1 = a0 + bw[s] * kSlotWords;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            if (j >= nch) break;
-            const lds_t v = Acc<DET>::conv(wt[q] * cs[j], sc);
-            if (in_box) atomicAdd(&lds[j * T + slot], v);
-            else gadd_out(b * V + 1 + s, j, yy, xx, v);
+            atomicAdd(a0 + j, Acc<DET>::conv(wt[0] * cs[j], sc));
+            atomicAdd(a0 + kSlotWords + j, Acc<DET>::conv(wt[1] * cs[j], sc));
+            atomicAdd(a1 + j, Acc<DET>::conv(wt[2] * cs[j], sc));
+            atomicAdd(a1 + kSlotWords + j, Acc<DET>::conv(wt[3] * cs[j], sc));
+          }
+        }
+        // no LDS image for this pass, or a rounding outlier: in-image taps to the accumulators
+        // (a wave-uniform test first: the common wave skips the whole path with one scalar branch)
+        if (__builtin_amdgcn_ballot_w64(valid && !inb) != 0 && valid && !inb) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int xx = cx + (q & 1), yy = cy + (q >> 1);
+            if (xx < 0 || xx >= w || yy < 0 || yy >= h) continue;   // zero padding: no gradient
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (j < nch) gadd_out(b * V + 1 + s, j, yy, xx, Acc<DET>::conv(wt[q] * cs[j], sc));
           }
         }
       }
@@ -374,11 +409,13 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
             by = ub[q].y0;
           }
         const int r = (e - o) / ww, c = (e - o) - r * ww;
+        const int yy = by + r, xx = bx + c;
+        if (xx < 0 || xx >= w || yy < 0 || yy >= h) continue;   // border slot: padding taps
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (j >= nch) break;
-          const lds_t v = lds[j * T + e];
-          if (v != (lds_t)0) gadd_out(b * V + 1 + s, j, by + r, bx + c, v);
+          const lds_t v = lds[e * kSlotWords + j];
+          if (v != (lds_t)0) gadd_out(b * V + 1 + s, j, yy, xx, v);
         }
       }
       __syncthreads();   // the next pass re-zeroes the image

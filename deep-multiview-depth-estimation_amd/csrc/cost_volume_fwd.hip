@@ -304,8 +304,9 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
     for (int s = 0; s < NS; ++s) {
       // planes past the group's end (last group only) compute a clamped plane, then drop it
       const int kk = k0 + (pl < npl ? pl : npl - 1);
-      src_coords(sampling + ((size_t)(b * V + 1 + s) * Dc + kk) * 9, xn, yn, h, w, active,
-                 pos[pl][s], fwx[pl][s], fwy[pl][s]);
+      float G[9];
+      load_matrix_uniform(sampling + ((size_t)(b * V + 1 + s) * Dc + kk) * 9, G);
+      src_coords(G, xn, yn, h, w, active, pos[pl][s], fwx[pl][s], fwy[pl][s]);
       if (pl >= npl) {
         pos[pl][s] = kInvalidTap;
         fwx[pl][s] = fwy[pl][s] = 0.0f;
