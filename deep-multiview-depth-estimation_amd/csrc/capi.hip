@@ -47,11 +47,12 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
   Geometry g;
   int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g);
   if (st != MVS_OK) return st;
-  st = mvs_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
-                          d_scale, workspace, stream);
-  if (st != MVS_OK) return st;
+  if (!cams_ok(K, R, T, d_min, d_int) || d_begin < 0) return MVS_ERR_INVALID_ARGUMENT;
   hipStream_t s = (hipStream_t)stream;
   if (n_views == 1) {  // the variance of a single view is identically zero (0 in fp32 and bf16)
+    st = mvs_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
+                            d_scale, workspace, stream);
+    if (st != MVS_OK) return st;
     const size_t ch = es == 16 ? (size_t)((channels + 3) / 4) : (size_t)channels;
     if (hipMemsetAsync(cv_out, 0, (size_t)batch_size * ch * d_count * h * w * es, s) != hipSuccess)
       return MVS_ERR_HIP;
@@ -60,14 +61,15 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
   float* packed = reinterpret_cast<float*>(
       reinterpret_cast<char*>(workspace) +
       mvs::align256((size_t)batch_size * n_views * d_count * 9 * sizeof(float)));
+  const mvs::Cams cm{K, R, T, d_min, d_int, d_begin, d_scale};
   if (es == 4)
-    mvs::launch_cost_volume_fwd(g, feat, workspace, packed, static_cast<float*>(cv_out), s,
+    mvs::launch_cost_volume_fwd(g, feat, cm, workspace, packed, static_cast<float*>(cv_out), s,
                                 (hipEvent_t)ev0, (hipEvent_t)ev1);
   else if (es == 16)
-    mvs::launch_cost_volume_fwd_c4(g, feat, workspace, packed, static_cast<float*>(cv_out), s,
+    mvs::launch_cost_volume_fwd_c4(g, feat, cm, workspace, packed, static_cast<float*>(cv_out), s,
                                    (hipEvent_t)ev0, (hipEvent_t)ev1);
   else
-    mvs::launch_cost_volume_fwd_bf16(g, feat, workspace, packed, cv_out, s, (hipEvent_t)ev0,
+    mvs::launch_cost_volume_fwd_bf16(g, feat, cm, workspace, packed, cv_out, s, (hipEvent_t)ev0,
                                      (hipEvent_t)ev1);
   return mvs::hip_status();
 }

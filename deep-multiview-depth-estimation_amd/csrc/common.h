@@ -192,6 +192,14 @@ __device__ inline void pixel_coords(uint32_t p, int w, int h, float& xn, float& 
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
+// camera inputs of one cost-volume launch (device pointers, homography.py:6-36) and the shard's
+// first plane
+struct Cams {
+  const float *K, *R, *T, *d_min, *d_int;
+  int d_begin;
+  float d_scale;
+};
+
 struct Geometry {
   int B, V, C, h, w, Dc;
   int tiles;  // flattened 256-pixel tiles per plane

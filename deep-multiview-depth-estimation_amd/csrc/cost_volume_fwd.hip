@@ -23,6 +23,7 @@
 // Workgroup ids are remapped so each XCD walks consecutive (tile, plane group) items.
 #include "launchers.h"
 #include "packed.h"
+#include "sampling_matrix.h"
 
 namespace mvs {
 namespace {
@@ -91,34 +92,6 @@ __global__ __launch_bounds__(kBlock) void cost_volume_kernel(
   }
 }
 
-// Padded channel-quad layout of the workspace: packed.h.
-
-__global__ __launch_bounds__(kBlock) void pack_pad_kernel(const float* __restrict__ feat,
-                                                          float4* __restrict__ packed, int N, int C,
-                                                          int h, int w) {
-  const int c4 = (C + 3) / 4;
-  const PadGeom pg = pad_geom(h, w);
-  const uint32_t hw = (uint32_t)h * (uint32_t)w;
-  const size_t n = (size_t)N * c4 * pg.plane;
-  for (size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (size_t)gridDim.x * kBlock) {
-    const uint32_t q = (uint32_t)(e % pg.plane);
-    const size_t t = e / pg.plane;
-    const int ch = (int)(t % c4);
-    const size_t i = t / c4;
-    const int y = (int)(q / (uint32_t)pg.pitch) - 1;
-    const int x = (int)(q % (uint32_t)pg.pitch) - 1;
-    float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (x >= 0 && x < w && y >= 0 && y < h) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = ch * 4 + j;
-        if (c < C) v[j] = feat[(i * C + c) * hw + (size_t)y * w + x];
-      }
-    }
-    packed[e] = make_float4(v[0], v[1], v[2], v[3]);
-  }
-}
-
 // costvolume.py:12-14: mean = sum / V, cv = sum (x - mean)^2 / V (two-pass), 4 channels at once;
 // every intermediate rounded as written (no contraction of the mean into the differences).
 template <int NS>
@@ -138,28 +111,82 @@ __device__ inline f4v variance4(const f4v& x0, const f4v (&xs)[NS], const f4v& i
   return acc * inv_v;
 }
 
-// refs[b][ch][p] = bilinear sample of the reference image b*V through G(b*V, plane 0).
-__global__ __launch_bounds__(kBlock) void ref_resample_kernel(const float4* __restrict__ packed,
-                                                              const float* __restrict__ sampling,
-                                                              float4* __restrict__ refs, int B, int V,
-                                                              int C, int h, int w, int Dc) {
+// Prologue of the fused launch: ONE kernel, three independent jobs by workgroup range (they used
+// to be three dependent launches; cfg 4's 32-plane shard is launch-bound):
+//   [0, nb_smp)                sampling matrices G[N][Dc][9] (sampling_matrix.h), one per thread;
+//   [nb_smp, nb_smp + nb_pack) padded channel-quad features (packed.h), grid-stride;
+//   the rest                   refs[b][ch][p]: the reference image b*V bilinearly sampled through its
+//                              own G (shard plane 0, computed here by the same function, so it is
+//                              the matrix the sampling job stores), read from the NCHW features
+//                              with the packed layout's rules (taps outside the image are 0; same
+//                              taps, weights and fma order as bilerp): bit-identical to sampling the
+//                              packed image.
+__global__ __launch_bounds__(kBlock) void prologue_kernel(const float* __restrict__ feat, Cams cm,
+                                                          float* __restrict__ sampling,
+                                                          float4* __restrict__ packed, float4* __restrict__ refs,
+                                                          int B, int V, int C, int h, int w, int Dc, int nb_smp,
+                                                          int nb_pack) {
+  const int N = B * V;
   const int c4 = (C + 3) / 4;
   const uint32_t hw = (uint32_t)h * (uint32_t)w;
-  const PadGeom pg = pad_geom(h, w);
-  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  const int ch = (int)blockIdx.y % c4;
-  const int b = (int)blockIdx.y / c4;
+  int blk = (int)blockIdx.x;
+  if (blk < nb_smp) {
+    const int t = blk * kBlock + (int)threadIdx.x;
+    if (t < N * Dc) {
+      const int i = t / Dc;
+      sampling_matrix(cm, B, V, h, w, i, t - i * Dc, sampling + 9 * (size_t)t);
+    }
+    return;
+  }
+  blk -= nb_smp;
+  if (blk < nb_pack) {
+    const PadGeom pg = pad_geom(h, w);
+    const size_t n = (size_t)N * c4 * pg.plane;
+    for (size_t e = (size_t)blk * kBlock + threadIdx.x; e < n; e += (size_t)nb_pack * kBlock) {
+      const uint32_t q = (uint32_t)(e % pg.plane);
+      const size_t t = e / pg.plane;
+      const int ch = (int)(t % c4);
+      const size_t i = t / c4;
+      const int y = (int)(q / (uint32_t)pg.pitch) - 1;
+      const int x = (int)(q % (uint32_t)pg.pitch) - 1;
+      float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (x >= 0 && x < w && y >= 0 && y < h) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = ch * 4 + j;
+          if (c < C) v[j] = feat[(i * C + c) * hw + (size_t)y * w + x];
+        }
+      }
+      packed[e] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    return;
+  }
+  blk -= nb_pack;
+  const int pblocks = (int)((hw + kBlock - 1) / kBlock);
+  const int bc = blk / pblocks;   // b * c4 + ch
+  const uint32_t p = (uint32_t)(blk - bc * pblocks) * kBlock + threadIdx.x;
+  const int ch = bc % c4, b = bc / c4;
   if (p >= hw) return;
+  float G[9];
+  sampling_matrix(cm, B, V, h, w, b * V, 0, G);
   const int y = (int)(p / (uint32_t)w), x = (int)(p % (uint32_t)w);
   uint32_t pos;
   float wx, wy;
-  src_coords(sampling + (size_t)(b * V) * Dc * 9, norm_coord(x, w), norm_coord(y, h), h, w, true, pos,
-             wx, wy);
-  const Rsrc rs = make_rsrc(packed + (size_t)(b * V) * c4 * pg.plane, (uint32_t)c4 * pg.plane * 16u);
-  f4v t[4];
-  load_taps(rs, tap_offset(pos, pg), (int)((uint32_t)ch * pg.plane * 16u), pg.pitch * 16, t);
+  src_coords(G, norm_coord(x, w), norm_coord(y, h), h, w, true, pos, wx, wy);
+  f4v t[4] = {};
+  if (pos != kInvalidTap) {
+    const float* fb = feat + ((size_t)(b * V) * C + (size_t)ch * 4) * hw;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int xx = pos_x(pos) + (q & 1), yy = pos_y(pos) + (q >> 1);
+      if (xx < 0 || xx >= w || yy < 0 || yy >= h) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ch * 4 + j < C) t[q][j] = fb[(size_t)j * hw + (size_t)yy * w + xx];
+    }
+  }
   const f4v r = bilerp(t, wx, wy);
-  refs[((size_t)b * c4 + ch) * hw + p] = make_float4(r.x, r.y, r.z, r.w);
+  refs[(size_t)bc * hw + p] = make_float4(r.x, r.y, r.z, r.w);
 }
 
 constexpr int kTileW = 32;                // pixels per tile row: every cost-volume store is a 128-B row
@@ -599,7 +626,7 @@ void launch_staged(int pg, dim3 grid, hipStream_t s, const float4* packed, const
 }
 
 template <int V, int ES>
-void launch_gather(const Geometry& g, const float* feat, const float* smp, float* ws, void* cv,
+void launch_gather(const Geometry& g, const float* feat, const Cams& cm, float* smp, float* ws, void* cv,
                    hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const int c4 = (g.C + 3) / 4;
   const PadGeom pgeo = pad_geom(g.h, g.w);
@@ -607,11 +634,12 @@ void launch_gather(const Geometry& g, const float* feat, const float* smp, float
   float4* refs = packed + (size_t)g.B * V * c4 * pgeo.plane;
   const size_t n_pack = (size_t)g.B * V * c4 * pgeo.plane;
   const size_t pblocks = (n_pack + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(pack_pad_kernel, dim3((unsigned)(pblocks < 8192 ? pblocks : 8192)), dim3(kBlock), 0,
-                     s, feat, packed, g.B * V, g.C, g.h, g.w);
+  const int nb_smp = (g.B * V * g.Dc + kBlock - 1) / kBlock;
+  const int nb_pack = (int)(pblocks < 8192 ? pblocks : 8192);
   const uint32_t hw = (uint32_t)g.h * (uint32_t)g.w;
-  hipLaunchKernelGGL(ref_resample_kernel, dim3((hw + kBlock - 1) / kBlock, (unsigned)(g.B * c4)),
-                     dim3(kBlock), 0, s, packed, smp, refs, g.B, V, g.C, g.h, g.w, g.Dc);
+  const int nb_ref = (int)((hw + kBlock - 1) / kBlock) * g.B * c4;
+  hipLaunchKernelGGL(prologue_kernel, dim3((unsigned)(nb_smp + nb_pack + nb_ref)), dim3(kBlock), 0, s, feat, cm,
+                     smp, packed, refs, g.B, V, g.C, g.h, g.w, g.Dc, nb_smp, nb_pack);
   constexpr int TW = kTileW, TH = kTileH;
   const int tiles_x = (g.w + TW - 1) / TW, tiles_y = (g.h + TH - 1) / TH;
   // planes per workgroup: the register maximum, halved until the grid has >= 4 workgroups per CU
@@ -645,47 +673,49 @@ size_t packed_bytes(int B, int V, int C, int h, int w) {
   return ((size_t)B * V * c4 * pad_geom(h, w).plane + (size_t)B * c4 * h * w) * sizeof(float4);
 }
 
-void launch_cost_volume_fwd_bf16(const Geometry& g, const float* feat, const float* sampling,
-                                 float* packed, void* cv, hipStream_t s, hipEvent_t ev0,
-                                 hipEvent_t ev1) {
+void launch_cost_volume_fwd_bf16(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
+                                 float* packed, void* cv, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   switch (g.V) {
-    case 2: launch_gather<2, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 3: launch_gather<3, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 4: launch_gather<4, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 5: launch_gather<5, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 6: launch_gather<6, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 7: launch_gather<7, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 8: launch_gather<8, 2>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 2: launch_gather<2, 2>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 3: launch_gather<3, 2>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 4: launch_gather<4, 2>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 5: launch_gather<5, 2>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 6: launch_gather<6, 2>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 7: launch_gather<7, 2>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 8: launch_gather<8, 2>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
     default: break;   // rejected by the C ABI (2 <= V <= 8 only)
   }
 }
 
-void launch_cost_volume_fwd_c4(const Geometry& g, const float* feat, const float* sampling,
+void launch_cost_volume_fwd_c4(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
                                float* packed, float* cv, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   switch (g.V) {
-    case 2: launch_gather<2, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 3: launch_gather<3, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 4: launch_gather<4, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 5: launch_gather<5, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 6: launch_gather<6, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 7: launch_gather<7, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 8: launch_gather<8, kQuad>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
+    case 2: launch_gather<2, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 3: launch_gather<3, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 4: launch_gather<4, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 5: launch_gather<5, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 6: launch_gather<6, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 7: launch_gather<7, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 8: launch_gather<8, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
     default: break;   // rejected by the C ABI (2 <= V <= 8 only)
   }
 }
 
-void launch_cost_volume_fwd(const Geometry& g, const float* feat, const float* sampling,
-                            float* packed, float* cv, hipStream_t s, hipEvent_t ev0,
-                            hipEvent_t ev1) {
+void launch_cost_volume_fwd(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
+                            float* packed, float* cv, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   switch (g.V) {
-    case 2: launch_gather<2, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 3: launch_gather<3, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 4: launch_gather<4, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 5: launch_gather<5, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 6: launch_gather<6, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 7: launch_gather<7, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    case 8: launch_gather<8, 4>(g, feat, sampling, packed, cv, s, ev0, ev1); break;
-    default: launch_direct<MVS_MAX_VIEWS, false>(g, feat, sampling, cv, s, ev0, ev1); break;
+    case 2: launch_gather<2, 4>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 3: launch_gather<3, 4>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 4: launch_gather<4, 4>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 5: launch_gather<5, 4>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 6: launch_gather<6, 4>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 7: launch_gather<7, 4>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 8: launch_gather<8, 4>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    default:   // generic kernel (9..16 views): sampling matrices first, then the direct gathers
+      launch_plane_sampling(cm.K, cm.R, cm.T, cm.d_min, cm.d_int, g.B, g.V, g.h, g.w, cm.d_begin, g.Dc, cm.d_scale,
+                            sampling, s);
+      launch_direct<MVS_MAX_VIEWS, false>(g, feat, sampling, cv, s, ev0, ev1);
+      break;
   }
 }
 

@@ -14,19 +14,21 @@ void launch_plane_sampling(const float* K, const float* R, const float* T, const
                            const float* d_int, int B, int V, int h, int w, int d_begin,
                            int d_count, float d_scale, float* sampling, hipStream_t s);
 
-// cost_volume_fwd.hip: fused warp + variance.  `packed` is the workspace area after the sampling
-// matrices (packed_bytes()).  ev0/ev1 (optional) are recorded on `s` right before and after the
-// main fused kernel (its live timing, bench.py).
+// cost_volume_fwd.hip: fused warp + variance.  `sampling` is the workspace's matrix area (written
+// by the launch: its prologue kernel forms the sampling matrices, packs the features and resamples
+// the reference views in one kernel), `packed` the area after it (packed_bytes()).  ev0/ev1
+// (optional) are recorded on `s` right before and after the main fused kernel (its live timing,
+// bench.py).
 size_t packed_bytes(int B, int V, int C, int h, int w);
-void launch_cost_volume_fwd(const Geometry& g, const float* feat, const float* sampling,
+void launch_cost_volume_fwd(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
                             float* packed, float* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
                             hipEvent_t ev1 = nullptr);
 // same, channel-quad layout cv[B][C/4][Dc][h][w][4] fp32, 2 <= V <= 8
-void launch_cost_volume_fwd_c4(const Geometry& g, const float* feat, const float* sampling,
+void launch_cost_volume_fwd_c4(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
                                float* packed, float* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
                                hipEvent_t ev1 = nullptr);
 // same, bf16 cost volume (uint16 storage, RNE), 2 <= V <= 8
-void launch_cost_volume_fwd_bf16(const Geometry& g, const float* feat, const float* sampling,
+void launch_cost_volume_fwd_bf16(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
                                  float* packed, void* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
                                  hipEvent_t ev1 = nullptr);
 

@@ -1,106 +1,19 @@
-// plane_sampling.hip -- per-(image, plane) sampling matrices in fp64.
-//
-// Reference: scripts/homography.py:24-26 (depth planes, d_batch tiling), :29-36 (reference index of
-// image i is V*floor(i/V)), :40-75 (H = K_i R_i (I - (C_i - C_r) n_r^T / d) R_r^T K_r^-1 with
-// C = -R^T T and n_r the third column of R_ref); kornia 0.6.3 normalize_homography + inverse.
-// One thread per (image, plane).  The result G maps kornia-normalised reference coordinates to
-// normalised source coordinates; it is stored fp32 (9 floats) and read as workgroup-uniform
-// scalars by the sampling kernels.
+// plane_sampling.hip -- per-(image, plane) sampling matrices (sampling_matrix.h), one thread per
+// (image, plane).  The fused cost-volume launches compute the same matrices inside their prologue
+// kernel (cost_volume_fwd.hip); this launcher serves mvs_plane_sampling and the generic (V > 8)
+// path.
 #include "launchers.h"
+#include "sampling_matrix.h"
 
 namespace mvs {
 namespace {
 
-struct Mat3 {
-  double a[9];
-};
-
-__device__ inline Mat3 mat_mul(const Mat3& x, const Mat3& y) {
-  Mat3 r;
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      r.a[3 * i + j] = x.a[3 * i] * y.a[j] + x.a[3 * i + 1] * y.a[3 + j] + x.a[3 * i + 2] * y.a[6 + j];
-  return r;
-}
-
-// Inverse by adjugate; a singular matrix yields non-finite entries (every tap then samples
-// outside the image and contributes zero; the reference's torch.inverse would raise instead).
-__device__ inline Mat3 mat_inv(const Mat3& m) {
-  const double* a = m.a;
-  double c00 = a[4] * a[8] - a[5] * a[7];
-  double c01 = a[5] * a[6] - a[3] * a[8];
-  double c02 = a[3] * a[7] - a[4] * a[6];
-  double det = a[0] * c00 + a[1] * c01 + a[2] * c02;
-  double id = 1.0 / det;
-  Mat3 r;
-  r.a[0] = c00 * id;
-  r.a[1] = (a[2] * a[7] - a[1] * a[8]) * id;
-  r.a[2] = (a[1] * a[5] - a[2] * a[4]) * id;
-  r.a[3] = c01 * id;
-  r.a[4] = (a[0] * a[8] - a[2] * a[6]) * id;
-  r.a[5] = (a[2] * a[3] - a[0] * a[5]) * id;
-  r.a[6] = c02 * id;
-  r.a[7] = (a[1] * a[6] - a[0] * a[7]) * id;
-  r.a[8] = (a[0] * a[4] - a[1] * a[3]) * id;
-  return r;
-}
-
-__device__ inline Mat3 load_mat(const float* p) {
-  Mat3 r;
-#pragma unroll
-  for (int e = 0; e < 9; ++e) r.a[e] = (double)p[e];
-  return r;
-}
-
-// homography.py:40-75 (H) + kornia normalize_homography / inverse, one thread per (i, kk).
-__global__ void plane_sampling_kernel(const float* __restrict__ K, const float* __restrict__ R,
-                                      const float* __restrict__ T, const float* __restrict__ d_min,
-                                      const float* __restrict__ d_int, int B, int V, int h, int w,
-                                      int d_begin, int d_count, float d_scale,
+__global__ void plane_sampling_kernel(Cams cm, int B, int V, int h, int w, int d_count,
                                       float* __restrict__ out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int N = B * V;
-  if (t >= N * d_count) return;
+  if (t >= B * V * d_count) return;
   const int i = t / d_count;
-  const int kk = t - i * d_count;
-  const int r = (i / V) * V;   // reference view of image i (homography.py:29-34)
-  const int bq = i % B;        // d_batch = tile(d_batch_0, (V,1,1,1)): row i is sample i mod B
-  // depth in fp32 exactly as homography.py:25 forms it: d_min + (D_SCALE * d_int) * k
-  const float d32 = d_min[bq] + (d_scale * d_int[bq]) * (float)(d_begin + kk);
-  const double d = (double)d32;
-
-  const Mat3 Ki = load_mat(K + 9 * i), Ri = load_mat(R + 9 * i);
-  const Mat3 Kr = load_mat(K + 9 * r), Rr = load_mat(R + 9 * r);
-  double Ci[3], Cr[3], nr[3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {  // C = -R^T T
-    Ci[a] = -(Ri.a[a] * (double)T[3 * i] + Ri.a[3 + a] * (double)T[3 * i + 1] +
-              Ri.a[6 + a] * (double)T[3 * i + 2]);
-    Cr[a] = -(Rr.a[a] * (double)T[3 * r] + Rr.a[3 + a] * (double)T[3 * r + 1] +
-              Rr.a[6 + a] * (double)T[3 * r + 2]);
-    nr[a] = Rr.a[3 * a + 2];  // third column of R_ref (homography.py:49)
-  }
-  Mat3 P;
-#pragma unroll
-  for (int a = 0; a < 3; ++a)
-#pragma unroll
-    for (int c = 0; c < 3; ++c) P.a[3 * a + c] = (a == c ? 1.0 : 0.0) - (Ci[a] - Cr[a]) * nr[c] / d;
-  Mat3 RrT;
-#pragma unroll
-  for (int a = 0; a < 3; ++a)
-#pragma unroll
-    for (int c = 0; c < 3; ++c) RrT.a[3 * a + c] = Rr.a[3 * c + a];
-  const Mat3 H = mat_mul(mat_mul(Ki, Ri), mat_mul(P, mat_mul(RrT, mat_inv(Kr))));
-  // kornia: dst_norm_T_src_norm = Nrm @ H @ Nrm^-1, then src_norm_T_dst_norm = inverse(.)
-  const double sx = 2.0 / (double)(w - 1), sy = 2.0 / (double)(h - 1);
-  Mat3 Nm = {{sx, 0.0, -1.0, 0.0, sy, -1.0, 0.0, 0.0, 1.0}};
-  Mat3 Ni = {{1.0 / sx, 0.0, 1.0 / sx, 0.0, 1.0 / sy, 1.0 / sy, 0.0, 0.0, 1.0}};
-  const Mat3 G = mat_inv(mat_mul(Nm, mat_mul(H, Ni)));
-  float* o = out + 9 * (size_t)t;
-#pragma unroll
-  for (int e = 0; e < 9; ++e) o[e] = (float)G.a[e];
+  sampling_matrix(cm, B, V, h, w, i, t - i * d_count, out + 9 * (size_t)t);
 }
 
 }  // namespace
@@ -109,8 +22,9 @@ void launch_plane_sampling(const float* K, const float* R, const float* T, const
                            const float* d_int, int B, int V, int h, int w, int d_begin,
                            int d_count, float d_scale, float* sampling, hipStream_t s) {
   const int n = B * V * d_count;
-  hipLaunchKernelGGL(plane_sampling_kernel, dim3((n + 127) / 128), dim3(128), 0, s, K, R, T, d_min,
-                     d_int, B, V, h, w, d_begin, d_count, d_scale, sampling);
+  const Cams cm{K, R, T, d_min, d_int, d_begin, d_scale};
+  hipLaunchKernelGGL(plane_sampling_kernel, dim3((n + 127) / 128), dim3(128), 0, s, cm, B, V, h, w, d_count,
+                     sampling);
 }
 
 }  // namespace mvs
