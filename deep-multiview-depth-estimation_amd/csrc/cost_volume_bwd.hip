@@ -368,12 +368,30 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
         if (inb) {
           lds_t* a0 = lds + (base[s] + (cy - ub[s].y0) * bw[s] + (cx - ub[s].x0)) * kSlotWords;
           lds_t* a1 = a0 + bw[s] * kSlotWords;
+          if constexpr (DET) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            atomicAdd(a0 + j, Acc<DET>::conv(wt[0] * cs[j], sc));
-            atomicAdd(a0 + kSlotWords + j, Acc<DET>::conv(wt[1] * cs[j], sc));
-            atomicAdd(a1 + j, Acc<DET>::conv(wt[2] * cs[j], sc));
-            atomicAdd(a1 + kSlotWords + j, Acc<DET>::conv(wt[3] * cs[j], sc));
+            for (int j = 0; j < 4; ++j) {
+              atomicAdd(a0 + j, Acc<DET>::conv(wt[0] * cs[j], sc));
+              atomicAdd(a0 + kSlotWords + j, Acc<DET>::conv(wt[1] * cs[j], sc));
+              atomicAdd(a1 + j, Acc<DET>::conv(wt[2] * cs[j], sc));
+              atomicAdd(a1 + kSlotWords + j, Acc<DET>::conv(wt[3] * cs[j], sc));
+            }
+          } else {
+            // products in fp64 from the widened factors: 8 conversions + 16 multiplies (fp64 runs at
+            // the unpacked fp32 rate) instead of 16 fp32 multiplies + 16 conversions, and exact
+            double w64[4], c64[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              w64[q] = (double)wt[q];
+              c64[q] = (double)cs[q];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              atomicAdd(a0 + j, w64[0] * c64[j]);
+              atomicAdd(a0 + kSlotWords + j, w64[1] * c64[j]);
+              atomicAdd(a1 + j, w64[2] * c64[j]);
+              atomicAdd(a1 + kSlotWords + j, w64[3] * c64[j]);
+            }
           }
         }
         // no LDS image for this pass, or a rounding outlier: in-image taps to the accumulators
