@@ -63,13 +63,23 @@ def _run_stack(seq, x):
             if bn.training:
                 p = _bn_train(bn, *channel_stats(y, False), y.numel() // y.shape[1])
             else:
-                p = (bn.weight / torch.sqrt(bn.running_var + bn.eps), bn.bias, bn.running_mean)
+                p = _bn_eval(bn)
             x = bn_relu_(y, False, *p)
             i += 3
         else:
             x = layer(x)
             i += 1
     return x
+
+
+def _bn_eval(bn):
+    """Eval BatchNorm as (scale, shift, mean): y = (x - mean) * scale + shift, scale = weight /
+    sqrt(running_var + eps) (torch's batch_norm_inference order); the scale is cached per parameter
+    state (ops.derived)."""
+    from .ops import derived
+    eps = bn.eps
+    scale = derived(("bn_scale", eps), (bn.weight, bn.running_var), lambda wt, var: wt / torch.sqrt(var + eps))
+    return scale, bn.bias, bn.running_mean
 
 
 def _run_tail(layers, x):
@@ -219,8 +229,7 @@ class CostVolumeReg(nn.Module):
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad = list(n), list(self.pad)
 
-        def bn_eval(bn):
-            return bn.weight / torch.sqrt(bn.running_var + bn.eps), bn.bias, bn.running_mean
+        bn_eval = _bn_eval
 
         # conv_0_0 (VALU-bound) runs on a side stream, concurrently with the region chain (MFMA /
         # memory-bound) that does not need it until deconv_1_0

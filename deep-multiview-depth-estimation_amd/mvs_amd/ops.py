@@ -13,6 +13,7 @@ Camera tensors (K, R, T, d_min, d_int) are moved to the feature device here, as 
 does with ``.to(DEVICE)`` (homography.py:25,43-58).
 """
 import ctypes
+import weakref
 from typing import Optional
 
 import torch
@@ -371,7 +372,7 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Te
     x = x.to(_F32).contiguous()
     cout = weight.shape[0]
     # the kernel reads weight[c_in][3][3][3][c_out] (pairs of output channels per 8-byte load)
-    w = weight.to(device=x.device, dtype=_F32).permute(1, 2, 3, 4, 0).contiguous()
+    w = derived("k3", (weight,), lambda wt: wt.to(device=x.device, dtype=_F32).permute(1, 2, 3, 4, 0).contiguous())
     bn = [t if t is None else t.to(device=x.device, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
     if any(t is None for t in bn) and not all(t is None for t in bn):
         raise ValueError("bn_scale, bn_shift and bn_mean go together")
@@ -442,12 +443,34 @@ def _(x, origin, weight, out_dims, pad, bn_scale, bn_shift, bn_mean, residual, x
 CONV_S1, CONV_S2, CONV_T2 = _lib.MVS_CONV_S1, _lib.MVS_CONV_S2, _lib.MVS_CONV_T2
 
 
+_DERIVED = {}
+
+
+def derived(tag, tensors, fn):
+    """fn(*tensors), cached for inference: a kernel-layout weight or an eval-BN scale is formed once
+    per parameter state instead of by a few small device ops on every forward.  The key is each
+    tensor's identity, storage and in-place version counter (optimizer steps, load_state_dict and
+    running-statistic updates all bump it); a weak reference guards against a freed tensor's id
+    being reused.  Never cached while autograd records (the result must carry the graph)."""
+    if torch.is_grad_enabled() and any(t.requires_grad for t in tensors):
+        return fn(*tensors)
+    key = (tag,) + tuple((id(t), t.data_ptr(), t._version) for t in tensors)
+    hit = _DERIVED.get(key)
+    if hit is not None and all(r() is t for r, t in zip(hit[0], tensors)):
+        return hit[1]
+    out = fn(*tensors)
+    if len(_DERIVED) < 4096 or key in _DERIVED:   # bounded; a full cache stops caching (entries in
+        _DERIVED[key] = ([weakref.ref(t) for t in tensors], out)   # use on other streams stay alive)
+    return out
+
+
 def region_weight(module):
     """weight[27][c_out][c_in] of an nn.Conv3d / nn.ConvTranspose3d (mvs_conv3d_region_fwd layout)."""
-    w = module.weight
     if isinstance(module, torch.nn.ConvTranspose3d):
-        return w.permute(2, 3, 4, 1, 0).reshape(27, w.shape[1], w.shape[0]).contiguous()
-    return w.permute(2, 3, 4, 0, 1).reshape(27, w.shape[0], w.shape[1]).contiguous()
+        return derived("region_t", (module.weight,),
+                       lambda w: w.permute(2, 3, 4, 1, 0).reshape(27, w.shape[1], w.shape[0]).contiguous())
+    return derived("region", (module.weight,),
+                   lambda w: w.permute(2, 3, 4, 0, 1).reshape(27, w.shape[0], w.shape[1]).contiguous())
 
 
 def _ints3(v):

@@ -88,3 +88,29 @@ def test_shard_helpers():
     with pytest.raises(ValueError):
         plane_shard(250, 8, 0)
     assert owned_samples(5, 2, 0) == [0, 2, 4] and owned_samples(1, 8, 3) == []
+
+
+def test_derived_parameter_cache_follows_parameter_state():
+    """ops.derived: a cached kernel-layout weight / eval-BN scale is reformed after any in-place
+    update of its inputs (optimizer step, load_state_dict, running statistics) and never cached
+    while autograd records."""
+    import torch
+    from mvs_amd.ops import derived
+    w = torch.randn(4, 3)
+    calls = []
+
+    def f(t):
+        calls.append(1)
+        return t * 2.0
+
+    with torch.no_grad():
+        a = derived("t", (w,), f)
+        b = derived("t", (w,), f)
+        assert b is a and len(calls) == 1
+        w.add_(1.0)   # in-place: version bump -> recomputed
+        c = derived("t", (w,), f)
+        assert len(calls) == 2 and torch.equal(c, w * 2.0)
+    p = torch.nn.Parameter(torch.randn(3))
+    derived("t", (p,), f)
+    derived("t", (p,), f)
+    assert len(calls) == 4   # requires_grad under grad mode: never cached
