@@ -493,8 +493,8 @@ def main():
                      "ncdhw_store": {"kernel_ms": nc_ms, "op_ms": nc_op_ms,
                                      "frac": alg / (nc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}},
         "hot_path": {"cost_volumes_per_s": B / (op_ms * 1e-3), "op_ms": op_ms,
-                     "op": "mvs_cost_volume_fwd%s: plane_sampling + pack_pad + ref_resample + "
-                           "cost_volume_staged kernels" % ("_c4" if quads else ""),
+                     "op": "mvs_cost_volume_fwd%s: prologue kernel (sampling matrices + channel-quad "
+                           "packing + reference resampling) + cost_volume_staged kernel" % ("_c4" if quads else ""),
                      "op_GBps": alg / (op_ms * 1e-3) / 1e9},
     }
     if "full" in result:
