@@ -328,6 +328,40 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
         g[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, o + (uint32_t)j * cst_bytes, 0, 0));
       return g;
     };
+    // Default mode: run-length accumulation in registers.  A sample's tap corner moves slowly with
+    // the plane (it repeats from one plane to the next for ~70 % of the samples at cfg 2, for every
+    // lane of the wave ~50 % of the time), so each lane sums its 16 tap x channel contributions in
+    // fp32 registers while its corner stays put and adds them to the LDS image (16 ds_add_f64) only
+    // when the corner moves and at the end of the pass; a wave with no moved corner skips the adds
+    // with one scalar branch.  Deterministic mode adds every contribution (fixed point) directly, as
+    // do more than 3 views (the accumulators would cost the third wave per SIMD).
+    constexpr bool RL = !DET && V <= 3;
+    uint32_t apos[NS];
+    f4v acc[NS][4];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      apos[s] = kInvalidTap;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[s][q] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+    // the lanes in `flush` add acc[s] at corner apos[s] to the LDS image and clear it
+    auto flush_acc = [&](int s, bool flush) {
+      if (__builtin_amdgcn_ballot_w64(flush) == 0) return;   // uniform
+      if (flush) {
+        const int cx = pos_x(apos[s]), cy = pos_y(apos[s]);
+        lds_t* a0 = lds + (base[s] + (cy - ub[s].y0) * bw[s] + (cx - ub[s].x0)) * kSlotWords;
+        lds_t* a1 = a0 + bw[s] * kSlotWords;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          atomicAdd(a0 + j, (lds_t)acc[s][0][j]);
+          atomicAdd(a0 + kSlotWords + j, (lds_t)acc[s][1][j]);
+          atomicAdd(a1 + j, (lds_t)acc[s][2][j]);
+          atomicAdd(a1 + kSlotWords + j, (lds_t)acc[s][3][j]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[s][q] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+    };
     // grad_cv one plane ahead, issued after the plane's tap gathers (vmcnt retires loads in issue
     // order: waiting for the gathers then leaves the next plane's grad_cv loads in flight)
     f4v g_next = load_g(kp);
@@ -364,11 +398,11 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
         const int cx = pos_x(pos[s]), cy = pos_y(pos[s]);
         const bool valid = pos[s] != kInvalidTap;
         const bool inb = use_lds && valid && cx >= ub[s].x0 && cx < ub[s].x1 && cy >= ub[s].y0 && cy < ub[s].y1;
-        // all 4 taps inside the pass's box: 16 LDS adds at immediate offsets of two addresses
-        if (inb) {
-          lds_t* a0 = lds + (base[s] + (cy - ub[s].y0) * bw[s] + (cx - ub[s].x0)) * kSlotWords;
-          lds_t* a1 = a0 + bw[s] * kSlotWords;
-          if constexpr (DET) {
+        if constexpr (!RL) {
+          // all 4 taps inside the pass's box: 16 LDS adds at immediate offsets of two addresses
+          if (inb) {
+            lds_t* a0 = lds + (base[s] + (cy - ub[s].y0) * bw[s] + (cx - ub[s].x0)) * kSlotWords;
+            lds_t* a1 = a0 + bw[s] * kSlotWords;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               atomicAdd(a0 + j, Acc<DET>::conv(wt[0] * cs[j], sc));
@@ -376,22 +410,14 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
               atomicAdd(a1 + j, Acc<DET>::conv(wt[2] * cs[j], sc));
               atomicAdd(a1 + kSlotWords + j, Acc<DET>::conv(wt[3] * cs[j], sc));
             }
-          } else {
-            // products in fp64 from the widened factors: 8 conversions + 16 multiplies (fp64 runs at
-            // the unpacked fp32 rate) instead of 16 fp32 multiplies + 16 conversions, and exact
-            double w64[4], c64[4];
+          }
+        } else {
+          // a corner inside the box that differs from the accumulated one flushes the registers
+          flush_acc(s, inb && apos[s] != kInvalidTap && apos[s] != pos[s]);
+          if (inb) {
+            apos[s] = pos[s];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              w64[q] = (double)wt[q];
-              c64[q] = (double)cs[q];
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              atomicAdd(a0 + j, w64[0] * c64[j]);
-              atomicAdd(a0 + kSlotWords + j, w64[1] * c64[j]);
-              atomicAdd(a1 + j, w64[2] * c64[j]);
-              atomicAdd(a1 + kSlotWords + j, w64[3] * c64[j]);
-            }
+            for (int q = 0; q < 4; ++q) acc[s][q] = __builtin_elementwise_fma(f4v{wt[q], wt[q], wt[q], wt[q]}, cs, acc[s][q]);
           }
         }
         // no LDS image for this pass, or a rounding outlier: in-image taps to the accumulators
@@ -406,6 +432,14 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
               if (j < nch) gadd_out(b * V + 1 + s, j, yy, xx, Acc<DET>::conv(wt[q] * cs[j], sc));
           }
         }
+      }
+    }
+
+    if constexpr (RL) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        if (s < s0 || s >= s1) continue;   // uniform
+        flush_acc(s, apos[s] != kInvalidTap);
       }
     }
 
