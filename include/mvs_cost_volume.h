@@ -85,8 +85,9 @@ int mvs_cost_volume_fwd(const float* feat, const float* K, const float* R, const
 /*
  * mvs_cost_volume_fwd with live timing of its main fused kernel: main_begin_event and
  * main_end_event (hipEvent_t, either may be NULL) are recorded on `stream` immediately before
- * and after that kernel's launch (the sampling-matrix, packing and reference-resampling kernels
- * run before main_begin_event).  Used by bench.py for the roofline's per-launch duration.
+ * and after that kernel's launch (the prologue kernel -- sampling matrices, packing and
+ * reference resampling in one launch -- runs before main_begin_event).  Used by bench.py for the
+ * roofline's per-launch duration.
  */
 int mvs_cost_volume_fwd_timed(const float* feat, const float* K, const float* R, const float* T,
                               const float* d_min, const float* d_int,
