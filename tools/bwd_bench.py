@@ -30,24 +30,32 @@ def main():
         def fwd():
             return warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feat, B, V, d_num=D)[0]
 
-        cv = fwd()
-        cv.backward(gcv)
-        torch.cuda.synchronize()
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-        n = 5
-        tf = tb = 0.0
-        for _ in range(n):
-            feat.grad = None
-            e[0].record()
+        def timed(n=5):
             cv = fwd()
-            e[1].record()
             cv.backward(gcv)
-            e[2].record()
             torch.cuda.synchronize()
-            tf += e[0].elapsed_time(e[1])
-            tb += e[1].elapsed_time(e[2])
-        print(json.dumps({"cfg": name, "B": B, "V": V, "D": D, "fwd_ms": round(tf / n, 3),
-                          "bwd_ms": round(tb / n, 3)}), flush=True)
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            tf = tb = 0.0
+            for _ in range(n):
+                feat.grad = None
+                e[0].record()
+                cv = fwd()
+                e[1].record()
+                cv.backward(gcv)
+                e[2].record()
+                torch.cuda.synchronize()
+                tf += e[0].elapsed_time(e[1])
+                tb += e[1].elapsed_time(e[2])
+            return tf / n, tb / n
+
+        tf, tb = timed()
+        torch.use_deterministic_algorithms(True)   # MVS_BWD_DETERMINISTIC (fixed-point backward)
+        try:
+            _, td = timed()
+        finally:
+            torch.use_deterministic_algorithms(False)
+        print(json.dumps({"cfg": name, "B": B, "V": V, "D": D, "fwd_ms": round(tf, 3),
+                          "bwd_ms": round(tb, 3), "det_bwd_ms": round(td, 3)}), flush=True)
 
 
 if __name__ == "__main__":
