@@ -333,11 +333,10 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
     // lane of the wave ~50 % of the time), so each lane sums its 16 tap x channel contributions in
     // fp32 registers while its corner stays put and adds them to the LDS image (16 ds_add_f64) only
     // when the corner moves and at the end of the pass; a wave with no moved corner skips the adds
-    // with one scalar branch.  In deterministic mode the register sums are converted to fixed point
-    // when they are added: each lane sums its own contributions in plane order, so the partial sums,
-    // and with them the integer totals, are the same on every run.  More than 3 views add every
-    // contribution directly (the accumulators would cost the third wave per SIMD).
-    constexpr bool RL = V <= 3;
+    // with one scalar branch.  More than 3 views add every contribution directly (the accumulators
+    // would cost the third wave per SIMD), as does the deterministic mode (fixed point per
+    // contribution: register sums converted at the flush measured 3.16 against 3.05 ms at cfg 2).
+    constexpr bool RL = !DET && V <= 3;
     uint32_t apos[NS];
     f4v acc[NS][4];
 #pragma unroll
@@ -355,10 +354,10 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
         lds_t* a1 = a0 + bw[s] * kSlotWords;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          atomicAdd(a0 + j, Acc<DET>::conv(acc[s][0][j], sc));
-          atomicAdd(a0 + kSlotWords + j, Acc<DET>::conv(acc[s][1][j], sc));
-          atomicAdd(a1 + j, Acc<DET>::conv(acc[s][2][j], sc));
-          atomicAdd(a1 + kSlotWords + j, Acc<DET>::conv(acc[s][3][j], sc));
+          atomicAdd(a0 + j, (lds_t)acc[s][0][j]);
+          atomicAdd(a0 + kSlotWords + j, (lds_t)acc[s][1][j]);
+          atomicAdd(a1 + j, (lds_t)acc[s][2][j]);
+          atomicAdd(a1 + kSlotWords + j, (lds_t)acc[s][3][j]);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[s][q] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
