@@ -236,6 +236,19 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
   return mvs::hip_status();
 }
 
+int mvs_conv2d_fwd(const float* x, const float* weight, float* y, int n, int c_in, int c_out, int h, int w,
+                   int k, int stride, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                   void* stream) {
+  if (!x || !weight || !y || n <= 0 || n > 65535 || h <= 0 || w <= 0 || stride <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
+    return MVS_ERR_INVALID_ARGUMENT;
+  // staging offsets inside one image are 32-bit
+  if ((uint64_t)c_in * (uint64_t)h * (uint64_t)w >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
+  const int st = mvs::launch_conv2d_narrow(x, weight, y, n, c_in, c_out, h, w, k, stride, bn_scale, bn_shift,
+                                           bn_mean, (hipStream_t)stream);
+  return st != MVS_OK ? st : mvs::hip_status();
+}
+
 int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, int batch, int c_in,
                       int c_out, int d, int h, int w, const float* bn_scale, const float* bn_shift,
                       const float* bn_mean, void* stream) {

@@ -57,6 +57,13 @@ void launch_conv3d_k3_narrow(const float* in, bool in_c4, const float* weight, f
                              int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
                              const float* bn_mean, hipStream_t s);
 
+// conv2d_narrow.hip: bias-free Conv2d of the encoder / refinement (padding k/2), NCHW fp32, weights
+// wt[c_in][k][k][c_out], optional eval BN + ReLU epilogue; MVS_ERR_INVALID_ARGUMENT for a shape
+// without an instantiation
+int launch_conv2d_narrow(const float* in, const float* wt, float* out, int N, int Cin, int Cout, int H, int W,
+                         int K, int stride, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                         hipStream_t s);
+
 // deconv3d_region.hip: stride-2 kernel-3 ConvTranspose3d (Cout 8) from a region tensor to the full
 // volume, optional fused BN(eval)+ReLU and residual add
 // (channels_last: x and x2 are [B][rd][rh][rw][Cin]; x2 (nullable) is added to x)

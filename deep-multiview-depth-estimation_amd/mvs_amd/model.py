@@ -44,30 +44,37 @@ def _conv_bn_relu_stack(spec, device):
 
 def _run_stack(seq, x):
     """A conv -> BatchNorm -> ReLU stack (encoder / refinement).  In fp32 no-grad inference on the
-    GPU every BatchNorm + ReLU pair is one in-place HIP pass (csrc/channel_ops.hip): eval BN from
-    the running statistics; train-mode BN (test.py:61) from one-pass float64 batch sums, with the
+    GPU the convolutions run on the direct HIP kernel (mvs::conv2d, csrc/conv2d_narrow.hip) with eval
+    BN + ReLU fused into its epilogue; train-mode BN (test.py:61) takes one-pass float64 batch sums
+    of the convolution's output and one in-place BN + ReLU pass (csrc/channel_ops.hip), with the
     running statistics updated as torch does.  Elsewhere the modules themselves."""
     if not _hip_inference(x):
         return seq(x)
-    from .ops import bn_relu_, channel_stats
+    from .ops import bn_relu_, channel_stats, conv2d, conv2d_supported
     layers = list(seq)
+
+    def conv(layer, x, bn=None):   # the HIP direct convolution for the reference's layer shapes
+        if isinstance(layer, nn.Conv2d) and conv2d_supported(layer):
+            return conv2d(x, layer.weight, layer.stride[0], *(bn or ()))
+        y = layer(x)
+        return y if bn is None else bn_relu_(y.contiguous(), False, *bn)
+
     i = 0
     while i < len(layers):
         layer = layers[i]
         if (i + 2 < len(layers) and isinstance(layers[i + 1], nn.BatchNorm2d)
                 and isinstance(layers[i + 2], nn.ReLU)):
-            y = layer(x).contiguous()
             bn = layers[i + 1]
             if bn.running_mean is None or not bn.affine:   # no running statistics: the module
                 return _run_tail(layers[i:], x)
             if bn.training:
-                p = _bn_train(bn, *channel_stats(y, False), y.numel() // y.shape[1])
-            else:
-                p = _bn_eval(bn)
-            x = bn_relu_(y, False, *p)
+                y = conv(layer, x).contiguous()
+                x = bn_relu_(y, False, *_bn_train(bn, *channel_stats(y, False), y.numel() // y.shape[1]))
+            else:   # eval BN + ReLU fused into the convolution's epilogue
+                x = conv(layer, x, _bn_eval(bn))
             i += 3
         else:
-            x = layer(x)
+            x = conv(layer, x)
             i += 1
     return x
 

@@ -390,6 +390,58 @@ def _(x, weight, bn_scale=None, bn_shift=None, bn_mean=None, in_c4=False):
 
 
 # ----------------------------------------------------------------------------------------------
+# mvs::conv2d -- FeatureEncoder / refinement Conv2d (+ eval BatchNorm2d + ReLU), model.py:22-65,134-145
+# ----------------------------------------------------------------------------------------------
+# (c_in, c_out, k, stride) with a kernel instantiation (csrc/conv2d_narrow.hip)
+CONV2D_SHAPES = frozenset({(3, 8, 3, 1), (8, 8, 3, 1), (8, 16, 5, 2), (16, 16, 3, 1), (16, 32, 5, 2),
+                           (32, 32, 3, 1), (4, 32, 3, 1), (32, 1, 3, 1)})
+
+
+def conv2d_supported(conv):
+    """nn.Conv2d the HIP kernel runs: bias-free, padding k/2, no dilation/groups, a listed shape."""
+    k = conv.kernel_size[0]
+    return (conv.bias is None and conv.kernel_size == (k, k) and conv.stride[0] == conv.stride[1]
+            and conv.padding == (k // 2, k // 2) and conv.dilation == (1, 1) and conv.groups == 1
+            and conv.padding_mode == "zeros"
+            and (conv.in_channels, conv.out_channels, k, conv.stride[0]) in CONV2D_SHAPES)
+
+
+@torch.library.custom_op("mvs::conv2d", mutates_args=())
+def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int, bn_scale: Optional[torch.Tensor] = None,
+           bn_shift: Optional[torch.Tensor] = None, bn_mean: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """nn.Conv2d(c_in, c_out, k, stride, padding=k // 2, bias=False) forward, fp32 NCHW, on the HIP
+    kernel (csrc/conv2d_narrow.hip); with bn_* given, max((y - mean) * scale + shift, 0) is fused
+    (eval BatchNorm2d + ReLU).  Shapes: CONV2D_SHAPES.  Inference only (no autograd formula)."""
+    _require_gpu(x, "x")
+    lib = _lib.load()
+    if x.dim() != 4 or weight.dim() != 4 or weight.shape[1] != x.shape[1] or weight.shape[2] != weight.shape[3]:
+        raise ValueError("x [N, C, H, W] and weight [Cout, C, k, k] expected, got %s, %s"
+                         % (tuple(x.shape), tuple(weight.shape)))
+    n, cin, h, wd = x.shape
+    cout, k = weight.shape[0], weight.shape[2]
+    x = x.to(_F32).contiguous()
+    # the kernel reads weight[c_in][k][k][c_out] (pairs of output channels per 8-byte scalar load)
+    w = derived("conv2d", (weight,), lambda wt: wt.to(device=x.device, dtype=_F32).permute(1, 2, 3, 0).contiguous())
+    bn = [t if t is None else t.to(device=x.device, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
+    if any(t is None for t in bn) and not all(t is None for t in bn):
+        raise ValueError("bn_scale, bn_shift and bn_mean go together")
+    bp = [None if t is None else _lib.ptr(t) for t in bn]
+    ho, wo = (h + 2 * (k // 2) - k) // stride + 1, (wd + 2 * (k // 2) - k) // stride + 1
+    y = torch.empty((n, cout, ho, wo), device=x.device, dtype=_F32)
+    st = lib.mvs_conv2d_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), n, cin, cout, h, wd, k, stride, *bp,
+                            _lib.stream_handle(x.device))
+    _lib.check(st, "mvs_conv2d_fwd")
+    return y
+
+
+@conv2d.register_fake
+def _(x, weight, stride, bn_scale=None, bn_shift=None, bn_mean=None):
+    k = weight.shape[2]
+    return x.new_empty((x.shape[0], weight.shape[0], (x.shape[2] + 2 * (k // 2) - k) // stride + 1,
+                        (x.shape[3] + 2 * (k // 2) - k) // stride + 1))
+
+
+# ----------------------------------------------------------------------------------------------
 # mvs::deconv3d_k3s2 -- CostVolumeReg.deconv_1_0 + BN_0 + ReLU + `+ y0` (model.py:121-123)
 # ----------------------------------------------------------------------------------------------
 @torch.library.custom_op("mvs::deconv3d_k3s2", mutates_args=())

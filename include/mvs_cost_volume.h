@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 4
+#define MVS_ABI_VERSION 5
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -216,6 +216,19 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
 int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, int batch, int c_in,
                       int c_out, int d, int h, int w, const float* bn_scale, const float* bn_shift,
                       const float* bn_mean, void* stream);
+
+/* Feature encoder and refinement layers (model.py:22-65 FeatureEncoder, model.py:134-145): nn.Conv2d(
+ * c_in, c_out, k, stride, padding=k/2, bias=False) over x[n][c_in][h][w] fp32 into
+ * y[n][c_out][ho][wo] (ho = (h + 2(k/2) - k)/stride + 1, likewise wo), with the weight TRANSPOSED to
+ * weight[c_in][k][k][c_out] (nn.Conv2d's weight.permute(1, 2, 3, 0)).  Supported (c_in, c_out, k,
+ * stride): the reference's layers (3,8,3,1) (8,8,3,1) (8,16,5,2) (16,16,3,1) (16,32,5,2) (32,32,3,1)
+ * (4,32,3,1) (32,1,3,1); MVS_ERR_INVALID_ARGUMENT otherwise.  Optional epilogue (all three BN pointers,
+ * c_out floats each, or none): y = max((y - bn_mean) * bn_scale + bn_shift, 0), the eval BN + ReLU
+ * that follows these convolutions.  Replaces the MIOpen convolution behind torch.nn.Conv2d.forward
+ * (and the BatchNorm2d + ReLU after it) in inference; same products, fp32 summation order differs. */
+int mvs_conv2d_fwd(const float* x, const float* weight, float* y, int n, int c_in, int c_out, int h, int w,
+                   int k, int stride, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                   void* stream);
 
 /* layout flag of mvs_deconv3d_k3s2_fwd: the region input is channels-last x[batch][rd][rh][rw][c_in] */
 #define MVS_LAYOUT_CHANNELS_LAST 1

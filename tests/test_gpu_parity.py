@@ -476,6 +476,42 @@ def test_narrow_conv3d_matches_torch(shape):
     assert err <= 4 * err_t + 1e-6 * scale, (err, err_t)   # no worse than MIOpen's own fp32 sums
 
 
+@pytest.mark.parametrize("shape", [(3, 8, 3, 1, 2, 37, 70), (8, 8, 3, 1, 1, 64, 96), (8, 16, 5, 2, 2, 33, 67),
+                                   (16, 16, 3, 1, 1, 20, 31), (16, 32, 5, 2, 1, 40, 64),
+                                   (32, 32, 3, 1, 2, 16, 40), (4, 32, 3, 1, 1, 24, 50), (32, 1, 3, 1, 2, 17, 33)])
+@pytest.mark.parametrize("bn", [False, True])
+def test_conv2d_matches_torch(shape, bn):
+    """mvs::conv2d (csrc/conv2d_narrow.hip: the FeatureEncoder / refinement Conv2d layers,
+    model.py:22-65,134-145) for every instantiated (c_in, c_out, k, stride), ragged tiles (sizes not
+    multiples of the 32 x 8 tile, odd sizes under stride 2), with and without the fused eval
+    BatchNorm2d + ReLU: against float64 on the CPU and no worse than the torch fp32 Conv2d (MIOpen)
+    on the same device."""
+    from mvs_amd.ops import conv2d
+    cin, cout, k, st, n, h, w = shape
+    g = torch.Generator().manual_seed(sum(shape) + bn)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, k, k, generator=g) * 0.2
+    ref64 = torch.nn.functional.conv2d(x.double(), wt.double(), stride=st, padding=k // 2)
+    p = None
+    if bn:
+        p = (torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g), torch.randn(cout, generator=g))
+        ref64 = torch.clamp((ref64 - p[2].double()[:, None, None]) * p[0].double()[:, None, None]
+                            + p[1].double()[:, None, None], min=0.0)
+    with torch.no_grad():
+        y = conv2d(x.to(DEV), wt.to(DEV), st, *([t.to(DEV) for t in p] if bn else [])).cpu()
+        yt = torch.nn.functional.conv2d(x.to(DEV), wt.to(DEV), stride=st, padding=k // 2)
+        if bn:
+            sc, sh, mu = (t.to(DEV)[:, None, None] for t in p)
+            yt = torch.clamp((yt - mu) * sc + sh, min=0.0)
+        yt = yt.cpu()
+    assert y.shape == ref64.shape
+    scale = ref64.abs().max().item()
+    err = (y.double() - ref64).abs().max().item()
+    err_t = (yt.double() - ref64).abs().max().item()
+    assert err <= 1e-5 * scale, (err, scale)
+    assert err <= 4 * err_t + 1e-6 * scale, (err, err_t)   # no worse than MIOpen's own fp32 sums
+
+
 def test_live_regulariser_gpu_matches_full_volume():
     """Eval-mode CostVolumeReg on the GPU: live-region path (region convs + HIP conv_0_0/conv_out)
     against the full-volume MIOpen path at a cfg-1-like shape."""
