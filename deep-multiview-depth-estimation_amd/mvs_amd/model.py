@@ -597,6 +597,21 @@ class DepthRefinement(nn.Module):
         return _run_stack(self.model, depth_and_input) + depth_and_input[:, 0].unsqueeze(1)
 
 
+def _select_images(images, idx):
+    """images[idx] for the reference-view indices (homography.py:29-36 returns them as a CPU int64
+    tensor 0, V, 2V, ...): a strided view when they form such a progression, since indexing a
+    device tensor with a CPU index copies it to the device, and that pageable copy synchronises
+    the host with every kernel queued before it (a bubble in each inference step)."""
+    if idx.device.type == "cpu" and idx.dim() == 1 and idx.numel() > 0 and not idx.is_floating_point():
+        n = idx.numel()
+        first = int(idx[0])
+        step = int(idx[1]) - first if n > 1 else 1
+        if step > 0 and first >= 0 and torch.equal(idx, first + step * torch.arange(n, dtype=idx.dtype)) \
+                and first + step * (n - 1) < images.shape[0]:
+            return images[first:first + step * (n - 1) + 1:step]
+    return images[idx.to(images.device)]
+
+
 class MVSNet(nn.Module):
     """model.py:155-207 with the fused MI355X cost volume.  ``cfg`` replaces the reference's
     import-time globals (D_NUM, D_SCALE, FEAT_H/W, PAD/OUTPAD); the default equals them."""
@@ -645,7 +660,6 @@ class MVSNet(nn.Module):
         norm_depth = torch.div(torch.subtract(initial_depth_map, d_trans), d_span)
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
-            ref_img = F.interpolate(nn_input[ref_views.to(nn_input.device)],
-                                    (c.feat_h, c.feat_w), mode="bilinear")
+            ref_img = F.interpolate(_select_images(nn_input, ref_views), (c.feat_h, c.feat_w), mode="bilinear")
         refined = self.depthmap_refine(torch.cat((norm_depth, ref_img), dim=1))
         return refined.mul(d_span).add(d_trans)

@@ -114,3 +114,15 @@ def test_derived_parameter_cache_follows_parameter_state():
     derived("t", (p,), f)
     derived("t", (p,), f)
     assert len(calls) == 4   # requires_grad under grad mode: never cached
+
+
+def test_select_images_matches_indexing():
+    """model._select_images: a strided view for the reference indices 0, V, 2V, ... (no host sync on
+    the GPU), plain indexing otherwise -- the same images either way."""
+    import torch
+    from mvs_amd.model import _select_images
+    imgs = torch.randn(12, 3, 4, 5)
+    for idx in (torch.tensor([0, 3, 6, 9]), torch.tensor([0]), torch.tensor([2, 5]), torch.tensor([1, 0, 4]),
+                torch.tensor([0, 4, 8])):
+        out = _select_images(imgs, idx)
+        assert torch.equal(out, imgs[idx])
