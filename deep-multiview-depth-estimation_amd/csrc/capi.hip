@@ -280,6 +280,8 @@ int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch,
   if (x0d < 0 || x0h < 0 || x0w < 0 || pd < 0 || ph < 0 || pw < 0) return MVS_ERR_INVALID_ARGUMENT;
   if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
     return MVS_ERR_INVALID_ARGUMENT;
+  // the region input is read through 32-bit buffer descriptors over the whole batch
+  if ((uint64_t)batch * c_in * rd * rh * rw * 4u >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
   mvs::launch_deconv3d_k3s2(x, x2, (flags & MVS_LAYOUT_CHANNELS_LAST) != 0, batch, c_in, rd, rh, rw, x0d, x0h,
                             x0w, weight, d, h, w, pd, ph, pw, bn_scale, bn_shift, bn_mean, residual, y,
                             (hipStream_t)stream);

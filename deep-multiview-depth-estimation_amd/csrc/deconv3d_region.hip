@@ -21,6 +21,7 @@
 // input), broadcast LDS reads of the staged 8 x 27 (padded to 28) per channel (channels-last).
 // HBM-bound: the full-size output (+ residual read) dominates.
 #include "launchers.h"
+#include "packed.h"
 
 namespace mvs {
 namespace {
@@ -46,7 +47,7 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
     int x0d, int x0h, int x0w, int D, int H, int W, int qd, int qh, int qw,
     const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
     const float* __restrict__ mean, const float* __restrict__ residual, float* __restrict__ y,
-    int md_n, int mh_n, int mw_n, size_t total) {
+    int md_n, int mh_n, int mw_n, size_t total, size_t total_in_bytes, size_t out_bytes) {
   extern __shared__ float4 wl4[];   // CL: [ci][co][7] float4 = W[ci][co][27] padded
   if constexpr (CL) {
     float* wl = reinterpret_cast<float*>(wl4);
@@ -167,6 +168,42 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
       }
     }
   } else {
+    // channel ci + 1's 8 (or 16, with the addend) input values are loaded before channel ci's
+    // 216 fmas: the loop is otherwise one exposed load latency per input channel.  Branch-free
+    // buffer loads (inputs outside the region: an out-of-range offset reads 0), so the waits for
+    // them are counted instead of draining every load at each branch join.
+    // (descriptors over the whole batch: a workgroup's threads may span two samples, and a
+    // descriptor built from a per-thread base would need a waterfall loop per load)
+    const uint32_t cbytes = (uint32_t)rvol * 4u;   // batch * Cin * rvol * 4 < 2^31 (mvs_deconv3d_k3s2_fwd checks)
+    const uint32_t tbytes = (uint32_t)total_in_bytes;
+    const Rsrc rs = make_rsrc(x, tbytes);
+    const Rsrc rs2 = make_rsrc(x2 ? x2 : x, x2 ? tbytes : 0u);
+    const uint32_t sbase = (uint32_t)b * (uint32_t)Cin * cbytes;
+    uint32_t voff[2][2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          voff[a][c][e] = (okd[a] && okh[c] && okw[e])
+                              ? sbase + (uint32_t)((((size_t)(ld + a) * rh + (lh + c)) * rw + (lw + e)) * 4u)
+                              : 0x80000000u;
+    auto load = [&](int ci, float (&v)[2][2][2]) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const uint32_t o = voff[a][c][e] + (uint32_t)ci * cbytes;
+            float t = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)o, 0, 0));
+            if (xb2) t += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs2, (int)o, 0, 0));
+            v[a][c][e] = t;
+          }
+    };
+    float vn[2][2][2];
+    load(0, vn);
     for (int ci = 0; ci < Cin; ++ci) {
       float v[2][2][2];
 #pragma unroll
@@ -174,16 +211,65 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
 #pragma unroll
         for (int c = 0; c < 2; ++c)
 #pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const size_t o = (size_t)ci * rvol + (((size_t)(ld + a) * rh + (lh + c)) * rw + (lw + e));
-            const bool ok = okd[a] && okh[c] && okw[e];
-            v[a][c][e] = ok ? (xb2 ? xb[o] + xb2[o] : xb[o]) : 0.0f;
-          }
+          for (int e = 0; e < 2; ++e) v[a][c][e] = vn[a][c][e];
+      if (ci + 1 < Cin) load(ci + 1, vn);
       channel(ci, v);
     }
   }
   const size_t plane = (size_t)D * H * W;
   const int od0 = 2 * md, oh0 = 2 * mh, ow0 = 2 * mw;
+  if (out_bytes) {
+    // even W (every block's x pair exists and is 8-byte aligned) and an output under 2^31 bytes:
+    // branch-free 8-byte buffer loads of the residual and stores (rows past D or H: out-of-range
+    // offsets), a group of four channels' residual loads in flight before their stores -- the
+    // branchy form waited for each residual load on its own
+    const Rsrc ry = make_rsrc(y, (uint32_t)out_bytes);
+    const Rsrc rr = make_rsrc(residual ? residual : y, residual ? (uint32_t)out_bytes : 0u);
+    const uint32_t pb = (uint32_t)plane * 4u;
+    uint32_t boff[2][2];
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int od = od0 + sd, oh = oh0 + s2;
+        boff[sd][s2] = (od < D && oh < H)
+                           ? ((uint32_t)b * kCout * pb + (uint32_t)(((size_t)od * H + oh) * W + ow0) * 4u)
+                           : 0x80000000u;
+      }
+#pragma unroll
+    for (int c0 = 0; c0 < kCout; c0 += 4) {
+      f2v r[4][2][2];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+            r[cc][sd][s2] = __builtin_bit_cast(
+                f2v, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(boff[sd][s2] + (uint32_t)(c0 + cc) * pb), 0, 0));
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        const int co = c0 + cc;
+        const float m = bn_scale ? mean[co] : 0.0f, sc = bn_scale ? bn_scale[co] : 0.0f,
+                    sh = bn_scale ? bn_shift[co] : 0.0f;
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            f2v o;
+#pragma unroll
+            for (int sw = 0; sw < 2; ++sw) {
+              float v = acc[sd][s2][sw][co];
+              if (bn_scale) v = fmaxf((v - m) * sc + sh, 0.0f);
+              o[sw] = v + r[cc][sd][s2][sw];
+            }
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, o), ry,
+                                                  (int)(boff[sd][s2] + (uint32_t)co * pb), 0, 0);
+          }
+      }
+    }
+    return;
+  }
   const bool w2 = ow0 + 1 < W;
   float* yb = y + (size_t)b * kCout * plane;
   const float* rb = residual ? residual + (size_t)b * kCout * plane : nullptr;
@@ -222,14 +308,19 @@ void launch_cls(dim3 grid, size_t lds, hipStream_t s, const float* x, const floa
                 int W, int pd, int ph, int pw, const float* bn_scale, const float* bn_shift,
                 const float* bn_mean, const float* residual, float* y, int md_n, int mh_n, int mw_n,
                 size_t total) {
+  // bytes of the whole region input (batch x Cin x rd x rh x rw floats)
+  const size_t in_bytes = total / ((size_t)md_n * mh_n * mw_n) * (size_t)Cin * rd * rh * rw * 4u;
+  // the epilogue's buffer-store path: even W and the whole output under 2^31 bytes (0 = the general path)
+  const size_t ob = total / ((size_t)md_n * mh_n * mw_n) * (size_t)kCout * D * H * W * 4u;
+  const size_t out_bytes = (W % 2 == 0 && ob < (1ull << 31)) ? ob : 0;
   if (cl)
     hipLaunchKernelGGL((deconv3d_k3s2_kernel<CD, CH, CW, true>), grid, dim3(kBlock), lds, s, x, x2, weight, Cin,
                        rd, rh, rw, x0d, x0h, x0w, D, H, W, pd >> 1, ph >> 1, pw >> 1, bn_scale, bn_shift,
-                       bn_mean, residual, y, md_n, mh_n, mw_n, total);
+                       bn_mean, residual, y, md_n, mh_n, mw_n, total, in_bytes, out_bytes);
   else
     hipLaunchKernelGGL((deconv3d_k3s2_kernel<CD, CH, CW, false>), grid, dim3(kBlock), lds, s, x, x2, weight, Cin,
                        rd, rh, rw, x0d, x0h, x0w, D, H, W, pd >> 1, ph >> 1, pw >> 1, bn_scale, bn_shift,
-                       bn_mean, residual, y, md_n, mh_n, mw_n, total);
+                       bn_mean, residual, y, md_n, mh_n, mw_n, total, in_bytes, out_bytes);
 }
 
 }  // namespace
