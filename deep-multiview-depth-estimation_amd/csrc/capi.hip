@@ -255,13 +255,15 @@ int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, 
   if (!x || !weight || !y || batch <= 0 || c_in <= 0 || d <= 0 || h <= 0 || w <= 0)
     return MVS_ERR_INVALID_ARGUMENT;
   if (c_out != 1 && c_out != 8) return MVS_ERR_INVALID_ARGUMENT;
-  if (flags & ~MVS_CONV_IN_C4) return MVS_ERR_INVALID_ARGUMENT;
+  if (flags & ~(MVS_CONV_IN_C4 | MVS_CONV_WINO_Z)) return MVS_ERR_INVALID_ARGUMENT;
+  if ((flags & MVS_CONV_WINO_Z) && c_out != 8) return MVS_ERR_INVALID_ARGUMENT;
   if ((flags & MVS_CONV_IN_C4) && (c_in % 4 || ((uintptr_t)x & 15u))) return MVS_ERR_INVALID_ARGUMENT;
   if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
     return MVS_ERR_INVALID_ARGUMENT;
   // staging offsets inside one channel volume are 32-bit
   if ((uint64_t)d * (uint64_t)h * (uint64_t)w >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
-  mvs::launch_conv3d_k3_narrow(x, (flags & MVS_CONV_IN_C4) != 0, weight, y, batch, c_in, c_out, d, h, w,
+  mvs::launch_conv3d_k3_narrow(x, (flags & MVS_CONV_IN_C4) != 0, (flags & MVS_CONV_WINO_Z) != 0, weight, y, batch,
+                               c_in, c_out, d, h, w,
                                bn_scale, bn_shift, bn_mean,
                                (hipStream_t)stream);
   return mvs::hip_status();

@@ -24,7 +24,14 @@ namespace {
 
 constexpr int kTX = 32, kTY = 8, kDT = 4;
 
-template <int COUT, bool C4>
+// WZ (COUT = 8): Winograd F(2,3) along depth.  The thread's 4 output depths are two windows of 2
+// (planes 0..3 and 2..5 of the staged 6); per (channel, ky, kx) each window's 4 depth values z are
+// transformed (v = B^T z: z0 - z2, z1 + z2, z2 - z1, z1 - z3, packed over the two windows) and
+// multiplied position-wise with the transformed weights U = G g (g0, (g0 + g1 + g2) / 2,
+// (g0 - g1 + g2) / 2, g2; formed in float64 on the host, ops.py), accumulated per position; the
+// outputs are A^T m (m0 + m1 + m2, m1 - m2 - m3) at the end.  Per input channel 288 packed FMAs +
+// 36 packed adds instead of 432 packed FMAs.  Weights wu[c][ky][kx][4][co].
+template <int COUT, bool C4, bool WZ = false>
 __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
     const float* __restrict__ in, const float* __restrict__ wt, float* __restrict__ out, int Cin,
     int D, int H, int W, int tiles_x, int tiles_y, int dgroups, const float* __restrict__ bn_scale,
@@ -89,6 +96,16 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
 #pragma unroll
     for (int q = 0; q < (NP > 0 ? NP : 1); ++q) acc2[d][q] = f2v{0.0f, 0.0f};
   }
+  // WZ: per (window, position, channel pair): the Winograd-domain sums
+  f2v accw[WZ ? 2 : 1][WZ ? 4 : 1][WZ ? NP : 1];
+  if constexpr (WZ) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int ps = 0; ps < 4; ++ps)
+#pragma unroll
+        for (int q = 0; q < NP; ++q) accw[a][ps][q] = f2v{0.0f, 0.0f};
+  }
 
   const int passes = C4 ? Cin / 4 : Cin;
   for (int q = 0; q < passes; ++q) {
@@ -106,6 +123,31 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
     for (int u = 0; u < NQ; ++u) {
       const int c = q * NQ + u;
       const float* lc = lds + u * kStage;
+      if constexpr (WZ) {
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            // the tap's 6 staged planes, read as needed (not held across taps: registers);
+            // windows A (planes 0..3) and B (planes 2..5) side by side in the two halves
+            float t[kPD];
+#pragma unroll
+            for (int p = 0; p < kPD; ++p) t[p] = lc[p * kPlane + (ly + ky) * kPX + lx + kx];
+            const f2v z0 = {t[0], t[2]}, z1 = {t[1], t[3]}, z2 = {t[2], t[4]}, z3 = {t[3], t[5]};
+            const f2v v[4] = {z0 - z2, z1 + z2, z2 - z1, z1 - z3};
+            asm volatile("" ::: "memory");
+            const f2v* wg = reinterpret_cast<const f2v*>(wt + ((size_t)(c * 9 + ky * 3 + kx) * 4) * 8);
+#pragma unroll
+            for (int ps = 0; ps < 4; ++ps)
+#pragma unroll
+              for (int qq = 0; qq < NP; ++qq) {
+                const f2v u = wg[ps * 4 + qq];
+                accw[0][ps][qq] = __builtin_elementwise_fma(f2v{v[ps].x, v[ps].x}, u, accw[0][ps][qq]);
+                accw[1][ps][qq] = __builtin_elementwise_fma(f2v{v[ps].y, v[ps].y}, u, accw[1][ps][qq]);
+              }
+          }
+        continue;
+      }
       // the 3 x 3 taps of every staged plane, read once
       float tap[kPD][3][3];
 #pragma unroll
@@ -153,6 +195,15 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
     }
   }
 
+  if constexpr (WZ) {   // A^T m: (m0 + m1 + m2, m1 - m2 - m3) per window
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int qq = 0; qq < NP; ++qq) {
+        acc2[2 * a][qq] = accw[a][0][qq] + accw[a][1][qq] + accw[a][2][qq];
+        acc2[2 * a + 1][qq] = accw[a][1][qq] - accw[a][2][qq] - accw[a][3][qq];
+      }
+  }
   const int gx = tx0 + lx, gy = ty0 + ly;
   if (gx >= W || gy >= H) return;
   float* ob = out + (size_t)b * COUT * vol + (size_t)gy * W + gx;
@@ -168,21 +219,25 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   }
 }
 
-template <int COUT, bool C4>
+template <int COUT, bool C4, bool WZ = false>
 void launch_narrow(const float* in, const float* weight, float* out, int B, int Cin, int D, int H, int W,
                    const float* bn_scale, const float* bn_shift, const float* bn_mean, hipStream_t s) {
   const int tiles_x = (W + kTX - 1) / kTX, tiles_y = (H + kTY - 1) / kTY, dgroups = (D + kDT - 1) / kDT;
   const dim3 grid((unsigned)((size_t)B * dgroups * tiles_y * tiles_x));
-  hipLaunchKernelGGL((conv3d_k3_narrow_kernel<COUT, C4>), grid, dim3(kBlock), 0, s, in, weight, out, Cin, D, H, W,
-                     tiles_x, tiles_y, dgroups, bn_scale, bn_shift, bn_mean);
+  hipLaunchKernelGGL((conv3d_k3_narrow_kernel<COUT, C4, WZ>), grid, dim3(kBlock), 0, s, in, weight, out, Cin, D, H,
+                     W, tiles_x, tiles_y, dgroups, bn_scale, bn_shift, bn_mean);
 }
 
 }  // namespace
 
-void launch_conv3d_k3_narrow(const float* in, bool in_c4, const float* weight, float* out, int B, int Cin,
-                             int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
+void launch_conv3d_k3_narrow(const float* in, bool in_c4, bool wino_z, const float* weight, float* out, int B,
+                             int Cin, int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
                              const float* bn_mean, hipStream_t s) {
-  if (Cout == 8 && in_c4)
+  if (wino_z && in_c4)
+    launch_narrow<8, true, true>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
+  else if (wino_z)
+    launch_narrow<8, false, true>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
+  else if (Cout == 8 && in_c4)
     launch_narrow<8, true>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
   else if (Cout == 8)
     launch_narrow<8, false>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);

@@ -53,8 +53,9 @@ void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, u
 // conv3d_narrow.hip: 3x3x3 stride-1 padding-1 bias-free Conv3d, NCDHW fp32, Cout in {1, 8}
 // (optional epilogue: max((v - bn_mean) * bn_scale + bn_shift, 0), all three or none); in_c4: the
 // input is channel-quad in[B][Cin/4][D][H][W][4]
-void launch_conv3d_k3_narrow(const float* in, bool in_c4, const float* weight, float* out, int B, int Cin,
-                             int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
+// wino_z (Cout = 8): Winograd F(2,3) along depth, weight = the transformed wu[Cin][3][3][4][8]
+void launch_conv3d_k3_narrow(const float* in, bool in_c4, bool wino_z, const float* weight, float* out, int B,
+                             int Cin, int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
                              const float* bn_mean, hipStream_t s);
 
 // conv2d_narrow.hip: bias-free Conv2d of the encoder / refinement (padding k/2), NCHW fp32, weights

@@ -244,7 +244,7 @@ class CostVolumeReg(nn.Module):
         side = _side_stream(cv.device)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            y0 = conv3d_k3(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), in_c4=c4)
+            y0 = conv3d_k3(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), in_c4=c4, wino_z=True)
         cv.record_stream(side)
         lv = []
         for conv_a, conv_b, bn, reg in ((self.conv_1_0, self.conv_1_1, self.BN_1, B),
@@ -336,7 +336,7 @@ class CostVolumeReg(nn.Module):
         side = _side_stream(cv.device)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            y0 = conv3d_k3(cv, self.conv_0_0.weight, in_c4=c4)
+            y0 = conv3d_k3(cv, self.conv_0_0.weight, in_c4=c4, wino_z=True)
             p0 = _bn_train(self.BN_0, *channel_stats(y0, False), count)
         cv.record_stream(side)
         stage = []

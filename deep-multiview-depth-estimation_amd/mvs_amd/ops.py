@@ -350,12 +350,13 @@ torch.library.register_autograd("mvs::extract_depth_map", _sam_backward, setup_c
 @torch.library.custom_op("mvs::conv3d_k3", mutates_args=())
 def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Tensor] = None,
               bn_shift: Optional[torch.Tensor] = None, bn_mean: Optional[torch.Tensor] = None,
-              in_c4: bool = False) -> torch.Tensor:
+              in_c4: bool = False, wino_z: bool = False) -> torch.Tensor:
     """nn.Conv3d(c_in, c_out, 3, stride=1, padding=1, bias=False) forward, c_out in {1, 8}, fp32
     NCDHW, on the HIP kernel (csrc/conv3d_narrow.hip); with bn_* given, max((y - mean) * scale +
     shift, 0) is fused (eval BN + ReLU).  ``in_c4``: x is the channel-quad [B, Cin/4, D, H, W, 4]
-    of cost_volume_c4.  Inference only (no autograd formula): CostVolumeReg uses it on the
-    eval-mode, no-grad path."""
+    of cost_volume_c4.  ``wino_z`` (c_out = 8): Winograd F(2,3) along depth (MVS_CONV_WINO_Z; the
+    transformed weights are formed in float64 here).  Inference only (no autograd formula):
+    CostVolumeReg uses it on the eval-mode, no-grad path."""
     _require_gpu(x, "x")
     lib = _lib.load()
     if in_c4:
@@ -372,20 +373,36 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Te
     x = x.to(_F32).contiguous()
     cout = weight.shape[0]
     # the kernel reads weight[c_in][3][3][3][c_out] (pairs of output channels per 8-byte load)
-    w = derived("k3", (weight,), lambda wt: wt.to(device=x.device, dtype=_F32).permute(1, 2, 3, 4, 0).contiguous())
+    if wino_z and cout != 8:
+        raise ValueError("wino_z needs c_out = 8")
+    if wino_z:
+        w = derived("k3wz", (weight,), lambda wt: _wino_z_weight(wt).to(device=x.device))
+    else:
+        w = derived("k3", (weight,), lambda wt: wt.to(device=x.device, dtype=_F32).permute(1, 2, 3, 4, 0).contiguous())
     bn = [t if t is None else t.to(device=x.device, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
     if any(t is None for t in bn) and not all(t is None for t in bn):
         raise ValueError("bn_scale, bn_shift and bn_mean go together")
     bp = [None if t is None else _lib.ptr(t) for t in bn]
     y = torch.empty((b, cout, d, h, wd), device=x.device, dtype=_F32)
-    st = lib.mvs_conv3d_k3_fwd(_lib.ptr(x), _lib.MVS_CONV_IN_C4 if in_c4 else 0, _lib.ptr(w), _lib.ptr(y),
+    flags = (_lib.MVS_CONV_IN_C4 if in_c4 else 0) | (_lib.MVS_CONV_WINO_Z if wino_z else 0)
+    st = lib.mvs_conv3d_k3_fwd(_lib.ptr(x), flags, _lib.ptr(w), _lib.ptr(y),
                                b, cin, cout, d, h, wd, *bp, _lib.stream_handle(x.device))
     _lib.check(st, "mvs_conv3d_k3_fwd")
     return y
 
 
+def _wino_z_weight(wt):
+    """Conv3d weight [co][ci][kd][ky][kx] -> the depth-Winograd F(2,3) weight wu[ci][ky][kx][4][co]:
+    per depth column g0..g2 the transformed taps (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2),
+    formed in float64 and rounded once (csrc/conv3d_narrow.hip, WZ)."""
+    g = wt.detach().double()
+    g0, g1, g2 = g[:, :, 0], g[:, :, 1], g[:, :, 2]
+    u = torch.stack((g0, (g0 + g1 + g2) * 0.5, (g0 - g1 + g2) * 0.5, g2), dim=2)   # [co][ci][4][ky][kx]
+    return u.permute(1, 3, 4, 2, 0).contiguous().to(_F32)
+
+
 @conv3d_k3.register_fake
-def _(x, weight, bn_scale=None, bn_shift=None, bn_mean=None, in_c4=False):
+def _(x, weight, bn_scale=None, bn_shift=None, bn_mean=None, in_c4=False, wino_z=False):
     return x.new_empty((x.shape[0], weight.shape[0]) + tuple(x.shape[2:5]))
 
 

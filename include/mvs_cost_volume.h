@@ -201,6 +201,10 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
 /* input-layout flag of mvs_conv3d_k3_fwd / mvs_conv3d_region_fwd (MVS_CONV_S2): the volume is
  * channel-quad x[batch][c_in/4][D][H][W][4], the layout of mvs_cost_volume_fwd_c4 */
 #define MVS_CONV_IN_C4 2
+/* flag of mvs_conv3d_k3_fwd (c_out = 8): Winograd F(2,3) along depth; the weight is then the
+ * transformed wu[c_in][3][3][4][8]: per (c_in, ky, kx, c_out) the depth taps g0..g2 become
+ * (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2) (formed in float64, rounded once) */
+#define MVS_CONV_WINO_Z 4
 
 /* Regulariser layers conv_0_0 (32 -> 8) and conv_out (8 -> 1) of CostVolumeReg (model.py:77,96 /
  * forward at model.py:101,123): nn.Conv3d(c_in, c_out, 3, stride=1, padding=1, bias=False) over

@@ -454,12 +454,15 @@ def test_depth_sharded_single_rank_equals_model():
     assert torch.equal(ini, ini_s) and torch.equal(ref, ref_s)
 
 
-@pytest.mark.parametrize("shape", [(2, 32, 8, 12, 20, 40), (1, 8, 1, 5, 9, 33), (1, 32, 8, 7, 8, 32),
-                                   (2, 8, 1, 16, 24, 70)])
-def test_narrow_conv3d_matches_torch(shape):
+@pytest.mark.parametrize("shape,wino", [((2, 32, 8, 12, 20, 40), False), ((1, 8, 1, 5, 9, 33), False),
+                                        ((1, 32, 8, 7, 8, 32), False), ((2, 8, 1, 16, 24, 70), False),
+                                        ((2, 32, 8, 12, 20, 40), True), ((1, 32, 8, 7, 8, 32), True),
+                                        ((1, 8, 8, 9, 17, 45), True)])
+def test_narrow_conv3d_matches_torch(shape, wino):
     """mvs::conv3d_k3 (csrc/conv3d_narrow.hip, CostVolumeReg.conv_0_0 / conv_out) against the torch
     fp32 Conv3d on the same device, and against float64 on the CPU: ragged x/y tiles, D not a
-    multiple of the 4-depth groups, both channel counts."""
+    multiple of the 4-depth groups, both channel counts, the direct and the depth-Winograd F(2,3)
+    (wino_z, conv_0_0's inference form) sums."""
     from mvs_amd.ops import conv3d_k3
     b, cin, cout, d, h, w = shape
     g = torch.Generator().manual_seed(sum(shape))
@@ -467,7 +470,7 @@ def test_narrow_conv3d_matches_torch(shape):
     wt = torch.randn(cout, cin, 3, 3, 3, generator=g) * 0.1
     ref64 = torch.nn.functional.conv3d(x.double(), wt.double(), padding=1)
     with torch.no_grad():
-        y = conv3d_k3(x.to(DEV), wt.to(DEV)).cpu()
+        y = conv3d_k3(x.to(DEV), wt.to(DEV), wino_z=wino).cpu()
         yt = torch.nn.functional.conv3d(x.to(DEV), wt.to(DEV), padding=1).cpu()
     scale = ref64.abs().max().item()
     err = (y.double() - ref64).abs().max().item()
