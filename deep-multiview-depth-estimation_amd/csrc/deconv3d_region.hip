@@ -27,6 +27,8 @@ namespace mvs {
 namespace {
 
 constexpr int kCout = 8;
+typedef float f2v_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(4))) const f2v_t const_f2v_t;
 constexpr int kWRow = 28;   // 27 taps padded to 7 float4
 
 // per dim: (input slot 0 = L, 1 = U, kernel tap k) pairs feeding output s
@@ -40,7 +42,7 @@ struct Stencil {
   static constexpr int k1[2] = {C ? 0 : 1, 2};
 };
 
-template <int CD, int CH, int CW, bool CL>
+template <int CD, int CH, int CW, int LM>
 __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
     const float* __restrict__ x, const float* __restrict__ x2, const float* __restrict__ wt, int Cin, int rd,
     int rh, int rw,
@@ -48,6 +50,8 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
     const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
     const float* __restrict__ mean, const float* __restrict__ residual, float* __restrict__ y,
     int md_n, int mh_n, int mw_n, size_t total, size_t total_in_bytes, size_t out_bytes) {
+  constexpr bool CL = LM == 1;   // channels-last input
+  constexpr bool WT = LM == 2;   // NCDHW input, tap-major weights wt[ci][27][co]: packed FMAs
   extern __shared__ float4 wl4[];   // CL: [ci][co][7] float4 = W[ci][co][27] padded
   if constexpr (CL) {
     float* wl = reinterpret_cast<float*>(wl4);
@@ -128,6 +132,35 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
                   acc[sd][sh][sw][co] = fmaf(v[id][ih][iw], w[kd * 9 + kh * 3 + kw], acc[sd][sh][sw][co]);
                 }
     }
+  };
+  // WT: each of the 27 taps feeds exactly one output voxel of the block from one input voxel (per
+  // dim, class 1: k0 -> (s1, U), k1 -> (s0, L), k2 -> (s1, L); class 0: k0 -> (s0, U),
+  // k1 -> (s1, U), k2 -> (s0, L)), so a channel is 27 taps x 4 channel pairs of packed FMAs with
+  // the pair's weights as one 64-bit scalar operand
+  auto channel_pk = [&](int ci, const float (&v)[2][2][2]) {
+    constexpr int sD[3] = {CD ? 1 : 0, CD ? 0 : 1, CD ? 1 : 0}, iD[3] = {1, CD ? 0 : 1, 0};
+    constexpr int sH[3] = {CH ? 1 : 0, CH ? 0 : 1, CH ? 1 : 0}, iH[3] = {1, CH ? 0 : 1, 0};
+    constexpr int sW[3] = {CW ? 1 : 0, CW ? 0 : 1, CW ? 1 : 0}, iW[3] = {1, CW ? 0 : 1, 0};
+#pragma unroll
+    for (int kd = 0; kd < 3; ++kd)
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        asm volatile("" ::: "memory");   // one (kd, kh) row of weights in SGPRs at a time
+        const const_f2v_t* wg =
+            (const const_f2v_t*)uniform_ptr(wt + ((size_t)ci * 27 + kd * 9 + kh * 3) * kCout);
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const float vv = v[iD[kd]][iH[kh]][iW[kw]];
+          float* a = acc[sD[kd]][sH[kh]][sW[kw]];
+#pragma unroll
+          for (int p = 0; p < kCout / 2; ++p) {
+            const f2v_t r = __builtin_elementwise_fma(f2v_t{vv, vv}, wg[kw * (kCout / 2) + p],
+                                                      f2v_t{a[2 * p], a[2 * p + 1]});
+            a[2 * p] = r.x;
+            a[2 * p + 1] = r.y;
+          }
+        }
+      }
   };
   if constexpr (CL) {
     // channels-last: 4 channels of each of the 8 input voxels per 16-byte load (Cin % 4 == 0)
@@ -213,7 +246,8 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
 #pragma unroll
           for (int e = 0; e < 2; ++e) v[a][c][e] = vn[a][c][e];
       if (ci + 1 < Cin) load(ci + 1, vn);
-      channel(ci, v);
+      if constexpr (WT) channel_pk(ci, v);
+      else channel(ci, v);
     }
   }
   const size_t plane = (size_t)D * H * W;
@@ -303,7 +337,7 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
 }
 
 template <int CD, int CH, int CW>
-void launch_cls(dim3 grid, size_t lds, hipStream_t s, const float* x, const float* x2, bool cl,
+void launch_cls(dim3 grid, size_t lds, hipStream_t s, const float* x, const float* x2, int lm,
                 const float* weight, int Cin, int rd, int rh, int rw, int x0d, int x0h, int x0w, int D, int H,
                 int W, int pd, int ph, int pw, const float* bn_scale, const float* bn_shift,
                 const float* bn_mean, const float* residual, float* y, int md_n, int mh_n, int mw_n,
@@ -313,30 +347,34 @@ void launch_cls(dim3 grid, size_t lds, hipStream_t s, const float* x, const floa
   // the epilogue's buffer-store path: even W and the whole output under 2^31 bytes (0 = the general path)
   const size_t ob = total / ((size_t)md_n * mh_n * mw_n) * (size_t)kCout * D * H * W * 4u;
   const size_t out_bytes = (W % 2 == 0 && ob < (1ull << 31)) ? ob : 0;
-  if (cl)
-    hipLaunchKernelGGL((deconv3d_k3s2_kernel<CD, CH, CW, true>), grid, dim3(kBlock), lds, s, x, x2, weight, Cin,
+  if (lm == 1)
+    hipLaunchKernelGGL((deconv3d_k3s2_kernel<CD, CH, CW, 1>), grid, dim3(kBlock), lds, s, x, x2, weight, Cin,
+                       rd, rh, rw, x0d, x0h, x0w, D, H, W, pd >> 1, ph >> 1, pw >> 1, bn_scale, bn_shift,
+                       bn_mean, residual, y, md_n, mh_n, mw_n, total, in_bytes, out_bytes);
+  else if (lm == 2)
+    hipLaunchKernelGGL((deconv3d_k3s2_kernel<CD, CH, CW, 2>), grid, dim3(kBlock), lds, s, x, x2, weight, Cin,
                        rd, rh, rw, x0d, x0h, x0w, D, H, W, pd >> 1, ph >> 1, pw >> 1, bn_scale, bn_shift,
                        bn_mean, residual, y, md_n, mh_n, mw_n, total, in_bytes, out_bytes);
   else
-    hipLaunchKernelGGL((deconv3d_k3s2_kernel<CD, CH, CW, false>), grid, dim3(kBlock), lds, s, x, x2, weight, Cin,
+    hipLaunchKernelGGL((deconv3d_k3s2_kernel<CD, CH, CW, 0>), grid, dim3(kBlock), lds, s, x, x2, weight, Cin,
                        rd, rh, rw, x0d, x0h, x0w, D, H, W, pd >> 1, ph >> 1, pw >> 1, bn_scale, bn_shift,
                        bn_mean, residual, y, md_n, mh_n, mw_n, total, in_bytes, out_bytes);
 }
 
 }  // namespace
 
-void launch_deconv3d_k3s2(const float* x, const float* x2, bool channels_last, int B, int Cin, int rd,
+void launch_deconv3d_k3s2(const float* x, const float* x2, int layout, int B, int Cin, int rd,
                           int rh, int rw, int x0d, int x0h, int x0w, const float* weight, int D, int H,
                           int W, int pd, int ph, int pw, const float* bn_scale, const float* bn_shift,
                           const float* bn_mean, const float* residual, float* y, hipStream_t s) {
   const int md_n = (D + 1) / 2, mh_n = (H + 1) / 2, mw_n = (W + 1) / 2;
   const size_t total = (size_t)B * md_n * mh_n * mw_n;
   const dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
-  const size_t lds = channels_last ? (size_t)Cin * kCout * kWRow * sizeof(float) : 0;
+  const size_t lds = layout == 1 ? (size_t)Cin * kCout * kWRow * sizeof(float) : 0;
   const int cls = (pd & 1) * 4 + (ph & 1) * 2 + (pw & 1);
 #define MVS_DECONV_CASE(c)                                                                         \
   case c:                                                                                          \
-    launch_cls<(c >> 2) & 1, (c >> 1) & 1, c & 1>(grid, lds, s, x, x2, channels_last, weight, Cin, rd, rh, rw, x0d, x0h, \
+    launch_cls<(c >> 2) & 1, (c >> 1) & 1, c & 1>(grid, lds, s, x, x2, layout, weight, Cin, rd, rh, rw, x0d, x0h, \
                                                   x0w, D, H, W, pd, ph, pw, bn_scale, bn_shift,     \
                                                   bn_mean, residual, y, md_n, mh_n, mw_n, total);   \
     break;

@@ -67,8 +67,9 @@ int launch_conv2d_narrow(const float* in, const float* wt, float* out, int N, in
 
 // deconv3d_region.hip: stride-2 kernel-3 ConvTranspose3d (Cout 8) from a region tensor to the full
 // volume, optional fused BN(eval)+ReLU and residual add
-// (channels_last: x and x2 are [B][rd][rh][rw][Cin]; x2 (nullable) is added to x)
-void launch_deconv3d_k3s2(const float* x, const float* x2, bool channels_last, int B, int Cin, int rd,
+// (layout 1: x and x2 are channels-last [B][rd][rh][rw][Cin]; 0: NCDHW, weight [Cin][8][27]; 2: NCDHW,
+// tap-major weight [Cin][27][8]; x2 (nullable) is added to x)
+void launch_deconv3d_k3s2(const float* x, const float* x2, int layout, int B, int Cin, int rd,
                           int rh, int rw, int x0d, int x0h, int x0w, const float* weight, int D, int H,
                           int W, int pd, int ph, int pw, const float* bn_scale, const float* bn_shift,
                           const float* bn_mean, const float* residual, float* y, hipStream_t s);

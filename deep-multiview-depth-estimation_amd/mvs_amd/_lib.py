@@ -27,6 +27,7 @@ MVS_CONV_S1, MVS_CONV_S2, MVS_CONV_T2 = 0, 1, 2
 MVS_CONV_OUT_NCDHW = 1
 MVS_CONV_IN_C4 = 2
 MVS_CONV_WINO_Z = 4
+MVS_DECONV_WEIGHT_TAPS = 2
 MVS_STATS_SLOTS = 64
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported n_views", -3: "too large",
           -4: "HIP runtime error"}

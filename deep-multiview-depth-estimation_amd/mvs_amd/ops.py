@@ -481,9 +481,15 @@ def deconv3d_k3s2(x: torch.Tensor, origin: list[int], weight: torch.Tensor, out_
         x2 = x2.to(_F32).contiguous()
         if x2.shape != x.shape:
             raise ValueError("x2 must have x's shape")
-    w = weight.to(device=x.device, dtype=_F32).contiguous()
-    if tuple(w.shape) != (cin, 8, 3, 3, 3):
-        raise ValueError("weight [c_in, 8, 3, 3, 3] expected, got %s" % (tuple(w.shape),))
+    if tuple(weight.shape) != (cin, 8, 3, 3, 3):
+        raise ValueError("weight [c_in, 8, 3, 3, 3] expected, got %s" % (tuple(weight.shape),))
+    if channels_last:
+        w = weight.to(device=x.device, dtype=_F32).contiguous()
+        flags = _lib.MVS_LAYOUT_CHANNELS_LAST
+    else:   # tap-major weight[c_in][27][8]: the NCDHW kernel's packed-FMA form
+        w = derived("deconv_taps", (weight,),
+                    lambda wt: wt.to(device=x.device, dtype=_F32).reshape(cin, 8, 27).transpose(1, 2).contiguous())
+        flags = _lib.MVS_DECONV_WEIGHT_TAPS
     d, h, wd = out_dims
     f = lambda t: None if t is None else t.to(device=x.device, dtype=_F32).contiguous()
     sc, sh, mu, res = f(bn_scale), f(bn_shift), f(bn_mean), f(residual)
@@ -493,8 +499,7 @@ def deconv3d_k3s2(x: torch.Tensor, origin: list[int], weight: torch.Tensor, out_
         raise ValueError("residual must be [B, 8, D, H, W]")
     y = torch.empty((b, 8, d, h, wd), device=x.device, dtype=_F32)
     pt = lambda t: None if t is None else _lib.ptr(t)
-    st = lib.mvs_deconv3d_k3s2_fwd(_lib.ptr(x), pt(x2),
-                                   _lib.MVS_LAYOUT_CHANNELS_LAST if channels_last else 0, b, cin, 8, rd, rh,
+    st = lib.mvs_deconv3d_k3s2_fwd(_lib.ptr(x), pt(x2), flags, b, cin, 8, rd, rh,
                                    rw, *origin, _lib.ptr(w), d, h, wd, *pad, pt(sc), pt(sh), pt(mu), pt(res),
                                    _lib.ptr(y), _lib.stream_handle(x.device))
     _lib.check(st, "mvs_deconv3d_k3s2_fwd")
