@@ -5,16 +5,18 @@ batch 4 per GPU, synthetic N(0,1) images already resident in HBM, real DTU scan-
 (tests/golden/dtu_scan1_cameras.npz), d_min=425, d_int=1, D_SCALE=25, random-init weights of the
 reference architecture (tests/golden/weights.py formula), fp32, BN eval mode, inference (no_grad).
 
-A step = one full MVSNet.forward over one batch (feature encoder -> fused warp+variance HIP kernel ->
-3-D regulariser (MIOpen) -> HIP soft-argmin -> refinement).  value = depth maps/s over all ranks.
+A step = one full MVSNet.forward over one batch (HIP feature encoder -> fused warp+variance HIP
+kernel -> 3-D regulariser on its live regions (HIP MFMA region convs) -> HIP softmax
+and soft-argmin -> HIP refinement).  value = depth maps/s over all ranks.
 
 Multi-GPU (torchrun, one process per GPU): --mode samples (default) shards SAMPLES across ranks --
 every rank runs its own batch, no collective in the data path, "scaling": "weak".  --mode dshard
 runs BASELINE configs[3]: D=256 planes split across ranks, each rank's fused kernel writes its
-D-slab, an RCCL all-gather reassembles the full cost volume, the sample's owner runs the regulariser.
+D-slab, and each sample's slab goes point to point (RCCL send/recv over xGMI,
+mvs_amd/depth_shards.py) to the rank that owns the sample, which runs the regulariser.
 
 Also reported (one JSON line, rank 0):
-  roofline      the fused kernel (cost_volume_kernel): algorithmic bytes per launch
+  roofline      the fused kernel (cost_volume_staged_kernel): algorithmic bytes per launch
                 (4*B*V*C*h*w features read once + 4*B*C*D*h*w cost volume written once) / average
                 launch time measured with HIP events on the launch stream, vs 8 TB/s HBM peak;
                 traffic = PMC HBM bytes from profiles/ (rocprofv3 --pmc, FETCH_SIZE x2 on gfx950)

@@ -9,7 +9,9 @@ namespace {
 
 using mvs::Geometry;
 
-int check_geometry(int B, int V, int C, int h, int w, int d_count, Geometry& g) {
+// store_es: output element bytes of the packed (2 <= V <= 8) fused kernel this geometry feeds (4 fp32
+// NCDHW, 2 bf16, 16 channel-quad), 0 for entry points that build no cost-volume store descriptors
+int check_geometry(int B, int V, int C, int h, int w, int d_count, Geometry& g, int store_es = 0) {
   if (B <= 0 || C <= 0 || h < 2 || w < 2 || d_count <= 0) return MVS_ERR_INVALID_ARGUMENT;
   if (V < 1 || V > MVS_MAX_VIEWS) return MVS_ERR_UNSUPPORTED_VIEWS;
   const uint64_t hw = (uint64_t)h * (uint64_t)w;
@@ -17,9 +19,10 @@ int check_geometry(int B, int V, int C, int h, int w, int d_count, Geometry& g) 
   if ((uint64_t)C * hw >= (1ull << 31) || h > 32000 || w > 32000) return MVS_ERR_TOO_LARGE;
   // the packed kernels build 32-bit buffer descriptors and offsets: a sample's padded channel-quad
   // images (V * ceil(C/4) * (h+2) * (w+2) float4, byte offsets held in ints) and a plane group's
-  // cost-volume run (8 planes * hw * 4 B)
+  // cost-volume run (up to 8 planes * hw * store_es bytes: the store offsets soff0 + pl * hw * es)
+  const bool packed = V >= 2 && V <= 8;
   const uint64_t padded = (uint64_t)V * (uint64_t)((C + 3) / 4) * (uint64_t)(h + 2) * (uint64_t)(w + 2) * 16u;
-  if ((V >= 2 && V <= 8 && padded >= (1ull << 31)) || 8ull * hw * 4ull >= (1ull << 32)) return MVS_ERR_TOO_LARGE;
+  if (packed && (padded >= (1ull << 31) || 8ull * hw * (uint64_t)store_es >= (1ull << 32))) return MVS_ERR_TOO_LARGE;
   const uint64_t tiles = (hw + mvs::kBlock - 1) / mvs::kBlock;
   const uint64_t total = (uint64_t)B * tiles * (uint64_t)d_count;
   if (total >= (1ull << 31) - 8) return MVS_ERR_TOO_LARGE;
@@ -45,9 +48,10 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
                          float* workspace, void* cv_out, int es, void* stream, void* ev0, void* ev1) {
   if (!feat || !workspace || !cv_out) return MVS_ERR_INVALID_ARGUMENT;
   Geometry g;
-  int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g);
+  int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g, es);
   if (st != MVS_OK) return st;
   if (!cams_ok(K, R, T, d_min, d_int) || d_begin < 0) return MVS_ERR_INVALID_ARGUMENT;
+  const mvs::LaunchCheck lc;
   hipStream_t s = (hipStream_t)stream;
   if (n_views == 1) {  // the variance of a single view is identically zero (0 in fp32 and bf16)
     st = mvs_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
@@ -56,7 +60,7 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
     const size_t ch = es == 16 ? (size_t)((channels + 3) / 4) : (size_t)channels;
     if (hipMemsetAsync(cv_out, 0, (size_t)batch_size * ch * d_count * h * w * es, s) != hipSuccess)
       return MVS_ERR_HIP;
-    return mvs::hip_status();
+    return lc.status();
   }
   float* packed = reinterpret_cast<float*>(
       reinterpret_cast<char*>(workspace) +
@@ -71,7 +75,7 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
   else
     mvs::launch_cost_volume_fwd_bf16(g, feat, cm, workspace, packed, cv_out, s, (hipEvent_t)ev0,
                                      (hipEvent_t)ev1);
-  return mvs::hip_status();
+  return lc.status();
 }
 
 }  // namespace
@@ -110,9 +114,10 @@ int mvs_plane_sampling(const float* K, const float* R, const float* T, const flo
   if (batch_size <= 0 || h < 2 || w < 2 || d_count <= 0 || d_begin < 0)
     return MVS_ERR_INVALID_ARGUMENT;
   if (n_views < 1 || n_views > MVS_MAX_VIEWS) return MVS_ERR_UNSUPPORTED_VIEWS;
+  const mvs::LaunchCheck lc;
   mvs::launch_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
                              d_scale, sampling, (hipStream_t)stream);
-  return mvs::hip_status();
+  return lc.status();
 }
 
 int mvs_cost_volume_fwd_timed(const float* feat, const float* K, const float* R, const float* T,
@@ -164,11 +169,12 @@ int mvs_homography_warp_fwd(const float* feat, const float* K, const float* R, c
   Geometry g;
   int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g);
   if (st != MVS_OK) return st;
+  const mvs::LaunchCheck lc;
   st = mvs_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
                           d_scale, workspace, stream);
   if (st != MVS_OK) return st;
   mvs::launch_warp(g, feat, workspace, warped_out, (hipStream_t)stream);
-  return mvs::hip_status();
+  return lc.status();
 }
 
 int mvs_assemble_cost_volume_fwd(const float* warped, int batch_size, int n_views, int channels,
@@ -176,15 +182,18 @@ int mvs_assemble_cost_volume_fwd(const float* warped, int batch_size, int n_view
   if (!warped || !cv_out || batch_size <= 0 || channels <= 0 || d <= 0 || h <= 0 || w <= 0)
     return MVS_ERR_INVALID_ARGUMENT;
   if (n_views < 1) return MVS_ERR_UNSUPPORTED_VIEWS;
+  const mvs::LaunchCheck lc;
   mvs::launch_variance(warped, batch_size, n_views, (size_t)channels * d * h * w, cv_out,
                        (hipStream_t)stream);
-  return mvs::hip_status();
+  return lc.status();
 }
 
 size_t mvs_cost_volume_bwd_workspace_bytes(int batch_size, int n_views, int channels, int h, int w,
-                                           int d_count) {
+                                           int d_count, int flags) {
   if (batch_size <= 0 || n_views <= 0 || channels <= 0 || h <= 0 || w <= 0 || d_count <= 0) return 0;
-  return mvs::cost_volume_bwd_workspace_bytes(batch_size, n_views, channels, h, w, d_count);
+  if (flags & ~MVS_BWD_DETERMINISTIC) return 0;
+  return mvs::cost_volume_bwd_workspace_bytes(batch_size, n_views, channels, h, w, d_count,
+                                              (flags & MVS_BWD_DETERMINISTIC) != 0);
 }
 
 int mvs_cost_volume_bwd(const float* feat, const float* workspace, const float* grad_cv,
@@ -199,8 +208,10 @@ int mvs_cost_volume_bwd(const float* feat, const float* workspace, const float* 
   // the packed backward reads grad_cv through a 32-bit descriptor over one 4-channel chunk
   if (n_views >= 2 && n_views <= 8 && 16ull * (uint64_t)d_count * (uint64_t)h * (uint64_t)w >= (1ull << 31))
     return MVS_ERR_TOO_LARGE;
-  return mvs::launch_cost_volume_bwd(g, feat, workspace, grad_cv, bwd_workspace, grad_feat,
-                                     (flags & MVS_BWD_DETERMINISTIC) != 0, (hipStream_t)stream);
+  const mvs::LaunchCheck lc;
+  const int ls = mvs::launch_cost_volume_bwd(g, feat, workspace, grad_cv, bwd_workspace, grad_feat,
+                                             (flags & MVS_BWD_DETERMINISTIC) != 0, (hipStream_t)stream);
+  return ls != MVS_OK ? ls : lc.status();
 }
 
 int mvs_extract_depth_map_fwd(const float* prob, const float* d_batch, int batch_size, int d,
@@ -210,9 +221,10 @@ int mvs_extract_depth_map_fwd(const float* prob, const float* d_batch, int batch
   if (n_est < 1) return MVS_ERR_INVALID_ARGUMENT;
   if (n_est > d) n_est = d;  // every plane index is < n_est: all planes kept
   if (n_est > 16) return MVS_ERR_INVALID_ARGUMENT;
+  const mvs::LaunchCheck lc;
   mvs::launch_soft_argmin(prob, d_batch, batch_size, d, (uint32_t)h * (uint32_t)w, n_est, depth_out,
                           (hipStream_t)stream);
-  return mvs::hip_status();
+  return lc.status();
 }
 
 int mvs_normalize_images(const unsigned char* rgb, int n_images, int h, int w, const float* mean,
@@ -224,16 +236,18 @@ int mvs_normalize_images(const unsigned char* rgb, int n_images, int h, int w, c
   if (hw >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
   for (int c = 0; c < 3; ++c)
     if (!(std_dev[c] != 0.0f)) return MVS_ERR_INVALID_ARGUMENT;
+  const mvs::LaunchCheck lc;
   mvs::launch_normalize_images(rgb, n_images, (uint32_t)hw, mean, std_dev, out, (hipStream_t)stream);
-  return mvs::hip_status();
+  return lc.status();
 }
 
 int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float* out, void* stream) {
   if (!depth || !out) return MVS_ERR_INVALID_ARGUMENT;
   if (((uintptr_t)depth & 15u) || ((uintptr_t)out & 15u)) return MVS_ERR_INVALID_ARGUMENT;
   if (n == 0) return MVS_OK;
+  const mvs::LaunchCheck lc;
   mvs::launch_depth_threshold(depth, n, lo, hi, out, (hipStream_t)stream);
-  return mvs::hip_status();
+  return lc.status();
 }
 
 int mvs_conv2d_fwd(const float* x, const float* weight, float* y, int n, int c_in, int c_out, int h, int w,
@@ -244,9 +258,10 @@ int mvs_conv2d_fwd(const float* x, const float* weight, float* y, int n, int c_i
     return MVS_ERR_INVALID_ARGUMENT;
   // staging offsets inside one image are 32-bit
   if ((uint64_t)c_in * (uint64_t)h * (uint64_t)w >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
   const int st = mvs::launch_conv2d_narrow(x, weight, y, n, c_in, c_out, h, w, k, stride, bn_scale, bn_shift,
                                            bn_mean, (hipStream_t)stream);
-  return st != MVS_OK ? st : mvs::hip_status();
+  return st != MVS_OK ? st : lc.status();
 }
 
 int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, int batch, int c_in,
@@ -262,11 +277,12 @@ int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, 
     return MVS_ERR_INVALID_ARGUMENT;
   // staging offsets inside one channel volume are 32-bit
   if ((uint64_t)d * (uint64_t)h * (uint64_t)w >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
   mvs::launch_conv3d_k3_narrow(x, (flags & MVS_CONV_IN_C4) != 0, (flags & MVS_CONV_WINO_Z) != 0, weight, y, batch,
                                c_in, c_out, d, h, w,
                                bn_scale, bn_shift, bn_mean,
                                (hipStream_t)stream);
-  return mvs::hip_status();
+  return lc.status();
 }
 
 int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch, int c_in, int c_out,
@@ -286,10 +302,11 @@ int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch,
   // the region input is read through 32-bit buffer descriptors over the whole batch
   if ((uint64_t)batch * c_in * rd * rh * rw * 4u >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
   const int layout = (flags & MVS_LAYOUT_CHANNELS_LAST) ? 1 : ((flags & MVS_DECONV_WEIGHT_TAPS) ? 2 : 0);
+  const mvs::LaunchCheck lc;
   mvs::launch_deconv3d_k3s2(x, x2, layout, batch, c_in, rd, rh, rw, x0d, x0h,
                             x0w, weight, d, h, w, pd, ph, pw, bn_scale, bn_shift, bn_mean, residual, y,
                             (hipStream_t)stream);
-  return mvs::hip_status();
+  return lc.status();
 }
 
 int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, const float* weight, float* y,
@@ -325,20 +342,22 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
   if (ovox >= (1ull << 31) || desc_bytes >= 0xFFFFFFC0ull || ivox * (uint64_t)c_in >= (1ull << 62) ||
       nvox >= (1ull << 62))
     return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
   const int st = mvs::launch_conv3d_region(mode, (flags & MVS_CONV_OUT_NCDHW) != 0, (flags & MVS_CONV_IN_C4) != 0,
                                            x, x2, weight, y, batch, c_in, c_out, dims, out_origin, out_size,
                                            in_origin, in_size, pad, bn_scale, bn_shift, bn_mean,
                                            (hipStream_t)stream);
   if (st != MVS_OK) return st;
-  return mvs::hip_status();
+  return lc.status();
 }
 
 
 int mvs_softmax_depth_fwd(const float* x, int batch, int d_count, int h, int w, float* y, void* stream) {
   if (!x || !y || batch <= 0 || d_count <= 0 || h <= 0 || w <= 0) return MVS_ERR_INVALID_ARGUMENT;
   if ((uint64_t)h * (uint64_t)w >= (1ull << 32) || (uint64_t)batch * h * w >= (1ull << 37)) return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
   mvs::launch_softmax_depth(x, batch, d_count, (uint32_t)((uint64_t)h * w), y, (hipStream_t)stream);
-  return mvs::hip_status();
+  return lc.status();
 }
 
 static bool channel_layout_ok(int layout, int channels, const void* a, const void* b, const void* c) {
@@ -349,14 +368,20 @@ static bool channel_layout_ok(int layout, int channels, const void* a, const voi
   return ((((uintptr_t)a) | ((uintptr_t)b) | ((uintptr_t)c)) & 15u) == 0;
 }
 
+size_t mvs_channel_stats_slots(int layout, int batch, int channels, long long voxels) {
+  if (batch <= 0 || channels <= 0 || voxels <= 0 || (layout & ~MVS_LAYOUT_CHANNELS_LAST)) return 0;
+  return mvs::channel_stats_slots((layout & MVS_LAYOUT_CHANNELS_LAST) != 0, batch, channels, (size_t)voxels);
+}
+
 int mvs_channel_stats(const float* x, int layout, int batch, int channels, long long voxels, double* stats,
                       void* stream) {
   if (!x || !stats || batch <= 0 || channels <= 0 || voxels <= 0) return MVS_ERR_INVALID_ARGUMENT;
   if (!channel_layout_ok(layout, channels, x, nullptr, nullptr)) return MVS_ERR_INVALID_ARGUMENT;
   if ((uint64_t)batch * channels > 65535u && !(layout & MVS_LAYOUT_CHANNELS_LAST)) return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
   mvs::launch_channel_stats(x, (layout & MVS_LAYOUT_CHANNELS_LAST) != 0, batch, channels, (size_t)voxels, stats,
                             (hipStream_t)stream);
-  return mvs::hip_status();
+  return lc.status();
 }
 
 int mvs_bn_relu(const float* x, int layout, int batch, int channels, long long voxels, const float* scale,
@@ -367,9 +392,10 @@ int mvs_bn_relu(const float* x, int layout, int batch, int channels, long long v
   if (r && (!r_scale || !r_shift || !r_mean)) return MVS_ERR_INVALID_ARGUMENT;
   if (!channel_layout_ok(layout, channels, x, r, y)) return MVS_ERR_INVALID_ARGUMENT;
   if ((uint64_t)batch * channels > 65535u && !(layout & MVS_LAYOUT_CHANNELS_LAST)) return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
   mvs::launch_bn_relu(x, (layout & MVS_LAYOUT_CHANNELS_LAST) != 0, batch, channels, (size_t)voxels, scale, shift,
                       mean, r, r_scale, r_shift, r_mean, y, (hipStream_t)stream);
-  return mvs::hip_status();
+  return lc.status();
 }
 
 }  // extern "C"

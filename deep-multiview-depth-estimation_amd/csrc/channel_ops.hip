@@ -8,21 +8,26 @@
 // are HBM-bound (sums: 4 B read per element; normalisation: 4 B read + 4 B written, + 4 B read for
 // the addend).
 //
-// Sums: float64 per thread, reduced across the wave's lanes of equal channel, then added into
-// stats[slot][0 / 1][c] (sum / sum of squares) with slot = workgroup % MVS_STATS_SLOTS, so the fp64
-// global atomics of different workgroups spread over 64 copies; the caller adds the copies.
+// Sums: float64 per thread, reduced across the wave's lanes of equal channel, then across the
+// workgroup's waves through LDS in a fixed order, and WRITTEN (no atomics) to the workgroup's own slot
+// stats[slot][0 / 1][c] (sum / sum of squares); the caller adds the slots (mvs_channel_stats_slots of
+// them) in a fixed order.  Every partial sum is formed in the same order on every run, so the batch
+// statistics -- and the BatchNorm outputs and running statistics built from them -- are bit-identical
+// run to run.
 #include "launchers.h"
 #include "packed.h"
 
 namespace mvs {
 namespace {
 
-constexpr int kStatSlots = 64;   // == MVS_STATS_SLOTS
+constexpr int kWaves = kBlock / 64;
+constexpr unsigned kStatsClBlocks = 1024;   // channels-last sums: at most this many workgroups (= slots)
 
 // channels-last: float4 j holds channels 4 (j % C4) .. + 3; the grid stride is a multiple of C4
-// (C4 divides kBlock), so a thread's quad never changes
+// (C4 divides kBlock), so a thread's quad never changes.  Slot = workgroup.
 __global__ __launch_bounds__(kBlock) void channel_stats_cl_kernel(const float4* __restrict__ x, size_t n4, int C4,
                                                                   double* __restrict__ stats) {
+  __shared__ double part[kWaves][64][8];
   double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
   const size_t stride = (size_t)gridDim.x * kBlock;
   for (size_t j = (size_t)blockIdx.x * kBlock + threadIdx.x; j < n4; j += stride) {
@@ -41,22 +46,40 @@ __global__ __launch_bounds__(kBlock) void channel_stats_cl_kernel(const float4* 
       s[k] += __shfl_xor(s[k], o);
       q[k] += __shfl_xor(q[k], o);
     }
-  const int lane = (int)threadIdx.x & 63;
+  const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
   if (lane < C4) {
-    const int C = 4 * C4;
-    double* st = stats + (size_t)(blockIdx.x % kStatSlots) * 2 * C;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      atomicAdd(st + 4 * lane + k, s[k]);
-      atomicAdd(st + C + 4 * lane + k, q[k]);
+      part[wave][lane][k] = s[k];
+      part[wave][lane][4 + k] = q[k];
+    }
+  }
+  __syncthreads();
+  if (wave == 0 && lane < C4) {
+    const int C = 4 * C4;
+    double* st = stats + (size_t)blockIdx.x * 2 * C;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      double a = part[0][lane][k], b = part[0][lane][4 + k];
+#pragma unroll
+      for (int v = 1; v < kWaves; ++v) {
+        a += part[v][lane][k];
+        b += part[v][lane][4 + k];
+      }
+      st[4 * lane + k] = a;
+      st[C + 4 * lane + k] = b;
     }
   }
 }
 
-// NCDHW: one (sample, channel) plane per blockIdx.y; float4 accesses when the plane is a multiple of 4
+// NCDHW: one (sample, channel) plane per blockIdx.y; float4 accesses when the plane is a multiple of 4.
+// Slot = blockIdx.x * B + sample: every (slot, channel) is written by exactly one workgroup.
 __global__ __launch_bounds__(kBlock) void channel_stats_cf_kernel(const float* __restrict__ x, size_t plane, int C,
                                                                   double* __restrict__ stats) {
+  __shared__ double part[kWaves][2];
   const int c = (int)blockIdx.y % C;
+  const int b = (int)blockIdx.y / C;
+  const int B = (int)gridDim.y / C;
   const float* p = x + (size_t)blockIdx.y * plane;
   double s = 0.0, q = 0.0;
   const size_t stride = (size_t)gridDim.x * kBlock;
@@ -78,10 +101,21 @@ __global__ __launch_bounds__(kBlock) void channel_stats_cf_kernel(const float* _
     s += __shfl_xor(s, o);
     q += __shfl_xor(q, o);
   }
+  const int wave = (int)threadIdx.x >> 6;
   if (((int)threadIdx.x & 63) == 0) {
-    double* st = stats + (size_t)((blockIdx.x + blockIdx.y) % kStatSlots) * 2 * C;
-    atomicAdd(st + c, s);
-    atomicAdd(st + C + c, q);
+    part[wave][0] = s;
+    part[wave][1] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int v = 1; v < kWaves; ++v) {
+      s += part[v][0];
+      q += part[v][1];
+    }
+    double* st = stats + ((size_t)blockIdx.x * B + b) * 2 * C;
+    st[c] = s;
+    st[C + c] = q;
   }
 }
 
@@ -175,11 +209,20 @@ unsigned grid_cf(size_t plane, size_t planes) {
 
 }  // namespace
 
+size_t channel_stats_slots(bool channels_last, int B, int C, size_t voxels) {
+  if (channels_last) {
+    const unsigned g = grid_cl((size_t)B * voxels * (size_t)C / 4);
+    return g < kStatsClBlocks ? g : kStatsClBlocks;
+  }
+  return (size_t)grid_cf(voxels, (size_t)B * C) * (size_t)B;
+}
+
 void launch_channel_stats(const float* x, bool channels_last, int B, int C, size_t voxels, double* stats,
                           hipStream_t s) {
   if (channels_last) {
     const size_t n4 = (size_t)B * voxels * (size_t)C / 4;
-    hipLaunchKernelGGL(channel_stats_cl_kernel, dim3(grid_cl(n4)), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL(channel_stats_cl_kernel, dim3((unsigned)channel_stats_slots(true, B, C, voxels)),
+                       dim3(kBlock), 0, s,
                        reinterpret_cast<const float4*>(x), n4, C / 4, stats);
   } else {
     hipLaunchKernelGGL(channel_stats_cf_kernel, dim3(grid_cf(voxels, (size_t)B * C), (unsigned)(B * C)),

@@ -206,7 +206,23 @@ struct Geometry {
   int total;  // flattened work items (B * tiles * Dc)
 };
 
-inline int hip_status() { return hipGetLastError() == hipSuccess ? MVS_OK : MVS_ERR_HIP; }
+// Launch status of ONE entry point.  HIP's last-error slot is per thread and sticky: an error left
+// there before the call (a torch kernel, another library) belongs to whoever caused it and is
+// neither consumed nor reported here; an error that appears during the call is this call's own, is
+// consumed, and becomes MVS_ERR_HIP.  (Construct at entry, status() after the launches.)
+class LaunchCheck {
+ public:
+  LaunchCheck() : before_(hipPeekAtLastError()) {}
+  int status() const {
+    const hipError_t now = hipPeekAtLastError();
+    if (now == hipSuccess || now == before_) return MVS_OK;
+    (void)hipGetLastError();
+    return MVS_ERR_HIP;
+  }
+
+ private:
+  hipError_t before_;
+};
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 

@@ -68,6 +68,7 @@ struct Fixed {
 
 __device__ inline Fixed fixed_scale(const unsigned* __restrict__ mx, int V, int Dc, uint32_t hw) {
   const double gmax = (double)__uint_as_float(mx[0]), fmax = (double)__uint_as_float(mx[1]);
+  // mx[2] != 0 (a NaN / Inf input): any finite scale; fixed_to_float_kernel writes NaN
   // |2/V g (x - mean)| <= 4 gmax fmax / V per contribution; a gradient element collects at most
   // Dc * hw of them (tap weights of one sample sum to 1); x2 margin for fp32 rounding
   const double bound = 8.0 * gmax * fmax / (double)V * (double)Dc * (double)hw;
@@ -89,9 +90,13 @@ __device__ inline u64 to_fixed(float v, float sc) { return (u64)(long long)__bui
 __device__ inline void gadd(u64* p, u64 v) { atomicAdd(p, v); }
 
 // ---- max|x| pre-pass ---------------------------------------------------------------------------
+// out: the maximum as float bits; nonfinite: set to 1 when any element is NaN or +-Inf (the gradient
+// is then NaN, fixed_to_float_kernel: fixed point cannot carry non-finite values)
 __global__ __launch_bounds__(kBlock) void abs_max_kernel(const float* __restrict__ a, size_t n,
-                                                         unsigned* __restrict__ out) {
+                                                         unsigned* __restrict__ out,
+                                                         unsigned* __restrict__ nonfinite) {
   float m = 0.0f;
+  bool bad = false;
   const size_t stride = (size_t)gridDim.x * kBlock;
   size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
   if (((uintptr_t)a & 15u) == 0) {
@@ -100,13 +105,18 @@ __global__ __launch_bounds__(kBlock) void abs_max_kernel(const float* __restrict
     for (size_t j = i; j < n4; j += stride) {
       const float4 v = a4[j];
       m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      bad |= !(isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w));
     }
     i += n4 * 4;
   }
-  for (; i < n; i += stride) m = fmaxf(m, fabsf(a[i]));
-  // NaN compares false in fmaxf's favour of the other operand; a non-finite maximum is kept as is
+  for (; i < n; i += stride) {
+    m = fmaxf(m, fabsf(a[i]));
+    bad |= !isfinite(a[i]);
+  }
+  // fmaxf drops NaN (it returns the other operand): NaN and Inf are tracked by `bad` instead
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));   // m >= 0: uint order = float order
+  if (__builtin_amdgcn_ballot_w64(bad) != 0 && (threadIdx.x & 63) == 0) atomicOr(nonfinite, 1u);
 }
 
 // ---- per-(plane, view) footprint boxes -----------------------------------------------------------
@@ -573,8 +583,12 @@ __global__ __launch_bounds__(kBlock) void fixed_to_float_kernel(const u64* __res
                                                                const unsigned* __restrict__ mx, int V,
                                                                int Dc, uint32_t hw, float* __restrict__ out) {
   const Fixed fx = fixed_scale(mx, V, Dc, hw);
+  // a non-finite grad_cv or feature element: the float path would propagate it (NaN * weight into
+  // some taps); fixed point cannot carry it, so the whole gradient is NaN -- what torch's NaN checks
+  // and GradScaler's inf/NaN skip look for
+  const bool nonfinite = mx[2] != 0u;
   for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock)
-    out[i] = (float)((double)(long long)acc[i] * fx.to_float);
+    out[i] = nonfinite ? __builtin_nanf("") : (float)((double)(long long)acc[i] * fx.to_float);
 }
 
 template <int V, bool DET>
@@ -604,27 +618,27 @@ void launch_views(const Geometry& g, const float4* packed, const float4* refs, c
   }
 }
 
-// backward workspace: [acc u64 N*C*hw (deterministic mode)][ref partials groups*B*C4*hw float4]
-// [2 uints max]
+// backward workspace: [3 uints: max|grad_cv|, max|feat|, non-finite flag (deterministic mode)]
+// [ref partials groups*B*C4*hw float4 (2 <= V <= 8)][acc u64 N*C*hw (deterministic mode only)]
 struct BwdLayout {
-  size_t acc, ref_part, mx, total;
+  size_t mx, ref_part, acc, total;
 };
 
-BwdLayout bwd_layout(int B, int V, int C, int h, int w, int Dc) {
+BwdLayout bwd_layout(int B, int V, int C, int h, int w, int Dc, bool deterministic) {
   BwdLayout L;
   const size_t hw = (size_t)h * w;
   const size_t groups = (size_t)(Dc + kBwdKPG - 1) / kBwdKPG;
-  L.acc = 0;
-  L.ref_part = align256((size_t)B * V * C * hw * 8);
-  L.mx = L.ref_part + (V >= 2 && V <= 8 ? align256(groups * B * ((C + 3) / 4) * hw * 16) : 0);
-  L.total = L.mx + 256;
+  L.mx = 0;
+  L.ref_part = 256;
+  L.acc = L.ref_part + (V >= 2 && V <= 8 ? align256(groups * B * ((C + 3) / 4) * hw * 16) : 0);
+  L.total = L.acc + (deterministic ? align256((size_t)B * V * C * hw * 8) : 0);
   return L;
 }
 
 }  // namespace
 
-size_t cost_volume_bwd_workspace_bytes(int B, int V, int C, int h, int w, int Dc) {
-  return bwd_layout(B, V, C, h, w, Dc).total;
+size_t cost_volume_bwd_workspace_bytes(int B, int V, int C, int h, int w, int Dc, bool deterministic) {
+  return bwd_layout(B, V, C, h, w, Dc, deterministic).total;
 }
 
 int launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* fwd_ws,
@@ -634,17 +648,17 @@ int launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* fw
   if (!deterministic || g.V == 1)   // V == 1: the variance of one view is identically 0, so is its gradient
     if (hipMemsetAsync(grad_feat, 0, n_feat * sizeof(float), s) != hipSuccess) return MVS_ERR_HIP;
   if (g.V == 1) return MVS_OK;
-  const BwdLayout L = bwd_layout(g.B, g.V, g.C, g.h, g.w, g.Dc);
+  const BwdLayout L = bwd_layout(g.B, g.V, g.C, g.h, g.w, g.Dc, deterministic);
   char* ws = static_cast<char*>(bwd_ws);
   u64* acc = reinterpret_cast<u64*>(ws + L.acc);
   float4* ref_part = reinterpret_cast<float4*>(ws + L.ref_part);
   unsigned* mx = reinterpret_cast<unsigned*>(ws + L.mx);
   if (deterministic) {
     if (hipMemsetAsync(acc, 0, n_feat * 8, s) != hipSuccess) return MVS_ERR_HIP;
-    if (hipMemsetAsync(mx, 0, 8, s) != hipSuccess) return MVS_ERR_HIP;
+    if (hipMemsetAsync(mx, 0, 12, s) != hipSuccess) return MVS_ERR_HIP;
     const size_t n_gcv = (size_t)g.B * g.C * g.Dc * g.h * g.w;
-    hipLaunchKernelGGL(abs_max_kernel, dim3(2048), dim3(kBlock), 0, s, grad_cv, n_gcv, mx);
-    hipLaunchKernelGGL(abs_max_kernel, dim3(256), dim3(kBlock), 0, s, feat, n_feat, mx + 1);
+    hipLaunchKernelGGL(abs_max_kernel, dim3(2048), dim3(kBlock), 0, s, grad_cv, n_gcv, mx, mx + 2);
+    hipLaunchKernelGGL(abs_max_kernel, dim3(256), dim3(kBlock), 0, s, feat, n_feat, mx + 1, mx + 2);
   }
   const float* smp = fwd_ws;
   if (g.V <= 8) {
@@ -675,7 +689,7 @@ int launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* fw
     hipLaunchKernelGGL(fixed_to_float_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(kBlock), 0,
                        s, acc, n_feat, mx, g.V, g.Dc, (uint32_t)((size_t)g.h * g.w), grad_feat);
   }
-  return hip_status();
+  return MVS_OK;
 }
 
 }  // namespace mvs

@@ -5,7 +5,7 @@
 // Here both are one pass: every view is sampled and the two-pass variance is formed in registers,
 // so the B*V x C x D x h x w warped volume never exists; cv[B][C][D][h][w] is written once.
 //
-// Structure of cost_volume_tile_kernel (V = 2..8 views):
+// Structure of cost_volume_staged_kernel (V = 2..8 views):
 //   * features are first packed channel-quad-last, packed[N][C/4][h][w][4] (one float4 per pixel
 //     and 4-channel chunk), so one LDS slot / one 16-B load carries 4 channels of a tap;
 //   * a 256-thread workgroup owns a 32 x 8 pixel tile of one sample and a group of `pg` depth
@@ -232,7 +232,9 @@ __device__ inline int wave_min_to_lane63(int x) {
   return x;
 }
 
-// Workgroup-wide min of NV ints; every thread gets the result as a wave-uniform value.
+// Workgroup-wide min of NV ints; every thread gets the result as a wave-uniform value.  The scratch
+// may alias LDS that the caller writes next (the staged kernel's staging slots): the closing barrier
+// orders every wave's scratch reads before any such write.
 template <int NV>
 __device__ inline void block_min(int (&v)[NV], int* scratch /* >= 4 * NV ints of LDS */) {
   const int wave = threadIdx.x >> 6;
@@ -249,6 +251,7 @@ __device__ inline void block_min(int (&v)[NV], int* scratch /* >= 4 * NV ints of
     for (int q = 1; q < kBlock / 64; ++q) x = min(x, scratch[q * NV + k]);
     v[k] = __builtin_amdgcn_readfirstlane(x);
   }
+  __syncthreads();   // scratch reads done before the caller's next LDS writes (WAR)
 }
 
 // Cost-volume stores through a buffer descriptor per (channel, plane group): planes past the group's
@@ -300,9 +303,11 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   constexpr int NS = V - 1;
   constexpr int SLOTS = staged_slots<V>();
   __shared__ f4v lds[SLOTS];
-  // block_min's scratch lives in the last slots of the staging area: it is read before the first
-  // chunk's barrier, and staging writes only follow that barrier (the zero area is at the front).
-  // Keeping the whole workgroup at exactly SLOTS * 16 B (40 KB at V = 3) fits 4 workgroups per CU.
+  // block_min's scratch lives in the last slots of the staging area (which include the dummy slot
+  // SLOTS - 1 and, near the budget, real staging slots): block_min ends with a barrier after its
+  // scratch reads, so the zero-area writes and stage(0) that follow cannot overwrite scratch another
+  // wave still reads.  Keeping the whole workgroup at exactly SLOTS * 16 B (40 KB at V = 3) fits 4
+  // workgroups per CU.
   int* scratch = reinterpret_cast<int*>(&lds[SLOTS - (4 * 4 * NS + 3) / 4]);
 
   const int wk = xcd_work_id(blockIdx.x, total);

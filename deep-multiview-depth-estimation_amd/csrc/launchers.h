@@ -40,7 +40,7 @@ void launch_variance(const float* warped, int B, int V, size_t M, float* cv, hip
 // cost_volume_bwd.hip: grad_feat (overwritten) from grad_cv, the forward's workspace (sampling
 // matrices + packed features + resampled reference views) and a backward workspace of
 // cost_volume_bwd_workspace_bytes(); deterministic = 64-bit fixed-point accumulation throughout
-size_t cost_volume_bwd_workspace_bytes(int B, int V, int C, int h, int w, int Dc);
+size_t cost_volume_bwd_workspace_bytes(int B, int V, int C, int h, int w, int Dc, bool deterministic);
 int launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* fwd_ws,
                            const float* grad_cv, void* bwd_ws, float* grad_feat, bool deterministic,
                            hipStream_t s);
@@ -86,6 +86,8 @@ int launch_conv3d_region(int mode, bool out_cf, bool in_c4, const float* x, cons
 
 // channel_ops.hip: train-mode BatchNorm pieces -- per-channel float64 sums into
 // stats[slot][2][C] (64 slots) and y = relu(BN(x)) [+ relu(BN'(r))], channels-last or NCDHW
+// slots (workgroups) of launch_channel_stats; stats is [slots][2][C], every entry written once
+size_t channel_stats_slots(bool channels_last, int B, int C, size_t voxels);
 void launch_channel_stats(const float* x, bool channels_last, int B, int C, size_t voxels, double* stats,
                           hipStream_t s);
 void launch_bn_relu(const float* x, bool channels_last, int B, int C, size_t voxels, const float* sc,

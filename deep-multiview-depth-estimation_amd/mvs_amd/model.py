@@ -9,8 +9,11 @@ checkpoints load unchanged, and ``forward`` has the reference signature:
 
 What changes is the hot path: ``model.py:177-181`` (per-plane kornia warp loop + torch.cat growth
 + 6-D variance) becomes ONE fused HIP kernel (``costvolume.warp_and_assemble_cost_volume``) and
-``model.py:187`` the HIP soft-argmin.  The 2-D/3-D convolutions stay on PyTorch-ROCm (MIOpen),
-as the north star prescribes.  Like the reference (``model.py:164-166``) the instance attribute
+``model.py:187`` the HIP soft-argmin.  In fp32 no-grad inference the 2-D encoder / refinement
+convolutions and the 3-D regulariser's layers run on hand-written HIP kernels too (direct 2-D convs
+with fused BN + ReLU, MFMA region convs on the live regions); autograd,
+other dtypes and the full-volume reference leg (``forward_full``) use PyTorch-ROCm (MIOpen).  Like
+the reference (``model.py:164-166``) the instance attribute
 ``parameters`` is a LIST of tensors (``train.py:160`` passes it to Adam); use
 ``named_parameters()`` / ``state_dict()`` for module-generic code.
 """

@@ -174,11 +174,11 @@ def cost_volume_backward(feat: torch.Tensor, workspace: torch.Tensor, grad_cv: t
     grad_cv = grad_cv.to(_F32).contiguous()
     n, c, h, w = feat.shape
     grad_feat = torch.empty_like(feat)
-    nb = lib.mvs_cost_volume_bwd_workspace_bytes(batch_size, n_views, c, h, w, d_count)
+    flags = _lib.MVS_BWD_DETERMINISTIC if deterministic else 0
+    nb = lib.mvs_cost_volume_bwd_workspace_bytes(batch_size, n_views, c, h, w, d_count, flags)
     bws = torch.empty((max(nb, 8) + 7) // 8, device=feat.device, dtype=torch.int64)
     st = lib.mvs_cost_volume_bwd(_lib.ptr(feat), _lib.ptr(workspace), _lib.ptr(grad_cv),
-                                 batch_size, n_views, c, h, w, d_count,
-                                 _lib.MVS_BWD_DETERMINISTIC if deterministic else 0, _lib.ptr(bws),
+                                 batch_size, n_views, c, h, w, d_count, flags, _lib.ptr(bws),
                                  _lib.ptr(grad_feat), _lib.stream_handle(feat.device))
     _lib.check(st, "mvs_cost_volume_bwd")
     return grad_feat
@@ -376,9 +376,10 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Te
     if wino_z and cout != 8:
         raise ValueError("wino_z needs c_out = 8")
     if wino_z:
-        w = derived("k3wz", (weight,), lambda wt: _wino_z_weight(wt).to(device=x.device))
+        w = derived("k3wz", (weight,), lambda wt: _wino_z_weight(wt).to(device=x.device), x.device)
     else:
-        w = derived("k3", (weight,), lambda wt: wt.to(device=x.device, dtype=_F32).permute(1, 2, 3, 4, 0).contiguous())
+        w = derived("k3", (weight,), lambda wt: wt.to(device=x.device, dtype=_F32).permute(1, 2, 3, 4, 0).contiguous(),
+                    x.device)
     bn = [t if t is None else t.to(device=x.device, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
     if any(t is None for t in bn) and not all(t is None for t in bn):
         raise ValueError("bn_scale, bn_shift and bn_mean go together")
@@ -438,7 +439,8 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int, bn_scale: Optiona
     cout, k = weight.shape[0], weight.shape[2]
     x = x.to(_F32).contiguous()
     # the kernel reads weight[c_in][k][k][c_out] (pairs of output channels per 8-byte scalar load)
-    w = derived("conv2d", (weight,), lambda wt: wt.to(device=x.device, dtype=_F32).permute(1, 2, 3, 0).contiguous())
+    w = derived("conv2d", (weight,), lambda wt: wt.to(device=x.device, dtype=_F32).permute(1, 2, 3, 0).contiguous(),
+                x.device)
     bn = [t if t is None else t.to(device=x.device, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
     if any(t is None for t in bn) and not all(t is None for t in bn):
         raise ValueError("bn_scale, bn_shift and bn_mean go together")
@@ -488,7 +490,8 @@ def deconv3d_k3s2(x: torch.Tensor, origin: list[int], weight: torch.Tensor, out_
         flags = _lib.MVS_LAYOUT_CHANNELS_LAST
     else:   # tap-major weight[c_in][27][8]: the NCDHW kernel's packed-FMA form
         w = derived("deconv_taps", (weight,),
-                    lambda wt: wt.to(device=x.device, dtype=_F32).reshape(cin, 8, 27).transpose(1, 2).contiguous())
+                    lambda wt: wt.to(device=x.device, dtype=_F32).reshape(cin, 8, 27).transpose(1, 2).contiguous(),
+                    x.device)
         flags = _lib.MVS_DECONV_WEIGHT_TAPS
     d, h, wd = out_dims
     f = lambda t: None if t is None else t.to(device=x.device, dtype=_F32).contiguous()
@@ -517,25 +520,40 @@ def _(x, origin, weight, out_dims, pad, bn_scale, bn_shift, bn_mean, residual, x
 CONV_S1, CONV_S2, CONV_T2 = _lib.MVS_CONV_S1, _lib.MVS_CONV_S2, _lib.MVS_CONV_T2
 
 
-_DERIVED = {}
+_DERIVED = {}   # (tag, id(t)...) -> (weak refs, state, out): ONE entry per (tag, tensors)
 
 
-def derived(tag, tensors, fn):
+def _evict(key):
+    return lambda _ref: _DERIVED.pop(key, None)
+
+
+def derived(tag, tensors, fn, device=None):
     """fn(*tensors), cached for inference: a kernel-layout weight or an eval-BN scale is formed once
-    per parameter state instead of by a few small device ops on every forward.  The key is each
-    tensor's identity, storage and in-place version counter (optimizer steps, load_state_dict and
-    running-statistic updates all bump it); a weak reference guards against a freed tensor's id
-    being reused.  Never cached while autograd records (the result must carry the graph)."""
+    per parameter state instead of by a few small device ops on every forward.
+
+    One entry per (tag, tensor identities), holding only the LATEST state: the tensors' storage and
+    in-place version counters (optimizer steps, load_state_dict and running-statistic updates all bump
+    them) and the target ``device`` the result is formed for (a CPU weight used with inputs on two
+    GPUs gets one result per call site's device, recomputed on a device change).  A state change
+    replaces the entry, so stale results are dropped instead of accumulating; the entry dies with its
+    tensors (weak-reference callbacks).  Writes through ``param.data`` do not bump the version counter
+    (``.data`` is a separate autograd view); code that updates weights that way must call
+    ``clear_derived()``.  Never cached while autograd records (the result must carry the graph)."""
     if torch.is_grad_enabled() and any(t.requires_grad for t in tensors):
         return fn(*tensors)
-    key = (tag,) + tuple((id(t), t.data_ptr(), t._version) for t in tensors)
+    key = (tag,) + tuple(id(t) for t in tensors)
+    state = tuple((t.data_ptr(), t._version) for t in tensors) + (None if device is None else str(device),)
     hit = _DERIVED.get(key)
-    if hit is not None and all(r() is t for r, t in zip(hit[0], tensors)):
-        return hit[1]
+    if hit is not None and all(r() is t for r, t in zip(hit[0], tensors)) and hit[1] == state:
+        return hit[2]
     out = fn(*tensors)
-    if len(_DERIVED) < 4096 or key in _DERIVED:   # bounded; a full cache stops caching (entries in
-        _DERIVED[key] = ([weakref.ref(t) for t in tensors], out)   # use on other streams stay alive)
+    _DERIVED[key] = ([weakref.ref(t, _evict(key)) for t in tensors], state, out)
     return out
+
+
+def clear_derived():
+    """Drop every cached derived weight (after weight writes the version counters do not see)."""
+    _DERIVED.clear()
 
 
 def region_weight(module):
@@ -601,15 +619,17 @@ def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, 
 # ----------------------------------------------------------------------------------------------
 def channel_stats(x: torch.Tensor, channels_last: bool):
     """Per-channel (sum, sum of squares) of x in float64 [C] each: channels on the last dim
-    (channels_last) or on dim 1 (NCDHW).  Inference only."""
+    (channels_last) or on dim 1 (NCDHW).  Slot-owned partial sums (no atomics) added in a fixed
+    order: bit-identical run to run.  Inference only."""
     _require_gpu(x, "x")
     lib = _lib.load()
     x = x.to(_F32).contiguous()
     c = x.shape[-1] if channels_last else x.shape[1]
     vox = x.numel() // (x.shape[0] * c)
-    st = torch.zeros((_lib.MVS_STATS_SLOTS, 2, c), device=x.device, dtype=torch.float64)
-    rc = lib.mvs_channel_stats(_lib.ptr(x), _lib.MVS_LAYOUT_CHANNELS_LAST if channels_last else 0, x.shape[0], c,
-                               vox, _lib.ptr(st), _lib.stream_handle(x.device))
+    layout = _lib.MVS_LAYOUT_CHANNELS_LAST if channels_last else 0
+    slots = lib.mvs_channel_stats_slots(layout, x.shape[0], c, vox)
+    st = torch.empty((max(slots, 1), 2, c), device=x.device, dtype=torch.float64)
+    rc = lib.mvs_channel_stats(_lib.ptr(x), layout, x.shape[0], c, vox, _lib.ptr(st), _lib.stream_handle(x.device))
     _lib.check(rc, "mvs_channel_stats")
     s = st.sum(0)
     return s[0], s[1]

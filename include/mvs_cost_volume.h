@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 5
+#define MVS_ABI_VERSION 6
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -141,20 +141,21 @@ int mvs_homography_warp_fwd(const float* feat, const float* K, const float* R, c
 int mvs_assemble_cost_volume_fwd(const float* warped, int batch_size, int n_views,
                                  int channels, int d, int h, int w, float* cv_out, void* stream);
 
-/* Bytes of the workspace mvs_cost_volume_bwd needs (64-bit accumulators for every feature element,
- * the reference view's per-plane-group partial sums, two scalars). */
-size_t mvs_cost_volume_bwd_workspace_bytes(int batch_size, int n_views, int channels, int h, int w,
-                                           int d_count);
-
 /* mvs_cost_volume_bwd flags */
 #define MVS_BWD_DETERMINISTIC 1
+
+/* Bytes of the workspace mvs_cost_volume_bwd needs with these flags: three scalars, the reference
+ * view's per-plane-group partial sums, and (flags = MVS_BWD_DETERMINISTIC only) 64-bit accumulators
+ * for every feature element.  0 for invalid arguments or unknown flags. */
+size_t mvs_cost_volume_bwd_workspace_bytes(int batch_size, int n_views, int channels, int h, int w,
+                                           int d_count, int flags);
 
 /*
  * Backward of the fused op w.r.t. the features (autograd of costvolume.py:14 + grid_sample,
  * exercised by train.py:103): grad_feat[N][C][h][w] is OVERWRITTEN with d<cv, grad_cv>/d feat.
  * `workspace` is the forward call's workspace (same geometry, not modified since): its sampling
  * matrices, packed features and resampled reference views are reused.  `bwd_workspace` holds
- * mvs_cost_volume_bwd_workspace_bytes(...) bytes.
+ * mvs_cost_volume_bwd_workspace_bytes(..., flags) bytes for the same flags.
  * flags = 0: per-tile partial sums are accumulated in fp64 on chip and added to grad_feat with
  *   fp32 atomics -- the summation order (and so the last bits) may vary between runs, like
  *   torch's grid_sample backward on GPU.
@@ -162,7 +163,8 @@ size_t mvs_cost_volume_bwd_workspace_bytes(int batch_size, int n_views, int chan
  *   so the result is bit-identical across runs whatever the scheduling; resolution
  *   2^-61 * d_count*h*w*8*max|grad_cv|*max|feat|/n_views (about 1e-12 of the largest possible
  *   contribution at BASELINE cfg 2); one extra pass reads grad_cv for its maximum.
- * Non-finite inputs give unspecified results in deterministic mode.
+ *   A NaN or Inf anywhere in grad_cv or feat makes every grad_feat element NaN in this mode (fixed
+ *   point cannot carry them; the default mode propagates them through the taps they reach).
  */
 int mvs_cost_volume_bwd(const float* feat, const float* workspace, const float* grad_cv,
                         int batch_size, int n_views, int channels, int h, int w, int d_count,
@@ -295,11 +297,14 @@ int mvs_softmax_depth_fwd(const float* x, int batch, int d_count, int h, int w, 
 
 /* ---- train-mode BatchNorm of the regulariser (model.py:101-121 with every BatchNorm3d in training
  * mode: test.py:53,61 runs `model.train()` under no_grad; CostVolumeReg.forward_live_train) ---- */
-#define MVS_STATS_SLOTS 64
+/* Number of partial-sum slots mvs_channel_stats writes for this tensor (0 for invalid arguments). */
+size_t mvs_channel_stats_slots(int layout, int batch, int channels, long long voxels);
 
-/* Per-channel batch sums of x: stats[slot][0][c] += sum of x over channel c, stats[slot][1][c] +=
- * sum of x^2, in float64, over MVS_STATS_SLOTS slots (the caller zeroes stats, then adds the slots):
- * the inputs of BatchNorm3d's batch mean and biased variance.  layout: MVS_LAYOUT_CHANNELS_LAST
+/* Per-channel batch sums of x in float64, as partial sums: stats[slot][0][c] = a partial sum of x over
+ * channel c, stats[slot][1][c] = of x^2, for slot < mvs_channel_stats_slots(...) -- every entry is
+ * WRITTEN (no zeroing needed), each partial summed in a fixed order without atomics; the caller adds
+ * the slots (in a fixed order: results are then bit-identical run to run).  The inputs of
+ * BatchNorm3d's batch mean and biased variance.  layout: MVS_LAYOUT_CHANNELS_LAST
  * (x[batch][voxels][channels], channels / 4 a power of two <= 64, 16-byte aligned) or 0 (NCDHW
  * x[batch][channels][voxels]). */
 int mvs_channel_stats(const float* x, int layout, int batch, int channels, long long voxels, double* stats,

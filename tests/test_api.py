@@ -116,6 +116,38 @@ def test_derived_parameter_cache_follows_parameter_state():
     assert len(calls) == 4   # requires_grad under grad mode: never cached
 
 
+def test_derived_cache_keeps_one_entry_per_tensor_and_device():
+    """ops.derived holds only the latest state per (tag, tensors): version bumps replace the entry
+    (no growth over optimizer steps), a different target device is a different state, and the entry
+    is evicted with its tensor."""
+    import gc
+    import torch
+    from mvs_amd import ops
+    w = torch.randn(5)
+    calls = []
+
+    def f(t):
+        calls.append(1)
+        return t + 1.0
+
+    with torch.no_grad():
+        n0 = len(ops._DERIVED)
+        for _ in range(50):
+            w.mul_(1.0)
+            ops.derived("dev", (w,), f, "cuda:0")
+        assert len(ops._DERIVED) == n0 + 1 and len(calls) == 50
+        ops.derived("dev", (w,), f, "cuda:0")
+        assert len(calls) == 50
+        ops.derived("dev", (w,), f, "cuda:1")          # another target device: recomputed
+        ops.derived("dev", (w,), f, "cuda:0")          # and back
+        assert len(calls) == 52 and len(ops._DERIVED) == n0 + 1
+        del w
+        gc.collect()
+        assert len(ops._DERIVED) == n0                  # evicted with its tensor
+        ops.clear_derived()
+        assert not ops._DERIVED
+
+
 def test_select_images_matches_indexing():
     """model._select_images: a strided view for the reference indices 0, V, 2V, ... (no host sync on
     the GPU), plain indexing otherwise -- the same images either way."""

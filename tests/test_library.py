@@ -23,7 +23,7 @@ def _declared():
 def test_header_declares_the_abi():
     names = _declared()
     assert "mvs_cost_volume_fwd" in names and "mvs_cost_volume_bwd" in names
-    assert len(names) == 23, names
+    assert len(names) == 24, names
 
 
 def test_library_exports_every_declared_symbol():
@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from mvs_amd import _lib
     lib = _lib.load()
-    assert lib.mvs_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.mvs_abi_version() == _lib.ABI_VERSION == 6
     assert lib.mvs_status_string(0) == b"ok"
     assert lib.mvs_status_string(-2).startswith(b"n_views")
     assert lib.mvs_sampling_workspace_bytes(12, 192) == 12 * 192 * 9 * 4
@@ -75,9 +75,22 @@ def test_invalid_arguments_rejected_before_any_launch():
     assert lib.mvs_cost_volume_bwd(fake, fake, fake, 1, 3, 32, 128, 160, 48, 0, null, fake, null) == -1
     assert lib.mvs_cost_volume_bwd(fake, fake, fake, 1, 17, 32, 128, 160, 48, 0, fake, fake, null) == -2
     assert lib.mvs_cost_volume_bwd(fake, fake, fake, 1, 3, 32, 128, 160, 48, 2, fake, fake, null) == -1
-    assert lib.mvs_cost_volume_bwd_workspace_bytes(1, 3, 32, 128, 160, 0) == 0
-    # 64-bit accumulators for every feature element + reference-view partials + scalars
-    assert lib.mvs_cost_volume_bwd_workspace_bytes(4, 3, 32, 128, 160, 192) >= 12 * 32 * 128 * 160 * 8
+    assert lib.mvs_cost_volume_bwd_workspace_bytes(1, 3, 32, 128, 160, 0, 0) == 0
+    assert lib.mvs_cost_volume_bwd_workspace_bytes(1, 3, 32, 128, 160, 48, 2) == 0      # unknown flag
+    # deterministic mode: 64-bit accumulators for every feature element + reference-view partials +
+    # scalars; the default mode needs no accumulators
+    det = lib.mvs_cost_volume_bwd_workspace_bytes(4, 3, 32, 128, 160, 192, 1)
+    dflt = lib.mvs_cost_volume_bwd_workspace_bytes(4, 3, 32, 128, 160, 192, 0)
+    assert det - dflt >= 12 * 32 * 128 * 160 * 8
+    # the channel-quad store (16 B per voxel quad, up to 8 planes per descriptor) wraps 32-bit offsets
+    # at hw >= 2^25: C=4, V=2, 6000x6000 passes every other bound but must be refused, not dropped
+    c4_out = ctypes.c_void_p(1 << 20)
+    assert lib.mvs_cost_volume_fwd_c4(fake, fake, fake, fake, fake, fake, 1, 2, 4, 6000, 6000, 0, 4, 25.0,
+                                      fake, c4_out, null, None, None) == -3
+    # deterministic partial-sum slots of the BN statistics (every slot written, none zeroed)
+    assert lib.mvs_channel_stats_slots(0, 2, 8, 1000) >= 2
+    assert lib.mvs_channel_stats_slots(1, 2, 16, 1000) >= 1
+    assert lib.mvs_channel_stats_slots(2, 2, 16, 1000) == 0 and lib.mvs_channel_stats_slots(0, 0, 8, 10) == 0
     # train-mode BN pieces: channels-last needs 4 | C with C / 4 a power of two, and 16-B alignment
     assert lib.mvs_channel_stats(fake, 1, 2, 24, 100, fake, null) == -1
     assert lib.mvs_channel_stats(ctypes.c_void_p(20), 1, 2, 16, 100, fake, null) == -1
