@@ -87,6 +87,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-planes", type=int, default=None, help="planes for the CPU sample")
     ap.add_argument("--kernel-only", action="store_true", help="skip the end-to-end forward")
+    ap.add_argument("--no-extra", action="store_true", help="skip the cfg 3/5 end-to-end and train-step fields")
     ap.add_argument("--conv-search", choices=("on", "off"), default="off",
                     help="torch.backends.cudnn.benchmark (MIOpen find) for the regulariser convs")
     return ap.parse_args()
@@ -245,6 +246,91 @@ def kernel_configs(device, iters):
                      "alg_bytes": alg, "GBps": gbs, "frac": gbs / HBM_PEAK_GBS,
                      "store": "channel-quad" if quads else "NCDHW"}
         torch.cuda.empty_cache()
+    return out
+
+
+E2E_CFGS = {   # BASELINE.json configs[2] and configs[4] end to end: (B, V, D, image H, image W)
+    "cfg3": (8, 5, 192, 512, 640),
+    "cfg5": (1, 3, 256, 1184, 1600),
+}
+
+
+def e2e_configs(device, steps):
+    """MVSNet.forward (BN eval, no_grad, the live-region HIP path of `value`) at cfg 3 (5 views, B=8)
+    and cfg 5 (1600x1184 full-resolution images, D=256, B=1): ms/step and depth maps/s on this GPU,
+    timed like the headline (warm-up, then `steps` steps between device synchronisations)."""
+    out = {}
+    for name, (B, V, D, H, W) in E2E_CFGS.items():
+        log("e2e %s: B=%d V=%d D=%d %dx%d" % (name, B, V, D, W, H))
+        net = build_model(D, H, W, device)
+        inputs = make_inputs(B, V, H, W, 0, device)
+        with torch.no_grad():
+            for _ in range(2):
+                net(*inputs, B, V)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                net(*inputs, B, V)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / steps
+        out[name] = {"B": B, "V": V, "planes": D, "image_hw": [H, W], "feature_hw": [H // 4, W // 4],
+                     "ms_per_step": 1000.0 * dt, "depth_maps_per_s": B / dt, "steps": steps}
+        del net, inputs
+        torch.cuda.empty_cache()
+    return out
+
+
+def masked_mae_loss(gt, initial, refined):
+    """The reference objective (scripts/loss.py:4-41): per sample the mean absolute error of the
+    initial and the refined depth over the valid (gt != 0) pixels, summed over both and the batch."""
+    mask = (gt != 0).to(gt.dtype)
+    valid = mask.sum((1, 2, 3))
+    l0 = (mask * (gt - initial).abs()).sum((1, 2, 3)) / valid
+    l1 = (mask * (gt - refined).abs()).sum((1, 2, 3)) / valid
+    return (l0 + l1).sum()
+
+
+def train_step_bench(B, V, D, H, W, device, steps):
+    """One train.py:86-104 step on the drop-in at the headline workload: model.train(),
+    optimizer.zero_grad, MVSNet.forward with autograd (BN batch statistics), the reference loss,
+    loss.backward() (HIP cost-volume backward + MIOpen for the convolutions), Adam.step over the
+    reference's `model.parameters` list (train.py:160).  Synthetic ground truth: depths uniform over
+    the plane range, 10 % invalid (0) pixels."""
+    log("train step: B=%d V=%d D=%d %dx%d" % (B, V, D, W, H))
+    net = build_model(D, H, W, device).train()
+    opt = torch.optim.Adam(net.parameters, lr=1e-3)
+    img, K, R, T, d_min, d_int = make_inputs(B, V, H, W, 0, device)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    gt = 425.0 + 25.0 * D * torch.rand(B, 1, H // 4, W // 4, generator=g)
+    gt[torch.rand(B, 1, H // 4, W // 4, generator=g) < 0.1] = 0.0
+    gt = gt.to(device)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        ini, ref = net(img, K, R, T, d_min, d_int, B, V)
+        loss = masked_mae_loss(gt, ini, ref)
+        loss.backward()
+        opt.step()
+        return loss
+
+    t0 = time.perf_counter()
+    step()
+    torch.cuda.synchronize()
+    first = time.perf_counter() - t0
+    n = steps if first < 20.0 else 1     # a very slow first step (solver search) is reported as is
+    t0 = time.perf_counter()
+    for _ in range(n):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / n
+    out = {"B": B, "V": V, "planes": D, "image_hw": [H, W], "ms_per_step": 1000.0 * dt,
+           "depth_maps_per_s": B / dt, "steps": n, "first_step_ms": 1000.0 * first,
+           "loss": float(loss.item()), "peak_mem_GB": torch.cuda.max_memory_allocated(device) / 1e9,
+           "note": "forward (autograd, train-mode BN, full-volume regulariser on MIOpen) + loss.py "
+                   "masked MAE + backward (HIP mvs::cost_volume_backward, MIOpen conv backward) + "
+                   "Adam.step"}
+    del net, opt
+    torch.cuda.empty_cache()
     return out
 
 
@@ -516,6 +602,9 @@ def main():
     if args.mode == "samples":
         log("timing the fused kernel at cfg 3/4/5")
         out["kernel_configs"] = kernel_configs(device, max(5, args.kernel_iters // 2))
+        if not args.kernel_only and not args.no_extra:
+            out["e2e_configs"] = e2e_configs(device, max(3, min(args.steps, 10)))
+            out["train_step"] = train_step_bench(B, V, D, H, W, device, 3)
     # opt-in bf16 cost volume: informational, not the headline (reduced precision)
     _, bf_op_ms, bf_alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count, bf16=True)
     out["bf16_cv_opt_in"] = {"op_ms": bf_op_ms, "alg_bytes_per_launch": bf_alg,

@@ -10,10 +10,19 @@ runs the regulariser, soft-argmin and refinement for it:
   * owner-targeted exchange (``exchange_to_owners``): every rank sends its slab of sample b only
     to b's owner -- a gather to the owner when B < P (cfg 4: B = 1, only rank 0 receives), an
     all-to-all by sample when B >= P; nothing goes to ranks that would discard it;
-  * the owner receives straight into the final [B_own, C, D, h, w] layout: for every (sample,
-    channel) a source rank's slab is one contiguous block of D/P planes of the destination, so
-    each block is its own point-to-point receive (one grouped ``batch_isend_irecv``, RCCL over
-    xGMI when the process group is ``nccl``); only the rank's own slab is copied locally.
+  * ONE message per (sample, peer): a source rank sends its whole [C, D/P, h, w] slab of the
+    sample (contiguous) and the owner receives it into a staging buffer [P, C, D/P, h, w]; one
+    strided device copy then interleaves the P slabs into the final [C, D, h, w] layout (the
+    regulariser's NCDHW input, where a slab is C separate blocks).  All messages of a step are one
+    grouped ``batch_isend_irecv`` (RCCL over xGMI when the process group is ``nccl``): at cfg 4
+    (B = 1, P = 8) rank 0 posts 7 receives of 84 MB instead of 7 x 32 per-channel ones.
+
+Expected cfg 4 step (B = 1, D = 256, 8 ranks): each rank's 32-plane shard kernel
+~0.05 ms, the exchange ~0.55 ms (the owner receives 7 x 84 MB, one slab per xGMI link in
+parallel: 84 MB / 153 GB/s), the interleaving copy ~0.15 ms (671 MB read + written),
+then the owner's D = 256 regulariser ~2 ms -- the other 7 GPUs idle through it, so at B = 1 the
+D-sharded job is no faster than one GPU computing the whole volume: the cost volume is ~7 % of the
+step, the regulariser (which cannot be D-sharded exactly) the rest.
 
 Eval-mode inference only: BatchNorm in train mode would normalise with the statistics of the
 owned samples instead of the whole batch (model.py:184), and the point-to-point exchange carries
@@ -40,58 +49,74 @@ def owned_samples(batch_size, world, rank):
     return [b for b in range(batch_size) if b % world == rank]
 
 
+def exchange_plan(batch_size, world, rank):
+    """The point-to-point messages of exchange_to_owners on this rank: a list of
+    ("send" | "recv", peer, sample), one per (sample, peer) pair that must move -- a sample's slab
+    goes from every non-owner rank to its owner and nowhere else."""
+    plan = []
+    for b in range(batch_size):
+        owner = b % world
+        if owner != rank:
+            plan.append(("send", owner, b))
+        else:
+            plan += [("recv", src, b) for src in range(world) if src != rank]
+    return plan
+
+
 def exchange_to_owners(slab, world, rank, group=None):
     """Owner-targeted exchange of cost-volume D-slabs.
 
     ``slab`` is this rank's [B, C, Dl, h, w] (planes [rank*Dl, (rank+1)*Dl) of every sample).
     Returns the full-D volume [len(owned_samples), C, world*Dl, h, w] of the samples this rank
-    owns (an empty tensor when it owns none).  Every rank must call it (collective)."""
+    owns (an empty tensor when it owns none).  Every rank must call it (collective).  One message
+    per (sample, peer) (``exchange_plan``), received into a per-sample staging buffer and
+    interleaved into the NCDHW result by one strided copy per owned sample."""
     slab = slab.contiguous()
     b_all, c, dl, h, w = slab.shape
     mine = owned_samples(b_all, world, rank)
     out = slab.new_empty((len(mine), c, world * dl, h, w))
-    for i, b in enumerate(mine):   # own planes: the one local copy
-        out[i, :, rank * dl:(rank + 1) * dl].copy_(slab[b])
     if world == 1:
+        for i, b in enumerate(mine):
+            out[i].copy_(slab[b])
         return out
+    stage = {b: slab.new_empty((world, c, dl, h, w)) for b in mine}
     ops = []
-    for b in range(b_all):
-        owner = b % world
-        if owner != rank:
-            ops += [dist.P2POp(dist.isend, slab[b, ch], owner, group) for ch in range(c)]
+    for kind, peer, b in exchange_plan(b_all, world, rank):
+        if kind == "send":
+            ops.append(dist.P2POp(dist.isend, slab[b], peer, group))
         else:
-            i = mine.index(b)
-            for src in range(world):
-                if src != rank:
-                    ops += [dist.P2POp(dist.irecv, out[i, ch, src * dl:(src + 1) * dl], src, group)
-                            for ch in range(c)]
+            ops.append(dist.P2POp(dist.irecv, stage[b][peer], peer, group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
+    for i, b in enumerate(mine):
+        stage[b][rank].copy_(slab[b])
+        # [P, C, Dl, h, w] -> [C, P*Dl, h, w]: slab p holds planes [p*Dl, (p+1)*Dl) of every channel
+        out[i].view(c, world, dl, h, w).copy_(stage[b].transpose(0, 1))
     return out
 
 
 def gather_depth_slabs(slab, world, group=None):
     """All-gather [B, C, Dl, h, w] slabs (rank order = plane order) into [B, C, world*Dl, h, w] on
     every rank (every rank then holds every sample: use exchange_to_owners when only the owner
-    needs a sample's volume)."""
+    needs a sample's volume).  One message per peer (the whole contiguous slab), staged and
+    interleaved by one strided copy."""
     if world == 1:
         return slab
     slab = slab.contiguous()
     b, c, dl, h, w = slab.shape
-    out = slab.new_empty((b, c, world * dl, h, w))
-    ops = []
     rank = dist.get_rank(group)
-    out[:, :, rank * dl:(rank + 1) * dl].copy_(slab)
+    stage = slab.new_empty((world, b, c, dl, h, w))
+    ops = []
     for peer in range(world):
-        if peer == rank:
-            continue
-        for bb in range(b):
-            for ch in range(c):
-                ops.append(dist.P2POp(dist.isend, slab[bb, ch], peer, group))
-                ops.append(dist.P2POp(dist.irecv, out[bb, ch, peer * dl:(peer + 1) * dl], peer, group))
+        if peer != rank:
+            ops.append(dist.P2POp(dist.isend, slab, peer, group))
+            ops.append(dist.P2POp(dist.irecv, stage[peer], peer, group))
     for req in dist.batch_isend_irecv(ops):
         req.wait()
+    stage[rank].copy_(slab)
+    out = slab.new_empty((b, c, world * dl, h, w))
+    out.view(b, c, world, dl, h, w).copy_(stage.permute(1, 2, 0, 3, 4, 5))
     return out
 
 

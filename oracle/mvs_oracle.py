@@ -14,6 +14,9 @@ op order so that timings and roundings track it:
   * ``assemble_cost_volume``-- ``scripts/costvolume.py:3-16``   (two-pass population variance over views)
   * ``extract_depth_map``   -- ``scripts/depthmap.py:4-22``     (permutation-indexed "top-N" mask soft-argmin)
   * ``mvsnet_forward``      -- ``scripts/model.py:168-207``     (the forward around the hot path)
+  * ``loss_fcn``            -- ``scripts/loss.py:4-41``         (masked MAE of initial + refined depth)
+  * ``mvsnet_forward64``    -- ``scripts/model.py:168-207`` in float64 with the float64 cost-volume law
+                               (the gradient oracle of the train.py:97-104 step)
 
 Parity pin: ``tests/golden/*.npz`` were produced by importing the reference's own
 ``homography.py`` / ``costvolume.py`` / ``depthmap.py`` / ``model.py`` (with the kornia 0.6.3
@@ -129,6 +132,42 @@ def mvsnet_forward(model, nn_input, K_batch, R_batch, T_batch, d_min, d_int, bat
     d_span = d_int.mul(d_num).mul(d_scale)
     norm = torch.div(torch.subtract(initial, d_trans), d_span)
     refine_in = torch.cat((norm, F.interpolate(nn_input[ref_views], feat_hw, mode="bilinear")), dim=1)
+    refined = model.depthmap_refine(refine_in).mul(d_span).add(d_trans)
+    return initial, refined, prob
+
+
+def loss_fcn(gt, initial, refined):
+    """loss.py:4-41: mask = gt != 0; per sample the masked mean absolute error of the initial and of
+    the refined depth map (sum over the map / valid pixels); loss = sum over samples of both;
+    accuracies = the per-sample MAEs averaged over the batch."""
+    mask = torch.ne(gt, torch.tensor(0.0, dtype=gt.dtype, device=gt.device)).to(gt.dtype)
+    p_valid = mask.sum((1, 2, 3))
+    initial_diff = torch.abs(torch.subtract(gt, initial))
+    refined_diff = torch.abs(torch.subtract(gt, refined))
+    loss_0 = torch.multiply(mask, initial_diff).sum((1, 2, 3)).div(p_valid)
+    loss_1 = torch.multiply(mask, refined_diff).sum((1, 2, 3)).div(p_valid)
+    return (loss_0 + loss_1).sum(), loss_0.mean(), loss_1.mean()
+
+
+def mvsnet_forward64(model, nn_input, K_batch, R_batch, T_batch, d_min, d_int, batch_size, n_views,
+                     d_num, feat_hw, d_scale=D_SCALE):
+    """model.py:168-207 in float64 on the CPU: ``model`` converted with ``.double()``, the cost
+    volume by the float64 law (``cost_volume_torch64``: differentiable in the features, free of the
+    reference's fp32 homography noise), the reference's regulariser op sequence, soft-argmin and
+    refinement in float64.  The gradient oracle of the training step (train.py:97-104)."""
+    x = nn_input.double()
+    feats = model.feature_encoder(x)
+    cv = cost_volume_torch64(feats, K_batch, R_batch, T_batch, d_min, d_int, batch_size, n_views, d_num,
+                             d_scale)
+    reg = model.cost_volume_reg
+    prob = reg.forward_full(cv) if hasattr(reg, "forward_full") else reg(cv)
+    d_batch = depth_planes(d_min.double(), d_int.double(), d_num, d_scale)
+    initial = extract_depth_map(prob, d_batch)
+    d_trans = d_min.double()
+    d_span = d_int.double().mul(d_num).mul(d_scale)
+    norm = torch.div(torch.subtract(initial, d_trans), d_span)
+    ref_views = view_indices(batch_size, n_views)[0]
+    refine_in = torch.cat((norm, F.interpolate(x[ref_views], feat_hw, mode="bilinear")), dim=1)
     refined = model.depthmap_refine(refine_in).mul(d_span).add(d_trans)
     return initial, refined, prob
 

@@ -33,3 +33,19 @@ def golden_dir():
 def load_golden(name):
     import numpy as np
     return np.load(os.path.join(GOLDEN, name))
+
+
+def record_parity(name, **values):
+    """Measured parity numbers of a test (mask-flip fraction, share of pixels within 1e-4 of the
+    oracle, error norms): printed as one "PARITY" JSON line and, when MVS_PARITY_OUT names a
+    directory, written there as <name>.json (profiles/parity_*.json are collected this way)."""
+    import json
+    rec = {"test": name}
+    rec.update({k: (float(v) if hasattr(v, "item") or isinstance(v, float) else v) for k, v in values.items()})
+    print("PARITY " + json.dumps(rec))
+    out = os.environ.get("MVS_PARITY_OUT")
+    if out:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, name + ".json"), "w") as f:
+            json.dump(rec, f, indent=1)
+    return rec

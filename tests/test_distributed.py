@@ -138,6 +138,46 @@ def _run(target, world, *args):
     return res
 
 
+def _opcount_worker(rank, world, port, q):
+    """exchange_to_owners / gather_depth_slabs at C = 32 (the model's channel count): the number of
+    point-to-point ops each posts, counted at dist.batch_isend_irecv, and the results."""
+    _setup(rank, world, port)
+    try:
+        from mvs_amd import depth_shards
+        from mvs_amd.depth_shards import exchange_plan, exchange_to_owners, gather_depth_slabs, owned_samples
+        B, C, Dl, h, w = 3, 32, 4, 6, 7
+        g = torch.Generator().manual_seed(0)
+        full = torch.randn(B, C, world * Dl, h, w, generator=g)       # same on every rank
+        slab = full[:, :, rank * Dl:(rank + 1) * Dl].clone()
+        counts = []
+        real = dist.batch_isend_irecv
+
+        def counting(ops):
+            counts.append(len(ops))
+            return real(ops)
+        depth_shards.dist.batch_isend_irecv = counting
+        try:
+            own = exchange_to_owners(slab, world, rank)
+            every = gather_depth_slabs(slab, world)
+        finally:
+            depth_shards.dist.batch_isend_irecv = real
+        mine = owned_samples(B, world, rank)
+        q.put((rank, counts, len(exchange_plan(B, world, rank)), torch.equal(own, full[mine]),
+               torch.equal(every, full)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_posts_one_message_per_sample_and_peer():
+    """At C = 32 the exchange posts one op per (sample, peer) -- 3 per rank for B = 3 on 2 ranks
+    (rank 0 owns samples 0 and 2: two receives, one send) -- not one per channel (96), and the
+    all-gather one send + one receive per peer; both still reassemble the volume bit for bit."""
+    res = _run(_opcount_worker, 2)
+    for rank, counts, planned, ok_own, ok_all in res:
+        assert counts == [planned, 2] and planned == 3, (rank, counts, planned)
+        assert ok_own and ok_all
+
+
 def test_exchange_to_owners_world2():
     res = _run(_exchange_worker, 2)
     assert [(r[1], r[2]) for r in res] == [(True, True), (True, True)]

@@ -866,3 +866,41 @@ def test_softmax_depth_matches_torch(shape):
     from mvs_amd.ops import softmax_depth
     x = (torch.randn(shape, generator=torch.Generator().manual_seed(shape[2])) * 4).to(DEV)
     torch.testing.assert_close(softmax_depth(x), torch.softmax(x, 2), rtol=2e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("where", ["grad_cv_nan", "grad_cv_inf", "feat_inf"])
+def test_backward_deterministic_mode_propagates_nonfinite(where):
+    """Under torch.use_deterministic_algorithms the backward accumulates in 64-bit fixed point, which
+    cannot carry NaN / Inf: a non-finite grad_cv or feature element must make the gradient NaN (as
+    the default float path propagates it), never an arbitrary finite value -- NaN checks and
+    GradScaler's skip logic rely on it."""
+    from cameras import camera_batch, depth_range, features
+    from mvs_amd import ops
+    B, nv, C, h, w, D = 1, 3, 8, 24, 32, 8
+    K, R, T = camera_batch(B, nv, h, w)
+    d_min, d_int = depth_range(B, d_int=20.0)
+    feat = features(B * nv, C, h, w, seed=4).to(DEV)
+    g = torch.randn(B, C, D, h, w, generator=torch.Generator().manual_seed(5)).to(DEV)
+    if where == "grad_cv_nan":
+        g[0, 3, 2, 10, 11] = float("nan")
+    elif where == "grad_cv_inf":
+        g[0, 1, 5, 3, 4] = float("inf")
+    else:
+        feat[1, 2, 7, 9] = float("inf")
+    _, ws = ops.cost_volume(feat, K, R, T, d_min, d_int, B, nv, 0, D, 25.0)
+    det = ops.cost_volume_backward(feat, ws, g, B, nv, D, True)
+    dflt = ops.cost_volume_backward(feat, ws, g, B, nv, D, False)
+    assert not torch.isfinite(dflt).all()          # the float path propagates it
+    assert torch.isnan(det).all()
+
+
+def test_channel_stats_bit_reproducible():
+    """Train-mode BN batch sums (csrc/channel_ops.hip) are slot-owned partial sums added in a fixed
+    order: two runs are bit-identical (no float atomics), both layouts."""
+    from mvs_amd.ops import channel_stats
+    g = torch.Generator().manual_seed(11)
+    for x, cl in ((torch.randn(4, 40, 33, 41, 16, generator=g), True), (torch.randn(4, 8, 48, 32, 40, generator=g), False)):
+        x = x.to(DEV)
+        a = channel_stats(x, cl)
+        b = channel_stats(x, cl)
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])

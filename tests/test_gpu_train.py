@@ -1,0 +1,158 @@
+"""The train.py step through the drop-in (train.py:97-104): MVSNet.forward with autograd in train
+mode (BatchNorm batch statistics), loss_fcn (loss.py:4-41), loss.backward(), optimizer step -- on the
+GPU, against the oracle model's CPU autograd.
+
+The GPU step runs the HIP cost volume forward (mvs::cost_volume) and its backward
+(mvs::cost_volume_backward), the HIP soft-argmin with its autograd formula, and PyTorch-ROCm (MIOpen)
+for the convolutions.  Three copies of the same deterministic weights (tests/golden/weights.py):
+
+  gpu   the product path on cuda:0 (fp32);
+  cpu   the oracle's reference op sequence on the CPU (fp32, oracle/mvs_oracle.py::mvsnet_forward):
+        the reference's own numerics;
+  law   the same model in float64 with the float64 cost-volume law (mvs_oracle.mvsnet_forward64).
+
+Tolerances are scaled from the reference's own fp32 error: for every parameter, the relative L2
+distance of the GPU gradient to the float64 gradient must be no larger than 3x the fp32 CPU
+gradient's (+ 1e-4).  Both fp32 paths differ from float64 mostly through the soft-argmin's
+permutation mask (depthmap.py:11-15, discontinuous in P): a pixel whose mask flips changes its
+d depth / d P terms, and train-mode BatchNorm (flat P) makes such flips common, so the CPU's own
+error is the scale.  BatchNorm running statistics after the step: 1e-4 relative against the CPU.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+def _rel(a, ref):
+    ref = ref.double()
+    n = ref.norm().item()
+    return (a.double() - ref).norm().item() / max(n, 1e-30)
+
+
+def test_train_step_gradients_match_oracle_autograd():
+    import mvs_oracle
+    from cameras import camera_batch, depth_range
+    from conftest import record_parity
+    from weights import deterministic_state_dict
+    from mvs_amd.config import MVSConfig
+    from mvs_amd.model import MVSNet
+    B, V, D, H, W = 1, 3, 48, 512, 640
+    h, w = H // 4, W // 4
+    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W), device=torch.device("cpu"))
+    net.load_state_dict(deterministic_state_dict(net.state_dict()))
+    net.train()
+    net_c, net_d = copy.deepcopy(net), copy.deepcopy(net).double()
+    net_g = copy.deepcopy(net).to(DEV)
+    rng = np.random.default_rng(77)
+    img = torch.from_numpy(rng.standard_normal((B * V, 3, H, W), dtype=np.float32))
+    K, R, T = camera_batch(B, V, h, w)
+    d_min, d_int = depth_range(B)
+    d_int = d_int.div(d_int)          # train.py:95
+    gt = torch.from_numpy((425.0 + 1200.0 * rng.random((B, 1, h, w))).astype(np.float32))
+    gt[torch.from_numpy(rng.random((B, 1, h, w)) < 0.1)] = 0.0     # invalid pixels (loss.py:8 mask)
+
+    ini_g, ref_g = net_g(img.to(DEV), K, R, T, d_min, d_int, B, V)
+    loss_g, acc1_g, acc2_g = mvs_oracle.loss_fcn(gt.to(DEV), ini_g, ref_g)
+    loss_g.backward()
+    torch.cuda.synchronize()
+
+    ini_c, ref_c, _ = mvs_oracle.mvsnet_forward(net_c, img, K, R, T, d_min, d_int, B, V, D, (h, w))
+    loss_c, _, _ = mvs_oracle.loss_fcn(gt, ini_c, ref_c)
+    loss_c.backward()
+
+    ini_d, ref_d, _ = mvs_oracle.mvsnet_forward64(net_d, img, K, R, T, d_min, d_int, B, V, D, (h, w))
+    loss_d, _, _ = mvs_oracle.loss_fcn(gt.double(), ini_d, ref_d)
+    loss_d.backward()
+
+    lg, lc, ld = loss_g.item(), loss_c.item(), loss_d.item()
+    assert np.isfinite(lg) and abs(lg - ld) <= 3 * abs(lc - ld) + 1e-4 * abs(ld), (lg, lc, ld)
+
+    pg = dict(net_g.named_parameters())
+    pc = dict(net_c.named_parameters())
+    pd = dict(net_d.named_parameters())
+    assert set(pg) == set(pc) == set(pd) and len(pg) > 0
+    worst = {}
+    for name in sorted(pd):
+        gd = pd[name].grad
+        assert pg[name].grad is not None and pc[name].grad is not None, name
+        gg = pg[name].grad.cpu()
+        assert torch.isfinite(gg).all(), name
+        e_g, e_c = _rel(gg, gd), _rel(pc[name].grad, gd)
+        worst[name] = (e_g, e_c)
+        assert e_g <= 3.0 * e_c + 1e-4, "%s: GPU grad %.3g from float64, CPU fp32 %.3g" % (name, e_g, e_c)
+    # the feature encoder's gradient flows back through the HIP cost-volume backward
+    assert any(n.startswith("feature_encoder") and pg[n].grad.abs().max() > 0 for n in pg)
+
+    bg, bc = dict(net_g.named_buffers()), dict(net_c.named_buffers())
+    for name in sorted(bc):
+        torch.testing.assert_close(bg[name].cpu(), bc[name], rtol=1e-4, atol=1e-6, msg=name)
+
+    # one Adam step (train.py:104, Adam(model.parameters, lr) with the reference's list attribute)
+    opt = torch.optim.Adam(net_g.parameters, lr=1e-3)
+    before = {n: p.detach().clone() for n, p in pg.items()}
+    opt.step()
+    assert all(not torch.equal(before[n], pg[n].detach()) for n in pg if pg[n].grad.abs().max() > 0)
+    record_parity("train_step_cfg1_grads", loss_gpu=lg, loss_cpu_fp32=lc, loss_f64=ld,
+                  grad_rel_l2_gpu_vs_f64_max=max(v[0] for v in worst.values()),
+                  grad_rel_l2_cpu_vs_f64_max=max(v[1] for v in worst.values()),
+                  per_parameter={k: [float(a), float(b)] for k, (a, b) in worst.items()})
+
+
+def test_train_mode_autograd_chain_smooth_loss():
+    """The same autograd chain without the soft-argmin's discontinuous mask: a smooth loss on the
+    probability volume, L = sum(P * Wr), through the train-mode regulariser (MIOpen), the HIP cost
+    volume backward and the encoder, B=2 with distinct depth ranges (the i mod B plane tiling), at a
+    reduced geometry (256x320 images, D=16).  Every parameter's gradient: relative L2 to float64
+    <= 2x the CPU fp32 gradient's + 1e-5 (here the fp32 noise is the only difference)."""
+    import mvs_oracle
+    from cameras import camera_batch, depth_range
+    from conftest import record_parity
+    from weights import deterministic_state_dict
+    from mvs_amd import warp_and_assemble_cost_volume
+    from mvs_amd.config import MVSConfig
+    from mvs_amd.model import MVSNet
+    B, V, D, H, W = 2, 3, 16, 256, 320
+    h, w = H // 4, W // 4
+    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W), device=torch.device("cpu"))
+    net.load_state_dict(deterministic_state_dict(net.state_dict(), seed=99))
+    net.train()
+    net_c, net_d = copy.deepcopy(net), copy.deepcopy(net).double()
+    net_g = copy.deepcopy(net).to(DEV)
+    rng = np.random.default_rng(78)
+    img = torch.from_numpy(rng.standard_normal((B * V, 3, H, W), dtype=np.float32))
+    K, R, T = camera_batch(B, V, h, w)
+    d_min, d_int = depth_range(B, d_int=4.0, distinct=True)
+    wr = torch.from_numpy(rng.standard_normal((B, 1, D, h, w), dtype=np.float32))
+
+    feats = net_g.feature_encoder(img.to(DEV))
+    cv, _, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, B, V, d_num=D)
+    (net_g.cost_volume_reg(cv) * wr.to(DEV)).sum().backward()
+
+    feats = net_c.feature_encoder(img)
+    wp, _, _ = mvs_oracle.homography_warping(K, R, T, d_min, d_int, feats, B, V, D, concat_growth=False)
+    (net_c.cost_volume_reg.forward_full(mvs_oracle.assemble_cost_volume(wp, V)) * wr).sum().backward()
+
+    feats = net_d.feature_encoder(img.double())
+    cv64 = mvs_oracle.cost_volume_torch64(feats, K, R, T, d_min, d_int, B, V, D)
+    (net_d.cost_volume_reg.forward_full(cv64) * wr.double()).sum().backward()
+
+    pg, pc, pd = (dict(n.named_parameters()) for n in (net_g, net_c, net_d))
+    errs = {}
+    for name in sorted(pd):
+        gd = pd[name].grad
+        if gd is None:   # depthmap_refine is not on this loss's path
+            assert pg[name].grad is None
+            continue
+        e_g, e_c = _rel(pg[name].grad.cpu(), gd), _rel(pc[name].grad, gd)
+        errs[name] = (e_g, e_c)
+        assert e_g <= 2.0 * e_c + 1e-5, "%s: GPU grad %.3g from float64, CPU fp32 %.3g" % (name, e_g, e_c)
+    assert any(k.startswith("feature_encoder") for k in errs)
+    record_parity("train_mode_smooth_loss_grads", grad_rel_l2_gpu_vs_f64_max=max(v[0] for v in errs.values()),
+                  grad_rel_l2_cpu_vs_f64_max=max(v[1] for v in errs.values()),
+                  per_parameter={k: [float(a), float(b)] for k, (a, b) in errs.items()})
