@@ -127,10 +127,10 @@ def make_inputs(B, V, H, W, seed, device):
     return img, K.to(device), R.to(device), T.to(device), d_min.to(device), d_int.to(device)
 
 
-def build_model(D, H, W, device):
+def build_model(D, H, W, device, cv_dtype="float32"):
     from mvs_amd.config import MVSConfig
     from mvs_amd.model import MVSNet
-    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W))
+    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W, cv_dtype=cv_dtype))
     net.load_state_dict(deterministic_state_dict(net.state_dict()))
     return net.to(device).eval()
 
@@ -154,13 +154,21 @@ def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=F
     g = torch.Generator(device="cpu").manual_seed(7)
     feat = torch.randn(B * V, C, h, w, generator=g).to(device)
     cv = torch.empty((B, C, d_count, h, w), device=device,
-                     dtype=torch.bfloat16 if bf16 else torch.float32)
+                     dtype=torch.bfloat16 if bf16 else torch.float32)   # (same bytes as the quad layouts)
     ws = torch.empty((lib.mvs_cost_volume_workspace_bytes(B, V, C, h, w, d_count) + 3) // 4,
                      device=device)
     stream = torch.cuda.current_stream(device)
     sp = _lib.stream_handle(device)
 
     def launch(e0=None, e1=None):
+        if bf16 and quads:
+            st = lib.mvs_cost_volume_fwd_c4_bf16(
+                _lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T), _lib.ptr(d_min), _lib.ptr(d_int),
+                B, V, C, h, w, d_begin, d_count, 25.0, _lib.ptr(ws), _lib.ptr(cv), sp,
+                None if e0 is None else ctypes.c_void_p(e0.cuda_event),
+                None if e1 is None else ctypes.c_void_p(e1.cuda_event))
+            _lib.check(st, "mvs_cost_volume_fwd_c4_bf16")
+            return
         if bf16:
             st = lib.mvs_cost_volume_fwd_bf16(
                 _lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T), _lib.ptr(d_min),
@@ -189,7 +197,7 @@ def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=F
         launch(e0, e1)
     op1.record(stream)
     torch.cuda.synchronize()
-    main_ms = None if bf16 else sum(e0.elapsed_time(e1) for e0, e1 in ev) / iters
+    main_ms = None if (bf16 and not quads) else sum(e0.elapsed_time(e1) for e0, e1 in ev) / iters
     op_ms = op0.elapsed_time(op1) / iters
     alg_bytes = 4.0 * B * V * C * h * w + (2.0 if bf16 else 4.0) * B * C * d_count * h * w
     return main_ms, op_ms, alg_bytes
@@ -277,6 +285,36 @@ def e2e_configs(device, steps):
                      "ms_per_step": 1000.0 * dt, "depth_maps_per_s": B / dt, "steps": steps}
         del net, inputs
         torch.cuda.empty_cache()
+    return out
+
+
+def bf16_step(net32, inputs, B, V, D, H, W, device, world, steps):
+    """The reduced-precision opt-in (MVSConfig(cv_dtype="bfloat16")) timed as the
+    headline step: the fused kernel stores the cost volume as bf16 channel quads (8 B per 4 channels,
+    half the write) and the regulariser's HIP layers read it widened to fp32.  Reported beside the
+    fp32 headline with the depth deviation it causes (initial depth vs the fp32 step, same inputs and
+    weights); never the headline value."""
+    log("bf16 cost-volume opt-in step")
+    net = build_model(D, H, W, device, cv_dtype="bfloat16")
+    with torch.no_grad():
+        ini32 = net32(*inputs, B, V)[0]
+        for _ in range(2):
+            ini16 = net(*inputs, B, V)[0]
+        barrier(world)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            net(*inputs, B, V)
+        barrier(world)
+        dt = time.perf_counter() - t0
+    rel = ((ini16 - ini32).abs() / ini32.abs()).flatten()
+    out = {"ms_per_step": 1000.0 * dt / steps, "value": B * world * steps / dt, "steps": steps,
+           "initial_depth_rel_diff_vs_fp32": {"median": rel.median().item(), "p99": rel.quantile(0.99).item()
+                                              if rel.numel() <= 16_000_000 else None, "max": rel.max().item(),
+                                              "frac_within_1e-4": (rel <= 1e-4).float().mean().item()},
+           "note": "cv stored bf16 (RNE of the fp32 variance), fp32 regulariser on the rounded values; "
+                   "bit-identical to the fp32 step run on the rounded volume (tests/test_bf16_cost_volume.py)"}
+    del net
+    torch.cuda.empty_cache()
     return out
 
 
@@ -521,6 +559,9 @@ def main():
             result["train_bn"] = {"ms_per_step": 1000.0 * dtt / train_steps,
                                   "value": B * world * train_steps / dtt, "steps": train_steps}
             log("train-mode BN step (test.py:61): %.2f ms/step" % result["train_bn"]["ms_per_step"])
+            if not args.no_extra:
+                net.eval()
+                result["bf16"] = bf16_step(net, inputs, B, V, D, H, W, device, world, args.steps)
         del net
 
     # fused kernel timing (this rank's share of planes in dshard mode)
@@ -607,9 +648,15 @@ def main():
             out["train_step"] = train_step_bench(B, V, D, H, W, device, 3)
     # opt-in bf16 cost volume: informational, not the headline (reduced precision)
     _, bf_op_ms, bf_alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count, bf16=True)
-    out["bf16_cv_opt_in"] = {"op_ms": bf_op_ms, "alg_bytes_per_launch": bf_alg,
-                             "op_GBps": bf_alg / (bf_op_ms * 1e-3) / 1e9,
-                             "cost_volumes_per_s": B / (bf_op_ms * 1e-3)}
+    q_ms, q_op_ms, q_alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count, bf16=True,
+                                       quads=True)
+    out["bf16_cv_opt_in"] = {"ncdhw_op_ms": bf_op_ms, "alg_bytes_per_launch": bf_alg,
+                             "ncdhw_op_GBps": bf_alg / (bf_op_ms * 1e-3) / 1e9,
+                             "channel_quad_kernel_ms": q_ms, "channel_quad_op_ms": q_op_ms,
+                             "channel_quad_GBps": q_alg / (q_ms * 1e-3) / 1e9,
+                             "cost_volumes_per_s": B / (q_op_ms * 1e-3)}
+    if "bf16" in result:
+        out["bf16_cv_opt_in"]["step"] = result["bf16"]
     if not args.no_cpu_baseline and world == 1:
         log("cpu baseline (oracle, one sample)")
         out["cpu_baseline"] = cpu_baseline(V, H, W, args.cpu_planes or D)

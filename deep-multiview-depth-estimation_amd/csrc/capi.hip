@@ -41,7 +41,8 @@ bool cams_ok(const float* K, const float* R, const float* T, const float* d_min,
   return K && R && T && d_min && d_int;
 }
 
-// Fused warp + variance into an fp32 (es = 4) or bf16 (es = 2) cost volume.
+// Fused warp + variance into an fp32 (es = 4) or bf16 (es = 2) NCDHW cost volume, or the channel-quad
+// layout in fp32 (es = 16) or bf16 (es = 8).
 int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, const float* T,
                          const float* d_min, const float* d_int, int batch_size, int n_views,
                          int channels, int h, int w, int d_begin, int d_count, float d_scale,
@@ -57,7 +58,7 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
     st = mvs_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
                             d_scale, workspace, stream);
     if (st != MVS_OK) return st;
-    const size_t ch = es == 16 ? (size_t)((channels + 3) / 4) : (size_t)channels;
+    const size_t ch = (es == 16 || es == 8) ? (size_t)((channels + 3) / 4) : (size_t)channels;
     if (hipMemsetAsync(cv_out, 0, (size_t)batch_size * ch * d_count * h * w * es, s) != hipSuccess)
       return MVS_ERR_HIP;
     return lc.status();
@@ -72,6 +73,9 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
   else if (es == 16)
     mvs::launch_cost_volume_fwd_c4(g, feat, cm, workspace, packed, static_cast<float*>(cv_out), s,
                                    (hipEvent_t)ev0, (hipEvent_t)ev1);
+  else if (es == 8)
+    mvs::launch_cost_volume_fwd_c4_bf16(g, feat, cm, workspace, packed, cv_out, s, (hipEvent_t)ev0,
+                                        (hipEvent_t)ev1);
   else
     mvs::launch_cost_volume_fwd_bf16(g, feat, cm, workspace, packed, cv_out, s, (hipEvent_t)ev0,
                                      (hipEvent_t)ev1);
@@ -158,6 +162,18 @@ int mvs_cost_volume_fwd_c4(const float* feat, const float* K, const float* R, co
   if ((uintptr_t)cv_out & 15u) return MVS_ERR_INVALID_ARGUMENT;
   return cost_volume_fwd_impl(feat, K, R, T, d_min, d_int, batch_size, n_views, channels, h, w,
                               d_begin, d_count, d_scale, workspace, cv_out, 16, stream,
+                              main_begin_event, main_end_event);
+}
+
+int mvs_cost_volume_fwd_c4_bf16(const float* feat, const float* K, const float* R, const float* T,
+                                const float* d_min, const float* d_int, int batch_size, int n_views,
+                                int channels, int h, int w, int d_begin, int d_count, float d_scale,
+                                float* workspace, void* cv_out, void* stream, void* main_begin_event,
+                                void* main_end_event) {
+  if (n_views > 8) return MVS_ERR_UNSUPPORTED_VIEWS;
+  if ((uintptr_t)cv_out & 7u) return MVS_ERR_INVALID_ARGUMENT;
+  return cost_volume_fwd_impl(feat, K, R, T, d_min, d_int, batch_size, n_views, channels, h, w,
+                              d_begin, d_count, d_scale, workspace, cv_out, 8, stream,
                               main_begin_event, main_end_event);
 }
 
@@ -270,15 +286,18 @@ int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, 
   if (!x || !weight || !y || batch <= 0 || c_in <= 0 || d <= 0 || h <= 0 || w <= 0)
     return MVS_ERR_INVALID_ARGUMENT;
   if (c_out != 1 && c_out != 8) return MVS_ERR_INVALID_ARGUMENT;
-  if (flags & ~(MVS_CONV_IN_C4 | MVS_CONV_WINO_Z)) return MVS_ERR_INVALID_ARGUMENT;
+  if (flags & ~(MVS_CONV_IN_C4 | MVS_CONV_WINO_Z | MVS_CONV_IN_BF16)) return MVS_ERR_INVALID_ARGUMENT;
+  if ((flags & MVS_CONV_IN_BF16) && (!(flags & MVS_CONV_IN_C4) || ((uintptr_t)x & 7u))) return MVS_ERR_INVALID_ARGUMENT;
   if ((flags & MVS_CONV_WINO_Z) && c_out != 8) return MVS_ERR_INVALID_ARGUMENT;
-  if ((flags & MVS_CONV_IN_C4) && (c_in % 4 || ((uintptr_t)x & 15u))) return MVS_ERR_INVALID_ARGUMENT;
+  if ((flags & MVS_CONV_IN_C4) && (c_in % 4 || (!(flags & MVS_CONV_IN_BF16) && ((uintptr_t)x & 15u))))
+    return MVS_ERR_INVALID_ARGUMENT;
   if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
     return MVS_ERR_INVALID_ARGUMENT;
   // staging offsets inside one channel volume are 32-bit
   if ((uint64_t)d * (uint64_t)h * (uint64_t)w >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
   const mvs::LaunchCheck lc;
-  mvs::launch_conv3d_k3_narrow(x, (flags & MVS_CONV_IN_C4) != 0, (flags & MVS_CONV_WINO_Z) != 0, weight, y, batch,
+  const int quads = (flags & MVS_CONV_IN_C4) ? ((flags & MVS_CONV_IN_BF16) ? 2 : 1) : 0;
+  mvs::launch_conv3d_k3_narrow(x, quads, (flags & MVS_CONV_WINO_Z) != 0, weight, y, batch,
                                c_in, c_out, d, h, w,
                                bn_scale, bn_shift, bn_mean,
                                (hipStream_t)stream);
@@ -315,8 +334,9 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
                           const int* pad, const float* bn_scale, const float* bn_shift,
                           const float* bn_mean, void* stream) {
   if (!x || !weight || !y || !dims || !out_origin || !out_size || batch <= 0) return MVS_ERR_INVALID_ARGUMENT;
-  if (mode < MVS_CONV_S1 || mode > MVS_CONV_T2 || (flags & ~(MVS_CONV_OUT_NCDHW | MVS_CONV_IN_C4)))
+  if (mode < MVS_CONV_S1 || mode > MVS_CONV_T2 || (flags & ~(MVS_CONV_OUT_NCDHW | MVS_CONV_IN_C4 | MVS_CONV_IN_BF16)))
     return MVS_ERR_INVALID_ARGUMENT;
+  if ((flags & MVS_CONV_IN_BF16) && !(flags & MVS_CONV_IN_C4)) return MVS_ERR_INVALID_ARGUMENT;
   if ((flags & MVS_CONV_IN_C4) && (mode != MVS_CONV_S2 || c_in % 4)) return MVS_ERR_INVALID_ARGUMENT;
   if (mode != MVS_CONV_S2 && (!in_origin || !in_size)) return MVS_ERR_INVALID_ARGUMENT;
   if (mode != MVS_CONV_S1 && !pad) return MVS_ERR_INVALID_ARGUMENT;
@@ -343,7 +363,8 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
       nvox >= (1ull << 62))
     return MVS_ERR_TOO_LARGE;
   const mvs::LaunchCheck lc;
-  const int st = mvs::launch_conv3d_region(mode, (flags & MVS_CONV_OUT_NCDHW) != 0, (flags & MVS_CONV_IN_C4) != 0,
+  const int quads = (flags & MVS_CONV_IN_C4) ? ((flags & MVS_CONV_IN_BF16) ? 2 : 1) : 0;
+  const int st = mvs::launch_conv3d_region(mode, (flags & MVS_CONV_OUT_NCDHW) != 0, quads,
                                            x, x2, weight, y, batch, c_in, c_out, dims, out_origin, out_size,
                                            in_origin, in_size, pad, bn_scale, bn_shift, bn_mean,
                                            (hipStream_t)stream);

@@ -10,8 +10,10 @@
 // stages the (DT + 2) x 10 x 34 halo block in LDS (zero-filled outside the volume), and every
 // thread reads the 9 taps of each staged plane once (54 VGPRs) and applies them to the output
 // depths they reach (plane p feeds depth p - kd).  The staging of channel c + 1 is loaded into
-// registers before channel c is computed.  Input NCDHW, or channel-quad (C4, the fused kernel's
-// NC4DHW4 output): then a pass stages 4 channels with one 16-byte load per element into 4 LDS planes.
+// registers before channel c is computed.  Input NCDHW (C4 = 0), or channel-quad (the fused kernel's
+// NC4DHW4 output): then a pass stages 4 channels with one 16-byte load per element (C4 = 1, fp32) or
+// one 8-byte load widened to 4 fp32 (C4 = 2, bf16: the reduced-precision opt-in; widening is exact, so
+// the arithmetic is the fp32 kernel's on the rounded values) into 4 LDS planes.
 //   COUT = 8: output channels in pairs on the packed fp32 FMA (v_pk_fma_f32: the tap broadcast to
 //   both halves, the two channels' weights as one 64-bit scalar operand), 2 FMAs per lane-
 //   instruction -- the weights arrive pre-transposed as wt[c][kd][ky][kx][co] (ops.py), so each
@@ -31,7 +33,7 @@ constexpr int kTX = 32, kTY = 8, kDT = 4;
 // (g0 - g1 + g2) / 2, g2; formed in float64 on the host, ops.py), accumulated per position; the
 // outputs are A^T m (m0 + m1 + m2, m1 - m2 - m3) at the end.  Per input channel 288 packed FMAs +
 // 36 packed adds instead of 432 packed FMAs.  Weights wu[c][ky][kx][4][co].
-template <int COUT, bool C4, bool WZ = false>
+template <int COUT, int C4, bool WZ = false>
 __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
     const float* __restrict__ in, const float* __restrict__ wt, float* __restrict__ out, int Cin,
     int D, int H, int W, int tiles_x, int tiles_y, int dgroups, const float* __restrict__ bn_scale,
@@ -53,6 +55,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   const size_t plane = (size_t)H * W;
   const size_t vol = (size_t)D * plane;
   const float* ib = in + (size_t)b * Cin * vol;   // (channel-quad layout: the same element count)
+  const uint2* ib16 = reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(in) + (size_t)b * Cin * vol * 2);
 
   // staging map: element e of the halo block -> (global offset inside one channel, valid)
   int goff[kPer];
@@ -69,7 +72,17 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   // one pass = one input channel (NCDHW) or one channel quad (C4: 16-byte loads, 4 LDS planes)
   float pre[kPer][NQ];
   auto fetch = [&](int q) {
-    if constexpr (C4) {
+    if constexpr (C4 == 2) {   // bf16 quad: the high halves of 4 fp32 words
+      const uint2* src = ib16 + (size_t)q * vol;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const uint2 v = gok[j] ? src[goff[j]] : make_uint2(0u, 0u);
+        pre[j][0] = __uint_as_float(v.x << 16);
+        pre[j][1] = __uint_as_float(v.x & 0xFFFF0000u);
+        pre[j][2] = __uint_as_float(v.y << 16);
+        pre[j][3] = __uint_as_float(v.y & 0xFFFF0000u);
+      }
+    } else if constexpr (C4) {
       const float4* src = reinterpret_cast<const float4*>(ib) + (size_t)q * vol;
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
@@ -219,7 +232,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   }
 }
 
-template <int COUT, bool C4, bool WZ = false>
+template <int COUT, int C4, bool WZ = false>
 void launch_narrow(const float* in, const float* weight, float* out, int B, int Cin, int D, int H, int W,
                    const float* bn_scale, const float* bn_shift, const float* bn_mean, hipStream_t s) {
   const int tiles_x = (W + kTX - 1) / kTX, tiles_y = (H + kTY - 1) / kTY, dgroups = (D + kDT - 1) / kDT;
@@ -230,21 +243,24 @@ void launch_narrow(const float* in, const float* weight, float* out, int B, int 
 
 }  // namespace
 
-void launch_conv3d_k3_narrow(const float* in, bool in_c4, bool wino_z, const float* weight, float* out, int B,
+void launch_conv3d_k3_narrow(const float* in, int in_c4, bool wino_z, const float* weight, float* out, int B,
                              int Cin, int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
                              const float* bn_mean, hipStream_t s) {
-  if (wino_z && in_c4)
-    launch_narrow<8, true, true>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
-  else if (wino_z)
-    launch_narrow<8, false, true>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
-  else if (Cout == 8 && in_c4)
-    launch_narrow<8, true>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
-  else if (Cout == 8)
-    launch_narrow<8, false>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
-  else if (in_c4)
-    launch_narrow<1, true>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
-  else
-    launch_narrow<1, false>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s);
+#define MVS_NARROW(CO, Q, WZ) launch_narrow<CO, Q, WZ>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s)
+  if (wino_z) {
+    if (in_c4 == 2) MVS_NARROW(8, 2, true);
+    else if (in_c4) MVS_NARROW(8, 1, true);
+    else MVS_NARROW(8, 0, true);
+  } else if (Cout == 8) {
+    if (in_c4 == 2) MVS_NARROW(8, 2, false);
+    else if (in_c4) MVS_NARROW(8, 1, false);
+    else MVS_NARROW(8, 0, false);
+  } else {
+    if (in_c4 == 2) MVS_NARROW(1, 2, false);
+    else if (in_c4) MVS_NARROW(1, 1, false);
+    else MVS_NARROW(1, 0, false);
+  }
+#undef MVS_NARROW
 }
 
 }  // namespace mvs

@@ -48,7 +48,7 @@ struct Geo {
   int in[3];    // input region size (S1, T2)
   int pad[3];   // P (S2, T2)
   int out_cf;   // 1: output region tensor channels-first y[b][co][z][y][x] (else channels-last)
-  int in_c4;    // S2: the volume is channel-quad x[b][C/4][D][H][W][4] (else NCDHW)
+  int in_c4;    // S2: the volume is channel-quad x[b][C/4][D][H][W][4], fp32 (1) or bf16 (2); 0 NCDHW
 };
 
 // T2 parity class: per dim, outputs o with (o + P) % 2 == par; first such o in the region and count
@@ -171,8 +171,12 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
         const int c4 = cb * 16 + kq * 4;
         Rsrc rs, rs2;
         if constexpr (MODE == kS2) {
-          rs = g.in_c4 ? make_rsrc(x + ((size_t)b * (CI / 4) + cb * 4) * nvol * 4, (uint32_t)(nvol * 64))
-                       : make_rsrc(x + ((size_t)b * CI + cb * 16) * nvol, (uint32_t)(nvol * 64));
+          if (g.in_c4 == 2)   // bf16 quads: 8 bytes per voxel and quad
+            rs = make_rsrc(reinterpret_cast<const char*>(x) + ((size_t)b * (CI / 4) + cb * 4) * nvol * 8,
+                           (uint32_t)(nvol * 32));
+          else
+            rs = g.in_c4 ? make_rsrc(x + ((size_t)b * (CI / 4) + cb * 4) * nvol * 4, (uint32_t)(nvol * 64))
+                         : make_rsrc(x + ((size_t)b * CI + cb * 16) * nvol, (uint32_t)(nvol * 64));
         } else {
           rs = make_rsrc(x + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
           if (x2) rs2 = make_rsrc(x2 + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
@@ -186,7 +190,13 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
             const uint32_t vx = vox[tx][rb];
             f4v_t v;
             if constexpr (MODE == kS2) {
-              if (g.in_c4) {   // the quad (c4 / 4) of the voxel: one 16-byte load
+              if (g.in_c4 == 2) {   // the bf16 quad: one 8-byte load, widened (exact)
+                typedef __attribute__((ext_vector_type(2))) unsigned v2u;
+                const v2u p = __builtin_amdgcn_raw_buffer_load_b64(
+                    rs, (int)(vx == kOob ? kOob : ((uint32_t)kq * (uint32_t)nvol + vx) * 8u), 0, 0);
+                v = f4v_t{__uint_as_float(p.x << 16), __uint_as_float(p.x & 0xFFFF0000u),
+                          __uint_as_float(p.y << 16), __uint_as_float(p.y & 0xFFFF0000u)};
+              } else if (g.in_c4) {   // the quad (c4 / 4) of the voxel: one 16-byte load
                 v = ld4(rs, vx == kOob ? kOob : ((uint32_t)kq * (uint32_t)nvol + vx) * 16u, 0);
               } else {
 #pragma unroll
@@ -259,13 +269,13 @@ void launch_mode(const float* x, const float* x2, const float* w, float* y, cons
 
 }  // namespace
 
-int launch_conv3d_region(int mode, bool out_cf, bool in_c4, const float* x, const float* x2, const float* w,
+int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const float* x2, const float* w,
                          float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on, const int* i0,
                          const int* in, const int* pad, const float* bn_scale, const float* bn_shift,
                          const float* bn_mean, hipStream_t s) {
   Geo g;
   g.out_cf = out_cf ? 1 : 0;
-  g.in_c4 = in_c4 ? 1 : 0;
+  g.in_c4 = in_c4;
   for (int d = 0; d < 3; ++d) {
     g.n[d] = n[d];
     g.o0[d] = o0[d];

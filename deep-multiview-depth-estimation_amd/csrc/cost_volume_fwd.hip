@@ -286,7 +286,15 @@ __device__ inline void store_out(Rsrc rs, uint32_t voff, float v) {
 //   ES = 16  fp32 channel-quad cv[B][C/4][D][h][w][4] ("NC4DHW4"): each (pixel, plane, chunk) is one
 //            16-byte store, a wave's 64 pixels one contiguous 1 KB run; the regulariser's HIP layers
 //            read 4 channels of a voxel per load from it (MVSNet.forward's inference path)
+//   ES = 8   bf16 channel-quad (SURVEY.md §8 f3 reduced-precision opt-in): the same layout with each
+//            fp32 variance rounded to nearest-even bf16, one 8-byte store per (pixel, plane, chunk), a
+//            wave's 64 pixels one contiguous 512-B run; the regulariser's HIP layers widen it on load
 constexpr int kQuad = 16;
+constexpr int kQuadBf16 = 8;
+template <int ES>
+constexpr bool quad_layout() {
+  return ES == kQuad || ES == kQuadBf16;
+}
 
 // staging pieces per thread carried in registers across a chunk: 4 covers the V = 3 footprints
 // (about 3.5 pieces per thread and chunk at cfg 2); 4 views of 4-plane groups average 6 (cfg 3)
@@ -420,8 +428,8 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   // store descriptors of chunk ch's four channels (planes k0 .. k0 + npl of this sample); the
   // channel-quad layout has one descriptor for the chunk's quad plane
   auto chunk_rsrc = [&](int ch, Rsrc (&rs)[4]) {
-    if constexpr (ES == kQuad) {
-      rs[0] = make_rsrc(static_cast<char*>(cv) + (((size_t)b * c4 + ch) * Dc + k0) * hw * kQuad, grp_bytes);
+    if constexpr (quad_layout<ES>()) {
+      rs[0] = make_rsrc(static_cast<char*>(cv) + (((size_t)b * c4 + ch) * Dc + k0) * hw * ES, grp_bytes);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -436,6 +444,11 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
     if constexpr (ES == kQuad) {
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc),
                                              rs[0], (int)(soff0 + (uint32_t)pl * hw * (uint32_t)kQuad), 0, kStoreAux);
+    } else if constexpr (ES == kQuadBf16) {
+      typedef __attribute__((ext_vector_type(2))) unsigned v2u;
+      const v2u pk = {bf16_rne(acc[0]) | (bf16_rne(acc[1]) << 16), bf16_rne(acc[2]) | (bf16_rne(acc[3]) << 16)};
+      __builtin_amdgcn_raw_buffer_store_b64(pk, rs[0], (int)(soff0 + (uint32_t)pl * hw * (uint32_t)kQuadBf16), 0,
+                                            kStoreAux);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) store_out<ES>(rs[j], soff0 + (uint32_t)pl * hw * (uint32_t)ES, acc[j]);
@@ -702,6 +715,20 @@ void launch_cost_volume_fwd_c4(const Geometry& g, const float* feat, const Cams&
     case 6: launch_gather<6, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
     case 7: launch_gather<7, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
     case 8: launch_gather<8, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    default: break;   // rejected by the C ABI (2 <= V <= 8 only)
+  }
+}
+
+void launch_cost_volume_fwd_c4_bf16(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
+                                    float* packed, void* cv, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  switch (g.V) {
+    case 2: launch_gather<2, kQuadBf16>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 3: launch_gather<3, kQuadBf16>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 4: launch_gather<4, kQuadBf16>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 5: launch_gather<5, kQuadBf16>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 6: launch_gather<6, kQuadBf16>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 7: launch_gather<7, kQuadBf16>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 8: launch_gather<8, kQuadBf16>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
     default: break;   // rejected by the C ABI (2 <= V <= 8 only)
   }
 }

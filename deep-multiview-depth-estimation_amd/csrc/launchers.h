@@ -27,6 +27,10 @@ void launch_cost_volume_fwd(const Geometry& g, const float* feat, const Cams& cm
 void launch_cost_volume_fwd_c4(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
                                float* packed, float* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
                                hipEvent_t ev1 = nullptr);
+// same, bf16 channel-quad layout cv[B][C/4][Dc][h][w][4] (RNE), 2 <= V <= 8
+void launch_cost_volume_fwd_c4_bf16(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
+                                    float* packed, void* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
+                                    hipEvent_t ev1 = nullptr);
 // same, bf16 cost volume (uint16 storage, RNE), 2 <= V <= 8
 void launch_cost_volume_fwd_bf16(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
                                  float* packed, void* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
@@ -52,9 +56,9 @@ void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, u
 
 // conv3d_narrow.hip: 3x3x3 stride-1 padding-1 bias-free Conv3d, NCDHW fp32, Cout in {1, 8}
 // (optional epilogue: max((v - bn_mean) * bn_scale + bn_shift, 0), all three or none); in_c4: the
-// input is channel-quad in[B][Cin/4][D][H][W][4]
+// input is channel-quad in[B][Cin/4][D][H][W][4], fp32 (1) or bf16 (2)
 // wino_z (Cout = 8): Winograd F(2,3) along depth, weight = the transformed wu[Cin][3][3][4][8]
-void launch_conv3d_k3_narrow(const float* in, bool in_c4, bool wino_z, const float* weight, float* out, int B,
+void launch_conv3d_k3_narrow(const float* in, int in_c4, bool wino_z, const float* weight, float* out, int B,
                              int Cin, int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
                              const float* bn_mean, hipStream_t s);
 
@@ -76,9 +80,10 @@ void launch_deconv3d_k3s2(const float* x, const float* x2, int layout, int B, in
 
 // conv3d_region.hip: region convolutions of the regulariser on the fp32 MFMA (mode 0 = stride 1,
 // 1 = stride 2 from the full NCDHW volume, 2 = transposed stride 2), channels-last region tensors,
-// optional fused eval BN + ReLU, output channels-last or (out_cf) channels-first;
+// optional fused eval BN + ReLU, output channels-last or (out_cf) channels-first; in_c4 (S2): the
+// volume is channel-quad, fp32 (1) or bf16 (2);
 // MVS_ERR_INVALID_ARGUMENT for an unsupported (mode, CI, CO)
-int launch_conv3d_region(int mode, bool out_cf, bool in_c4, const float* x, const float* x2, const float* w,
+int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const float* x2, const float* w,
                          float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on, const int* i0,
                          const int* in,
                          const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,

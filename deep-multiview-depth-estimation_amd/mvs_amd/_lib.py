@@ -27,6 +27,7 @@ MVS_CONV_S1, MVS_CONV_S2, MVS_CONV_T2 = 0, 1, 2
 MVS_CONV_OUT_NCDHW = 1
 MVS_CONV_IN_C4 = 2
 MVS_CONV_WINO_Z = 4
+MVS_CONV_IN_BF16 = 8
 MVS_DECONV_WEIGHT_TAPS = 2
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported n_views", -3: "too large",
           -4: "HIP runtime error"}
@@ -48,6 +49,8 @@ SIGNATURES = {
                                            _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p]),
     "mvs_cost_volume_fwd_c4": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
                                         _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p]),
+    "mvs_cost_volume_fwd_c4_bf16": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
+                                             _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p]),
     "mvs_cost_volume_fwd_bf16": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
                                           _c_int, _c_int, _c_int, _c_float, _p, _p, _p]),
     "mvs_homography_warp_fwd": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,

@@ -44,8 +44,10 @@ class MVSConfig:
     dim_reduce: int = DIM_REDUCE
     feat_h: int = field(default=None)
     feat_w: int = field(default=None)
-    # opt-in reduced precision: "bfloat16" stores the cost volume in bf16 and runs
-    # the 3-D regulariser under bf16 autocast; the default "float32" is the reference's numerics
+    # opt-in reduced precision: "bfloat16" stores the cost volume in bf16 (the
+    # fused kernel rounds each fp32 variance once; half the HBM bytes written and read) and the 3-D
+    # regulariser computes in fp32 from the rounded values; the default "float32" is the reference's
+    # numerics
     cv_dtype: str = "float32"
 
     def __post_init__(self):

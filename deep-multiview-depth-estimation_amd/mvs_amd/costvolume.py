@@ -26,8 +26,9 @@ def warp_and_assemble_cost_volume(K_batch, R_batch, T_batch, d_min, d_int, featu
 
     ``cv_dtype=torch.bfloat16`` (opt-in) returns the fp32 variance rounded to
     bf16 in the kernel's store (half the write); the default fp32 is the reference's.
-    ``channel_quads=True`` (fp32 inference) returns the same values in the channel-quad layout
-    [B, C/4, d_count, h, w, 4] that CostVolumeReg's HIP path reads 16 bytes at a time."""
+    ``channel_quads=True`` (inference) returns the same values in the channel-quad layout
+    [B, C/4, d_count, h, w, 4] that CostVolumeReg's HIP path reads 16 (fp32) or 8 (bf16) bytes at a
+    time."""
     if d_count is None:
         d_count = d_num - d_begin
     if d_begin < 0 or d_count <= 0 or d_begin + d_count > d_num:
@@ -35,10 +36,11 @@ def warp_and_assemble_cost_volume(K_batch, R_batch, T_batch, d_min, d_int, featu
     device = feature_maps.device
     d_batch_0 = depth_hypotheses(d_min, d_int, d_num, d_scale).to(device)
     if channel_quads:
-        if cv_dtype != torch.float32:
-            raise ValueError("the channel-quad cost volume is fp32")
-        cv = ops.cost_volume_c4(feature_maps, K_batch, R_batch, T_batch, d_min, d_int, int(batch_size),
-                                int(n_views), int(d_begin), int(d_count), float(d_scale))
+        if cv_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("the channel-quad cost volume is fp32 or bf16, got %s" % (cv_dtype,))
+        op = ops.cost_volume_c4 if cv_dtype == torch.float32 else ops.cost_volume_c4_bf16
+        cv = op(feature_maps, K_batch, R_batch, T_batch, d_min, d_int, int(batch_size), int(n_views),
+                int(d_begin), int(d_count), float(d_scale))
         return cv, d_batch_0, reference_indices(batch_size, n_views)
     if cv_dtype == torch.float32:
         op = ops.cost_volume

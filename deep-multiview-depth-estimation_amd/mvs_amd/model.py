@@ -147,15 +147,16 @@ class CostVolumeReg(nn.Module):
         self.live_region = True
 
     def forward(self, cv):
-        """cv [B, C, D, H, W], or the channel-quad [B, C/4, D, H, W, 4] of ops.cost_volume_c4 (HIP
-        inference feed, MVSNet.forward); the latter is read in place by the HIP live path and
-        re-laid to NCDHW for any other path."""
+        """cv [B, C, D, H, W], or the channel-quad [B, C/4, D, H, W, 4] of ops.cost_volume_c4 (fp32)
+        or ops.cost_volume_c4_bf16 (the bf16 opt-in) -- the HIP inference feed of MVSNet.forward; the
+        latter is read in place by the HIP live paths (bf16 widened on load, fp32 arithmetic) and
+        re-laid to NCDHW fp32 for any other path."""
         if cv.dim() == 6:
-            if self.live_ok(cv.shape[2:5]) and _hip_inference(cv):
+            if self.live_ok(cv.shape[2:5]) and _hip_cv(cv):
                 return self.forward_live(cv)
-            if self.live_train_ok(cv.shape[2:5]) and _hip_inference(cv):
+            if self.live_train_ok(cv.shape[2:5]) and _hip_cv(cv):
                 return self.forward_live_train(cv)
-            cv = cv.permute(0, 1, 5, 2, 3, 4).reshape((cv.shape[0], 4 * cv.shape[1]) + tuple(cv.shape[2:5]))
+            cv = cv.permute(0, 1, 5, 2, 3, 4).reshape((cv.shape[0], 4 * cv.shape[1]) + tuple(cv.shape[2:5])).float()
         if self.live_ok(cv.shape[2:]):
             return self.forward_live(cv)
         if self.live_train_ok(cv.shape[2:]):
@@ -209,7 +210,7 @@ class CostVolumeReg(nn.Module):
         B = _tconv_input_region(full, n, self.pad)
         C2 = _tconv_input_region(B, n, self.pad)
         C3 = _tconv_input_region(C2, n, self.pad)
-        if _hip_inference(cv):
+        if _hip_cv(cv):
             return self._forward_live_hip(cv, n, B, C2, C3, c4)
         # torch layers (CPU, autograd): the same regions through PyTorch's convolutions
         y0 = act(self.BN_0, self.conv_0_0(cv))
@@ -295,7 +296,7 @@ class CostVolumeReg(nn.Module):
         R1, R2 = _grow(M, n, 1), _grow(M, n, 2)
         bsz = cv.shape[0]
         count = bsz * n[0] * n[1] * n[2]
-        if _hip_inference(cv):
+        if _hip_cv(cv):
             return self._forward_live_train_hip(cv, n, full, M, R1, R2, count)
         y0 = _narrow_conv(self.conv_0_0, cv)
         y0 = act(y0, _bn_train(self.BN_0, *_sums(y0), count))
@@ -412,6 +413,13 @@ def _hip_inference(x):
     full-resolution layers apply."""
     return (x.is_cuda and x.dtype == torch.float32 and not torch.is_grad_enabled()
             and not torch.is_autocast_enabled())
+
+
+def _hip_cv(cv):
+    """_hip_inference for the regulariser's input: also the bf16 channel-quad cost volume of the
+    reduced-precision opt-in (its HIP layers widen it to fp32 on load)."""
+    return _hip_inference(cv) or (cv.is_cuda and cv.dim() == 6 and cv.dtype == torch.bfloat16
+                                  and not torch.is_grad_enabled() and not torch.is_autocast_enabled())
 
 
 def _narrow_conv(conv, x):
@@ -636,9 +644,10 @@ class MVSNet(nn.Module):
         feature_maps = self.feature_encoder(nn_input)
         bf16 = c.cv_dtype == "bfloat16"
         reg = self.cost_volume_reg
-        # fp32 HIP inference on the live path: the cost volume goes straight to the regulariser's
-        # kernels in the channel-quad layout (ops.cost_volume_c4, the fused kernel's 16-byte store)
-        quads = (not bf16 and _hip_inference(feature_maps) and 2 <= n_views <= 8
+        # HIP inference on the live paths: the cost volume goes straight to the regulariser's kernels
+        # in the channel-quad layout (ops.cost_volume_c4: the fused kernel's 16-byte store; with the
+        # bf16 opt-in ops.cost_volume_c4_bf16, 8 bytes)
+        quads = (_hip_inference(feature_maps) and 2 <= n_views <= 8
                  and feature_maps.shape[1] % 4 == 0
                  and (reg.live_ok((c.d_num,) + tuple(feature_maps.shape[2:]))
                       or reg.live_train_ok((c.d_num,) + tuple(feature_maps.shape[2:]))))
@@ -646,11 +655,11 @@ class MVSNet(nn.Module):
             K_batch, R_batch, T_batch, d_min, d_int, feature_maps, batch_size, n_views,
             d_num=c.d_num, d_scale=c.d_scale,
             cv_dtype=torch.bfloat16 if bf16 else torch.float32, channel_quads=quads)
-        if bf16:   # opt-in: regulariser under bf16 autocast, fp32 probabilities
-            with torch.autocast(device.type, dtype=torch.bfloat16):
-                prob_volume = self.cost_volume_reg(cost_volume).float()
-        else:
-            prob_volume = self.cost_volume_reg(cost_volume)
+        if bf16 and not quads:
+            # opt-in: the volume is STORED in bf16 (rounded once); the regulariser
+            # computes in fp32 from the rounded values, as the HIP channel-quad path does
+            cost_volume = cost_volume.float()
+        prob_volume = self.cost_volume_reg(cost_volume)
         initial_depth_map = extract_depth_map(prob_volume, d_batch, c.n_depth_est)
         return initial_depth_map, self.refine(nn_input, initial_depth_map, d_min, d_int, ref_views)
 

@@ -3,6 +3,7 @@
   mvs::cost_volume            fused warp + variance      (homography.py:6-92 + costvolume.py:3-16)
   mvs::cost_volume_bf16       same, bf16 cost volume     (SURVEY.md §8 f3, opt-in)
   mvs::cost_volume_c4         same, channel-quad layout  (inference feed of the HIP regulariser)
+  mvs::cost_volume_c4_bf16    same, bf16 channel-quad    (SURVEY.md §8 f3 opt-in inference feed)
   mvs::cost_volume_backward   d cv / d feat              (autograd of the above, train.py:103)
   mvs::homography_warp        warp only                  (homography.py:6-92 warped volume)
   mvs::assemble_cost_volume   variance of a warped volume (costvolume.py:3-16)
@@ -159,6 +160,42 @@ def cost_volume_c4(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torc
 def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scale):
     n, c, h, w = feat.shape
     return feat.new_empty((batch_size, c // 4, d_count, h, w, 4))
+
+
+@torch.library.custom_op("mvs::cost_volume_c4_bf16", mutates_args=())
+def cost_volume_c4_bf16(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.Tensor,
+                        d_min: torch.Tensor, d_int: torch.Tensor, batch_size: int, n_views: int,
+                        d_begin: int, d_count: int, d_scale: float) -> torch.Tensor:
+    """mvs::cost_volume_c4 stored in bf16 (SURVEY.md §8 f3 reduced-precision opt-in): the same
+    layout [B, C/4, d_count, h, w, 4], each value the fp32 variance rounded to nearest-even (equal to
+    cost_volume_c4(...).to(torch.bfloat16)); half the HBM write, and conv3d_k3 / conv3d_region (S2)
+    read it widened to fp32.  Inference only, 2 <= n_views <= 8, C % 4 == 0."""
+    _require_gpu(feat, "feature_maps")
+    lib = _lib.load()
+    feat = feat.to(_F32).contiguous()
+    K, R, T, d_min, d_int = _cams(K, R, T, d_min, d_int, feat.device, batch_size)
+    _check_geometry(feat, K, batch_size, n_views)
+    n, c, h, w = feat.shape
+    if c % 4:
+        raise ValueError("the channel-quad cost volume needs C % 4 == 0, got C=%d" % c)
+    cv = torch.empty((batch_size, c // 4, d_count, h, w, 4), device=feat.device, dtype=torch.bfloat16)
+    ws = torch.empty((_ws_floats(batch_size, n_views, c, h, w, d_count),), device=feat.device,
+                     dtype=_F32)
+    evs = (None, None)
+    if KERNEL_EVENT_HOOK is not None:
+        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK())
+    st = lib.mvs_cost_volume_fwd_c4_bf16(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T),
+                                         _lib.ptr(d_min), _lib.ptr(d_int), batch_size, n_views, c, h, w,
+                                         d_begin, d_count, float(d_scale), _lib.ptr(ws), _lib.ptr(cv),
+                                         _lib.stream_handle(feat.device), *evs)
+    _lib.check(st, "mvs_cost_volume_fwd_c4_bf16")
+    return cv
+
+
+@cost_volume_c4_bf16.register_fake
+def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scale):
+    n, c, h, w = feat.shape
+    return feat.new_empty((batch_size, c // 4, d_count, h, w, 4), dtype=torch.bfloat16)
 
 
 @torch.library.custom_op("mvs::cost_volume_backward", mutates_args=())
@@ -354,7 +391,8 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Te
     """nn.Conv3d(c_in, c_out, 3, stride=1, padding=1, bias=False) forward, c_out in {1, 8}, fp32
     NCDHW, on the HIP kernel (csrc/conv3d_narrow.hip); with bn_* given, max((y - mean) * scale +
     shift, 0) is fused (eval BN + ReLU).  ``in_c4``: x is the channel-quad [B, Cin/4, D, H, W, 4]
-    of cost_volume_c4.  ``wino_z`` (c_out = 8): Winograd F(2,3) along depth (MVS_CONV_WINO_Z; the
+    of cost_volume_c4 (fp32) or cost_volume_c4_bf16 (bf16: widened on load, fp32 arithmetic).
+    ``wino_z`` (c_out = 8): Winograd F(2,3) along depth (MVS_CONV_WINO_Z; the
     transformed weights are formed in float64 here).  Inference only (no autograd formula):
     CostVolumeReg uses it on the eval-mode, no-grad path."""
     _require_gpu(x, "x")
@@ -370,7 +408,8 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Te
         b, cin, d, h, wd = x.shape
     if weight.dim() != 5 or tuple(weight.shape[2:]) != (3, 3, 3) or weight.shape[1] != cin:
         raise ValueError("weight [Cout, %d, 3, 3, 3] expected, got %s" % (cin, tuple(weight.shape)))
-    x = x.to(_F32).contiguous()
+    quad_bf16 = in_c4 and x.dtype == torch.bfloat16
+    x = x.contiguous() if quad_bf16 else x.to(_F32).contiguous()
     cout = weight.shape[0]
     # the kernel reads weight[c_in][3][3][3][c_out] (pairs of output channels per 8-byte load)
     if wino_z and cout != 8:
@@ -385,7 +424,8 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Te
         raise ValueError("bn_scale, bn_shift and bn_mean go together")
     bp = [None if t is None else _lib.ptr(t) for t in bn]
     y = torch.empty((b, cout, d, h, wd), device=x.device, dtype=_F32)
-    flags = (_lib.MVS_CONV_IN_C4 if in_c4 else 0) | (_lib.MVS_CONV_WINO_Z if wino_z else 0)
+    flags = ((_lib.MVS_CONV_IN_C4 if in_c4 else 0) | (_lib.MVS_CONV_WINO_Z if wino_z else 0)
+             | (_lib.MVS_CONV_IN_BF16 if quad_bf16 else 0))
     st = lib.mvs_conv3d_k3_fwd(_lib.ptr(x), flags, _lib.ptr(w), _lib.ptr(y),
                                b, cin, cout, d, h, wd, *bp, _lib.stream_handle(x.device))
     _lib.check(st, "mvs_conv3d_k3_fwd")
@@ -577,13 +617,14 @@ def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Ten
                   bn_mean: Optional[torch.Tensor] = None, out_ncdhw: bool = False,
                   in_c4: bool = False) -> torch.Tensor:
     """Region convolution (mvs_conv3d_region_fwd): mode CONV_S2 reads the full NCDHW volume x
-    (in_c4: the channel-quad [B, C/4, D, H, W, 4] of cost_volume_c4),
+    (in_c4: the channel-quad [B, C/4, D, H, W, 4] of cost_volume_c4, or bf16 of cost_volume_c4_bf16),
     CONV_S1 / CONV_T2 a channels-last region tensor x (+ x2) on in_origin + [0, in_size); returns the
     channels-last region tensor [B, *out_size, c_out] ([B, c_out, *out_size] with out_ncdhw), eval
     BN + ReLU fused when bn_* are given.  ``weight`` is region_weight(module).  Inference only."""
     _require_gpu(x, "x")
     lib = _lib.load()
-    x = x.to(_F32).contiguous()
+    quad_bf16 = in_c4 and x.dtype == torch.bfloat16
+    x = x.contiguous() if quad_bf16 else x.to(_F32).contiguous()
     if x2 is not None:
         x2 = x2.to(_F32).contiguous()
     w = weight.to(device=x.device, dtype=_F32).contiguous()
@@ -594,7 +635,8 @@ def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Ten
         raise ValueError("bn_scale, bn_shift and bn_mean go together")
     shape = (b, cout) + tuple(out_size) if out_ncdhw else (b,) + tuple(out_size) + (cout,)
     y = torch.empty(shape, device=x.device, dtype=_F32)
-    flags = (_lib.MVS_CONV_OUT_NCDHW if out_ncdhw else 0) | (_lib.MVS_CONV_IN_C4 if in_c4 else 0)
+    flags = ((_lib.MVS_CONV_OUT_NCDHW if out_ncdhw else 0) | (_lib.MVS_CONV_IN_C4 if in_c4 else 0)
+             | (_lib.MVS_CONV_IN_BF16 if quad_bf16 else 0))
     st = lib.mvs_conv3d_region_fwd(int(mode), flags, _lib.ptr(x), None if x2 is None else _lib.ptr(x2), _lib.ptr(w),
                                    _lib.ptr(y), b, cin, cout, _ints3(dims), _ints3(out_origin), _ints3(out_size),
                                    None if in_origin is None else _ints3(in_origin),

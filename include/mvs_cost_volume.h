@@ -125,6 +125,21 @@ int mvs_cost_volume_fwd_c4(const float* feat, const float* K, const float* R, co
                            void* main_begin_event, void* main_end_event);
 
 /*
+ * mvs_cost_volume_fwd_c4 with bf16 storage (SURVEY.md §8 f3 reduced-precision cost volume, opt-in):
+ * cv_out[B][ceil(C/4)][d_count][h][w][4] bf16 (uint16 storage, 8-byte aligned), each element the fp32
+ * variance of mvs_cost_volume_fwd rounded to nearest-even (bit-identical to torch's .to(torch.bfloat16)
+ * of it); one 8-byte store per (pixel, plane, 4 channels), half the bytes of the fp32 layout.  Read by
+ * mvs_conv3d_k3_fwd / mvs_conv3d_region_fwd with MVS_CONV_IN_C4 | MVS_CONV_IN_BF16, which widen it to
+ * fp32 on load (exact) and compute in fp32.  2 <= n_views <= 8 or n_views == 1 (zeros).
+ */
+int mvs_cost_volume_fwd_c4_bf16(const float* feat, const float* K, const float* R, const float* T,
+                                const float* d_min, const float* d_int,
+                                int batch_size, int n_views, int channels, int h, int w,
+                                int d_begin, int d_count, float d_scale,
+                                float* workspace, void* cv_out, void* stream,
+                                void* main_begin_event, void* main_end_event);
+
+/*
  * Warp only (API-compatible homography_warping, homography.py:6-92):
  * warped[N][C][d_count][h][w].  Same workspace contract as mvs_cost_volume_fwd.
  */
@@ -203,6 +218,9 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
 /* input-layout flag of mvs_conv3d_k3_fwd / mvs_conv3d_region_fwd (MVS_CONV_S2): the volume is
  * channel-quad x[batch][c_in/4][D][H][W][4], the layout of mvs_cost_volume_fwd_c4 */
 #define MVS_CONV_IN_C4 2
+/* with MVS_CONV_IN_C4: the channel-quad volume is bf16 (mvs_cost_volume_fwd_c4_bf16, 8-byte aligned),
+ * widened to fp32 on load (exact); the arithmetic is the fp32 path's, bit for bit */
+#define MVS_CONV_IN_BF16 8
 /* flag of mvs_conv3d_k3_fwd (c_out = 8): Winograd F(2,3) along depth; the weight is then the
  * transformed wu[c_in][3][3][4][8]: per (c_in, ky, kx, c_out) the depth taps g0..g2 become
  * (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2) (formed in float64, rounded once) */

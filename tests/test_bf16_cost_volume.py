@@ -1,9 +1,12 @@
-"""Opt-in bf16 cost volume (reduced-precision cv behind a flag).
+"""Opt-in bf16 cost volume (reduced-precision cv behind a flag,
+MVSConfig(cv_dtype="bfloat16")).
 
-Parity bar: the bf16 kernel's output is BIT-IDENTICAL to the fp32 kernel's output rounded by torch's
-own float -> bfloat16 conversion (round to nearest even), on the same inputs -- the variance is
-computed in fp32 exactly as in the default path and rounded only in the store.  The fp32 path's
-parity with the reference is covered in test_gpu_parity.py.  The backward passes the rounding
+Parity bar: the bf16 kernels' output (NCDHW and channel-quad) is BIT-IDENTICAL to the fp32 kernel's
+output rounded by torch's own float -> bfloat16 conversion (round to nearest even), on the same
+inputs -- the variance is computed in fp32 exactly as in the default path and rounded only in the
+store.  Downstream, the regulariser's HIP layers widen the bf16 quads to fp32 on load (exact), so the
+whole bf16 inference step is BIT-IDENTICAL to the fp32 step run on the rounded volume.  The fp32
+path's parity with the reference is covered in test_gpu_parity.py.  The backward passes the rounding
 straight through: with the same (bf16-representable) upstream gradient it equals the fp32 op's
 gradient up to the float-atomic summation order.
 """
@@ -63,11 +66,10 @@ def test_bf16_backward_is_straight_through():
     assert (grads[0] - grads[1]).abs().max().item() <= 1e-5 * max(scale, 1.0)
 
 
-@pytest.mark.timeout(400)   # first bf16 Conv3d use compiles MIOpen kernels on a fresh box (~2 min)
 def test_bf16_mvsnet_runs_close_to_fp32():
-    """End to end with the opt-in: bf16 cv + bf16-autocast regulariser.  No parity claim against
-    the reference (reduced precision by design); bounded against the fp32 model: median relative
-    depth difference < 1 %."""
+    """End to end with the opt-in: bf16 cv, fp32 regulariser on the rounded values.  No parity
+    claim against the reference (reduced precision by design); bounded against the fp32 model:
+    median relative depth difference < 1 %."""
     from weights import deterministic_state_dict
     from mvs_amd.config import MVSConfig
     from mvs_amd.model import MVSNet
@@ -86,3 +88,90 @@ def test_bf16_mvsnet_runs_close_to_fp32():
         assert torch.isfinite(b).all()
         rel = ((a - b).abs() / a.abs().clamp_min(1.0)).median().item()
         assert rel < 1e-2, rel
+
+
+def _to_c4(x):
+    b, c = x.shape[:2]
+    return x.reshape((b, c // 4, 4) + tuple(x.shape[2:])).permute(0, 1, 3, 4, 5, 2).contiguous()
+
+
+@pytest.mark.parametrize("B,V,C,h,w,D", [(2, 3, 32, 64, 80, 24), (1, 5, 8, 37, 53, 7), (1, 2, 4, 16, 16, 3)])
+def test_bf16_channel_quad_is_rounded_fp32(B, V, C, h, w, D):
+    """mvs::cost_volume_c4_bf16 == mvs::cost_volume_c4(...).to(bfloat16), bit for bit, also for a
+    depth shard."""
+    from mvs_amd import ops
+    K, R, T = camera_batch(B, V, h, w)
+    d_min, d_int = depth_range(B, d_int=6.0, distinct=True)
+    f = features(B * V, C, h, w, seed=C + D).to(DEV)
+    for d_begin, d_count in ((0, D), (D // 3, D - D // 3)):
+        c32 = ops.cost_volume_c4(f, K, R, T, d_min, d_int, B, V, d_begin, d_count, 25.0)
+        c16 = ops.cost_volume_c4_bf16(f, K, R, T, d_min, d_int, B, V, d_begin, d_count, 25.0)
+        assert c16.dtype == torch.bfloat16 and c16.shape == c32.shape
+        assert torch.equal(c16.view(torch.int16), c32.to(torch.bfloat16).view(torch.int16))
+
+
+@pytest.mark.parametrize("cout,wino", [(8, True), (8, False), (1, False)])
+def test_narrow_conv_reads_bf16_quads_exactly(cout, wino):
+    """conv3d_k3 on the bf16 channel-quad volume == conv3d_k3 on the same values widened to fp32:
+    the widening is exact and the arithmetic the fp32 kernel's (bit-equal)."""
+    from mvs_amd.ops import conv3d_k3
+    g = torch.Generator().manual_seed(cout)
+    x = _to_c4(torch.randn(2, 32 if cout == 8 else 8, 9, 13, 37, generator=g)).to(torch.bfloat16).to(DEV)
+    wt = (torch.randn(cout, x.shape[1] * 4, 3, 3, 3, generator=g) * 0.1).to(DEV)
+    with torch.no_grad():
+        a = conv3d_k3(x, wt, in_c4=True, wino_z=wino)
+        b = conv3d_k3(x.float(), wt, in_c4=True, wino_z=wino)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("cout", [16, 32, 64])
+def test_region_s2_reads_bf16_quads_exactly(cout):
+    """conv3d_region (CONV_S2) on the bf16 channel-quad volume == on the widened fp32 quads."""
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _grow, _tconv_input_region
+    from mvs_amd.ops import CONV_S2, conv3d_region, region_weight
+    n = (24, 20, 26)
+    pad, _ = pad_outpad(*n)
+    Bx = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
+    out_reg = _grow(Bx, n, 1)
+    g = torch.Generator().manual_seed(cout)
+    x = _to_c4(torch.randn(2, 32, *n, generator=g)).to(torch.bfloat16).to(DEV)
+    w27 = region_weight(torch.nn.Conv3d(32, cout, 3)).detach().to(DEV)
+    args = (list(n), [lo for lo, _ in out_reg], [hi - lo + 1 for lo, hi in out_reg], None, None, list(pad))
+    with torch.no_grad():
+        a = conv3d_region(x, None, w27, CONV_S2, *args, in_c4=True)
+        b = conv3d_region(x.float(), None, w27, CONV_S2, *args, in_c4=True)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("train_bn", [False, True])
+def test_bf16_mvsnet_step_is_fp32_step_on_rounded_volume(train_bn):
+    """MVSNet.forward with cv_dtype="bfloat16" (the HIP channel-quad bf16 feed; BN eval, and the
+    test.py:61 train-mode-BN mode) == the fp32 network whose cost volume is rounded to bf16 and
+    widened back, bit for bit (initial depth and BN running statistics)."""
+    import copy
+    from weights import deterministic_state_dict
+    from mvs_amd import extract_depth_map, ops
+    from mvs_amd.config import MVSConfig
+    from mvs_amd.homography import depth_hypotheses
+    from mvs_amd.model import MVSNet
+    B, V, D, H, W = 2, 3, 16, 256, 320
+    K, R, T = camera_batch(B, V, H // 4, W // 4)
+    d_min, d_int = depth_range(B, d_int=4.0)
+    img = torch.randn(B * V, 3, H, W, generator=torch.Generator().manual_seed(6)).to(DEV)
+    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W, cv_dtype="bfloat16"))
+    net.load_state_dict(deterministic_state_dict(net.state_dict()))
+    net = net.to(DEV).train(train_bn)
+    ref = copy.deepcopy(net)
+    with torch.no_grad():
+        ini, _ = net(img, K, R, T, d_min, d_int, B, V)
+        feats = ref.feature_encoder(img)
+        cv = ops.cost_volume_c4(feats, K, R, T, d_min, d_int, B, V, 0, D, 25.0)
+        prob = ref.cost_volume_reg(cv.to(torch.bfloat16).float())
+        d_batch = depth_hypotheses(d_min, d_int, D, 25).to(DEV)
+        ini_ref = extract_depth_map(prob, d_batch)
+    assert torch.equal(ini, ini_ref)
+    if train_bn:
+        sa, sb = net.cost_volume_reg.state_dict(), ref.cost_volume_reg.state_dict()
+        for k in sb:
+            assert torch.equal(sa[k], sb[k]), k
