@@ -131,6 +131,12 @@ def _kept_planes(P, n_est):
     return (order < n_est).numpy()
 
 
+def _log(msg):
+    """Progress of the long end-to-end tests (a GPU run silent for minutes is taken to be hung)."""
+    import time
+    print("[%s] %s" % (time.strftime("%H:%M:%S"), msg), flush=True)
+
+
 def _prob_diff(live, full):
     """Live-region vs full-volume probabilities: max |diff| and max relative diff where P > 1e-6."""
     d = (live - full).abs()
@@ -177,10 +183,12 @@ def test_cfg2_end_to_end_as_benchmarked():
     cpu = []
     with torch.no_grad():
         for b in range(B):
+            _log("cfg2: CPU oracle forward of sample %d" % b)
             sl = slice(b * V, (b + 1) * V)
             c_ini, _, c_prob = mvs_oracle.mvsnet_forward(net, img[sl], K[sl], R[sl], T[sl], d_min[b:b + 1],
                                                          d_int[b:b + 1], 1, V, D, (H // 4, W // 4))
             cpu.append((c_ini[0, 0].numpy(), c_prob[0, 0].numpy()))
+        _log("cfg2: GPU forward (live) and forward_full")
         g = net.to(DEV)
         g_img = img.to(DEV)
         g_ini_full, g_ref = g(g_img, K, R, T, d_min, d_int, B, V)      # the benchmarked call
@@ -190,25 +198,28 @@ def test_cfg2_end_to_end_as_benchmarked():
         g_prob = g.cost_volume_reg(cv)
         g_ini = extract_depth_map(g_prob, d_batch)
         prob_full = g.cost_volume_reg.forward_full(cv)
-    assert torch.equal(g_ini, g_ini_full)
-    torch.testing.assert_close(g_prob, prob_full, rtol=1e-4, atol=1e-9)
-    flips, within, within_unflipped, worst = [], [], [], 0.0
+    flips, within, within_unflipped, worst, p_rel = [], [], [], [], []
     for b in range(B):
         c_ini, Pc = cpu[b]
         Pg = g_prob[b, 0].cpu().numpy()
-        np.testing.assert_allclose(Pg, Pc, rtol=2e-3, atol=1e-8)
+        p_rel.append(float((np.abs(Pg - Pc) / np.maximum(np.abs(Pc), 1e-8 / 2e-3)).max()))
         flip, rel = _depth_parity(Pg, Pc, g_ini_full[b, 0].cpu().numpy(), c_ini)
-        assert flip.mean() < 0.02, "sample %d: %.2f %% of pixels change their mask" % (b, 100 * flip.mean())
-        bad = (rel > 1e-4) & ~flip
-        assert bad.mean() <= 5e-4, "sample %d: %d unflipped pixels differ" % (b, bad.sum())
-        assert rel[~flip].max() <= 1e-2, rel[~flip].max()
         flips.append(float(flip.mean()))
         within.append(float((rel <= 1e-4).mean()))
         within_unflipped.append(float((rel[~flip] <= 1e-4).mean()))
-        worst = max(worst, float(rel[~flip].max()))
+        worst.append(float(rel[~flip].max()))
+    # the measured numbers first (recorded even when an assertion below fails)
     record_parity("cfg2_e2e_vs_cpu_oracle", samples=B, mask_flip_frac=flips, within_1e4_frac=within,
                   within_1e4_frac_unflipped=within_unflipped, max_rel_unflipped=worst,
-                  **_prob_diff(g_prob, prob_full))
+                  prob_max_rel_vs_cpu=p_rel, **_prob_diff(g_prob, prob_full))
+    assert torch.equal(g_ini, g_ini_full)
+    torch.testing.assert_close(g_prob, prob_full, rtol=1e-4, atol=1e-9)
+    for b in range(B):
+        np.testing.assert_allclose(g_prob[b, 0].cpu().numpy(), cpu[b][1], rtol=2e-3, atol=1e-8)
+        assert flips[b] < 0.02, "sample %d: %.2f %% of pixels change their mask" % (b, 100 * flips[b])
+        assert within_unflipped[b] >= 1 - 5e-4, "sample %d: %.4f of unflipped pixels within 1e-4" % (
+            b, within_unflipped[b])
+        assert worst[b] <= 1e-2, worst[b]
     # refinement (model.py:189-205) isolated: the CPU refine net applied to the GPU's own initial
     # depth must give the GPU's refined depth (the random-weight refine net amplifies initial-depth
     # differences ~1e3x at D=192, so comparing against the oracle's refined depth would test the
@@ -255,20 +266,21 @@ def test_model_end_to_end_at_cfg3_cfg5(cfg):
     K, R, T = camera_batch(B, V, H // 4, W // 4)
     d_min, d_int = depth_range(B)
     img = torch.randn(B * V, 3, H, W, generator=torch.Generator().manual_seed(2000 + B)).to(DEV)
+    _log("%s: GPU forward (live)" % cfg)
     with torch.no_grad():
         ini, ref = g(img, K, R, T, d_min, d_int, B, V)                 # the benchmarked call
         cv, d_batch, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, g.feature_encoder(img),
                                                        B, V, d_num=D)
         P_live = g.cost_volume_reg(cv)
         del cv
+        _log("%s: forward_full (MIOpen)" % cfg)
         P_full = g.cost_volume_reg.forward_full(
             warp_and_assemble_cost_volume(K, R, T, d_min, d_int, g.feature_encoder(img), B, V, d_num=D)[0])
         ini_live = extract_depth_map(P_live, d_batch)
-    assert torch.isfinite(ini).all() and torch.isfinite(ref).all()
-    assert torch.equal(ini_live, ini)
-    torch.testing.assert_close(P_live, P_full, rtol=1e-4, atol=1e-9)
+    torch.cuda.synchronize()
+    _log("%s: oracle soft-argmin (CPU)" % cfg)
     Pl, Pf, db = P_live.cpu(), P_full.cpu(), d_batch.cpu()
-    np.testing.assert_allclose(ini.cpu().numpy(), mvs_oracle.extract_depth_map(Pl, db).numpy(), rtol=1e-5, atol=0)
+    d_live_oracle = mvs_oracle.extract_depth_map(Pl, db).numpy()
     d_ref = mvs_oracle.extract_depth_map(Pf, db).numpy()
     flips, within, within_unflipped = [], [], []
     for b in range(B):
@@ -279,4 +291,8 @@ def test_model_end_to_end_at_cfg3_cfg5(cfg):
     record_parity("%s_e2e_live_vs_reference_sequence" % cfg, B=B, V=V, D=D, image_hw=[H, W],
                   mask_flip_frac=flips, within_1e4_frac=within, within_1e4_frac_unflipped=within_unflipped,
                   **_prob_diff(P_live, P_full))
+    assert torch.isfinite(ini).all() and torch.isfinite(ref).all()
+    assert torch.equal(ini_live, ini)
+    torch.testing.assert_close(P_live, P_full, rtol=1e-4, atol=1e-9)
+    np.testing.assert_allclose(ini.cpu().numpy(), d_live_oracle, rtol=1e-5, atol=0)
     assert max(flips) < 0.02 and min(within_unflipped) >= 0.9995, (flips, within_unflipped)
