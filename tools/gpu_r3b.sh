@@ -7,6 +7,9 @@ OUT=gpurun_out/r3b
 mkdir -p $OUT gpurun_out/miopen_db
 cp tools/miopen_db/*.txt gpurun_out/miopen_db/ 2>/dev/null
 export MIOPEN_USER_DB_PATH=$PWD/gpurun_out/miopen_db
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -w -o /tmp/store_c4 tools/microbench/store_c4_patterns.hip && \
+    timeout -k 10 120 /tmp/store_c4 > $OUT/store_c4_patterns.log 2>&1
+cat $OUT/store_c4_patterns.log
 timeout -k 10 780 python -u tools/miopen_find.py > $OUT/find.log 2>&1
 rc=$?
 tail -12 $OUT/find.log
