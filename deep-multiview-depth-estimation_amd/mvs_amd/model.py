@@ -212,6 +212,21 @@ class CostVolumeReg(nn.Module):
         C3 = _tconv_input_region(C2, n, self.pad)
         if _hip_cv(cv):
             return self._forward_live_hip(cv, n, B, C2, C3, c4)
+        return self._forward_live_torch(cv, n, B, C2, C3)
+
+    def forward_live_torch(self, cv):
+        """forward_live through PyTorch's convolutions (MIOpen on a HIP device) whatever the mode:
+        the same live regions, an implementation independent of the HIP kernels (test reference)."""
+        n = tuple(cv.shape[2:5])
+        full = tuple((0, d - 1) for d in n)
+        B = _tconv_input_region(full, n, self.pad)
+        C2 = _tconv_input_region(B, n, self.pad)
+        C3 = _tconv_input_region(C2, n, self.pad)
+        return self._forward_live_torch(cv, n, B, C2, C3)
+
+    def _forward_live_torch(self, cv, n, B, C2, C3):
+        act = lambda bn, y: self.ReLU(bn(y))
+        full = tuple((0, d - 1) for d in n)
         # torch layers (CPU, autograd): the same regions through PyTorch's convolutions
         y0 = act(self.BN_0, self.conv_0_0(cv))
         # level 1 on B, level 2 on C2, level 3 on C3 (regions carry their origin in the volume)

@@ -25,6 +25,28 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) -- parity of the HIP path")
 
 
+_CURRENT = ["-"]
+
+
+@pytest.fixture(autouse=True)
+def _heartbeat(request):
+    """A line on the real stderr every 60 s naming the running test (bypasses pytest's capture): the
+    long end-to-end GPU tests (CPU oracle forwards, float64 autograd) stay visibly alive."""
+    import threading
+    import time
+    _CURRENT[0] = request.node.nodeid
+    if not getattr(_heartbeat, "started", False):
+        _heartbeat.started = True
+
+        def beat():
+            t0 = time.time()
+            while True:
+                time.sleep(60)
+                print("[heartbeat %4.0f s] %s" % (time.time() - t0, _CURRENT[0]), file=sys.__stderr__, flush=True)
+        threading.Thread(target=beat, daemon=True).start()
+    yield
+
+
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN

@@ -124,11 +124,30 @@ def test_cfg5_full_resolution_planes():
         _close(cv[:, :, k:k + 1], _law(fn, K, R, T, d_min, d_int, 0, V, k))
 
 
-def _kept_planes(P, n_est):
-    """[D,h,w] -> boolean mask of the planes depthmap.py keeps (stable descending ranks)."""
+def _kept_planes(P, n_est, stable=True):
+    """[D,h,w] -> boolean mask of the planes depthmap.py keeps.  stable=True: ties in P ranked by
+    ascending plane index (the HIP kernel's rule); stable=False: torch.sort exactly as the reference
+    calls it (CPU introsort for D > 16: exact ties ordered arbitrarily)."""
     t = torch.from_numpy(np.ascontiguousarray(P))
-    _, order = torch.sort(t, dim=0, descending=True, stable=True)
+    _, order = torch.sort(t, dim=0, descending=True, stable=stable)
     return (order < n_est).numpy()
+
+
+def _stable_depth(P, d):
+    """depthmap.py:4-22 with the stable tie rule, float64: P [B,1,D,h,w], d [B,D,1,1] -> [B,1,h,w]."""
+    P = np.asarray(P, np.float64)
+    out = np.empty((P.shape[0], 1) + P.shape[3:])
+    for b in range(P.shape[0]):
+        m = _kept_planes(P[b, 0].astype(np.float32), 5)
+        num = (np.asarray(d, np.float64)[b].reshape(-1, 1, 1) * P[b, 0] * m).sum(0)
+        out[b, 0] = num / (P[b, 0] * m).sum(0)
+    return out
+
+
+def _tie_pixels(P):
+    """[D,h,w] -> pixels whose reference mask (torch.sort, unstable) differs from the stable rule:
+    an exact tie in P at the rank-5 boundary, decided arbitrarily by the reference's sort."""
+    return (_kept_planes(P, 5, stable=False) != _kept_planes(P, 5)).any(0)
 
 
 def _log(msg):
@@ -146,8 +165,10 @@ def _prob_diff(live, full):
 
 
 def _depth_parity(P_gpu, P_ref, d_gpu, d_ref):
-    """Mask flips and relative depth error of one sample: P [D, h, w], depth [h, w] (numpy)."""
-    flip = (_kept_planes(P_gpu, 5) != _kept_planes(P_ref, 5)).any(0)
+    """Mask flips and relative depth error of one sample: P [D, h, w], depth [h, w] (numpy).  A
+    pixel counts as flipped when the two P give different masks, or when the reference's own
+    (unstable-sort) mask is tie-ambiguous there."""
+    flip = (_kept_planes(P_gpu, 5) != _kept_planes(P_ref, 5)).any(0) | _tie_pixels(P_ref)
     rel = np.abs(d_gpu - d_ref) / np.abs(d_ref)
     return flip, rel
 
@@ -273,14 +294,28 @@ def test_model_end_to_end_at_cfg3_cfg5(cfg):
                                                        B, V, d_num=D)
         P_live = g.cost_volume_reg(cv)
         del cv
-        _log("%s: forward_full (MIOpen)" % cfg)
-        P_full = g.cost_volume_reg.forward_full(
-            warp_and_assemble_cost_volume(K, R, T, d_min, d_int, g.feature_encoder(img), B, V, d_num=D)[0])
+        cv = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, g.feature_encoder(img), B, V, d_num=D)[0]
+        if cfg == "cfg5":
+            # forward_full's conv_3_0 (32 -> 64, stride 2, padding 129/149/201) has only MIOpen's naive
+            # solver at this size (~10 s per call, the find-db): the reference sequence here is
+            # forward_live's PyTorch branch -- the same regions on MIOpen's implicit-GEMM convs, an
+            # implementation independent of the HIP kernels (forward_live == forward_full is pinned on
+            # the CPU at 8 geometries, tests/test_regulariser_live.py, and on the GPU at cfg 1-3)
+            ref_kind = "forward_live torch branch (MIOpen region convs)"
+            _log("%s: forward_live torch branch (MIOpen)" % cfg)
+            P_full = g.cost_volume_reg.forward_live_torch(cv)
+        else:
+            ref_kind = "forward_full (MIOpen, model.py:100-126 op sequence)"
+            _log("%s: forward_full (MIOpen)" % cfg)
+            P_full = g.cost_volume_reg.forward_full(cv)
+        del cv
         ini_live = extract_depth_map(P_live, d_batch)
     torch.cuda.synchronize()
     _log("%s: oracle soft-argmin (CPU)" % cfg)
     Pl, Pf, db = P_live.cpu(), P_full.cpu(), d_batch.cpu()
     d_live_oracle = mvs_oracle.extract_depth_map(Pl, db).numpy()
+    d_live_stable = _stable_depth(Pl.numpy(), db.numpy())
+    ties = np.stack([_tie_pixels(Pl[b, 0].numpy()) for b in range(B)])[:, None]
     d_ref = mvs_oracle.extract_depth_map(Pf, db).numpy()
     flips, within, within_unflipped = [], [], []
     for b in range(B):
@@ -288,11 +323,19 @@ def test_model_end_to_end_at_cfg3_cfg5(cfg):
         flips.append(float(flip.mean()))
         within.append(float((rel <= 1e-4).mean()))
         within_unflipped.append(float((rel[~flip] <= 1e-4).mean()))
+    g_ini = ini.cpu().numpy()
+    sa_rel = np.abs(g_ini - d_live_oracle) / np.abs(d_live_oracle)
     record_parity("%s_e2e_live_vs_reference_sequence" % cfg, B=B, V=V, D=D, image_hw=[H, W],
-                  mask_flip_frac=flips, within_1e4_frac=within, within_1e4_frac_unflipped=within_unflipped,
+                  reference=ref_kind, mask_flip_frac=flips, within_1e4_frac=within,
+                  within_1e4_frac_unflipped=within_unflipped, tie_pixel_frac=float(ties.mean()),
+                  soft_argmin_vs_oracle_max_rel_untied=float(sa_rel[~ties].max()),
                   **_prob_diff(P_live, P_full))
     assert torch.isfinite(ini).all() and torch.isfinite(ref).all()
     assert torch.equal(ini_live, ini)
     torch.testing.assert_close(P_live, P_full, rtol=1e-4, atol=1e-9)
-    np.testing.assert_allclose(ini.cpu().numpy(), d_live_oracle, rtol=1e-5, atol=0)
+    # the HIP soft-argmin on the live P: the oracle's (torch.sort) depth wherever the reference's mask
+    # is not tie-ambiguous, and the stable-rule float64 depth everywhere
+    assert ties.mean() < 1e-3, ties.mean()
+    np.testing.assert_allclose(g_ini[~ties], d_live_oracle[~ties], rtol=1e-5, atol=0)
+    np.testing.assert_allclose(g_ini, d_live_stable, rtol=1e-5, atol=0)
     assert max(flips) < 0.02 and min(within_unflipped) >= 0.9995, (flips, within_unflipped)
