@@ -65,7 +65,11 @@ __device__ inline void store_out(float* __restrict__ y, const Geo& g, int b, int
   else y[((size_t)b * rvol + vox) * CO + co] = v;
 }
 
-template <int MODE, int CI, int CO, int RB>
+// QM (S2 only): input layout of the volume -- 0 NCDHW, 1 fp32 channel quads, 2 bf16 channel quads --
+// a template parameter, so the K loop has no per-load layout branches and (S1 / S2: no parity
+// classes) unrolls into one basic block the scheduler can software-pipeline (loads of later taps
+// issued under the MFMAs of earlier ones)
+template <int MODE, int CI, int CO, int RB, int QM = 0>
 __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
     const float* __restrict__ x, const float* __restrict__ x2, const float* __restrict__ w,
     float* __restrict__ y, const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
@@ -148,8 +152,10 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
   // ---- K loop: taps by rows (tz, ty); per row and 16-channel block the A values of its (up to)
   // three x taps and every row block and the matching weights are loaded together, then fed to
   // the MFMAs (3x the loads in flight of a tap-at-a-time loop) ----
+#pragma unroll
   for (int tz = 0; tz < 3; ++tz) {
     if (MODE == kT2 && ((tz & 1) != par[0])) continue;   // t of o + P's parity only
+#pragma unroll
     for (int ty = 0; ty < 3; ++ty) {
       if (MODE == kT2 && ((ty & 1) != par[1])) continue;
       const int dz = MODE == kT2 ? -(tz >> 1) : tz, dy = MODE == kT2 ? -(ty >> 1) : ty;
@@ -171,12 +177,13 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
         const int c4 = cb * 16 + kq * 4;
         Rsrc rs, rs2;
         if constexpr (MODE == kS2) {
-          if (g.in_c4 == 2)   // bf16 quads: 8 bytes per voxel and quad
+          if constexpr (QM == 2)   // bf16 quads: 8 bytes per voxel and quad
             rs = make_rsrc(reinterpret_cast<const char*>(x) + ((size_t)b * (CI / 4) + cb * 4) * nvol * 8,
                            (uint32_t)(nvol * 32));
+          else if constexpr (QM == 1)
+            rs = make_rsrc(x + ((size_t)b * (CI / 4) + cb * 4) * nvol * 4, (uint32_t)(nvol * 64));
           else
-            rs = g.in_c4 ? make_rsrc(x + ((size_t)b * (CI / 4) + cb * 4) * nvol * 4, (uint32_t)(nvol * 64))
-                         : make_rsrc(x + ((size_t)b * CI + cb * 16) * nvol, (uint32_t)(nvol * 64));
+            rs = make_rsrc(x + ((size_t)b * CI + cb * 16) * nvol, (uint32_t)(nvol * 64));
         } else {
           rs = make_rsrc(x + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
           if (x2) rs2 = make_rsrc(x2 + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
@@ -190,13 +197,13 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
             const uint32_t vx = vox[tx][rb];
             f4v_t v;
             if constexpr (MODE == kS2) {
-              if (g.in_c4 == 2) {   // the bf16 quad: one 8-byte load, widened (exact)
+              if constexpr (QM == 2) {   // the bf16 quad: one 8-byte load, widened (exact)
                 typedef __attribute__((ext_vector_type(2))) unsigned v2u;
                 const v2u p = __builtin_amdgcn_raw_buffer_load_b64(
                     rs, (int)(vx == kOob ? kOob : ((uint32_t)kq * (uint32_t)nvol + vx) * 8u), 0, 0);
                 v = f4v_t{__uint_as_float(p.x << 16), __uint_as_float(p.x & 0xFFFF0000u),
                           __uint_as_float(p.y << 16), __uint_as_float(p.y & 0xFFFF0000u)};
-              } else if (g.in_c4) {   // the quad (c4 / 4) of the voxel: one 16-byte load
+              } else if constexpr (QM == 1) {   // the quad (c4 / 4) of the voxel: one 16-byte load
                 v = ld4(rs, vx == kOob ? kOob : ((uint32_t)kq * (uint32_t)nvol + vx) * 16u, 0);
               } else {
 #pragma unroll
@@ -254,7 +261,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
   }
 }
 
-template <int MODE, int CI, int CO, int RB>
+template <int MODE, int CI, int CO, int RB, int QM = 0>
 void launch_mode(const float* x, const float* x2, const float* w, float* y, const float* sc, const float* sh,
                  const float* mu, int B, const Geo& g, hipStream_t s) {
   const int classes = MODE == kT2 ? 8 : 1;
@@ -264,7 +271,8 @@ void launch_mode(const float* x, const float* x2, const float* w, float* y, cons
   const int rows = rz * ry * rx;
   const int per_block = (kBlock / 64) * 16 * RB;
   const dim3 grid((unsigned)((rows + per_block - 1) / per_block), (unsigned)classes, (unsigned)B);
-  hipLaunchKernelGGL((conv3d_region_kernel<MODE, CI, CO, RB>), grid, dim3(kBlock), 0, s, x, x2, w, y, sc, sh, mu, g);
+  hipLaunchKernelGGL((conv3d_region_kernel<MODE, CI, CO, RB, QM>), grid, dim3(kBlock), 0, s, x, x2, w, y, sc, sh, mu,
+                     g);
 }
 
 }  // namespace
@@ -290,12 +298,20 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
     launch_mode<MD, A, C, 2>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s);        \
     return MVS_OK;                                                                      \
   }
+#define MVS_REGION_S2(A, C)                                                                                   \
+  if (mode == kS2 && CI == A && CO == C) {                                                                    \
+    if (in_c4 == 2) launch_mode<kS2, A, C, 2, 2>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s);         \
+    else if (in_c4) launch_mode<kS2, A, C, 2, 1>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s);         \
+    else launch_mode<kS2, A, C, 2, 0>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s);                    \
+    return MVS_OK;                                                                                            \
+  }
   // S2: conv_1_0 / conv_2_0 / conv_3_0 (32 -> 16 / 32 / 64); S1: conv_k_1; T2: deconv_3_0 (64 -> 32),
   // deconv_2_0 (32 -> 16)
-  MVS_REGION_CASE(kS2, 32, 16) MVS_REGION_CASE(kS2, 32, 32) MVS_REGION_CASE(kS2, 32, 64)
+  MVS_REGION_S2(32, 16) MVS_REGION_S2(32, 32) MVS_REGION_S2(32, 64)
   MVS_REGION_CASE(kS1, 16, 16) MVS_REGION_CASE(kS1, 32, 32) MVS_REGION_CASE(kS1, 64, 64)
   MVS_REGION_CASE(kT2, 64, 32) MVS_REGION_CASE(kT2, 32, 16)
 #undef MVS_REGION_CASE
+#undef MVS_REGION_S2
   return MVS_ERR_INVALID_ARGUMENT;
 }
 

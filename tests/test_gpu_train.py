@@ -16,7 +16,7 @@ distance of the GPU gradient to the float64 gradient must be no larger than 3x t
 gradient's (+ 1e-4).  Both fp32 paths differ from float64 mostly through the soft-argmin's
 permutation mask (depthmap.py:11-15, discontinuous in P): a pixel whose mask flips changes its
 d depth / d P terms, and train-mode BatchNorm (flat P) makes such flips common, so the CPU's own
-error is the scale.  BatchNorm running statistics after the step: 1e-4 relative against the CPU.
+error is the scale.  BatchNorm running statistics after the step: no further from float64 than the CPU's (x 3).
 """
 import copy
 
@@ -91,9 +91,17 @@ def test_train_step_gradients_match_oracle_autograd():
     # the feature encoder's gradient flows back through the HIP cost-volume backward
     assert any(n.startswith("feature_encoder") and pg[n].grad.abs().max() > 0 for n in pg)
 
-    bg, bc = dict(net_g.named_buffers()), dict(net_c.named_buffers())
+    # BatchNorm running statistics after the step: the regulariser's and the encoder's are fed by the
+    # cost volume / images (fp32 noise only); the refinement's see the initial depth, whose flipped
+    # pixels differ between any two fp32 paths -- every buffer no further from float64 than the CPU
+    # fp32 reference's (x 3, + 1e-6 relative)
+    bg, bc, bd = dict(net_g.named_buffers()), dict(net_c.named_buffers()), dict(net_d.named_buffers())
     for name in sorted(bc):
-        torch.testing.assert_close(bg[name].cpu(), bc[name], rtol=1e-4, atol=1e-6, msg=name)
+        if name.endswith("num_batches_tracked"):
+            assert torch.equal(bg[name].cpu(), bc[name]), name
+            continue
+        e_g, e_c = _rel(bg[name].cpu(), bd[name]), _rel(bc[name], bd[name])
+        assert e_g <= 3.0 * e_c + 1e-6, "%s: GPU %.3g from float64, CPU fp32 %.3g" % (name, e_g, e_c)
 
     # one Adam step (train.py:104, Adam(model.parameters, lr) with the reference's list attribute)
     opt = torch.optim.Adam(net_g.parameters, lr=1e-3)

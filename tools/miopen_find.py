@@ -27,6 +27,7 @@ SHAPES = {
     "cfg1_train": (1, 3, 48, 512, 640, "train"),
     "smooth_train": (2, 3, 16, 256, 320, "train"),
     "cfg2_train": (4, 3, 192, 512, 640, "train"),
+    "cfg5_live_torch": (1, 3, 256, 1184, 1600, "live_torch"),
 }
 
 
@@ -42,13 +43,14 @@ def run(name, dev):
     net = bench.build_model(D, H, W, dev)
     img, K, R, T, d_min, d_int = bench.make_inputs(B, V, H, W, 0, dev)
     t = time.time()
-    if what == "full":
+    if what in ("full", "live_torch"):
         from mvs_amd import warp_and_assemble_cost_volume
         with torch.no_grad():
             feats = net.feature_encoder(img)
             cv, _, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, B, V, d_num=D)
+            reg = net.cost_volume_reg
             for _ in range(2):
-                net.cost_volume_reg.forward_full(cv)
+                reg.forward_full(cv) if what == "full" else reg.forward_live_torch(cv)
     else:
         net.train()
         opt = torch.optim.Adam(net.parameters, lr=1e-3)
