@@ -36,7 +36,7 @@ constexpr int kTX = 32, kTY = 8, kDT = 4;
 template <int COUT, int C4, bool WZ = false>
 __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
     const float* __restrict__ in, const float* __restrict__ wt, float* __restrict__ out, int Cin,
-    int D, int H, int W, int tiles_x, int tiles_y, int dgroups, const float* __restrict__ bn_scale,
+    int D, int H, int W, int tiles_x, int tiles_y, int dgroups, int n_batch, const float* __restrict__ bn_scale,
     const float* __restrict__ bn_shift, const float* __restrict__ bn_mean) {
   constexpr int kPX = kTX + 2, kPY = kTY + 2, kPD = kDT + 2;
   constexpr int kPlane = kPX * kPY;
@@ -45,7 +45,11 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   constexpr int NP = COUT / 2;                              // channel pairs (COUT = 8)
   constexpr int NQ = C4 ? 4 : 1;                            // channels staged per pass
   __shared__ float lds[NQ * kStage];
-  int t = blockIdx.x;
+  // XCD-contiguous tiles: the halo-sharing neighbours (next x tile, next y row of tiles, next depth
+  // group) run on the same XCD's L2 (common.h xcd_work_id)
+  const int total = (int)gridDim.x;
+  int t = xcd_work_id((int)blockIdx.x, total);
+  if (t >= tiles_x * tiles_y * dgroups * n_batch) return;   // grid padding (no barrier passed yet)
   const int tx0 = (t % tiles_x) * kTX;
   t /= tiles_x;
   const int ty0 = (t % tiles_y) * kTY;
@@ -236,9 +240,9 @@ template <int COUT, int C4, bool WZ = false>
 void launch_narrow(const float* in, const float* weight, float* out, int B, int Cin, int D, int H, int W,
                    const float* bn_scale, const float* bn_shift, const float* bn_mean, hipStream_t s) {
   const int tiles_x = (W + kTX - 1) / kTX, tiles_y = (H + kTY - 1) / kTY, dgroups = (D + kDT - 1) / kDT;
-  const dim3 grid((unsigned)((size_t)B * dgroups * tiles_y * tiles_x));
+  const dim3 grid = xcd_grid(B * dgroups * tiles_y * tiles_x);
   hipLaunchKernelGGL((conv3d_k3_narrow_kernel<COUT, C4, WZ>), grid, dim3(kBlock), 0, s, in, weight, out, Cin, D, H,
-                     W, tiles_x, tiles_y, dgroups, bn_scale, bn_shift, bn_mean);
+                     W, tiles_x, tiles_y, dgroups, B, bn_scale, bn_shift, bn_mean);
 }
 
 }  // namespace

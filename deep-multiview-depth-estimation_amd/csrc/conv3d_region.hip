@@ -99,7 +99,12 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
   const int rows = cn[0] * cn[1] * cn[2];
   const int step = MODE == kT2 ? 2 : 1;
   constexpr int kRows = 16 * RB;
-  const int row0 = ((int)blockIdx.x * (kBlock / 64) + ((int)threadIdx.x >> 6)) * kRows;
+  // XCD-contiguous row blocks (gridDim.x is a multiple of 8): workgroups are dealt round-robin over
+  // the 8 XCDs, so without the remap the neighbours that share input rows / planes (the next output
+  // row, the next plane ~ one row of workgroups later) sit in 8 different L2s; remapped, each XCD
+  // sweeps a contiguous run of the region and re-reads them from its own L2
+  const int bx = xcd_work_id((int)blockIdx.x, (int)gridDim.x);
+  const int row0 = (bx * (kBlock / 64) + ((int)threadIdx.x >> 6)) * kRows;
   if (row0 >= rows) return;   // wave-uniform; no barriers in this kernel
 
   // per row block: this lane's input base voxel in the addressed space (the volume for S2, the
@@ -270,7 +275,8 @@ void launch_mode(const float* x, const float* x2, const float* w, float* y, cons
             rx = MODE == kT2 ? (g.on[2] + 1) / 2 : g.on[2];
   const int rows = rz * ry * rx;
   const int per_block = (kBlock / 64) * 16 * RB;
-  const dim3 grid((unsigned)((rows + per_block - 1) / per_block), (unsigned)classes, (unsigned)B);
+  const int blocks = (rows + per_block - 1) / per_block;
+  const dim3 grid((unsigned)((blocks + 7) / 8 * 8), (unsigned)classes, (unsigned)B);   // XCD remap: multiple of 8
   hipLaunchKernelGGL((conv3d_region_kernel<MODE, CI, CO, RB, QM>), grid, dim3(kBlock), 0, s, x, x2, w, y, sc, sh, mu,
                      g);
 }

@@ -62,7 +62,8 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
     }
     __syncthreads();
   }
-  const size_t gid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  // XCD-contiguous blocks (gridDim.x a multiple of 8): neighbouring output rows share input rows
+  const size_t gid = (size_t)xcd_work_id((int)blockIdx.x, (int)gridDim.x) * kBlock + threadIdx.x;
   if (gid >= total) return;
   const int mw = (int)(gid % mw_n);
   size_t t = gid / mw_n;
@@ -369,7 +370,7 @@ void launch_deconv3d_k3s2(const float* x, const float* x2, int layout, int B, in
                           const float* bn_mean, const float* residual, float* y, hipStream_t s) {
   const int md_n = (D + 1) / 2, mh_n = (H + 1) / 2, mw_n = (W + 1) / 2;
   const size_t total = (size_t)B * md_n * mh_n * mw_n;
-  const dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
+  const dim3 grid = xcd_grid((int)((total + kBlock - 1) / kBlock));
   const size_t lds = layout == 1 ? (size_t)Cin * kCout * kWRow * sizeof(float) : 0;
   const int cls = (pd & 1) * 4 + (ph & 1) * 2 + (pw & 1);
 #define MVS_DECONV_CASE(c)                                                                         \
