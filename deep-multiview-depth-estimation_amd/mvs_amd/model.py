@@ -257,15 +257,13 @@ class CostVolumeReg(nn.Module):
 
         bn_eval = _bn_eval
 
-        # three independent branches until deconv_1_0, on three HIP streams: conv_0_0 (VALU-bound),
-        # level 1 (conv_1_0 -> conv_1_1, the longest MFMA chain) and levels 2-3 with the two deeper
-        # transposed convs (conv_2_*, conv_3_*, deconv_3_0, deconv_2_0); the region kernels are
-        # latency-bound, so branches running side by side fill each other's stalls
+        # conv_0_0 (VALU-bound) runs on a side stream, concurrently with the region chain (MFMA /
+        # memory-latency-bound) that does not need it until deconv_1_0.  (Levels 2-3 on a third
+        # stream beside level 1 measured no gain: 6.21-6.25 against 6.18-6.22 ms per cfg-2 step,
+        # tools/hip_reg_layers.py, profiles/r03e_reg_layers.log)
         main = torch.cuda.current_stream(cv.device)
         side = _side_stream(cv.device)
-        deep = _side_stream(cv.device, 1) if _LEVEL_STREAMS else main
-        for st in (side, deep):
-            st.wait_stream(main)
+        side.wait_stream(main)
         with torch.cuda.stream(side):
             y0 = conv3d_k3(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), in_c4=c4, wino_z=True)
         cv.record_stream(side)
@@ -277,20 +275,15 @@ class CostVolumeReg(nn.Module):
             # level 1's output only feeds deconv_1_0's input sum: channels-first for its loads
             return conv3d_region(ya, None, region_weight(conv_b), CONV_S1, dims, org(reg), size(reg),
                                  org(halo), size(halo), None, *bn_eval(bn), out_ncdhw=reg is B)
-        with torch.cuda.stream(deep):
-            y3 = level(self.conv_3_0, self.conv_3_1, self.BN_3, C3)
-            y2 = level(self.conv_2_0, self.conv_2_1, self.BN_2, C2)
-            y3 = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, org(C2), size(C2),
-                               org(C3), size(C3), pad, *bn_eval(self.BN_2))
-            y2 = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, org(B), size(B), org(C2),
-                               size(C2), pad, *bn_eval(self.BN_1), out_ncdhw=True)
-        if deep is not main:
-            cv.record_stream(deep)
         y1 = level(self.conv_1_0, self.conv_1_1, self.BN_1, B)
+        y2 = level(self.conv_2_0, self.conv_2_1, self.BN_2, C2)
+        y3 = level(self.conv_3_0, self.conv_3_1, self.BN_3, C3)
+        y3 = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, org(C2), size(C2),
+                           org(C3), size(C3), pad, *bn_eval(self.BN_2))
+        y2 = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, org(B), size(B), org(C2),
+                           size(C2), pad, *bn_eval(self.BN_1), out_ncdhw=True)
         main.wait_stream(side)
-        main.wait_stream(deep)
         y0.record_stream(main)
-        y2.record_stream(main)
         z = deconv3d_k3s2(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0, x2=y1)
         return softmax_depth(conv3d_k3(z, self.conv_out.weight))
 
@@ -422,12 +415,10 @@ class CostVolumeReg(nn.Module):
 
 
 _SIDE_STREAMS = {}
-# levels 2-3 of the eval-mode regulariser on their own stream (forward_live's HIP path)
-_LEVEL_STREAMS = True
 
 
 def _side_stream(device, which=0):
-    """Extra HIP streams per device (which = 0, 1) for independent branches of the inference step."""
+    """Extra HIP streams per device for independent branches of the inference step."""
     key = (torch.device(device).index, which)
     if key not in _SIDE_STREAMS:
         _SIDE_STREAMS[key] = torch.cuda.Stream(device)

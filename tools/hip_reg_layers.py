@@ -91,16 +91,13 @@ def main():
         for name, fn in layers.items():
             timed(name, fn, a.reps)
         step = lambda: net(img, K, R, T, d_min, d_int, B, V)
-        timed("eval step (3 streams)", step, a.reps)
-        M._LEVEL_STREAMS = False
-        timed("eval step (2 streams)", step, a.reps)
+        timed("eval step (side stream)", step, a.reps)
         saved = M._side_stream
         M._side_stream = lambda device, which=0: torch.cuda.current_stream(device)
         try:
             timed("eval step (serialised)", step, a.reps)
         finally:
             M._side_stream = saved
-            M._LEVEL_STREAMS = True
 
 
 if __name__ == "__main__":
