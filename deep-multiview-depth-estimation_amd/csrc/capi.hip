@@ -3,6 +3,10 @@
 // Validates arguments, lays out the caller-provided workspace and enqueues the launchers of the
 // other translation units on the caller's stream.  No allocation, no synchronisation, no global
 // mutable state: every entry point is re-entrant per stream and graph-capturable.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
 #include "launchers.h"
 
 namespace {
@@ -46,7 +50,8 @@ bool cams_ok(const float* K, const float* R, const float* T, const float* d_min,
 int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, const float* T,
                          const float* d_min, const float* d_int, int batch_size, int n_views,
                          int channels, int h, int w, int d_begin, int d_count, float d_scale,
-                         float* workspace, void* cv_out, int es, void* stream, void* ev0, void* ev1) {
+                         float* workspace, void* cv_out, int es, void* stream, void* ev0, void* ev1,
+                         uint32_t* absmax = nullptr) {
   if (!feat || !workspace || !cv_out) return MVS_ERR_INVALID_ARGUMENT;
   Geometry g;
   int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g, es);
@@ -54,6 +59,7 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
   if (!cams_ok(K, R, T, d_min, d_int) || d_begin < 0) return MVS_ERR_INVALID_ARGUMENT;
   const mvs::LaunchCheck lc;
   hipStream_t s = (hipStream_t)stream;
+  if (absmax && hipMemsetAsync(absmax, 0, 8 * sizeof(uint32_t), s) != hipSuccess) return MVS_ERR_HIP;
   if (n_views == 1) {  // the variance of a single view is identically zero (0 in fp32 and bf16)
     st = mvs_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
                             d_scale, workspace, stream);
@@ -72,7 +78,7 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
                                 (hipEvent_t)ev0, (hipEvent_t)ev1);
   else if (es == 16)
     mvs::launch_cost_volume_fwd_c4(g, feat, cm, workspace, packed, static_cast<float*>(cv_out), s,
-                                   (hipEvent_t)ev0, (hipEvent_t)ev1);
+                                   (hipEvent_t)ev0, (hipEvent_t)ev1, absmax);
   else if (es == 8)
     mvs::launch_cost_volume_fwd_c4_bf16(g, feat, cm, workspace, packed, cv_out, s, (hipEvent_t)ev0,
                                         (hipEvent_t)ev1);
@@ -163,6 +169,64 @@ int mvs_cost_volume_fwd_c4(const float* feat, const float* K, const float* R, co
   return cost_volume_fwd_impl(feat, K, R, T, d_min, d_int, batch_size, n_views, channels, h, w,
                               d_begin, d_count, d_scale, workspace, cv_out, 16, stream,
                               main_begin_event, main_end_event);
+}
+
+int mvs_cost_volume_fwd_c4_absmax(const float* feat, const float* K, const float* R, const float* T,
+                                  const float* d_min, const float* d_int, int batch_size, int n_views,
+                                  int channels, int h, int w, int d_begin, int d_count, float d_scale,
+                                  float* workspace, float* cv_out, void* stream, void* main_begin_event,
+                                  void* main_end_event, unsigned* feat_absmax) {
+  if (n_views > 8) return MVS_ERR_UNSUPPORTED_VIEWS;
+  if (((uintptr_t)cv_out & 15u) || !feat_absmax || ((uintptr_t)feat_absmax & 3u)) return MVS_ERR_INVALID_ARGUMENT;
+  return cost_volume_fwd_impl(feat, K, R, T, d_min, d_int, batch_size, n_views, channels, h, w,
+                              d_begin, d_count, d_scale, workspace, cv_out, 16, stream,
+                              main_begin_event, main_end_event, feat_absmax);
+}
+
+int mvs_conv3d_split_weights(const float* weight, unsigned short* frag, int* weight_exp) {
+  if (!weight || !frag || !weight_exp) return MVS_ERR_INVALID_ARGUMENT;
+  // scale 2^ew with max|w| 2^ew < 2^14 (all-zero weights: ew = 0)
+  float m = 0.0f;
+  for (int k = 0; k < 8 * 32 * 27; ++k) {
+    if (!std::isfinite(weight[k])) return MVS_ERR_INVALID_ARGUMENT;
+    m = std::max(m, std::fabs(weight[k]));
+  }
+  int e = 0;
+  if (m > 0.0f) (void)std::frexp(m, &e);
+  const int ew = m > 0.0f ? std::min(std::max(14 - e, -120), 120) : 0;
+  // frag[tap][lane][j]: lane (c = lane & 15, g = lane >> 4) holds B[k = 8g + j][col c] of the
+  // 16x16x32 MFMA, column c < 8 = w_hi of output channel c, c >= 8 = w_lo of channel c - 8, k = input
+  // channel; tap = (kz * 3 + ky) * 3 + kx; nn.Conv3d weight [8][32][3][3][3]
+  for (int tap = 0; tap < 27; ++tap)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int j = 0; j < 8; ++j) {
+        const int c = lane & 15, ci = 8 * (lane >> 4) + j, co = c & 7;
+        const float v = std::ldexp(weight[(co * 32 + ci) * 27 + tap], ew);
+        const _Float16 hi = (_Float16)v;
+        const _Float16 part = c < 8 ? hi : (_Float16)(v - (float)hi);
+        uint16_t bits;
+        std::memcpy(&bits, &part, 2);
+        frag[(tap * 64 + lane) * 8 + j] = bits;
+      }
+  *weight_exp = ew;
+  return MVS_OK;
+}
+
+int mvs_conv3d_k3_split_fwd(const float* x, const void* weight_frag, int weight_exp, const unsigned* x_absmax,
+                            float* y, int batch, int d, int h, int w, const float* bn_scale,
+                            const float* bn_shift, const float* bn_mean, void* stream) {
+  if (!x || !weight_frag || !y || batch <= 0 || d <= 0 || h <= 0 || w <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if (((uintptr_t)x & 15u) || ((uintptr_t)weight_frag & 15u) || ((uintptr_t)x_absmax & 3u))
+    return MVS_ERR_INVALID_ARGUMENT;
+  if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (weight_exp < -120 || weight_exp > 120) return MVS_ERR_INVALID_ARGUMENT;
+  // one 32-bit buffer descriptor per sample volume (8 quads of 16 B per voxel) and 32-bit staging offsets
+  if (128ull * (uint64_t)d * (uint64_t)h * (uint64_t)w > 0xFFFFFFF0ull) return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
+  const int st = mvs::launch_conv3d_split(x, weight_frag, weight_exp, x_absmax, y, batch, d, h, w, bn_scale,
+                                          bn_shift, bn_mean, (hipStream_t)stream);
+  return st != MVS_OK ? st : lc.status();
 }
 
 int mvs_cost_volume_fwd_c4_bf16(const float* feat, const float* K, const float* R, const float* T,

@@ -1,0 +1,279 @@
+// conv3d_split.hip -- conv_0_0 of CostVolumeReg (model.py:77, applied at model.py:101: 32 -> 8
+// channels, 3x3x3, stride 1, padding 1, then the eval BN_0 + ReLU) on the f16 matrix cores, with
+// fp32-level accuracy through split operands.
+//
+// Why: gfx950's fp32 MFMA runs at the fp32 VALU rate, 1/16 of the f16 MFMA.  conv_0_0 is 2.2e11
+// FLOP per cfg-2 step and compute-bound in fp32 (conv3d_narrow.hip: ~1.9 ms, VALU ~91 % busy).
+//
+// Split arithmetic.  Every fp32 operand v is scaled by a power of two (exact) and written as
+// v = hi + lo + r with hi = fp16(v), lo = fp16(v - hi) (round to nearest): |r| <= 2^-22 |v| for
+// v in fp16's normal range (lo below it is a subnormal with absolute error <= 2^-25, ~2^-39 of the
+// scaled maximum 2^14).  One 16x16x32 f16 MFMA with the weight operand's 16 columns laid out as
+// [8 output channels of w_hi | the same 8 of w_lo] gives x_hi*w_hi and x_hi*w_lo, a second one with
+// x_lo gives x_lo*w_hi and x_lo*w_lo: all four partial products, each exact in fp32 (11-bit x 11-bit
+// significands), accumulated by the MFMA in fp32.  Per product the error is that of the operand
+// residuals (~2^-21 relative) -- small against the fp32 accumulation error of the 864-term sums,
+// so the outputs carry fp32-level error (measured against float64 and the fp32 kernels in
+// tests/test_split_conv.py).  The scales: weights 2^ew with max|w| 2^ew < 2^14 (host, with the
+// fragments); the cost volume 2^ex with (max|feat|)^2 2^ex < 2^14 -- a variance over views is at
+// most max|x_v|^2, and mvs_cost_volume_fwd_c4 records max|feat| (per-XCD words) when asked.  The
+// output is the fp32 sum times 2^-(ex + ew), exact.
+//
+// GEMM mapping.  Rows = 16 consecutive x voxels of one output row (MFMA M), columns = 8 channels
+// x {hi, lo} weights (N = 16), K = the 32 input channels of one tap (one K-32 MFMA per tap and
+// split part).  Lane (i = l & 15, g = l >> 4) supplies channels 8g .. 8g + 7 of voxel i's tap
+// input: one ds_read_b128 per (tap, part).
+//
+// Tiling.  A 512-thread workgroup (8 waves, 2 per SIMD) owns a 16 x 8 (x, y) column of outputs,
+// one y row per wave, and walks kZC depths in steps of 4.  LDS holds 6 input planes (the 18 x 10
+// halo of the column, 32 channels, hi and lo parts: 23 KB per plane, 138 KB in all) as a ring; a
+// step reads planes zs-1 .. zs+4, and each (plane, ky, kx) A fragment feeds every output depth it
+// reaches (up to 3): 108 LDS reads for 216 MFMAs per wave and step.  The next step's 4 planes are
+// loaded into registers during the step (global loads in flight under the MFMAs) and split into
+// the freed ring slots after it.  Octets are swizzled by voxel column ((x >> 1) & 3), which makes
+// every ds_read_b128 lane group hit 16 distinct 16-byte bank groups for all three kx shifts.
+#include "launchers.h"
+#include "packed.h"
+
+namespace mvs {
+namespace {
+
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+
+constexpr int kSX = 16, kSY = 8, kZS = 4, kZC = 32;
+constexpr int kPX = kSX + 2, kPY = kSY + 2, kPV = kPX * kPY;   // 18 x 10 voxels per staged plane
+constexpr int kNPL = kZS + 2;                                   // resident planes (ring slots)
+constexpr int kVoxB = 64;                                       // 32 channels x fp16 per part
+constexpr int kRowB = kPX * kVoxB;                              // 1,152 B
+constexpr int kPartB = kPV * kVoxB;                             // 11,520 B
+constexpr int kSlotB = 2 * kPartB;                              // hi + lo parts
+constexpr int kLdsB = kNPL * kSlotB;                            // 138,240 B
+constexpr int kThreads = 512;
+constexpr int kPlaneQ = kPV * 8;                                // channel quads per plane: 1,440
+constexpr int kPre = (4 * kPlaneQ + kThreads - 1) / kThreads;  // 12 staging quads per thread
+constexpr uint32_t kOob = 0xFFFFFFF0u;                          // buffer offset past every descriptor
+
+// 2^e with bound * 2^e < 2^14 for every element of the cost volume: it is at most (max|feat|)^2
+__device__ inline int cv_split_exponent(const uint32_t* __restrict__ absmax) {
+  if (!absmax) return 0;
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m = max(m, absmax[i]);
+  if (m == 0u || m >= 0x7F800000u) return 0;   // all zero, or Inf/NaN present: unscaled
+  int e;
+  (void)frexpf(__uint_as_float(m), &e);   // max|feat| < 2^e
+  return min(max(14 - 2 * e, -120), 120);
+}
+
+// hi / lo fp16 parts of 4 fp32 values times 2^e, packed 2 per dword
+__device__ inline void split4(const f4v v, int e, uint2& hi, uint2& lo) {
+  const float s[4] = {ldexpf(v[0], e), ldexpf(v[1], e), ldexpf(v[2], e), ldexpf(v[3], e)};
+  _Float16 h[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    h[j] = (_Float16)s[j];
+    l[j] = (_Float16)(s[j] - (float)h[j]);
+  }
+  auto pk = [](_Float16 a, _Float16 b) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+  };
+  hi = make_uint2(pk(h[0], h[1]), pk(h[2], h[3]));
+  lo = make_uint2(pk(l[0], l[1]), pk(l[2], l[3]));
+}
+
+__device__ inline float ror8(float v) {   // value of lane (l ^ 8) inside each 16-lane row
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+}
+
+__global__ __launch_bounds__(kThreads) void conv0_split_kernel(
+    const f4v* __restrict__ cv, const h8v* __restrict__ wfrag, const uint32_t* __restrict__ absmax, int w_exp,
+    float* __restrict__ out, int D, int H, int W, int tiles_x, int tiles_y, int zchunks, int total,
+    const float* __restrict__ bn_scale, const float* __restrict__ bn_shift, const float* __restrict__ bn_mean) {
+  __shared__ __attribute__((aligned(16))) char lds[kLdsB];
+  const int wk = xcd_work_id((int)blockIdx.x, (int)gridDim.x);
+  if (wk >= total) return;   // workgroup-uniform, before any barrier
+  int t = wk;
+  const int x0 = (t % tiles_x) * kSX;
+  t /= tiles_x;
+  const int y0 = (t % tiles_y) * kSY;
+  t /= tiles_y;
+  const int z0 = (t % zchunks) * kZC;
+  const int b = t / zchunks;
+  const int z1 = min(z0 + kZC, D);
+  const int nsteps = (z1 - z0 + kZS - 1) / kZS;
+  const int ex = cv_split_exponent(absmax);
+  const int tid = (int)threadIdx.x;
+  const size_t HW = (size_t)H * W, DHW = (size_t)D * HW;
+  // the sample's volume through one buffer descriptor (8 D H W quads of 16 B <= 2^32 - 16, checked by
+  // the C ABI); out-of-range offsets read 0: halo outside the image and planes outside the volume
+  const uint64_t vbytes = 8ull * DHW * 16ull;
+  const Rsrc rcv = make_rsrc(cv + (size_t)b * 8 * DHW, (uint32_t)(vbytes < kOob ? vbytes : kOob));
+  const Rsrc rwf = make_rsrc(wfrag, 27u * 64u * 16u);
+
+  // ---- staging map: quad e = tid + 512 j of a 4-plane group -> (plane in group, global offset
+  // inside that plane's (quad) volume, LDS byte offset inside a ring slot) ----
+  // gpl: plane in the group (99: no element -- outside the image or past the group) << 16 | LDS
+  // byte offset inside a ring slot
+  int goff[kPre], gsl[kPre];
+#pragma unroll
+  for (int j = 0; j < kPre; ++j) {
+    const int e = tid + kThreads * j;
+    const int pl = e / kPlaneQ, r = e - pl * kPlaneQ;
+    const int q = r / kPV, v = r - q * kPV;
+    const int yy = v / kPX, xx = v - yy * kPX;
+    const int gy = y0 - 1 + yy, gx = x0 - 1 + xx;
+    const bool ok = e < 4 * kPlaneQ && gy >= 0 && gy < H && gx >= 0 && gx < W;
+    goff[j] = ok ? (int)((size_t)q * DHW + (size_t)gy * W + gx) : 0;
+    gsl[j] = ((ok ? pl : 99) << 16) | (v * kVoxB + (((q >> 1) ^ ((xx >> 1) & 3)) << 4) + ((q & 1) << 3));
+  }
+  f4v pre[kPre];
+  // planes zg .. zg + cnt - 1 -> registers (zero outside the volume)
+  auto fetch = [&](int zg, int cnt) {
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const int pl = gsl[j] >> 16, z = zg + pl;
+      const bool ok = pl < cnt && z >= 0 && z < D;
+      pre[j] = ld4(rcv, ok ? ((uint32_t)goff[j] + (uint32_t)z * (uint32_t)HW) * 16u : kOob, 0);
+    }
+  };
+  // registers -> ring slots (slot of the group's first plane: s0), split into hi / lo parts
+  auto stage = [&](int s0, int cnt) {
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const int pl = gsl[j] >> 16;
+      if (pl >= cnt) continue;   // 99: outside the image, the slot keeps the zeros written first
+      int s = s0 + pl;
+      s = s >= kNPL ? s - kNPL : s;
+      uint2 hi, lo;
+      split4(pre[j], ex, hi, lo);
+      char* p = lds + s * kSlotB + (gsl[j] & 0xFFFF);
+      *reinterpret_cast<uint2*>(p) = hi;
+      *reinterpret_cast<uint2*>(p + kPartB) = lo;
+    }
+  };
+  // halo voxels outside the image are never written by stage(): zero the whole ring once
+  for (int i = tid; i < kLdsB / 16; i += kThreads) reinterpret_cast<uint4*>(lds)[i] = make_uint4(0u, 0u, 0u, 0u);
+  fetch(z0 - 1, 4);
+  __syncthreads();
+  stage(0, 4);
+  fetch(z0 + 3, 2);
+  stage(4, 2);
+
+  // ---- per-lane constants ----
+  const int lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  // B fragments: 27 x 1 KB (wfrag[tap][lane]), read per step through L1 / L2
+  int aoff[3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) aoff[kx] = wave * kRowB + (i + kx) * kVoxB + ((g ^ (((i + kx) >> 1) & 3)) << 4);
+  const int co = lane & 7;
+  const float sc = bn_scale ? bn_scale[co] : 1.0f, sh = bn_scale ? bn_shift[co] : 0.0f,
+              mu = bn_scale ? bn_mean[co] : 0.0f;
+  const int oexp = -(ex + w_exp);
+  const int gy = y0 + wave;
+  const int gx0 = x0 + 4 * g;
+  const bool store_lane = (lane & 15) < 8 && gy < H;
+  const bool vec_store = (W & 3) == 0 && gx0 + 3 < W;
+  __syncthreads();
+
+  for (int k = 0; k < nsteps; ++k) {
+    const int zs = z0 + kZS * k;
+    if (k + 1 < nsteps) fetch(zs + 5, 4);   // the next step's new planes, in flight under the MFMAs
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    f4 ah[kZS], al[kZS];
+#pragma unroll
+    for (int d = 0; d < kZS; ++d) {
+      ah[d] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+      al[d] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+    const int sb = (kZS * k) % kNPL;   // ring slot of plane zs - 1
+    const char* base[kNPL];
+#pragma unroll
+    for (int p = 0; p < kNPL; ++p) base[p] = lds + (sb + p >= kNPL ? sb + p - kNPL : sb + p) * kSlotB;
+    // 54 items (ky, kx, p) in order; per item the A fragments (hi, lo) of plane p at tap (ky, kx)
+    // feed every output depth they reach (d = p - kz).  Software pipeline: the next item's A is
+    // read from LDS before this item's MFMAs, the next (ky, kx)'s 3 weight fragments (L1 / L2) at
+    // the start of this one's 6 items; the empty asm keeps the compiler from hoisting further loads
+    // (fully unrolled it would otherwise issue them all at once and spill)
+    auto lda = [&](int it, h8v& hi, h8v& lo) {
+      const int ky = it / 18, kx = (it / 6) % 3, p = it % 6;
+      hi = *reinterpret_cast<const h8v*>(base[p] + ky * kRowB + aoff[kx]);
+      lo = *reinterpret_cast<const h8v*>(base[p] + kPartB + ky * kRowB + aoff[kx]);
+    };
+    auto ldw = [&](int grp, h8v (&wb)[3]) {   // grp = ky * 3 + kx
+#pragma unroll
+      for (int kz = 0; kz < 3; ++kz)
+        wb[kz] = __builtin_bit_cast(h8v, __builtin_amdgcn_raw_buffer_load_b128(rwf, lane * 16, (kz * 9 + grp) * 1024, 0));
+    };
+    h8v wc[3], wn[3], ch, cl;
+    ldw(0, wc);
+    lda(0, ch, cl);
+#pragma unroll
+    for (int it = 0; it < 54; ++it) {
+      const int p = it % 6, grp = it / 6;
+      if (p == 0 && grp + 1 < 9) ldw(grp + 1, wn);
+      h8v nh = ch, nl = cl;
+      if (it + 1 < 54) lda(it + 1, nh, nl);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int kz = 0; kz < 3; ++kz) {
+        const int d = p - kz;   // output depth zs + d reads plane zs - 1 + p through tap kz
+        if (d < 0 || d >= kZS) continue;
+        ah[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch, wc[kz], ah[d], 0, 0, 0);
+        al[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cl, wc[kz], al[d], 0, 0, 0);
+      }
+      ch = nh;
+      cl = nl;
+      if (p == 5) {
+#pragma unroll
+        for (int kz = 0; kz < 3; ++kz) wc[kz] = wn[kz];
+      }
+    }
+    // ---- epilogue: lane (j < 8) of each row group adds its partner's (j + 8) w_lo columns;
+    // acc[r] = output (x = 4 g + r, channel j) ----
+#pragma unroll
+    for (int d = 0; d < kZS; ++d) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float hh = ah[d][r], lh = al[d][r];
+        const float hl = ror8(hh), ll = ror8(lh);
+        float s = ldexpf(hh + ((lh + hl) + ll), oexp);
+        if (bn_scale) s = fmaxf((s - mu) * sc + sh, 0.0f);
+        v[r] = s;
+      }
+      const int z = zs + d;
+      if (store_lane && z < z1) {
+        float* o = out + ((size_t)(b * 8 + co) * D + z) * HW + (size_t)gy * W + gx0;
+        if (vec_store) {
+          *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (gx0 + r < W) o[r] = v[r];
+        }
+      }
+    }
+    if (k + 1 < nsteps) {
+      __syncthreads();   // every wave is done with planes zs - 1 .. zs + 2
+      stage(sb, 4);      // planes zs + 5 .. zs + 8 replace them
+      __syncthreads();
+    }
+  }
+}
+
+}  // namespace
+
+int launch_conv3d_split(const float* x, const void* wfrag, int w_exp, const uint32_t* absmax, float* y, int B,
+                        int D, int H, int W, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                        hipStream_t s) {
+  const int tiles_x = (W + kSX - 1) / kSX, tiles_y = (H + kSY - 1) / kSY, zchunks = (D + kZC - 1) / kZC;
+  const long total = (long)tiles_x * tiles_y * zchunks * B;
+  if (total >= (1L << 31) - 8) return MVS_ERR_TOO_LARGE;
+  hipLaunchKernelGGL(conv0_split_kernel, xcd_grid((int)total), dim3(kThreads), 0, s,
+                     reinterpret_cast<const f4v*>(x), reinterpret_cast<const h8v*>(wfrag), absmax, w_exp, y, D, H,
+                     W, tiles_x, tiles_y, zchunks, (int)total, bn_scale, bn_shift, bn_mean);
+  return MVS_OK;
+}
+
+}  // namespace mvs

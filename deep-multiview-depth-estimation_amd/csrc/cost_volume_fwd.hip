@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kBlock) void prologue_kernel(const float* __restric
                                                           float* __restrict__ sampling,
                                                           float4* __restrict__ packed, float4* __restrict__ refs,
                                                           int B, int V, int C, int h, int w, int Dc, int nb_smp,
-                                                          int nb_pack) {
+                                                          int nb_pack, uint32_t* __restrict__ absmax) {
   const int N = B * V;
   const int c4 = (C + 3) / 4;
   const uint32_t hw = (uint32_t)h * (uint32_t)w;
@@ -142,6 +142,7 @@ __global__ __launch_bounds__(kBlock) void prologue_kernel(const float* __restric
   if (blk < nb_pack) {
     const PadGeom pg = pad_geom(h, w);
     const size_t n = (size_t)N * c4 * pg.plane;
+    uint32_t am = 0;   // max |feature| bits (absmax requested): bounds every variance by am^2
     for (size_t e = (size_t)blk * kBlock + threadIdx.x; e < n; e += (size_t)nb_pack * kBlock) {
       const uint32_t q = (uint32_t)(e % pg.plane);
       const size_t t = e / pg.plane;
@@ -158,6 +159,13 @@ __global__ __launch_bounds__(kBlock) void prologue_kernel(const float* __restric
         }
       }
       packed[e] = make_float4(v[0], v[1], v[2], v[3]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) am = max(am, __float_as_uint(v[j]) & 0x7FFFFFFFu);   // NaN > Inf > finite
+    }
+    if (absmax) {   // one atomic per wave, into the word of this XCD (workgroups go round-robin)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) am = max(am, (uint32_t)__shfl_xor((int)am, o));
+      if ((threadIdx.x & 63) == 0) atomicMax(absmax + (blockIdx.x & 7), am);
     }
     return;
   }
@@ -645,7 +653,7 @@ void launch_staged(int pg, dim3 grid, hipStream_t s, const float4* packed, const
 
 template <int V, int ES>
 void launch_gather(const Geometry& g, const float* feat, const Cams& cm, float* smp, float* ws, void* cv,
-                   hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+                   hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, uint32_t* absmax = nullptr) {
   const int c4 = (g.C + 3) / 4;
   const PadGeom pgeo = pad_geom(g.h, g.w);
   float4* packed = reinterpret_cast<float4*>(ws);
@@ -657,7 +665,7 @@ void launch_gather(const Geometry& g, const float* feat, const Cams& cm, float* 
   const uint32_t hw = (uint32_t)g.h * (uint32_t)g.w;
   const int nb_ref = (int)((hw + kBlock - 1) / kBlock) * g.B * c4;
   hipLaunchKernelGGL(prologue_kernel, dim3((unsigned)(nb_smp + nb_pack + nb_ref)), dim3(kBlock), 0, s, feat, cm,
-                     smp, packed, refs, g.B, V, g.C, g.h, g.w, g.Dc, nb_smp, nb_pack);
+                     smp, packed, refs, g.B, V, g.C, g.h, g.w, g.Dc, nb_smp, nb_pack, absmax);
   constexpr int TW = kTileW, TH = kTileH;
   const int tiles_x = (g.w + TW - 1) / TW, tiles_y = (g.h + TH - 1) / TH;
   // planes per workgroup: the register maximum, halved until the grid has >= 4 workgroups per CU
@@ -706,15 +714,16 @@ void launch_cost_volume_fwd_bf16(const Geometry& g, const float* feat, const Cam
 }
 
 void launch_cost_volume_fwd_c4(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
-                               float* packed, float* cv, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+                               float* packed, float* cv, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
+                               uint32_t* absmax) {
   switch (g.V) {
-    case 2: launch_gather<2, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
-    case 3: launch_gather<3, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
-    case 4: launch_gather<4, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
-    case 5: launch_gather<5, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
-    case 6: launch_gather<6, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
-    case 7: launch_gather<7, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
-    case 8: launch_gather<8, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1); break;
+    case 2: launch_gather<2, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
+    case 3: launch_gather<3, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
+    case 4: launch_gather<4, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
+    case 5: launch_gather<5, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
+    case 6: launch_gather<6, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
+    case 7: launch_gather<7, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
+    case 8: launch_gather<8, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
     default: break;   // rejected by the C ABI (2 <= V <= 8 only)
   }
 }

@@ -26,7 +26,7 @@ void launch_cost_volume_fwd(const Geometry& g, const float* feat, const Cams& cm
 // same, channel-quad layout cv[B][C/4][Dc][h][w][4] fp32, 2 <= V <= 8
 void launch_cost_volume_fwd_c4(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
                                float* packed, float* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
-                               hipEvent_t ev1 = nullptr);
+                               hipEvent_t ev1 = nullptr, uint32_t* absmax = nullptr);
 // same, bf16 channel-quad layout cv[B][C/4][Dc][h][w][4] (RNE), 2 <= V <= 8
 void launch_cost_volume_fwd_c4_bf16(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
                                     float* packed, void* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
@@ -61,6 +61,13 @@ void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, u
 void launch_conv3d_k3_narrow(const float* in, int in_c4, bool wino_z, const float* weight, float* out, int B,
                              int Cin, int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
                              const float* bn_mean, hipStream_t s);
+
+// conv3d_split.hip: conv_0_0 (32 -> 8, 3x3x3, padding 1) on the f16 MFMA with split-fp16 operands;
+// x channel-quad fp32 [B][8][D][H][W][4], wfrag [27][64][8] fp16 fragments (mvs_conv3d_split_weights),
+// absmax 8 words bounding max|feat| of the cost volume (or NULL: unscaled); y NCDHW fp32
+int launch_conv3d_split(const float* x, const void* wfrag, int w_exp, const uint32_t* absmax, float* y, int B,
+                        int D, int H, int W, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                        hipStream_t s);
 
 // conv2d_narrow.hip: bias-free Conv2d of the encoder / refinement (padding k/2), NCHW fp32, weights
 // wt[c_in][k][k][c_out], optional eval BN + ReLU epilogue; MVS_ERR_INVALID_ARGUMENT for a shape

@@ -12,7 +12,8 @@ SOURCES = [os.path.join(CSRC, f) for f in ("capi.hip", "plane_sampling.hip", "co
                                            "cost_volume_bwd.hip", "warp_variance.hip",
                                            "soft_argmin.hip", "dtu_input.hip",
                                            "conv3d_narrow.hip", "deconv3d_region.hip",
-                                           "conv3d_region.hip", "channel_ops.hip", "conv2d_narrow.hip")]
+                                           "conv3d_region.hip", "channel_ops.hip", "conv2d_narrow.hip",
+                                           "conv3d_split.hip")]
 HEADERS = [os.path.join(REPO_ROOT, "include", "mvs_cost_volume.h"),
            os.path.join(CSRC, "common.h"), os.path.join(CSRC, "launchers.h"),
            os.path.join(CSRC, "packed.h"), os.path.join(CSRC, "sampling_matrix.h")]

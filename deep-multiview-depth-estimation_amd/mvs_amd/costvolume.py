@@ -38,9 +38,15 @@ def warp_and_assemble_cost_volume(K_batch, R_batch, T_batch, d_min, d_int, featu
     if channel_quads:
         if cv_dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("the channel-quad cost volume is fp32 or bf16, got %s" % (cv_dtype,))
-        op = ops.cost_volume_c4 if cv_dtype == torch.float32 else ops.cost_volume_c4_bf16
-        cv = op(feature_maps, K_batch, R_batch, T_batch, d_min, d_int, int(batch_size), int(n_views),
+        args = (feature_maps, K_batch, R_batch, T_batch, d_min, d_int, int(batch_size), int(n_views),
                 int(d_begin), int(d_count), float(d_scale))
+        if cv_dtype == torch.float32:
+            # with its bound words (max |feat|), registered beside the tensor for the split-fp16
+            # conv_0_0 (ops.conv3d_k3_split)
+            cv, absmax = ops.cost_volume_c4_absmax(*args)
+            ops.register_cv_bound(cv, absmax)
+        else:
+            cv = ops.cost_volume_c4_bf16(*args)
         return cv, d_batch_0, reference_indices(batch_size, n_views)
     if cv_dtype == torch.float32:
         op = ops.cost_volume

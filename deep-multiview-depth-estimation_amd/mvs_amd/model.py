@@ -17,6 +17,7 @@ the reference (``model.py:164-166``) the instance attribute
 ``parameters`` is a LIST of tensors (``train.py:160`` passes it to Adam); use
 ``named_parameters()`` / ``state_dict()`` for module-generic code.
 """
+import os
 import warnings
 
 import torch
@@ -145,6 +146,10 @@ class CostVolumeReg(nn.Module):
         self.pad, self.outpad = tuple(pad), tuple(outpad)
         # eval-mode live-region evaluation (see forward_live); False = always the full-volume path
         self.live_region = True
+        # conv_0_0 of the HIP eval path on the f16 matrix cores with split-fp16 operands (fp32-level
+        # error, csrc/conv3d_split.hip) when the cost volume carries its bound words; False (or
+        # MVS_SPLIT_F16=0) = the exact-fp32 VALU kernel
+        self.split_f16 = os.environ.get("MVS_SPLIT_F16", "1") != "0"
 
     def forward(self, cv):
         """cv [B, C, D, H, W], or the channel-quad [B, C/4, D, H, W, 4] of ops.cost_volume_c4 (fp32)
@@ -249,8 +254,8 @@ class CostVolumeReg(nn.Module):
         ReLU fused (csrc/conv3d_region.hip), deconv_1_0 + BN_0 + ReLU + `+ y0` and the `y2 + y1`
         sum in one kernel (csrc/deconv3d_region.hip), conv_out (conv3d_narrow.hip).  ``c4``: cv is
         the channel-quad volume, read by conv_0_0 and the three stride-2 convs with 16-byte loads."""
-        from .ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_region, deconv3d_k3s2, region_weight,
-                          softmax_depth)
+        from .ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_k3_split, conv3d_region, cv_bound,
+                          deconv3d_k3s2, region_weight, softmax_depth)
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad = list(n), list(self.pad)
@@ -264,8 +269,13 @@ class CostVolumeReg(nn.Module):
         main = torch.cuda.current_stream(cv.device)
         side = _side_stream(cv.device)
         side.wait_stream(main)
+        bound = cv_bound(cv) if c4 and self.split_f16 and cv.dtype == torch.float32 else None
         with torch.cuda.stream(side):
-            y0 = conv3d_k3(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), in_c4=c4, wino_z=True)
+            if bound is not None:
+                y0 = conv3d_k3_split(cv, bound, self.conv_0_0.weight, *bn_eval(self.BN_0))
+                bound.record_stream(side)
+            else:
+                y0 = conv3d_k3(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), in_c4=c4, wino_z=True)
         cv.record_stream(side)
 
         def level(conv_a, conv_b, bn, reg):

@@ -162,6 +162,59 @@ def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scal
     return feat.new_empty((batch_size, c // 4, d_count, h, w, 4))
 
 
+@torch.library.custom_op("mvs::cost_volume_c4_absmax", mutates_args=())
+def cost_volume_c4_absmax(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.Tensor,
+                          d_min: torch.Tensor, d_int: torch.Tensor, batch_size: int, n_views: int,
+                          d_begin: int, d_count: int, d_scale: float) -> tuple[torch.Tensor, torch.Tensor]:
+    """cost_volume_c4 plus its bound words (mvs_cost_volume_fwd_c4_absmax): absmax int32[8] holds the
+    per-XCD maxima of the |feat| bit patterns, every cost-volume element is <= (the largest, as a
+    float)^2 -- what the split-fp16 conv_0_0 (conv3d_k3_split) scales its operands by."""
+    _require_gpu(feat, "feature_maps")
+    lib = _lib.load()
+    feat = feat.to(_F32).contiguous()
+    K, R, T, d_min, d_int = _cams(K, R, T, d_min, d_int, feat.device, batch_size)
+    _check_geometry(feat, K, batch_size, n_views)
+    n, c, h, w = feat.shape
+    if c % 4:
+        raise ValueError("the channel-quad cost volume needs C % 4 == 0, got C=%d" % c)
+    cv = torch.empty((batch_size, c // 4, d_count, h, w, 4), device=feat.device, dtype=_F32)
+    absmax = torch.empty((8,), device=feat.device, dtype=torch.int32)
+    ws = torch.empty((_ws_floats(batch_size, n_views, c, h, w, d_count),), device=feat.device,
+                     dtype=_F32)
+    evs = (None, None)
+    if KERNEL_EVENT_HOOK is not None:
+        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK())
+    st = lib.mvs_cost_volume_fwd_c4_absmax(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T),
+                                           _lib.ptr(d_min), _lib.ptr(d_int), batch_size, n_views, c, h, w,
+                                           d_begin, d_count, float(d_scale), _lib.ptr(ws), _lib.ptr(cv),
+                                           _lib.stream_handle(feat.device), *evs, _lib.ptr(absmax))
+    _lib.check(st, "mvs_cost_volume_fwd_c4_absmax")
+    return cv, absmax
+
+
+@cost_volume_c4_absmax.register_fake
+def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scale):
+    n, c, h, w = feat.shape
+    return feat.new_empty((batch_size, c // 4, d_count, h, w, 4)), feat.new_empty((8,), dtype=torch.int32)
+
+
+# bound words of channel-quad cost volumes made by cost_volume_c4_absmax (id(cv) -> (weak cv, words)):
+# CostVolumeReg keeps the reference's forward(cv) signature, so the bound travels beside the tensor
+_CV_BOUNDS = {}
+
+
+def register_cv_bound(cv, absmax):
+    key = id(cv)
+    _CV_BOUNDS[key] = (weakref.ref(cv, lambda _r: _CV_BOUNDS.pop(key, None)), absmax)
+    return cv
+
+
+def cv_bound(cv):
+    """The bound words registered for this cost-volume tensor, or None."""
+    hit = _CV_BOUNDS.get(id(cv))
+    return hit[1] if hit is not None and hit[0]() is cv else None
+
+
 @torch.library.custom_op("mvs::cost_volume_c4_bf16", mutates_args=())
 def cost_volume_c4_bf16(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.Tensor,
                         d_min: torch.Tensor, d_int: torch.Tensor, batch_size: int, n_views: int,
@@ -430,6 +483,57 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Te
                                b, cin, cout, d, h, wd, *bp, _lib.stream_handle(x.device))
     _lib.check(st, "mvs_conv3d_k3_fwd")
     return y
+
+
+@torch.library.custom_op("mvs::conv3d_k3_split", mutates_args=())
+def conv3d_k3_split(x: torch.Tensor, absmax: Optional[torch.Tensor], weight: torch.Tensor,
+                    bn_scale: Optional[torch.Tensor] = None, bn_shift: Optional[torch.Tensor] = None,
+                    bn_mean: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """conv_0_0 (nn.Conv3d(32, 8, 3, padding=1, bias=False), + eval BN + ReLU when bn_* are given)
+    over the channel-quad fp32 cost volume x [B, 8, D, H, W, 4] on the f16 matrix cores with split
+    operands (csrc/conv3d_split.hip, mvs_conv3d_k3_split_fwd): fp32-level error, not bit-equal to
+    conv3d_k3.  ``absmax``: the volume's bound words (cost_volume_c4_absmax); None = unscaled (every
+    |x| < 2^15 must hold).  Inference only."""
+    _require_gpu(x, "x")
+    lib = _lib.load()
+    if x.dim() != 6 or tuple(x.shape[1:2]) + tuple(x.shape[-1:]) != (8, 4) or x.dtype != _F32:
+        raise ValueError("x: fp32 channel-quad [B, 8, D, H, W, 4] expected, got %s %s" % (tuple(x.shape), x.dtype))
+    if tuple(weight.shape) != (8, 32, 3, 3, 3):
+        raise ValueError("weight [8, 32, 3, 3, 3] expected, got %s" % (tuple(weight.shape),))
+    x = x.contiguous()
+    b, _, d, h, wd, _ = x.shape
+    frag, wexp = derived("k3split", (weight,), lambda wt: split_weight_fragments(wt, x.device), x.device)
+    bn = [t if t is None else t.to(device=x.device, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
+    if any(t is None for t in bn) and not all(t is None for t in bn):
+        raise ValueError("bn_scale, bn_shift and bn_mean go together")
+    bp = [None if t is None else _lib.ptr(t) for t in bn]
+    if absmax is not None:
+        if absmax.numel() != 8 or absmax.dtype != torch.int32 or absmax.device != x.device:
+            raise ValueError("absmax: int32[8] on the volume's device expected")
+        absmax = absmax.contiguous()
+    y = torch.empty((b, 8, d, h, wd), device=x.device, dtype=_F32)
+    st = lib.mvs_conv3d_k3_split_fwd(_lib.ptr(x), _lib.ptr(frag), int(wexp),
+                                     None if absmax is None else _lib.ptr(absmax), _lib.ptr(y),
+                                     b, d, h, wd, *bp, _lib.stream_handle(x.device))
+    _lib.check(st, "mvs_conv3d_k3_split_fwd")
+    return y
+
+
+@conv3d_k3_split.register_fake
+def _(x, absmax, weight, bn_scale=None, bn_shift=None, bn_mean=None):
+    return x.new_empty((x.shape[0], 8) + tuple(x.shape[2:5]))
+
+
+def split_weight_fragments(weight, device):
+    """(fp16 MFMA fragments [27*64*8] int16 on ``device``, exponent) of conv_0_0's weight, formed on
+    the host by mvs_conv3d_split_weights (the C ABI's own split, so every caller gets the same)."""
+    lib = _lib.load()
+    w = weight.detach().to(device="cpu", dtype=_F32).contiguous()
+    frag = torch.empty((27 * 64 * 8,), dtype=torch.int16)
+    e = ctypes.c_int(0)
+    st = lib.mvs_conv3d_split_weights(_lib.ptr(w), _lib.ptr(frag), ctypes.byref(e))
+    _lib.check(st, "mvs_conv3d_split_weights")
+    return frag.to(device), e.value
 
 
 def _wino_z_weight(wt):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 6
+#define MVS_ABI_VERSION 7
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -123,6 +123,21 @@ int mvs_cost_volume_fwd_c4(const float* feat, const float* K, const float* R, co
                            int d_begin, int d_count, float d_scale,
                            float* workspace, float* cv_out, void* stream,
                            void* main_begin_event, void* main_end_event);
+
+/*
+ * mvs_cost_volume_fwd_c4 that also records a bound for the split-fp16 consumers
+ * (mvs_conv3d_k3_split_fwd): feat_absmax (8 uint32 words, DEVICE, 4-byte aligned) is zeroed on the
+ * stream and then receives, per XCD, the maximum of the |feat| bit patterns (NaN sorts above Inf
+ * above every finite value).  A variance over views is at most the largest squared sample, and a
+ * bilinear sample (zero padding) at most max|feat|, so every element of cv_out is <= B^2 with
+ * B = the float of the largest of the 8 words.  Otherwise as mvs_cost_volume_fwd_c4.
+ */
+int mvs_cost_volume_fwd_c4_absmax(const float* feat, const float* K, const float* R, const float* T,
+                                  const float* d_min, const float* d_int,
+                                  int batch_size, int n_views, int channels, int h, int w,
+                                  int d_begin, int d_count, float d_scale,
+                                  float* workspace, float* cv_out, void* stream,
+                                  void* main_begin_event, void* main_end_event, unsigned* feat_absmax);
 
 /*
  * mvs_cost_volume_fwd_c4 with bf16 storage (SURVEY.md §8 f3 reduced-precision cost volume, opt-in):
@@ -240,6 +255,29 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
 int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, int batch, int c_in,
                       int c_out, int d, int h, int w, const float* bn_scale, const float* bn_shift,
                       const float* bn_mean, void* stream);
+
+/* conv_0_0 (model.py:77, 101: nn.Conv3d(32, 8, 3, padding=1, bias=False) + optional eval BN_0 + ReLU)
+ * on the f16 matrix cores with split operands (csrc/conv3d_split.hip): every fp32 operand is scaled by
+ * a power of two and carried as fp16 hi + lo parts, the four partial products of each term are exact
+ * in fp32 and accumulated in fp32, so the result has fp32-level error.
+ *   x: the channel-quad cost volume x[batch][8][d][h][w][4] fp32 of mvs_cost_volume_fwd_c4(_absmax),
+ *      16-byte aligned; x_absmax: its 8 bound words (every |x| <= B^2, see
+ *      mvs_cost_volume_fwd_c4_absmax), DEVICE, or NULL when every |x| < 2^15 is known (unscaled);
+ *   weight_frag / weight_exp: from mvs_conv3d_split_weights (copied to the device, 16-byte aligned);
+ *   y[batch][8][d][h][w] fp32; BN pointers as mvs_conv3d_k3_fwd (8 floats each, all or none).
+ * 128*d*h*w <= 2^32 - 16 (one sample's volume bytes).  Replaces the Conv3d behind model.py:101's
+ * conv_0_0 in eval inference. */
+int mvs_conv3d_k3_split_fwd(const float* x, const void* weight_frag, int weight_exp, const unsigned* x_absmax,
+                            float* y, int batch, int d, int h, int w, const float* bn_scale,
+                            const float* bn_shift, const float* bn_mean, void* stream);
+
+/* HOST function (no device work): the fp16 MFMA operand fragments of conv_0_0's weight for
+ * mvs_conv3d_k3_split_fwd.  weight: nn.Conv3d layout [8][32][3][3][3] fp32, HOST, finite (else
+ * MVS_ERR_INVALID_ARGUMENT); frag: HOST, 27*64*8 uint16 (fp16 bits); *weight_exp = ew with
+ * max|w| * 2^ew < 2^14.  frag[tap][lane][j] (tap = (kz*3 + ky)*3 + kx): lane (c = lane & 15,
+ * g = lane >> 4) holds input channel 8g + j of column c: c < 8 the hi part of output channel c,
+ * c >= 8 the lo part of channel c - 8, where hi = fp16(w 2^ew), lo = fp16(w 2^ew - hi), nearest. */
+int mvs_conv3d_split_weights(const float* weight, unsigned short* frag, int* weight_exp);
 
 /* Feature encoder and refinement layers (model.py:22-65 FeatureEncoder, model.py:134-145): nn.Conv2d(
  * c_in, c_out, k, stride, padding=k/2, bias=False) over x[n][c_in][h][w] fp32 into

@@ -30,8 +30,10 @@ _CURRENT = ["-"]
 
 @pytest.fixture(autouse=True)
 def _heartbeat(request):
-    """A line on the real stderr every 60 s naming the running test (bypasses pytest's capture): the
-    long end-to-end GPU tests (CPU oracle forwards, float64 autograd) stay visibly alive."""
+    """A line on the real stderr every 60 s naming the running test: the long end-to-end GPU tests
+    (CPU oracle forwards, float64 autograd) stay visibly alive.  pytest.ini selects
+    --capture=tee-sys (sys-level capture only), so fd 2 -- sys.__stderr__ -- is never redirected
+    into pytest's capture file, with or without -s."""
     import threading
     import time
     _CURRENT[0] = request.node.nodeid

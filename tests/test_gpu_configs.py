@@ -296,14 +296,17 @@ def test_model_end_to_end_at_cfg3_cfg5(cfg):
         del cv
         cv = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, g.feature_encoder(img), B, V, d_num=D)[0]
         if cfg == "cfg5":
-            # forward_full's conv_3_0 (32 -> 64, stride 2, padding 129/149/201) has only MIOpen's naive
-            # solver at this size (~10 s per call, the find-db): the reference sequence here is
-            # forward_live's PyTorch branch -- the same regions on MIOpen's implicit-GEMM convs, an
-            # implementation independent of the HIP kernels (forward_live == forward_full is pinned on
-            # the CPU at 8 geometries, tests/test_regulariser_live.py, and on the GPU at cfg 1-3)
-            ref_kind = "forward_live torch branch (MIOpen region convs)"
-            _log("%s: forward_live torch branch (MIOpen)" % cfg)
-            P_full = g.cost_volume_reg.forward_live_torch(cv)
+            # MIOpen has only slow solvers for several cfg-5 shapes (forward_full's conv_3_0 ~10 s per
+            # call; forward_live's torch branch ~7 minutes in all): the reference sequence here is
+            # forward_live's PyTorch branch with every Conv3d / ConvTranspose3d as one fp32 rocBLAS
+            # GEMM per tap (tests/tap_conv.py) -- independent of the HIP kernels and of MIOpen
+            # (forward_live == forward_full is pinned on the CPU at 8 geometries,
+            # tests/test_regulariser_live.py, and on the GPU at cfg 1-3)
+            from tap_conv import tap_convs
+            ref_kind = "forward_live torch branch, convs as per-tap fp32 GEMMs (tests/tap_conv.py)"
+            _log("%s: forward_live torch branch (tap GEMMs)" % cfg)
+            with tap_convs():
+                P_full = g.cost_volume_reg.forward_live_torch(cv)
         else:
             ref_kind = "forward_full (MIOpen, model.py:100-126 op sequence)"
             _log("%s: forward_full (MIOpen)" % cfg)

@@ -36,26 +36,16 @@ def _rel(a, ref):
 
 
 def test_train_step_gradients_match_oracle_autograd():
+    """The GPU step against the CPU oracle's, precomputed by tests/golden/make_train_step.py (the two
+    CPU autograd runs take ~4 minutes; the fixture holds the float64-law gradients / buffers and the
+    fp32 CPU run's distance to them)."""
     import mvs_oracle
-    from cameras import camera_batch, depth_range
-    from conftest import record_parity
-    from weights import deterministic_state_dict
-    from mvs_amd.config import MVSConfig
-    from mvs_amd.model import MVSNet
-    B, V, D, H, W = 1, 3, 48, 512, 640
-    h, w = H // 4, W // 4
-    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W), device=torch.device("cpu"))
-    net.load_state_dict(deterministic_state_dict(net.state_dict()))
-    net.train()
-    net_c, net_d = copy.deepcopy(net), copy.deepcopy(net).double()
+    from conftest import load_golden, record_parity
+    from make_train_step import GEOM, train_step_inputs
+    B, V, D, H, W = GEOM
+    gold = load_golden("train_step_cfg1.npz")
+    net, img, K, R, T, d_min, d_int, gt = train_step_inputs()
     net_g = copy.deepcopy(net).to(DEV)
-    rng = np.random.default_rng(77)
-    img = torch.from_numpy(rng.standard_normal((B * V, 3, H, W), dtype=np.float32))
-    K, R, T = camera_batch(B, V, h, w)
-    d_min, d_int = depth_range(B)
-    d_int = d_int.div(d_int)          # train.py:95
-    gt = torch.from_numpy((425.0 + 1200.0 * rng.random((B, 1, h, w))).astype(np.float32))
-    gt[torch.from_numpy(rng.random((B, 1, h, w)) < 0.1)] = 0.0     # invalid pixels (loss.py:8 mask)
 
     print("train step: GPU", flush=True)
     ini_g, ref_g = net_g(img.to(DEV), K, R, T, d_min, d_int, B, V)
@@ -63,23 +53,13 @@ def test_train_step_gradients_match_oracle_autograd():
     loss_g.backward()
     torch.cuda.synchronize()
 
-    print("train step: CPU fp32 oracle", flush=True)
-    ini_c, ref_c, _ = mvs_oracle.mvsnet_forward(net_c, img, K, R, T, d_min, d_int, B, V, D, (h, w))
-    loss_c, _, _ = mvs_oracle.loss_fcn(gt, ini_c, ref_c)
-    loss_c.backward()
-
-    print("train step: CPU float64 law", flush=True)
-    ini_d, ref_d, _ = mvs_oracle.mvsnet_forward64(net_d, img, K, R, T, d_min, d_int, B, V, D, (h, w))
-    loss_d, _, _ = mvs_oracle.loss_fcn(gt.double(), ini_d, ref_d)
-    loss_d.backward()
-
-    lg, lc, ld = loss_g.item(), loss_c.item(), loss_d.item()
+    lg, lc, ld = loss_g.item(), float(gold["loss_cpu_fp32"]), float(gold["loss_f64"])
     pg = dict(net_g.named_parameters())
-    pc = dict(net_c.named_parameters())
-    pd = dict(net_d.named_parameters())
-    assert set(pg) == set(pc) == set(pd) and len(pg) > 0
-    assert all(pg[n].grad is not None and pc[n].grad is not None for n in pd)
-    worst = {n: (_rel(pg[n].grad.cpu(), pd[n].grad), _rel(pc[n].grad, pd[n].grad)) for n in sorted(pd)}
+    names = sorted(k[4:] for k in gold.files if k.startswith("g64/"))
+    assert set(pg) == set(names) and len(pg) > 0
+    assert all(pg[n].grad is not None for n in names)
+    worst = {n: (_rel(pg[n].grad.cpu(), torch.from_numpy(gold["g64/" + n])), float(gold["ec/" + n]))
+             for n in names}
     record_parity("train_step_cfg1_grads", loss_gpu=lg, loss_cpu_fp32=lc, loss_f64=ld,
                   grad_rel_l2_gpu_vs_f64_max=max(v[0] for v in worst.values()),
                   grad_rel_l2_cpu_vs_f64_max=max(v[1] for v in worst.values()),
@@ -94,14 +74,19 @@ def test_train_step_gradients_match_oracle_autograd():
     # BatchNorm running statistics after the step: the regulariser's and the encoder's are fed by the
     # cost volume / images (fp32 noise only); the refinement's see the initial depth, whose flipped
     # pixels differ between any two fp32 paths -- every buffer no further from float64 than the CPU
-    # fp32 reference's (x 3, + 1e-6 relative)
-    bg, bc, bd = dict(net_g.named_buffers()), dict(net_c.named_buffers()), dict(net_d.named_buffers())
-    for name in sorted(bc):
+    # fp32 reference's (x 3), with a floor of 1e-5 relative: a mean / variance over 10^5-10^7
+    # elements summed in fp32 in another order than the CPU's (MIOpen's batch statistics) is
+    # ~1e-6 from float64 where the CPU's pairwise sums may happen to be 1e-7
+    bg = dict(net_g.named_buffers())
+    bufs = sorted(k[4:] for k in gold.files if k.startswith("b64/"))
+    assert set(bufs) == set(bg)
+    for name in bufs:
+        ref = torch.from_numpy(gold["b64/" + name])
         if name.endswith("num_batches_tracked"):
-            assert torch.equal(bg[name].cpu(), bc[name]), name
+            assert torch.equal(bg[name].cpu(), ref), name
             continue
-        e_g, e_c = _rel(bg[name].cpu(), bd[name]), _rel(bc[name], bd[name])
-        assert e_g <= 3.0 * e_c + 1e-6, "%s: GPU %.3g from float64, CPU fp32 %.3g" % (name, e_g, e_c)
+        e_g, e_c = _rel(bg[name].cpu(), ref), float(gold["ecb/" + name])
+        assert e_g <= 3.0 * e_c + 1e-5, "%s: GPU %.3g from float64, CPU fp32 %.3g" % (name, e_g, e_c)
 
     # one Adam step (train.py:104, Adam(model.parameters, lr) with the reference's list attribute)
     opt = torch.optim.Adam(net_g.parameters, lr=1e-3)

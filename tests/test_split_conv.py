@@ -1,0 +1,159 @@
+"""Split-fp16 conv_0_0 (csrc/conv3d_split.hip, mvs_conv3d_k3_split_fwd / ops.conv3d_k3_split).
+
+CPU (no GPU): the host-side weight split (mvs_conv3d_split_weights) -- fragment layout against the
+16x16x32 MFMA operand map, hi + lo within 2^-22 of the scaled weight, the exponent rule.
+
+GPU: the kernel against float64 (torch CPU) on the same volumes, and against the exact-fp32 kernel
+(conv3d_k3) and torch's fp32 Conv3d (MIOpen): the split arithmetic must carry fp32-level error --
+max error <= 1e-5 of the output scale and no more than 1.5x the larger of the two fp32 kernels'
+own errors (+ 1e-7 of scale).  Cases: ragged x / y tiles and depth chunks, with and without the fused
+eval BN + ReLU, volumes from the fused cost-volume kernel with their bound words, and synthetic
+volumes far outside fp16's range (values to 1e9, the bound scales them) and far below it (1e-6).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from mvs_amd import _lib
+
+
+def _split_host(w):
+    lib = _lib.load()
+    w = w.to(torch.float32).contiguous()
+    frag = torch.empty((27 * 64 * 8,), dtype=torch.int16)
+    e = ctypes.c_int(0)
+    st = lib.mvs_conv3d_split_weights(_lib.ptr(w), _lib.ptr(frag), ctypes.byref(e))
+    return st, frag.view(torch.float16).reshape(27, 64, 8).to(torch.float64), e.value
+
+
+def test_split_weights_layout_and_accuracy():
+    g = torch.Generator().manual_seed(5)
+    w = torch.randn(8, 32, 3, 3, 3, generator=g) * 0.05
+    st, frag, ew = _split_host(w)
+    assert st == 0
+    m = w.abs().max().item()
+    assert m * 2.0 ** ew < 2 ** 14 <= 2 * m * 2.0 ** ew          # the largest power of two that fits
+    ws = w.double() * 2.0 ** ew
+    lane = torch.arange(64)
+    col, grp = lane & 15, lane >> 4
+    for tap in (0, 4, 13, 26):
+        kz, ky, kx = tap // 9, (tap // 3) % 3, tap % 3
+        hi = torch.zeros(8, 32, dtype=torch.float64)
+        lo = torch.zeros(8, 32, dtype=torch.float64)
+        for l in range(64):
+            for j in range(8):
+                c, ci = int(col[l]), 8 * int(grp[l]) + j
+                (hi if c < 8 else lo)[c & 7, ci] = frag[tap, l, j]
+        ref = ws[:, :, kz, ky, kx]
+        assert torch.equal(hi, ref.to(torch.float16).double())            # hi = nearest fp16
+        assert (hi + lo - ref).abs().max() <= 2.0 ** -22 * ref.abs().max() + 2.0 ** -24
+
+
+def test_split_weights_rejects_non_finite():
+    w = torch.zeros(8, 32, 3, 3, 3)
+    st, _, ew = _split_host(w)
+    assert st == 0 and ew == 0
+    w[1, 2, 0, 1, 2] = float("nan")
+    assert _split_host(w)[0] == -1   # MVS_ERR_INVALID_ARGUMENT
+
+
+DEV = torch.device("cuda:0")
+
+
+def _bound_words(x_ncdhw):
+    """int32[8] bound words for a synthetic volume: sqrt(max|x|) rounded up, in word 3."""
+    b = np.float32(np.sqrt(float(x_ncdhw.abs().max())) * (1 + 1e-6))
+    words = torch.zeros(8, dtype=torch.int32)
+    words[3] = int(np.frombuffer(b.tobytes(), dtype=np.int32)[0])
+    return words
+
+
+def _to_c4(x):
+    b, c, d, h, w = x.shape
+    return x.reshape(b, c // 4, 4, d, h, w).permute(0, 1, 3, 4, 5, 2).contiguous()
+
+
+def _check(x, wt, bn, absmax, label):
+    from mvs_amd.ops import conv3d_k3, conv3d_k3_split
+    ref64 = torch.nn.functional.conv3d(x.double(), wt.double(), padding=1)
+    if bn is not None:
+        sc, sh, mu = (t.double()[:, None, None, None] for t in bn)
+        ref64 = torch.clamp((ref64 - mu) * sc + sh, min=0.0)
+    bdev = [t.to(DEV) for t in bn] if bn is not None else []
+    with torch.no_grad():
+        xc = _to_c4(x).to(DEV)
+        y = conv3d_k3_split(xc, None if absmax is None else absmax.to(DEV), wt.to(DEV), *bdev).cpu()
+        y32 = conv3d_k3(xc, wt.to(DEV), *bdev, in_c4=True).cpu()
+        yt = torch.nn.functional.conv3d(x.to(DEV), wt.to(DEV), padding=1)
+        if bn is not None:
+            sc, sh, mu = (t.to(DEV)[:, None, None, None] for t in bn)
+            yt = torch.clamp((yt - mu) * sc + sh, min=0.0)
+        yt = yt.cpu()
+    scale = ref64.abs().max().item()
+    err = (y.double() - ref64).abs().max().item()
+    err32 = (y32.double() - ref64).abs().max().item()
+    errt = (yt.double() - ref64).abs().max().item()
+    print("%s: split %.3g, fp32 kernel %.3g, MIOpen %.3g (scale %.3g)" % (label, err, err32, errt, scale))
+    assert torch.isfinite(y).all()
+    assert err <= 1e-5 * scale, (label, err, scale)
+    assert err <= 1.5 * max(err32, errt) + 1e-7 * scale, (label, err, err32, errt)
+    return err, err32, errt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(1, 9, 20, 33), (2, 37, 17, 48), (1, 64, 24, 160)])
+@pytest.mark.parametrize("bn", [False, True])
+def test_split_conv_synthetic(shape, bn):
+    """Ragged tiles (W not a multiple of 16 or 4, H of 8, D of 4 / 32), BN epilogue on / off, a
+    cost-volume-like non-negative input with its bound words."""
+    b, d, h, w = shape
+    g = torch.Generator().manual_seed(sum(shape) + bn)
+    x = torch.randn(b, 32, d, h, w, generator=g).square()
+    wt = torch.randn(8, 32, 3, 3, 3, generator=g) * 0.05
+    p = (torch.rand(8, generator=g) + 0.5, torch.randn(8, generator=g), torch.randn(8, generator=g) * 0.1) if bn else None
+    _check(x, wt, p, _bound_words(x), "synthetic %s bn=%s" % (shape, bn))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mag", [1e-6, 1.0, 1e9])
+def test_split_conv_magnitudes(mag):
+    """Values far below fp16's normal range and far above its maximum: the bound's power-of-two scale
+    keeps the split exact-ish (unscaled, 1e9 would overflow fp16)."""
+    g = torch.Generator().manual_seed(int(np.log10(mag)) + 40)
+    x = torch.rand(1, 32, 10, 16, 40, generator=g) * mag
+    wt = torch.randn(8, 32, 3, 3, 3, generator=g) * 3.0
+    _check(x, wt, None, _bound_words(x), "magnitude %g" % mag)
+
+
+@pytest.mark.gpu
+def test_split_conv_unscaled_small_values():
+    """absmax = None: unscaled (values < 2^15 by contract)."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(1, 32, 8, 12, 20, generator=g) * 100.0
+    wt = torch.randn(8, 32, 3, 3, 3, generator=g) * 0.05
+    _check(x, wt, None, None, "unscaled")
+
+
+@pytest.mark.gpu
+def test_split_conv_on_fused_cost_volume():
+    """The production pairing: cost_volume_c4_absmax (bound words from the prologue's max|feat|)
+    feeding conv3d_k3_split, B=2 V=3 with distinct depth ranges, against float64 of that volume;
+    every volume element within the bound."""
+    from cameras import camera_batch, depth_range, features
+    from mvs_amd import ops
+    B, V, C, h, w, D = 2, 3, 32, 40, 52, 12
+    K, R, T = camera_batch(B, V, h, w)
+    d_min, d_int = depth_range(B, d_int=4.0, distinct=True)
+    feat = features(B * V, C, h, w, seed=11) * 7.0
+    with torch.no_grad():
+        cv, absmax = ops.cost_volume_c4_absmax(feat.to(DEV), K, R, T, d_min, d_int, B, V, 0, D, 25.0)
+    words = absmax.cpu()
+    bound = np.frombuffer(words.numpy().astype(np.int32).tobytes(), dtype=np.float32).max()
+    assert bound == np.float32(feat.abs().max().item())          # exactly max|feat|
+    x = cv.cpu().permute(0, 1, 5, 2, 3, 4).reshape(B, C, D, h, w)
+    assert x.max().item() <= float(bound) ** 2
+    g = torch.Generator().manual_seed(12)
+    wt = torch.randn(8, 32, 3, 3, 3, generator=g) * 0.05
+    _check(x, wt, None, words, "fused cost volume")

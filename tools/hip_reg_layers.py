@@ -15,8 +15,8 @@ sys.path.insert(0, REPO)
 import bench  # noqa: E402
 import torch  # noqa: E402
 from mvs_amd import model as M  # noqa: E402
-from mvs_amd.ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_region, deconv3d_k3s2,  # noqa: E402
-                         region_weight, softmax_depth)
+from mvs_amd.ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_k3_split, conv3d_region,  # noqa: E402
+                         cv_bound, deconv3d_k3s2, region_weight, softmax_depth)
 
 
 def timed(name, fn, n):
@@ -57,7 +57,11 @@ def main():
         bn = M._bn_eval
         layers = {}
         layers["conv_0_0"] = lambda: conv3d_k3(cv, reg.conv_0_0.weight, *bn(reg.BN_0), in_c4=True, wino_z=True)
+        layers["conv_0_0_split"] = lambda: conv3d_k3_split(cv, cv_bound(cv), reg.conv_0_0.weight, *bn(reg.BN_0))
         y0 = layers["conv_0_0"]()
+        y0s = layers["conv_0_0_split"]()
+        print("conv_0_0 split vs exact fp32: max|d| %.3g (max|y| %.3g)"
+              % ((y0s - y0).abs().max().item(), y0.abs().max().item()), flush=True)
         lv = []
         for k, (ca, cb, bnm, r) in enumerate(((reg.conv_1_0, reg.conv_1_1, reg.BN_1, Bq),
                                               (reg.conv_2_0, reg.conv_2_1, reg.BN_2, C2),
@@ -92,6 +96,9 @@ def main():
             timed(name, fn, a.reps)
         step = lambda: net(img, K, R, T, d_min, d_int, B, V)
         timed("eval step (side stream)", step, a.reps)
+        reg.split_f16 = False
+        timed("eval step (exact fp32 conv_0_0)", step, a.reps)
+        reg.split_f16 = True
         saved = M._side_stream
         M._side_stream = lambda device, which=0: torch.cuda.current_stream(device)
         try:
