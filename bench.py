@@ -87,7 +87,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-planes", type=int, default=None, help="planes for the CPU sample")
     ap.add_argument("--kernel-only", action="store_true", help="skip the end-to-end forward")
-    ap.add_argument("--no-extra", action="store_true", help="skip the cfg 3/5 end-to-end and train-step fields")
+    ap.add_argument("--no-extra", action="store_true", help="skip the cfg 3/5 end-to-end fields")
+    ap.add_argument("--train-step", action="store_true",
+                    help="also time the train.py step (autograd through the full-volume regulariser)")
     ap.add_argument("--conv-search", choices=("on", "off"), default="off",
                     help="torch.backends.cudnn.benchmark (MIOpen find) for the regulariser convs")
     return ap.parse_args()
@@ -522,6 +524,24 @@ def main():
         ms_step = 1000.0 * dt / args.steps
         maps = (B * world if args.mode == "samples" else B) * args.steps
         result["value"] = maps / dt
+        # the same step with every product in exact fp32 (conv_0_0 on the fp32 VALU kernel instead
+        # of the split-fp16 MFMA kernel): reported beside value
+        reg = net.cost_volume_reg
+        if reg.split_f16:
+            reg.split_f16 = False
+            with torch.no_grad():
+                step()
+                barrier(world)
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    step()
+                barrier(world)
+                dte = time.perf_counter() - t0
+            reg.split_f16 = True
+            dte = max_over_ranks(dte, world, device)
+            result["exact_fp32"] = {"ms_per_step": 1000.0 * dte / args.steps,
+                                    "value": (B * world if args.mode == "samples" else B) * args.steps / dte}
+            log("exact-fp32 conv_0_0 step: %.2f ms/step" % result["exact_fp32"]["ms_per_step"])
         # the same step with the regulariser over the WHOLE volume (CostVolumeReg.forward_full,
         # the reference's op sequence) instead of its eval-mode live regions: reported beside
         # value so the gain of the live-region evaluation is visible
@@ -626,6 +646,13 @@ def main():
                            "packing + reference resampling) + cost_volume_staged kernel" % ("_c4" if quads else ""),
                      "op_GBps": alg / (op_ms * 1e-3) / 1e9},
     }
+    out["arithmetic"] = ("fp32 throughout, except conv_0_0 (model.py:101) in samples mode: f16 MFMA with "
+                         "split-fp16 operands (hi + lo parts, all four partial products, fp32 accumulation), "
+                         "max error 0.3-0.5x that of the exact fp32 kernels vs float64 "
+                         "(tests/test_split_conv.py, DESIGN.md 3.5)")
+    if "exact_fp32" in result:
+        out["exact_fp32_step"] = dict(result["exact_fp32"], unit="depth maps/s", note=(
+            "the same step with conv_0_0 on the exact-fp32 VALU kernel (MVS_SPLIT_F16=0)"))
     if "full" in result:
         out["full_volume_regulariser"] = dict(result["full"], unit="depth maps/s", note=(
             "same step with CostVolumeReg.forward_full (every voxel of every level, as "
@@ -645,6 +672,7 @@ def main():
         out["kernel_configs"] = kernel_configs(device, max(5, args.kernel_iters // 2))
         if not args.kernel_only and not args.no_extra:
             out["e2e_configs"] = e2e_configs(device, max(3, min(args.steps, 10)))
+        if args.train_step:
             out["train_step"] = train_step_bench(B, V, D, H, W, device, 3)
     # opt-in bf16 cost volume: informational, not the headline (reduced precision)
     _, bf_op_ms, bf_alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count, bf16=True)

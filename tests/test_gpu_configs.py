@@ -213,11 +213,17 @@ def test_cfg2_end_to_end_as_benchmarked():
         g = net.to(DEV)
         g_img = img.to(DEV)
         g_ini_full, g_ref = g(g_img, K, R, T, d_min, d_int, B, V)      # the benchmarked call
-        cv, d_batch, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, g.feature_encoder(g_img),
-                                                       B, V, d_num=D)
+        feats = g.feature_encoder(g_img)
+        # the benchmarked regulariser input: the channel-quad volume with its bound words (split-fp16
+        # conv_0_0); the NCDHW volume of the same values feeds the exact-fp32 live path and forward_full
+        cv4, d_batch, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, B, V, d_num=D,
+                                                        channel_quads=True)
         assert g.cost_volume_reg.live_region
-        g_prob = g.cost_volume_reg(cv)
+        g_prob = g.cost_volume_reg(cv4)
+        del cv4
         g_ini = extract_depth_map(g_prob, d_batch)
+        cv, _, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, B, V, d_num=D)
+        prob_exact = g.cost_volume_reg(cv)
         prob_full = g.cost_volume_reg.forward_full(cv)
     flips, within, within_unflipped, worst, p_rel = [], [], [], [], []
     for b in range(B):
@@ -232,9 +238,11 @@ def test_cfg2_end_to_end_as_benchmarked():
     # the measured numbers first (recorded even when an assertion below fails)
     record_parity("cfg2_e2e_vs_cpu_oracle", samples=B, mask_flip_frac=flips, within_1e4_frac=within,
                   within_1e4_frac_unflipped=within_unflipped, max_rel_unflipped=worst,
-                  prob_max_rel_vs_cpu=p_rel, **_prob_diff(g_prob, prob_full))
+                  prob_max_rel_vs_cpu=p_rel, **_prob_diff(g_prob, prob_full),
+                  split_vs_exact_fp32_conv_0_0=_prob_diff(g_prob, prob_exact))
     assert torch.equal(g_ini, g_ini_full)
     torch.testing.assert_close(g_prob, prob_full, rtol=1e-4, atol=1e-9)
+    torch.testing.assert_close(g_prob, prob_exact, rtol=1e-4, atol=1e-9)
     for b in range(B):
         np.testing.assert_allclose(g_prob[b, 0].cpu().numpy(), cpu[b][1], rtol=2e-3, atol=1e-8)
         assert flips[b] < 0.02, "sample %d: %.2f %% of pixels change their mask" % (b, 100 * flips[b])
@@ -264,8 +272,8 @@ def test_model_end_to_end_at_cfg3_cfg5(cfg):
     """MVSNet.forward end to end at cfg 3 (B=8, V=5, 640x512, D=192) and cfg 5 (B=1, V=3, 1600x1184
     full-resolution images -> 296x400 features, D=256), BN eval, no_grad, as bench.py's e2e_configs
     times it:
-      * the benchmarked call (channel-quad cost volume -> live-region HIP regulariser) gives the same
-        initial depth as the live path fed the NCDHW volume;
+      * the benchmarked call (channel-quad cost volume + bound words -> live-region HIP regulariser,
+        split-fp16 conv_0_0) gives the same initial depth as that regulariser path called directly;
       * live-path probabilities against CostVolumeReg.forward_full (the reference's op sequence,
         model.py:100-126, on MIOpen) on every voxel of every sample: 1e-4 relative;
       * the HIP soft-argmin on that P against the oracle's extract_depth_map (depthmap.py:4-22,
@@ -290,8 +298,9 @@ def test_model_end_to_end_at_cfg3_cfg5(cfg):
     _log("%s: GPU forward (live)" % cfg)
     with torch.no_grad():
         ini, ref = g(img, K, R, T, d_min, d_int, B, V)                 # the benchmarked call
+        # the benchmarked regulariser input (channel-quad volume + bound words: split-fp16 conv_0_0)
         cv, d_batch, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, g.feature_encoder(img),
-                                                       B, V, d_num=D)
+                                                       B, V, d_num=D, channel_quads=True)
         P_live = g.cost_volume_reg(cv)
         del cv
         cv = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, g.feature_encoder(img), B, V, d_num=D)[0]

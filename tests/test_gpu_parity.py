@@ -393,7 +393,9 @@ def test_mvsnet_end_to_end(mode):
         g_img = img.to(DEV)
         g_ini_full, g_ref = net(g_img, K, R, T, d_min, d_int, 1, 3)
         feats = net.feature_encoder(g_img)
-        cv, d_batch, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, 1, 3, d_num=D)
+        # the benchmarked feed: channel-quad volume + bound words (split-fp16 conv_0_0 in eval mode)
+        cv, d_batch, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, 1, 3, d_num=D,
+                                                       channel_quads=True)
         g_prob = net.cost_volume_reg(cv)
         g_ini = extract_depth_map(g_prob, d_batch)
     if mode == "eval":
@@ -434,7 +436,8 @@ def test_mvsnet_end_to_end(mode):
 
 def test_depth_sharded_single_rank_equals_model():
     """mvs_amd.depth_shards at world size 1 (one GPU here; N > 1 is covered by the gloo test and
-    the driver's multi-GPU bench) reproduces MVSNet.forward bit for bit."""
+    the driver's multi-GPU bench) reproduces MVSNet.forward bit for bit (exact-fp32 conv_0_0 on both:
+    the owner's regulariser reads the assembled NCDHW volume, which carries no bound words)."""
     from weights import deterministic_state_dict
     from cameras import camera_batch, depth_range
     from mvs_amd.config import MVSConfig
@@ -444,6 +447,7 @@ def test_depth_sharded_single_rank_equals_model():
     net = MVSNet(MVSConfig(d_num=D, in_h=256, in_w=320))
     net.load_state_dict(deterministic_state_dict(net.state_dict()))
     net = net.to(DEV).eval()
+    net.cost_volume_reg.split_f16 = False
     K, R, T = camera_batch(2, 3, 64, 80)
     d_min, d_int = depth_range(2, d_int=4.0)
     img = torch.from_numpy(np.random.default_rng(5).standard_normal((6, 3, 256, 320), dtype=np.float32)).to(DEV)
@@ -773,7 +777,10 @@ def test_region_conv_s2_channel_quad_input_is_bit_equal(cout):
 
 def test_mvsnet_channel_quad_feed_equals_ncdhw_feed():
     """MVSNet.forward's HIP inference feed (channel-quad cost volume into the live regulariser)
-    against the same network fed the NCDHW volume: identical depth maps."""
+    against the same network fed the NCDHW volume: identical depth maps with the exact-fp32
+    conv_0_0 (split_f16 off: the layouts carry the same values and sums); with the split-fp16
+    conv_0_0 (the default) the probabilities agree to fp32 level and the depth maps to 1e-4 outside
+    mask flips."""
     from cameras import camera_batch, depth_range
     from mvs_amd.config import MVSConfig
     from mvs_amd.model import MVSNet
@@ -786,6 +793,7 @@ def test_mvsnet_channel_quad_feed_equals_ncdhw_feed():
     img = torch.rand(B * V, 3, H, W, generator=torch.Generator().manual_seed(3)).to(DEV)
     calls = []
     orig = cvmod.warp_and_assemble_cost_volume
+    net.cost_volume_reg.split_f16 = False
 
     def spy(*a, **kw):
         calls.append(kw.get("channel_quads", False))
@@ -801,6 +809,19 @@ def test_mvsnet_channel_quad_feed_equals_ncdhw_feed():
             model_mod.warp_and_assemble_cost_volume = orig
     assert calls == [True]
     assert torch.equal(d4, d5) and torch.equal(r4, r5)
+    net.cost_volume_reg.split_f16 = True
+    with torch.no_grad():
+        feats = net.feature_encoder(img)
+        cv4, d_batch, _ = orig(K, R, T, d_min, d_int, feats, B, V, d_num=D, channel_quads=True)
+        p_split = net.cost_volume_reg(cv4)
+        cv, _, _ = orig(K, R, T, d_min, d_int, feats, B, V, d_num=D)
+        p_exact = net.cost_volume_reg(cv)
+        ds, _ = net(img, K, R, T, d_min, d_int, B, V)
+    torch.testing.assert_close(p_split, p_exact, rtol=1e-4, atol=1e-9)
+    flip = torch.from_numpy((_kept_planes(p_split[0, 0].cpu().numpy(), 5)
+                             != _kept_planes(p_exact[0, 0].cpu().numpy(), 5)).any(0))
+    rel = ((ds - d4).abs() / d4.abs())[0, 0].cpu()
+    assert flip.float().mean() < 0.02 and (rel[~flip] <= 1e-4).float().mean() >= 0.9995
 
 
 @pytest.mark.parametrize("channels_last,C,shape", [(True, 16, (2, 5, 7, 9)), (True, 64, (1, 6, 6, 10)),
