@@ -25,12 +25,12 @@
 // input: one ds_read_b128 per (tap, part).
 //
 // Tiling.  A 512-thread workgroup (8 waves, 2 per SIMD) owns a 16 x 8 (x, y) column of outputs,
-// one y row per wave, and walks kZC depths in steps of 4.  LDS holds 6 input planes (the 18 x 10
-// halo of the column, 32 channels, hi and lo parts: 23 KB per plane, 138 KB in all) as a ring; a
-// step reads planes zs-1 .. zs+4, and each (plane, ky, kx) A fragment feeds every output depth it
-// reaches (up to 3): 108 LDS reads for 216 MFMAs per wave and step.  The next step's 4 planes are
-// loaded into registers during the step (global loads in flight under the MFMAs) and split into
-// the freed ring slots after it.  Octets are swizzled by voxel column ((x >> 1) & 3), which makes
+// one y row per wave, and walks kZC depths in steps of 3.  LDS holds 5 input planes (the 18 x 10
+// halo of the column, 32 channels, hi and lo parts: 23 KB per plane, 115 KB in all) as a ring; a
+// step reads planes zs-1 .. zs+3, and each (plane, ky, kx) A fragment feeds every output depth it
+// reaches (up to 3): 90 LDS reads for 162 MFMAs per wave and step.  The weight fragments stay in
+// registers (108 VGPRs), so the step's only vector-memory loads are the next step's 3 planes,
+// issued at its start (in flight under the MFMAs) and split into the freed ring slots after it.  Octets are swizzled by voxel column ((x >> 1) & 3), which makes
 // every ds_read_b128 lane group hit 16 distinct 16-byte bank groups for all three kx shifts.
 #include "launchers.h"
 #include "packed.h"
@@ -40,17 +40,17 @@ namespace {
 
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 
-constexpr int kSX = 16, kSY = 8, kZS = 4, kZC = 32;
+constexpr int kSX = 16, kSY = 8, kZS = 3, kZC = 48;
 constexpr int kPX = kSX + 2, kPY = kSY + 2, kPV = kPX * kPY;   // 18 x 10 voxels per staged plane
 constexpr int kNPL = kZS + 2;                                   // resident planes (ring slots)
 constexpr int kVoxB = 64;                                       // 32 channels x fp16 per part
 constexpr int kRowB = kPX * kVoxB;                              // 1,152 B
 constexpr int kPartB = kPV * kVoxB;                             // 11,520 B
 constexpr int kSlotB = 2 * kPartB;                              // hi + lo parts
-constexpr int kLdsB = kNPL * kSlotB;                            // 138,240 B
+constexpr int kLdsB = kNPL * kSlotB;                            // 115,200 B
 constexpr int kThreads = 512;
 constexpr int kPlaneQ = kPV * 8;                                // channel quads per plane: 1,440
-constexpr int kPre = (4 * kPlaneQ + kThreads - 1) / kThreads;  // 12 staging quads per thread
+constexpr int kPre = (kZS * kPlaneQ + kThreads - 1) / kThreads;  // 9 staging quads per thread
 constexpr uint32_t kOob = 0xFFFFFFF0u;                          // buffer offset past every descriptor
 
 // 2^e with bound * 2^e < 2^14 for every element of the cost volume: it is at most (max|feat|)^2
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(kThreads) void conv0_split_kernel(
   const Rsrc rcv = make_rsrc(cv + (size_t)b * 8 * DHW, (uint32_t)(vbytes < kOob ? vbytes : kOob));
   const Rsrc rwf = make_rsrc(wfrag, 27u * 64u * 16u);
 
-  // ---- staging map: quad e = tid + 512 j of a 4-plane group -> (plane in group, global offset
+  // ---- staging map: quad e = tid + 512 j of a kZS-plane group -> (plane in group, global offset
   // inside that plane's (quad) volume, LDS byte offset inside a ring slot) ----
   // gpl: plane in the group (99: no element -- outside the image or past the group) << 16 | LDS
   // byte offset inside a ring slot
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(kThreads) void conv0_split_kernel(
     const int q = r / kPV, v = r - q * kPV;
     const int yy = v / kPX, xx = v - yy * kPX;
     const int gy = y0 - 1 + yy, gx = x0 - 1 + xx;
-    const bool ok = e < 4 * kPlaneQ && gy >= 0 && gy < H && gx >= 0 && gx < W;
+    const bool ok = e < kZS * kPlaneQ && gy >= 0 && gy < H && gx >= 0 && gx < W;
     goff[j] = ok ? (int)((size_t)q * DHW + (size_t)gy * W + gx) : 0;
     gsl[j] = ((ok ? pl : 99) << 16) | (v * kVoxB + (((q >> 1) ^ ((xx >> 1) & 3)) << 4) + ((q & 1) << 3));
   }
@@ -153,16 +153,21 @@ __global__ __launch_bounds__(kThreads) void conv0_split_kernel(
   };
   // halo voxels outside the image are never written by stage(): zero the whole ring once
   for (int i = tid; i < kLdsB / 16; i += kThreads) reinterpret_cast<uint4*>(lds)[i] = make_uint4(0u, 0u, 0u, 0u);
-  fetch(z0 - 1, 4);
+  fetch(z0 - 1, kZS);
   __syncthreads();
-  stage(0, 4);
-  fetch(z0 + 3, 2);
-  stage(4, 2);
+  stage(0, kZS);
+  fetch(z0 - 1 + kZS, kNPL - kZS);
+  stage(kZS, kNPL - kZS);
 
   // ---- per-lane constants ----
   const int lane = tid & 63, wave = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
-  // B fragments: 27 x 1 KB (wfrag[tap][lane]), read per step through L1 / L2
+  // B fragments (wfrag[tap][lane], 27 x 1 KB): held in registers for the whole kernel, so the MFMA
+  // loop issues no vector-memory load that a wait could make the plane prefetch drain for
+  h8v bw[27];
+#pragma unroll
+  for (int t = 0; t < 27; ++t)
+    bw[t] = __builtin_bit_cast(h8v, __builtin_amdgcn_raw_buffer_load_b128(rwf, lane * 16, t * 1024, 0));
   int aoff[3];
 #pragma unroll
   for (int kx = 0; kx < 3; ++kx) aoff[kx] = wave * kRowB + (i + kx) * kVoxB + ((g ^ (((i + kx) >> 1) & 3)) << 4);
@@ -178,7 +183,7 @@ __global__ __launch_bounds__(kThreads) void conv0_split_kernel(
 
   for (int k = 0; k < nsteps; ++k) {
     const int zs = z0 + kZS * k;
-    if (k + 1 < nsteps) fetch(zs + 5, 4);   // the next step's new planes, in flight under the MFMAs
+    if (k + 1 < nsteps) fetch(zs + kNPL - 1, kZS);   // the next step's new planes, in flight under the MFMAs
     typedef float f4 __attribute__((ext_vector_type(4)));
     f4 ah[kZS], al[kZS];
 #pragma unroll
@@ -190,44 +195,33 @@ __global__ __launch_bounds__(kThreads) void conv0_split_kernel(
     const char* base[kNPL];
 #pragma unroll
     for (int p = 0; p < kNPL; ++p) base[p] = lds + (sb + p >= kNPL ? sb + p - kNPL : sb + p) * kSlotB;
-    // 54 items (ky, kx, p) in order; per item the A fragments (hi, lo) of plane p at tap (ky, kx)
-    // feed every output depth they reach (d = p - kz).  Software pipeline: the next item's A is
-    // read from LDS before this item's MFMAs, the next (ky, kx)'s 3 weight fragments (L1 / L2) at
-    // the start of this one's 6 items; the empty asm keeps the compiler from hoisting further loads
+    // 45 items (ky, kx, p) in order; per item the A fragments (hi, lo) of plane p at tap (ky, kx)
+    // feed every output depth they reach (d = p - kz).  Software pipeline: the next item's A is read
+    // from LDS before this item's MFMAs; the empty asm keeps the compiler from hoisting further loads
     // (fully unrolled it would otherwise issue them all at once and spill)
+    constexpr int kItems = 9 * kNPL;
     auto lda = [&](int it, h8v& hi, h8v& lo) {
-      const int ky = it / 18, kx = (it / 6) % 3, p = it % 6;
+      const int grp = it / kNPL, p = it % kNPL, ky = grp / 3, kx = grp % 3;
       hi = *reinterpret_cast<const h8v*>(base[p] + ky * kRowB + aoff[kx]);
       lo = *reinterpret_cast<const h8v*>(base[p] + kPartB + ky * kRowB + aoff[kx]);
     };
-    auto ldw = [&](int grp, h8v (&wb)[3]) {   // grp = ky * 3 + kx
-#pragma unroll
-      for (int kz = 0; kz < 3; ++kz)
-        wb[kz] = __builtin_bit_cast(h8v, __builtin_amdgcn_raw_buffer_load_b128(rwf, lane * 16, (kz * 9 + grp) * 1024, 0));
-    };
-    h8v wc[3], wn[3], ch, cl;
-    ldw(0, wc);
+    h8v ch, cl;
     lda(0, ch, cl);
 #pragma unroll
-    for (int it = 0; it < 54; ++it) {
-      const int p = it % 6, grp = it / 6;
-      if (p == 0 && grp + 1 < 9) ldw(grp + 1, wn);
+    for (int it = 0; it < kItems; ++it) {
+      const int p = it % kNPL, grp = it / kNPL;
       h8v nh = ch, nl = cl;
-      if (it + 1 < 54) lda(it + 1, nh, nl);
+      if (it + 1 < kItems) lda(it + 1, nh, nl);
       asm volatile("" ::: "memory");
 #pragma unroll
       for (int kz = 0; kz < 3; ++kz) {
         const int d = p - kz;   // output depth zs + d reads plane zs - 1 + p through tap kz
         if (d < 0 || d >= kZS) continue;
-        ah[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch, wc[kz], ah[d], 0, 0, 0);
-        al[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cl, wc[kz], al[d], 0, 0, 0);
+        ah[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch, bw[kz * 9 + grp], ah[d], 0, 0, 0);
+        al[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cl, bw[kz * 9 + grp], al[d], 0, 0, 0);
       }
       ch = nh;
       cl = nl;
-      if (p == 5) {
-#pragma unroll
-        for (int kz = 0; kz < 3; ++kz) wc[kz] = wn[kz];
-      }
     }
     // ---- epilogue: lane (j < 8) of each row group adds its partner's (j + 8) w_lo columns;
     // acc[r] = output (x = 4 g + r, channel j) ----
@@ -255,8 +249,8 @@ __global__ __launch_bounds__(kThreads) void conv0_split_kernel(
       }
     }
     if (k + 1 < nsteps) {
-      __syncthreads();   // every wave is done with planes zs - 1 .. zs + 2
-      stage(sb, 4);      // planes zs + 5 .. zs + 8 replace them
+      __syncthreads();   // every wave is done with planes zs - 1 .. zs + kZS - 2
+      stage(sb, kZS);    // planes zs + kNPL - 1 .. replace them
       __syncthreads();
     }
   }

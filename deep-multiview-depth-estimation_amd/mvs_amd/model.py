@@ -410,17 +410,20 @@ class CostVolumeReg(nn.Module):
         act = lambda bn, y: self.ReLU(bn(y))
         # the BN modules are shared between levels exactly as in model.py:101-121; the two narrow
         # full-resolution layers run on the HIP kernel in no-grad fp32 inference (_narrow_conv),
-        # e.g. test.py:61's train-mode BatchNorm under no_grad
+        # e.g. test.py:61's train-mode BatchNorm under no_grad; under autograd on a HIP device
+        # (train.py:97-104) every convolution runs as per-tap rocBLAS GEMMs (tap_gemm.py: MIOpen's
+        # backward solvers for these shapes take minutes per step)
+        conv = _train_conv if cv.is_cuda and torch.is_grad_enabled() else (lambda m, x: m(x))
         y0 = act(self.BN_0, _narrow_conv(self.conv_0_0, cv))
-        y1 = act(self.BN_1, self.conv_1_0(cv))
-        y2 = act(self.BN_2, self.conv_2_0(cv))
-        y3 = act(self.BN_3, self.conv_3_0(cv))
-        y1 = act(self.BN_1, self.conv_1_1(y1))
-        y2 = act(self.BN_2, self.conv_2_1(y2))
-        y3 = act(self.BN_3, self.conv_3_1(y3))
-        y3 = act(self.BN_2, self.deconv_3_0(y3))
-        y2 = act(self.BN_1, self.deconv_2_0(y3 + y2))
-        y1 = act(self.BN_0, self.deconv_1_0(y2 + y1))
+        y1 = act(self.BN_1, conv(self.conv_1_0, cv))
+        y2 = act(self.BN_2, conv(self.conv_2_0, cv))
+        y3 = act(self.BN_3, conv(self.conv_3_0, cv))
+        y1 = act(self.BN_1, conv(self.conv_1_1, y1))
+        y2 = act(self.BN_2, conv(self.conv_2_1, y2))
+        y3 = act(self.BN_3, conv(self.conv_3_1, y3))
+        y3 = act(self.BN_2, conv(self.deconv_3_0, y3))
+        y2 = act(self.BN_1, conv(self.deconv_2_0, y3 + y2))
+        y1 = act(self.BN_0, conv(self.deconv_1_0, y2 + y1))
         return self.Norm(_narrow_conv(self.conv_out, y1 + y0))
 
 
@@ -452,11 +455,23 @@ def _hip_cv(cv):
 def _narrow_conv(conv, x):
     """conv_0_0 (32 -> 8) / conv_out (8 -> 1) at full resolution: on a HIP device, in fp32 and
     without autograd, the hand-written kernel (mvs::conv3d_k3, csrc/conv3d_narrow.hip: MIOpen
-    runs these narrow full-volume layers at a few TFLOP/s); otherwise the module itself."""
+    runs these narrow full-volume layers at a few TFLOP/s); under autograd on a HIP device the
+    per-tap GEMMs (_train_conv); otherwise the module itself."""
     if _hip_inference(x):
         from .ops import conv3d_k3
         return conv3d_k3(x, conv.weight)
+    if x.is_cuda and torch.is_grad_enabled():
+        return _train_conv(conv, x)
     return conv(x)
+
+
+def _train_conv(m, x):
+    """A regulariser Conv3d / ConvTranspose3d under autograd on a HIP device: per-tap rocBLAS GEMMs
+    with their own backward (tap_gemm.py) instead of MIOpen (fp32 in and out)."""
+    from . import tap_gemm
+    if x.dtype != torch.float32 or torch.is_autocast_enabled():
+        return m(x)
+    return tap_gemm.conv_module(m, x)
 
 
 # ---- train-mode BatchNorm from sums (CostVolumeReg.forward_live_train) ----------------------

@@ -1,0 +1,57 @@
+"""mvs_amd/tap_gemm.py (the training path's Conv3d / ConvTranspose3d as per-tap GEMMs with their own
+backward) against PyTorch's autograd of F.conv3d / F.conv_transpose3d in float64 on the CPU: outputs,
+input gradients and weight gradients, for the regulariser's shapes (stride 1 padding 1; stride 2
+padding n//2 + 1; transposed stride 2 with output padding), odd and even extents."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mvs_amd import tap_gemm
+
+
+def _grads(fn, x, w, gy):
+    x = x.clone().requires_grad_(True)
+    w = w.clone().requires_grad_(True)
+    y = fn(x, w)
+    (y * gy).sum().backward()
+    return y.detach(), x.grad, w.grad
+
+
+@pytest.mark.parametrize("n", [(5, 6, 7), (8, 9, 10)])
+@pytest.mark.parametrize("stride,pad", [(1, 1), (2, None)])
+def test_conv3d_taps_autograd(n, stride, pad):
+    g = torch.Generator().manual_seed(sum(n) + stride)
+    p = tuple(d // 2 + 1 for d in n) if pad is None else pad
+    x = torch.randn(2, 5, *n, generator=g, dtype=torch.float64)
+    w = torch.randn(3, 5, 3, 3, 3, generator=g, dtype=torch.float64)
+    y_ref = F.conv3d(x, w, stride=stride, padding=p)
+    gy = torch.randn(y_ref.shape, generator=g, dtype=torch.float64)
+    ref = _grads(lambda a, b: F.conv3d(a, b, stride=stride, padding=p), x, w, gy)
+    got = _grads(lambda a, b: tap_gemm.conv3d(a, b, stride, p), x, w, gy)
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a, b, rtol=1e-11, atol=1e-11)
+
+
+@pytest.mark.parametrize("n", [(5, 6, 7), (8, 9, 10)])
+def test_conv_transpose3d_taps_autograd(n):
+    g = torch.Generator().manual_seed(sum(n))
+    p = tuple(d // 2 + 1 for d in n)
+    op = tuple((d + 1) % 2 for d in n)
+    x = torch.randn(2, 4, *n, generator=g, dtype=torch.float64)
+    w = torch.randn(4, 3, 3, 3, 3, generator=g, dtype=torch.float64)
+    f_ref = lambda a, b: F.conv_transpose3d(a, b, stride=2, padding=p, output_padding=op)
+    y_ref = f_ref(x, w)
+    gy = torch.randn(y_ref.shape, generator=g, dtype=torch.float64)
+    ref = _grads(f_ref, x, w, gy)
+    got = _grads(lambda a, b: tap_gemm.conv_transpose3d(a, b, 2, p, op), x, w, gy)
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a, b, rtol=1e-11, atol=1e-11)
+
+
+def test_conv_module_dispatch():
+    c = torch.nn.Conv3d(3, 2, 3, stride=2, padding=2, bias=False).double()
+    t = torch.nn.ConvTranspose3d(2, 3, 3, stride=2, padding=2, output_padding=1, bias=False).double()
+    x = torch.randn(1, 3, 6, 7, 8, dtype=torch.float64)
+    torch.testing.assert_close(tap_gemm.conv_module(c, x), c(x), rtol=1e-12, atol=1e-12)
+    z = torch.randn(1, 2, 4, 5, 6, dtype=torch.float64)
+    torch.testing.assert_close(tap_gemm.conv_module(t, z), t(z), rtol=1e-12, atol=1e-12)
