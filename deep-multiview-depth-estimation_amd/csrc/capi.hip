@@ -212,6 +212,61 @@ int mvs_conv3d_split_weights(const float* weight, unsigned short* frag, int* wei
   return MVS_OK;
 }
 
+int mvs_conv3d_s2_split_weights(const float* weight, unsigned short* frag, int* weight_exp) {
+  if (!weight || !frag || !weight_exp) return MVS_ERR_INVALID_ARGUMENT;
+  float m = 0.0f;
+  for (int k = 0; k < 16 * 32 * 27; ++k) {
+    if (!std::isfinite(weight[k])) return MVS_ERR_INVALID_ARGUMENT;
+    m = std::max(m, std::fabs(weight[k]));
+  }
+  int e = 0;
+  if (m > 0.0f) (void)std::frexp(m, &e);
+  const int ew = m > 0.0f ? std::min(std::max(14 - e, -120), 120) : 0;
+  // frag[tap][part][lane][j]: lane (c = lane & 15, g = lane >> 4) holds B[k = 8g + j][col c], column
+  // c = output channel c, k = input channel; part 0 = hi, 1 = lo; nn.Conv3d weight [16][32][3][3][3]
+  for (int tap = 0; tap < 27; ++tap)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int j = 0; j < 8; ++j) {
+        const int co = lane & 15, ci = 8 * (lane >> 4) + j;
+        const float v = std::ldexp(weight[(co * 32 + ci) * 27 + tap], ew);
+        const _Float16 hi = (_Float16)v;
+        const _Float16 lo = (_Float16)(v - (float)hi);
+        uint16_t bh, bl;
+        std::memcpy(&bh, &hi, 2);
+        std::memcpy(&bl, &lo, 2);
+        frag[((tap * 2 + 0) * 64 + lane) * 8 + j] = bh;
+        frag[((tap * 2 + 1) * 64 + lane) * 8 + j] = bl;
+      }
+  *weight_exp = ew;
+  return MVS_OK;
+}
+
+int mvs_conv3d_s2_split_fwd(const float* x, const void* weight_frag, int weight_exp, const unsigned* x_absmax,
+                            float* y, int batch, const int* dims, const int* out_origin, const int* out_size,
+                            const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                            void* stream) {
+  if (!x || !weight_frag || !y || !dims || !out_origin || !out_size || !pad || batch <= 0)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (((uintptr_t)x & 15u) || ((uintptr_t)weight_frag & 15u) || ((uintptr_t)x_absmax & 3u))
+    return MVS_ERR_INVALID_ARGUMENT;
+  if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (weight_exp < -120 || weight_exp > 120) return MVS_ERR_INVALID_ARGUMENT;
+  uint64_t vox = 1, ovox = 1;
+  for (int d = 0; d < 3; ++d) {
+    if (dims[d] <= 0 || out_size[d] <= 0 || out_origin[d] < 0 || pad[d] < 0) return MVS_ERR_INVALID_ARGUMENT;
+    // outputs of conv3d(stride 2, padding pad): (n + 2 pad - 3) / 2 + 1 per dim
+    if (out_origin[d] + out_size[d] > (dims[d] + 2 * pad[d] - 3) / 2 + 1) return MVS_ERR_INVALID_ARGUMENT;
+    vox *= (uint64_t)dims[d];
+    ovox *= (uint64_t)out_size[d];
+  }
+  if (128ull * vox > 0xFFFFFFF0ull || (uint64_t)batch * ovox * 16ull >= (1ull << 40)) return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
+  const int st = mvs::launch_conv_s2_split(x, weight_frag, weight_exp, x_absmax, y, batch, dims, out_origin,
+                                           out_size, pad, bn_scale, bn_shift, bn_mean, (hipStream_t)stream);
+  return st != MVS_OK ? st : lc.status();
+}
+
 int mvs_conv3d_k3_split_fwd(const float* x, const void* weight_frag, int weight_exp, const unsigned* x_absmax,
                             float* y, int batch, int d, int h, int w, const float* bn_scale,
                             const float* bn_shift, const float* bn_mean, void* stream) {

@@ -24,9 +24,10 @@
 // split part).  Lane (i = l & 15, g = l >> 4) supplies channels 8g .. 8g + 7 of voxel i's tap
 // input: one ds_read_b128 per (tap, part).
 //
-// Tiling.  A 512-thread workgroup (8 waves, 2 per SIMD) owns a 16 x 8 (x, y) column of outputs,
-// one y row per wave, and walks kZC depths in steps of 3.  LDS holds 5 input planes (the 18 x 10
-// halo of the column, 32 channels, hi and lo parts: 23 KB per plane, 115 KB in all) as a ring; a
+// Tiling.  A 256-thread workgroup (4 waves) owns a 16 x 4 (x, y) column of outputs, one y row per
+// wave, and walks kZC depths in steps of 3.  LDS holds 5 input planes (the 18 x 6 halo of the
+// column, 32 channels, hi and lo parts: 13.5 KB per plane, 69 KB in all) as a ring, so two
+// workgroups share a CU and one's staging overlaps the other's MFMAs; a
 // step reads planes zs-1 .. zs+3, and each (plane, ky, kx) A fragment feeds every output depth it
 // reaches (up to 3): 90 LDS reads for 162 MFMAs per wave and step.  The weight fragments stay in
 // registers (108 VGPRs), so the step's only vector-memory loads are the next step's 3 planes,
@@ -40,17 +41,18 @@ namespace {
 
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 
-constexpr int kSX = 16, kSY = 8, kZS = 3, kZC = 48;
-constexpr int kPX = kSX + 2, kPY = kSY + 2, kPV = kPX * kPY;   // 18 x 10 voxels per staged plane
+constexpr int kSX = 16, kSY = 4, kZS = 2, kZC = 48;
+constexpr int kPX = kSX + 2, kPY = kSY + 2, kPV = kPX * kPY;   // 18 x 6 voxels per staged plane
 constexpr int kNPL = kZS + 2;                                   // resident planes (ring slots)
 constexpr int kVoxB = 64;                                       // 32 channels x fp16 per part
 constexpr int kRowB = kPX * kVoxB;                              // 1,152 B
-constexpr int kPartB = kPV * kVoxB;                             // 11,520 B
+constexpr int kPartB = kPV * kVoxB;                             // 6,912 B
 constexpr int kSlotB = 2 * kPartB;                              // hi + lo parts
-constexpr int kLdsB = kNPL * kSlotB;                            // 115,200 B
-constexpr int kThreads = 512;
+constexpr int kLdsB = kNPL * kSlotB;                            // 55,296 B: 2 workgroups per CU
+constexpr int kThreads = 256;
 constexpr int kPlaneQ = kPV * 8;                                // channel quads per plane: 1,440
-constexpr int kPre = (kZS * kPlaneQ + kThreads - 1) / kThreads;  // 9 staging quads per thread
+constexpr int kPre = (kZS * kPlaneQ + kThreads - 1) / kThreads;  // 7 staging quads per thread
+constexpr int kPF = 3;                                           // A-fragment prefetch distance (items)
 constexpr uint32_t kOob = 0xFFFFFFF0u;                          // buffer offset past every descriptor
 
 // 2^e with bound * 2^e < 2^14 for every element of the cost volume: it is at most (max|feat|)^2
@@ -85,7 +87,7 @@ __device__ inline float ror8(float v) {   // value of lane (l ^ 8) inside each 1
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
 }
 
-__global__ __launch_bounds__(kThreads) void conv0_split_kernel(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void conv0_split_kernel(
     const f4v* __restrict__ cv, const h8v* __restrict__ wfrag, const uint32_t* __restrict__ absmax, int w_exp,
     float* __restrict__ out, int D, int H, int W, int tiles_x, int tiles_y, int zchunks, int total,
     const float* __restrict__ bn_scale, const float* __restrict__ bn_shift, const float* __restrict__ bn_mean) {
@@ -112,41 +114,56 @@ __global__ __launch_bounds__(kThreads) void conv0_split_kernel(
 
   // ---- staging map: quad e = tid + 512 j of a kZS-plane group -> (plane in group, global offset
   // inside that plane's (quad) volume, LDS byte offset inside a ring slot) ----
-  // gpl: plane in the group (99: no element -- outside the image or past the group) << 16 | LDS
-  // byte offset inside a ring slot
-  int goff[kPre], gsl[kPre];
+  // B fragments (wfrag[tap][lane], 27 x 1 KB): held in registers for the whole kernel, so the MFMA
+  // loop issues no vector-memory load that a wait could make the plane prefetch drain for.  Loaded
+  // before the first planes, whose staging waits retire them: none is outstanding in the step loop
+  // (the loop's counted waits would otherwise drain each step's prefetch)
+  const int lane = tid & 63;
+  h8v bw[27];
+#pragma unroll
+  for (int t = 0; t < 27; ++t)
+    bw[t] = __builtin_bit_cast(h8v, __builtin_amdgcn_raw_buffer_load_b128(rwf, lane * 16, t * 1024, 0));
+  // per staging element, one packed word: LDS byte offset inside a ring slot (bits 0-12), quad q
+  // (13-15), plane in the group (16-17; 3 = no element: outside the image or past the group), halo
+  // row yy (18-20) and column xx (21-25); the global offset is re-formed at each fetch (registers)
+  int em[kPre];
 #pragma unroll
   for (int j = 0; j < kPre; ++j) {
+    // quad fastest: 8 lanes write one voxel's 64 B (a 16-lane ds_write_b64 group two whole voxels,
+    // conflict-free) and load its 8 quads; 8 voxels of a row per wave-instruction and quad
     const int e = tid + kThreads * j;
-    const int pl = e / kPlaneQ, r = e - pl * kPlaneQ;
-    const int q = r / kPV, v = r - q * kPV;
+    const int q = e & 7, t = e >> 3;
+    const int pl = t / kPV, v = t - pl * kPV;
     const int yy = v / kPX, xx = v - yy * kPX;
     const int gy = y0 - 1 + yy, gx = x0 - 1 + xx;
     const bool ok = e < kZS * kPlaneQ && gy >= 0 && gy < H && gx >= 0 && gx < W;
-    goff[j] = ok ? (int)((size_t)q * DHW + (size_t)gy * W + gx) : 0;
-    gsl[j] = ((ok ? pl : 99) << 16) | (v * kVoxB + (((q >> 1) ^ ((xx >> 1) & 3)) << 4) + ((q & 1) << 3));
+    const int loff = v * kVoxB + (((q >> 1) ^ ((xx >> 1) & 3)) << 4) + ((q & 1) << 3);
+    em[j] = loff | (q << 13) | ((ok ? pl : 3) << 16) | ((ok ? yy : 0) << 18) | ((ok ? xx : 0) << 21);
   }
   f4v pre[kPre];
+  const uint32_t gbase = (uint32_t)(y0 - 1) * (uint32_t)W + (uint32_t)(x0 - 1);   // (may wrap: re-added)
   // planes zg .. zg + cnt - 1 -> registers (zero outside the volume)
   auto fetch = [&](int zg, int cnt) {
 #pragma unroll
     for (int j = 0; j < kPre; ++j) {
-      const int pl = gsl[j] >> 16, z = zg + pl;
+      const int pl = (em[j] >> 16) & 3, z = zg + pl;
       const bool ok = pl < cnt && z >= 0 && z < D;
-      pre[j] = ld4(rcv, ok ? ((uint32_t)goff[j] + (uint32_t)z * (uint32_t)HW) * 16u : kOob, 0);
+      const uint32_t goff = (uint32_t)((em[j] >> 13) & 7) * (uint32_t)DHW + gbase +
+                            (uint32_t)((em[j] >> 18) & 7) * (uint32_t)W + (uint32_t)((em[j] >> 21) & 31);
+      pre[j] = ld4(rcv, ok ? (goff + (uint32_t)z * (uint32_t)HW) * 16u : kOob, 0);
     }
   };
   // registers -> ring slots (slot of the group's first plane: s0), split into hi / lo parts
   auto stage = [&](int s0, int cnt) {
 #pragma unroll
     for (int j = 0; j < kPre; ++j) {
-      const int pl = gsl[j] >> 16;
-      if (pl >= cnt) continue;   // 99: outside the image, the slot keeps the zeros written first
+      const int pl = (em[j] >> 16) & 3;
+      if (pl >= cnt) continue;   // 3: outside the image, the slot keeps the zeros written first
       int s = s0 + pl;
       s = s >= kNPL ? s - kNPL : s;
       uint2 hi, lo;
       split4(pre[j], ex, hi, lo);
-      char* p = lds + s * kSlotB + (gsl[j] & 0xFFFF);
+      char* p = lds + s * kSlotB + (em[j] & 0x1FFF);
       *reinterpret_cast<uint2*>(p) = hi;
       *reinterpret_cast<uint2*>(p + kPartB) = lo;
     }
@@ -160,14 +177,8 @@ __global__ __launch_bounds__(kThreads) void conv0_split_kernel(
   stage(kZS, kNPL - kZS);
 
   // ---- per-lane constants ----
-  const int lane = tid & 63, wave = tid >> 6;
+  const int wave = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
-  // B fragments (wfrag[tap][lane], 27 x 1 KB): held in registers for the whole kernel, so the MFMA
-  // loop issues no vector-memory load that a wait could make the plane prefetch drain for
-  h8v bw[27];
-#pragma unroll
-  for (int t = 0; t < 27; ++t)
-    bw[t] = __builtin_bit_cast(h8v, __builtin_amdgcn_raw_buffer_load_b128(rwf, lane * 16, t * 1024, 0));
   int aoff[3];
 #pragma unroll
   for (int kx = 0; kx < 3; ++kx) aoff[kx] = wave * kRowB + (i + kx) * kVoxB + ((g ^ (((i + kx) >> 1) & 3)) << 4);
@@ -196,23 +207,23 @@ __global__ __launch_bounds__(kThreads) void conv0_split_kernel(
 #pragma unroll
     for (int p = 0; p < kNPL; ++p) base[p] = lds + (sb + p >= kNPL ? sb + p - kNPL : sb + p) * kSlotB;
     // 45 items (ky, kx, p) in order; per item the A fragments (hi, lo) of plane p at tap (ky, kx)
-    // feed every output depth they reach (d = p - kz).  Software pipeline: the next item's A is read
-    // from LDS before this item's MFMAs; the empty asm keeps the compiler from hoisting further loads
-    // (fully unrolled it would otherwise issue them all at once and spill)
+    // feed every output depth they reach (d = p - kz).  Software pipeline: item it + kPF's A is read
+    // from LDS before item it's MFMAs issue
     constexpr int kItems = 9 * kNPL;
     auto lda = [&](int it, h8v& hi, h8v& lo) {
       const int grp = it / kNPL, p = it % kNPL, ky = grp / 3, kx = grp % 3;
       hi = *reinterpret_cast<const h8v*>(base[p] + ky * kRowB + aoff[kx]);
       lo = *reinterpret_cast<const h8v*>(base[p] + kPartB + ky * kRowB + aoff[kx]);
     };
-    h8v ch, cl;
-    lda(0, ch, cl);
+    // register ring of kPF + 1 A-fragment pairs: item it + kPF is read while item it's MFMAs issue
+    h8v rh[kPF + 1], rl[kPF + 1];
+#pragma unroll
+    for (int it = 0; it < kPF; ++it) lda(it, rh[it], rl[it]);
 #pragma unroll
     for (int it = 0; it < kItems; ++it) {
       const int p = it % kNPL, grp = it / kNPL;
-      h8v nh = ch, nl = cl;
-      if (it + 1 < kItems) lda(it + 1, nh, nl);
-      asm volatile("" ::: "memory");
+      if (it + kPF < kItems) lda(it + kPF, rh[(it + kPF) % (kPF + 1)], rl[(it + kPF) % (kPF + 1)]);
+      const h8v ch = rh[it % (kPF + 1)], cl = rl[it % (kPF + 1)];
 #pragma unroll
       for (int kz = 0; kz < 3; ++kz) {
         const int d = p - kz;   // output depth zs + d reads plane zs - 1 + p through tap kz
@@ -220,8 +231,8 @@ __global__ __launch_bounds__(kThreads) void conv0_split_kernel(
         ah[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch, bw[kz * 9 + grp], ah[d], 0, 0, 0);
         al[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cl, bw[kz * 9 + grp], al[d], 0, 0, 0);
       }
-      ch = nh;
-      cl = nl;
+      // pin the schedule: the scheduler would otherwise sink each read next to its first use
+      __builtin_amdgcn_sched_barrier(0);
     }
     // ---- epilogue: lane (j < 8) of each row group adds its partner's (j + 8) w_lo columns;
     // acc[r] = output (x = 4 g + r, channel j) ----

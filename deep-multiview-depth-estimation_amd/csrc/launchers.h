@@ -69,6 +69,13 @@ int launch_conv3d_split(const float* x, const void* wfrag, int w_exp, const uint
                         int D, int H, int W, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                         hipStream_t s);
 
+// conv3d_s2_split.hip: conv_1_0 (32 -> 16, 3x3x3, stride 2, padding pad) on an output region, split-fp16
+// MFMA; x channel-quad fp32, wfrag [27][2][64][8] fp16 (mvs_conv3d_s2_split_weights), y channels-last
+// region [B][on0][on1][on2][16]
+int launch_conv_s2_split(const float* x, const void* wfrag, int w_exp, const uint32_t* absmax, float* y, int B,
+                         const int* n, const int* o0, const int* on, const int* pad, const float* bn_scale,
+                         const float* bn_shift, const float* bn_mean, hipStream_t s);
+
 // conv2d_narrow.hip: bias-free Conv2d of the encoder / refinement (padding k/2), NCHW fp32, weights
 // wt[c_in][k][k][c_out], optional eval BN + ReLU epilogue; MVS_ERR_INVALID_ARGUMENT for a shape
 // without an instantiation

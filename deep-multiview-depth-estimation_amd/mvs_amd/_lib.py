@@ -53,6 +53,8 @@ SIGNATURES = {
                                                _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p, _p]),
     "mvs_conv3d_k3_split_fwd": (_c_int, [_p, _p, _c_int, _p, _p] + [_c_int] * 4 + [_p] * 4),
     "mvs_conv3d_split_weights": (_c_int, [_p, _p, _p]),
+    "mvs_conv3d_s2_split_fwd": (_c_int, [_p, _p, _c_int, _p, _p, _c_int] + [_p] * 8),
+    "mvs_conv3d_s2_split_weights": (_c_int, [_p, _p, _p]),
     "mvs_cost_volume_fwd_c4_bf16": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
                                              _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p]),
     "mvs_cost_volume_fwd_bf16": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,

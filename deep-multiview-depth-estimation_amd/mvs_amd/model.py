@@ -254,8 +254,8 @@ class CostVolumeReg(nn.Module):
         ReLU fused (csrc/conv3d_region.hip), deconv_1_0 + BN_0 + ReLU + `+ y0` and the `y2 + y1`
         sum in one kernel (csrc/deconv3d_region.hip), conv_out (conv3d_narrow.hip).  ``c4``: cv is
         the channel-quad volume, read by conv_0_0 and the three stride-2 convs with 16-byte loads."""
-        from .ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_k3_split, conv3d_region, cv_bound,
-                          deconv3d_k3s2, region_weight, softmax_depth)
+        from .ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_k3_split, conv3d_region, conv_s2_split,
+                          cv_bound, deconv3d_k3s2, region_weight, softmax_depth)
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad = list(n), list(self.pad)
@@ -280,8 +280,12 @@ class CostVolumeReg(nn.Module):
 
         def level(conv_a, conv_b, bn, reg):
             halo = _grow(reg, n, 1)
-            ya = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(halo), size(halo), None,
-                               None, pad, *bn_eval(bn), in_c4=c4)
+            if bound is not None and conv_a.weight.shape[0] == 16:
+                # conv_1_0 reads the whole volume: LDS-staged split-fp16 kernel (csrc/conv3d_s2_split.hip)
+                ya = conv_s2_split(cv, bound, conv_a.weight, dims, org(halo), size(halo), pad, *bn_eval(bn))
+            else:
+                ya = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(halo), size(halo), None,
+                                   None, pad, *bn_eval(bn), in_c4=c4)
             # level 1's output only feeds deconv_1_0's input sum: channels-first for its loads
             return conv3d_region(ya, None, region_weight(conv_b), CONV_S1, dims, org(reg), size(reg),
                                  org(halo), size(halo), None, *bn_eval(bn), out_ncdhw=reg is B)

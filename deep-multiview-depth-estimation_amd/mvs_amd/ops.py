@@ -524,6 +524,57 @@ def _(x, absmax, weight, bn_scale=None, bn_shift=None, bn_mean=None):
     return x.new_empty((x.shape[0], 8) + tuple(x.shape[2:5]))
 
 
+@torch.library.custom_op("mvs::conv_s2_split", mutates_args=())
+def conv_s2_split(x: torch.Tensor, absmax: Optional[torch.Tensor], weight: torch.Tensor, dims: list[int],
+                  out_origin: list[int], out_size: list[int], pad: list[int], bn_scale: Optional[torch.Tensor] = None,
+                  bn_shift: Optional[torch.Tensor] = None, bn_mean: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """conv_1_0 (nn.Conv3d(32, 16, 3, stride=2, padding=pad, bias=False), + eval BN + ReLU when bn_*
+    are given) of the channel-quad fp32 cost volume x [B, 8, D, H, W, 4] on the output region
+    [out_origin, out_origin + out_size), split-fp16 MFMA (csrc/conv3d_s2_split.hip,
+    mvs_conv3d_s2_split_fwd) -> channels-last region [B, out_size..., 16] (conv3d_region's S2 layout).
+    ``absmax``: the volume's bound words (cost_volume_c4_absmax), None = unscaled.  Inference only."""
+    _require_gpu(x, "x")
+    lib = _lib.load()
+    if x.dim() != 6 or x.shape[1] != 8 or x.shape[-1] != 4 or x.dtype != _F32:
+        raise ValueError("x: fp32 channel-quad [B, 8, D, H, W, 4] expected, got %s %s" % (tuple(x.shape), x.dtype))
+    if tuple(weight.shape) != (16, 32, 3, 3, 3):
+        raise ValueError("weight [16, 32, 3, 3, 3] expected, got %s" % (tuple(weight.shape),))
+    if list(x.shape[2:5]) != [int(v) for v in dims]:
+        raise ValueError("dims %s do not match the volume %s" % (list(dims), list(x.shape[2:5])))
+    x = x.contiguous()
+    frag, wexp = derived("s2split", (weight,), lambda wt: _s2_split_fragments(wt, x.device), x.device)
+    bn = [t if t is None else t.to(device=x.device, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
+    if any(t is None for t in bn) and not all(t is None for t in bn):
+        raise ValueError("bn_scale, bn_shift and bn_mean go together")
+    bp = [None if t is None else _lib.ptr(t) for t in bn]
+    if absmax is not None:
+        if absmax.numel() != 8 or absmax.dtype != torch.int32 or absmax.device != x.device:
+            raise ValueError("absmax: int32[8] on the volume's device expected")
+        absmax = absmax.contiguous()
+    y = torch.empty([x.shape[0]] + [int(v) for v in out_size] + [16], device=x.device, dtype=_F32)
+    st = lib.mvs_conv3d_s2_split_fwd(_lib.ptr(x), _lib.ptr(frag), int(wexp),
+                                     None if absmax is None else _lib.ptr(absmax), _lib.ptr(y), x.shape[0],
+                                     _ints3(dims), _ints3(out_origin), _ints3(out_size), _ints3(pad), *bp,
+                                     _lib.stream_handle(x.device))
+    _lib.check(st, "mvs_conv3d_s2_split_fwd")
+    return y
+
+
+@conv_s2_split.register_fake
+def _(x, absmax, weight, dims, out_origin, out_size, pad, bn_scale=None, bn_shift=None, bn_mean=None):
+    return x.new_empty([x.shape[0]] + [int(v) for v in out_size] + [16])
+
+
+def _s2_split_fragments(weight, device):
+    lib = _lib.load()
+    w = weight.detach().to(device="cpu", dtype=_F32).contiguous()
+    frag = torch.empty((27 * 2 * 64 * 8,), dtype=torch.int16)
+    e = ctypes.c_int(0)
+    st = lib.mvs_conv3d_s2_split_weights(_lib.ptr(w), _lib.ptr(frag), ctypes.byref(e))
+    _lib.check(st, "mvs_conv3d_s2_split_weights")
+    return frag.to(device), e.value
+
+
 def split_weight_fragments(weight, device):
     """(fp16 MFMA fragments [27*64*8] int16 on ``device``, exponent) of conv_0_0's weight, formed on
     the host by mvs_conv3d_split_weights (the C ABI's own split, so every caller gets the same)."""

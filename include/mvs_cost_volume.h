@@ -279,6 +279,26 @@ int mvs_conv3d_k3_split_fwd(const float* x, const void* weight_frag, int weight_
  * c >= 8 the lo part of channel c - 8, where hi = fp16(w 2^ew), lo = fp16(w 2^ew - hi), nearest. */
 int mvs_conv3d_split_weights(const float* weight, unsigned short* frag, int* weight_exp);
 
+/* conv_1_0 (model.py:78, 103: nn.Conv3d(32, 16, 3, stride=2, padding=pad, bias=False) + optional eval
+ * BN_1 + ReLU) over the channel-quad cost volume on the output region [out_origin, out_origin +
+ * out_size) per dim (forward_live's halo(B)), f16 matrix cores with split operands
+ * (csrc/conv3d_s2_split.hip; three partial products x_hi w_hi + x_hi w_lo + x_lo w_hi, fp32 accumulation).
+ *   x: x[batch][8][dims[0]][dims[1]][dims[2]][4] fp32 (mvs_cost_volume_fwd_c4_absmax), 16-byte aligned;
+ *   x_absmax: its bound words (or NULL: unscaled, every |x| < 2^15 known); weight_frag / weight_exp:
+ *   mvs_conv3d_s2_split_weights (copied to the device); y: channels-last region
+ *   y[batch][out_size[0]][out_size[1]][out_size[2]][16] fp32; BN pointers 16 floats each, all or none.
+ * 128 * dims[0]*dims[1]*dims[2] <= 2^32 - 16.  Replaces model.py:103's conv_1_0 in eval inference. */
+int mvs_conv3d_s2_split_fwd(const float* x, const void* weight_frag, int weight_exp, const unsigned* x_absmax,
+                            float* y, int batch, const int* dims, const int* out_origin, const int* out_size,
+                            const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                            void* stream);
+
+/* HOST function: the fp16 MFMA operand fragments of conv_1_0's weight for mvs_conv3d_s2_split_fwd.
+ * weight [16][32][3][3][3] fp32 HOST, finite; frag HOST 27*2*64*8 uint16: frag[tap][part][lane][j] =
+ * part (0 hi, 1 lo) of w[c = lane & 15][8 (lane >> 4) + j][tap] * 2^ew, *weight_exp = ew (max|w| 2^ew
+ * < 2^14). */
+int mvs_conv3d_s2_split_weights(const float* weight, unsigned short* frag, int* weight_exp);
+
 /* Feature encoder and refinement layers (model.py:22-65 FeatureEncoder, model.py:134-145): nn.Conv2d(
  * c_in, c_out, k, stride, padding=k/2, bias=False) over x[n][c_in][h][w] fp32 into
  * y[n][c_out][ho][wo] (ho = (h + 2(k/2) - k)/stride + 1, likewise wo), with the weight TRANSPOSED to

@@ -157,3 +157,81 @@ def test_split_conv_on_fused_cost_volume():
     g = torch.Generator().manual_seed(12)
     wt = torch.randn(8, 32, 3, 3, 3, generator=g) * 0.05
     _check(x, wt, None, words, "fused cost volume")
+
+
+# ---- conv_1_0: stride-2 split kernel (csrc/conv3d_s2_split.hip) ------------------------------------
+def _split_host_s2(w):
+    lib = _lib.load()
+    w = w.to(torch.float32).contiguous()
+    frag = torch.empty((27 * 2 * 64 * 8,), dtype=torch.int16)
+    e = ctypes.c_int(0)
+    st = lib.mvs_conv3d_s2_split_weights(_lib.ptr(w), _lib.ptr(frag), ctypes.byref(e))
+    return st, frag.view(torch.float16).reshape(27, 2, 64, 8).to(torch.float64), e.value
+
+
+def test_s2_split_weights_layout():
+    g = torch.Generator().manual_seed(8)
+    w = torch.randn(16, 32, 3, 3, 3, generator=g) * 0.03
+    st, frag, ew = _split_host_s2(w)
+    assert st == 0
+    m = w.abs().max().item()
+    assert m * 2.0 ** ew < 2 ** 14 <= 2 * m * 2.0 ** ew
+    ws = w.double() * 2.0 ** ew
+    for tap in (0, 5, 26):
+        kz, ky, kx = tap // 9, (tap // 3) % 3, tap % 3
+        hi = torch.zeros(16, 32, dtype=torch.float64)
+        lo = torch.zeros(16, 32, dtype=torch.float64)
+        for l in range(64):
+            for j in range(8):
+                hi[l & 15, 8 * (l >> 4) + j] = frag[tap, 0, l, j]
+                lo[l & 15, 8 * (l >> 4) + j] = frag[tap, 1, l, j]
+        ref = ws[:, :, kz, ky, kx]
+        assert torch.equal(hi, ref.to(torch.float16).double())
+        assert (hi + lo - ref).abs().max() <= 2.0 ** -22 * ref.abs().max() + 2.0 ** -24
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [(12, 16, 20), (15, 21, 37), (24, 33, 50)])
+@pytest.mark.parametrize("bn", [False, True])
+def test_s2_split_conv_on_live_region(n, bn):
+    """conv_1_0 on forward_live's halo(B) (stride 2, padding n//2 + 1: windows leave the volume on
+    every side), ragged output tiles, against float64 of the same volume and no worse than 1.5x the
+    fp32 region kernel's / MIOpen's own error; the output region is channels-last."""
+    from mvs_amd import model as M
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.ops import CONV_S2, conv3d_region, conv_s2_split
+    pad, _ = pad_outpad(*n)
+    full = tuple((0, d - 1) for d in n)
+    halo = M._grow(M._tconv_input_region(full, n, pad), n, 1)
+    org = [lo for lo, _ in halo]
+    size = [hi - lo + 1 for lo, hi in halo]
+    g = torch.Generator().manual_seed(sum(n) + bn)
+    B = 2
+    x = torch.randn(B, 32, *n, generator=g).square()
+    wt = torch.randn(16, 32, 3, 3, 3, generator=g) * 0.05
+    p = (torch.rand(16, generator=g) + 0.5, torch.randn(16, generator=g), torch.randn(16, generator=g) * 0.1) if bn else None
+    ref = torch.nn.functional.conv3d(x.double(), wt.double(), stride=2, padding=pad)
+    if bn:
+        sc, sh, mu = (t.double()[:, None, None, None] for t in p)
+        ref = torch.clamp((ref - mu) * sc + sh, min=0.0)
+    sl = tuple(slice(o, o + s) for o, s in zip(org, size))
+    ref = ref[(slice(None), slice(None)) + sl].permute(0, 2, 3, 4, 1)          # channels-last region
+    bdev = [t.to(DEV) for t in p] if bn else []
+    with torch.no_grad():
+        xc = _to_c4(x).to(DEV)
+        y = conv_s2_split(xc, _bound_words(x).to(DEV), wt.to(DEV), list(n), org, size, list(pad), *bdev).cpu()
+        w27 = wt.permute(2, 3, 4, 0, 1).reshape(27, 16, 32).contiguous().to(DEV)
+        y32 = conv3d_region(xc, None, w27, CONV_S2, list(n), org, size, None, None, list(pad), *bdev, in_c4=True).cpu()
+        yt = torch.nn.functional.conv3d(x.to(DEV), wt.to(DEV), stride=2, padding=pad)
+        if bn:
+            sc, sh, mu = (t.to(DEV)[:, None, None, None] for t in p)
+            yt = torch.clamp((yt - mu) * sc + sh, min=0.0)
+        yt = yt[(slice(None), slice(None)) + sl].permute(0, 2, 3, 4, 1).cpu()
+    assert y.shape == ref.shape == y32.shape, (y.shape, ref.shape, y32.shape)
+    scale = ref.abs().max().item()
+    err = (y.double() - ref).abs().max().item()
+    err32 = (y32.double() - ref).abs().max().item()
+    errt = (yt.double() - ref).abs().max().item()
+    print("s2 %s bn=%s: split %.3g, fp32 region kernel %.3g, MIOpen %.3g (scale %.3g)" % (n, bn, err, err32, errt, scale))
+    assert err <= 1e-5 * scale, (err, scale)
+    assert err <= 1.5 * max(err32, errt) + 1e-7 * scale, (err, err32, errt)

@@ -15,6 +15,7 @@ sys.path.insert(0, REPO)
 import bench  # noqa: E402
 import torch  # noqa: E402
 from mvs_amd import model as M  # noqa: E402
+from mvs_amd.ops import conv_s2_split  # noqa: E402
 from mvs_amd.ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_k3_split, conv3d_region,  # noqa: E402
                          cv_bound, deconv3d_k3s2, region_weight, softmax_depth)
 
@@ -74,6 +75,12 @@ def main():
                 ya, None, region_weight(cb), CONV_S1, dims, org(r), size(r), org(halo), size(halo), None, *bn(bnm),
                 out_ncdhw=r is Bq))
             layers["conv_%d_0" % (k + 1)] = fa
+            if k == 0:
+                layers["conv_1_0_split"] = (lambda ca=ca, bnm=bnm, halo=halo: conv_s2_split(
+                    cv, cv_bound(cv), ca.weight, dims, org(halo), size(halo), pad, *bn(bnm)))
+                ys = layers["conv_1_0_split"]()
+                print("conv_1_0 split vs exact fp32: max|d| %.3g (max|y| %.3g)"
+                      % ((ys - ya).abs().max().item(), ya.abs().max().item()), flush=True)
             layers["conv_%d_1" % (k + 1)] = fb
             lv.append(fb())
         y1, y2, y3 = lv
