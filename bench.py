@@ -143,8 +143,8 @@ def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=F
     Returns (main_ms, op_ms, alg_bytes): main_ms = average duration of the main fused kernel
     (events recorded by mvs_cost_volume_fwd_timed right around its launch), op_ms = average
     duration of the whole op (sampling matrices + packing + reference resampling + main kernel).
-    quads=True times the channel-quad variant (mvs_cost_volume_fwd_c4, what MVSNet.forward's
-    inference step runs; same bytes).  bf16=True times the opt-in bf16 cost volume
+    quads=True times the split channel-quad variant (mvs_cost_volume_fwd_c4_split, what
+    MVSNet.forward's inference step runs; same bytes).  bf16=True times the opt-in bf16 cost volume
     (mvs_cost_volume_fwd_bf16): op-level only (main_ms None), algorithmic bytes with a 2-byte
     cost volume."""
     from mvs_amd import _lib, ops
@@ -159,6 +159,7 @@ def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=F
                      dtype=torch.bfloat16 if bf16 else torch.float32)   # (same bytes as the quad layouts)
     ws = torch.empty((lib.mvs_cost_volume_workspace_bytes(B, V, C, h, w, d_count) + 3) // 4,
                      device=device)
+    absmax = torch.empty((8,), device=device, dtype=torch.int32)
     stream = torch.cuda.current_stream(device)
     sp = _lib.stream_handle(device)
 
@@ -177,13 +178,16 @@ def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=F
                 _lib.ptr(d_int), B, V, C, h, w, d_begin, d_count, 25.0, _lib.ptr(ws), _lib.ptr(cv), sp)
             _lib.check(st, "mvs_cost_volume_fwd_bf16")
             return
-        fn = lib.mvs_cost_volume_fwd_c4 if quads else lib.mvs_cost_volume_fwd_timed
-        st = fn(
-            _lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T), _lib.ptr(d_min), _lib.ptr(d_int),
-            B, V, C, h, w, d_begin, d_count, 25.0, _lib.ptr(ws), _lib.ptr(cv), sp,
-            None if e0 is None else ctypes.c_void_p(e0.cuda_event),
-            None if e1 is None else ctypes.c_void_p(e1.cuda_event))
-        _lib.check(st, "mvs_cost_volume_fwd_c4" if quads else "mvs_cost_volume_fwd_timed")
+        evs = (None if e0 is None else ctypes.c_void_p(e0.cuda_event),
+               None if e1 is None else ctypes.c_void_p(e1.cuda_event))
+        args = (_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T), _lib.ptr(d_min), _lib.ptr(d_int),
+                B, V, C, h, w, d_begin, d_count, 25.0, _lib.ptr(ws), _lib.ptr(cv), sp) + evs
+        if quads:   # the split cost volume the eval step writes (16-byte elements, bound words)
+            st = lib.mvs_cost_volume_fwd_c4_split(*args, _lib.ptr(absmax))
+            _lib.check(st, "mvs_cost_volume_fwd_c4_split")
+        else:
+            st = lib.mvs_cost_volume_fwd_timed(*args)
+            _lib.check(st, "mvs_cost_volume_fwd_timed")
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(iters)]
@@ -634,7 +638,8 @@ def main():
                      "frac": gbs / HBM_PEAK_GBS,
                      "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
                      "kernel": "cost_volume_staged_kernel<V=%d, planes=8, %s>" % (
-                         V, "channel-quad store" if quads else "NCDHW store"), "kernel_ms": k_ms,
+                         V, "split-fp16 channel-quad store (16 B per voxel and 4 channels)" if quads
+                         else "NCDHW store"), "kernel_ms": k_ms,
                      "alg_bytes_per_launch": alg,
                      "timing": ("HIP events around each launch inside the %d timed steps" % args.steps
                                 if "step_kernel_ms" in result else "HIP events, isolated launches"),

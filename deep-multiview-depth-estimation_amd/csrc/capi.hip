@@ -54,7 +54,7 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
                          uint32_t* absmax = nullptr) {
   if (!feat || !workspace || !cv_out) return MVS_ERR_INVALID_ARGUMENT;
   Geometry g;
-  int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g, es);
+  int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g, es == 17 ? 16 : es);
   if (st != MVS_OK) return st;
   if (!cams_ok(K, R, T, d_min, d_int) || d_begin < 0) return MVS_ERR_INVALID_ARGUMENT;
   const mvs::LaunchCheck lc;
@@ -64,8 +64,8 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
     st = mvs_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
                             d_scale, workspace, stream);
     if (st != MVS_OK) return st;
-    const size_t ch = (es == 16 || es == 8) ? (size_t)((channels + 3) / 4) : (size_t)channels;
-    if (hipMemsetAsync(cv_out, 0, (size_t)batch_size * ch * d_count * h * w * es, s) != hipSuccess)
+    const size_t ch = (es == 16 || es == 17 || es == 8) ? (size_t)((channels + 3) / 4) : (size_t)channels;
+    if (hipMemsetAsync(cv_out, 0, (size_t)batch_size * ch * d_count * h * w * (es == 17 ? 16 : es), s) != hipSuccess)
       return MVS_ERR_HIP;
     return lc.status();
   }
@@ -76,9 +76,9 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
   if (es == 4)
     mvs::launch_cost_volume_fwd(g, feat, cm, workspace, packed, static_cast<float*>(cv_out), s,
                                 (hipEvent_t)ev0, (hipEvent_t)ev1);
-  else if (es == 16)
+  else if (es == 16 || es == 17)   // 17: the split cost volume (16-byte elements)
     mvs::launch_cost_volume_fwd_c4(g, feat, cm, workspace, packed, static_cast<float*>(cv_out), s,
-                                   (hipEvent_t)ev0, (hipEvent_t)ev1, absmax);
+                                   (hipEvent_t)ev0, (hipEvent_t)ev1, absmax, es == 17);
   else if (es == 8)
     mvs::launch_cost_volume_fwd_c4_bf16(g, feat, cm, workspace, packed, cv_out, s, (hipEvent_t)ev0,
                                         (hipEvent_t)ev1);
@@ -183,6 +183,18 @@ int mvs_cost_volume_fwd_c4_absmax(const float* feat, const float* K, const float
                               main_begin_event, main_end_event, feat_absmax);
 }
 
+int mvs_cost_volume_fwd_c4_split(const float* feat, const float* K, const float* R, const float* T,
+                                 const float* d_min, const float* d_int, int batch_size, int n_views,
+                                 int channels, int h, int w, int d_begin, int d_count, float d_scale,
+                                 float* workspace, void* cv_out, void* stream, void* main_begin_event,
+                                 void* main_end_event, unsigned* feat_absmax) {
+  if (n_views > 8) return MVS_ERR_UNSUPPORTED_VIEWS;
+  if (((uintptr_t)cv_out & 15u) || !feat_absmax || ((uintptr_t)feat_absmax & 3u)) return MVS_ERR_INVALID_ARGUMENT;
+  return cost_volume_fwd_impl(feat, K, R, T, d_min, d_int, batch_size, n_views, channels, h, w,
+                              d_begin, d_count, d_scale, workspace, cv_out, 17, stream,
+                              main_begin_event, main_end_event, feat_absmax);
+}
+
 int mvs_conv3d_split_weights(const float* weight, unsigned short* frag, int* weight_exp) {
   if (!weight || !frag || !weight_exp) return MVS_ERR_INVALID_ARGUMENT;
   // scale 2^ew with max|w| 2^ew < 2^14 (all-zero weights: ew = 0)
@@ -241,12 +253,13 @@ int mvs_conv3d_s2_split_weights(const float* weight, unsigned short* frag, int* 
   return MVS_OK;
 }
 
-int mvs_conv3d_s2_split_fwd(const float* x, const void* weight_frag, int weight_exp, const unsigned* x_absmax,
-                            float* y, int batch, const int* dims, const int* out_origin, const int* out_size,
-                            const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                            void* stream) {
+int mvs_conv3d_s2_split_fwd(const void* x, int flags, const void* weight_frag, int weight_exp,
+                            const unsigned* x_absmax, float* y, int batch, const int* dims,
+                            const int* out_origin, const int* out_size, const int* pad, const float* bn_scale,
+                            const float* bn_shift, const float* bn_mean, void* stream) {
   if (!x || !weight_frag || !y || !dims || !out_origin || !out_size || !pad || batch <= 0)
     return MVS_ERR_INVALID_ARGUMENT;
+  if ((flags & ~MVS_CONV_IN_SPLIT) || ((flags & MVS_CONV_IN_SPLIT) && !x_absmax)) return MVS_ERR_INVALID_ARGUMENT;
   if (((uintptr_t)x & 15u) || ((uintptr_t)weight_frag & 15u) || ((uintptr_t)x_absmax & 3u))
     return MVS_ERR_INVALID_ARGUMENT;
   if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
@@ -262,15 +275,17 @@ int mvs_conv3d_s2_split_fwd(const float* x, const void* weight_frag, int weight_
   }
   if (128ull * vox > 0xFFFFFFF0ull || (uint64_t)batch * ovox * 16ull >= (1ull << 40)) return MVS_ERR_TOO_LARGE;
   const mvs::LaunchCheck lc;
-  const int st = mvs::launch_conv_s2_split(x, weight_frag, weight_exp, x_absmax, y, batch, dims, out_origin,
-                                           out_size, pad, bn_scale, bn_shift, bn_mean, (hipStream_t)stream);
+  const int st = mvs::launch_conv_s2_split(x, (flags & MVS_CONV_IN_SPLIT) != 0, weight_frag, weight_exp, x_absmax,
+                                           y, batch, dims, out_origin, out_size, pad, bn_scale, bn_shift, bn_mean,
+                                           (hipStream_t)stream);
   return st != MVS_OK ? st : lc.status();
 }
 
-int mvs_conv3d_k3_split_fwd(const float* x, const void* weight_frag, int weight_exp, const unsigned* x_absmax,
-                            float* y, int batch, int d, int h, int w, const float* bn_scale,
-                            const float* bn_shift, const float* bn_mean, void* stream) {
+int mvs_conv3d_k3_split_fwd(const void* x, int flags, const void* weight_frag, int weight_exp,
+                            const unsigned* x_absmax, float* y, int batch, int d, int h, int w,
+                            const float* bn_scale, const float* bn_shift, const float* bn_mean, void* stream) {
   if (!x || !weight_frag || !y || batch <= 0 || d <= 0 || h <= 0 || w <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if ((flags & ~MVS_CONV_IN_SPLIT) || ((flags & MVS_CONV_IN_SPLIT) && !x_absmax)) return MVS_ERR_INVALID_ARGUMENT;
   if (((uintptr_t)x & 15u) || ((uintptr_t)weight_frag & 15u) || ((uintptr_t)x_absmax & 3u))
     return MVS_ERR_INVALID_ARGUMENT;
   if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
@@ -279,8 +294,8 @@ int mvs_conv3d_k3_split_fwd(const float* x, const void* weight_frag, int weight_
   // one 32-bit buffer descriptor per sample volume (8 quads of 16 B per voxel) and 32-bit staging offsets
   if (128ull * (uint64_t)d * (uint64_t)h * (uint64_t)w > 0xFFFFFFF0ull) return MVS_ERR_TOO_LARGE;
   const mvs::LaunchCheck lc;
-  const int st = mvs::launch_conv3d_split(x, weight_frag, weight_exp, x_absmax, y, batch, d, h, w, bn_scale,
-                                          bn_shift, bn_mean, (hipStream_t)stream);
+  const int st = mvs::launch_conv3d_split(x, (flags & MVS_CONV_IN_SPLIT) != 0, weight_frag, weight_exp, x_absmax,
+                                          y, batch, d, h, w, bn_scale, bn_shift, bn_mean, (hipStream_t)stream);
   return st != MVS_OK ? st : lc.status();
 }
 
@@ -451,11 +466,15 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
                           int batch, int c_in, int c_out, const int* dims, const int* out_origin,
                           const int* out_size, const int* in_origin, const int* in_size,
                           const int* pad, const float* bn_scale, const float* bn_shift,
-                          const float* bn_mean, void* stream) {
+                          const float* bn_mean, const unsigned* x_absmax, void* stream) {
   if (!x || !weight || !y || !dims || !out_origin || !out_size || batch <= 0) return MVS_ERR_INVALID_ARGUMENT;
-  if (mode < MVS_CONV_S1 || mode > MVS_CONV_T2 || (flags & ~(MVS_CONV_OUT_NCDHW | MVS_CONV_IN_C4 | MVS_CONV_IN_BF16)))
+  if (mode < MVS_CONV_S1 || mode > MVS_CONV_T2 ||
+      (flags & ~(MVS_CONV_OUT_NCDHW | MVS_CONV_IN_C4 | MVS_CONV_IN_BF16 | MVS_CONV_IN_SPLIT)))
     return MVS_ERR_INVALID_ARGUMENT;
   if ((flags & MVS_CONV_IN_BF16) && !(flags & MVS_CONV_IN_C4)) return MVS_ERR_INVALID_ARGUMENT;
+  if ((flags & MVS_CONV_IN_SPLIT) && (!(flags & MVS_CONV_IN_C4) || (flags & MVS_CONV_IN_BF16) || !x_absmax ||
+                                      ((uintptr_t)x_absmax & 3u)))
+    return MVS_ERR_INVALID_ARGUMENT;
   if ((flags & MVS_CONV_IN_C4) && (mode != MVS_CONV_S2 || c_in % 4)) return MVS_ERR_INVALID_ARGUMENT;
   if (mode != MVS_CONV_S2 && (!in_origin || !in_size)) return MVS_ERR_INVALID_ARGUMENT;
   if (mode != MVS_CONV_S1 && !pad) return MVS_ERR_INVALID_ARGUMENT;
@@ -482,11 +501,12 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
       nvox >= (1ull << 62))
     return MVS_ERR_TOO_LARGE;
   const mvs::LaunchCheck lc;
-  const int quads = (flags & MVS_CONV_IN_C4) ? ((flags & MVS_CONV_IN_BF16) ? 2 : 1) : 0;
+  const int quads = (flags & MVS_CONV_IN_C4)
+                        ? ((flags & MVS_CONV_IN_SPLIT) ? 3 : ((flags & MVS_CONV_IN_BF16) ? 2 : 1)) : 0;
   const int st = mvs::launch_conv3d_region(mode, (flags & MVS_CONV_OUT_NCDHW) != 0, quads,
                                            x, x2, weight, y, batch, c_in, c_out, dims, out_origin, out_size,
                                            in_origin, in_size, pad, bn_scale, bn_shift, bn_mean,
-                                           (hipStream_t)stream);
+                                           (hipStream_t)stream, reinterpret_cast<const uint32_t*>(x_absmax));
   if (st != MVS_OK) return st;
   return lc.status();
 }

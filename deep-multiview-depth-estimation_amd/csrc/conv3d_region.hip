@@ -25,6 +25,7 @@
 // fp32 rounding-level differences.
 #include "launchers.h"
 #include "packed.h"
+#include "split.h"
 
 namespace mvs {
 namespace {
@@ -48,7 +49,9 @@ struct Geo {
   int in[3];    // input region size (S1, T2)
   int pad[3];   // P (S2, T2)
   int out_cf;   // 1: output region tensor channels-first y[b][co][z][y][x] (else channels-last)
-  int in_c4;    // S2: the volume is channel-quad x[b][C/4][D][H][W][4], fp32 (1) or bf16 (2); 0 NCDHW
+  int in_c4;    // S2: the volume is channel-quad x[b][C/4][D][H][W][4], fp32 (1), bf16 (2) or the split
+                //     cost volume (3, split.h: fp32 re-formed on load as (hi + lo) 2^-e); 0 NCDHW
+  const uint32_t* absmax;   // in_c4 = 3: the volume's bound words (its scale)
 };
 
 // T2 parity class: per dim, outputs o with (o + P) % 2 == par; first such o in the region and count
@@ -97,6 +100,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
     }
   }
   const int rows = cn[0] * cn[1] * cn[2];
+  const int sx = QM == 3 ? cv_split_exponent(g.absmax) : 0;
   const int step = MODE == kT2 ? 2 : 1;
   constexpr int kRows = 16 * RB;
   // XCD-contiguous row blocks (gridDim.x is a multiple of 8): workgroups are dealt round-robin over
@@ -185,7 +189,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
           if constexpr (QM == 2)   // bf16 quads: 8 bytes per voxel and quad
             rs = make_rsrc(reinterpret_cast<const char*>(x) + ((size_t)b * (CI / 4) + cb * 4) * nvol * 8,
                            (uint32_t)(nvol * 32));
-          else if constexpr (QM == 1)
+          else if constexpr (QM == 1 || QM == 3)
             rs = make_rsrc(x + ((size_t)b * (CI / 4) + cb * 4) * nvol * 4, (uint32_t)(nvol * 64));
           else
             rs = make_rsrc(x + ((size_t)b * CI + cb * 16) * nvol, (uint32_t)(nvol * 64));
@@ -208,6 +212,10 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
                     rs, (int)(vx == kOob ? kOob : ((uint32_t)kq * (uint32_t)nvol + vx) * 8u), 0, 0);
                 v = f4v_t{__uint_as_float(p.x << 16), __uint_as_float(p.x & 0xFFFF0000u),
                           __uint_as_float(p.y << 16), __uint_as_float(p.y & 0xFFFF0000u)};
+              } else if constexpr (QM == 3) {   // split quad: 16-byte load, (hi + lo) 2^-sx (exact sum)
+                v = unsplit4(__builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                 rs, (int)(vx == kOob ? kOob : ((uint32_t)kq * (uint32_t)nvol + vx) * 16u), 0, 0)),
+                             sx);
               } else if constexpr (QM == 1) {   // the quad (c4 / 4) of the voxel: one 16-byte load
                 v = ld4(rs, vx == kOob ? kOob : ((uint32_t)kq * (uint32_t)nvol + vx) * 16u, 0);
               } else {
@@ -286,10 +294,11 @@ void launch_mode(const float* x, const float* x2, const float* w, float* y, cons
 int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const float* x2, const float* w,
                          float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on, const int* i0,
                          const int* in, const int* pad, const float* bn_scale, const float* bn_shift,
-                         const float* bn_mean, hipStream_t s) {
+                         const float* bn_mean, hipStream_t s, const uint32_t* absmax) {
   Geo g;
   g.out_cf = out_cf ? 1 : 0;
   g.in_c4 = in_c4;
+  g.absmax = absmax;
   for (int d = 0; d < 3; ++d) {
     g.n[d] = n[d];
     g.o0[d] = o0[d];
@@ -306,7 +315,8 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
   }
 #define MVS_REGION_S2(A, C)                                                                                   \
   if (mode == kS2 && CI == A && CO == C) {                                                                    \
-    if (in_c4 == 2) launch_mode<kS2, A, C, 2, 2>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s);         \
+    if (in_c4 == 3) launch_mode<kS2, A, C, 2, 3>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s);         \
+    else if (in_c4 == 2) launch_mode<kS2, A, C, 2, 2>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s);    \
     else if (in_c4) launch_mode<kS2, A, C, 2, 1>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s);         \
     else launch_mode<kS2, A, C, 2, 0>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s);                    \
     return MVS_OK;                                                                                            \

@@ -24,6 +24,7 @@
 // ds_read_b128 lane group hits 16 distinct bank groups.
 #include "launchers.h"
 #include "packed.h"
+#include "split.h"
 
 namespace mvs {
 namespace {
@@ -56,35 +57,10 @@ struct S2Geo {
   int tiles_x, tiles_y, zchunks, zc;   // workgroup grid; output depths per chunk (even)
 };
 
-__device__ inline int s2_split_exponent(const uint32_t* __restrict__ absmax) {
-  if (!absmax) return 0;
-  uint32_t m = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) m = max(m, absmax[i]);
-  if (m == 0u || m >= 0x7F800000u) return 0;
-  int e;
-  (void)frexpf(__uint_as_float(m), &e);
-  return min(max(14 - 2 * e, -120), 120);
-}
-
-__device__ inline void split4(const f4v v, int e, uint2& hi, uint2& lo) {
-  _Float16 h[4], l[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float s = ldexpf(v[j], e);
-    h[j] = (_Float16)s;
-    l[j] = (_Float16)(s - (float)h[j]);
-  }
-  auto pk = [](_Float16 a, _Float16 b) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
-  };
-  hi = make_uint2(pk(h[0], h[1]), pk(h[2], h[3]));
-  lo = make_uint2(pk(l[0], l[1]), pk(l[2], l[3]));
-}
-
 // deinterleaved footprint column of input column c (0 .. 32): even columns first
 __device__ inline int fcol(int c) { return (c & 1) ? (kOX + 1) + (c >> 1) : (c >> 1); }
 
+template <bool PRESPLIT>   // input: the split cost volume (SCV, split.h) or fp32 channel quads
 __global__ __launch_bounds__(kThreads) void conv_s2_split_kernel(
     const f4v* __restrict__ cv, const h8v* __restrict__ wfrag, const uint32_t* __restrict__ absmax, int w_exp,
     float* __restrict__ y, S2Geo g, int total, const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
@@ -101,7 +77,7 @@ __global__ __launch_bounds__(kThreads) void conv_s2_split_kernel(
   const int b = t / g.zchunks;
   const int oz1 = min(oz0 + g.zc, g.o0[0] + g.on[0]);
   const int nsteps = (oz1 - oz0 + kOZ - 1) / kOZ;
-  const int ex = s2_split_exponent(absmax);
+  const int ex = cv_split_exponent(absmax);
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int D = g.n[0], H = g.n[1], W = g.n[2];
   const size_t HW = (size_t)H * W, DHW = (size_t)D * HW;
@@ -157,7 +133,13 @@ __global__ __launch_bounds__(kThreads) void conv_s2_split_kernel(
       int s = s0 + pl;
       s = s >= kNPL ? s - kNPL : s;
       uint2 hi, lo;
-      split4(pre[j], ex, hi, lo);
+      if constexpr (PRESPLIT) {   // already the consumer's operands: two 8-byte halves
+        const uint4 w = __builtin_bit_cast(uint4, pre[j]);
+        hi = make_uint2(w.x, w.y);
+        lo = make_uint2(w.z, w.w);
+      } else {
+        split4(pre[j], ex, hi, lo);
+      }
       char* p = lds + s * kSlotB + (em[j] & 0x3FFF);
       *reinterpret_cast<uint2*>(p) = hi;
       *reinterpret_cast<uint2*>(p + kPartB) = lo;
@@ -244,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void conv_s2_split_kernel(
 
 }  // namespace
 
-int launch_conv_s2_split(const float* x, const void* wfrag, int w_exp, const uint32_t* absmax, float* y, int B,
+int launch_conv_s2_split(const void* x, bool presplit, const void* wfrag, int w_exp, const uint32_t* absmax, float* y, int B,
                          const int* n, const int* o0, const int* on, const int* pad, const float* bn_scale,
                          const float* bn_shift, const float* bn_mean, hipStream_t s) {
   S2Geo g;
@@ -260,7 +242,8 @@ int launch_conv_s2_split(const float* x, const void* wfrag, int w_exp, const uin
   g.zchunks = (on[0] + g.zc - 1) / g.zc;
   const long total = (long)g.tiles_x * g.tiles_y * g.zchunks * B;
   if (total >= (1L << 31) - 8) return MVS_ERR_TOO_LARGE;
-  hipLaunchKernelGGL(conv_s2_split_kernel, xcd_grid((int)total), dim3(kThreads), 0, s, reinterpret_cast<const f4v*>(x),
+  hipLaunchKernelGGL(presplit ? conv_s2_split_kernel<true> : conv_s2_split_kernel<false>, xcd_grid((int)total),
+                     dim3(kThreads), 0, s, reinterpret_cast<const f4v*>(x),
                      reinterpret_cast<const h8v*>(wfrag), absmax, w_exp, y, g, (int)total, bn_scale, bn_shift, bn_mean);
   return MVS_OK;
 }

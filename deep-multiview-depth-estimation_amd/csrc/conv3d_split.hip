@@ -35,6 +35,7 @@
 // every ds_read_b128 lane group hit 16 distinct 16-byte bank groups for all three kx shifts.
 #include "launchers.h"
 #include "packed.h"
+#include "split.h"
 
 namespace mvs {
 namespace {
@@ -55,38 +56,11 @@ constexpr int kPre = (kZS * kPlaneQ + kThreads - 1) / kThreads;  // 7 staging qu
 constexpr int kPF = 3;                                           // A-fragment prefetch distance (items)
 constexpr uint32_t kOob = 0xFFFFFFF0u;                          // buffer offset past every descriptor
 
-// 2^e with bound * 2^e < 2^14 for every element of the cost volume: it is at most (max|feat|)^2
-__device__ inline int cv_split_exponent(const uint32_t* __restrict__ absmax) {
-  if (!absmax) return 0;
-  uint32_t m = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) m = max(m, absmax[i]);
-  if (m == 0u || m >= 0x7F800000u) return 0;   // all zero, or Inf/NaN present: unscaled
-  int e;
-  (void)frexpf(__uint_as_float(m), &e);   // max|feat| < 2^e
-  return min(max(14 - 2 * e, -120), 120);
-}
-
-// hi / lo fp16 parts of 4 fp32 values times 2^e, packed 2 per dword
-__device__ inline void split4(const f4v v, int e, uint2& hi, uint2& lo) {
-  const float s[4] = {ldexpf(v[0], e), ldexpf(v[1], e), ldexpf(v[2], e), ldexpf(v[3], e)};
-  _Float16 h[4], l[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    h[j] = (_Float16)s[j];
-    l[j] = (_Float16)(s[j] - (float)h[j]);
-  }
-  auto pk = [](_Float16 a, _Float16 b) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
-  };
-  hi = make_uint2(pk(h[0], h[1]), pk(h[2], h[3]));
-  lo = make_uint2(pk(l[0], l[1]), pk(l[2], l[3]));
-}
-
 __device__ inline float ror8(float v) {   // value of lane (l ^ 8) inside each 16-lane row
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
 }
 
+template <bool PRESPLIT>   // input: the split cost volume (SCV, split.h) or fp32 channel quads
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void conv0_split_kernel(
     const f4v* __restrict__ cv, const h8v* __restrict__ wfrag, const uint32_t* __restrict__ absmax, int w_exp,
     float* __restrict__ out, int D, int H, int W, int tiles_x, int tiles_y, int zchunks, int total,
@@ -162,7 +136,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
       int s = s0 + pl;
       s = s >= kNPL ? s - kNPL : s;
       uint2 hi, lo;
-      split4(pre[j], ex, hi, lo);
+      if constexpr (PRESPLIT) {   // already the consumer's operands: two 8-byte halves
+        const uint4 w = __builtin_bit_cast(uint4, pre[j]);
+        hi = make_uint2(w.x, w.y);
+        lo = make_uint2(w.z, w.w);
+      } else {
+        split4(pre[j], ex, hi, lo);
+      }
       char* p = lds + s * kSlotB + (em[j] & 0x1FFF);
       *reinterpret_cast<uint2*>(p) = hi;
       *reinterpret_cast<uint2*>(p + kPartB) = lo;
@@ -269,13 +249,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
 
 }  // namespace
 
-int launch_conv3d_split(const float* x, const void* wfrag, int w_exp, const uint32_t* absmax, float* y, int B,
-                        int D, int H, int W, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+int launch_conv3d_split(const void* x, bool presplit, const void* wfrag, int w_exp, const uint32_t* absmax, float* y,
+                        int B, int D, int H, int W, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                         hipStream_t s) {
   const int tiles_x = (W + kSX - 1) / kSX, tiles_y = (H + kSY - 1) / kSY, zchunks = (D + kZC - 1) / kZC;
   const long total = (long)tiles_x * tiles_y * zchunks * B;
   if (total >= (1L << 31) - 8) return MVS_ERR_TOO_LARGE;
-  hipLaunchKernelGGL(conv0_split_kernel, xcd_grid((int)total), dim3(kThreads), 0, s,
+  hipLaunchKernelGGL(presplit ? conv0_split_kernel<true> : conv0_split_kernel<false>, xcd_grid((int)total),
+                     dim3(kThreads), 0, s,
                      reinterpret_cast<const f4v*>(x), reinterpret_cast<const h8v*>(wfrag), absmax, w_exp, y, D, H,
                      W, tiles_x, tiles_y, zchunks, (int)total, bn_scale, bn_shift, bn_mean);
   return MVS_OK;

@@ -22,6 +22,7 @@
 //     plane; a plane that still does not fit samples straight from the packed global features.
 // Workgroup ids are remapped so each XCD walks consecutive (tile, plane group) items.
 #include "launchers.h"
+#include "split.h"
 #include "packed.h"
 #include "sampling_matrix.h"
 
@@ -297,11 +298,19 @@ __device__ inline void store_out(Rsrc rs, uint32_t voff, float v) {
 //   ES = 8   bf16 channel-quad (SURVEY.md §8 f3 reduced-precision opt-in): the same layout with each
 //            fp32 variance rounded to nearest-even bf16, one 8-byte store per (pixel, plane, chunk), a
 //            wave's 64 pixels one contiguous 512-B run; the regulariser's HIP layers widen it on load
+//   ES = kQuadSplit  the split cost volume (split.h "SCV", the split-fp16 consumers' operands): the
+//            channel-quad layout with each 16-byte element the fp16 hi / lo parts of the 4 fp32
+//            variances scaled by 2^e, e from the prologue's max|feat| bound words
 constexpr int kQuad = 16;
 constexpr int kQuadBf16 = 8;
+constexpr int kQuadSplit = 32;   // a tag: 16-byte elements
 template <int ES>
 constexpr bool quad_layout() {
-  return ES == kQuad || ES == kQuadBf16;
+  return ES == kQuad || ES == kQuadBf16 || ES == kQuadSplit;
+}
+template <int ES>
+constexpr uint32_t elem_bytes() {
+  return ES == kQuadSplit ? 16u : (uint32_t)ES;
 }
 
 // staging pieces per thread carried in registers across a chunk: 4 covers the V = 3 footprints
@@ -311,11 +320,11 @@ constexpr int prefetch_pieces() {
   return V <= 3 ? 4 : 8;
 }
 
-template <int V, int KPG, int ES /* output element bytes: 4 fp32, 2 bf16 */>
+template <int V, int KPG, int ES /* output layout: 4 fp32, 2 bf16, 16 / 8 / kQuadSplit channel quads */>
 __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_kernel(
     const float4* __restrict__ packed, const float4* __restrict__ refs,
     const float* __restrict__ sampling, void* __restrict__ cv, int C, int h, int w, int Dc, int pg_n,
-    int tiles_x, int tiles_y, int groups, int total) {
+    int tiles_x, int tiles_y, int groups, int total, const uint32_t* __restrict__ absmax) {
   constexpr int NS = V - 1;
   constexpr int SLOTS = staged_slots<V>();
   __shared__ f4v lds[SLOTS];
@@ -430,14 +439,16 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   const uint32_t pix = (uint32_t)(active ? py : 0) * (uint32_t)w + (uint32_t)(active ? px : 0);
   const float4* rbase = refs + (size_t)b * c4 * hw + pix;
   // store byte offset of (plane 0, this pixel) inside a (channel, group) descriptor
-  const uint32_t soff0 = active ? pix * (uint32_t)ES : kOobOffset;
-  const uint32_t grp_bytes = (uint32_t)npl * hw * (uint32_t)ES;
+  constexpr uint32_t EB = elem_bytes<ES>();
+  const uint32_t soff0 = active ? pix * EB : kOobOffset;
+  const uint32_t grp_bytes = (uint32_t)npl * hw * EB;
+  const int sx = ES == kQuadSplit ? cv_split_exponent(absmax) : 0;   // split scale 2^sx (split.h)
 
   // store descriptors of chunk ch's four channels (planes k0 .. k0 + npl of this sample); the
   // channel-quad layout has one descriptor for the chunk's quad plane
   auto chunk_rsrc = [&](int ch, Rsrc (&rs)[4]) {
     if constexpr (quad_layout<ES>()) {
-      rs[0] = make_rsrc(static_cast<char*>(cv) + (((size_t)b * c4 + ch) * Dc + k0) * hw * ES, grp_bytes);
+      rs[0] = make_rsrc(static_cast<char*>(cv) + (((size_t)b * c4 + ch) * Dc + k0) * hw * EB, grp_bytes);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -452,6 +463,12 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
     if constexpr (ES == kQuad) {
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc),
                                              rs[0], (int)(soff0 + (uint32_t)pl * hw * (uint32_t)kQuad), 0, kStoreAux);
+    } else if constexpr (ES == kQuadSplit) {
+      uint2 hi, lo;
+      split4(acc, sx, hi, lo);
+      typedef __attribute__((ext_vector_type(4))) unsigned v4u;
+      __builtin_amdgcn_raw_buffer_store_b128(v4u{hi.x, hi.y, lo.x, lo.y}, rs[0],
+                                             (int)(soff0 + (uint32_t)pl * hw * EB), 0, kStoreAux);
     } else if constexpr (ES == kQuadBf16) {
       typedef __attribute__((ext_vector_type(2))) unsigned v2u;
       const v2u pk = {bf16_rne(acc[0]) | (bf16_rne(acc[1]) << 16), bf16_rne(acc[2]) | (bf16_rne(acc[3]) << 16)};
@@ -640,15 +657,15 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
 template <int V, int KPG, int ES>
 void launch_staged(int pg, dim3 grid, hipStream_t s, const float4* packed, const float4* refs,
                    const float* smp, void* cv, const Geometry& g, int tiles_x, int tiles_y, int groups,
-                   int total) {
+                   int total, const uint32_t* absmax) {
   if constexpr (KPG > 1) {
     if (pg < KPG) {
-      launch_staged<V, KPG / 2, ES>(pg, grid, s, packed, refs, smp, cv, g, tiles_x, tiles_y, groups, total);
+      launch_staged<V, KPG / 2, ES>(pg, grid, s, packed, refs, smp, cv, g, tiles_x, tiles_y, groups, total, absmax);
       return;
     }
   }
   hipLaunchKernelGGL((cost_volume_staged_kernel<V, KPG, ES>), grid, dim3(kBlock), 0, s, packed, refs, smp, cv,
-                     g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total);
+                     g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total, absmax);
 }
 
 template <int V, int ES>
@@ -677,7 +694,7 @@ void launch_gather(const Geometry& g, const float* feat, const Cams& cm, float* 
   const int total = g.B * tiles_x * tiles_y * groups;
   if (ev0) (void)hipEventRecord(ev0, s);
   launch_staged<V, group_planes<V>(), ES>(pg, xcd_grid(total), s, packed, refs, smp, cv, g, tiles_x, tiles_y,
-                                         groups, total);
+                                         groups, total, absmax);
   if (ev1) (void)hipEventRecord(ev1, s);
 }
 
@@ -715,7 +732,20 @@ void launch_cost_volume_fwd_bf16(const Geometry& g, const float* feat, const Cam
 
 void launch_cost_volume_fwd_c4(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
                                float* packed, float* cv, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
-                               uint32_t* absmax) {
+                               uint32_t* absmax, bool split) {
+  if (split) {   // the split cost volume (split.h): absmax required (its bound sets the scale)
+    switch (g.V) {
+      case 2: launch_gather<2, kQuadSplit>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
+      case 3: launch_gather<3, kQuadSplit>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
+      case 4: launch_gather<4, kQuadSplit>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
+      case 5: launch_gather<5, kQuadSplit>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
+      case 6: launch_gather<6, kQuadSplit>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
+      case 7: launch_gather<7, kQuadSplit>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
+      case 8: launch_gather<8, kQuadSplit>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
+      default: break;
+    }
+    return;
+  }
   switch (g.V) {
     case 2: launch_gather<2, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;
     case 3: launch_gather<3, kQuad>(g, feat, cm, sampling, packed, cv, s, ev0, ev1, absmax); break;

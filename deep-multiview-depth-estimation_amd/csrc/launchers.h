@@ -26,7 +26,7 @@ void launch_cost_volume_fwd(const Geometry& g, const float* feat, const Cams& cm
 // same, channel-quad layout cv[B][C/4][Dc][h][w][4] fp32, 2 <= V <= 8
 void launch_cost_volume_fwd_c4(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
                                float* packed, float* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
-                               hipEvent_t ev1 = nullptr, uint32_t* absmax = nullptr);
+                               hipEvent_t ev1 = nullptr, uint32_t* absmax = nullptr, bool split = false);
 // same, bf16 channel-quad layout cv[B][C/4][Dc][h][w][4] (RNE), 2 <= V <= 8
 void launch_cost_volume_fwd_c4_bf16(const Geometry& g, const float* feat, const Cams& cm, float* sampling,
                                     float* packed, void* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
@@ -65,14 +65,14 @@ void launch_conv3d_k3_narrow(const float* in, int in_c4, bool wino_z, const floa
 // conv3d_split.hip: conv_0_0 (32 -> 8, 3x3x3, padding 1) on the f16 MFMA with split-fp16 operands;
 // x channel-quad fp32 [B][8][D][H][W][4], wfrag [27][64][8] fp16 fragments (mvs_conv3d_split_weights),
 // absmax 8 words bounding max|feat| of the cost volume (or NULL: unscaled); y NCDHW fp32
-int launch_conv3d_split(const float* x, const void* wfrag, int w_exp, const uint32_t* absmax, float* y, int B,
+int launch_conv3d_split(const void* x, bool presplit, const void* wfrag, int w_exp, const uint32_t* absmax, float* y, int B,
                         int D, int H, int W, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                         hipStream_t s);
 
 // conv3d_s2_split.hip: conv_1_0 (32 -> 16, 3x3x3, stride 2, padding pad) on an output region, split-fp16
 // MFMA; x channel-quad fp32, wfrag [27][2][64][8] fp16 (mvs_conv3d_s2_split_weights), y channels-last
 // region [B][on0][on1][on2][16]
-int launch_conv_s2_split(const float* x, const void* wfrag, int w_exp, const uint32_t* absmax, float* y, int B,
+int launch_conv_s2_split(const void* x, bool presplit, const void* wfrag, int w_exp, const uint32_t* absmax, float* y, int B,
                          const int* n, const int* o0, const int* on, const int* pad, const float* bn_scale,
                          const float* bn_shift, const float* bn_mean, hipStream_t s);
 
@@ -95,13 +95,13 @@ void launch_deconv3d_k3s2(const float* x, const float* x2, int layout, int B, in
 // conv3d_region.hip: region convolutions of the regulariser on the fp32 MFMA (mode 0 = stride 1,
 // 1 = stride 2 from the full NCDHW volume, 2 = transposed stride 2), channels-last region tensors,
 // optional fused eval BN + ReLU, output channels-last or (out_cf) channels-first; in_c4 (S2): the
-// volume is channel-quad, fp32 (1) or bf16 (2);
+// volume is channel-quad, fp32 (1), bf16 (2) or the split cost volume (3, with its bound words absmax);
 // MVS_ERR_INVALID_ARGUMENT for an unsupported (mode, CI, CO)
 int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const float* x2, const float* w,
                          float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on, const int* i0,
                          const int* in,
                          const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                         hipStream_t s);
+                         hipStream_t s, const uint32_t* absmax = nullptr);
 
 // channel_ops.hip: train-mode BatchNorm pieces -- per-channel float64 sums into
 // stats[slot][2][C] (64 slots) and y = relu(BN(x)) [+ relu(BN'(r))], channels-last or NCDHW

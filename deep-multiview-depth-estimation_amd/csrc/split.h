@@ -1,0 +1,52 @@
+// split.h -- split-fp16 operands of the f16 matrix-core kernels (conv3d_split.hip, conv3d_s2_split.hip)
+// and of the cost volume that feeds them (cost_volume_fwd.hip, ES = kQuadSplit).
+//
+// A fp32 value v is scaled by 2^e (exact) and carried as hi = fp16(v 2^e), lo = fp16(v 2^e - hi), both
+// rounded to nearest: hi + lo is v 2^e to 2^-22 relative (fp16's normal range; below it lo is a
+// subnormal with absolute error <= 2^-25 of the 2^14 scale).  For a cost volume the scale comes from
+// the bound words the prologue writes (max |feat|, per XCD): every variance over views is at most
+// max|feat|^2, so e = 14 - 2 exponent(max|feat|) keeps every scaled element below 2^14 (fp16 max 65504).
+//
+// Split cost-volume layout ("SCV"): the channel-quad layout cv[B][C/4][D][h][w] with each 16-byte
+// element {hi(c0) hi(c1) hi(c2) hi(c3) lo(c0) lo(c1) lo(c2) lo(c3)} (fp16), scaled by 2^e.
+#pragma once
+#include "common.h"
+#include "packed.h"
+
+namespace mvs {
+
+__device__ inline int cv_split_exponent(const uint32_t* __restrict__ absmax) {
+  if (!absmax) return 0;
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m = max(m, absmax[i]);
+  if (m == 0u || m >= 0x7F800000u) return 0;   // all zero, or Inf/NaN present: unscaled
+  int e;
+  (void)frexpf(__uint_as_float(m), &e);   // max|feat| < 2^e
+  return min(max(14 - 2 * e, -120), 120);
+}
+
+// hi / lo fp16 parts of 4 fp32 values times 2^e, packed 2 per dword
+__device__ inline void split4(const f4v v, int e, uint2& hi, uint2& lo) {
+  _Float16 h[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float s = ldexpf(v[j], e);
+    h[j] = (_Float16)s;
+    l[j] = (_Float16)(s - (float)h[j]);
+  }
+  auto pk = [](_Float16 a, _Float16 b) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+  };
+  hi = make_uint2(pk(h[0], h[1]), pk(h[2], h[3]));
+  lo = make_uint2(pk(l[0], l[1]), pk(l[2], l[3]));
+}
+
+// fp32 of one split element (4 channels): (hi + lo) 2^-e, exact sum of the parts
+__device__ inline f4v unsplit4(const uint4 p, int e) {
+  auto h = [](uint32_t w, int k) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> (16 * k))); };
+  return f4v{ldexpf(h(p.x, 0) + h(p.z, 0), -e), ldexpf(h(p.x, 1) + h(p.z, 1), -e),
+             ldexpf(h(p.y, 0) + h(p.w, 0), -e), ldexpf(h(p.y, 1) + h(p.w, 1), -e)};
+}
+
+}  // namespace mvs

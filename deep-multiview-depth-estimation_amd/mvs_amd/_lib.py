@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmvs_cost_volume.so"
 # MVS_LIB_PATH: load another build of the same ABI (A/B kernel experiments, tools/gpu_*_ab.sh)
 LIB_PATH = os.environ.get("MVS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 MVS_OK = 0
 MVS_BWD_DETERMINISTIC = 1
@@ -28,6 +28,7 @@ MVS_CONV_OUT_NCDHW = 1
 MVS_CONV_IN_C4 = 2
 MVS_CONV_WINO_Z = 4
 MVS_CONV_IN_BF16 = 8
+MVS_CONV_IN_SPLIT = 16
 MVS_DECONV_WEIGHT_TAPS = 2
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported n_views", -3: "too large",
           -4: "HIP runtime error"}
@@ -51,9 +52,11 @@ SIGNATURES = {
                                         _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p]),
     "mvs_cost_volume_fwd_c4_absmax": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
                                                _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p, _p]),
-    "mvs_conv3d_k3_split_fwd": (_c_int, [_p, _p, _c_int, _p, _p] + [_c_int] * 4 + [_p] * 4),
+    "mvs_conv3d_k3_split_fwd": (_c_int, [_p, _c_int, _p, _c_int, _p, _p] + [_c_int] * 4 + [_p] * 4),
+    "mvs_cost_volume_fwd_c4_split": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
+                                              _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p, _p]),
     "mvs_conv3d_split_weights": (_c_int, [_p, _p, _p]),
-    "mvs_conv3d_s2_split_fwd": (_c_int, [_p, _p, _c_int, _p, _p, _c_int] + [_p] * 8),
+    "mvs_conv3d_s2_split_fwd": (_c_int, [_p, _c_int, _p, _c_int, _p, _p, _c_int] + [_p] * 8),
     "mvs_conv3d_s2_split_weights": (_c_int, [_p, _p, _p]),
     "mvs_cost_volume_fwd_c4_bf16": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
                                              _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p]),
@@ -74,7 +77,7 @@ SIGNATURES = {
     "mvs_conv3d_k3_fwd": (_c_int, [_p, _c_int, _p, _p] + [_c_int] * 6 + [_p] * 4),
     "mvs_conv2d_fwd": (_c_int, [_p, _p, _p] + [_c_int] * 7 + [_p] * 4),
     "mvs_deconv3d_k3s2_fwd": (_c_int, [_p, _p] + [_c_int] * 10 + [_p] + [_c_int] * 6 + [_p] * 6),
-    "mvs_conv3d_region_fwd": (_c_int, [_c_int, _c_int, _p, _p, _p, _p, _c_int, _c_int, _c_int] + [_p] * 10),
+    "mvs_conv3d_region_fwd": (_c_int, [_c_int, _c_int, _p, _p, _p, _p, _c_int, _c_int, _c_int] + [_p] * 11),
     "mvs_softmax_depth_fwd": (_c_int, [_p, _c_int, _c_int, _c_int, _c_int, _p, _p]),
     "mvs_channel_stats_slots": (ctypes.c_size_t, [_c_int, _c_int, _c_int, ctypes.c_longlong]),
     "mvs_channel_stats": (_c_int, [_p, _c_int, _c_int, _c_int, ctypes.c_longlong, _p, _p]),

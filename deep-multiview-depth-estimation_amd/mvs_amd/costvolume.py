@@ -21,14 +21,17 @@ def assemble_cost_volume(warped_feature_maps, n_views: int):
 
 def warp_and_assemble_cost_volume(K_batch, R_batch, T_batch, d_min, d_int, feature_maps,
                                   batch_size, n_views, d_num=D_NUM, d_scale=D_SCALE,
-                                  d_begin=0, d_count=None, cv_dtype=torch.float32, channel_quads=False):
+                                  d_begin=0, d_count=None, cv_dtype=torch.float32, channel_quads=False,
+                                  split=False):
     """-> (cv [B, C, d_count, h, w], d_batch_0 [B, d_num, 1, 1], ref_idx_0 [B] CPU int64).
 
     ``cv_dtype=torch.bfloat16`` (opt-in) returns the fp32 variance rounded to
     bf16 in the kernel's store (half the write); the default fp32 is the reference's.
     ``channel_quads=True`` (inference) returns the same values in the channel-quad layout
     [B, C/4, d_count, h, w, 4] that CostVolumeReg's HIP path reads 16 (fp32) or 8 (bf16) bytes at a
-    time."""
+    time.  ``split=True`` (with channel_quads, fp32): the SPLIT cost volume (int32 elements holding
+    the fp16 hi / lo parts the split-fp16 regulariser kernels read, csrc/split.h), its bound words
+    registered beside it (ops.cv_bound)."""
     if d_count is None:
         d_count = d_num - d_begin
     if d_begin < 0 or d_count <= 0 or d_begin + d_count > d_num:
@@ -42,8 +45,8 @@ def warp_and_assemble_cost_volume(K_batch, R_batch, T_batch, d_min, d_int, featu
                 int(d_begin), int(d_count), float(d_scale))
         if cv_dtype == torch.float32:
             # with its bound words (max |feat|), registered beside the tensor for the split-fp16
-            # conv_0_0 (ops.conv3d_k3_split)
-            cv, absmax = ops.cost_volume_c4_absmax(*args)
+            # regulariser kernels (ops.conv3d_k3_split, ops.conv_s2_split)
+            cv, absmax = (ops.cost_volume_c4_split if split else ops.cost_volume_c4_absmax)(*args)
             ops.register_cv_bound(cv, absmax)
         else:
             cv = ops.cost_volume_c4_bf16(*args)

@@ -159,6 +159,9 @@ class CostVolumeReg(nn.Module):
         if cv.dim() == 6:
             if self.live_ok(cv.shape[2:5]) and _hip_cv(cv):
                 return self.forward_live(cv)
+            if cv.dtype == torch.int32:   # the split cost volume: fp32 values back (to 2^-22) for other paths
+                from .ops import cv_bound, unsplit_cost_volume
+                cv = unsplit_cost_volume(cv, cv_bound(cv))
             if self.live_train_ok(cv.shape[2:5]) and _hip_cv(cv):
                 return self.forward_live_train(cv)
             cv = cv.permute(0, 1, 5, 2, 3, 4).reshape((cv.shape[0], 4 * cv.shape[1]) + tuple(cv.shape[2:5])).float()
@@ -269,7 +272,12 @@ class CostVolumeReg(nn.Module):
         main = torch.cuda.current_stream(cv.device)
         side = _side_stream(cv.device)
         side.wait_stream(main)
-        bound = cv_bound(cv) if c4 and self.split_f16 and cv.dtype == torch.float32 else None
+        # the split cost volume (int32, csrc/split.h) always goes to the split-fp16 kernels; an fp32
+        # channel-quad volume does when split_f16 is on and it carries bound words
+        split_cv = c4 and cv.dtype == torch.int32
+        bound = cv_bound(cv) if split_cv or (c4 and self.split_f16 and cv.dtype == torch.float32) else None
+        if split_cv and bound is None:
+            raise ValueError("split cost volume without its bound words")
         with torch.cuda.stream(side):
             if bound is not None:
                 y0 = conv3d_k3_split(cv, bound, self.conv_0_0.weight, *bn_eval(self.BN_0))
@@ -285,7 +293,7 @@ class CostVolumeReg(nn.Module):
                 ya = conv_s2_split(cv, bound, conv_a.weight, dims, org(halo), size(halo), pad, *bn_eval(bn))
             else:
                 ya = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(halo), size(halo), None,
-                                   None, pad, *bn_eval(bn), in_c4=c4)
+                                   None, pad, *bn_eval(bn), in_c4=c4, absmax=bound if split_cv else None)
             # level 1's output only feeds deconv_1_0's input sum: channels-first for its loads
             return conv3d_region(ya, None, region_weight(conv_b), CONV_S1, dims, org(reg), size(reg),
                                  org(halo), size(halo), None, *bn_eval(bn), out_ncdhw=reg is B)
@@ -451,8 +459,9 @@ def _hip_inference(x):
 
 def _hip_cv(cv):
     """_hip_inference for the regulariser's input: also the bf16 channel-quad cost volume of the
-    reduced-precision opt-in (its HIP layers widen it to fp32 on load)."""
-    return _hip_inference(cv) or (cv.is_cuda and cv.dim() == 6 and cv.dtype == torch.bfloat16
+    reduced-precision opt-in (its HIP layers widen it to fp32 on load) and the split cost volume
+    (int32 elements of fp16 hi / lo parts, read by the split-fp16 kernels)."""
+    return _hip_inference(cv) or (cv.is_cuda and cv.dim() == 6 and cv.dtype in (torch.bfloat16, torch.int32)
                                   and not torch.is_grad_enabled() and not torch.is_autocast_enabled())
 
 
@@ -697,10 +706,13 @@ class MVSNet(nn.Module):
                  and feature_maps.shape[1] % 4 == 0
                  and (reg.live_ok((c.d_num,) + tuple(feature_maps.shape[2:]))
                       or reg.live_train_ok((c.d_num,) + tuple(feature_maps.shape[2:]))))
+        # eval mode with the split-fp16 regulariser: the fused kernel writes the split cost volume
+        split = (quads and not bf16 and reg.split_f16
+                 and reg.live_ok((c.d_num,) + tuple(feature_maps.shape[2:])) and feature_maps.shape[1] == 32)
         cost_volume, d_batch, ref_views = warp_and_assemble_cost_volume(
             K_batch, R_batch, T_batch, d_min, d_int, feature_maps, batch_size, n_views,
             d_num=c.d_num, d_scale=c.d_scale,
-            cv_dtype=torch.bfloat16 if bf16 else torch.float32, channel_quads=quads)
+            cv_dtype=torch.bfloat16 if bf16 else torch.float32, channel_quads=quads, split=split)
         if bf16 and not quads:
             # opt-in: the volume is STORED in bf16 (rounded once); the regulariser
             # computes in fp32 from the rounded values, as the HIP channel-quad path does

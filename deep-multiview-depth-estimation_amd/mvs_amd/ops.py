@@ -198,7 +198,63 @@ def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scal
     return feat.new_empty((batch_size, c // 4, d_count, h, w, 4)), feat.new_empty((8,), dtype=torch.int32)
 
 
-# bound words of channel-quad cost volumes made by cost_volume_c4_absmax (id(cv) -> (weak cv, words)):
+@torch.library.custom_op("mvs::cost_volume_c4_split", mutates_args=())
+def cost_volume_c4_split(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.Tensor,
+                         d_min: torch.Tensor, d_int: torch.Tensor, batch_size: int, n_views: int,
+                         d_begin: int, d_count: int, d_scale: float) -> tuple[torch.Tensor, torch.Tensor]:
+    """The SPLIT cost volume (mvs_cost_volume_fwd_c4_split, csrc/split.h): int32 [B, C/4, d_count, h, w, 4]
+    holding, per 16-byte element, the fp16 hi / lo parts of 4 variances scaled by 2^e (e from the bound
+    words, returned beside it) -- the operands the split-fp16 regulariser kernels read without
+    converting.  unsplit_cost_volume() gives the fp32 values back (to 2^-22)."""
+    _require_gpu(feat, "feature_maps")
+    lib = _lib.load()
+    feat = feat.to(_F32).contiguous()
+    K, R, T, d_min, d_int = _cams(K, R, T, d_min, d_int, feat.device, batch_size)
+    _check_geometry(feat, K, batch_size, n_views)
+    n, c, h, w = feat.shape
+    if c % 4:
+        raise ValueError("the channel-quad cost volume needs C % 4 == 0, got C=%d" % c)
+    cv = torch.empty((batch_size, c // 4, d_count, h, w, 4), device=feat.device, dtype=torch.int32)
+    absmax = torch.empty((8,), device=feat.device, dtype=torch.int32)
+    ws = torch.empty((_ws_floats(batch_size, n_views, c, h, w, d_count),), device=feat.device,
+                     dtype=_F32)
+    evs = (None, None)
+    if KERNEL_EVENT_HOOK is not None:
+        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK())
+    st = lib.mvs_cost_volume_fwd_c4_split(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T),
+                                          _lib.ptr(d_min), _lib.ptr(d_int), batch_size, n_views, c, h, w,
+                                          d_begin, d_count, float(d_scale), _lib.ptr(ws), _lib.ptr(cv),
+                                          _lib.stream_handle(feat.device), *evs, _lib.ptr(absmax))
+    _lib.check(st, "mvs_cost_volume_fwd_c4_split")
+    return cv, absmax
+
+
+@cost_volume_c4_split.register_fake
+def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scale):
+    n, c, h, w = feat.shape
+    return (feat.new_empty((batch_size, c // 4, d_count, h, w, 4), dtype=torch.int32),
+            feat.new_empty((8,), dtype=torch.int32))
+
+
+def split_exponent(absmax):
+    """The scale exponent e of a split cost volume from its bound words (csrc/split.h rule, host side)."""
+    import math
+    m = int(absmax.to(torch.int64).max().item())
+    if m == 0 or m >= 0x7F800000:
+        return 0
+    b = torch.tensor([m], dtype=torch.int32).view(torch.float32).item()
+    return min(max(14 - 2 * math.frexp(b)[1], -120), 120)
+
+
+def unsplit_cost_volume(cv, absmax):
+    """fp32 channel-quad [B, C/4, D, h, w, 4] of a split cost volume: (hi + lo) 2^-e per element."""
+    e = split_exponent(absmax)
+    halves = cv.contiguous().view(torch.float16).reshape(cv.shape[:-1] + (2, 4)).float()
+    return torch.ldexp(halves[..., 0, :] + halves[..., 1, :], torch.tensor(-e, device=cv.device,
+                                                                            dtype=torch.float32))
+
+
+# bound words of channel-quad cost volumes made by cost_volume_c4_absmax / cost_volume_c4_split (id(cv) -> (weak cv, words)):
 # CostVolumeReg keeps the reference's forward(cv) signature, so the bound travels beside the tensor
 _CV_BOUNDS = {}
 
@@ -496,8 +552,12 @@ def conv3d_k3_split(x: torch.Tensor, absmax: Optional[torch.Tensor], weight: tor
     |x| < 2^15 must hold).  Inference only."""
     _require_gpu(x, "x")
     lib = _lib.load()
-    if x.dim() != 6 or tuple(x.shape[1:2]) + tuple(x.shape[-1:]) != (8, 4) or x.dtype != _F32:
-        raise ValueError("x: fp32 channel-quad [B, 8, D, H, W, 4] expected, got %s %s" % (tuple(x.shape), x.dtype))
+    if x.dim() != 6 or tuple(x.shape[1:2]) + tuple(x.shape[-1:]) != (8, 4) or x.dtype not in (_F32, torch.int32):
+        raise ValueError("x: fp32 or split (int32) channel-quad [B, 8, D, H, W, 4] expected, got %s %s"
+                         % (tuple(x.shape), x.dtype))
+    split_in = x.dtype == torch.int32
+    if split_in and absmax is None:
+        raise ValueError("the split cost volume needs its bound words (absmax)")
     if tuple(weight.shape) != (8, 32, 3, 3, 3):
         raise ValueError("weight [8, 32, 3, 3, 3] expected, got %s" % (tuple(weight.shape),))
     x = x.contiguous()
@@ -512,7 +572,7 @@ def conv3d_k3_split(x: torch.Tensor, absmax: Optional[torch.Tensor], weight: tor
             raise ValueError("absmax: int32[8] on the volume's device expected")
         absmax = absmax.contiguous()
     y = torch.empty((b, 8, d, h, wd), device=x.device, dtype=_F32)
-    st = lib.mvs_conv3d_k3_split_fwd(_lib.ptr(x), _lib.ptr(frag), int(wexp),
+    st = lib.mvs_conv3d_k3_split_fwd(_lib.ptr(x), _lib.MVS_CONV_IN_SPLIT if split_in else 0, _lib.ptr(frag), int(wexp),
                                      None if absmax is None else _lib.ptr(absmax), _lib.ptr(y),
                                      b, d, h, wd, *bp, _lib.stream_handle(x.device))
     _lib.check(st, "mvs_conv3d_k3_split_fwd")
@@ -521,7 +581,7 @@ def conv3d_k3_split(x: torch.Tensor, absmax: Optional[torch.Tensor], weight: tor
 
 @conv3d_k3_split.register_fake
 def _(x, absmax, weight, bn_scale=None, bn_shift=None, bn_mean=None):
-    return x.new_empty((x.shape[0], 8) + tuple(x.shape[2:5]))
+    return x.new_empty((x.shape[0], 8) + tuple(x.shape[2:5]), dtype=_F32)
 
 
 @torch.library.custom_op("mvs::conv_s2_split", mutates_args=())
@@ -535,8 +595,12 @@ def conv_s2_split(x: torch.Tensor, absmax: Optional[torch.Tensor], weight: torch
     ``absmax``: the volume's bound words (cost_volume_c4_absmax), None = unscaled.  Inference only."""
     _require_gpu(x, "x")
     lib = _lib.load()
-    if x.dim() != 6 or x.shape[1] != 8 or x.shape[-1] != 4 or x.dtype != _F32:
-        raise ValueError("x: fp32 channel-quad [B, 8, D, H, W, 4] expected, got %s %s" % (tuple(x.shape), x.dtype))
+    if x.dim() != 6 or x.shape[1] != 8 or x.shape[-1] != 4 or x.dtype not in (_F32, torch.int32):
+        raise ValueError("x: fp32 or split (int32) channel-quad [B, 8, D, H, W, 4] expected, got %s %s"
+                         % (tuple(x.shape), x.dtype))
+    split_in = x.dtype == torch.int32
+    if split_in and absmax is None:
+        raise ValueError("the split cost volume needs its bound words (absmax)")
     if tuple(weight.shape) != (16, 32, 3, 3, 3):
         raise ValueError("weight [16, 32, 3, 3, 3] expected, got %s" % (tuple(weight.shape),))
     if list(x.shape[2:5]) != [int(v) for v in dims]:
@@ -552,7 +616,7 @@ def conv_s2_split(x: torch.Tensor, absmax: Optional[torch.Tensor], weight: torch
             raise ValueError("absmax: int32[8] on the volume's device expected")
         absmax = absmax.contiguous()
     y = torch.empty([x.shape[0]] + [int(v) for v in out_size] + [16], device=x.device, dtype=_F32)
-    st = lib.mvs_conv3d_s2_split_fwd(_lib.ptr(x), _lib.ptr(frag), int(wexp),
+    st = lib.mvs_conv3d_s2_split_fwd(_lib.ptr(x), _lib.MVS_CONV_IN_SPLIT if split_in else 0, _lib.ptr(frag), int(wexp),
                                      None if absmax is None else _lib.ptr(absmax), _lib.ptr(y), x.shape[0],
                                      _ints3(dims), _ints3(out_origin), _ints3(out_size), _ints3(pad), *bp,
                                      _lib.stream_handle(x.device))
@@ -562,7 +626,7 @@ def conv_s2_split(x: torch.Tensor, absmax: Optional[torch.Tensor], weight: torch
 
 @conv_s2_split.register_fake
 def _(x, absmax, weight, dims, out_origin, out_size, pad, bn_scale=None, bn_shift=None, bn_mean=None):
-    return x.new_empty([x.shape[0]] + [int(v) for v in out_size] + [16])
+    return x.new_empty([x.shape[0]] + [int(v) for v in out_size] + [16], dtype=_F32)
 
 
 def _s2_split_fragments(weight, device):
@@ -770,7 +834,7 @@ def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Ten
                   in_origin: Optional[list[int]], in_size: Optional[list[int]], pad: Optional[list[int]],
                   bn_scale: Optional[torch.Tensor] = None, bn_shift: Optional[torch.Tensor] = None,
                   bn_mean: Optional[torch.Tensor] = None, out_ncdhw: bool = False,
-                  in_c4: bool = False) -> torch.Tensor:
+                  in_c4: bool = False, absmax: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Region convolution (mvs_conv3d_region_fwd): mode CONV_S2 reads the full NCDHW volume x
     (in_c4: the channel-quad [B, C/4, D, H, W, 4] of cost_volume_c4, or bf16 of cost_volume_c4_bf16),
     CONV_S1 / CONV_T2 a channels-last region tensor x (+ x2) on in_origin + [0, in_size); returns the
@@ -779,7 +843,10 @@ def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Ten
     _require_gpu(x, "x")
     lib = _lib.load()
     quad_bf16 = in_c4 and x.dtype == torch.bfloat16
-    x = x.contiguous() if quad_bf16 else x.to(_F32).contiguous()
+    quad_split = in_c4 and x.dtype == torch.int32   # the split cost volume (absmax: its bound words)
+    if quad_split and (absmax is None or absmax.numel() != 8 or absmax.dtype != torch.int32):
+        raise ValueError("the split cost volume needs its bound words (absmax, int32[8])")
+    x = x.contiguous() if (quad_bf16 or quad_split) else x.to(_F32).contiguous()
     if x2 is not None:
         x2 = x2.to(_F32).contiguous()
     w = weight.to(device=x.device, dtype=_F32).contiguous()
@@ -791,13 +858,14 @@ def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Ten
     shape = (b, cout) + tuple(out_size) if out_ncdhw else (b,) + tuple(out_size) + (cout,)
     y = torch.empty(shape, device=x.device, dtype=_F32)
     flags = ((_lib.MVS_CONV_OUT_NCDHW if out_ncdhw else 0) | (_lib.MVS_CONV_IN_C4 if in_c4 else 0)
-             | (_lib.MVS_CONV_IN_BF16 if quad_bf16 else 0))
+             | (_lib.MVS_CONV_IN_BF16 if quad_bf16 else 0) | (_lib.MVS_CONV_IN_SPLIT if quad_split else 0))
     st = lib.mvs_conv3d_region_fwd(int(mode), flags, _lib.ptr(x), None if x2 is None else _lib.ptr(x2), _lib.ptr(w),
                                    _lib.ptr(y), b, cin, cout, _ints3(dims), _ints3(out_origin), _ints3(out_size),
                                    None if in_origin is None else _ints3(in_origin),
                                    None if in_size is None else _ints3(in_size),
                                    None if pad is None else _ints3(pad),
                                    *[None if t is None else _lib.ptr(t) for t in bn],
+                                   _lib.ptr(absmax.contiguous()) if quad_split else None,
                                    _lib.stream_handle(x.device))
     _lib.check(st, "mvs_conv3d_region_fwd")
     return y
@@ -805,10 +873,10 @@ def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Ten
 
 @conv3d_region.register_fake
 def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, bn_scale=None, bn_shift=None,
-      bn_mean=None, out_ncdhw=False, in_c4=False):
+      bn_mean=None, out_ncdhw=False, in_c4=False, absmax=None):
     if out_ncdhw:
-        return x.new_empty((x.shape[0], weight.shape[1]) + tuple(out_size))
-    return x.new_empty((x.shape[0],) + tuple(out_size) + (weight.shape[1],))
+        return x.new_empty((x.shape[0], weight.shape[1]) + tuple(out_size), dtype=_F32)
+    return x.new_empty((x.shape[0],) + tuple(out_size) + (weight.shape[1],), dtype=_F32)
 
 
 # ----------------------------------------------------------------------------------------------

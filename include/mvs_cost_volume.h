@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 7
+#define MVS_ABI_VERSION 8
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -140,6 +140,21 @@ int mvs_cost_volume_fwd_c4_absmax(const float* feat, const float* K, const float
                                   void* main_begin_event, void* main_end_event, unsigned* feat_absmax);
 
 /*
+ * mvs_cost_volume_fwd_c4_absmax writing the SPLIT cost volume: the channel-quad layout with each
+ * 16-byte element {hi(c0..c3), lo(c0..c3)} fp16, hi = fp16(v 2^e), lo = fp16(v 2^e - hi) (nearest),
+ * e = 14 - 2 exponent(B) with B = max of the feat_absmax words (clamped to [-120, 120]; 0 when B is 0,
+ * Inf or NaN) -- the operands of the split-fp16 consumers (MVS_CONV_IN_SPLIT), which then convert
+ * nothing.  hi + lo = v 2^e to 2^-22 relative.  feat_absmax required; otherwise as
+ * mvs_cost_volume_fwd_c4_absmax.
+ */
+int mvs_cost_volume_fwd_c4_split(const float* feat, const float* K, const float* R, const float* T,
+                                 const float* d_min, const float* d_int,
+                                 int batch_size, int n_views, int channels, int h, int w,
+                                 int d_begin, int d_count, float d_scale,
+                                 float* workspace, void* cv_out, void* stream,
+                                 void* main_begin_event, void* main_end_event, unsigned* feat_absmax);
+
+/*
  * mvs_cost_volume_fwd_c4 with bf16 storage (SURVEY.md §8 f3 reduced-precision cost volume, opt-in):
  * cv_out[B][ceil(C/4)][d_count][h][w][4] bf16 (uint16 storage, 8-byte aligned), each element the fp32
  * variance of mvs_cost_volume_fwd rounded to nearest-even (bit-identical to torch's .to(torch.bfloat16)
@@ -240,6 +255,10 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
  * transformed wu[c_in][3][3][4][8]: per (c_in, ky, kx, c_out) the depth taps g0..g2 become
  * (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2) (formed in float64, rounded once) */
 #define MVS_CONV_WINO_Z 4
+/* input flag of mvs_conv3d_k3_split_fwd / mvs_conv3d_s2_split_fwd / mvs_conv3d_region_fwd (MVS_CONV_S2):
+ * the volume is the split cost volume of mvs_cost_volume_fwd_c4_split (the channel-quad layout, each
+ * 16-byte element the fp16 hi / lo parts of 4 values scaled by 2^e, e from its bound words) */
+#define MVS_CONV_IN_SPLIT 16
 
 /* Regulariser layers conv_0_0 (32 -> 8) and conv_out (8 -> 1) of CostVolumeReg (model.py:77,96 /
  * forward at model.py:101,123): nn.Conv3d(c_in, c_out, 3, stride=1, padding=1, bias=False) over
@@ -260,16 +279,18 @@ int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, 
  * on the f16 matrix cores with split operands (csrc/conv3d_split.hip): every fp32 operand is scaled by
  * a power of two and carried as fp16 hi + lo parts, the four partial products of each term are exact
  * in fp32 and accumulated in fp32, so the result has fp32-level error.
- *   x: the channel-quad cost volume x[batch][8][d][h][w][4] fp32 of mvs_cost_volume_fwd_c4(_absmax),
- *      16-byte aligned; x_absmax: its 8 bound words (every |x| <= B^2, see
- *      mvs_cost_volume_fwd_c4_absmax), DEVICE, or NULL when every |x| < 2^15 is known (unscaled);
+ *   x: the channel-quad cost volume x[batch][8][d][h][w][4] fp32 of mvs_cost_volume_fwd_c4(_absmax)
+ *      (flags 0), or the split cost volume of mvs_cost_volume_fwd_c4_split (flags MVS_CONV_IN_SPLIT:
+ *      read as the kernel's own operands, no conversion), 16-byte aligned; x_absmax: its 8 bound words
+ *      (every |x| <= B^2, see mvs_cost_volume_fwd_c4_absmax), DEVICE, required with
+ *      MVS_CONV_IN_SPLIT, else NULL when every |x| < 2^15 is known (unscaled);
  *   weight_frag / weight_exp: from mvs_conv3d_split_weights (copied to the device, 16-byte aligned);
  *   y[batch][8][d][h][w] fp32; BN pointers as mvs_conv3d_k3_fwd (8 floats each, all or none).
  * 128*d*h*w <= 2^32 - 16 (one sample's volume bytes).  Replaces the Conv3d behind model.py:101's
  * conv_0_0 in eval inference. */
-int mvs_conv3d_k3_split_fwd(const float* x, const void* weight_frag, int weight_exp, const unsigned* x_absmax,
-                            float* y, int batch, int d, int h, int w, const float* bn_scale,
-                            const float* bn_shift, const float* bn_mean, void* stream);
+int mvs_conv3d_k3_split_fwd(const void* x, int flags, const void* weight_frag, int weight_exp,
+                            const unsigned* x_absmax, float* y, int batch, int d, int h, int w,
+                            const float* bn_scale, const float* bn_shift, const float* bn_mean, void* stream);
 
 /* HOST function (no device work): the fp16 MFMA operand fragments of conv_0_0's weight for
  * mvs_conv3d_k3_split_fwd.  weight: nn.Conv3d layout [8][32][3][3][3] fp32, HOST, finite (else
@@ -283,15 +304,17 @@ int mvs_conv3d_split_weights(const float* weight, unsigned short* frag, int* wei
  * BN_1 + ReLU) over the channel-quad cost volume on the output region [out_origin, out_origin +
  * out_size) per dim (forward_live's halo(B)), f16 matrix cores with split operands
  * (csrc/conv3d_s2_split.hip; three partial products x_hi w_hi + x_hi w_lo + x_lo w_hi, fp32 accumulation).
- *   x: x[batch][8][dims[0]][dims[1]][dims[2]][4] fp32 (mvs_cost_volume_fwd_c4_absmax), 16-byte aligned;
- *   x_absmax: its bound words (or NULL: unscaled, every |x| < 2^15 known); weight_frag / weight_exp:
+ *   x: x[batch][8][dims[0]][dims[1]][dims[2]][4] fp32 (mvs_cost_volume_fwd_c4_absmax; flags 0) or the
+ *   split cost volume (mvs_cost_volume_fwd_c4_split; flags MVS_CONV_IN_SPLIT), 16-byte aligned;
+ *   x_absmax: its bound words (required with MVS_CONV_IN_SPLIT; else NULL: unscaled, every |x| < 2^15
+ *   known); weight_frag / weight_exp:
  *   mvs_conv3d_s2_split_weights (copied to the device); y: channels-last region
  *   y[batch][out_size[0]][out_size[1]][out_size[2]][16] fp32; BN pointers 16 floats each, all or none.
  * 128 * dims[0]*dims[1]*dims[2] <= 2^32 - 16.  Replaces model.py:103's conv_1_0 in eval inference. */
-int mvs_conv3d_s2_split_fwd(const float* x, const void* weight_frag, int weight_exp, const unsigned* x_absmax,
-                            float* y, int batch, const int* dims, const int* out_origin, const int* out_size,
-                            const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                            void* stream);
+int mvs_conv3d_s2_split_fwd(const void* x, int flags, const void* weight_frag, int weight_exp,
+                            const unsigned* x_absmax, float* y, int batch, const int* dims,
+                            const int* out_origin, const int* out_size, const int* pad, const float* bn_scale,
+                            const float* bn_shift, const float* bn_mean, void* stream);
 
 /* HOST function: the fp16 MFMA operand fragments of conv_1_0's weight for mvs_conv3d_s2_split_fwd.
  * weight [16][32][3][3][3] fp32 HOST, finite; frag HOST 27*2*64*8 uint16: frag[tap][part][lane][j] =
@@ -358,13 +381,15 @@ int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch,
  * (kd * 3 + kh) * 3 + kw): nn.Conv3d's weight.permute(2, 3, 4, 0, 1), nn.ConvTranspose3d's
  * weight.permute(2, 3, 4, 1, 0).  Supported (mode, c_in, c_out): S2 (32, 16|32|64), S1 (16, 16),
  * (32, 32), (64, 64), T2 (64, 32), (32, 16); else MVS_ERR_INVALID_ARGUMENT.  dims, origins, sizes and
- * pad are HOST pointers to 3 ints.  Eval-mode inference only; products summed in the order (tap,
+ * pad are HOST pointers to 3 ints.  flags = MVS_CONV_S2 input MVS_CONV_IN_C4 | MVS_CONV_IN_SPLIT: the split
+ * cost volume, re-formed to fp32 on load as (hi + lo) 2^-e (2^-22 of each element), x_absmax its bound
+ * words (DEVICE; NULL otherwise).  Eval-mode inference only; products summed in the order (tap,
  * c_in) -- MIOpen sums them in other orders (fp32 rounding-level differences). */
 int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, const float* weight, float* y,
                           int batch, int c_in, int c_out, const int* dims, const int* out_origin,
                           const int* out_size, const int* in_origin, const int* in_size,
                           const int* pad, const float* bn_scale, const float* bn_shift,
-                          const float* bn_mean, void* stream);
+                          const float* bn_mean, const unsigned* x_absmax, void* stream);
 
 /* Softmax over the depth planes of the regulariser's output (CostVolumeReg.Norm = nn.Softmax(2),
  * model.py:97 / :125): y[b][0][d][p] = exp(x - max_d x) / sum_d exp(x - max_d x) per pixel p, in

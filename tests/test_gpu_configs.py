@@ -217,7 +217,7 @@ def test_cfg2_end_to_end_as_benchmarked():
         # the benchmarked regulariser input: the channel-quad volume with its bound words (split-fp16
         # conv_0_0); the NCDHW volume of the same values feeds the exact-fp32 live path and forward_full
         cv4, d_batch, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, B, V, d_num=D,
-                                                        channel_quads=True)
+                                                        channel_quads=True, split=True)
         assert g.cost_volume_reg.live_region
         g_prob = g.cost_volume_reg(cv4)
         del cv4
@@ -300,7 +300,7 @@ def test_model_end_to_end_at_cfg3_cfg5(cfg):
         ini, ref = g(img, K, R, T, d_min, d_int, B, V)                 # the benchmarked call
         # the benchmarked regulariser input (channel-quad volume + bound words: split-fp16 conv_0_0)
         cv, d_batch, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, g.feature_encoder(img),
-                                                       B, V, d_num=D, channel_quads=True)
+                                                       B, V, d_num=D, channel_quads=True, split=True)
         P_live = g.cost_volume_reg(cv)
         del cv
         cv = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, g.feature_encoder(img), B, V, d_num=D)[0]

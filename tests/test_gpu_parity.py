@@ -395,7 +395,7 @@ def test_mvsnet_end_to_end(mode):
         feats = net.feature_encoder(g_img)
         # the benchmarked feed: channel-quad volume + bound words (split-fp16 conv_0_0 in eval mode)
         cv, d_batch, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, 1, 3, d_num=D,
-                                                       channel_quads=True)
+                                                       channel_quads=True, split=mode == "eval")
         g_prob = net.cost_volume_reg(cv)
         g_ini = extract_depth_map(g_prob, d_batch)
     if mode == "eval":
@@ -812,7 +812,7 @@ def test_mvsnet_channel_quad_feed_equals_ncdhw_feed():
     net.cost_volume_reg.split_f16 = True
     with torch.no_grad():
         feats = net.feature_encoder(img)
-        cv4, d_batch, _ = orig(K, R, T, d_min, d_int, feats, B, V, d_num=D, channel_quads=True)
+        cv4, d_batch, _ = orig(K, R, T, d_min, d_int, feats, B, V, d_num=D, channel_quads=True, split=True)
         p_split = net.cost_volume_reg(cv4)
         cv, _, _ = orig(K, R, T, d_min, d_int, feats, B, V, d_num=D)
         p_exact = net.cost_volume_reg(cv)

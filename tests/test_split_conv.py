@@ -235,3 +235,69 @@ def test_s2_split_conv_on_live_region(n, bn):
     print("s2 %s bn=%s: split %.3g, fp32 region kernel %.3g, MIOpen %.3g (scale %.3g)" % (n, bn, err, err32, errt, scale))
     assert err <= 1e-5 * scale, (err, scale)
     assert err <= 1.5 * max(err32, errt) + 1e-7 * scale, (err, err32, errt)
+
+
+# ---- the split cost volume (mvs_cost_volume_fwd_c4_split, csrc/split.h) ---------------------------
+def _fused_volumes(B=2, V=3, C=32, h=40, w=52, D=12, seed=11, scale=7.0):
+    from cameras import camera_batch, depth_range, features
+    from mvs_amd import ops
+    K, R, T = camera_batch(B, V, h, w)
+    d_min, d_int = depth_range(B, d_int=4.0, distinct=True)
+    feat = (features(B * V, C, h, w, seed=seed) * scale).to(DEV)
+    with torch.no_grad():
+        c4, a4 = ops.cost_volume_c4_absmax(feat, K, R, T, d_min, d_int, B, V, 0, D, 25.0)
+        sp, asp = ops.cost_volume_c4_split(feat, K, R, T, d_min, d_int, B, V, 0, D, 25.0)
+    return c4, a4, sp, asp
+
+
+@pytest.mark.gpu
+def test_split_cost_volume_is_the_split_of_the_fp32_volume():
+    """Every 16-byte element of the split volume is exactly (fp16(v 2^e), fp16(v 2^e - hi)) of the fp32
+    channel-quad volume's values (same kernel arithmetic, split in the store), e from the bound words
+    (the same words as the fp32 op's); unsplit gives the values back to 2^-22."""
+    from mvs_amd import ops
+    c4, a4, sp, asp = _fused_volumes()
+    assert torch.equal(a4, asp)
+    e = ops.split_exponent(asp)
+    v = torch.ldexp(c4.double().cpu(), torch.tensor(float(e), dtype=torch.float64))
+    hi = v.float().half()
+    lo = (v - hi.double()).float().half()
+    got = sp.cpu().view(torch.float16).reshape(sp.shape[:-1] + (2, 4))
+    assert torch.equal(got[..., 0, :].view(torch.int16), hi.view(torch.int16))
+    assert torch.equal(got[..., 1, :].view(torch.int16), lo.view(torch.int16))
+    # to 2^-22 relative in fp16's normal range; below it lo is a subnormal (spacing 2^-24 scaled)
+    back = ops.unsplit_cost_volume(sp, asp).cpu()
+    assert ((back - c4.cpu()).abs() <= 2.0 ** -21 * c4.cpu().abs() + 2.0 ** (-24 - e)).all()
+
+
+@pytest.mark.gpu
+def test_split_consumers_read_the_split_volume_like_fp32():
+    """conv_0_0 and conv_1_0 on the split volume: bit-identical to the same kernels converting the fp32
+    volume themselves (the same operands reach the MFMAs); conv_2_0 on the region kernel reading the
+    split volume: within 2^-21 relative of the input perturbation (fp32 re-formed as hi + lo)."""
+    from mvs_amd import model as M
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.ops import CONV_S2, conv3d_k3_split, conv3d_region, conv_s2_split
+    c4, a4, sp, asp = _fused_volumes()
+    n = tuple(c4.shape[2:5])
+    g = torch.Generator().manual_seed(21)
+    w0 = (torch.randn(8, 32, 3, 3, 3, generator=g) * 0.05).to(DEV)
+    w1 = (torch.randn(16, 32, 3, 3, 3, generator=g) * 0.05).to(DEV)
+    w2 = (torch.randn(32, 32, 3, 3, 3, generator=g) * 0.05).to(DEV)
+    pad, _ = pad_outpad(*n)
+    full = tuple((0, d - 1) for d in n)
+    Bq = M._tconv_input_region(full, n, pad)
+    h1 = M._grow(Bq, n, 1)
+    h2 = M._grow(M._tconv_input_region(Bq, n, pad), n, 1)
+    org = lambda r: [lo for lo, _ in r]
+    size = lambda r: [hi - lo + 1 for lo, hi in r]
+    with torch.no_grad():
+        assert torch.equal(conv3d_k3_split(sp, asp, w0), conv3d_k3_split(c4, a4, w0))
+        assert torch.equal(conv_s2_split(sp, asp, w1, list(n), org(h1), size(h1), list(pad)),
+                           conv_s2_split(c4, a4, w1, list(n), org(h1), size(h1), list(pad)))
+        w27 = w2.permute(2, 3, 4, 0, 1).reshape(27, 32, 32).contiguous()
+        ys = conv3d_region(sp, None, w27, CONV_S2, list(n), org(h2), size(h2), None, None, list(pad), in_c4=True,
+                           absmax=asp)
+        yf = conv3d_region(c4, None, w27, CONV_S2, list(n), org(h2), size(h2), None, None, list(pad), in_c4=True)
+    scale = yf.abs().max().item()
+    assert (ys - yf).abs().max().item() <= 1e-6 * scale

@@ -47,6 +47,8 @@ def main():
     with torch.no_grad():
         feats = net.feature_encoder(img)
         cv, _, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, B, V, d_num=D, channel_quads=True)
+        cvs, _, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, B, V, d_num=D, channel_quads=True,
+                                                  split=True)
         n = tuple(cv.shape[2:5])
         full = tuple((0, d - 1) for d in n)
         Bq = M._tconv_input_region(full, n, reg.pad)
@@ -58,7 +60,7 @@ def main():
         bn = M._bn_eval
         layers = {}
         layers["conv_0_0"] = lambda: conv3d_k3(cv, reg.conv_0_0.weight, *bn(reg.BN_0), in_c4=True, wino_z=True)
-        layers["conv_0_0_split"] = lambda: conv3d_k3_split(cv, cv_bound(cv), reg.conv_0_0.weight, *bn(reg.BN_0))
+        layers["conv_0_0_split"] = lambda: conv3d_k3_split(cvs, cv_bound(cvs), reg.conv_0_0.weight, *bn(reg.BN_0))
         y0 = layers["conv_0_0"]()
         y0s = layers["conv_0_0_split"]()
         print("conv_0_0 split vs exact fp32: max|d| %.3g (max|y| %.3g)"
@@ -77,7 +79,7 @@ def main():
             layers["conv_%d_0" % (k + 1)] = fa
             if k == 0:
                 layers["conv_1_0_split"] = (lambda ca=ca, bnm=bnm, halo=halo: conv_s2_split(
-                    cv, cv_bound(cv), ca.weight, dims, org(halo), size(halo), pad, *bn(bnm)))
+                    cvs, cv_bound(cvs), ca.weight, dims, org(halo), size(halo), pad, *bn(bnm)))
                 ys = layers["conv_1_0_split"]()
                 print("conv_1_0 split vs exact fp32: max|d| %.3g (max|y| %.3g)"
                       % ((ys - ya).abs().max().item(), ya.abs().max().item()), flush=True)
