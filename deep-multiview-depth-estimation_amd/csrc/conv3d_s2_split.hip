@@ -165,6 +165,9 @@ __global__ __launch_bounds__(kThreads) void conv_s2_split_kernel(
   const int co = lane & 15;
   const float sc = bn_scale ? bn_scale[co] : 1.0f, sh = bn_scale ? bn_shift[co] : 0.0f,
               mu = bn_scale ? bn_mean[co] : 0.0f;
+  // consume the BN loads here: first used inside the step loop, their wait would be a vmcnt(0) there
+  // that also drains every step's plane prefetch
+  asm volatile("" ::"v"(sc), "v"(sh), "v"(mu));
   const int oexp = -(ex + w_exp);
   const int oy = oy0 + wy;
   const char* wl = lds + kRingB + lane * 16;
