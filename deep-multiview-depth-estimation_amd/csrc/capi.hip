@@ -59,8 +59,8 @@ int cost_volume_fwd_impl(const float* feat, const float* K, const float* R, cons
   if (!cams_ok(K, R, T, d_min, d_int) || d_begin < 0) return MVS_ERR_INVALID_ARGUMENT;
   const mvs::LaunchCheck lc;
   hipStream_t s = (hipStream_t)stream;
-  if (absmax && hipMemsetAsync(absmax, 0, 8 * sizeof(uint32_t), s) != hipSuccess) return MVS_ERR_HIP;
   if (n_views == 1) {  // the variance of a single view is identically zero (0 in fp32 and bf16)
+    if (absmax && hipMemsetAsync(absmax, 0, 8 * sizeof(uint32_t), s) != hipSuccess) return MVS_ERR_HIP;
     st = mvs_plane_sampling(K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count,
                             d_scale, workspace, stream);
     if (st != MVS_OK) return st;

@@ -163,10 +163,18 @@ __global__ __launch_bounds__(kBlock) void prologue_kernel(const float* __restric
 #pragma unroll
       for (int j = 0; j < 4; ++j) am = max(am, __float_as_uint(v[j]) & 0x7FFFFFFFu);   // NaN > Inf > finite
     }
-    if (absmax) {   // one atomic per wave, into the word of this XCD (workgroups go round-robin)
+    if (absmax) {   // this workgroup's maximum -> its own partial slot (absmax_reduce_kernel folds them)
+      __shared__ uint32_t wmax[kBlock / 64];
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) am = max(am, (uint32_t)__shfl_xor((int)am, o));
-      if ((threadIdx.x & 63) == 0) atomicMax(absmax + (blockIdx.x & 7), am);
+      if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = am;
+      __syncthreads();   // the pack job is workgroup-uniform: every thread of the block is here
+      if (threadIdx.x == 0) {
+        uint32_t m = wmax[0];
+#pragma unroll
+        for (int i = 1; i < kBlock / 64; ++i) m = max(m, wmax[i]);
+        absmax[blk] = m;
+      }
     }
     return;
   }
@@ -198,6 +206,26 @@ __global__ __launch_bounds__(kBlock) void prologue_kernel(const float* __restric
   refs[(size_t)bc * hw + p] = make_float4(r.x, r.y, r.z, r.w);
 }
 
+// max|feat| bound words: one workgroup folds the pack workgroups' partial maxima (no atomics, no
+// memset: every word is written) into the caller's 8 words
+__global__ __launch_bounds__(kBlock) void absmax_reduce_kernel(const uint32_t* __restrict__ partial, int n,
+                                                               uint32_t* __restrict__ absmax) {
+  __shared__ uint32_t wmax[kBlock / 64];
+  uint32_t m = 0;
+  for (int i = (int)threadIdx.x; i < n; i += kBlock) m = max(m, partial[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    uint32_t r = wmax[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / 64; ++i) r = max(r, wmax[i]);
+    absmax[threadIdx.x] = r;
+  }
+}
+
+constexpr int kPackPartials = 1024;
 constexpr int kTileW = 32;                // pixels per tile row: every cost-volume store is a 128-B row
 constexpr int kTileH = kBlock / kTileW;   // 8
 
@@ -678,11 +706,17 @@ void launch_gather(const Geometry& g, const float* feat, const Cams& cm, float* 
   const size_t n_pack = (size_t)g.B * V * c4 * pgeo.plane;
   const size_t pblocks = (n_pack + kBlock - 1) / kBlock;
   const int nb_smp = (g.B * V * g.Dc + kBlock - 1) / kBlock;
-  const int nb_pack = (int)(pblocks < 8192 ? pblocks : 8192);
+  // with the bound words requested, at most kPackPartials pack workgroups (grid-stride loops): one
+  // partial maximum each (8192 atomicMax on 8 words serialised at L2 for ~0.3 ms)
+  const size_t max_pack = absmax ? (size_t)kPackPartials : 8192;
+  const int nb_pack = (int)(pblocks < max_pack ? pblocks : max_pack);
   const uint32_t hw = (uint32_t)g.h * (uint32_t)g.w;
   const int nb_ref = (int)((hw + kBlock - 1) / kBlock) * g.B * c4;
+  // partial maxima of the pack workgroups: the 4 KB after the reference views (packed_bytes)
+  uint32_t* partial = absmax ? reinterpret_cast<uint32_t*>(refs + (size_t)g.B * c4 * ((size_t)g.h * g.w)) : nullptr;
   hipLaunchKernelGGL(prologue_kernel, dim3((unsigned)(nb_smp + nb_pack + nb_ref)), dim3(kBlock), 0, s, feat, cm,
-                     smp, packed, refs, g.B, V, g.C, g.h, g.w, g.Dc, nb_smp, nb_pack, absmax);
+                     smp, packed, refs, g.B, V, g.C, g.h, g.w, g.Dc, nb_smp, nb_pack, partial);
+  if (absmax) hipLaunchKernelGGL(absmax_reduce_kernel, dim3(1), dim3(kBlock), 0, s, partial, nb_pack, absmax);
   constexpr int TW = kTileW, TH = kTileH;
   const int tiles_x = (g.w + TW - 1) / TW, tiles_y = (g.h + TH - 1) / TH;
   // planes per workgroup: the register maximum, halved until the grid has >= 4 workgroups per CU
@@ -713,7 +747,9 @@ size_t packed_bytes(int B, int V, int C, int h, int w) {
   if (V < 2 || V > 8)  // generic kernel: reads the NCHW features directly
     return 0;
   const size_t c4 = (size_t)((C + 3) / 4);
-  return ((size_t)B * V * c4 * pad_geom(h, w).plane + (size_t)B * c4 * h * w) * sizeof(float4);
+  // + the pack workgroups' partial maxima of the bound words (kPackPartials uint32)
+  return ((size_t)B * V * c4 * pad_geom(h, w).plane + (size_t)B * c4 * h * w) * sizeof(float4) +
+         kPackPartials * sizeof(uint32_t);
 }
 
 void launch_cost_volume_fwd_bf16(const Geometry& g, const float* feat, const Cams& cm, float* sampling,

@@ -270,14 +270,17 @@ class CostVolumeReg(nn.Module):
         # stream beside level 1 measured no gain: 6.21-6.25 against 6.18-6.22 ms per cfg-2 step,
         # tools/hip_reg_layers.py, profiles/r03e_reg_layers.log)
         main = torch.cuda.current_stream(cv.device)
-        side = _side_stream(cv.device)
-        side.wait_stream(main)
         # the split cost volume (int32, csrc/split.h) always goes to the split-fp16 kernels; an fp32
         # channel-quad volume does when split_f16 is on and it carries bound words
         split_cv = c4 and cv.dtype == torch.int32
         bound = cv_bound(cv) if split_cv or (c4 and self.split_f16 and cv.dtype == torch.float32) else None
         if split_cv and bound is None:
             raise ValueError("split cost volume without its bound words")
+        # the split-fp16 conv_0_0 (MFMA, LDS-staged) gains nothing beside the region chain: both compete
+        # for the same CUs (cfg 2: 5.67 ms serialised against 5.78 ms on a side stream,
+        # profiles/r03/r03u_reg_layers.log); the exact-fp32 VALU kernel overlaps the MFMA chain
+        side = main if bound is not None else _side_stream(cv.device)
+        side.wait_stream(main)
         with torch.cuda.stream(side):
             if bound is not None:
                 y0 = conv3d_k3_split(cv, bound, self.conv_0_0.weight, *bn_eval(self.BN_0))
