@@ -26,20 +26,19 @@ __device__ inline int cv_split_exponent(const uint32_t* __restrict__ absmax) {
   return min(max(14 - 2 * e, -120), 120);
 }
 
-// hi / lo fp16 parts of 4 fp32 values times 2^e, packed 2 per dword
+// hi / lo fp16 parts of 4 fp32 values times 2^e, packed 2 per dword.  Packed arithmetic: the scale as
+// one fp32 multiply by 2^e (exact, e in [-120, 120]), v_cvt_pk_f16_f32 (nearest) for the parts, and
+// the remainder v 2^e - hi as one packed fma (exact: hi holds the leading 11 bits)
 __device__ inline void split4(const f4v v, int e, uint2& hi, uint2& lo) {
-  _Float16 h[4], l[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float s = ldexpf(v[j], e);
-    h[j] = (_Float16)s;
-    l[j] = (_Float16)(s - (float)h[j]);
-  }
-  auto pk = [](_Float16 a, _Float16 b) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
-  };
-  hi = make_uint2(pk(h[0], h[1]), pk(h[2], h[3]));
-  lo = make_uint2(pk(l[0], l[1]), pk(l[2], l[3]));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  const float sc = __builtin_ldexpf(1.0f, e);
+  const f2 a = f2{v[0], v[1]} * sc, b = f2{v[2], v[3]} * sc;
+  const h2 ha = __builtin_convertvector(a, h2), hb = __builtin_convertvector(b, h2);
+  const h2 la = __builtin_convertvector(a - __builtin_convertvector(ha, f2), h2);
+  const h2 lb = __builtin_convertvector(b - __builtin_convertvector(hb, f2), h2);
+  hi = make_uint2(__builtin_bit_cast(uint32_t, ha), __builtin_bit_cast(uint32_t, hb));
+  lo = make_uint2(__builtin_bit_cast(uint32_t, la), __builtin_bit_cast(uint32_t, lb));
 }
 
 // fp32 of one split element (4 channels): (hi + lo) 2^-e, exact sum of the parts
