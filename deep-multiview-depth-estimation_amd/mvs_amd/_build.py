@@ -16,7 +16,8 @@ SOURCES = [os.path.join(CSRC, f) for f in ("capi.hip", "plane_sampling.hip", "co
                                            "conv3d_split.hip", "conv3d_s2_split.hip")]
 HEADERS = [os.path.join(REPO_ROOT, "include", "mvs_cost_volume.h"),
            os.path.join(CSRC, "common.h"), os.path.join(CSRC, "launchers.h"),
-           os.path.join(CSRC, "packed.h"), os.path.join(CSRC, "sampling_matrix.h")]
+           os.path.join(CSRC, "packed.h"), os.path.join(CSRC, "sampling_matrix.h"),
+           os.path.join(CSRC, "split.h")]
 OUTPUT = os.path.join(_HERE, "libmvs_cost_volume.so")
 ARCH = os.environ.get("MVS_OFFLOAD_ARCH", "gfx950")
 
