@@ -98,8 +98,9 @@ def main():
         layers["conv_out"] = lambda: conv3d_k3(z, reg.conv_out.weight)
         o = layers["conv_out"]()
         layers["softmax"] = lambda: softmax_depth(o)
-        if a.only:
-            timed(a.only, layers[a.only], a.reps)
+        if a.only:   # one layer or a comma-separated list
+            for name in a.only.split(","):
+                timed(name, layers[name], a.reps)
             return
         for name, fn in layers.items():
             timed(name, fn, a.reps)
