@@ -74,6 +74,34 @@ __global__ void k_tile_chunkwise(f4* o, int total) {
   for (int pl = 0; pl < PG; ++pl) st(o + (((size_t)b * C4 + ch) * D + g * PG + pl) * HW + pix, f4{1, 2, 3, 4});
 }
 
+// (e) VOXEL-MAJOR layout cv[B][D][h][w][C/4] (a voxel's 8 quads = one 128-B line): the fused
+// kernel's mapping (lane = pixel, chunk-outer), so one wave-store writes 64 lines 16 B each and the
+// 8 chunk passes complete them; (f) the same layout with lane = (pixel, quad): 8 lanes fill a line
+template <int PG>
+__global__ void k_vox_chunk_outer(f4* o, int total) {
+  int wk = xcd(blockIdx.x, total);
+  if (wk >= total) return;
+  const int tx = W / 32, ty = H / 8, groups = D / PG;
+  const int g = wk % groups, t = wk / groups, tile = t % (tx * ty), b = t / (tx * ty);
+  const int px = (tile % tx) * 32 + threadIdx.x % 32, py = (tile / tx) * 8 + threadIdx.x / 32;
+  const size_t pix = (size_t)py * W + px;
+  for (int ch = 0; ch < C4; ++ch)
+    for (int pl = 0; pl < PG; ++pl) st(o + (((size_t)b * D + g * PG + pl) * HW + pix) * C4 + ch, f4{1, 2, 3, 4});
+}
+template <int PG>
+__global__ void k_vox_lane_quad(f4* o, int total) {
+  int wk = xcd(blockIdx.x, total);
+  if (wk >= total) return;
+  const int tx = W / 32, ty = H / 8, groups = D / PG;
+  const int g = wk % groups, t = wk / groups, tile = t % (tx * ty), b = t / (tx * ty);
+  for (int pass = 0; pass < C4; ++pass) {   // 8 passes of 32 pixels x 8 quads per 256 lanes
+    const int e = pass * 256 + threadIdx.x, ch = e & 7, p = e >> 3;
+    const int px = (tile % tx) * 32 + p % 32, py = (tile / tx) * 8 + p / 32;
+    const size_t pix = (size_t)py * W + px;
+    for (int pl = 0; pl < PG; ++pl) st(o + (((size_t)b * D + g * PG + pl) * HW + pix) * C4 + ch, f4{1, 2, 3, 4});
+  }
+}
+
 template <typename F>
 void timeit(const char* name, F launch, size_t bytes) {
   hipEvent_t a, b;
@@ -118,6 +146,9 @@ int main() {
   timeit("tile32x8 pg8 chunk per WG", [&] { k_tile_chunkwise<8><<<g(tc), 256>>>(o, tc); }, bytes);
   const int tc2 = B * C4 * (W / 32) * (H / 8) * (D / 32);
   timeit("tile32x8 pg32 chunk per WG", [&] { k_tile_chunkwise<32><<<g(tc2), 256>>>(o, tc2); }, bytes);
+  timeit("voxel-major, lane=pixel chunk-outer", [&] { k_vox_chunk_outer<8><<<g(t32_8), 256>>>(o, t32_8); }, bytes);
+  timeit("voxel-major, lane=(pixel,quad)", [&] { k_vox_lane_quad<8><<<g(t32_8), 256>>>(o, t32_8); }, bytes);
+  timeit("tile32x8 pg8 chunk-outer (fused)", [&] { k_tile<32, 8, false><<<g(t32_8), 256>>>(o, t32_8); }, bytes);
   hipFree(o);
   return 0;
 }
