@@ -89,6 +89,17 @@ __global__ void k_vox_chunk_outer(f4* o, int total) {
     for (int pl = 0; pl < PG; ++pl) st(o + (((size_t)b * D + g * PG + pl) * HW + pix) * C4 + ch, f4{1, 2, 3, 4});
 }
 template <int PG>
+__global__ void k_vox_chunk_outer_plain(f4* o, int total) {   // (e) with plain (L2-allocating) stores
+  int wk = xcd(blockIdx.x, total);
+  if (wk >= total) return;
+  const int tx = W / 32, ty = H / 8, groups = D / PG;
+  const int g = wk % groups, t = wk / groups, tile = t % (tx * ty), b = t / (tx * ty);
+  const int px = (tile % tx) * 32 + threadIdx.x % 32, py = (tile / tx) * 8 + threadIdx.x / 32;
+  const size_t pix = (size_t)py * W + px;
+  for (int ch = 0; ch < C4; ++ch)
+    for (int pl = 0; pl < PG; ++pl) o[(((size_t)b * D + g * PG + pl) * HW + pix) * C4 + ch] = f4{1, 2, 3, 4};
+}
+template <int PG>
 __global__ void k_vox_lane_quad(f4* o, int total) {
   int wk = xcd(blockIdx.x, total);
   if (wk >= total) return;
@@ -147,6 +158,7 @@ int main() {
   const int tc2 = B * C4 * (W / 32) * (H / 8) * (D / 32);
   timeit("tile32x8 pg32 chunk per WG", [&] { k_tile_chunkwise<32><<<g(tc2), 256>>>(o, tc2); }, bytes);
   timeit("voxel-major, lane=pixel chunk-outer", [&] { k_vox_chunk_outer<8><<<g(t32_8), 256>>>(o, t32_8); }, bytes);
+  timeit("voxel-major, lane=pixel chunk-outer, plain", [&] { k_vox_chunk_outer_plain<8><<<g(t32_8), 256>>>(o, t32_8); }, bytes);
   timeit("voxel-major, lane=(pixel,quad)", [&] { k_vox_lane_quad<8><<<g(t32_8), 256>>>(o, t32_8); }, bytes);
   timeit("tile32x8 pg8 chunk-outer (fused)", [&] { k_tile<32, 8, false><<<g(t32_8), 256>>>(o, t32_8); }, bytes);
   hipFree(o);
