@@ -11,8 +11,12 @@ What changes is the hot path: ``model.py:177-181`` (per-plane kornia warp loop +
 + 6-D variance) becomes ONE fused HIP kernel (``costvolume.warp_and_assemble_cost_volume``) and
 ``model.py:187`` the HIP soft-argmin.  In fp32 no-grad inference the 2-D encoder / refinement
 convolutions and the 3-D regulariser's layers run on hand-written HIP kernels too (direct 2-D convs
-with fused BN + ReLU, MFMA region convs on the live regions); autograd,
-other dtypes and the full-volume reference leg (``forward_full``) use PyTorch-ROCm (MIOpen).  Like
+with fused BN + ReLU, MFMA region convs on the live regions; conv_0_0 and
+conv_1_0 on split-fp16 matrix-core kernels fed by the fused kernel's split volume, §3.5, exact-fp32
+kernels with ``MVS_SPLIT_F16=0``).  Under autograd the regulariser's Conv3d / ConvTranspose3d run as
+per-tap rocBLAS GEMMs with their own backward (``tap_gemm.py``) and the 2-D layers as
+the PyTorch-ROCm modules; other dtypes and the full-volume reference leg (``forward_full`` without
+grad) use PyTorch-ROCm (MIOpen).  Like
 the reference (``model.py:164-166``) the instance attribute
 ``parameters`` is a LIST of tensors (``train.py:160`` passes it to Adam); use
 ``named_parameters()`` / ``state_dict()`` for module-generic code.
