@@ -4,7 +4,8 @@
 // A fp32 value v is scaled by 2^e (exact) and carried as hi = fp16(v 2^e), lo = fp16(v 2^e - hi), both
 // rounded to nearest: hi + lo is v 2^e to 2^-22 relative (fp16's normal range; below it lo is a
 // subnormal with absolute error <= 2^-25 of the 2^14 scale).  For a cost volume the scale comes from
-// the bound words the prologue writes (max |feat|, per XCD): every variance over views is at most
+// the bound words (max |feat|: the prologue's per-workgroup partial maxima, folded into 8 words by
+// absmax_reduce_kernel; cost_volume_fwd.hip): every variance over views is at most
 // max|feat|^2, so e = 14 - 2 exponent(max|feat|) keeps every scaled element below 2^14 (fp16 max 65504).
 //
 // Split cost-volume layout ("SCV"): the channel-quad layout cv[B][C/4][D][h][w] with each 16-byte
