@@ -651,10 +651,11 @@ def main():
                            "packing + reference resampling) + cost_volume_staged kernel" % ("_c4" if quads else ""),
                      "op_GBps": alg / (op_ms * 1e-3) / 1e9},
     }
-    out["arithmetic"] = ("fp32 throughout, except conv_0_0 (model.py:101) in samples mode: f16 MFMA with "
-                         "split-fp16 operands (hi + lo parts, all four partial products, fp32 accumulation), "
-                         "max error 0.3-0.5x that of the exact fp32 kernels vs float64 "
-                         "(tests/test_split_conv.py, DESIGN.md 3.5)")
+    out["arithmetic"] = ("fp32 throughout, except conv_0_0 and conv_1_0 (model.py:101,103) in samples mode: "
+                         "f16 MFMA with split-fp16 operands (hi + lo parts of the fp32 values; conv_0_0 all four "
+                         "partial products, conv_1_0 three; fp32 accumulation), fed by the fused kernel storing "
+                         "the cost volume as those hi/lo parts; max error 0.3-0.5x that of the exact fp32 kernels "
+                         "vs float64 (tests/test_split_conv.py, DESIGN.md 3.5)")
     if "exact_fp32" in result:
         out["exact_fp32_step"] = dict(result["exact_fp32"], unit="depth maps/s", note=(
             "the same step with conv_0_0 on the exact-fp32 VALU kernel (MVS_SPLIT_F16=0)"))
