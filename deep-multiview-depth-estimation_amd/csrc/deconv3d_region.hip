@@ -27,6 +27,9 @@ namespace mvs {
 namespace {
 
 constexpr int kCout = 8;
+// the full-size output and the residual y0 stream through once: non-temporal policy for both
+// (cfg 2 deconv_1_0 0.53 -> 0.43 ms alone; profiles/r03/r03z_split_conv_experiments.md)
+constexpr int kNtAux = 2;
 typedef float f2v_t __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(4))) const f2v_t const_f2v_t;
 constexpr int kWRow = 28;   // 27 taps padded to 7 float4
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2)
             r[cc][sd][s2] = __builtin_bit_cast(
-                f2v, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(boff[sd][s2] + (uint32_t)(c0 + cc) * pb), 0, 0));
+                f2v, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(boff[sd][s2] + (uint32_t)(c0 + cc) * pb), 0, kNtAux));
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) {
         const int co = c0 + cc;
@@ -299,7 +302,7 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
               o[sw] = v + r[cc][sd][s2][sw];
             }
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, o), ry,
-                                                  (int)(boff[sd][s2] + (uint32_t)co * pb), 0, 0);
+                                                  (int)(boff[sd][s2] + (uint32_t)co * pb), 0, kNtAux);
           }
       }
     }
