@@ -234,7 +234,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
       if (store_lane && z < z1) {
         float* o = out + ((size_t)(b * 8 + co) * D + z) * HW + (size_t)gy * W + gx0;
         if (vec_store) {
-          *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+          // non-temporal: the 0.5 GB output is read once, by deconv_1_0 much later in the step
+          // (1.10 -> 1.07 ms alone; profiles/r03/r03z_split_conv_experiments.md)
+          __builtin_nontemporal_store(f4v{v[0], v[1], v[2], v[3]}, reinterpret_cast<f4v*>(o));
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
