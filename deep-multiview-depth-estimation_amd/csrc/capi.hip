@@ -281,6 +281,54 @@ int mvs_conv3d_s2_split_fwd(const void* x, int flags, const void* weight_frag, i
   return st != MVS_OK ? st : lc.status();
 }
 
+int mvs_cost_volume_head_fwd(const float* feat, const float* K, const float* R, const float* T,
+                             const float* d_min, const float* d_int, int batch_size, int n_views,
+                             int channels, int h, int w, int d_begin, int d_count, float d_scale,
+                             const void* w0_frag, int w0_exp, const float* bn0_scale, const float* bn0_shift,
+                             const float* bn0_mean, const void* w1_frag, int w1_exp, const float* bn1_scale,
+                             const float* bn1_shift, const float* bn1_mean, const int* pad,
+                             const int* y1_origin, const int* y1_size, const int* scv_lo, const int* scv_hi,
+                             float* workspace, unsigned* feat_absmax, float* y0, float* y1, void* scv,
+                             void* stream, void* main_begin_event, void* main_end_event) {
+  if (!feat || !workspace || !feat_absmax || !y0 || !y1 || !w0_frag || !w1_frag || !pad || !y1_origin ||
+      !y1_size || !scv_lo || !scv_hi)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (!cams_ok(K, R, T, d_min, d_int) || d_begin < 0) return MVS_ERR_INVALID_ARGUMENT;
+  if (n_views < 2 || n_views > 3) return MVS_ERR_UNSUPPORTED_VIEWS;
+  if (channels != 32 || (d_count & 1)) return MVS_ERR_INVALID_ARGUMENT;
+  if ((((uintptr_t)w0_frag) | ((uintptr_t)w1_frag) | ((uintptr_t)y0) | ((uintptr_t)scv)) & 15u) return MVS_ERR_INVALID_ARGUMENT;
+  if (((uintptr_t)feat_absmax) & 3u) return MVS_ERR_INVALID_ARGUMENT;
+  if ((bn0_scale != nullptr) != (bn0_shift != nullptr) || (bn0_scale != nullptr) != (bn0_mean != nullptr) ||
+      (bn1_scale != nullptr) != (bn1_shift != nullptr) || (bn1_scale != nullptr) != (bn1_mean != nullptr))
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (w0_exp < -120 || w0_exp > 120 || w1_exp < -120 || w1_exp > 120) return MVS_ERR_INVALID_ARGUMENT;
+  Geometry g;
+  int st = check_geometry(batch_size, n_views, channels, h, w, d_count, g, 16);
+  if (st != MVS_OK) return st;
+  const int n[3] = {d_count, h, w};
+  uint64_t ovox = 1;
+  for (int d = 0; d < 3; ++d) {
+    if (pad[d] < 1 || !(pad[d] & 1)) return MVS_ERR_INVALID_ARGUMENT;
+    if (y1_size[d] <= 0 || y1_origin[d] < 0 || y1_origin[d] + y1_size[d] > (n[d] + 2 * pad[d] - 3) / 2 + 1)
+      return MVS_ERR_INVALID_ARGUMENT;
+    if (scv_lo[d] < 0 || scv_hi[d] > n[d] || scv_lo[d] > scv_hi[d]) return MVS_ERR_INVALID_ARGUMENT;
+    ovox *= (uint64_t)y1_size[d];
+  }
+  if (128ull * (uint64_t)d_count * (uint64_t)h * (uint64_t)w > 0xFFFFFFF0ull ||
+      (uint64_t)batch_size * ovox * 16ull >= (1ull << 40))
+    return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
+  hipStream_t s = (hipStream_t)stream;
+  const mvs::Cams cm{K, R, T, d_min, d_int, d_begin, d_scale};
+  const float* bn0[3] = {bn0_scale, bn0_shift, bn0_mean};
+  const float* bn1[3] = {bn1_scale, bn1_shift, bn1_mean};
+  st = mvs::launch_cv_head(g, feat, cm, workspace, reinterpret_cast<uint32_t*>(feat_absmax), w0_frag, w0_exp, w1_frag,
+                           w1_exp, bn0, bn1, y0, y1, scv, pad, y1_origin, y1_size, scv_lo, scv_hi, s,
+                           (hipEvent_t)main_begin_event, (hipEvent_t)main_end_event);
+  if (st != MVS_OK) return st;
+  return lc.status();
+}
+
 int mvs_conv3d_k3_split_fwd(const void* x, int flags, const void* weight_frag, int weight_exp,
                             const unsigned* x_absmax, float* y, int batch, int d, int h, int w,
                             const float* bn_scale, const float* bn_shift, const float* bn_mean, void* stream) {

@@ -122,11 +122,14 @@ __device__ inline f4v variance4(const f4v& x0, const f4v (&xs)[NS], const f4v& i
 //                              with the packed layout's rules (taps outside the image are 0; same
 //                              taps, weights and fma order as bilerp): bit-identical to sampling the
 //                              packed image.
+//   pixel_major: the pack job writes packed[N][h + 2][w + 2][C4] instead (cv_head.hip: one tap's C4
+//                quads are one contiguous run), same values, same zero border.
 __global__ __launch_bounds__(kBlock) void prologue_kernel(const float* __restrict__ feat, Cams cm,
                                                           float* __restrict__ sampling,
                                                           float4* __restrict__ packed, float4* __restrict__ refs,
                                                           int B, int V, int C, int h, int w, int Dc, int nb_smp,
-                                                          int nb_pack, uint32_t* __restrict__ absmax) {
+                                                          int nb_pack, uint32_t* __restrict__ absmax,
+                                                          int pixel_major) {
   const int N = B * V;
   const int c4 = (C + 3) / 4;
   const uint32_t hw = (uint32_t)h * (uint32_t)w;
@@ -145,10 +148,20 @@ __global__ __launch_bounds__(kBlock) void prologue_kernel(const float* __restric
     const size_t n = (size_t)N * c4 * pg.plane;
     uint32_t am = 0;   // max |feature| bits (absmax requested): bounds every variance by am^2
     for (size_t e = (size_t)blk * kBlock + threadIdx.x; e < n; e += (size_t)nb_pack * kBlock) {
-      const uint32_t q = (uint32_t)(e % pg.plane);
-      const size_t t = e / pg.plane;
-      const int ch = (int)(t % c4);
-      const size_t i = t / c4;
+      uint32_t q;
+      int ch;
+      size_t i;
+      if (pixel_major) {   // e = (i * plane + q) * c4 + ch
+        ch = (int)(e % c4);
+        const size_t t = e / c4;
+        q = (uint32_t)(t % pg.plane);
+        i = t / pg.plane;
+      } else {             // e = (i * c4 + ch) * plane + q
+        q = (uint32_t)(e % pg.plane);
+        const size_t t = e / pg.plane;
+        ch = (int)(t % c4);
+        i = t / c4;
+      }
       const int y = (int)(q / (uint32_t)pg.pitch) - 1;
       const int x = (int)(q % (uint32_t)pg.pitch) - 1;
       float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -715,7 +728,7 @@ void launch_gather(const Geometry& g, const float* feat, const Cams& cm, float* 
   // partial maxima of the pack workgroups: the 4 KB after the reference views (packed_bytes)
   uint32_t* partial = absmax ? reinterpret_cast<uint32_t*>(refs + (size_t)g.B * c4 * ((size_t)g.h * g.w)) : nullptr;
   hipLaunchKernelGGL(prologue_kernel, dim3((unsigned)(nb_smp + nb_pack + nb_ref)), dim3(kBlock), 0, s, feat, cm,
-                     smp, packed, refs, g.B, V, g.C, g.h, g.w, g.Dc, nb_smp, nb_pack, partial);
+                     smp, packed, refs, g.B, V, g.C, g.h, g.w, g.Dc, nb_smp, nb_pack, partial, 0);
   if (absmax) hipLaunchKernelGGL(absmax_reduce_kernel, dim3(1), dim3(kBlock), 0, s, partial, nb_pack, absmax);
   constexpr int TW = kTileW, TH = kTileH;
   const int tiles_x = (g.w + TW - 1) / TW, tiles_y = (g.h + TH - 1) / TH;
@@ -742,6 +755,28 @@ void launch_direct(const Geometry& g, const float* feat, const float* smp, float
 }
 
 }  // namespace
+
+// The prologue alone, for the fused consumer (cv_head.hip): sampling matrices, PIXEL-MAJOR padded
+// features packed[N][h + 2][w + 2][C4] float4, the resampled reference views refs[B][C4][h][w] and the
+// bound words (max |feat|, folded into absmax[8]); same workspace layout as launch_gather.
+void launch_cv_prologue_pm(const Geometry& g, const float* feat, const Cams& cm, float* smp, float* ws,
+                           uint32_t* absmax, hipStream_t s) {
+  const int V = g.V;
+  const int c4 = (g.C + 3) / 4;
+  const PadGeom pgeo = pad_geom(g.h, g.w);
+  float4* packed = reinterpret_cast<float4*>(ws);
+  float4* refs = packed + (size_t)g.B * V * c4 * pgeo.plane;
+  const size_t n_pack = (size_t)g.B * V * c4 * pgeo.plane;
+  const size_t pblocks = (n_pack + kBlock - 1) / kBlock;
+  const int nb_smp = (g.B * V * g.Dc + kBlock - 1) / kBlock;
+  const int nb_pack = (int)(pblocks < (size_t)kPackPartials ? pblocks : (size_t)kPackPartials);
+  const uint32_t hw = (uint32_t)g.h * (uint32_t)g.w;
+  const int nb_ref = (int)((hw + kBlock - 1) / kBlock) * g.B * c4;
+  uint32_t* partial = reinterpret_cast<uint32_t*>(refs + (size_t)g.B * c4 * ((size_t)g.h * g.w));
+  hipLaunchKernelGGL(prologue_kernel, dim3((unsigned)(nb_smp + nb_pack + nb_ref)), dim3(kBlock), 0, s, feat, cm,
+                     smp, packed, refs, g.B, V, g.C, g.h, g.w, g.Dc, nb_smp, nb_pack, partial, 1);
+  hipLaunchKernelGGL(absmax_reduce_kernel, dim3(1), dim3(kBlock), 0, s, partial, nb_pack, absmax);
+}
 
 size_t packed_bytes(int B, int V, int C, int h, int w) {
   if (V < 2 || V > 8)  // generic kernel: reads the NCHW features directly

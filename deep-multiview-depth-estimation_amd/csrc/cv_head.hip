@@ -1,0 +1,564 @@
+// cv_head.hip -- the cost volume consumed where it is formed (north_star: "the
+// B x C x D x H x W volume is never materialised before it is consumed").
+//
+// Reference: scripts/homography.py:6-92 + scripts/costvolume.py:3-16 (warp every source view onto D
+// planes, variance over views) feeding scripts/model.py:101-103 (conv_0_0 + BN_0 + ReLU and conv_1_0 +
+// BN_1 + ReLU both read cv in full).  One kernel forms the variance of a tile's voxels plane by plane
+// on chip and applies both convolutions to it; nothing of the 2 GB volume reaches HBM except the
+// middle region that conv_2_0 / conv_3_0 read.
+//
+// Workgroup: 512 threads = 4 CONSUMER waves (0-3, matrix cores) + 4 PRODUCER waves (4-7, gathers +
+// variance).  It owns a 16 x 4 (x, y) column of conv_0_0 outputs and a chunk of kZC output depths;
+// per step of two depths:
+//   * producers compute the variance of the column's 18 x 6 halo on the next two planes -- the
+//     fused forward's arithmetic exactly (same sampling coordinates, bilinear taps, two-pass variance,
+//     split4 into fp16 hi / lo): taps are 16-byte gathers from PIXEL-MAJOR padded features (one tap
+//     pixel's 8 channel quads are one 128-B line; L2 / MALL resident), per-(voxel, view) sampling
+//     state computed one step ahead into an LDS table -- and write the split operands into a 6-plane
+//     LDS ring in the layout conv3d_split.hip stages (so the conv_0_0 MFMA loop below is that kernel's);
+//     voxels inside conv_2_0's input box are also stored to the split cost volume (SCV, split.h);
+//   * consumers run conv_0_0 (split-fp16 f16 MFMA, 2 per (16 voxels, tap), conv3d_split.hip's order)
+//     on the 4 resident planes, and conv_1_0 (stride 2, padding P odd in every dim): the tile owns the
+//     8 x 2 stride-2 windows starting at (x0 - 1 + 2 jx, y0 - 1 + 2 jy) -- one 16-row MFMA block -- and
+//     the depth windows starting at z0 - 1 + 2k; consumer wave w < 3 accumulates product w of the
+//     three split products (x_hi w_hi, x_hi w_lo, x_lo w_hi, conv3d_s2_split.hip's), tap by tap in
+//     that kernel's order, and wave 3 combines a completed window's three partials (aa + (ab + ac)) one
+//     step later and applies BN_1 + ReLU.
+// Results are bit-identical to the materialising path (fused forward -> SCV -> conv3d_split /
+// conv3d_s2_split): the same operands meet the same MFMAs in the same order.
+#include "launchers.h"
+#include "packed.h"
+#include "split.h"
+
+#include <algorithm>
+
+namespace mvs {
+namespace {
+
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kC4 = 8;                                   // 32 channels = 8 quads (fixed: conv_0_0 / conv_1_0)
+constexpr int kTX = 16, kTY = 4;                         // conv_0_0 outputs per tile
+constexpr int kHX = kTX + 2, kHY = kTY + 2, kHV = kHX * kHY;   // 18 x 6 halo voxels
+constexpr int kVoxB = 64;                                // 32 channels x fp16 per part
+constexpr int kRowB = kHX * kVoxB;                       // 1,152 B
+constexpr int kPartB = kHY * kRowB;                      // 6,912 B
+constexpr int kSlotB = 2 * kPartB;                       // hi + lo: 13,824 B per plane
+constexpr int kRing = 6;                                 // 4 planes read + 2 being written
+constexpr int kRingB = kRing * kSlotB;                   // 82,944 B
+constexpr int kW1B = 27 * 2 * 64 * 16;                   // conv_1_0 fragments: 55,296 B
+constexpr int kScrB = 2 * 3 * 64 * 16;                   // conv_1_0 partials, double buffered
+constexpr int kZC = 48;                                  // output depths per workgroup
+constexpr int kThreads = 512;
+constexpr int kPlaneItems = kHV * kC4;                   // 864 (voxel, quad) items per plane
+constexpr int kBatchItems = 2 * kPlaneItems;             // two planes per step
+constexpr int kItems = (kBatchItems + 255) / 256;        // 7 per producer thread
+constexpr int kPF = 3;                                   // conv_0_0 A-fragment prefetch (items)
+
+template <int NS>
+constexpr int coord_bytes() {   // [2 buffers][2 planes][NS views][108 voxels] x {off, wx, wy, -}
+  return 2 * 2 * NS * kHV * 16;
+}
+template <int NS>
+constexpr int lds_bytes() {
+  return kRingB + kW1B + coord_bytes<NS>() + kScrB;
+}
+
+struct HeadArgs {
+  const float4* packed;       // pixel-major padded features [N][h + 2][w + 2][8] float4
+  const float4* refs;         // resampled reference views [B][8][h][w] float4
+  const float* sampling;      // [N][D][9]
+  const uint32_t* absmax;     // bound words (split scale)
+  const h8v* w0;              // conv_0_0 fragments [27][64]
+  const h8v* w1;              // conv_1_0 fragments [27][2][64]
+  const float *bn0_sc, *bn0_sh, *bn0_mu;   // BN_0 (8), all or none
+  const float *bn1_sc, *bn1_sh, *bn1_mu;   // BN_1 (16), all or none
+  float* y0;                  // [B][8][D][H][W]
+  float* y1;                  // [B][on0][on1][on2][16]
+  void* scv;                  // split cost volume [B][8][D][H][W] x 16 B (box written), or null
+  int V, D, H, W;
+  int w_exp0, w_exp1;
+  int tiles_x, tiles_y, zchunks, total;
+  int pad[3];                 // (z, y, x), odd
+  int o0[3], on[3];           // conv_1_0 output region
+  int r0[3], r1[3];           // SCV box [r0, r1)
+};
+
+__device__ inline float ror8(float v) {   // value of lane (l ^ 8) inside each 16-lane row
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+}
+
+// costvolume.py:12-14 -- as cost_volume_fwd.hip::variance4 (same operation order, no contraction)
+template <int NS>
+__device__ inline f4v head_variance4(const f4v& x0, const f4v (&xs)[NS], const f4v& inv_v) {
+#pragma clang fp contract(off)
+  f4v sum = x0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) sum += xs[s];
+  const f4v nmean = -(sum * inv_v);
+  f4v d = x0 + nmean;
+  f4v acc = d * d;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    d = xs[s] + nmean;
+    acc = __builtin_elementwise_fma(d, d, acc);
+  }
+  return acc * inv_v;
+}
+
+template <int V>
+__global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
+  constexpr int NS = V - 1;
+  __shared__ __attribute__((aligned(16))) char lds[lds_bytes<NS>()];
+  char* const ring = lds;
+  char* const w1l = lds + kRingB;
+  char* const coord = lds + kRingB + kW1B;
+  char* const scr = coord + coord_bytes<NS>();
+
+  const int wk = xcd_work_id((int)blockIdx.x, (int)gridDim.x);
+  if (wk >= a.total) return;   // workgroup-uniform, before any barrier
+  int t = wk;
+  const int x0 = (t % a.tiles_x) * kTX;
+  t /= a.tiles_x;
+  const int y0 = (t % a.tiles_y) * kTY;
+  t /= a.tiles_y;
+  const int z0 = (t % a.zchunks) * kZC;
+  const int b = t / a.zchunks;
+  const int D = a.D, H = a.H, W = a.W;
+  const int z1 = min(z0 + kZC, D);
+  const int nsteps = (z1 - z0) >> 1;   // D even (checked by the C ABI)
+  const int nbatch = nsteps + 1;       // batch j = planes z0 - 1 + 2j, z0 + 2j
+  const int ex = cv_split_exponent(a.absmax);
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool consumer = wave < 4;
+
+  // conv_1_0 weight fragments -> LDS (every thread)
+  {
+    const Rsrc rw = make_rsrc(a.w1, (uint32_t)kW1B);
+#pragma unroll
+    for (int j = 0; j < (kW1B / 16 + kThreads - 1) / kThreads; ++j) {
+      const int e = tid + kThreads * j;
+      if (e < kW1B / 16)
+        *reinterpret_cast<f4v*>(w1l + e * 16) = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rw, e * 16, 0, 0));
+    }
+  }
+  // ring slot of plane p (batch j = (p - z0 + 1) / 2 lives in slots 2j, 2j + 1 mod kRing)
+  auto slot_of = [&](int p) { return (p - z0 + 1) % kRing; };
+
+  // ================================ producer state ================================
+  const int ptid = tid - 256, pw = wave - 4;
+  const size_t HW = (size_t)H * W;
+  const PadGeom pg = pad_geom(H, W);
+  const uint32_t pstride = (uint32_t)kC4 * 16u;   // bytes per padded pixel
+  Rsrc rsv[NS];
+  f4v ref[kItems];
+  if (!consumer) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      rsv[s] = make_rsrc(a.packed + (size_t)(b * V + 1 + s) * pg.plane * kC4, pg.plane * pstride);
+#pragma unroll
+    for (int u = 0; u < kItems; ++u) {   // the thread's (voxel, quad) items: the same every batch
+      const int e = ptid + 256 * u;
+      const int r = e >= kPlaneItems ? e - kPlaneItems : e;
+      const int v = r >> 3, q = r & 7;
+      const int yy = v / kHX, xx = v - yy * kHX;
+      const int gx = x0 - 1 + xx, gy = y0 - 1 + yy;
+      const bool in = e < kBatchItems && gx >= 0 && gx < W && gy >= 0 && gy < H;
+      const float4 r4 = in ? a.refs[((size_t)(b * kC4 + q) * H + gy) * W + gx] : make_float4(0.f, 0.f, 0.f, 0.f);
+      ref[u] = f4v{r4.x, r4.y, r4.z, r4.w};
+    }
+  }
+  // sampling state of batch j's planes for every (plane, view, halo voxel) -> coordinate buffer tb
+  auto coords = [&](int j, int tb) {
+    const int pbase = z0 - 1 + 2 * j;
+    for (int c = pw; c < 2 * NS; c += 4) {   // wave-uniform (plane, view) combos
+      const int pl = c / NS, s = c - pl * NS;
+      const int p = pbase + pl;
+      const bool pok = p >= 0 && p < D;
+      float G[9];
+      load_matrix_uniform(a.sampling + ((size_t)(b * V + 1 + s) * D + (pok ? p : 0)) * 9, G);
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        const int v = lane + 64 * pass;
+        if (v < kHV) {
+          const int yy = v / kHX, xx = v - yy * kHX;
+          const int gx = x0 - 1 + xx, gy = y0 - 1 + yy;
+          const bool act = pok && gx >= 0 && gx < W && gy >= 0 && gy < H;
+          uint32_t pos;
+          float wx, wy;
+          src_coords(G, norm_coord(act ? gx : 0, W), norm_coord(act ? gy : 0, H), H, W, act, pos, wx, wy);
+          const uint32_t off = pos == kInvalidTap ? kOobOffset
+                                                  : ((uint32_t)(pos_y(pos) + 1) * (uint32_t)pg.pitch +
+                                                     (uint32_t)(pos_x(pos) + 1)) * pstride;
+          *reinterpret_cast<uint4*>(coord + (((tb * 2 + pl) * NS + s) * kHV + v) * 16) =
+              make_uint4(off, __float_as_uint(wx), __float_as_uint(wy), 0u);
+        }
+      }
+    }
+  };
+  const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
+  const Rsrc rscv = make_rsrc(a.scv ? static_cast<char*>(a.scv) + (size_t)b * kC4 * D * HW * 16 : nullptr,
+                              a.scv ? (uint32_t)min((uint64_t)kC4 * D * HW * 16ull, 0xFFFFFFF0ull) : 0u);
+  // variance of batch j's two planes -> ring slots (and the SCV box)
+  auto items = [&](int j, int tb) {
+    const int pbase = z0 - 1 + 2 * j;
+#pragma unroll
+    for (int u = 0; u < kItems; ++u) {
+      const int e = ptid + 256 * u;
+      if (e >= kBatchItems) break;   // wave-uniform (last pass: waves 4-6 only)
+      const int pl = e >= kPlaneItems ? 1 : 0;
+      const int r = e - pl * kPlaneItems;
+      const int v = r >> 3, q = r & 7;
+      const int yy = v / kHX, xx = v - yy * kHX;
+      const int p = pbase + pl;
+      const int gx = x0 - 1 + xx, gy = y0 - 1 + yy;
+      const bool valid = p >= 0 && p < D && gx >= 0 && gx < W && gy >= 0 && gy < H;
+      f4v xs[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const uint4 ce = *reinterpret_cast<const uint4*>(coord + (((tb * 2 + pl) * NS + s) * kHV + v) * 16);
+        const uint32_t o = ce.x + (uint32_t)q * 16u;
+        f4v tp[4];
+        tp[0] = ld4(rsv[s], o, 0);
+        tp[1] = ld4(rsv[s], o + pstride, 0);
+        tp[2] = ld4(rsv[s], o + (uint32_t)pg.pitch * pstride, 0);
+        tp[3] = ld4(rsv[s], o + (uint32_t)pg.pitch * pstride + pstride, 0);
+        xs[s] = bilerp(tp, __uint_as_float(ce.y), __uint_as_float(ce.z));
+      }
+      const f4v acc = head_variance4<NS>(ref[u], xs, inv_v);
+      uint2 hi, lo;
+      split4(acc, ex, hi, lo);
+      if (!valid) hi = lo = make_uint2(0u, 0u);
+      char* dst = ring + slot_of(p) * kSlotB + yy * kRowB + xx * kVoxB + ((((q >> 1) ^ ((xx >> 1) & 3))) << 4) +
+                  ((q & 1) << 3);
+      *reinterpret_cast<uint2*>(dst) = hi;
+      *reinterpret_cast<uint2*>(dst + kPartB) = lo;
+      // conv_2_0 / conv_3_0 read the SCV on their input box: the tile-interior voxels of this chunk's
+      // planes (every in-volume voxel is interior to exactly one tile and one chunk)
+      const bool st = valid && xx >= 1 && xx <= kTX && yy >= 1 && yy <= kTY && p >= z0 && p < z1 &&
+                      p >= a.r0[0] && p < a.r1[0] && gy >= a.r0[1] && gy < a.r1[1] && gx >= a.r0[2] && gx < a.r1[2];
+      typedef __attribute__((ext_vector_type(4))) unsigned v4u;
+      const uint32_t so = st ? (uint32_t)((((size_t)q * D + p) * HW + (size_t)gy * W + gx) * 16) : kOobOffset;
+      __builtin_amdgcn_raw_buffer_store_b128(v4u{hi.x, hi.y, lo.x, lo.y}, rscv, (int)so, 0, 0);
+    }
+  };
+
+  // ================================ consumer state ================================
+  const int i16 = lane & 15, g4 = lane >> 4;
+  h8v bw[27];
+  float sc0 = 1.0f, sh0 = 0.0f, mu0 = 0.0f, sc1 = 1.0f, sh1 = 0.0f, mu1 = 0.0f;
+  if (consumer) {
+    const Rsrc rwf = make_rsrc(a.w0, 27u * 64u * 16u);
+#pragma unroll
+    for (int tp = 0; tp < 27; ++tp)
+      bw[tp] = __builtin_bit_cast(h8v, __builtin_amdgcn_raw_buffer_load_b128(rwf, lane * 16, tp * 1024, 0));
+    if (a.bn0_sc) {
+      sc0 = a.bn0_sc[lane & 7];
+      sh0 = a.bn0_sh[lane & 7];
+      mu0 = a.bn0_mu[lane & 7];
+    }
+    if (a.bn1_sc) {
+      sc1 = a.bn1_sc[i16];
+      sh1 = a.bn1_sh[i16];
+      mu1 = a.bn1_mu[i16];
+    }
+    asm volatile("" ::"v"(sc0), "v"(sh0), "v"(mu0), "v"(sc1), "v"(sh1), "v"(mu1));
+  }
+  const int gy_out = y0 + wave;   // consumer wave's conv_0_0 output row
+  const bool row_on = consumer && gy_out < H && x0 < W;
+  int aoff[3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx)
+    aoff[kx] = (wave & 3) * kRowB + (i16 + kx) * kVoxB + ((g4 ^ (((i16 + kx) >> 1) & 3)) << 4);
+  const int oexp0 = -(ex + a.w_exp0), oexp1 = -(ex + a.w_exp1);
+  const int gx0 = x0 + 4 * g4;
+  const bool store_lane = (lane & 15) < 8;
+  const bool vec_store = (W & 3) == 0 && gx0 + 3 < W;
+  const size_t DHW = (size_t)D * HW;
+  // conv_1_0: MFMA row i16 = window (jx, jy); product wave w < 3
+  const int jx = i16 & 7, jy = i16 >> 3;
+  const int apart = wave == 2 ? kPartB : 0;    // x_lo for product 2
+  const int bpart = wave == 1 ? 1 : 0;         // w_lo for product 1
+  int acol[3];
+#pragma unroll
+  for (int tx = 0; tx < 3; ++tx) {
+    const int c = 2 * jx + tx;
+    acol[tx] = apart + c * kVoxB + ((g4 ^ ((c >> 1) & 3)) << 4);
+  }
+  f4 cur = {0.f, 0.f, 0.f, 0.f}, nxt = cur;
+  // acc += the 9 (ty, tx) taps of depth tap tz on plane slot sl (product wave's operands)
+  auto mac1 = [&](f4& acc, int sl, int tz) {
+    const char* base = ring + sl * kSlotB;
+#pragma unroll
+    for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+      for (int tx = 0; tx < 3; ++tx) {
+        const h8v x = *reinterpret_cast<const h8v*>(base + (2 * jy + ty) * kRowB + acol[tx]);
+        const h8v wv = *reinterpret_cast<const h8v*>(w1l + (((tz * 9 + ty * 3 + tx) * 2 + bpart) * 64 + lane) * 16);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, wv, acc, 0, 0, 0);
+      }
+  };
+  // wave 3: the completed window of depth start s from the partials in scratch buffer sb
+  auto finish1 = [&](int s, int sb) {
+    const f4 aa = *reinterpret_cast<const f4*>(scr + ((sb * 3 + 0) * 64 + lane) * 16);
+    const f4 ab = *reinterpret_cast<const f4*>(scr + ((sb * 3 + 1) * 64 + lane) * 16);
+    const f4 ac = *reinterpret_cast<const f4*>(scr + ((sb * 3 + 2) * 64 + lane) * 16);
+    const int oz = (s + a.pad[0]) >> 1;
+    if (oz < a.o0[0] || oz >= a.o0[0] + a.on[0]) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * g4 + r, wx_ = row & 7, wy_ = row >> 3;
+      const int oy = (y0 - 1 + 2 * wy_ + a.pad[1]) >> 1, ox = (x0 - 1 + 2 * wx_ + a.pad[2]) >> 1;
+      if (oy < a.o0[1] || oy >= a.o0[1] + a.on[1] || ox < a.o0[2] || ox >= a.o0[2] + a.on[2]) continue;
+      float v = ldexpf(aa[r] + (ab[r] + ac[r]), oexp1);
+      if (a.bn1_sc) v = fmaxf((v - mu1) * sc1 + sh1, 0.0f);
+      const size_t vx = (((size_t)(oz - a.o0[0]) * a.on[1] + (oy - a.o0[1])) * a.on[2] + (ox - a.o0[2]));
+      a.y1[(((size_t)b * a.on[0] * a.on[1] * a.on[2]) + vx) * 16 + i16] = v;
+    }
+  };
+
+  // ================================ schedule ================================
+  // Both roles pass the same barriers (nsteps + 3): producers fill batches 0, 1 before step 0 and batch
+  // k + 2 during step k; the sampling state of a batch is formed at least one barrier before its items.
+  if (!consumer) {
+    coords(0, 0);
+    coords(1, 1);
+    __syncthreads();
+    items(0, 0);
+    items(1, 1);
+    __syncthreads();
+    if (2 < nbatch) coords(2, 0);   // buffer 0 is free again (batch 0's items are done)
+    __syncthreads();
+    for (int k = 0; k < nsteps; ++k) {
+      if (k + 2 < nbatch) items(k + 2, (k + 2) & 1);
+      if (k + 3 < nbatch) coords(k + 3, (k + 3) & 1);
+      __syncthreads();
+    }
+    __syncthreads();
+    return;
+  }
+  __syncthreads();
+  __syncthreads();
+  __syncthreads();
+  for (int k = 0; k < nsteps; ++k) {
+    const int zs = z0 + 2 * k;
+    // ---- conv_0_0 on planes zs - 1 .. zs + 2 (conv3d_split.hip's item order) ----
+    if (row_on) {
+      f4 ah[2], al[2];
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        ah[d] = f4{0.f, 0.f, 0.f, 0.f};
+        al[d] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+      const char* base[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) base[p] = ring + ((2 * k + p) % kRing) * kSlotB;
+      constexpr int kIt = 9 * 4;
+      auto lda = [&](int it, h8v& hi, h8v& lo) {
+        const int grp = it / 4, p = it % 4, ky = grp / 3, kx = grp % 3;
+        hi = *reinterpret_cast<const h8v*>(base[p] + ky * kRowB + aoff[kx]);
+        lo = *reinterpret_cast<const h8v*>(base[p] + kPartB + ky * kRowB + aoff[kx]);
+      };
+      h8v rh[kPF + 1], rl[kPF + 1];
+#pragma unroll
+      for (int it = 0; it < kPF; ++it) lda(it, rh[it], rl[it]);
+#pragma unroll
+      for (int it = 0; it < kIt; ++it) {
+        const int p = it % 4, grp = it / 4;
+        if (it + kPF < kIt) lda(it + kPF, rh[(it + kPF) % (kPF + 1)], rl[(it + kPF) % (kPF + 1)]);
+        const h8v ch = rh[it % (kPF + 1)], cl = rl[it % (kPF + 1)];
+#pragma unroll
+        for (int kz = 0; kz < 3; ++kz) {
+          const int d = p - kz;
+          if (d < 0 || d >= 2) continue;
+          ah[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch, bw[kz * 9 + grp], ah[d], 0, 0, 0);
+          al[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cl, bw[kz * 9 + grp], al[d], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float hh = ah[d][r], lh = al[d][r];
+          const float hl = ror8(hh), ll = ror8(lh);
+          float s = ldexpf(hh + ((lh + hl) + ll), oexp0);
+          if (a.bn0_sc) s = fmaxf((s - mu0) * sc0 + sh0, 0.0f);
+          v[r] = s;
+        }
+        const int z = zs + d;
+        if (store_lane) {
+          float* o = a.y0 + ((size_t)(b * 8 + (lane & 7)) * D + z) * HW + (size_t)gy_out * W + gx0;
+          if (vec_store) {
+            // non-temporal: the 0.5 GB output is read once, by deconv_1_0 much later in the step
+            __builtin_nontemporal_store(f4v{v[0], v[1], v[2], v[3]}, reinterpret_cast<f4v*>(o));
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (gx0 + r < W) o[r] = v[r];
+          }
+        }
+      }
+    }
+    // ---- conv_1_0: window zs - 1 completes (depth tap 2 on plane zs + 1), window zs + 1 starts ----
+    if (wave < 3) {
+      if (k == 0) {
+        mac1(cur, slot_of(z0 - 1), 0);
+        mac1(cur, slot_of(z0), 1);
+      }
+      {
+        const char* base = ring + slot_of(zs + 1) * kSlotB;
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) {
+            const h8v x = *reinterpret_cast<const h8v*>(base + (2 * jy + ty) * kRowB + acol[tx]);
+            const h8v w2 = *reinterpret_cast<const h8v*>(w1l + (((18 + ty * 3 + tx) * 2 + bpart) * 64 + lane) * 16);
+            const h8v w0 = *reinterpret_cast<const h8v*>(w1l + (((ty * 3 + tx) * 2 + bpart) * 64 + lane) * 16);
+            cur = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, w2, cur, 0, 0, 0);
+            nxt = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, w0, nxt, 0, 0, 0);
+          }
+      }
+      mac1(nxt, slot_of(zs + 2), 1);
+      *reinterpret_cast<f4*>(scr + (((k & 1) * 3 + wave) * 64 + lane) * 16) = cur;
+      cur = nxt;
+      nxt = f4{0.f, 0.f, 0.f, 0.f};
+    } else if (k > 0) {
+      finish1(zs - 3, (k - 1) & 1);   // the window completed in step k - 1
+    }
+    __syncthreads();
+  }
+  // the last step's window; the last chunk also owns the window starting at D - 1 (its taps on
+  // planes D, D + 1 are zero: complete after the last step)
+  const bool tail = z1 == D;
+  if (wave < 3 && tail) *reinterpret_cast<f4*>(scr + (((nsteps & 1) * 3 + wave) * 64 + lane) * 16) = cur;
+  if (wave == 3) finish1(z1 - 3, (nsteps - 1) & 1);
+  __syncthreads();
+  if (wave == 3 && tail) finish1(z1 - 1, nsteps & 1);
+}
+
+// Outputs of the conv_1_0 region whose depth / row / column window no tile owns: windows entirely in
+// the zero padding (conv value 0), written as relu(BN_1(0)) exactly as conv3d_s2_split.hip's epilogue
+// forms it.  Per sample three slabs: z faces (lz + hz planes, whole rows), then y faces of the other
+// planes, then x faces of the rest; one thread per (voxel, channel).
+__global__ __launch_bounds__(256) void head_faces_kernel(float* __restrict__ y1, int B, int on0, int on1, int on2,
+                                                         int lz, int hz, int ly, int hy, int lx, int hx,
+                                                         const float* __restrict__ sc, const float* __restrict__ sh,
+                                                         const float* __restrict__ mu) {
+  const long nzf = lz + hz, nyf = ly + hy, nxf = lx + hx;
+  const long mz = on0 - nzf, my = on1 - nyf;
+  const long n0 = nzf * on1 * on2, n1 = mz * nyf * on2, n2 = mz * my * nxf;
+  const long per = n0 + n1 + n2;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < (long)B * per * 16; e += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(e & 15);
+    long i = e >> 4;
+    const long bb = i / per;
+    i -= bb * per;
+    int oz, oy, ox;
+    if (i < n0) {
+      const int zi = (int)(i / ((long)on1 * on2));
+      const long r = i - (long)zi * on1 * on2;
+      oz = zi < lz ? zi : on0 - hz + (zi - lz);
+      oy = (int)(r / on2);
+      ox = (int)(r - (long)oy * on2);
+    } else if (i < n0 + n1) {
+      i -= n0;
+      const int zi = (int)(i / (nyf * on2));
+      const long r = i - (long)zi * nyf * on2;
+      const int yi = (int)(r / on2);
+      oz = lz + zi;
+      oy = yi < ly ? yi : on1 - hy + (yi - ly);
+      ox = (int)(r - (long)yi * on2);
+    } else {
+      i -= n0 + n1;
+      const int zi = (int)(i / (my * nxf));
+      const long r = i - (long)zi * my * nxf;
+      const int yi = (int)(r / nxf);
+      const int xi = (int)(r - (long)yi * nxf);
+      oz = lz + zi;
+      oy = ly + yi;
+      ox = xi < lx ? xi : on2 - hx + (xi - lx);
+    }
+    float v = ldexpf(0.0f + (0.0f + 0.0f), 0);
+    if (sc) v = fmaxf((v - mu[co]) * sc[co] + sh[co], 0.0f);
+    y1[((((size_t)bb * on0 + oz) * on1 + oy) * on2 + ox) * 16 + co] = v;
+  }
+}
+
+}  // namespace
+
+size_t cv_head_lds_bytes(int V) { return V == 2 ? (size_t)lds_bytes<1>() : (size_t)lds_bytes<2>(); }
+
+int launch_cv_head(const Geometry& g, const float* feat, const Cams& cm, float* ws, uint32_t* absmax,
+                   const void* w0frag, int w_exp0, const void* w1frag, int w_exp1, const float* const* bn0,
+                   const float* const* bn1, float* y0, float* y1, void* scv, const int* pad, const int* o0,
+                   const int* on, const int* r0, const int* r1, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  float* smp = ws;
+  float* packed = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) +
+                                           align256((size_t)g.B * g.V * g.Dc * 9 * sizeof(float)));
+  launch_cv_prologue_pm(g, feat, cm, smp, packed, absmax, s);
+  HeadArgs a;
+  a.packed = reinterpret_cast<const float4*>(packed);
+  a.refs = a.packed + (size_t)g.B * g.V * kC4 * pad_geom(g.h, g.w).plane;
+  a.sampling = smp;
+  a.absmax = absmax;
+  a.w0 = reinterpret_cast<const h8v*>(w0frag);
+  a.w1 = reinterpret_cast<const h8v*>(w1frag);
+  a.bn0_sc = bn0[0];
+  a.bn0_sh = bn0[1];
+  a.bn0_mu = bn0[2];
+  a.bn1_sc = bn1[0];
+  a.bn1_sh = bn1[1];
+  a.bn1_mu = bn1[2];
+  a.y0 = y0;
+  a.y1 = y1;
+  a.scv = scv;
+  a.V = g.V;
+  a.D = g.Dc;
+  a.H = g.h;
+  a.W = g.w;
+  a.w_exp0 = w_exp0;
+  a.w_exp1 = w_exp1;
+  // tiles cover conv_0_0's outputs and every stride-2 window that touches the volume: a tile owns
+  // window starts [x0 - 1, x0 + 15) / [y0 - 1, y0 + 3), the last start is n - 1 (P odd, n even)
+  a.tiles_x = g.w / kTX + 1;
+  a.tiles_y = g.h / kTY + 1;
+  a.zchunks = (g.Dc + kZC - 1) / kZC;
+  const long total = (long)a.tiles_x * a.tiles_y * a.zchunks * g.B;
+  if (total >= (1L << 31) - 8) return MVS_ERR_TOO_LARGE;
+  a.total = (int)total;
+  for (int d = 0; d < 3; ++d) {
+    a.pad[d] = pad[d];
+    a.o0[d] = o0[d];
+    a.on[d] = on[d];
+    a.r0[d] = r0[d];
+    a.r1[d] = r1[d];
+  }
+  if (ev0) (void)hipEventRecord(ev0, s);
+  if (g.V == 2)
+    hipLaunchKernelGGL(cv_head_kernel<2>, xcd_grid(a.total), dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(cv_head_kernel<3>, xcd_grid(a.total), dim3(kThreads), 0, s, a);
+  if (ev1) (void)hipEventRecord(ev1, s);
+  // faces: per dim, region outputs whose window start 2 o - P lies below -1 (before tile 0) or at /
+  // beyond the last owned start (n_tiles * tile - 1 in x / y, D - 1 + 2 in z)
+  int lo[3], hi[3];
+  const int own_hi[3] = {g.Dc - 1, a.tiles_y * kTY - 1, a.tiles_x * kTX - 1};   // first unowned start
+  for (int d = 0; d < 3; ++d) {
+    lo[d] = 0;
+    while (lo[d] < on[d] && 2 * (o0[d] + lo[d]) - pad[d] < -1) ++lo[d];
+    hi[d] = 0;
+    while (hi[d] < on[d] - lo[d] && 2 * (o0[d] + on[d] - 1 - hi[d]) - pad[d] > own_hi[d] - (d == 0 ? 0 : 1)) ++hi[d];
+  }
+  if (lo[0] + hi[0] + lo[1] + hi[1] + lo[2] + hi[2] > 0) {
+    const long n = (long)g.B * on[0] * on[1] * on[2] * 16;
+    const int blocks = (int)std::min<long>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(head_faces_kernel, dim3(blocks), dim3(256), 0, s, y1, g.B, on[0], on[1], on[2], lo[0], hi[0],
+                       lo[1], hi[1], lo[2], hi[2], bn1[0], bn1[1], bn1[2]);
+  }
+  return MVS_OK;
+}
+
+}  // namespace mvs

@@ -36,6 +36,22 @@ void launch_cost_volume_fwd_bf16(const Geometry& g, const float* feat, const Cam
                                  float* packed, void* cv, hipStream_t s, hipEvent_t ev0 = nullptr,
                                  hipEvent_t ev1 = nullptr);
 
+// the fused launch's prologue alone with PIXEL-MAJOR packed features packed[N][h+2][w+2][C4] float4
+// (+ refs, bound words folded into absmax[8]); ws = the area after the sampling matrices
+void launch_cv_prologue_pm(const Geometry& g, const float* feat, const Cams& cm, float* sampling, float* ws,
+                           uint32_t* absmax, hipStream_t s);
+
+// cv_head.hip: the cost volume consumed where it is formed -- prologue, then ONE kernel forming the
+// variance plane by plane on chip and applying conv_0_0 (+ BN_0 + ReLU, y0 [B][8][D][H][W]) and the
+// stride-2 conv_1_0 (+ BN_1 + ReLU, channels-last region y1 [B][on...][16]); optionally stores the split
+// cost volume on the box [r0, r1) (scv, full-size [B][8][D][H][W] x 16 B).  C = 32, V in {2, 3}, pad odd,
+// D even (validated by the caller).  bn0 / bn1: {scale, shift, mean} or three nulls.
+int launch_cv_head(const Geometry& g, const float* feat, const Cams& cm, float* ws, uint32_t* absmax,
+                   const void* w0frag, int w_exp0, const void* w1frag, int w_exp1, const float* const* bn0,
+                   const float* const* bn1, float* y0, float* y1, void* scv, const int* pad, const int* o0,
+                   const int* on, const int* r0, const int* r1, hipStream_t s, hipEvent_t ev0 = nullptr,
+                   hipEvent_t ev1 = nullptr);
+
 // warp_variance.hip
 void launch_warp(const Geometry& g, const float* feat, const float* sampling, float* warped,
                  hipStream_t s);

@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmvs_cost_volume.so"
 # MVS_LIB_PATH: load another build of the same ABI (A/B kernel experiments, tools/gpu_*_ab.sh)
 LIB_PATH = os.environ.get("MVS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 MVS_OK = 0
 MVS_BWD_DETERMINISTIC = 1
@@ -58,6 +58,11 @@ SIGNATURES = {
     "mvs_conv3d_split_weights": (_c_int, [_p, _p, _p]),
     "mvs_conv3d_s2_split_fwd": (_c_int, [_p, _c_int, _p, _c_int, _p, _p, _c_int] + [_p] * 8),
     "mvs_conv3d_s2_split_weights": (_c_int, [_p, _p, _p]),
+    "mvs_cost_volume_head_fwd": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int,
+                                          _c_int, _c_int, _c_float,
+                                          _p, _c_int, _p, _p, _p, _p, _c_int, _p, _p, _p,
+                                          _p, _p, _p, _p, _p,
+                                          _p, _p, _p, _p, _p, _p, _p, _p]),
     "mvs_cost_volume_fwd_c4_bf16": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
                                              _c_int, _c_int, _c_int, _c_float, _p, _p, _p, _p, _p]),
     "mvs_cost_volume_fwd_bf16": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,

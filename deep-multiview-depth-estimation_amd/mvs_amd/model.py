@@ -156,16 +156,29 @@ class CostVolumeReg(nn.Module):
         self.split_f16 = os.environ.get("MVS_SPLIT_F16", "1") != "0"
 
     def forward(self, cv):
-        """cv [B, C, D, H, W], or the channel-quad [B, C/4, D, H, W, 4] of ops.cost_volume_c4 (fp32)
-        or ops.cost_volume_c4_bf16 (the bf16 opt-in) -- the HIP inference feed of MVSNet.forward; the
-        latter is read in place by the HIP live paths (bf16 widened on load, fp32 arithmetic) and
-        re-laid to NCDHW fp32 for any other path."""
+        """cv [B, C, D, H, W] (the reference's input), an ops.BoundCostVolume (the channel-quad layout
+        [B, C/4, D, H, W, 4] fp32 or split int32 with its bound words, ops.cost_volume_c4_absmax /
+        cost_volume_c4_split), the bf16 channel-quad volume of ops.cost_volume_c4_bf16 (opt-in), or a
+        costvolume.DeferredCostVolume -- the volume's inputs, consumed where it is formed by the fused
+        head kernel (forward_live_head) or materialised for any other path.  The HIP live paths read
+        the channel-quad volumes in place; other paths get the reference layout in fp32."""
+        from .costvolume import DeferredCostVolume
+        from .ops import BoundCostVolume, unsplit_cost_volume
+        if isinstance(cv, DeferredCostVolume):
+            if self.head_ok(cv):
+                return self.forward_live_head(cv)
+            cv = cv.materialize()
+        bound = None
+        if isinstance(cv, BoundCostVolume):
+            cv, bound = cv.data, cv.absmax
+        elif cv.dim() == 6 and cv.dtype == torch.int32:
+            raise ValueError("a split cost volume is meaningless without its bound words: pass "
+                             "ops.BoundCostVolume(cv, absmax) (what warp_and_assemble_cost_volume returns)")
         if cv.dim() == 6:
             if self.live_ok(cv.shape[2:5]) and _hip_cv(cv):
-                return self.forward_live(cv)
+                return self.forward_live(cv, bound)
             if cv.dtype == torch.int32:   # the split cost volume: fp32 values back (to 2^-22) for other paths
-                from .ops import cv_bound, unsplit_cost_volume
-                cv = unsplit_cost_volume(cv, cv_bound(cv))
+                cv = unsplit_cost_volume(cv, bound)
             if self.live_train_ok(cv.shape[2:5]) and _hip_cv(cv):
                 return self.forward_live_train(cv)
             cv = cv.permute(0, 1, 5, 2, 3, 4).reshape((cv.shape[0], 4 * cv.shape[1]) + tuple(cv.shape[2:5])).float()
@@ -174,6 +187,35 @@ class CostVolumeReg(nn.Module):
         if self.live_train_ok(cv.shape[2:]):
             return self.forward_live_train(cv)
         return self.forward_full(cv)
+
+    def head_ok(self, dcv):
+        """The fused head kernel applies to this deferred cost volume: eval-mode live regions with the
+        split-fp16 convolutions, fp32 HIP inference, C = 32, 2-3 views, D even and every stride-2
+        padding odd (the kernel's window ownership), MVS_CV_HEAD not 0."""
+        n = tuple(dcv.shape[2:])
+        return (os.environ.get("MVS_CV_HEAD", "1") != "0" and self.split_f16 and self.live_ok(n)
+                and _hip_inference(dcv.feature_maps) and dcv.shape[1] == 32 and dcv.n_views in (2, 3)
+                and n[0] % 2 == 0 and all(p % 2 == 1 for p in self.pad))
+
+    def forward_live_head(self, dcv):
+        """forward_live with the cost volume consumed where it is formed: one fused
+        kernel (ops.cost_volume_head, csrc/cv_head.hip) forms the variance plane by plane on chip and
+        applies conv_0_0 + BN_0 + ReLU (full volume) and conv_1_0 + BN_1 + ReLU (on halo(B)); the only
+        part of the volume written is conv_2_0's input box (the stride-2 windows of halo(C2), which
+        contain conv_3_0's), as the split cost volume.  The rest of the live evaluation is
+        _forward_live_hip's."""
+        n = tuple(dcv.shape[2:])
+        full = tuple((0, d - 1) for d in n)
+        B = _tconv_input_region(full, n, self.pad)
+        C2 = _tconv_input_region(B, n, self.pad)
+        C3 = _tconv_input_region(C2, n, self.pad)
+        h1, h2 = _grow(B, n, 1), _grow(C2, n, 1)
+        lo = [max(2 * a - p, 0) for (a, _), p in zip(h2, self.pad)]
+        hi = [min(2 * b - p + 2, d - 1) + 1 for (_, b), p, d in zip(h2, self.pad, n)]
+        y0, y1, box = dcv.head(self.conv_0_0.weight, _bn_eval(self.BN_0), self.conv_1_0.weight,
+                               _bn_eval(self.BN_1), self.pad, [a for a, _ in h1], [b - a + 1 for a, b in h1],
+                               lo, hi)
+        return self._forward_live_hip(box.data, n, B, C2, C3, True, box.absmax, head=(y0, y1))
 
     def live_train_ok(self, n):
         """forward_live_train applies: every BN in train mode with running statistics (test.py:61's
@@ -199,7 +241,7 @@ class CostVolumeReg(nn.Module):
         return any(bn.training or bn.running_mean is None
                    for bn in (self.BN_0, self.BN_1, self.BN_2, self.BN_3))
 
-    def forward_live(self, cv):
+    def forward_live(self, cv, bound=None):
         """Eval-mode regulariser evaluated only where its values reach the output.
 
         The stride-2 convs pad every dim by n//2 + 1 (config.py:20), so output j of conv_k_0 reads
@@ -223,7 +265,7 @@ class CostVolumeReg(nn.Module):
         C2 = _tconv_input_region(B, n, self.pad)
         C3 = _tconv_input_region(C2, n, self.pad)
         if _hip_cv(cv):
-            return self._forward_live_hip(cv, n, B, C2, C3, c4)
+            return self._forward_live_hip(cv, n, B, C2, C3, c4, bound)
         return self._forward_live_torch(cv, n, B, C2, C3)
 
     def forward_live_torch(self, cv):
@@ -255,14 +297,17 @@ class CostVolumeReg(nn.Module):
         z = act(self.BN_0, _tconv_region(y2 + y1, B, self.deconv_1_0.weight, full, self.pad)) + y0
         return self.Norm(self.conv_out(z))
 
-    def _forward_live_hip(self, cv, n, B, C2, C3, c4=False):
+    def _forward_live_hip(self, cv, n, B, C2, C3, c4=False, bound=None, head=None):
         """forward_live on the HIP kernels: conv_0_0 (csrc/conv3d_narrow.hip), every region conv
         and transposed conv on the fp32 MFMA with channels-last region tensors and the eval BN +
         ReLU fused (csrc/conv3d_region.hip), deconv_1_0 + BN_0 + ReLU + `+ y0` and the `y2 + y1`
         sum in one kernel (csrc/deconv3d_region.hip), conv_out (conv3d_narrow.hip).  ``c4``: cv is
-        the channel-quad volume, read by conv_0_0 and the three stride-2 convs with 16-byte loads."""
+        the channel-quad volume, read by conv_0_0 and the three stride-2 convs with 16-byte loads;
+        ``bound``: its bound words (the split-fp16 kernels' scale).  ``head``: (y0, y1) from the fused
+        head kernel (forward_live_head) -- conv_0_0's and conv_1_0's outputs; cv is then the split
+        volume on conv_2_0's input box only."""
         from .ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_k3_split, conv3d_region, conv_s2_split,
-                          cv_bound, deconv3d_k3s2, region_weight, softmax_depth)
+                          deconv3d_k3s2, region_weight, softmax_depth)
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad = list(n), list(self.pad)
@@ -277,25 +322,30 @@ class CostVolumeReg(nn.Module):
         # the split cost volume (int32, csrc/split.h) always goes to the split-fp16 kernels; an fp32
         # channel-quad volume does when split_f16 is on and it carries bound words
         split_cv = c4 and cv.dtype == torch.int32
-        bound = cv_bound(cv) if split_cv or (c4 and self.split_f16 and cv.dtype == torch.float32) else None
+        bound = bound if split_cv or (c4 and self.split_f16 and cv.dtype == torch.float32) else None
         if split_cv and bound is None:
             raise ValueError("split cost volume without its bound words")
         # the split-fp16 conv_0_0 (MFMA, LDS-staged) gains nothing beside the region chain: both compete
         # for the same CUs (cfg 2: 5.67 ms serialised against 5.78 ms on a side stream,
         # profiles/r03/r03u_reg_layers.log); the exact-fp32 VALU kernel overlaps the MFMA chain
         side = main if bound is not None else _side_stream(cv.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            if bound is not None:
-                y0 = conv3d_k3_split(cv, bound, self.conv_0_0.weight, *bn_eval(self.BN_0))
-                bound.record_stream(side)
-            else:
-                y0 = conv3d_k3(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), in_c4=c4, wino_z=True)
-        cv.record_stream(side)
+        if head is not None:
+            y0, y1_head = head
+        else:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                if bound is not None:
+                    y0 = conv3d_k3_split(cv, bound, self.conv_0_0.weight, *bn_eval(self.BN_0))
+                    bound.record_stream(side)
+                else:
+                    y0 = conv3d_k3(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), in_c4=c4, wino_z=True)
+            cv.record_stream(side)
 
         def level(conv_a, conv_b, bn, reg):
             halo = _grow(reg, n, 1)
-            if bound is not None and conv_a.weight.shape[0] == 16:
+            if head is not None and reg is B:
+                ya = y1_head   # conv_1_0 + BN_1 + ReLU on halo(B), from the fused head kernel
+            elif bound is not None and conv_a.weight.shape[0] == 16:
                 # conv_1_0 reads the whole volume: LDS-staged split-fp16 kernel (csrc/conv3d_s2_split.hip)
                 ya = conv_s2_split(cv, bound, conv_a.weight, dims, org(halo), size(halo), pad, *bn_eval(bn))
             else:
@@ -716,10 +766,15 @@ class MVSNet(nn.Module):
         # eval mode with the split-fp16 regulariser: the fused kernel writes the split cost volume
         split = (quads and not bf16 and reg.split_f16
                  and reg.live_ok((c.d_num,) + tuple(feature_maps.shape[2:])) and feature_maps.shape[1] == 32)
+        # ... and where the fused head kernel applies, the volume is not formed here at all: the
+        # regulariser forms it on chip inside conv_0_0 / conv_1_0
+        deferred = split and (c.d_num % 2 == 0 and n_views in (2, 3) and all(p % 2 == 1 for p in reg.pad)
+                              and os.environ.get("MVS_CV_HEAD", "1") != "0")
         cost_volume, d_batch, ref_views = warp_and_assemble_cost_volume(
             K_batch, R_batch, T_batch, d_min, d_int, feature_maps, batch_size, n_views,
             d_num=c.d_num, d_scale=c.d_scale,
-            cv_dtype=torch.bfloat16 if bf16 else torch.float32, channel_quads=quads, split=split)
+            cv_dtype=torch.bfloat16 if bf16 else torch.float32, channel_quads=quads and not deferred,
+            split=split, deferred=deferred)
         if bf16 and not quads:
             # opt-in: the volume is STORED in bf16 (rounded once); the regulariser
             # computes in fp32 from the rounded values, as the HIP channel-quad path does

@@ -254,21 +254,105 @@ def unsplit_cost_volume(cv, absmax):
                                                                             dtype=torch.float32))
 
 
-# bound words of channel-quad cost volumes made by cost_volume_c4_absmax / cost_volume_c4_split (id(cv) -> (weak cv, words)):
-# CostVolumeReg keeps the reference's forward(cv) signature, so the bound travels beside the tensor
-_CV_BOUNDS = {}
+class BoundCostVolume:
+    """A channel-quad cost volume together with its bound words (csrc/split.h): ``data`` is the fp32
+    channel-quad volume [B, C/4, D, h, w, 4] (cost_volume_c4_absmax) or the split volume (int32,
+    cost_volume_c4_split), ``absmax`` its int32[8] bound words (every element <= max|feat|^2; the split
+    scale).  The two travel as ONE object, so no copy, view or re-layout of the tensor can separate the
+    volume from its scale (CostVolumeReg.forward raises on a bare split tensor)."""
+    __slots__ = ("data", "absmax")
+
+    def __init__(self, data: torch.Tensor, absmax: torch.Tensor):
+        if data.dim() != 6 or data.dtype not in (_F32, torch.int32):
+            raise ValueError("channel-quad cost volume [B, C/4, D, h, w, 4] fp32 or int32 expected")
+        if absmax.numel() != 8 or absmax.dtype != torch.int32 or absmax.device != data.device:
+            raise ValueError("absmax: int32[8] on the volume's device expected")
+        self.data, self.absmax = data, absmax
+
+    shape = property(lambda self: self.data.shape)
+    dtype = property(lambda self: self.data.dtype)
+    device = property(lambda self: self.data.device)
+    is_cuda = property(lambda self: self.data.is_cuda)
+    split = property(lambda self: self.data.dtype == torch.int32)
+
+    def dim(self):
+        return self.data.dim()
+
+    def clone(self):
+        return BoundCostVolume(self.data.clone(), self.absmax.clone())
+
+    def quads(self):
+        """fp32 channel-quad values (the split volume re-formed to 2^-22 relative)."""
+        return unsplit_cost_volume(self.data, self.absmax) if self.split else self.data
+
+    def to_ncdhw(self):
+        """The reference layout [B, C, D, h, w] fp32."""
+        q = self.quads()
+        return q.permute(0, 1, 5, 2, 3, 4).reshape((q.shape[0], 4 * q.shape[1]) + tuple(q.shape[2:5]))
 
 
-def register_cv_bound(cv, absmax):
-    key = id(cv)
-    _CV_BOUNDS[key] = (weakref.ref(cv, lambda _r: _CV_BOUNDS.pop(key, None)), absmax)
-    return cv
+@torch.library.custom_op("mvs::cost_volume_head", mutates_args=())
+def cost_volume_head(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torch.Tensor,
+                     d_min: torch.Tensor, d_int: torch.Tensor, batch_size: int, n_views: int,
+                     d_begin: int, d_count: int, d_scale: float, w0: torch.Tensor,
+                     bn0_scale: Optional[torch.Tensor], bn0_shift: Optional[torch.Tensor],
+                     bn0_mean: Optional[torch.Tensor], w1: torch.Tensor, bn1_scale: Optional[torch.Tensor],
+                     bn1_shift: Optional[torch.Tensor], bn1_mean: Optional[torch.Tensor], pad: list[int],
+                     y1_origin: list[int], y1_size: list[int], scv_lo: list[int],
+                     scv_hi: list[int]) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """The cost volume consumed where it is formed (mvs_cost_volume_head_fwd, csrc/cv_head.hip; SURVEY.md
+    §8 f3): warp + variance (homography.py:6-92, costvolume.py:3-16) fused with conv_0_0 + BN_0 + ReLU
+    (model.py:101) and conv_1_0 + BN_1 + ReLU (model.py:103) on the split-fp16 matrix cores.  Returns
+    (y0 [B, 8, d_count, h, w], y1 channels-last [B, *y1_size, 16], scv, absmax): scv is the split cost
+    volume [B, 8, d_count, h, w, 4] int32 written ONLY on the box [scv_lo, scv_hi) (what conv_2_0 /
+    conv_3_0 read), absmax its bound words.  Bit-identical to cost_volume_c4_split -> conv3d_k3_split /
+    conv_s2_split.  C = 32, 2 <= n_views <= 3, d_count even, pad odd; inference only."""
+    _require_gpu(feat, "feature_maps")
+    lib = _lib.load()
+    feat = feat.to(_F32).contiguous()
+    K, R, T, d_min, d_int = _cams(K, R, T, d_min, d_int, feat.device, batch_size)
+    _check_geometry(feat, K, batch_size, n_views)
+    n, c, h, w = feat.shape
+    if tuple(w0.shape) != (8, 32, 3, 3, 3) or tuple(w1.shape) != (16, 32, 3, 3, 3):
+        raise ValueError("conv_0_0 [8, 32, 3, 3, 3] and conv_1_0 [16, 32, 3, 3, 3] weights expected")
+    dev = feat.device
+    f0, e0 = derived("k3split", (w0,), lambda wt: split_weight_fragments(wt, dev), dev)
+    f1, e1 = derived("s2split", (w1,), lambda wt: _s2_split_fragments(wt, dev), dev)
+
+    def bn(ts):
+        ts = [t if t is None else t.to(device=dev, dtype=_F32).contiguous() for t in ts]
+        if any(t is None for t in ts) and not all(t is None for t in ts):
+            raise ValueError("BN scale, shift and mean go together")
+        return ts, [None if t is None else _lib.ptr(t) for t in ts]
+    bn0, bp0 = bn((bn0_scale, bn0_shift, bn0_mean))
+    bn1, bp1 = bn((bn1_scale, bn1_shift, bn1_mean))
+    y0 = torch.empty((batch_size, 8, d_count, h, w), device=dev, dtype=_F32)
+    y1 = torch.empty([batch_size] + [int(v) for v in y1_size] + [16], device=dev, dtype=_F32)
+    boxed = all(int(hi_) > int(lo_) for lo_, hi_ in zip(scv_lo, scv_hi))
+    scv = torch.empty((batch_size, 8, d_count, h, w, 4) if boxed else (0,), device=dev, dtype=torch.int32)
+    absmax = torch.empty((8,), device=dev, dtype=torch.int32)
+    ws = torch.empty((_ws_floats(batch_size, n_views, c, h, w, d_count),), device=dev, dtype=_F32)
+    evs = (None, None)
+    if KERNEL_EVENT_HOOK is not None:
+        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK())
+    st = lib.mvs_cost_volume_head_fwd(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T), _lib.ptr(d_min),
+                                      _lib.ptr(d_int), batch_size, n_views, c, h, w, d_begin, d_count,
+                                      float(d_scale), _lib.ptr(f0), int(e0), *bp0, _lib.ptr(f1), int(e1), *bp1,
+                                      _ints3(pad), _ints3(y1_origin), _ints3(y1_size), _ints3(scv_lo),
+                                      _ints3(scv_hi), _lib.ptr(ws), _lib.ptr(absmax), _lib.ptr(y0), _lib.ptr(y1),
+                                      _lib.ptr(scv) if boxed else None, _lib.stream_handle(dev), *evs)
+    _lib.check(st, "mvs_cost_volume_head_fwd")
+    return y0, y1, scv, absmax
 
 
-def cv_bound(cv):
-    """The bound words registered for this cost-volume tensor, or None."""
-    hit = _CV_BOUNDS.get(id(cv))
-    return hit[1] if hit is not None and hit[0]() is cv else None
+@cost_volume_head.register_fake
+def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scale, w0, bn0_scale, bn0_shift,
+      bn0_mean, w1, bn1_scale, bn1_shift, bn1_mean, pad, y1_origin, y1_size, scv_lo, scv_hi):
+    n, c, h, w = feat.shape
+    boxed = all(int(hi_) > int(lo_) for lo_, hi_ in zip(scv_lo, scv_hi))
+    return (feat.new_empty((batch_size, 8, d_count, h, w)), feat.new_empty([batch_size] + list(y1_size) + [16]),
+            feat.new_empty((batch_size, 8, d_count, h, w, 4) if boxed else (0,), dtype=torch.int32),
+            feat.new_empty((8,), dtype=torch.int32))
 
 
 @torch.library.custom_op("mvs::cost_volume_c4_bf16", mutates_args=())

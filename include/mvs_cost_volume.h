@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 8
+#define MVS_ABI_VERSION 9
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -126,9 +126,10 @@ int mvs_cost_volume_fwd_c4(const float* feat, const float* K, const float* R, co
 
 /*
  * mvs_cost_volume_fwd_c4 that also records a bound for the split-fp16 consumers
- * (mvs_conv3d_k3_split_fwd): feat_absmax (8 uint32 words, DEVICE, 4-byte aligned) is zeroed on the
- * stream and then receives, per XCD, the maximum of the |feat| bit patterns (NaN sorts above Inf
- * above every finite value).  A variance over views is at most the largest squared sample, and a
+ * (mvs_conv3d_k3_split_fwd): feat_absmax (8 uint32 words, DEVICE, 4-byte aligned) receives the
+ * maximum of the |feat| bit patterns (NaN sorts above Inf above every finite value) in all 8 words:
+ * the prologue's packing workgroups write per-workgroup partial maxima into the workspace and one
+ * 1-workgroup kernel folds them (no memset, no atomics).  A variance over views is at most the largest squared sample, and a
  * bilinear sample (zero padding) at most max|feat|, so every element of cv_out is <= B^2 with
  * B = the float of the largest of the 8 words.  Otherwise as mvs_cost_volume_fwd_c4.
  */
@@ -321,6 +322,41 @@ int mvs_conv3d_s2_split_fwd(const void* x, int flags, const void* weight_frag, i
  * part (0 hi, 1 lo) of w[c = lane & 15][8 (lane >> 4) + j][tap] * 2^ew, *weight_exp = ew (max|w| 2^ew
  * < 2^14). */
 int mvs_conv3d_s2_split_weights(const float* weight, unsigned short* frag, int* weight_exp);
+
+/* The cost volume CONSUMED WHERE IT IS FORMED (replaces model.py:177-181 + 101-103 in
+ * eval inference): homography_warping + assemble_cost_volume (homography.py:6-92, costvolume.py:3-16)
+ * fused with the regulariser's two full-volume readers, conv_0_0 (model.py:101) and conv_1_0
+ * (model.py:103), so the B x C x D x h x w volume is never written (csrc/cv_head.hip).
+ * One prologue kernel (sampling matrices, pixel-major packed features, reference resampling, bound
+ * words) and one fused kernel: per 16 x 4 x 48 tile the variance of every plane is formed on chip,
+ * split into fp16 hi / lo parts (mvs_cost_volume_fwd_c4_split's arithmetic: bit-identical operands)
+ * and fed to both convolutions on the f16 matrix cores (mvs_conv3d_k3_split_fwd's and
+ * mvs_conv3d_s2_split_fwd's arithmetic: bit-identical outputs).
+ *   feat, K, R, T, d_min, d_int, batch_size, n_views, h, w, d_begin, d_count, d_scale, workspace: as
+ *     mvs_cost_volume_fwd (workspace: mvs_cost_volume_workspace_bytes); channels must be 32,
+ *     n_views 2 or 3 (else MVS_ERR_UNSUPPORTED_VIEWS), d_count even;
+ *   w0_frag / w0_exp: conv_0_0 (mvs_conv3d_split_weights, DEVICE); bn0_*: BN_0 eval epilogue (8 floats
+ *     each, all or none); w1_frag / w1_exp: conv_1_0 (mvs_conv3d_s2_split_weights, DEVICE); bn1_*: 16
+ *     floats each, all or none;
+ *   pad[3] (HOST, (d, h, w) order): conv_1_0's stride-2 padding, every entry odd (n // 2 + 1 with
+ *     n % 4 in {0, 1}, config.py:20);
+ *   y1_origin[3], y1_size[3] (HOST): conv_1_0's output region, inside its (n + 2 pad - 3) / 2 + 1 outputs;
+ *   scv_lo[3], scv_hi[3] (HOST): a box [lo, hi) of the volume whose split cost volume is also stored
+ *     into scv (the input box of the regulariser's conv_2_0 / conv_3_0; scv NULL: nothing stored);
+ *   feat_absmax: 8 bound words (DEVICE), written as mvs_cost_volume_fwd_c4_absmax does;
+ *   y0: [batch][8][d_count][h][w] fp32 = relu(BN_0(conv_0_0(cv))); y1: channels-last region
+ *     [batch][y1_size...][16] fp32 = relu(BN_1(conv_1_0(cv))); scv: [batch][8][d_count][h][w] x 16 B
+ *     (full-size allocation, 16-byte aligned; only the box is written).
+ * 128 * d_count * h * w <= 2^32 - 16.  Events (either may be NULL) are recorded around the fused kernel. */
+int mvs_cost_volume_head_fwd(const float* feat, const float* K, const float* R, const float* T,
+                             const float* d_min, const float* d_int, int batch_size, int n_views,
+                             int channels, int h, int w, int d_begin, int d_count, float d_scale,
+                             const void* w0_frag, int w0_exp, const float* bn0_scale, const float* bn0_shift,
+                             const float* bn0_mean, const void* w1_frag, int w1_exp, const float* bn1_scale,
+                             const float* bn1_shift, const float* bn1_mean, const int* pad,
+                             const int* y1_origin, const int* y1_size, const int* scv_lo, const int* scv_hi,
+                             float* workspace, unsigned* feat_absmax, float* y0, float* y1, void* scv,
+                             void* stream, void* main_begin_event, void* main_end_event);
 
 /* Feature encoder and refinement layers (model.py:22-65 FeatureEncoder, model.py:134-145): nn.Conv2d(
  * c_in, c_out, k, stride, padding=k/2, bias=False) over x[n][c_in][h][w] fp32 into

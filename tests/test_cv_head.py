@@ -1,0 +1,134 @@
+"""The cost volume consumed where it is formed (csrc/cv_head.hip, ops.cost_volume_head).
+
+The fused head forms the variance of homography_warping + assemble_cost_volume (homography.py:6-92,
+costvolume.py:3-16) on chip and applies conv_0_0 + BN_0 + ReLU (model.py:101) and conv_1_0 + BN_1 +
+ReLU (model.py:103) to it.  It uses the materialising path's arithmetic operand for operand and MFMA
+for MFMA, so its outputs must be BIT-EQUAL to that path: the split cost volume
+(mvs_cost_volume_fwd_c4_split) fed to the split-fp16 conv_0_0 (mvs_conv3d_k3_split_fwd) and conv_1_0
+(mvs_conv3d_s2_split_fwd), whose own parity against float64 and the oracle is pinned in
+test_split_conv.py / test_gpu_configs.py.  The split volume the head stores on conv_2_0's input box
+must equal the materialised one there.
+"""
+import os
+
+import pytest
+import torch
+
+DEV = torch.device("cuda", 0)
+
+
+def _regions(n, pad):
+    from mvs_amd import model as M
+    full = tuple((0, d - 1) for d in n)
+    B = M._tconv_input_region(full, n, pad)
+    C2 = M._tconv_input_region(B, n, pad)
+    h1, h2 = M._grow(B, n, 1), M._grow(C2, n, 1)
+    lo = [max(2 * a - p, 0) for (a, _), p in zip(h2, pad)]
+    hi = [min(2 * b - p + 2, d - 1) + 1 for (_, b), p, d in zip(h2, pad, n)]
+    return h1, lo, hi
+
+
+def test_bare_split_volume_is_rejected():
+    """CPU: a split (int32) channel-quad volume without its bound words raises a clear error instead
+    of silently dropping to another scale (the bound travels in ops.BoundCostVolume)."""
+    from mvs_amd.model import CostVolumeReg
+    from mvs_amd.config import pad_outpad
+    reg = CostVolumeReg(pad=pad_outpad(8, 8, 8)[0], outpad=pad_outpad(8, 8, 8)[1]).eval()
+    with pytest.raises(ValueError, match="bound words"):
+        reg(torch.zeros((1, 8, 8, 8, 8, 4), dtype=torch.int32))
+
+
+def test_bound_cost_volume_travels_with_its_bound():
+    """CPU: BoundCostVolume keeps data and bound together through clone(); to_ncdhw() is the reference
+    layout of the channel-quad values."""
+    from mvs_amd.ops import BoundCostVolume
+    q = torch.randn(2, 3, 4, 5, 6, 4)
+    b = BoundCostVolume(q, torch.zeros(8, dtype=torch.int32))
+    c = b.clone()
+    assert c.data is not q and torch.equal(c.data, q) and torch.equal(c.absmax, b.absmax)
+    ref = q.permute(0, 1, 5, 2, 3, 4).reshape(2, 12, 4, 5, 6)
+    assert torch.equal(b.to_ncdhw(), ref)
+    with pytest.raises(ValueError):
+        BoundCostVolume(q, torch.zeros(4, dtype=torch.int32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,V,D,h,w", [(2, 3, 16, 32, 48), (1, 2, 20, 24, 40), (1, 3, 100, 36, 44),
+                                       (2, 3, 48, 28, 64)])
+def test_head_is_bit_equal_to_the_split_path(B, V, D, h, w):
+    """y0, y1 and the stored box are bit-equal to cost_volume_c4_split -> conv3d_k3_split /
+    conv_s2_split; geometries with one and several 48-plane chunks (a partial last one at D = 100),
+    V = 2 and 3, widths / heights not multiples of the 16 x 4 tile."""
+    from cameras import camera_batch, depth_range
+    from mvs_amd import ops
+    from mvs_amd.config import pad_outpad
+    C = 32
+    pad = list(pad_outpad(D, h, w)[0])
+    assert all(p % 2 for p in pad)
+    n = (D, h, w)
+    h1, lo, hi = _regions(n, pad)
+    K, R, T = camera_batch(B, V, h, w)
+    d_min, d_int = depth_range(B, d_int=200.0 / D)
+    g = torch.Generator().manual_seed(D + h + w)
+    feat = torch.randn(B * V, C, h, w, generator=g).to(DEV)
+    w0 = (torch.randn(8, 32, 3, 3, 3, generator=g) * 0.1).to(DEV)
+    w1 = (torch.randn(16, 32, 3, 3, 3, generator=g) * 0.1).to(DEV)
+    bn0 = [(torch.rand(8, generator=g) + 0.5).to(DEV), (torch.randn(8, generator=g) * 0.1).to(DEV),
+           (torch.randn(8, generator=g) * 0.1).to(DEV)]
+    bn1 = [(torch.rand(16, generator=g) + 0.5).to(DEV), (torch.randn(16, generator=g) * 0.1).to(DEV),
+           (torch.randn(16, generator=g) * 0.1).to(DEV)]
+    org, size = [a for a, _ in h1], [b - a + 1 for a, b in h1]
+    with torch.no_grad():
+        scv, absmax = ops.cost_volume_c4_split(feat, K, R, T, d_min, d_int, B, V, 0, D, 25.0)
+        y0_ref = ops.conv3d_k3_split(scv, absmax, w0, *bn0)
+        y1_ref = ops.conv_s2_split(scv, absmax, w1, list(n), org, size, pad, *bn1)
+        y0, y1, box, am = ops.cost_volume_head(feat, K, R, T, d_min, d_int, B, V, 0, D, 25.0, w0, *bn0, w1, *bn1,
+                                               pad, org, size, lo, hi)
+        torch.cuda.synchronize()
+    assert torch.equal(am, absmax)
+    assert torch.equal(y0, y0_ref), (y0 - y0_ref).abs().max().item()
+    assert torch.equal(y1, y1_ref), (y1 - y1_ref).abs().max().item()
+    sl = (slice(None), slice(None)) + tuple(slice(a, b) for a, b in zip(lo, hi))
+    assert torch.equal(box[sl], scv[sl])
+    # without BN epilogues (raw convolution values) as well
+    with torch.no_grad():
+        y0n, y1n, _, _ = ops.cost_volume_head(feat, K, R, T, d_min, d_int, B, V, 0, D, 25.0, w0, None, None, None,
+                                              w1, None, None, None, pad, org, size, lo, hi)
+        assert torch.equal(y0n, ops.conv3d_k3_split(scv, absmax, w0))
+        assert torch.equal(y1n, ops.conv_s2_split(scv, absmax, w1, list(n), org, size, pad))
+
+
+@pytest.mark.gpu
+def test_mvsnet_head_equals_split_volume_path():
+    """MVSNet.forward with the fused head (the default eval path) gives the same depth maps, bit for
+    bit, as the same network fed the materialised split volume (MVS_CV_HEAD=0), at cfg 1's geometry
+    with B = 2."""
+    from cameras import camera_batch, depth_range
+    from mvs_amd.config import MVSConfig
+    from mvs_amd.model import MVSNet
+    B, V, D, H, W = 2, 3, 48, 512, 640
+    torch.manual_seed(0)
+    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W)).to(DEV).eval()
+    K, R, T = camera_batch(B, V, H // 4, W // 4)
+    d_min, d_int = depth_range(B)
+    img = torch.randn(B * V, 3, H, W, generator=torch.Generator().manual_seed(5)).to(DEV)
+    import mvs_amd.costvolume as cvmod
+    calls = []
+    orig = cvmod.DeferredCostVolume.head
+
+    def spy(self, *a, **kw):
+        calls.append(1)
+        return orig(self, *a, **kw)
+    with torch.no_grad():
+        cvmod.DeferredCostVolume.head = spy
+        try:
+            d_head, r_head = net(img, K, R, T, d_min, d_int, B, V)
+        finally:
+            cvmod.DeferredCostVolume.head = orig
+        os.environ["MVS_CV_HEAD"] = "0"
+        try:
+            d_split, r_split = net(img, K, R, T, d_min, d_int, B, V)
+        finally:
+            os.environ.pop("MVS_CV_HEAD")
+    assert calls == [1]
+    assert torch.equal(d_head, d_split) and torch.equal(r_head, r_split)

@@ -17,7 +17,7 @@ import torch  # noqa: E402
 from mvs_amd import model as M  # noqa: E402
 from mvs_amd.ops import conv_s2_split  # noqa: E402
 from mvs_amd.ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_k3_split, conv3d_region,  # noqa: E402
-                         cv_bound, deconv3d_k3s2, region_weight, softmax_depth)
+                         deconv3d_k3s2, region_weight, softmax_depth)
 
 
 def timed(name, fn, n):
@@ -49,6 +49,7 @@ def main():
         cv, _, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, B, V, d_num=D, channel_quads=True)
         cvs, _, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, B, V, d_num=D, channel_quads=True,
                                                   split=True)
+        cv, cvs, bound = cv.data, cvs.data, cvs.absmax   # BoundCostVolume: (volume, bound words)
         n = tuple(cv.shape[2:5])
         full = tuple((0, d - 1) for d in n)
         Bq = M._tconv_input_region(full, n, reg.pad)
@@ -60,7 +61,7 @@ def main():
         bn = M._bn_eval
         layers = {}
         layers["conv_0_0"] = lambda: conv3d_k3(cv, reg.conv_0_0.weight, *bn(reg.BN_0), in_c4=True, wino_z=True)
-        layers["conv_0_0_split"] = lambda: conv3d_k3_split(cvs, cv_bound(cvs), reg.conv_0_0.weight, *bn(reg.BN_0))
+        layers["conv_0_0_split"] = lambda: conv3d_k3_split(cvs, bound, reg.conv_0_0.weight, *bn(reg.BN_0))
         y0 = layers["conv_0_0"]()
         y0s = layers["conv_0_0_split"]()
         print("conv_0_0 split vs exact fp32: max|d| %.3g (max|y| %.3g)"
@@ -79,7 +80,7 @@ def main():
             layers["conv_%d_0" % (k + 1)] = fa
             if k == 0:
                 layers["conv_1_0_split"] = (lambda ca=ca, bnm=bnm, halo=halo: conv_s2_split(
-                    cvs, cv_bound(cvs), ca.weight, dims, org(halo), size(halo), pad, *bn(bnm)))
+                    cvs, bound, ca.weight, dims, org(halo), size(halo), pad, *bn(bnm)))
                 ys = layers["conv_1_0_split"]()
                 print("conv_1_0 split vs exact fp32: max|d| %.3g (max|y| %.3g)"
                       % ((ys - ya).abs().max().item(), ya.abs().max().item()), flush=True)
@@ -98,6 +99,22 @@ def main():
         layers["conv_out"] = lambda: conv3d_k3(z, reg.conv_out.weight)
         o = layers["conv_out"]()
         layers["softmax"] = lambda: softmax_depth(o)
+        # the fused head (csrc/cv_head.hip): variance + conv_0_0 + conv_1_0 on chip, against the split
+        # producer + the two split consumers it replaces
+        dcv, _, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, B, V, d_num=D, deferred=True)
+        h1, h2 = M._grow(Bq, n, 1), M._grow(C2, n, 1)
+        lo = [max(2 * a0 - p, 0) for (a0, _), p in zip(h2, pad)]
+        hi = [min(2 * b1 - p + 2, d - 1) + 1 for (_, b1), p, d in zip(h2, pad, n)]
+        layers["cv_split"] = lambda: warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, B, V, d_num=D,
+                                                                   channel_quads=True, split=True)
+        layers["cv_head"] = lambda: dcv.head(reg.conv_0_0.weight, bn(reg.BN_0), reg.conv_1_0.weight, bn(reg.BN_1),
+                                             pad, org(h1), size(h1), lo, hi)
+        y0h, y1h, box = layers["cv_head"]()
+        y1s = conv_s2_split(cvs, bound, reg.conv_1_0.weight, dims, org(h1), size(h1), pad, *bn(reg.BN_1))
+        sl = (slice(None), slice(None)) + tuple(slice(a0, b1) for a0, b1 in zip(lo, hi))
+        print("cv_head vs split path: y0 equal %s (max|d| %.3g), y1 equal %s (max|d| %.3g), box equal %s" % (
+            torch.equal(y0h, y0s), (y0h - y0s).abs().max().item(), torch.equal(y1h, y1s),
+            (y1h - y1s).abs().max().item(), torch.equal(box.data[sl], cvs[sl])), flush=True)
         if a.only:   # one layer or a comma-separated list ("step": the whole eval step)
             for name in a.only.split(","):
                 timed(name, (lambda: net(img, K, R, T, d_min, d_int, B, V)) if name == "step" else layers[name],
@@ -106,7 +123,10 @@ def main():
         for name, fn in layers.items():
             timed(name, fn, a.reps)
         step = lambda: net(img, K, R, T, d_min, d_int, B, V)
-        timed("eval step (side stream)", step, a.reps)
+        timed("eval step (fused head)", step, a.reps)
+        os.environ["MVS_CV_HEAD"] = "0"
+        timed("eval step (split volume)", step, a.reps)
+        os.environ.pop("MVS_CV_HEAD")
         reg.split_f16 = False
         timed("eval step (exact fp32 conv_0_0)", step, a.reps)
         reg.split_f16 = True
