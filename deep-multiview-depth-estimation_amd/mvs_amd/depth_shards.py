@@ -15,7 +15,11 @@ runs the regulariser, soft-argmin and refinement for it:
     strided device copy then interleaves the P slabs into the final [C, D, h, w] layout (the
     regulariser's NCDHW input, where a slab is C separate blocks).  All messages of a step are one
     grouped ``batch_isend_irecv`` (RCCL over xGMI when the process group is ``nccl``): at cfg 4
-    (B = 1, P = 8) rank 0 posts 7 receives of 84 MB instead of 7 x 32 per-channel ones.
+    (B = 1, P = 8) rank 0 posts 7 receives of 84 MB instead of 7 x 32 per-channel ones;
+  * the depth maps come back to ONE rank (``gather_depth_maps``, SURVEY.md §8 e step 4): every owner
+    sends its samples' initial and refined maps as one [n_owned, 2, h, w] message to rank ``dst``,
+    which returns the whole batch in sample order -- ``DepthShardedMVSNet.forward`` then has
+    MVSNet.forward's return value on that rank.
 
 Expected cfg 4 step (B = 1, D = 256, 8 ranks): each rank's 32-plane shard kernel
 ~0.05 ms, the exchange ~0.55 ms (the owner receives 7 x 84 MB, one slab per xGMI link in
@@ -120,6 +124,43 @@ def gather_depth_slabs(slab, world, group=None):
     return out
 
 
+def gather_depth_maps(initial, refined, batch_size, world, rank, h, w, dst=0, group=None, device=None,
+                      dtype=torch.float32):
+    """The owners' depth maps -> rank ``dst`` in sample order (SURVEY.md §8 e step 4).
+
+    ``initial`` / ``refined``: this rank's owned samples' maps [len(owned_samples), 1, h, w] (None
+    when it owns none).  Every rank must call it.  Each owner other than ``dst`` sends ONE message
+    ([n_owned, 2, h, w]: initial and refined stacked, 160 KB per sample at 128 x 160); ``dst`` posts
+    one receive per such peer, sized from owned_samples.  Returns (initial [B, 1, h, w], refined
+    [B, 1, h, w]) on ``dst``, (None, None) elsewhere."""
+    mine = owned_samples(batch_size, world, rank)
+    pack = None if not mine else torch.cat((initial, refined), dim=1).contiguous()
+    if rank != dst:
+        if mine and world > 1:
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, pack, dst, group)]):
+                req.wait()
+        return None, None
+    dev, dt = (pack.device, pack.dtype) if pack is not None else (device, dtype)
+    out = torch.empty((batch_size, 2, h, w), device=dev, dtype=dt)
+    ops, recvd = [], []
+    for src in range(world):
+        own = owned_samples(batch_size, world, src)
+        if not own:
+            continue
+        if src == rank:
+            out[torch.tensor(own, device=dev)] = pack
+            continue
+        buf = torch.empty((len(own), 2, h, w), device=dev, dtype=dt)
+        ops.append(dist.P2POp(dist.irecv, buf, src, group))
+        recvd.append((own, buf))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    for own, buf in recvd:
+        out[torch.tensor(own, device=dev)] = buf
+    return out[:, 0:1], out[:, 1:2]
+
+
 class _HipOps:
     """The product path: fused HIP cost volume slab + HIP soft-argmin."""
 
@@ -141,17 +182,21 @@ class DepthShardedMVSNet(nn.Module):
     """Wraps an ``MVSNet``: D-sharded cost volume + owner-targeted exchange + owner-computes
     regulariser.
 
-    ``forward`` returns ``(samples, initial, refined)``: the indices of the samples this rank owns
-    and their depth maps ([len(samples), 1, h, w] each; ``None`` when the rank owns none).
-    ``ops`` supplies the slab producer and the soft-argmin (default: the HIP kernels)."""
+    ``forward`` returns MVSNet.forward's ``(initial, refined)`` [B, 1, h, w] for the whole batch on
+    rank ``dst`` (the owners' maps gathered there, ``gather_depth_maps``) and ``(None, None)`` on the
+    other ranks; with ``gather=False`` it returns ``(samples, initial, refined)`` on every rank: the
+    samples this rank owns and their maps (``None`` when it owns none).  ``ops`` supplies the slab
+    producer and the soft-argmin (default: the HIP kernels)."""
 
-    def __init__(self, net, world, rank, group=None, ops=None):
+    def __init__(self, net, world, rank, group=None, ops=None, gather=True, dst=0):
         super().__init__()
         self.net = net
         self.world = world
         self.rank = rank
         self.group = group
         self.ops = ops or _HipOps
+        self.gather = gather
+        self.dst = dst
 
     def _check_mode(self):
         if torch.is_grad_enabled():
@@ -172,13 +217,17 @@ class DepthShardedMVSNet(nn.Module):
             d_begin, d_count)
         cv = exchange_to_owners(slab, self.world, self.rank, self.group)
         mine = owned_samples(batch_size, self.world, self.rank)
-        if not mine:
-            return mine, None, None
-        idx = torch.tensor(mine, device=cv.device)
-        prob = self.net.cost_volume_reg(cv)
-        d_sel = d_batch.to(cv.device).index_select(0, idx)
-        initial = self.ops.extract_depth_map(prob, d_sel, c.n_depth_est)
-        dm = d_min.reshape(-1, 1, 1, 1).expand(batch_size, 1, 1, 1).to(cv.device).index_select(0, idx)
-        di = d_int.reshape(-1, 1, 1, 1).expand(batch_size, 1, 1, 1).to(cv.device).index_select(0, idx)
-        refined = self.net.refine(nn_input, initial, dm, di, ref_views[mine])
-        return mine, initial, refined
+        initial = refined = None
+        if mine:
+            idx = torch.tensor(mine, device=cv.device)
+            prob = self.net.cost_volume_reg(cv)
+            d_sel = d_batch.to(cv.device).index_select(0, idx)
+            initial = self.ops.extract_depth_map(prob, d_sel, c.n_depth_est)
+            dm = d_min.reshape(-1, 1, 1, 1).expand(batch_size, 1, 1, 1).to(cv.device).index_select(0, idx)
+            di = d_int.reshape(-1, 1, 1, 1).expand(batch_size, 1, 1, 1).to(cv.device).index_select(0, idx)
+            refined = self.net.refine(nn_input, initial, dm, di, ref_views[mine])
+        if not self.gather:
+            return mine, initial, refined
+        h, w = feats.shape[2:]
+        return gather_depth_maps(initial, refined, batch_size, self.world, self.rank, h, w, self.dst, self.group,
+                                 feats.device, feats.dtype)

@@ -6,8 +6,10 @@
   each sample must end with exactly the single-process volume of that sample, bit for bit.
 * ``DepthShardedMVSNet.forward`` end to end with the oracle injected as the slab producer and
   soft-argmin (``ops=``) and the regulariser/refinement on the CPU: every rank's owned depth maps
-  must equal the single-process model's (model.py:168-207 via oracle.mvsnet_forward); B=3 (rank 0
-  owns samples 0 and 2, rank 1 owns sample 1) and B=1 (cfg 4's shape: rank 1 owns nothing).
+  must equal the single-process model's (model.py:168-207 via oracle.mvsnet_forward), and with the
+  default ``gather=True`` rank 0 must hold ALL B maps (SURVEY.md §8 e step 4) equal to the
+  single-process model's; B=3 (rank 0 owns samples 0 and 2, rank 1 owns sample 1) and B=1 (cfg 4's
+  shape: rank 1 owns nothing).
 """
 import os
 import socket
@@ -96,17 +98,26 @@ def _model_worker(rank, world, port, B, q):
         K, R, T = camera_batch(B, V, H // 4, W // 4)
         d_min, d_int = depth_range(B, d_int=6.0, distinct=True)
         img = torch.randn(B * V, 3, H, W, generator=torch.Generator().manual_seed(11))
-        sharded = DepthShardedMVSNet(net, world, rank, ops=_OracleOps)
+        sharded = DepthShardedMVSNet(net, world, rank, ops=_OracleOps, gather=False)
         with torch.no_grad():
             ini1, ref1, _ = mvs_oracle.mvsnet_forward(net, img, K, R, T, d_min, d_int, B, V, D,
                                                       (H // 4, W // 4))
             mine, ini, ref = sharded(img, K, R, T, d_min, d_int, B, V)
+            # the default: every sample's maps gathered on rank 0 (MVSNet.forward's return value there)
+            g_ini, g_ref = DepthShardedMVSNet(net, world, rank, ops=_OracleOps)(img, K, R, T, d_min, d_int, B, V)
         ok = True
         if mine:
             ok = (torch.allclose(ini, ini1[mine], rtol=1e-6, atol=0)
                   and torch.allclose(ref, ref1[mine], rtol=1e-5, atol=1e-3))
         else:
             ok = ini is None and ref is None
+        if rank == 0:
+            ok = ok and (tuple(g_ini.shape) == (B, 1, H // 4, W // 4) and torch.allclose(g_ini, ini1, rtol=1e-6, atol=0)
+                         and torch.allclose(g_ref, ref1, rtol=1e-5, atol=1e-3))
+            if mine:   # the gathered maps of rank 0's own samples are its own results, bit for bit
+                ok = ok and torch.equal(g_ini[mine], ini) and torch.equal(g_ref[mine], ref)
+        else:
+            ok = ok and g_ini is None and g_ref is None
         # inference-only: autograd enabled or train-mode BN must raise, not silently diverge
         raised = 0
         try:
