@@ -130,7 +130,8 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   const int nsteps = (z1 - z0) >> 1;   // D even (checked by the C ABI)
   const int nbatch = nsteps + 1;       // batch j = planes z0 - 1 + 2j, z0 + 2j
   const int ex = cv_split_exponent(a.absmax);
-  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the wave index through readfirstlane: role branches are scalar (s_cbranch_scc), not exec-masked
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool consumer = wave < 4;
 
   // conv_1_0 weight fragments -> LDS (every thread)
@@ -287,17 +288,25 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     acol[tx] = apart + c * kVoxB + ((g4 ^ ((c >> 1) & 3)) << 4);
   }
   f4 cur = {0.f, 0.f, 0.f, 0.f}, nxt = cur;
-  // acc += the 9 (ty, tx) taps of depth tap tz on plane slot sl (product wave's operands)
+  // acc += the 9 (ty, tx) taps of depth tap tz on plane slot sl (product wave's operands), in tap order;
+  // conv3d_s2_split.hip's pipeline: operands read two taps ahead into a register ring, the schedule
+  // pinned (sched_barrier) so no LDS read is re-targeted at registers an in-flight MFMA still reads
   auto mac1 = [&](f4& acc, int sl, int tz) {
     const char* base = ring + sl * kSlotB;
+    auto ld = [&](int t, h8v& x, h8v& wv) {
+      const int ty = t / 3, tx = t - 3 * (t / 3);
+      x = *reinterpret_cast<const h8v*>(base + (2 * jy + ty) * kRowB + acol[tx]);
+      wv = *reinterpret_cast<const h8v*>(w1l + (((tz * 9 + t) * 2 + bpart) * 64 + lane) * 16);
+    };
+    h8v xr[3], wr[3];
+    ld(0, xr[0], wr[0]);
+    ld(1, xr[1], wr[1]);
 #pragma unroll
-    for (int ty = 0; ty < 3; ++ty)
-#pragma unroll
-      for (int tx = 0; tx < 3; ++tx) {
-        const h8v x = *reinterpret_cast<const h8v*>(base + (2 * jy + ty) * kRowB + acol[tx]);
-        const h8v wv = *reinterpret_cast<const h8v*>(w1l + (((tz * 9 + ty * 3 + tx) * 2 + bpart) * 64 + lane) * 16);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, wv, acc, 0, 0, 0);
-      }
+    for (int t = 0; t < 9; ++t) {
+      if (t + 2 < 9) ld(t + 2, xr[(t + 2) % 3], wr[(t + 2) % 3]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xr[t % 3], wr[t % 3], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   };
   // wave 3: the completed window of depth start s from the partials in scratch buffer sb
   auto finish1 = [&](int s, int sb) {
@@ -408,19 +417,8 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
         mac1(cur, slot_of(z0 - 1), 0);
         mac1(cur, slot_of(z0), 1);
       }
-      {
-        const char* base = ring + slot_of(zs + 1) * kSlotB;
-#pragma unroll
-        for (int ty = 0; ty < 3; ++ty)
-#pragma unroll
-          for (int tx = 0; tx < 3; ++tx) {
-            const h8v x = *reinterpret_cast<const h8v*>(base + (2 * jy + ty) * kRowB + acol[tx]);
-            const h8v w2 = *reinterpret_cast<const h8v*>(w1l + (((18 + ty * 3 + tx) * 2 + bpart) * 64 + lane) * 16);
-            const h8v w0 = *reinterpret_cast<const h8v*>(w1l + (((ty * 3 + tx) * 2 + bpart) * 64 + lane) * 16);
-            cur = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, w2, cur, 0, 0, 0);
-            nxt = __builtin_amdgcn_mfma_f32_16x16x32_f16(x, w0, nxt, 0, 0, 0);
-          }
-      }
+      mac1(cur, slot_of(zs + 1), 2);   // completes window zs - 1
+      mac1(nxt, slot_of(zs + 1), 0);   // window zs + 1: depth taps 0, 1
       mac1(nxt, slot_of(zs + 2), 1);
       *reinterpret_cast<f4*>(scr + (((k & 1) * 3 + wave) * 64 + lane) * 16) = cur;
       cur = nxt;

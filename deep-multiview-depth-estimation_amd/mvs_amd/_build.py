@@ -36,7 +36,7 @@ def build_library(force=False, verbose=False, extra_flags=(), output=None):
         newest = max(os.path.getmtime(p) for p in SOURCES + HEADERS)
         if os.path.getmtime(out) >= newest:
             return out
-    cmd = [hipcc(), "-O3", "-std=c++17", "--offload-arch=%s" % ARCH, "-fPIC", "-shared",
+    cmd = [hipcc(), "-O3", "-std=c++17", "-Wno-pass-failed", "--offload-arch=%s" % ARCH, "-fPIC", "-shared",
            "-parallel-jobs=%d" % min(8, os.cpu_count() or 1), "-o", out + ".tmp"] + list(extra_flags) + SOURCES
     if verbose:
         print(" ".join(cmd))
