@@ -337,7 +337,8 @@ def masked_mae_loss(gt, initial, refined):
 def train_step_bench(B, V, D, H, W, device, steps):
     """One train.py:86-104 step on the drop-in at the headline workload: model.train(),
     optimizer.zero_grad, MVSNet.forward with autograd (BN batch statistics), the reference loss,
-    loss.backward() (HIP cost-volume backward + MIOpen for the convolutions), Adam.step over the
+    loss.backward() (HIP cost-volume backward + per-tap rocBLAS GEMMs for the convolutions, tap_gemm.py),
+    Adam.step over the
     reference's `model.parameters` list (train.py:160).  Synthetic ground truth: depths uniform over
     the plane range, 10 % invalid (0) pixels."""
     log("train step: B=%d V=%d D=%d %dx%d" % (B, V, D, W, H))
@@ -370,8 +371,9 @@ def train_step_bench(B, V, D, H, W, device, steps):
     out = {"B": B, "V": V, "planes": D, "image_hw": [H, W], "ms_per_step": 1000.0 * dt,
            "depth_maps_per_s": B / dt, "steps": n, "first_step_ms": 1000.0 * first,
            "loss": float(loss.item()), "peak_mem_GB": torch.cuda.max_memory_allocated(device) / 1e9,
-           "note": "forward (autograd, train-mode BN, full-volume regulariser on MIOpen) + loss.py "
-                   "masked MAE + backward (HIP mvs::cost_volume_backward, MIOpen conv backward) + "
+           "note": "forward (autograd, train-mode BN, full-volume regulariser as per-tap rocBLAS GEMMs, "
+                   "mvs_amd/tap_gemm.py) + loss.py masked MAE + backward (HIP mvs::cost_volume_backward, "
+                   "tap_gemm per-tap rocBLAS GEMM conv backward) + "
                    "Adam.step"}
     del net, opt
     torch.cuda.empty_cache()

@@ -206,22 +206,20 @@ struct Geometry {
   int total;  // flattened work items (B * tiles * Dc)
 };
 
-// Launch status of ONE entry point.  HIP's last-error slot is per thread and sticky: an error left
-// there before the call (a torch kernel, another library) belongs to whoever caused it and is
-// neither consumed nor reported here; an error that appears during the call is this call's own, is
-// consumed, and becomes MVS_ERR_HIP.  (Construct at entry, status() after the launches.)
+// Launch status of ONE entry point.  HIP's last-error slot is per thread and sticky.  An error left
+// there before the call (a torch kernel, another library) would otherwise mask this call's own:
+// comparing the slot before and after cannot tell a new failure with the same code from the old one.
+// So the slot is CLEARED at entry (the earlier error belonged to an earlier call, which had its chance
+// to read it; it is kept in prior() for diagnostics) and any error in it after the launches is this
+// call's own: consumed, and reported as MVS_ERR_HIP.  (Construct at entry, status() after the launches.)
 class LaunchCheck {
  public:
-  LaunchCheck() : before_(hipPeekAtLastError()) {}
-  int status() const {
-    const hipError_t now = hipPeekAtLastError();
-    if (now == hipSuccess || now == before_) return MVS_OK;
-    (void)hipGetLastError();
-    return MVS_ERR_HIP;
-  }
+  LaunchCheck() : prior_(hipGetLastError()) {}
+  int status() const { return hipGetLastError() == hipSuccess ? MVS_OK : MVS_ERR_HIP; }
+  hipError_t prior() const { return prior_; }
 
  private:
-  hipError_t before_;
+  hipError_t prior_;
 };
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }

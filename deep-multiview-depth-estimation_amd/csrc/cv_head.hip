@@ -31,6 +31,11 @@
 #include "split.h"
 
 #include <algorithm>
+#ifdef MVS_HEAD_STAMP
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#endif
 
 namespace mvs {
 namespace {
@@ -83,7 +88,14 @@ struct HeadArgs {
   int pad[3];                 // (z, y, x), odd
   int o0[3], on[3];           // conv_1_0 output region
   int r0[3], r1[3];           // SCV box [r0, r1)
+#ifdef MVS_HEAD_STAMP
+  unsigned long long* stamps;   // diagnostic build: [kStampWG][8 waves][kStampN] s_memtime stamps
+#endif
 };
+
+#ifdef MVS_HEAD_STAMP
+constexpr int kStampWG = 512, kStampN = 128;
+#endif
 
 __device__ inline float ror8(float v) {   // value of lane (l ^ 8) inside each 16-lane row
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
@@ -129,10 +141,28 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   const int z1 = min(z0 + kZC, D);
   const int nsteps = (z1 - z0) >> 1;   // D even (checked by the C ABI)
   const int nbatch = nsteps + 1;       // batch j = planes z0 - 1 + 2j, z0 + 2j
+#ifdef MVS_HEAD_ABL_E
+  if (x0 >= W || y0 >= H) return;
+#endif
   const int ex = cv_split_exponent(a.absmax);
   // the wave index through readfirstlane: role branches are scalar (s_cbranch_scc), not exec-masked
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool consumer = wave < 4;
+#ifdef MVS_HEAD_STAMP
+  // diagnostic: lane 0 of every wave of the first kStampWG workgroups stamps s_memtime at segment ends
+  unsigned long long* const stp = wk < kStampWG ? a.stamps + ((size_t)wk * 8 + wave) * kStampN : nullptr;
+  int sti = 0;
+  auto stamp = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (stp && lane == 0 && sti < kStampN) stp[sti] = t;
+    ++sti;
+  };
+#else
+  auto stamp = [&]() {};
+#endif
 
   // conv_1_0 weight fragments -> LDS (every thread)
   {
@@ -170,6 +200,22 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       ref[u] = f4v{r4.x, r4.y, r4.z, r4.w};
     }
   }
+  // plane-independent per-lane constants of the coordinate jobs: halo voxels lane and lane + 64, their
+  // kornia-normalised reference coordinates (norm_coord: two IEEE divisions each, formed once) and
+  // whether they lie in the image
+  float cxn[2] = {0.f, 0.f}, cyn[2] = {0.f, 0.f};
+  bool cin[2] = {false, false};
+  if (!consumer) {
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int v = lane + 64 * pass;
+      const int yy = v / kHX, xx = v - yy * kHX;
+      const int gx = x0 - 1 + xx, gy = y0 - 1 + yy;
+      cin[pass] = v < kHV && gx >= 0 && gx < W && gy >= 0 && gy < H;
+      cxn[pass] = norm_coord(cin[pass] ? gx : 0, W);
+      cyn[pass] = norm_coord(cin[pass] ? gy : 0, H);
+    }
+  }
   // sampling state of batch j's planes for every (plane, view, halo voxel) -> coordinate buffer tb
   auto coords = [&](int j, int tb) {
     const int pbase = z0 - 1 + 2 * j;
@@ -183,12 +229,9 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       for (int pass = 0; pass < 2; ++pass) {
         const int v = lane + 64 * pass;
         if (v < kHV) {
-          const int yy = v / kHX, xx = v - yy * kHX;
-          const int gx = x0 - 1 + xx, gy = y0 - 1 + yy;
-          const bool act = pok && gx >= 0 && gx < W && gy >= 0 && gy < H;
           uint32_t pos;
           float wx, wy;
-          src_coords(G, norm_coord(act ? gx : 0, W), norm_coord(act ? gy : 0, H), H, W, act, pos, wx, wy);
+          src_coords(G, cxn[pass], cyn[pass], H, W, pok && cin[pass], pos, wx, wy);
           const uint32_t off = pos == kInvalidTap ? kOobOffset
                                                   : ((uint32_t)(pos_y(pos) + 1) * (uint32_t)pg.pitch +
                                                      (uint32_t)(pos_x(pos) + 1)) * pstride;
@@ -201,55 +244,183 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
   const Rsrc rscv = make_rsrc(a.scv ? static_cast<char*>(a.scv) + (size_t)b * kC4 * D * HW * 16 : nullptr,
                               a.scv ? (uint32_t)min((uint64_t)kC4 * D * HW * 16ull, 0xFFFFFFF0ull) : 0u);
-  // variance of batch j's two planes -> ring slots (and the SCV box)
-  auto items = [&](int j, int tb) {
-    const int pbase = z0 - 1 + 2 * j;
+  // variance of batch j's two planes -> ring slots (and the SCV box).  Software-pipelined so the
+  // gathers of several items are in flight together: item u + kAhead's sampling state (LDS) and 4
+  // taps x NS views are issued before item u is reduced (each wave keeps up to (kAhead + 1) x 4 x NS
+  // 16-byte gathers in flight, waited by counted vmcnt)
+#ifdef MVS_HEAD_KA
+  constexpr int kAhead = MVS_HEAD_KA;
+#else
+  constexpr int kAhead = 2;
+#endif
+  // per-item constants (the same every batch), packed: LDS offset inside a ring slot (bits 0-12), in
+  // the image (13), stored to the SCV box in (y, x) (14), plane of the batch (15), quad (16-18), halo
+  // voxel (19-25); and the item's SCV byte offset at plane 0
+  uint32_t meta[kItems], sbase[kItems];
+  if (!consumer) {
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
-      const int e = ptid + 256 * u;
-      if (e >= kBatchItems) break;   // wave-uniform (last pass: waves 4-6 only)
+      const int e = min(ptid + 256 * u, kBatchItems - 1);
       const int pl = e >= kPlaneItems ? 1 : 0;
       const int r = e - pl * kPlaneItems;
       const int v = r >> 3, q = r & 7;
       const int yy = v / kHX, xx = v - yy * kHX;
-      const int p = pbase + pl;
       const int gx = x0 - 1 + xx, gy = y0 - 1 + yy;
-      const bool valid = p >= 0 && p < D && gx >= 0 && gx < W && gy >= 0 && gy < H;
-      f4v xs[NS];
+      const bool vin = gx >= 0 && gx < W && gy >= 0 && gy < H;
+      const bool sxy = vin && xx >= 1 && xx <= kTX && yy >= 1 && yy <= kTY && gy >= a.r0[1] && gy < a.r1[1] &&
+                       gx >= a.r0[2] && gx < a.r1[2];
+      const uint32_t lo = (uint32_t)(yy * kRowB + xx * kVoxB + (((q >> 1) ^ ((xx >> 1) & 3)) << 4) + ((q & 1) << 3));
+      meta[u] = lo | ((uint32_t)vin << 13) | ((uint32_t)sxy << 14) | ((uint32_t)pl << 15) | ((uint32_t)q << 16) |
+                ((uint32_t)v << 19);
+      sbase[u] = vin ? (uint32_t)(((size_t)q * D * HW + (size_t)gy * W + gx) * 16) : 0u;
+    }
+  }
+  const uint32_t plane_b = (uint32_t)HW * 16u;   // SCV bytes per plane
+  const int zst0 = max(z0, a.r0[0]), zst1 = min(z1, a.r1[0]);   // planes stored to the SCV box
+  auto items = [&](int j, int tb) {
+    const int pbase = z0 - 1 + 2 * j;
+    const int sl0 = slot_of(pbase);   // even: the batch's second plane is the next slot
+    const int nu = ptid + 256 * (kItems - 1) < kBatchItems ? kItems : kItems - 1;   // wave-uniform
+    f4v tp[kAhead + 1][NS][4];
+    float fx[kAhead + 1][NS], fy[kAhead + 1][NS];
+    // item u's sampling state, read from LDS one item before its gathers are issued (the LDS round
+    // trip off the gather issue path)
+    uint32_t co[2][NS];
+    float cx[2][NS], cy[2][NS];
+    auto rdc = [&](int u) {
+      const uint32_t m = meta[u];
+      const int pl = (m >> 15) & 1, v = (int)(m >> 19);
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         const uint4 ce = *reinterpret_cast<const uint4*>(coord + (((tb * 2 + pl) * NS + s) * kHV + v) * 16);
-        const uint32_t o = ce.x + (uint32_t)q * 16u;
-        f4v tp[4];
-        tp[0] = ld4(rsv[s], o, 0);
-        tp[1] = ld4(rsv[s], o + pstride, 0);
-        tp[2] = ld4(rsv[s], o + (uint32_t)pg.pitch * pstride, 0);
-        tp[3] = ld4(rsv[s], o + (uint32_t)pg.pitch * pstride + pstride, 0);
-        xs[s] = bilerp(tp, __uint_as_float(ce.y), __uint_as_float(ce.z));
+        co[u & 1][s] = ce.x;
+        cx[u & 1][s] = __uint_as_float(ce.y);
+        cy[u & 1][s] = __uint_as_float(ce.z);
       }
+    };
+    auto issue = [&](int u) {   // item u's 4 x NS tap gathers (its sampling state read by rdc(u))
+      const int rr = u % (kAhead + 1);
+      const uint32_t qo = ((meta[u] >> 16) & 7) * 16u;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const uint32_t o = co[u & 1][s] + qo;
+        fx[rr][s] = cx[u & 1][s];
+        fy[rr][s] = cy[u & 1][s];
+#ifdef MVS_HEAD_ABL_G
+        {
+          const float f = __uint_as_float(o);
+          tp[rr][s][0] = f4v{f, f, f, f};
+          tp[rr][s][1] = f4v{f, 1.f, f, f};
+          tp[rr][s][2] = f4v{f, f, 2.f, f};
+          tp[rr][s][3] = f4v{f, f, f, 3.f};
+        }
+#else
+        tp[rr][s][0] = ld4(rsv[s], o, 0);
+        tp[rr][s][1] = ld4(rsv[s], o + pstride, 0);
+        tp[rr][s][2] = ld4(rsv[s], o + (uint32_t)pg.pitch * pstride, 0);
+        tp[rr][s][3] = ld4(rsv[s], o + (uint32_t)pg.pitch * pstride + pstride, 0);
+#endif
+      }
+    };
+    // items that exist for this wave: u < nu (wave-uniform)
+    auto has = [&](int u) { return u < kItems - 1 || (u == kItems - 1 && nu == kItems); };
+    rdc(0);
+#pragma unroll
+    for (int u = 0; u < kAhead; ++u) {
+      if (has(u + 1)) rdc(u + 1);
+      issue(u);
+    }
+#ifdef MVS_HEAD_FIX_KEEP
+    uint32_t kaddr = 0;
+    uint2 khi = make_uint2(0u, 0u), klo = khi;
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < kItems; ++u) {
+      if (!has(u)) break;   // wave-uniform (the last pass: waves 4-6 only)
+      if (has(u + kAhead)) {
+        if (has(u + kAhead + 1)) rdc(u + kAhead + 1);
+        issue(u + kAhead);
+      }
+      const uint32_t m = meta[u];
+      const int pl = (m >> 15) & 1;
+      const int p = pbase + pl;
+      const bool valid = (m & (1u << 13)) && (unsigned)p < (unsigned)D;
+      const int rr = u % (kAhead + 1);
+      f4v xs[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) xs[s] = bilerp(tp[rr][s], fx[rr][s], fy[rr][s]);
       const f4v acc = head_variance4<NS>(ref[u], xs, inv_v);
       uint2 hi, lo;
       split4(acc, ex, hi, lo);
       if (!valid) hi = lo = make_uint2(0u, 0u);
-      char* dst = ring + slot_of(p) * kSlotB + yy * kRowB + xx * kVoxB + ((((q >> 1) ^ ((xx >> 1) & 3))) << 4) +
-                  ((q & 1) << 3);
+      char* dst = ring + (sl0 + pl) * kSlotB + (m & 0x1FFFu);
+#ifdef MVS_HEAD_FIX_KEEP
+      asm volatile("" ::"v"(kaddr), "v"(khi.x), "v"(khi.y), "v"(klo.x), "v"(klo.y));
+#endif
       *reinterpret_cast<uint2*>(dst) = hi;
       *reinterpret_cast<uint2*>(dst + kPartB) = lo;
+#ifdef MVS_HEAD_FIX_KEEP
+      kaddr = (uint32_t)(uintptr_t)dst;
+      khi = hi;
+      klo = lo;
+#endif
+#ifdef MVS_HEAD_FIX_WAIT
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
       // conv_2_0 / conv_3_0 read the SCV on their input box: the tile-interior voxels of this chunk's
       // planes (every in-volume voxel is interior to exactly one tile and one chunk)
-      const bool st = valid && xx >= 1 && xx <= kTX && yy >= 1 && yy <= kTY && p >= z0 && p < z1 &&
-                      p >= a.r0[0] && p < a.r1[0] && gy >= a.r0[1] && gy < a.r1[1] && gx >= a.r0[2] && gx < a.r1[2];
+      const bool st = (m & (1u << 14)) && p >= zst0 && p < zst1;
       typedef __attribute__((ext_vector_type(4))) unsigned v4u;
-      const uint32_t so = st ? (uint32_t)((((size_t)q * D + p) * HW + (size_t)gy * W + gx) * 16) : kOobOffset;
-      __builtin_amdgcn_raw_buffer_store_b128(v4u{hi.x, hi.y, lo.x, lo.y}, rscv, (int)so, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(v4u{hi.x, hi.y, lo.x, lo.y}, rscv,
+                                             (int)(st ? sbase[u] + (uint32_t)p * plane_b : kOobOffset), 0, 0);
+      // one item per scheduling region: without it the scheduler hoists every item's loads to the
+      // top (all 7 items' gathers live at once: VGPR spills)
+      __builtin_amdgcn_sched_barrier(0);
     }
+#ifdef MVS_HEAD_FIX_KEEP
+    asm volatile("" ::"v"(kaddr), "v"(khi.x), "v"(khi.y), "v"(klo.x), "v"(klo.y));
+#endif
   };
 
+  // ================================ schedule ================================
+  // Both roles pass the same barriers (nsteps + 3): producers fill batches 0, 1 before step 0 and batch
+  // k + 2 during step k; the sampling state of a batch is formed at least one barrier before its items.
+  if (!consumer) {
+#ifdef MVS_HEAD_PRIO
+    __builtin_amdgcn_s_setprio(MVS_HEAD_PRIO);
+#endif
+    stamp();
+    coords(0, 0);
+    coords(1, 1);
+    stamp();
+    __syncthreads();
+    stamp();
+    items(0, 0);
+    items(1, 1);
+    stamp();
+    __syncthreads();
+    stamp();
+    if (2 < nbatch) coords(2, 0);   // buffer 0 is free again (batch 0's items are done)
+    stamp();
+    __syncthreads();
+    stamp();
+    for (int k = 0; k < nsteps; ++k) {
+      if (k + 2 < nbatch) items(k + 2, (k + 2) & 1);
+      stamp();
+      if (k + 3 < nbatch) coords(k + 3, (k + 3) & 1);
+      stamp();
+      __syncthreads();
+      stamp();
+    }
+    __syncthreads();
+    return;
+  }
   // ================================ consumer state ================================
   const int i16 = lane & 15, g4 = lane >> 4;
   h8v bw[27];
   float sc0 = 1.0f, sh0 = 0.0f, mu0 = 0.0f, sc1 = 1.0f, sh1 = 0.0f, mu1 = 0.0f;
-  if (consumer) {
+  {
     const Rsrc rwf = make_rsrc(a.w0, 27u * 64u * 16u);
 #pragma unroll
     for (int tp = 0; tp < 27; ++tp)
@@ -327,33 +498,24 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     }
   };
 
-  // ================================ schedule ================================
-  // Both roles pass the same barriers (nsteps + 3): producers fill batches 0, 1 before step 0 and batch
-  // k + 2 during step k; the sampling state of a batch is formed at least one barrier before its items.
-  if (!consumer) {
-    coords(0, 0);
-    coords(1, 1);
-    __syncthreads();
-    items(0, 0);
-    items(1, 1);
-    __syncthreads();
-    if (2 < nbatch) coords(2, 0);   // buffer 0 is free again (batch 0's items are done)
-    __syncthreads();
-    for (int k = 0; k < nsteps; ++k) {
-      if (k + 2 < nbatch) items(k + 2, (k + 2) & 1);
-      if (k + 3 < nbatch) coords(k + 3, (k + 3) & 1);
-      __syncthreads();
-    }
-    __syncthreads();
-    return;
-  }
+  stamp();
+  stamp();
   __syncthreads();
+  stamp();
+  stamp();
   __syncthreads();
+  stamp();
+  stamp();
   __syncthreads();
+  stamp();
   for (int k = 0; k < nsteps; ++k) {
     const int zs = z0 + 2 * k;
     // ---- conv_0_0 on planes zs - 1 .. zs + 2 (conv3d_split.hip's item order) ----
+#ifdef MVS_HEAD_ABL_C
+    if (false) {
+#else
     if (row_on) {
+#endif
       f4 ah[2], al[2];
 #pragma unroll
       for (int d = 0; d < 2; ++d) {
@@ -411,8 +573,13 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
         }
       }
     }
+    stamp();
     // ---- conv_1_0: window zs - 1 completes (depth tap 2 on plane zs + 1), window zs + 1 starts ----
+#ifdef MVS_HEAD_ABL_C
+    if (false) {
+#else
     if (wave < 3) {
+#endif
       if (k == 0) {
         mac1(cur, slot_of(z0 - 1), 0);
         mac1(cur, slot_of(z0), 1);
@@ -426,7 +593,9 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     } else if (k > 0) {
       finish1(zs - 3, (k - 1) & 1);   // the window completed in step k - 1
     }
+    stamp();
     __syncthreads();
+    stamp();
   }
   // the last step's window; the last chunk also owns the window starting at D - 1 (its taps on
   // planes D, D + 1 are zero: complete after the last step)
@@ -534,12 +703,30 @@ int launch_cv_head(const Geometry& g, const float* feat, const Cams& cm, float* 
     a.r0[d] = r0[d];
     a.r1[d] = r1[d];
   }
+#ifdef MVS_HEAD_STAMP
+  static unsigned long long* stamps = nullptr;
+  const size_t stamp_bytes = (size_t)kStampWG * 8 * kStampN * sizeof(unsigned long long);
+  if (!stamps) (void)hipMalloc(&stamps, stamp_bytes);
+  (void)hipMemsetAsync(stamps, 0, stamp_bytes, s);
+  a.stamps = stamps;
+#endif
   if (ev0) (void)hipEventRecord(ev0, s);
   if (g.V == 2)
     hipLaunchKernelGGL(cv_head_kernel<2>, xcd_grid(a.total), dim3(kThreads), 0, s, a);
   else
     hipLaunchKernelGGL(cv_head_kernel<3>, xcd_grid(a.total), dim3(kThreads), 0, s, a);
   if (ev1) (void)hipEventRecord(ev1, s);
+#ifdef MVS_HEAD_STAMP
+  if (const char* path = getenv("MVS_HEAD_STAMPS")) {   // diagnostic build only: synchronous dump
+    std::vector<unsigned long long> h(stamp_bytes / sizeof(unsigned long long));
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h.data(), stamps, stamp_bytes, hipMemcpyDeviceToHost);
+    if (FILE* f = fopen(path, "ab")) {
+      fwrite(h.data(), 1, stamp_bytes, f);
+      fclose(f);
+    }
+  }
+#endif
   // faces: per dim, region outputs whose window start 2 o - P lies below -1 (before tile 0) or at /
   // beyond the last owned start (n_tiles * tile - 1 in x / y, D - 1 + 2 in z)
   int lo[3], hi[3];

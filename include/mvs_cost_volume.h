@@ -34,7 +34,10 @@ extern "C" {
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
 #define MVS_ERR_UNSUPPORTED_VIEWS (-2) /* n_views outside [1, MVS_MAX_VIEWS]               */
 #define MVS_ERR_TOO_LARGE (-3)         /* a tensor exceeds the kernel's 32-bit index space */
-#define MVS_ERR_HIP (-4)               /* a HIP launch/runtime error (see hipGetLastError)  */
+#define MVS_ERR_HIP (-4)               /* a HIP launch/runtime error of THIS call (the thread's HIP
+                                        last-error slot is cleared on entry, then read after the
+                                        launches: an error pending from an earlier call is not
+                                        reported as this call's, nor can it mask this call's)  */
 
 #define MVS_MAX_VIEWS 16
 

@@ -1,0 +1,98 @@
+"""The CPU fp32 oracle at cfg 5, precomputed.
+
+test_gpu_configs.py::test_model_end_to_end_at_cfg3_cfg5[cfg5] checks the benchmarked path against a
+GPU restatement of the reference sequence (forward_live's torch branch on per-tap GEMMs: MIOpen is
+too slow there).  This script runs the ORACLE itself -- oracle/mvs_oracle.py's homography_warping
+(concat_growth=False: the same values as the reference's growing torch.cat, test speed) ->
+assemble_cost_volume -> CostVolumeReg.forward_full (model.py:100-126) -> extract_depth_map
+(depthmap.py:4-22) -- on the CPU, in fp32, at cfg 5 (B=1, V=3, 1600x1184 images -> 296x400 features,
+D=256, eval BN) on the test's weights and seed-2001 images, and commits
+
+  cfg5_oracle.npz   ini [296,400] f32       initial depth
+                    keep [5,296,400] u8     the kept planes (ascending; ties by ascending plane index)
+                    sig [5,296,400] bool    their P >= 1e-7 (make_cfg2_selfnoise.significant_flips)
+                    tie [296,400] bool      pixels whose mask is tie-ambiguous under torch.sort
+                    pz, py, px [4096] i16   4,096 sampled probability voxels (seed 5) ...
+                    pv [4096] f32           ... and their probabilities
+
+The variance is formed in depth chunks of assemble_cost_volume's own expression (elementwise per
+voxel, so bit-identical to the one-shot call) to keep the peak near 25 GB; ~15 min on 8 cores.
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_cfg5_oracle.py
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+for sub in ("deep-multiview-depth-estimation_amd", "oracle", os.path.join("tests", "golden")):
+    if os.path.join(REPO, sub) not in sys.path:
+        sys.path.insert(0, os.path.join(REPO, sub))
+
+OUT = os.path.join(HERE, "cfg5_oracle.npz")
+GEOM = (1, 3, 256, 1184, 1600)   # B, V, D, image H, W
+N_SAMPLES = 4096
+
+
+def cfg5_inputs():
+    """(net [CPU, eval], img, K, R, T, d_min, d_int) exactly as test_model_end_to_end_at_cfg3_cfg5[cfg5]."""
+    from cameras import camera_batch, depth_range
+    from weights import deterministic_state_dict
+    from mvs_amd.config import MVSConfig
+    from mvs_amd.model import MVSNet
+    B, V, D, H, W = GEOM
+    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W), device=torch.device("cpu"))
+    net.load_state_dict(deterministic_state_dict(net.state_dict()))
+    net.eval()
+    K, R, T = camera_batch(B, V, H // 4, W // 4)
+    d_min, d_int = depth_range(B)
+    img = torch.randn(B * V, 3, H, W, generator=torch.Generator().manual_seed(2000 + B))
+    return net, img, K, R, T, d_min, d_int
+
+
+def sample_voxels(D, h, w, n=N_SAMPLES, seed=5):
+    rng = np.random.default_rng(seed)
+    return (rng.integers(0, D, n).astype(np.int16), rng.integers(0, h, n).astype(np.int16),
+            rng.integers(0, w, n).astype(np.int16))
+
+
+def main():
+    import mvs_oracle
+    from make_cfg2_selfnoise import SIG_P, kept_with_p, kept_planes
+    B, V, D, H, W = GEOM
+    h, w = H // 4, W // 4
+    torch.set_num_threads(os.cpu_count() or 8)
+    net, img, K, R, T, d_min, d_int = cfg5_inputs()
+    t0 = time.time()
+    with torch.no_grad():
+        feats = net.feature_encoder(img)
+        warped, d_batch, _ = mvs_oracle.homography_warping(K, R, T, d_min, d_int, feats, B, V, D,
+                                                           concat_growth=False)
+        print("warp %.0f s" % (time.time() - t0), flush=True)
+        x = warped.reshape(B, V, 32, D, h, w)
+        cv = torch.empty((B, 32, D, h, w))
+        for d0 in range(0, D, 16):   # assemble_cost_volume (costvolume.py:3-16) per depth chunk
+            xs = x[:, :, :, d0:d0 + 16]
+            cv[:, :, d0:d0 + 16] = mvs_oracle.assemble_cost_volume(
+                xs.reshape((B * V,) + xs.shape[2:]), V)
+        del warped, x, xs
+        print("cost volume %.0f s" % (time.time() - t0), flush=True)
+        prob = net.cost_volume_reg.forward_full(cv)
+        del cv
+        print("regulariser %.0f s" % (time.time() - t0), flush=True)
+        ini = mvs_oracle.extract_depth_map(prob, d_batch)
+    P = prob[0, 0].numpy()
+    keep, p = kept_with_p(P)
+    tie = (kept_planes(P, stable=False) != keep).any(0)
+    pz, py, px = sample_voxels(D, h, w)
+    np.savez_compressed(OUT, ini=ini[0, 0].numpy().astype(np.float32), keep=keep, sig=p >= SIG_P, tie=tie,
+                        pz=pz, py=py, px=px, pv=P[pz, py, px].astype(np.float32))
+    print("tie pixels %.4f %%; wrote %s (%d bytes), %.0f s" % (100 * tie.mean(), OUT, os.path.getsize(OUT),
+                                                          time.time() - t0))
+
+
+if __name__ == "__main__":
+    main()

@@ -261,6 +261,59 @@ def test_cfg2_end_to_end_as_benchmarked():
     assert rel_r.max() <= 1e-4, rel_r.max()
 
 
+
+def test_cfg2_depth_flips_within_reference_self_noise():
+    """cfg 2's depth against the float64 law, with the reference's OWN fp32 noise as the yardstick
+    (tests/golden/make_cfg2_selfnoise.py: the CPU fp32 oracle and mvs_oracle.mvsnet_forward64 on the
+    same weights / images, committed).  The benchmarked call (MVSNet.forward: fused head, split-fp16
+    conv_0_0 / conv_1_0, HIP soft-argmin) is run on all 4 samples; with its probability volume (the
+    regulariser's output, captured by a forward hook):
+
+      * GPU-vs-f64 mask flips (the depthmap.py:11-15 kept-plane sets differ in a plane that carries
+        weight, P >= 1e-7: swaps among the fp32 softmax's exact zeros move no depth) <= 1.5 x the
+        CPU fp32 oracle's own flips against f64 (+ 0.05 % of the pixels, for samples where the CPU
+        flips on almost none: sample 0 flips 0.04 %), per sample;
+      * on the pixels unflipped against f64: the fraction within 1e-4 relative of the f64 depth is no
+        worse than the CPU oracle's own (99.10-99.32 %) by more than 0.1 percentage point, and the
+        worst relative error <= 1.5 x the CPU oracle's worst (5-9 %: the f64 law is free of the
+        reference's fp32 homography rounding, so "every unflipped pixel within 1e-4" does not hold
+        for the reference itself -- DESIGN.md §4)."""
+    import os
+    from conftest import record_parity
+    from make_cfg2_selfnoise import GEOM, cfg2_inputs, kept_with_p, significant_flips
+    fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cfg2_selfnoise.npz"))
+    B, V, D, H, W = GEOM
+    net, img, K, R, T, d_min, d_int = cfg2_inputs()
+    g = net.to(DEV)
+    probs = []
+    hook = g.cost_volume_reg.register_forward_hook(lambda m, i, o: probs.append(o.detach()))
+    try:
+        with torch.no_grad():
+            ini, _ = g(img.to(DEV), K, R, T, d_min, d_int, B, V)
+    finally:
+        hook.remove()
+    assert len(probs) == 1
+    P = probs[0].cpu().numpy()
+    ini = ini.cpu().numpy()
+    flips, within, worst = [], [], []
+    for b in range(B):
+        kg, pg = kept_with_p(P[b, 0])
+        flip = significant_flips(kg, pg, fx["keep64"][b], fx["sig64"][b].astype(np.float32))
+        rel = np.abs(ini[b, 0].astype(np.float64) - fx["ini64"][b]) / np.abs(fx["ini64"][b])
+        flips.append(float(flip.mean()))
+        within.append(float((rel[~flip] <= 1e-4).mean()))
+        worst.append(float(rel[~flip].max()))
+    cpu_flip, cpu_within, cpu_worst = (fx["cpu_flip_frac"], fx["cpu_within_1e4_unflipped"],
+                                       fx["cpu_max_rel_unflipped"])
+    record_parity("cfg2_vs_float64_law", samples=B, gpu_flip_frac=flips, cpu_fp32_flip_frac=cpu_flip.tolist(),
+                  gpu_within_1e4_unflipped=within, cpu_fp32_within_1e4_unflipped=cpu_within.tolist(),
+                  gpu_max_rel_unflipped=worst, cpu_fp32_max_rel_unflipped=cpu_worst.tolist())
+    for b in range(B):
+        assert flips[b] <= 1.5 * cpu_flip[b] + 5e-4, (b, flips[b], cpu_flip[b])
+        assert within[b] >= cpu_within[b] - 1e-3, (b, within[b], cpu_within[b])
+        assert worst[b] <= 1.5 * cpu_worst[b], (b, worst[b], cpu_worst[b])
+
+
 E2E_CFGS = {   # BASELINE.json configs[2] and configs[4]: (B, V, D, image H, image W)
     "cfg3": (8, 5, 192, 512, 640),
     "cfg5": (1, 3, 256, 1184, 1600),
@@ -342,6 +395,26 @@ def test_model_end_to_end_at_cfg3_cfg5(cfg):
                   within_1e4_frac_unflipped=within_unflipped, tie_pixel_frac=float(ties.mean()),
                   soft_argmin_vs_oracle_max_rel_untied=float(sa_rel[~ties].max()),
                   **_prob_diff(P_live, P_full))
+    if cfg == "cfg5":
+        # and against the CPU fp32 ORACLE itself (tests/golden/make_cfg5_oracle.py: homography_warping
+        # -> assemble_cost_volume -> forward_full -> extract_depth_map on the CPU, committed): mask
+        # flips counted on weight-carrying planes (P >= 1e-7; tie-ambiguous oracle pixels included),
+        # the unflipped pixels' depth within 1e-4, 4,096 sampled probabilities within 2e-3
+        import os
+        from make_cfg2_selfnoise import kept_with_p, significant_flips
+        fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cfg5_oracle.npz"))
+        kg, pgv = kept_with_p(Pl[0, 0].numpy())
+        flip_o = significant_flips(kg, pgv, fx["keep"], fx["sig"].astype(np.float32)) | fx["tie"]
+        rel_o = np.abs(g_ini[0, 0].astype(np.float64) - fx["ini"]) / np.abs(fx["ini"].astype(np.float64))
+        pv = Pl[0, 0].numpy()[fx["pz"].astype(np.int64), fx["py"].astype(np.int64), fx["px"].astype(np.int64)]
+        p_rel = np.abs(pv - fx["pv"]) / np.maximum(np.abs(fx["pv"]), 1e-8 / 2e-3)
+        record_parity("cfg5_e2e_vs_cpu_oracle", mask_flip_frac=float(flip_o.mean()),
+                      within_1e4_frac_unflipped=float((rel_o[~flip_o] <= 1e-4).mean()),
+                      max_rel_unflipped=float(rel_o[~flip_o].max()), sampled_p_max_rel=float(p_rel.max()),
+                      oracle_tie_pixel_frac=float(fx["tie"].mean()))
+        assert flip_o.mean() < 0.02, flip_o.mean()
+        assert (rel_o[~flip_o] <= 1e-4).mean() >= 0.9995, (rel_o[~flip_o] <= 1e-4).mean()
+        np.testing.assert_allclose(pv, fx["pv"], rtol=2e-3, atol=1e-8)
     assert torch.isfinite(ini).all() and torch.isfinite(ref).all()
     assert torch.equal(ini_live, ini)
     torch.testing.assert_close(P_live, P_full, rtol=1e-4, atol=1e-9)

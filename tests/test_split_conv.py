@@ -128,6 +128,53 @@ def test_split_conv_magnitudes(mag):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("small", [1e-6, 1e-8])
+def test_split_conv_dynamic_range(small):
+    """One volume, two dynamic ranges: depth planes 0-5 at scale 1, planes 6-11 at `small` x that
+    (the split's power-of-two scale is set by the volume's bound, so the small region's values sit
+    near fp16's subnormal range).  Per output region, split vs float64, exact fp32 (conv3d_k3) and
+    MIOpen vs float64.  The split's element contract:
+
+        |x - (hi + lo) 2^-e| <= 2^-22 |x| + 2^-25 2^-e,   2^-e <= B^2 2^-12   (B = the bound word)
+
+    -- fp32-level relative error down to ~1e-5 of the volume's bound, an ABSOLUTE floor of
+    B^2 2^-37 (7e-12 B^2) below.  Asserted: the large region at fp32 level (as every other test
+    here); in the small region the error within the contract's propagated bound
+    sum_taps |w| (2^-22 max|x| + 2^-37 B^2) + the fp32 kernels' own error, and the measured
+    relative errors recorded."""
+    from conftest import record_parity
+    from mvs_amd.ops import conv3d_k3, conv3d_k3_split
+    g = torch.Generator().manual_seed(71)
+    x = torch.rand(1, 32, 12, 16, 40, generator=g)
+    x[:, :, 6:] *= small
+    wt = torch.randn(8, 32, 3, 3, 3, generator=g) * 0.05
+    words = _bound_words(x)
+    bound2 = float(np.frombuffer(np.int32(words[3].item()).tobytes(), dtype=np.float32)[0]) ** 2
+    ref64 = torch.nn.functional.conv3d(x.double(), wt.double(), padding=1)
+    with torch.no_grad():
+        xc = _to_c4(x).to(DEV)
+        y = conv3d_k3_split(xc, words.to(DEV), wt.to(DEV)).cpu().double()
+        y32 = conv3d_k3(xc, wt.to(DEV), in_c4=True).cpu().double()
+        yt = torch.nn.functional.conv3d(x.to(DEV), wt.to(DEV), padding=1).cpu().double()
+    big, sm = (slice(None), slice(None), slice(0, 5)), (slice(None), slice(None), slice(7, 12))
+    out = {}
+    for name, r in (("large", big), ("small", sm)):
+        scale = ref64[r].abs().max().item()
+        e_s, e_32, e_t = ((v[r] - ref64[r]).abs().max().item() for v in (y, y32, yt))
+        out[name] = dict(scale=scale, split_rel=e_s / scale, fp32_kernel_rel=e_32 / scale, miopen_rel=e_t / scale)
+        print("%s region (x %g): split %.3g, fp32 kernel %.3g, MIOpen %.3g relative to %.3g" % (
+            name, 1.0 if name == "large" else small, e_s / scale, e_32 / scale, e_t / scale, scale))
+        if name == "large":
+            assert e_s <= 1e-5 * scale and e_s <= 1.5 * max(e_32, e_t) + 1e-7 * scale, out[name]
+        else:
+            sw = wt.double().abs().sum((1, 2, 3, 4)).max().item()
+            contract = sw * (2.0 ** -22 * x[:, :, 6:].abs().max().item() + 2.0 ** -37 * bound2)
+            out[name]["contract_bound"] = contract / scale
+            assert e_s <= contract + 2 * max(e_32, e_t), out[name]
+    record_parity("split_dynamic_range_%g" % small, **out)
+
+
+@pytest.mark.gpu
 def test_split_conv_unscaled_small_values():
     """absmax = None: unscaled (values < 2^15 by contract)."""
     g = torch.Generator().manual_seed(3)
