@@ -16,10 +16,15 @@ D-slab, and each sample's slab goes point to point (RCCL send/recv over xGMI,
 mvs_amd/depth_shards.py) to the rank that owns the sample, which runs the regulariser.
 
 Also reported (one JSON line, rank 0):
-  roofline      the fused kernel (cost_volume_staged_kernel): algorithmic bytes per launch
-                (4*B*V*C*h*w features read once + 4*B*C*D*h*w cost volume written once) / average
-                launch time measured with HIP events on the launch stream, vs 8 TB/s HBM peak;
-                traffic = PMC HBM bytes from profiles/ (rocprofv3 --pmc, FETCH_SIZE x2 on gfx950)
+  roofline      the step's dominant kernel, the fused head (cv_head_kernel: the cost volume formed on
+                chip and consumed by conv_0_0 + conv_1_0): executed f16 MFMA flops per
+                launch / its average launch time (HIP events on the launch stream inside the timed
+                steps) vs the 2.5 PF dense f16 peak; beside it the fp32 convolution flops it computes
+                and its algorithmic HBM bytes (no cost volume round trip: features in, y0 / y1 / the
+                conv_2_0 box out); traffic = PMC HBM bytes from profiles/ when measured
+  warp_kernel   the standalone fused warp + variance kernel (cost_volume_staged_kernel, channel-quad
+                split store): algorithmic bytes (features read once + cost volume written once) /
+                launch time vs 8 TB/s -- the metric's "warp-kernel HBM GB/s"; traffic = PMC bytes
   cpu_baseline  the oracle (oracle/mvs_oracle.py: the reference's op sequence in torch CPU,
                 per-plane warp loop with torch.cat growth) on ONE sample of the same workload
   hot_path      cost volumes/s of the fused kernel alone
@@ -49,6 +54,8 @@ from cameras import camera_batch, depth_range  # noqa: E402
 from weights import deterministic_state_dict  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFMA_F16_PEAK_TFS = 2500.0   # MI355X_MICROARCH.md: BF16/F16 ~2.5 PF dense
+MFMA_F32_PEAK_TFS = 157.3    # f32-input MFMA = f32 vector peak
 _T0 = time.perf_counter()
 
 
@@ -380,6 +387,39 @@ def train_step_bench(B, V, D, H, W, device, steps):
     return out
 
 
+def head_work(B, V, D, h, w):
+    """Work of one cv_head launch at the eval step's regions (CostVolumeReg.forward_live_head):
+    executed f16 MFMA flops, the fp32 convolution flops they compute (model.py:101,103), and the
+    algorithmic HBM bytes (pixel-major padded features + resampled reference views read once; y0,
+    the conv_1_0 window region and the split cost volume on conv_2_0's input box written once)."""
+    from mvs_amd import model as M
+    from mvs_amd.config import pad_outpad
+    n = (D, h, w)
+    pad = pad_outpad(D, h, w)[0]
+    full = tuple((0, d - 1) for d in n)
+    b_reg = M._tconv_input_region(full, n, pad)
+    c2 = M._tconv_input_region(b_reg, n, pad)
+    h1, h2 = M._grow(b_reg, n, 1), M._grow(c2, n, 1)
+    lo = [max(2 * a - p, 0) for (a, _), p in zip(h2, pad)]
+    hi = [min(2 * b - p + 2, d - 1) + 1 for (_, b), p, d in zip(h2, pad, n)]
+    vox = D * h * w
+    win = int(np.prod([b - a + 1 for a, b in h1]))
+    box = int(np.prod([b - a for a, b in zip(lo, hi)]))
+    return {"mfma_flops": B * (vox * 55296 + win * 82944),
+            "alg_flops": B * (vox * 8 * 32 * 27 * 2 + win * 16 * 32 * 27 * 2),
+            "hbm_bytes": B * V * (h + 2) * (w + 2) * 128 + B * h * w * 128 + B * (vox * 8 * 4 + win * 16 * 4 + box * 8 * 16),
+            "regions": {"conv_1_0_windows": list(h1), "scv_box": [lo, hi]}}
+
+
+def head_traffic(tag):
+    """PMC HBM bytes per cv_head launch (profiles/, rocprofv3 --pmc), or None."""
+    path = os.path.join(REPO, "profiles", "head_traffic_%s.json" % tag)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
+
+
 def load_traffic(tag):
     p = os.path.join(REPO, "profiles", "traffic_%s.json" % tag)
     if os.path.exists(p):
@@ -504,11 +544,11 @@ def main():
         step_events = []
         stream = torch.cuda.current_stream(device)
 
-        def hook():
+        def hook(kind):
             pair = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             for e in pair:   # materialise the HIP event (torch creates it on first record)
                 e.record(stream)
-            step_events.append(pair)
+            step_events.append((kind, pair))
             return pair
         with torch.no_grad():
             for i in range(args.warmup):
@@ -523,8 +563,9 @@ def main():
             barrier(world)
             dt = time.perf_counter() - t0
             mvs_ops.KERNEL_EVENT_HOOK = None
-        if step_events:
-            result["step_kernel_ms"] = sum(a.elapsed_time(b) for a, b in step_events) / len(step_events)
+        for kind in sorted(set(k for k, _ in step_events)):
+            ev = [p for k, p in step_events if k == kind]
+            result.setdefault("step_kernel_ms", {})[kind] = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
         log("timed %d steps: %.2f ms/step" % (args.steps, 1000.0 * dt / args.steps))
         dt = max_over_ranks(dt, world, device)
         ms_step = 1000.0 * dt / args.steps
@@ -601,14 +642,16 @@ def main():
     op_ms = max_over_ranks(op_ms, world, device)
     nc_ms, nc_op_ms, _ = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count)
     nc_ms = max_over_ranks(nc_ms, world, device)
-    # roofline duration: the kernel's launches inside the timed steps when the step runs it
-    # (samples mode); the isolated back-to-back launches otherwise (dshard: NCDHW slabs)
+    # warp-kernel duration: its launches inside the timed steps when the step runs it; the isolated
+    # back-to-back launches otherwise (samples mode: the step forms the volume inside the fused head)
+    step_k = result.get("step_kernel_ms", {})
     iso_ms = k_ms
-    if "step_kernel_ms" in result:
-        k_ms = max_over_ranks(result["step_kernel_ms"], world, device)
+    if "cost_volume" in step_k:
+        k_ms = max_over_ranks(step_k["cost_volume"], world, device)
     gbs = alg / (k_ms * 1e-3) / 1e9
     tag = "b%dv%dd%dh%dw%d" % (B, V, d_count, h, w)
     traffic = load_traffic(tag)
+    head_ms = max_over_ranks(step_k["cv_head"], world, device) if "cv_head" in step_k else None
 
     if rank != 0:
         if world > 1:
@@ -636,31 +679,56 @@ def main():
                    "global_batch": B * (world if args.mode == "samples" else 1),
                    "views": V, "planes": D, "image_hw": [H, W], "feature_hw": [h, w],
                    "parallelism": ("samples%d" % world) if args.mode == "samples" else ("dshard%d" % world)},
-        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": gbs / HBM_PEAK_GBS,
-                     "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
-                     "kernel": "cost_volume_staged_kernel<V=%d, planes=8, %s>" % (
-                         V, "split-fp16 channel-quad store (16 B per voxel and 4 channels)" if quads
-                         else "NCDHW store"), "kernel_ms": k_ms,
-                     "alg_bytes_per_launch": alg,
-                     "timing": ("HIP events around each launch inside the %d timed steps" % args.steps
-                                if "step_kernel_ms" in result else "HIP events, isolated launches"),
-                     "isolated_kernel_ms": iso_ms,
-                     "ncdhw_store": {"kernel_ms": nc_ms, "op_ms": nc_op_ms,
-                                     "frac": alg / (nc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}},
+        "warp_kernel": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": gbs / HBM_PEAK_GBS,
+                        "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
+                        "kernel": "cost_volume_staged_kernel<V=%d, planes=8, %s>" % (
+                            V, "split-fp16 channel-quad store (16 B per voxel and 4 channels)" if quads
+                            else "NCDHW store"), "kernel_ms": k_ms,
+                        "alg_bytes_per_launch": alg,
+                        "timing": ("HIP events around each launch inside the %d timed steps" % args.steps
+                                   if "cost_volume" in step_k else "HIP events, isolated launches"),
+                        "isolated_kernel_ms": iso_ms,
+                        "ncdhw_store": {"kernel_ms": nc_ms, "op_ms": nc_op_ms,
+                                        "frac": alg / (nc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}},
         "hot_path": {"cost_volumes_per_s": B / (op_ms * 1e-3), "op_ms": op_ms,
                      "op": "mvs_cost_volume_fwd%s: prologue kernel (sampling matrices + channel-quad "
                            "packing + reference resampling) + cost_volume_staged kernel" % ("_c4" if quads else ""),
                      "op_GBps": alg / (op_ms * 1e-3) / 1e9},
     }
+    if head_ms is not None:
+        # the step's dominant kernel: the fused head (cost volume formed on chip + conv_0_0 + conv_1_0)
+        hw_ = head_work(B, V, D, h, w)
+        tf = hw_["mfma_flops"] / (head_ms * 1e-3) / 1e12
+        out["roofline"] = {
+            "bound": "mfma", "achieved": tf, "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": tf / MFMA_F16_PEAK_TFS, "traffic": None if head_traffic(tag) is None else head_traffic(tag),
+            "kernel": "cv_head_kernel<V=%d>" % V, "kernel_ms": head_ms,
+            "timing": "HIP events around each launch inside the %d timed steps" % args.steps,
+            "flops_per_launch": hw_["mfma_flops"],
+            "flops": "executed f16 MFMA flops: conv_0_0 B*D*h*w voxels x 27 taps x 2 v_mfma_f32_16x16x32_f16 "
+                     "per 16 voxels (x_hi, x_lo rows against w_hi|w_lo columns) = 55,296 per voxel; conv_1_0 "
+                     "B*|window region| x 27 taps x 3 per 16 windows (three split products) = 82,944 per window",
+            "alg_fp32_conv_flops_per_launch": hw_["alg_flops"],
+            "alg_fp32_conv_tflops": hw_["alg_flops"] / (head_ms * 1e-3) / 1e12,
+            "alg_fp32_conv_frac_of_f32_mfma_peak": hw_["alg_flops"] / (head_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS,
+            "hbm_alg_bytes_per_launch": hw_["hbm_bytes"],
+            "hbm_GBps": hw_["hbm_bytes"] / (head_ms * 1e-3) / 1e9,
+            "hbm_frac": hw_["hbm_bytes"] / (head_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "regions": hw_["regions"]}
+    else:
+        out["roofline"] = dict(out["warp_kernel"])
     out["arithmetic"] = ("fp32 throughout, except conv_0_0 and conv_1_0 (model.py:101,103) in samples mode: "
                          "f16 MFMA with split-fp16 operands (hi + lo parts of the fp32 values; conv_0_0 all four "
-                         "partial products, conv_1_0 three; fp32 accumulation), fed by the fused kernel storing "
-                         "the cost volume as those hi/lo parts; max error 0.3-0.5x that of the exact fp32 kernels "
-                         "vs float64 (tests/test_split_conv.py, DESIGN.md 3.5)")
+                         "partial products, conv_1_0 three; fp32 accumulation), the cost volume formed on chip by "
+                         "the fused head kernel as those hi/lo parts; max error 0.3-0.5x that of the exact fp32 "
+                         "kernels vs float64 (tests/test_split_conv.py, DESIGN.md 3.5); element contract |x - "
+                         "(hi + lo) 2^-e| <= 2^-22 |x| + 2^-37 B^2 (B = max|feat|): fp32-level relative error down "
+                         "to ~1e-5 of the volume bound, an absolute floor below (test_split_conv_dynamic_range)")
     if "exact_fp32" in result:
         out["exact_fp32_step"] = dict(result["exact_fp32"], unit="depth maps/s", note=(
-            "the same step with conv_0_0 on the exact-fp32 VALU kernel (MVS_SPLIT_F16=0)"))
+            "the same step with every product in exact fp32: the materialised cost volume, conv_0_0 on "
+            "the exact-fp32 kernel and conv_1_0 on the fp32 MFMA region kernel (split_f16 off)"))
     if "full" in result:
         out["full_volume_regulariser"] = dict(result["full"], unit="depth maps/s", note=(
             "same step with CostVolumeReg.forward_full (every voxel of every level, as "

@@ -60,6 +60,9 @@ constexpr int kPlaneItems = kHV * kC4;                   // 864 (voxel, quad) it
 constexpr int kBatchItems = 2 * kPlaneItems;             // two planes per step
 constexpr int kItems = (kBatchItems + 255) / 256;        // 7 per producer thread
 constexpr int kPF = 3;                                   // conv_0_0 A-fragment prefetch (items)
+// the sampling state of a batch is formed by the CONSUMER waves after their matrix work (they wait at
+// the step barrier otherwise; the producers' gathers are the step's critical path: cfg 2 2.28 -> 2.19 ms)
+constexpr bool kCoordsByConsumers = true;
 
 template <int NS>
 constexpr int coord_bytes() {   // [2 buffers][2 planes][NS views][108 voxels] x {off, wx, wy, -}
@@ -141,9 +144,6 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   const int z1 = min(z0 + kZC, D);
   const int nsteps = (z1 - z0) >> 1;   // D even (checked by the C ABI)
   const int nbatch = nsteps + 1;       // batch j = planes z0 - 1 + 2j, z0 + 2j
-#ifdef MVS_HEAD_ABL_E
-  if (x0 >= W || y0 >= H) return;
-#endif
   const int ex = cv_split_exponent(a.absmax);
   // the wave index through readfirstlane: role branches are scalar (s_cbranch_scc), not exec-masked
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   // whether they lie in the image
   float cxn[2] = {0.f, 0.f}, cyn[2] = {0.f, 0.f};
   bool cin[2] = {false, false};
-  if (!consumer) {
+  if (kCoordsByConsumers == consumer) {
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
       const int v = lane + 64 * pass;
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   // sampling state of batch j's planes for every (plane, view, halo voxel) -> coordinate buffer tb
   auto coords = [&](int j, int tb) {
     const int pbase = z0 - 1 + 2 * j;
-    for (int c = pw; c < 2 * NS; c += 4) {   // wave-uniform (plane, view) combos
+    for (int c = wave & 3; c < 2 * NS; c += 4) {   // wave-uniform (plane, view) combos
       const int pl = c / NS, s = c - pl * NS;
       const int p = pbase + pl;
       const bool pok = p >= 0 && p < D;
@@ -232,7 +232,12 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
           uint32_t pos;
           float wx, wy;
           src_coords(G, cxn[pass], cyn[pass], H, W, pok && cin[pass], pos, wx, wy);
-          const uint32_t off = pos == kInvalidTap ? kOobOffset
+          // an invalid sample's 4 taps read the zero padding at padded (w + 1, 0): (w + 1, 0), (0, 1)
+          // [the next padded row], (w + 1, 1), (0, 2) -- in range, so the loads complete in issue
+          // order (out-of-range buffer loads return early, out of order: counted vmcnt waits on older
+          // gathers then pass before those land -- DESIGN.md §3.7); zero weights keep the sum exactly 0
+          if (pos == kInvalidTap) wx = wy = 0.0f;
+          const uint32_t off = pos == kInvalidTap ? (uint32_t)(W + 1) * pstride
                                                   : ((uint32_t)(pos_y(pos) + 1) * (uint32_t)pg.pitch +
                                                      (uint32_t)(pos_x(pos) + 1)) * pstride;
           *reinterpret_cast<uint4*>(coord + (((tb * 2 + pl) * NS + s) * kHV + v) * 16) =
@@ -248,11 +253,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   // gathers of several items are in flight together: item u + kAhead's sampling state (LDS) and 4
   // taps x NS views are issued before item u is reduced (each wave keeps up to (kAhead + 1) x 4 x NS
   // 16-byte gathers in flight, waited by counted vmcnt)
-#ifdef MVS_HEAD_KA
-  constexpr int kAhead = MVS_HEAD_KA;
-#else
   constexpr int kAhead = 2;
-#endif
   // per-item constants (the same every batch), packed: LDS offset inside a ring slot (bits 0-12), in
   // the image (13), stored to the SCV box in (y, x) (14), plane of the batch (15), quad (16-18), halo
   // voxel (19-25); and the item's SCV byte offset at plane 0
@@ -330,10 +331,6 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       if (has(u + 1)) rdc(u + 1);
       issue(u);
     }
-#ifdef MVS_HEAD_FIX_KEEP
-    uint32_t kaddr = 0;
-    uint2 khi = make_uint2(0u, 0u), klo = khi;
-#endif
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
@@ -355,44 +352,34 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       split4(acc, ex, hi, lo);
       if (!valid) hi = lo = make_uint2(0u, 0u);
       char* dst = ring + (sl0 + pl) * kSlotB + (m & 0x1FFFu);
-#ifdef MVS_HEAD_FIX_KEEP
-      asm volatile("" ::"v"(kaddr), "v"(khi.x), "v"(khi.y), "v"(klo.x), "v"(klo.y));
-#endif
       *reinterpret_cast<uint2*>(dst) = hi;
       *reinterpret_cast<uint2*>(dst + kPartB) = lo;
-#ifdef MVS_HEAD_FIX_KEEP
-      kaddr = (uint32_t)(uintptr_t)dst;
-      khi = hi;
-      klo = lo;
-#endif
-#ifdef MVS_HEAD_FIX_WAIT
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
       // conv_2_0 / conv_3_0 read the SCV on their input box: the tile-interior voxels of this chunk's
       // planes (every in-volume voxel is interior to exactly one tile and one chunk)
       const bool st = (m & (1u << 14)) && p >= zst0 && p < zst1;
       typedef __attribute__((ext_vector_type(4))) unsigned v4u;
-      __builtin_amdgcn_raw_buffer_store_b128(v4u{hi.x, hi.y, lo.x, lo.y}, rscv,
-                                             (int)(st ? sbase[u] + (uint32_t)p * plane_b : kOobOffset), 0, 0);
+      // lanes outside the box are masked off, a wave with none skips the store (no out-of-range
+      // store: it could complete ahead of older gathers, as above)
+      if (__builtin_amdgcn_ballot_w64(st)) {
+        if (st)
+          __builtin_amdgcn_raw_buffer_store_b128(v4u{hi.x, hi.y, lo.x, lo.y}, rscv,
+                                                 (int)(sbase[u] + (uint32_t)p * plane_b), 0, 0);
+      }
       // one item per scheduling region: without it the scheduler hoists every item's loads to the
       // top (all 7 items' gathers live at once: VGPR spills)
       __builtin_amdgcn_sched_barrier(0);
     }
-#ifdef MVS_HEAD_FIX_KEEP
-    asm volatile("" ::"v"(kaddr), "v"(khi.x), "v"(khi.y), "v"(klo.x), "v"(klo.y));
-#endif
   };
 
   // ================================ schedule ================================
   // Both roles pass the same barriers (nsteps + 3): producers fill batches 0, 1 before step 0 and batch
   // k + 2 during step k; the sampling state of a batch is formed at least one barrier before its items.
   if (!consumer) {
-#ifdef MVS_HEAD_PRIO
-    __builtin_amdgcn_s_setprio(MVS_HEAD_PRIO);
-#endif
     stamp();
-    coords(0, 0);
-    coords(1, 1);
+    if (!kCoordsByConsumers) {
+      coords(0, 0);
+      coords(1, 1);
+    }
     stamp();
     __syncthreads();
     stamp();
@@ -401,14 +388,14 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     stamp();
     __syncthreads();
     stamp();
-    if (2 < nbatch) coords(2, 0);   // buffer 0 is free again (batch 0's items are done)
+    if (!kCoordsByConsumers && 2 < nbatch) coords(2, 0);   // buffer 0 is free again (batch 0's items are done)
     stamp();
     __syncthreads();
     stamp();
     for (int k = 0; k < nsteps; ++k) {
       if (k + 2 < nbatch) items(k + 2, (k + 2) & 1);
       stamp();
-      if (k + 3 < nbatch) coords(k + 3, (k + 3) & 1);
+      if (!kCoordsByConsumers && k + 3 < nbatch) coords(k + 3, (k + 3) & 1);
       stamp();
       __syncthreads();
       stamp();
@@ -499,12 +486,17 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   };
 
   stamp();
+  if (kCoordsByConsumers) {
+    coords(0, 0);
+    coords(1, 1);
+  }
   stamp();
   __syncthreads();
   stamp();
   stamp();
   __syncthreads();
   stamp();
+  if (kCoordsByConsumers && 2 < nbatch) coords(2, 0);
   stamp();
   __syncthreads();
   stamp();
@@ -593,6 +585,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     } else if (k > 0) {
       finish1(zs - 3, (k - 1) & 1);   // the window completed in step k - 1
     }
+    if (kCoordsByConsumers && k + 3 < nbatch) coords(k + 3, (k + 3) & 1);
     stamp();
     __syncthreads();
     stamp();

@@ -122,8 +122,9 @@ def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scal
 
 
 # Live timing of the main fused kernel inside a real step (bench.py): when set, a callable returning a
-# (begin, end) pair of torch.cuda.Event for each cost_volume_c4 call; the C ABI records them on the
-# launch stream right around the main kernel (mvs_cost_volume_fwd_c4's event arguments).
+# KERNEL_EVENT_HOOK(kind) -> (begin, end) pair of torch.cuda.Event for each fused-kernel call (kind
+# "cost_volume": the cost_volume_c4* ops' warp kernel; "cv_head": the fused head kernel); the C ABI
+# records them on the launch stream right around that kernel (the ops' event arguments).
 KERNEL_EVENT_HOOK = None
 
 
@@ -147,7 +148,7 @@ def cost_volume_c4(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: torc
                      dtype=_F32)
     evs = (None, None)
     if KERNEL_EVENT_HOOK is not None:
-        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK())
+        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK("cost_volume"))
     st = lib.mvs_cost_volume_fwd_c4(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T),
                                     _lib.ptr(d_min), _lib.ptr(d_int), batch_size, n_views, c, h, w,
                                     d_begin, d_count, float(d_scale), _lib.ptr(ws), _lib.ptr(cv),
@@ -183,7 +184,7 @@ def cost_volume_c4_absmax(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, 
                      dtype=_F32)
     evs = (None, None)
     if KERNEL_EVENT_HOOK is not None:
-        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK())
+        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK("cost_volume"))
     st = lib.mvs_cost_volume_fwd_c4_absmax(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T),
                                            _lib.ptr(d_min), _lib.ptr(d_int), batch_size, n_views, c, h, w,
                                            d_begin, d_count, float(d_scale), _lib.ptr(ws), _lib.ptr(cv),
@@ -220,7 +221,7 @@ def cost_volume_c4_split(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T
                      dtype=_F32)
     evs = (None, None)
     if KERNEL_EVENT_HOOK is not None:
-        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK())
+        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK("cost_volume"))
     st = lib.mvs_cost_volume_fwd_c4_split(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T),
                                           _lib.ptr(d_min), _lib.ptr(d_int), batch_size, n_views, c, h, w,
                                           d_begin, d_count, float(d_scale), _lib.ptr(ws), _lib.ptr(cv),
@@ -334,7 +335,7 @@ def cost_volume_head(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: to
     ws = torch.empty((_ws_floats(batch_size, n_views, c, h, w, d_count),), device=dev, dtype=_F32)
     evs = (None, None)
     if KERNEL_EVENT_HOOK is not None:
-        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK())
+        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK("cv_head"))
     st = lib.mvs_cost_volume_head_fwd(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T), _lib.ptr(d_min),
                                       _lib.ptr(d_int), batch_size, n_views, c, h, w, d_begin, d_count,
                                       float(d_scale), _lib.ptr(f0), int(e0), *bp0, _lib.ptr(f1), int(e1), *bp1,
@@ -376,7 +377,7 @@ def cost_volume_c4_bf16(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T:
                      dtype=_F32)
     evs = (None, None)
     if KERNEL_EVENT_HOOK is not None:
-        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK())
+        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK("cost_volume"))
     st = lib.mvs_cost_volume_fwd_c4_bf16(_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T),
                                          _lib.ptr(d_min), _lib.ptr(d_int), batch_size, n_views, c, h, w,
                                          d_begin, d_count, float(d_scale), _lib.ptr(ws), _lib.ptr(cv),

@@ -148,3 +148,39 @@ def test_reference_fp32_noise_level():
     d = np.abs(cv32 - cv64)
     rel = np.linalg.norm(d) / np.linalg.norm(cv64)
     assert 1e-5 < rel < 1.5e-4 and d.max() < 1e-3, (rel, d.max())
+
+
+def test_cfg2_selfnoise_fixture_is_consistent():
+    """CPU: tests/golden/cfg2_selfnoise.npz (make_cfg2_selfnoise.py) -- the recorded CPU-fp32-vs-f64
+    flip and within-1e-4 fractions follow from its stored kept-plane sets and depths; kept planes are
+    sorted plane indices < D; the f64 depth is finite and positive."""
+    import os
+    from make_cfg2_selfnoise import significant_flips
+    fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cfg2_selfnoise.npz"))
+    assert fx["keep64"].shape == fx["keep32"].shape == (4, 5, 128, 160)
+    assert fx["ini64"].shape == (4, 128, 160) and np.isfinite(fx["ini64"]).all() and (fx["ini64"] > 0).all()
+    for k in ("keep64", "keep32"):
+        assert (np.diff(fx[k].astype(int), axis=1) > 0).all() and fx[k].max() < 192
+    for b in range(4):
+        flip = significant_flips(fx["keep32"][b], fx["sig32"][b].astype(np.float32), fx["keep64"][b],
+                                 fx["sig64"][b].astype(np.float32))
+        assert flip.mean() == fx["cpu_flip_frac"][b]
+        rel = np.abs(fx["ini32"][b].astype(np.float64) - fx["ini64"][b]) / np.abs(fx["ini64"][b])
+        assert (rel[~flip] <= 1e-4).mean() == fx["cpu_within_1e4_unflipped"][b]
+        assert rel[~flip].max() == fx["cpu_max_rel_unflipped"][b]
+    # the reference's own noise is what the GPU test is measured against: recorded, non-trivial
+    assert 0 < fx["cpu_flip_frac"].max() < 0.01 and fx["cpu_within_1e4_unflipped"].min() > 0.98
+
+
+def test_cfg5_oracle_fixture_is_consistent():
+    """CPU: tests/golden/cfg5_oracle.npz (make_cfg5_oracle.py) -- shapes, sorted kept planes, the
+    4,096 sampled voxels are the script's seeded draw, probabilities in [0, 1], depth finite."""
+    import os
+    from make_cfg5_oracle import sample_voxels
+    fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cfg5_oracle.npz"))
+    assert fx["ini"].shape == (296, 400) and np.isfinite(fx["ini"]).all() and (fx["ini"] > 0).all()
+    assert fx["keep"].shape == fx["sig"].shape == (5, 296, 400) and fx["sig"].dtype == bool
+    assert (np.diff(fx["keep"].astype(int), axis=0) > 0).all() and fx["keep"].max() < 256
+    pz, py, px = sample_voxels(256, 296, 400)
+    assert np.array_equal(pz, fx["pz"]) and np.array_equal(py, fx["py"]) and np.array_equal(px, fx["px"])
+    assert ((fx["pv"] >= 0) & (fx["pv"] <= 1)).all() and fx["tie"].mean() < 0.01

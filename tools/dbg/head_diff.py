@@ -9,6 +9,7 @@ from mvs_amd import ops
 from mvs_amd.config import pad_outpad
 from mvs_amd import model as M
 DEV = torch.device("cuda", 0)
+RUNS = [0]
 CFGS = [(1, 3, 48, 28, 64), (1, 3, 24, 28, 64), (1, 3, 32, 32, 48), (1, 3, 48, 32, 48)]
 if os.environ.get('HEAD_DIFF_BIG'): CFGS = [(4, 3, 192, 128, 160)] * int(os.environ['HEAD_DIFF_BIG'])
 for (B, V, D, h, w) in CFGS:
@@ -33,7 +34,10 @@ for (B, V, D, h, w) in CFGS:
         y0, y1, box, _ = ops.cost_volume_head(feat, K, R, T, d_min, d_int, B, V, 0, D, 25.0, w0, None, None, None,
                                               w1, None, None, None, pad, org, size, lo, hi)
     torch.cuda.synchronize()
+    RUNS[0] += 1
     bad = (y0 != y0r)
+    if os.environ.get('HEAD_DIFF_QUIET') and not bad.any() and torch.equal(y1, y1r) and torch.equal(box, scv):
+        continue
     print("cfg", (B, V, D, h, w), "y0 bad", int(bad.sum()), "of", bad.numel(), "maxd %.3g" % (y0 - y0r).abs().max().item())
     if bad.any():
         bz = bad.any(4).any(3).any(1)[0].nonzero().flatten().tolist()
@@ -46,6 +50,7 @@ for (B, V, D, h, w) in CFGS:
         import collections
         tiles = collections.Counter(zip(nz[:, 0].tolist(), tz, ty, tx))
         print("  tiles (b, zc, ty, tx): count", len(tiles), sorted(tiles.items())[:20])
+        print("  y0 bad voxels (b,c,z,y,x)", nz[:24].tolist())
         print("  z within chunk", sorted(collections.Counter((nz[:, 2] % 48).tolist()).items())[:48])
         print("  y within tile", sorted(collections.Counter((nz[:, 3] % 4).tolist()).items()))
         bc = bad.any(4).any(3).any(2)[0].nonzero().flatten().tolist(); print("  c", bc)
@@ -60,5 +65,7 @@ for (B, V, D, h, w) in CFGS:
         idx = bb.nonzero()[:8].tolist()
         print("  box bad at (b,q,z,y,x) + origin", [tuple(i[:2]) + tuple(a + o for a, o in zip(i[2:], lo)) for i in idx])
         nzb = bb.nonzero()
+        print("  box bad voxels (b,q,z,y,x)", [tuple(i[:2]) + tuple(a + o for a, o in zip(i[2:], lo)) for i in nzb[:40].tolist()])
         print("  box bad z-in-chunk", sorted(set(((nzb[:, 2] + lo[0]) % 48).tolist())), "y", sorted(set((nzb[:, 3] + lo[1]).tolist()))[:20],
               "x", sorted(set((nzb[:, 4] + lo[2]).tolist()))[:20], "q", sorted(set(nzb[:, 1].tolist())))
+print("runs", RUNS[0])
