@@ -16,14 +16,17 @@
 //     pixel's 8 channel quads are one 128-B line; L2 / MALL resident), per-(voxel, view) sampling
 //     state computed one step ahead into an LDS table -- and write the split operands into a 6-plane
 //     LDS ring in the layout conv3d_split.hip stages (so the conv_0_0 MFMA loop below is that kernel's);
-//     voxels inside conv_2_0's input box are also stored to the split cost volume (SCV, split.h);
 //   * consumers run conv_0_0 (split-fp16 f16 MFMA, 2 per (16 voxels, tap), conv3d_split.hip's order)
 //     on the 4 resident planes, and conv_1_0 (stride 2, padding P odd in every dim): the tile owns the
 //     8 x 2 stride-2 windows starting at (x0 - 1 + 2 jx, y0 - 1 + 2 jy) -- one 16-row MFMA block -- and
 //     the depth windows starting at z0 - 1 + 2k; consumer wave w < 3 accumulates product w of the
 //     three split products (x_hi w_hi, x_hi w_lo, x_lo w_hi, conv3d_s2_split.hip's), tap by tap in
 //     that kernel's order, and wave 3 combines a completed window's three partials (aa + (ab + ac)) one
-//     step later and applies BN_1 + ReLU.
+//     step later and applies BN_1 + ReLU; then all four form the sampling state of the batch after next
+//     and copy the tile's voxels inside conv_2_0's input box from the ring to the split cost volume
+//     (SCV, split.h).  The producers issue nothing but in-range gathers (see items()).
+// Per step: producers ~6.6k cycles of gathers + variance, consumers ~4k of MFMA (stamps,
+// tools/dbg/stamps.py): the producers' gather latency is the critical path.
 // Results are bit-identical to the materialising path (fused forward -> SCV -> conv3d_split /
 // conv3d_s2_split): the same operands meet the same MFMAs in the same order.
 #include "launchers.h"
@@ -249,15 +252,17 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
   const Rsrc rscv = make_rsrc(a.scv ? static_cast<char*>(a.scv) + (size_t)b * kC4 * D * HW * 16 : nullptr,
                               a.scv ? (uint32_t)min((uint64_t)kC4 * D * HW * 16ull, 0xFFFFFFF0ull) : 0u);
-  // variance of batch j's two planes -> ring slots (and the SCV box).  Software-pipelined so the
-  // gathers of several items are in flight together: item u + kAhead's sampling state (LDS) and 4
-  // taps x NS views are issued before item u is reduced (each wave keeps up to (kAhead + 1) x 4 x NS
-  // 16-byte gathers in flight, waited by counted vmcnt)
+  // variance of batch j's two planes -> ring slots.  Software-pipelined so the gathers of several
+  // items are in flight together: item u + kAhead's sampling state (LDS) and 4 taps x NS views are
+  // issued before item u is reduced (each wave keeps up to (kAhead + 1) x 4 x NS 16-byte gathers in
+  // flight, waited by counted vmcnt).  The producers issue no other vector-memory operation in the
+  // loop -- every gather in range, no stores -- so the counted waits hold: an out-of-range buffer
+  // load or store completes early, out of issue order, and a count then passes before older gathers
+  // have landed
   constexpr int kAhead = 2;
   // per-item constants (the same every batch), packed: LDS offset inside a ring slot (bits 0-12), in
-  // the image (13), stored to the SCV box in (y, x) (14), plane of the batch (15), quad (16-18), halo
-  // voxel (19-25); and the item's SCV byte offset at plane 0
-  uint32_t meta[kItems], sbase[kItems];
+  // the image (13), plane of the batch (15), quad (16-18), halo voxel (19-25)
+  uint32_t meta[kItems];
   if (!consumer) {
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
@@ -268,20 +273,15 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       const int yy = v / kHX, xx = v - yy * kHX;
       const int gx = x0 - 1 + xx, gy = y0 - 1 + yy;
       const bool vin = gx >= 0 && gx < W && gy >= 0 && gy < H;
-      const bool sxy = vin && xx >= 1 && xx <= kTX && yy >= 1 && yy <= kTY && gy >= a.r0[1] && gy < a.r1[1] &&
-                       gx >= a.r0[2] && gx < a.r1[2];
       const uint32_t lo = (uint32_t)(yy * kRowB + xx * kVoxB + (((q >> 1) ^ ((xx >> 1) & 3)) << 4) + ((q & 1) << 3));
-      meta[u] = lo | ((uint32_t)vin << 13) | ((uint32_t)sxy << 14) | ((uint32_t)pl << 15) | ((uint32_t)q << 16) |
-                ((uint32_t)v << 19);
-      sbase[u] = vin ? (uint32_t)(((size_t)q * D * HW + (size_t)gy * W + gx) * 16) : 0u;
+      meta[u] = lo | ((uint32_t)vin << 13) | ((uint32_t)pl << 15) | ((uint32_t)q << 16) | ((uint32_t)v << 19);
     }
   }
-  const uint32_t plane_b = (uint32_t)HW * 16u;   // SCV bytes per plane
   const int zst0 = max(z0, a.r0[0]), zst1 = min(z1, a.r1[0]);   // planes stored to the SCV box
   auto items = [&](int j, int tb) {
     const int pbase = z0 - 1 + 2 * j;
     const int sl0 = slot_of(pbase);   // even: the batch's second plane is the next slot
-    const int nu = ptid + 256 * (kItems - 1) < kBatchItems ? kItems : kItems - 1;   // wave-uniform
+    const int nu = __builtin_amdgcn_readfirstlane(ptid + 256 * (kItems - 1) < kBatchItems ? kItems : kItems - 1);
     f4v tp[kAhead + 1][NS][4];
     float fx[kAhead + 1][NS], fy[kAhead + 1][NS];
     // item u's sampling state, read from LDS one item before its gathers are issued (the LDS round
@@ -325,20 +325,28 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     };
     // items that exist for this wave: u < nu (wave-uniform)
     auto has = [&](int u) { return u < kItems - 1 || (u == kItems - 1 && nu == kItems); };
+    // No gather is issued while an LDS instruction of this wave is outstanding (s_waitcnt lgkmcnt(0)
+    // first): under the consumers' LDS load a ds_write / ds_read can still be reading its data or
+    // address registers when a younger gather's data lands in them -- the register allocator reuses
+    // a finished item's registers for the next gathers -- and the last lanes then write or address
+    // the wrong values (sporadic, the first steps of a chunk).  So per item: its
+    // gathers' wait, its variance, then the wait for the previous item's LDS operations (which had
+    // the whole variance to finish), item u + kAhead's gathers, and only then this item's LDS work.
+    auto lds_drain = [&]() {
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
     rdc(0);
+    rdc(1);
+    lds_drain();
 #pragma unroll
-    for (int u = 0; u < kAhead; ++u) {
-      if (has(u + 1)) rdc(u + 1);
-      issue(u);
-    }
+    for (int u = 0; u < kAhead; ++u) issue(u);
+    rdc(kAhead);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
       if (!has(u)) break;   // wave-uniform (the last pass: waves 4-6 only)
-      if (has(u + kAhead)) {
-        if (has(u + kAhead + 1)) rdc(u + kAhead + 1);
-        issue(u + kAhead);
-      }
       const uint32_t m = meta[u];
       const int pl = (m >> 15) & 1;
       const int p = pbase + pl;
@@ -351,20 +359,12 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       uint2 hi, lo;
       split4(acc, ex, hi, lo);
       if (!valid) hi = lo = make_uint2(0u, 0u);
+      lds_drain();
+      if (has(u + kAhead)) issue(u + kAhead);
+      if (has(u + kAhead + 1)) rdc(u + kAhead + 1);
       char* dst = ring + (sl0 + pl) * kSlotB + (m & 0x1FFFu);
       *reinterpret_cast<uint2*>(dst) = hi;
       *reinterpret_cast<uint2*>(dst + kPartB) = lo;
-      // conv_2_0 / conv_3_0 read the SCV on their input box: the tile-interior voxels of this chunk's
-      // planes (every in-volume voxel is interior to exactly one tile and one chunk)
-      const bool st = (m & (1u << 14)) && p >= zst0 && p < zst1;
-      typedef __attribute__((ext_vector_type(4))) unsigned v4u;
-      // lanes outside the box are masked off, a wave with none skips the store (no out-of-range
-      // store: it could complete ahead of older gathers, as above)
-      if (__builtin_amdgcn_ballot_w64(st)) {
-        if (st)
-          __builtin_amdgcn_raw_buffer_store_b128(v4u{hi.x, hi.y, lo.x, lo.y}, rscv,
-                                                 (int)(sbase[u] + (uint32_t)p * plane_b), 0, 0);
-      }
       // one item per scheduling region: without it the scheduler hoists every item's loads to the
       // top (all 7 items' gathers live at once: VGPR spills)
       __builtin_amdgcn_sched_barrier(0);
@@ -464,6 +464,27 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       if (t + 2 < 9) ld(t + 2, xr[(t + 2) % 3], wr[(t + 2) % 3]);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xr[t % 3], wr[t % 3], acc, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // conv_2_0 / conv_3_0 read the SCV on their input box: the tile-interior voxels of this chunk's
+  // planes (every in-volume voxel is interior to exactly one tile and one chunk), copied from plane p's
+  // ring slot -- 512 (voxel, quad) items of 16 B, a wave's 64 lanes four 256-B rows of one quad
+  auto box_store = [&](int p) {
+    if (p < zst0 || p >= zst1) return;   // uniform
+    const char* base = ring + slot_of(p) * kSlotB;
+    typedef __attribute__((ext_vector_type(4))) unsigned v4u;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int i = lane + 64 * (wave + 4 * r);
+      const int xx = i & 15, yy = (i >> 4) & 3, q = i >> 6;
+      const int gx = x0 + xx, gy = y0 + yy, hx = xx + 1;
+      const int off = (yy + 1) * kRowB + hx * kVoxB + (((q >> 1) ^ ((hx >> 1) & 3)) << 4) + ((q & 1) << 3);
+      const uint2 h = *reinterpret_cast<const uint2*>(base + off);
+      const uint2 l = *reinterpret_cast<const uint2*>(base + kPartB + off);
+      if (gx < W && gy < H && gx >= a.r0[2] && gx < a.r1[2] && gy >= a.r0[1] && gy < a.r1[1])
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{h.x, h.y, l.x, l.y}, rscv,
+                                               (int)((((uint32_t)q * D + p) * (uint32_t)HW + (uint32_t)(gy * W + gx)) * 16u),
+                                               0, 0);
     }
   };
   // wave 3: the completed window of depth start s from the partials in scratch buffer sb
@@ -586,6 +607,10 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       finish1(zs - 3, (k - 1) & 1);   // the window completed in step k - 1
     }
     if (kCoordsByConsumers && k + 3 < nbatch) coords(k + 3, (k + 3) & 1);
+    // batch k + 1's planes (and plane z0 of batch 0) to the box: resident in their slots this step
+    if (k == 0) box_store(z0);
+    box_store(zs + 1);
+    box_store(zs + 2);
     stamp();
     __syncthreads();
     stamp();

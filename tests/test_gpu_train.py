@@ -74,19 +74,27 @@ def test_train_step_gradients_match_oracle_autograd():
     # BatchNorm running statistics after the step: the regulariser's and the encoder's are fed by the
     # cost volume / images (fp32 noise only); the refinement's see the initial depth, whose flipped
     # pixels differ between any two fp32 paths -- every buffer no further from float64 than the CPU
-    # fp32 reference's (x 3), with a floor of 1e-5 relative: a mean / variance over 10^5-10^7
-    # elements summed in fp32 in another order than the CPU's (MIOpen's batch statistics) is
-    # ~1e-6 from float64 where the CPU's pairwise sums may happen to be 1e-7
+    # fp32 reference's (x 3), with a floor of 2e-6 relative: a blocked / pairwise fp32 sum of n terms
+    # is within ~log2(n) * 2^-24 of float64 (n <= 10^7 here: 23 * 6e-8 = 1.4e-6), and the GPU's batch
+    # statistics sum in another order than the CPU's, whose error on a given buffer may happen to be
+    # 1e-7; the measured distances are recorded (PARITY train_step_bn_buffers)
     bg = dict(net_g.named_buffers())
     bufs = sorted(k[4:] for k in gold.files if k.startswith("b64/"))
     assert set(bufs) == set(bg)
+    dist = {}
+    for name in bufs:
+        ref = torch.from_numpy(gold["b64/" + name])
+        if not name.endswith("num_batches_tracked"):
+            dist[name] = [_rel(bg[name].cpu(), ref), float(gold["ecb/" + name])]
+    from conftest import record_parity
+    record_parity("train_step_bn_buffers", gpu_vs_cpu_fp32_rel_to_f64=dist)
     for name in bufs:
         ref = torch.from_numpy(gold["b64/" + name])
         if name.endswith("num_batches_tracked"):
             assert torch.equal(bg[name].cpu(), ref), name
             continue
-        e_g, e_c = _rel(bg[name].cpu(), ref), float(gold["ecb/" + name])
-        assert e_g <= 3.0 * e_c + 1e-5, "%s: GPU %.3g from float64, CPU fp32 %.3g" % (name, e_g, e_c)
+        e_g, e_c = dist[name]
+        assert e_g <= 3.0 * e_c + 2e-6, "%s: GPU %.3g from float64, CPU fp32 %.3g" % (name, e_g, e_c)
 
     # one Adam step (train.py:104, Adam(model.parameters, lr) with the reference's list attribute)
     opt = torch.optim.Adam(net_g.parameters, lr=1e-3)
