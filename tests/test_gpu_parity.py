@@ -453,9 +453,11 @@ def test_depth_sharded_single_rank_equals_model():
     img = torch.from_numpy(np.random.default_rng(5).standard_normal((6, 3, 256, 320), dtype=np.float32)).to(DEV)
     with torch.no_grad():
         ini, ref = net(img, K, R, T, d_min, d_int, 2, 3)
-        owned, ini_s, ref_s = DepthShardedMVSNet(net, 1, 0)(img, K, R, T, d_min, d_int, 2, 3)
+        owned, ini_s, ref_s = DepthShardedMVSNet(net, 1, 0, gather=False)(img, K, R, T, d_min, d_int, 2, 3)
+        ini_g, ref_g = DepthShardedMVSNet(net, 1, 0)(img, K, R, T, d_min, d_int, 2, 3)   # gathered on rank 0
     assert owned == [0, 1]
     assert torch.equal(ini, ini_s) and torch.equal(ref, ref_s)
+    assert torch.equal(ini, ini_g) and torch.equal(ref, ref_g)
 
 
 @pytest.mark.parametrize("shape,wino", [((2, 32, 8, 12, 20, 40), False), ((1, 8, 1, 5, 9, 33), False),
