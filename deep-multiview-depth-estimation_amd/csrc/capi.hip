@@ -510,6 +510,24 @@ int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch,
   return lc.status();
 }
 
+int mvs_deconv_out_fwd(const float* x, const float* x2, int batch, int c_in, int rd, int rh, int rw, int x0d,
+                       int x0h, int x0w, const float* weight_taps, int d, int h, int w, int pd, int ph, int pw,
+                       const float* bn_scale, const float* bn_shift, const float* bn_mean, const float* residual,
+                       const float* conv_out_weight, float* out, void* stream) {
+  if (!x || !weight_taps || !conv_out_weight || !out || batch <= 0 || c_in <= 0 || c_in > 64)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (rd <= 0 || rh <= 0 || rw <= 0 || d <= 0 || h <= 0 || w <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if (x0d < 0 || x0h < 0 || x0w < 0 || pd < 0 || ph < 0 || pw < 0) return MVS_ERR_INVALID_ARGUMENT;
+  if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
+    return MVS_ERR_INVALID_ARGUMENT;
+  const mvs::LaunchCheck lc;
+  const int st = mvs::launch_deconv_out(x, x2, batch, c_in, rd, rh, rw, x0d, x0h, x0w, weight_taps, d, h, w, pd, ph,
+                                        pw, bn_scale, bn_shift, bn_mean, residual, conv_out_weight, out,
+                                        (hipStream_t)stream);
+  if (st != MVS_OK) return st;
+  return lc.status();
+}
+
 int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, const float* weight, float* y,
                           int batch, int c_in, int c_out, const int* dims, const int* out_origin,
                           const int* out_size, const int* in_origin, const int* in_size,

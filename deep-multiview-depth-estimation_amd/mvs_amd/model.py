@@ -307,7 +307,7 @@ class CostVolumeReg(nn.Module):
         head kernel (forward_live_head) -- conv_0_0's and conv_1_0's outputs; cv is then the split
         volume on conv_2_0's input box only."""
         from .ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_k3_split, conv3d_region, conv_s2_split,
-                          deconv3d_k3s2, region_weight, softmax_depth)
+                          deconv3d_k3s2, deconv_out, region_weight, softmax_depth)
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad = list(n), list(self.pad)
@@ -363,6 +363,13 @@ class CostVolumeReg(nn.Module):
                            size(C2), pad, *bn_eval(self.BN_1), out_ncdhw=True)
         main.wait_stream(side)
         y0.record_stream(main)
+        if os.environ.get("MVS_DECONV_OUT", "0") == "1":
+            # opt-in: deconv_1_0 + BN_0 + ReLU + y0 and conv_out in one kernel, the 8-channel volume
+            # kept on chip (csrc/deconv_out.hip; bit-identical to the two calls below, but slower at
+            # cfg 2: 1.9 ms against 0.72 -- its per-(c_in, tap row) scalar weight loads are latency-
+            # bound at the one or two workgroups per CU its LDS ring allows)
+            return softmax_depth(deconv_out(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0,
+                                            self.conv_out.weight, x2=y1))
         z = deconv3d_k3s2(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0, x2=y1)
         return softmax_depth(conv3d_k3(z, self.conv_out.weight))
 

@@ -858,6 +858,52 @@ def _(x, origin, weight, out_dims, pad, bn_scale, bn_shift, bn_mean, residual, x
     return x.new_empty((x.shape[0], 8) + tuple(out_dims))
 
 
+@torch.library.custom_op("mvs::deconv_out", mutates_args=())
+def deconv_out(x: torch.Tensor, origin: list[int], weight: torch.Tensor, out_dims: list[int], pad: list[int],
+               bn_scale: Optional[torch.Tensor], bn_shift: Optional[torch.Tensor], bn_mean: Optional[torch.Tensor],
+               residual: Optional[torch.Tensor], conv_out_weight: torch.Tensor,
+               x2: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """deconv3d_k3s2 (NCDHW region input x (+ x2), BN + ReLU + residual epilogue) followed by conv_out
+    (Conv3d(8, 1, 3, padding 1), conv_out_weight [1, 8, 3, 3, 3]) in one kernel (csrc/deconv_out.hip):
+    [B, 1, D, H, W], bit-identical to conv3d_k3(deconv3d_k3s2(...), conv_out_weight), the 8-channel
+    volume between them never written.  Inference only."""
+    _require_gpu(x, "x")
+    lib = _lib.load()
+    x = x.to(_F32).contiguous()
+    b, cin, rd, rh, rw = x.shape
+    if x2 is not None:
+        x2 = x2.to(_F32).contiguous()
+        if x2.shape != x.shape:
+            raise ValueError("x2 must have x's shape")
+    if tuple(weight.shape) != (cin, 8, 3, 3, 3):
+        raise ValueError("weight [c_in, 8, 3, 3, 3] expected, got %s" % (tuple(weight.shape),))
+    if tuple(conv_out_weight.shape) != (1, 8, 3, 3, 3):
+        raise ValueError("conv_out_weight [1, 8, 3, 3, 3] expected, got %s" % (tuple(conv_out_weight.shape),))
+    w = derived("deconv_taps", (weight,),
+                lambda wt: wt.to(device=x.device, dtype=_F32).reshape(cin, 8, 27).transpose(1, 2).contiguous(),
+                x.device)
+    wo = conv_out_weight.to(device=x.device, dtype=_F32).contiguous()
+    d, h, wd = out_dims
+    f = lambda t: None if t is None else t.to(device=x.device, dtype=_F32).contiguous()
+    sc, sh, mu, res = f(bn_scale), f(bn_shift), f(bn_mean), f(residual)
+    if (sc is None) != (sh is None) or (sc is None) != (mu is None):
+        raise ValueError("bn_scale, bn_shift and bn_mean go together")
+    if res is not None and tuple(res.shape) != (b, 8, d, h, wd):
+        raise ValueError("residual must be [B, 8, D, H, W]")
+    y = torch.empty((b, 1, d, h, wd), device=x.device, dtype=_F32)
+    pt = lambda t: None if t is None else _lib.ptr(t)
+    st = lib.mvs_deconv_out_fwd(_lib.ptr(x), pt(x2), b, cin, rd, rh, rw, *origin, _lib.ptr(w), d, h, wd, *pad,
+                                pt(sc), pt(sh), pt(mu), pt(res), _lib.ptr(wo), _lib.ptr(y),
+                                _lib.stream_handle(x.device))
+    _lib.check(st, "mvs_deconv_out_fwd")
+    return y
+
+
+@deconv_out.register_fake
+def _(x, origin, weight, out_dims, pad, bn_scale, bn_shift, bn_mean, residual, conv_out_weight, x2=None):
+    return x.new_empty((x.shape[0], 1) + tuple(out_dims))
+
+
 # ----------------------------------------------------------------------------------------------
 # mvs::conv3d_region -- the regulariser's region convolutions on the fp32 MFMA (model.py:101-121)
 # ----------------------------------------------------------------------------------------------

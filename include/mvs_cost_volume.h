@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 9
+#define MVS_ABI_VERSION 10
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -396,6 +396,20 @@ int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch,
                           int h, int w, int pd, int ph, int pw, const float* bn_scale,
                           const float* bn_shift, const float* bn_mean, const float* residual, float* y,
                           void* stream);
+
+/* Regulariser layers deconv_1_0 + BN_0 + ReLU + `+ y0` and conv_out in ONE launch (model.py:121-125,
+ * eval-mode inference): mvs_deconv3d_k3s2_fwd's NCDHW form (x[batch][c_in][rd][rh][rw] region input on
+ * [x0, x0 + r) per dim, x2 nullable and added on load, weight_taps[c_in][27][8] tap-major as with
+ * MVS_DECONV_WEIGHT_TAPS, padding (pd, ph, pw), BN pointers all or none, residual nullable) followed by
+ * nn.Conv3d(8, 1, 3, padding=1, bias=False) with conv_out_weight[1][8][3][3][3], into
+ * out[batch][1][d][h][w] fp32.  The 8-channel volume between the two layers is never written: the
+ * kernel forms it per tile in LDS.  Bit-identical to mvs_deconv3d_k3s2_fwd followed by
+ * mvs_conv3d_k3_fwd (same products, same order).  c_in <= 64; batch*c_in*rd*rh*rw*4 < 2^31 and
+ * batch*8*d*h*w*4 < 2^32 - 16 (MVS_ERR_TOO_LARGE).  Replaces the two calls at model.py:121 and :125. */
+int mvs_deconv_out_fwd(const float* x, const float* x2, int batch, int c_in, int rd, int rh, int rw, int x0d,
+                       int x0h, int x0w, const float* weight_taps, int d, int h, int w, int pd, int ph, int pw,
+                       const float* bn_scale, const float* bn_shift, const float* bn_mean, const float* residual,
+                       const float* conv_out_weight, float* out, void* stream);
 
 /* mvs_conv3d_region_fwd modes */
 #define MVS_CONV_S1 0   /* Conv3d 3x3x3, stride 1, padding 1: region -> region                     */

@@ -713,6 +713,36 @@ def test_region_deconv_channels_last_with_addend():
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("n", [(13, 10, 17), (14, 11, 22), (48, 32, 40), (20, 37, 70), (96, 64, 80)])
+def test_deconv_out_equals_deconv_then_conv_out(n):
+    """mvs::deconv_out (csrc/deconv_out.hip: deconv_1_0 + BN_0 + ReLU + y0 and conv_out in one kernel,
+    the 8-channel volume kept on chip) is BIT-EQUAL to mvs::deconv3d_k3s2 followed by mvs::conv3d_k3
+    (model.py:121-125 as the two-kernel path runs it): pad classes odd and even per dim (n mod 4),
+    widths / heights / depths not multiples of the 32 x 16 x 32 tile, with and without the BN
+    epilogue, residual and addend."""
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _tconv_input_region
+    from mvs_amd.ops import conv3d_k3, deconv3d_k3s2, deconv_out
+    pad, _ = pad_outpad(*n)
+    reg = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
+    org = [lo for lo, _ in reg]
+    g = torch.Generator().manual_seed(sum(n))
+    r = [hi - lo + 1 for lo, hi in reg]
+    a, b = torch.randn(2, 16, *r, generator=g).to(DEV), torch.randn(2, 16, *r, generator=g).to(DEV)
+    wt = (torch.randn(16, 8, 3, 3, 3, generator=g) * 0.1).to(DEV)
+    wo = (torch.randn(1, 8, 3, 3, 3, generator=g) * 0.1).to(DEV)
+    sc, sh, mu = (t.to(DEV) for t in _bn_params(8, g))
+    y0 = torch.randn(2, 8, *n, generator=g).to(DEV)
+    with torch.no_grad():
+        ref = conv3d_k3(deconv3d_k3s2(a, org, wt, list(n), list(pad), sc, sh, mu, y0, x2=b), wo)
+        got = deconv_out(a, org, wt, list(n), list(pad), sc, sh, mu, y0, wo, x2=b)
+        assert got.shape == ref.shape == (2, 1) + tuple(n)
+        assert torch.equal(got, ref), (got - ref).abs().max().item()
+        ref = conv3d_k3(deconv3d_k3s2(a, org, wt, list(n), list(pad), None, None, None, None), wo)
+        got = deconv_out(a, org, wt, list(n), list(pad), None, None, None, None, wo)
+        assert torch.equal(got, ref), (got - ref).abs().max().item()
+
+
 def _to_c4(x):
     """[B, C, D, H, W] -> channel-quad [B, C/4, D, H, W, 4]."""
     b, c = x.shape[:2]
