@@ -180,7 +180,7 @@ class CostVolumeReg(nn.Module):
             if cv.dtype == torch.int32:   # the split cost volume: fp32 values back (to 2^-22) for other paths
                 cv = unsplit_cost_volume(cv, bound)
             if self.live_train_ok(cv.shape[2:5]) and _hip_cv(cv):
-                return self.forward_live_train(cv)
+                return self.forward_live_train(cv, bound)
             cv = cv.permute(0, 1, 5, 2, 3, 4).reshape((cv.shape[0], 4 * cv.shape[1]) + tuple(cv.shape[2:5])).float()
         if self.live_ok(cv.shape[2:]):
             return self.forward_live(cv)
@@ -373,7 +373,7 @@ class CostVolumeReg(nn.Module):
         z = deconv3d_k3s2(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0, x2=y1)
         return softmax_depth(conv3d_k3(z, self.conv_out.weight))
 
-    def forward_live_train(self, cv):
+    def forward_live_train(self, cv, bound=None):
         """Train-mode-BatchNorm regulariser (test.py:53,61: `model.train()` under `no_grad`)
         evaluated on live regions, exactly.
 
@@ -400,7 +400,7 @@ class CostVolumeReg(nn.Module):
         bsz = cv.shape[0]
         count = bsz * n[0] * n[1] * n[2]
         if _hip_cv(cv):
-            return self._forward_live_train_hip(cv, n, full, M, R1, R2, count)
+            return self._forward_live_train_hip(cv, n, full, M, R1, R2, count, bound)
         y0 = _narrow_conv(self.conv_0_0, cv)
         y0 = act(y0, _bn_train(self.BN_0, *_sums(y0), count))
         stage = []
@@ -425,15 +425,15 @@ class CostVolumeReg(nn.Module):
         z = act(z, _bn_train(self.BN_0, *_sums(z), count)) + y0
         return self.Norm(_narrow_conv(self.conv_out, z))
 
-    def _forward_live_train_hip(self, cv, n, full, M, R1, R2, count):
+    def _forward_live_train_hip(self, cv, n, full, M, R1, R2, count, bound=None):
         """forward_live_train on the HIP kernels: raw (BN-free) region convs on the fp32 MFMA
         (conv3d_region.hip), conv_0_0 / conv_out (conv3d_narrow.hip), deconv_1_0
         (deconv3d_region.hip); batch statistics as float64 sums of the raw outputs; BN + ReLU
         applied in place to the region tensors (channels-last).  The transposed convs run over
         the full output volume (their statistics) and keep the M-region part.  ``cv`` may be the
         channel-quad volume (conv_0_0 and the stride-2 convs read it with 16-byte loads)."""
-        from .ops import (CONV_S1, CONV_S2, CONV_T2, bn_relu_, channel_stats, conv3d_k3, conv3d_region,
-                          deconv3d_k3s2, region_weight, softmax_depth)
+        from .ops import (CONV_S1, CONV_S2, CONV_T2, bn_relu_, channel_stats, conv3d_k3, conv3d_k3_split,
+                          conv3d_region, deconv3d_k3s2, region_weight, softmax_depth)
         c4 = cv.dim() == 6
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
@@ -443,7 +443,12 @@ class CostVolumeReg(nn.Module):
         side = _side_stream(cv.device)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            y0 = conv3d_k3(cv, self.conv_0_0.weight, in_c4=c4, wino_z=True)
+            if bound is not None and c4 and cv.dtype == torch.float32 and self.split_f16 and cv.shape[1] == 8:
+                # the channel-quad volume with its bound words: conv_0_0 on the split-fp16 matrix cores
+                # (fp32-level error; 4.4 -> ~1 ms at cfg 2), raw output for the batch sums
+                y0 = conv3d_k3_split(cv, bound, self.conv_0_0.weight)
+            else:
+                y0 = conv3d_k3(cv, self.conv_0_0.weight, in_c4=c4, wino_z=True)
             p0 = _bn_train(self.BN_0, *channel_stats(y0, False), count)
         cv.record_stream(side)
         stage = []

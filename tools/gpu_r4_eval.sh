@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4: eval-step kernel trace (the bench step alone) + per-layer times
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; OUT=gpurun_out/${1:-r4e}; mkdir -p $OUT; export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/eval" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/step_trace.py" --mode eval > $OUT/eval.log 2>&1; rc=$?; echo "eval prof rc=$rc"; grep "step:" $OUT/eval.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/eval" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/step_trace.py" --mode ${MODE:-eval} > $OUT/eval.log 2>&1; rc=$?; echo "eval prof rc=$rc"; grep "step:" $OUT/eval.log
 python3 - $OUT/eval/run_kernel_stats.csv <<'PY'
 import csv, sys
 r = list(csv.DictReader(open(sys.argv[1])))
