@@ -95,8 +95,9 @@ def parse():
     ap.add_argument("--cpu-planes", type=int, default=None, help="planes for the CPU sample")
     ap.add_argument("--kernel-only", action="store_true", help="skip the end-to-end forward")
     ap.add_argument("--no-extra", action="store_true", help="skip the cfg 3/5 end-to-end fields")
-    ap.add_argument("--train-step", action="store_true",
-                    help="also time the train.py step (autograd through the full-volume regulariser)")
+    ap.add_argument("--no-train-step", action="store_true",
+                    help="skip the train.py step field (autograd through the full-volume regulariser; "
+                         "timed by default at N=1)")
     ap.add_argument("--conv-search", choices=("on", "off"), default="off",
                     help="torch.backends.cudnn.benchmark (MIOpen find) for the regulariser convs")
     return ap.parse_args()
@@ -748,7 +749,8 @@ def main():
         out["kernel_configs"] = kernel_configs(device, max(5, args.kernel_iters // 2))
         if not args.kernel_only and not args.no_extra:
             out["e2e_configs"] = e2e_configs(device, max(3, min(args.steps, 10)))
-        if args.train_step:
+        if not args.no_train_step and world == 1:
+            log("timing the train.py step")
             out["train_step"] = train_step_bench(B, V, D, H, W, device, 3)
     # opt-in bf16 cost volume: informational, not the headline (reduced precision)
     _, bf_op_ms, bf_alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count, bf16=True)

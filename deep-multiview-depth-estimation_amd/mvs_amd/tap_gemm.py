@@ -4,14 +4,23 @@ convolutions on the TRAINING path (train.py:97-104: MVSNet.forward under autogra
 Why: MIOpen has only slow (naive) solvers for the backward passes of the regulariser's 3-D shapes --
 the stride-2 convolutions with padding n//2 + 1 (config.py:20) and the full-volume transposed
 convolutions -- so one cfg-2 training step took minutes.  Per tap, every convolution pass is a plain
-GEMM over channels on channels-last views of the volume (hipBLASLt / rocBLAS through torch.matmul):
+GEMM over channels on channels-last views of the volume (hipBLASLt / rocBLAS through torch.addmm_):
 
   conv3d forward        y[o] += x[o*s - p + t] @ W_t^T          (o, t per dim; inputs outside = 0)
          d/dx           gx[o*s - p + t] += gy[o] @ W_t
          d/dW           gW_t = sum_o gy[o]^T x[o*s - p + t]
-  conv_transpose3d      y[i*s - p + t] += x[i] @ W_t            (outputs outside [0, O) dropped)
-         d/dx           gx[i] += gy[i*s - p + t] @ W_t^T
-         d/dW           gW_t = sum_i x[i]^T gy[i*s - p + t]
+  conv_transpose3d      = the d/dx of the conv3d whose input has the transposed conv's output shape;
+                          its d/dx = that conv3d's forward, its d/dW the same sum with x and gy swapped
+
+Layout (no per-tap copies): the conv input is split into its s^3 stride parities and each parity is
+stored channels-last on a grid G of the outputs that touch the input (o in [o_lo, o_hi] per dim) plus
+(k - 1) // s extra rows: P_a[j] = x[s (o_lo + j) + a - p] (zero outside the input).  Tap t = s d + a
+then reads P_a at j = u + d (u = o - o_lo): flattened over (N, G), a CONSTANT row offset
+d_z J_y J_x + d_y J_x + d_x, so every tap's operand is a contiguous row range of one matrix and every
+pass accumulates in place (beta = 1) into another -- one copy of the volume in and out per pass
+instead of one per tap.  Rows whose u falls in the extra rows (or wraps into the next row / sample)
+compute garbage that is never read back: the output is taken on [0, O) per dim, and the gradients fed
+to the scatters are zero there.
 
 fp32 throughout (gfx950 has no reduced-precision fp32 GEMM mode to fall into); each tap's GEMM sums
 over channels, taps are added in a fixed order.  Groups 1, dilation 1, no bias (the reference's
@@ -26,55 +35,142 @@ def _t3(v):
     return tuple(v) if isinstance(v, (tuple, list)) else (v, v, v)
 
 
-def _conv_taps(n, out_n, k, s, p):
-    """Per tap (tz, ty, tx): (output slices, input slices) of the voxels it connects in a conv3d;
-    taps that connect nothing are skipped."""
-    taps = []
-    for tz in range(k[0]):
-        for ty in range(k[1]):
-            for tx in range(k[2]):
-                osl, isl = [], []
-                for t, d, o, pp, ss in zip((tz, ty, tx), n, out_n, p, s):
-                    o0 = max(-((t - pp) // ss), 0)             # ceil((p - t) / s)
-                    o1 = min((d - 1 + pp - t) // ss, o - 1)
-                    if o1 < o0:
-                        break
-                    osl.append(slice(o0, o1 + 1))
-                    isl.append(slice(o0 * ss - pp + t, o1 * ss - pp + t + 1, ss))
-                if len(osl) == 3:
-                    taps.append(((tz, ty, tx), tuple(osl), tuple(isl)))
-    return taps
+class _Geom:
+    """Parity-grid geometry of a conv3d with input extent n, output extent out_n, kernel k, stride s,
+    padding p (per dim)."""
+
+    def __init__(self, n, out_n, k, s, p):
+        self.n, self.out_n, self.k, self.s, self.p = n, out_n, k, s, p
+        self.lo, self.O, self.J = [], [], []
+        for d, o, kk, ss, pp in zip(n, out_n, k, s, p):
+            lo = max(0, -((kk - 1 - pp) // ss))          # ceil((p - k + 1) / s)
+            hi = min(o - 1, (d - 1 + pp) // ss)
+            cnt = max(hi - lo + 1, 0)
+            self.lo.append(lo)
+            self.O.append(cnt)
+            self.J.append(cnt + (kk - 1) // ss)
+        self.empty = min(self.O) == 0
+        self.npar = s[0] * s[1] * s[2]
+        Jz, Jy, Jx = self.J
+        # per tap (tz, ty, tx): (parity index, row offset)
+        self.taps = []
+        for tz in range(k[0]):
+            for ty in range(k[1]):
+                for tx in range(k[2]):
+                    a = [t % ss for t, ss in zip((tz, ty, tx), s)]
+                    dd = [t // ss for t, ss in zip((tz, ty, tx), s)]
+                    pa = (a[0] * s[1] + a[1]) * s[2] + a[2]
+                    self.taps.append(((tz, ty, tx), pa, (dd[0] * Jy + dd[1]) * Jx + dd[2]))
+
+    def _par_slices(self, a):
+        """(input slices, grid slices) of parity a: the j with 0 <= s (lo + j) + a - p < n."""
+        isl, gsl = [], []
+        for d, ss, pp, lo, J, aa in zip(self.n, self.s, self.p, self.lo, self.J, a):
+            j0 = max(0, -((lo * ss + aa - pp) // ss))       # first j with a nonnegative input index
+            j1 = min(J - 1, (d - 1 + pp - aa) // ss - lo)
+            if j1 < j0:
+                return None
+            i0 = ss * (lo + j0) + aa - pp
+            isl.append(slice(i0, ss * (lo + j1) + aa - pp + 1, ss))
+            gsl.append(slice(j0, j1 + 1))
+        return tuple(isl), tuple(gsl)
+
+    def _parities(self):
+        s = self.s
+        for a0 in range(s[0]):
+            for a1 in range(s[1]):
+                for a2 in range(s[2]):
+                    yield (a0 * s[1] + a1) * s[2] + a2, (a0, a1, a2)
+
+    def to_par(self, xc):
+        """channels-last input [N, n..., C] -> [npar, N * J^3, C] parity grids (zeros outside)."""
+        N, C = xc.shape[0], xc.shape[-1]
+        P = xc.new_zeros((self.npar, N) + tuple(self.J) + (C,))
+        for pa, a in self._parities():
+            sl = self._par_slices(a)
+            if sl is not None:
+                P[(pa, slice(None)) + sl[1]] = xc[(slice(None),) + sl[0]]
+        return P.view(self.npar, -1, C)
+
+    def from_par(self, P, N):
+        """[npar, N * J^3, C] -> channels-last input-shaped [N, n..., C] (each input voxel lies in one
+        parity grid)."""
+        C = P.shape[-1]
+        P = P.view((self.npar, N) + tuple(self.J) + (C,))
+        x = P.new_zeros((N,) + tuple(self.n) + (C,))
+        for pa, a in self._parities():
+            sl = self._par_slices(a)
+            if sl is not None:
+                x[(slice(None),) + sl[0]] = P[(pa, slice(None)) + sl[1]]
+        return x
+
+    def _osl(self):
+        return tuple(slice(lo, lo + o) for lo, o in zip(self.lo, self.O))
+
+    def to_grid(self, uc):
+        """channels-last output-shaped [N, out_n..., C] -> [N * J^3, C], zero off the valid box."""
+        N, C = uc.shape[0], uc.shape[-1]
+        G = uc.new_zeros((N,) + tuple(self.J) + (C,))
+        G[(slice(None),) + tuple(slice(0, o) for o in self.O)] = uc[(slice(None),) + self._osl()]
+        return G.view(-1, C)
+
+    def from_grid(self, G, N):
+        """[N * J^3, C] -> channels-last output-shaped [N, out_n..., C] (zeros off the valid box)."""
+        C = G.shape[-1]
+        G = G.view((N,) + tuple(self.J) + (C,))
+        y = G.new_zeros((N,) + tuple(self.out_n) + (C,))
+        y[(slice(None),) + self._osl()] = G[(slice(None),) + tuple(slice(0, o) for o in self.O)]
+        return y
+
+    # ---- the three passes on parity grids / output grids ----
+    def forward(self, P, wt):
+        """Y[m] = sum_t P_a(t)[m + off_t] @ wt(t); wt(t) [C_in, C_out]."""
+        M = P.shape[1]
+        Y = P.new_zeros((M, wt(self.taps[0][0]).shape[1]))
+        for t, pa, off in self.taps:
+            L = M - off
+            Y[:L].addmm_(P[pa, off:off + L], wt(t))
+        return Y
+
+    def scatter(self, G, wt, C):
+        """gP_a(t)[m + off_t] += G[m] @ wt(t); wt(t) [C_g, C]."""
+        M = G.shape[0]
+        gP = G.new_zeros((self.npar, M, C))
+        for t, pa, off in self.taps:
+            L = M - off
+            gP[pa, off:off + L].addmm_(G[:L], wt(t))
+        return gP
+
+    def weight_grad(self, G, P, out):
+        """out(t) = G[:R]^T @ P_a(t)[off_t : off_t + R] for every tap (G zero off the valid box, so
+        every tap may use the same R = M - max offset rows).  The sum over ~N J^3 rows is split
+        into chunks (a batched GEMM, then a sum over chunks): one GEMM with a K of millions and a
+        C_out x C_in output has no parallelism to speak of."""
+        M = G.shape[0]
+        R = M - max(off for _, _, off in self.taps)
+        nch = max(1, min(_KSPLIT, R // 4096))
+        rows = R // nch
+        Rm = rows * nch
+        Cg, Cp = G.shape[1], P.shape[2]
+        for t, pa, off in self.taps:
+            a = G[:Rm].view(nch, rows, Cg).transpose(1, 2)
+            b = P[pa, off:off + Rm].view(nch, rows, Cp)
+            v = torch.bmm(a, b).sum(0)
+            if Rm < R:
+                v = v + torch.matmul(G[Rm:R].t(), P[pa, off + Rm:off + R])
+            out(t, v)
 
 
-def _tconv_taps(n, out_n, k, s, p):
-    """Per tap: (input slices, output slices) of a conv_transpose3d."""
-    taps = []
-    for tz in range(k[0]):
-        for ty in range(k[1]):
-            for tx in range(k[2]):
-                isl, osl = [], []
-                for t, d, o, pp, ss in zip((tz, ty, tx), n, out_n, p, s):
-                    i0 = max(-((t - pp) // ss), 0)
-                    i1 = min((o - 1 + pp - t) // ss, d - 1)
-                    if i1 < i0:
-                        break
-                    isl.append(slice(i0, i1 + 1))
-                    osl.append(slice(i0 * ss - pp + t, i1 * ss - pp + t + 1, ss))
-                if len(isl) == 3:
-                    taps.append(((tz, ty, tx), tuple(isl), tuple(osl)))
-    return taps
+_KSPLIT = 256   # row chunks of the weight-gradient GEMMs
 
 
 def _cl(x):   # [N, C, D, H, W] -> channels-last contiguous [N, D, H, W, C]
     return x.permute(0, 2, 3, 4, 1).contiguous()
 
 
-def _cf(x):   # channels-last -> [N, C, D, H, W] contiguous
-    return x.permute(0, 4, 1, 2, 3).contiguous()
-
-
-def _acc(dst, sl, v):
-    dst[(slice(None),) + sl].add_(v)   # in place on the strided view
+def _cf(x):   # channels-last [N, D, H, W, C] -> [N, C, D, H, W] view in channels_last_3d strides
+    # (no copy: the next layer's _cl, BatchNorm and the elementwise ops take channels-last as it is)
+    return x.permute(0, 4, 1, 2, 3)
 
 
 class _Conv3dTaps(torch.autograd.Function):
@@ -83,71 +179,77 @@ class _Conv3dTaps(torch.autograd.Function):
         s, p, k = _t3(stride), _t3(padding), tuple(w.shape[2:])
         n = tuple(x.shape[2:])
         out_n = tuple((d + 2 * pp - kk) // ss + 1 for d, pp, kk, ss in zip(n, p, k, s))
-        taps = _conv_taps(n, out_n, k, s, p)
-        xc = _cl(x)
-        y = torch.zeros((x.shape[0],) + out_n + (w.shape[0],), dtype=x.dtype, device=x.device)
-        for (tz, ty, tx), osl, isl in taps:
-            _acc(y, osl, torch.matmul(xc[(slice(None),) + isl], w[:, :, tz, ty, tx].t()))
+        g = _Geom(n, out_n, k, s, p)
+        N = x.shape[0]
         ctx.save_for_backward(x, w)
-        ctx.geo = (n, out_n, k, s, p)
-        return _cf(y)
+        ctx.geo = g
+        if g.empty:
+            return x.new_zeros((N, w.shape[0]) + out_n)
+        P = g.to_par(_cl(x))
+        Y = g.forward(P, lambda t: w[(slice(None), slice(None)) + t].t())
+        return _cf(g.from_grid(Y, N))
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        n, out_n, k, s, p = ctx.geo
-        taps = _conv_taps(n, out_n, k, s, p)
-        gyc = _cl(gy)
+        g = ctx.geo
+        N = x.shape[0]
         gx = gw = None
+        if g.empty:
+            return (torch.zeros_like(x) if ctx.needs_input_grad[0] else None,
+                    torch.zeros_like(w) if ctx.needs_input_grad[1] else None, None, None)
+        G = g.to_grid(_cl(gy))
         if ctx.needs_input_grad[0]:
-            gxc = torch.zeros((x.shape[0],) + n + (x.shape[1],), dtype=gy.dtype, device=gy.device)
-            for (tz, ty, tx), osl, isl in taps:
-                _acc(gxc, isl, torch.matmul(gyc[(slice(None),) + osl], w[:, :, tz, ty, tx]))
-            gx = _cf(gxc)
+            gP = g.scatter(G, lambda t: w[(slice(None), slice(None)) + t], x.shape[1])
+            gx = _cf(g.from_par(gP, N))
         if ctx.needs_input_grad[1]:
-            xc = _cl(x)
+            P = g.to_par(_cl(x))
             gw = torch.zeros_like(w)
-            co, ci = w.shape[0], w.shape[1]
-            for (tz, ty, tx), osl, isl in taps:
-                g = gyc[(slice(None),) + osl].reshape(-1, co)
-                gw[:, :, tz, ty, tx] = torch.matmul(g.t(), xc[(slice(None),) + isl].reshape(-1, ci))
+
+            def put(t, v):
+                gw[(slice(None), slice(None)) + t] = v
+            g.weight_grad(G, P, put)
         return gx, gw, None, None
 
 
 class _ConvTranspose3dTaps(torch.autograd.Function):
+    """conv_transpose3d(x) = d/dx of the conv3d g (input extent = this output's, output extent = n)."""
+
     @staticmethod
     def forward(ctx, x, w, stride, padding, output_padding):
         s, p, op, k = _t3(stride), _t3(padding), _t3(output_padding), tuple(w.shape[2:])
         n = tuple(x.shape[2:])
         out_n = tuple((d - 1) * ss - 2 * pp + kk + oo for d, ss, pp, kk, oo in zip(n, s, p, k, op))
-        taps = _tconv_taps(n, out_n, k, s, p)
-        xc = _cl(x)
-        y = torch.zeros((x.shape[0],) + out_n + (w.shape[1],), dtype=x.dtype, device=x.device)
-        for (tz, ty, tx), isl, osl in taps:
-            _acc(y, osl, torch.matmul(xc[(slice(None),) + isl], w[:, :, tz, ty, tx]))
+        g = _Geom(out_n, n, k, s, p)
+        N = x.shape[0]
         ctx.save_for_backward(x, w)
-        ctx.geo = (n, out_n, k, s, p)
-        return _cf(y)
+        ctx.geo = g
+        if g.empty:
+            return x.new_zeros((N, w.shape[1]) + out_n)
+        G = g.to_grid(_cl(x))
+        gP = g.scatter(G, lambda t: w[(slice(None), slice(None)) + t], w.shape[1])
+        return _cf(g.from_par(gP, N))
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        n, out_n, k, s, p = ctx.geo
-        taps = _tconv_taps(n, out_n, k, s, p)
-        gyc = _cl(gy)
+        g = ctx.geo
+        N = x.shape[0]
         gx = gw = None
+        if g.empty:
+            return (torch.zeros_like(x) if ctx.needs_input_grad[0] else None,
+                    torch.zeros_like(w) if ctx.needs_input_grad[1] else None, None, None, None)
+        P = g.to_par(_cl(gy))
         if ctx.needs_input_grad[0]:
-            gxc = torch.zeros((x.shape[0],) + n + (x.shape[1],), dtype=gy.dtype, device=gy.device)
-            for (tz, ty, tx), isl, osl in taps:
-                _acc(gxc, isl, torch.matmul(gyc[(slice(None),) + osl], w[:, :, tz, ty, tx].t()))
-            gx = _cf(gxc)
+            Y = g.forward(P, lambda t: w[(slice(None), slice(None)) + t].t())
+            gx = _cf(g.from_grid(Y, N))
         if ctx.needs_input_grad[1]:
-            xc = _cl(x)
+            G = g.to_grid(_cl(x))
             gw = torch.zeros_like(w)
-            ci, co = w.shape[0], w.shape[1]
-            for (tz, ty, tx), isl, osl in taps:
-                gw[:, :, tz, ty, tx] = torch.matmul(xc[(slice(None),) + isl].reshape(-1, ci).t(),
-                                                    gyc[(slice(None),) + osl].reshape(-1, co))
+
+            def put(t, v):
+                gw[(slice(None), slice(None)) + t] = v
+            g.weight_grad(G, P, put)
         return gx, gw, None, None, None
 
 

@@ -1,7 +1,8 @@
 """mvs_amd/tap_gemm.py (the training path's Conv3d / ConvTranspose3d as per-tap GEMMs with their own
 backward) against PyTorch's autograd of F.conv3d / F.conv_transpose3d in float64 on the CPU: outputs,
 input gradients and weight gradients, for the regulariser's shapes (stride 1 padding 1; stride 2
-padding n//2 + 1; transposed stride 2 with output padding), odd and even extents."""
+padding n//2 + 1; transposed stride 2 with output padding), odd and even extents, extents of 1-3
+(parity grids with an empty parity) and paddings 0 / 1."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -17,11 +18,13 @@ def _grads(fn, x, w, gy):
     return y.detach(), x.grad, w.grad
 
 
-@pytest.mark.parametrize("n", [(5, 6, 7), (8, 9, 10)])
-@pytest.mark.parametrize("stride,pad", [(1, 1), (2, None)])
+@pytest.mark.parametrize("n", [(5, 6, 7), (8, 9, 10), (2, 3, 1)])
+@pytest.mark.parametrize("stride,pad", [(1, 1), (2, None), (2, 1), (1, 0)])
 def test_conv3d_taps_autograd(n, stride, pad):
     g = torch.Generator().manual_seed(sum(n) + stride)
     p = tuple(d // 2 + 1 for d in n) if pad is None else pad
+    if any(d + 2 * pp < 3 for d, pp in zip(n, p if isinstance(p, tuple) else (p,) * 3)):
+        pytest.skip("kernel larger than the padded input")
     x = torch.randn(2, 5, *n, generator=g, dtype=torch.float64)
     w = torch.randn(3, 5, 3, 3, 3, generator=g, dtype=torch.float64)
     y_ref = F.conv3d(x, w, stride=stride, padding=p)
@@ -32,7 +35,7 @@ def test_conv3d_taps_autograd(n, stride, pad):
         torch.testing.assert_close(a, b, rtol=1e-11, atol=1e-11)
 
 
-@pytest.mark.parametrize("n", [(5, 6, 7), (8, 9, 10)])
+@pytest.mark.parametrize("n", [(5, 6, 7), (8, 9, 10), (2, 3, 1)])
 def test_conv_transpose3d_taps_autograd(n):
     g = torch.Generator().manual_seed(sum(n))
     p = tuple(d // 2 + 1 for d in n)
