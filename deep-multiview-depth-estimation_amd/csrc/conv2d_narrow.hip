@@ -15,6 +15,8 @@
 // halo of the tile ((8-1)*S + K rows x (32-1)*S + K columns, zero outside the image) is staged in
 // LDS NC channels per pass; the next pass's elements are loaded into registers before this pass's
 // arithmetic.
+#include <cstdlib>
+
 #include "launchers.h"
 
 namespace mvs {
@@ -32,7 +34,7 @@ constexpr int pass_channels(int cin, int cap) {
   return nc;
 }
 
-template <int CIN, int COUT, int K, int S>
+template <int CIN, int COUT, int K, int S, int SPLIT>
 __global__ __launch_bounds__(kBlock) void conv2d_narrow_kernel(
     const float* __restrict__ in, const float* __restrict__ wt, float* __restrict__ out, int H, int W, int Ho,
     int Wo, int tiles_x, const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
@@ -44,8 +46,11 @@ __global__ __launch_bounds__(kBlock) void conv2d_narrow_kernel(
   constexpr int NC = pass_channels(CIN, 5120 / kPlane);
   constexpr int kStage = NC * kPlane;
   constexpr int kPer = (kStage + kBlock - 1) / kBlock;
-  constexpr int NP = COUT / 2;
+  // SPLIT workgroups per tile (blockIdx.z) share the output channels: CO each, from co0
+  constexpr int CO = COUT / SPLIT;
+  constexpr int NP = CO / 2;
   __shared__ float lds[kStage];
+  const int co0 = (int)blockIdx.z * CO;
 
   const int tile = (int)blockIdx.x;
   const int ox0 = (tile % tiles_x) * k2TX, oy0 = (tile / tiles_x) * k2TY;
@@ -100,7 +105,7 @@ __global__ __launch_bounds__(kBlock) void conv2d_narrow_kernel(
         if constexpr (NP > 0) {
           // the K x COUT weights of (c, ky): workgroup-uniform, scalar loads
           const const_f2v* wg =
-              (const const_f2v*)uniform_ptr(wt + ((size_t)(c * K + ky) * K) * COUT);
+              (const const_f2v*)uniform_ptr(wt + ((size_t)(c * K + ky) * K) * COUT + co0);
 #pragma unroll
           for (int kx = 0; kx < K; ++kx) {
             // the memory clobber keeps the compiler from hoisting more than one tap's COUT weights
@@ -108,7 +113,7 @@ __global__ __launch_bounds__(kBlock) void conv2d_narrow_kernel(
             asm volatile("" ::: "memory");
 #pragma unroll
             for (int p = 0; p < NP; ++p)
-              acc2[p] = __builtin_elementwise_fma(f2v_t{tap[kx], tap[kx]}, wg[kx * NP + p], acc2[p]);
+              acc2[p] = __builtin_elementwise_fma(f2v_t{tap[kx], tap[kx]}, wg[kx * (COUT / 2) + p], acc2[p]);
           }
         } else {
           const const_float* wg = (const const_float*)uniform_ptr(wt + (size_t)(c * K + ky) * K);
@@ -122,22 +127,46 @@ __global__ __launch_bounds__(kBlock) void conv2d_narrow_kernel(
   const int gx = ox0 + lx, gy = oy0 + ly;
   if (gx >= Wo || gy >= Ho) return;
   const size_t oplane = (size_t)Ho * Wo;
-  float* ob = out + (size_t)n * COUT * oplane + (size_t)gy * Wo + gx;
+  float* ob = out + ((size_t)n * COUT + co0) * oplane + (size_t)gy * Wo + gx;
 #pragma unroll
-  for (int co = 0; co < COUT; ++co) {
-    float v = NP > 0 ? acc2[co / 2][co & 1] : acc1;
+  for (int c = 0; c < CO; ++c) {
+    const int co = co0 + c;
+    float v = NP > 0 ? acc2[c / 2][c & 1] : acc1;
     if (bn_scale) v = fmaxf((v - bn_mean[co]) * bn_scale[co] + bn_shift[co], 0.0f);
-    ob[(size_t)co * oplane] = v;
+    ob[(size_t)c * oplane] = v;
   }
 }
 
-template <int CIN, int COUT, int K, int S>
+// output-channel split: a small grid leaves SIMDs idle (the refinement net's 4 x 128 x 160 layers:
+// 320 workgroups), so grids under kSplitTarget workgroups split COUT over up to MAXS workgroups per
+// tile (the staging is repeated, the FMAs are not; each channel's sum is unchanged, bit for bit).
+// Measured at cfg 2 (tools/enc_layers.py): refinement 32 -> 32 0.051 -> 0.028 ms at split 4; the
+// encoder's 960-workgroup layers gain nothing from a split (32 -> 32) or lose (16 -> 32: 0.104 ->
+// 0.108 / 0.132 ms at 2 / 4).  MVS_CONV2D_SPLIT forces a split (<= MAXS).
+constexpr int kSplitTarget = 960;
+
+template <int CIN, int COUT, int K, int S, int MAXS>
 void launch2d(const float* in, const float* wt, float* out, int N, int H, int W, const float* sc,
               const float* sh, const float* mu, hipStream_t s) {
   const int Ho = (H + 2 * (K / 2) - K) / S + 1, Wo = (W + 2 * (K / 2) - K) / S + 1;
   const int tiles_x = (Wo + k2TX - 1) / k2TX, tiles_y = (Ho + k2TY - 1) / k2TY;
-  hipLaunchKernelGGL((conv2d_narrow_kernel<CIN, COUT, K, S>), dim3((unsigned)(tiles_x * tiles_y), (unsigned)N),
-                     dim3(kBlock), 0, s, in, wt, out, H, W, Ho, Wo, tiles_x, sc, sh, mu);
+  const long wgs = (long)tiles_x * tiles_y * N;
+  int split = 1;
+  while (split < MAXS && wgs * split < kSplitTarget) split *= 2;
+  if (const char* e = getenv("MVS_CONV2D_SPLIT")) {
+    const int f = atoi(e);
+    if (f >= 1) split = f > MAXS ? MAXS : f;
+  }
+  const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)N, (unsigned)split);
+  if (split >= 4 && MAXS >= 4)
+    hipLaunchKernelGGL((conv2d_narrow_kernel<CIN, COUT, K, S, (MAXS >= 4 ? 4 : 1)>), grid, dim3(kBlock), 0, s, in,
+                       wt, out, H, W, Ho, Wo, tiles_x, sc, sh, mu);
+  else if (split >= 2 && MAXS >= 2)
+    hipLaunchKernelGGL((conv2d_narrow_kernel<CIN, COUT, K, S, (MAXS >= 2 ? 2 : 1)>), dim3(grid.x, grid.y, 2),
+                       dim3(kBlock), 0, s, in, wt, out, H, W, Ho, Wo, tiles_x, sc, sh, mu);
+  else
+    hipLaunchKernelGGL((conv2d_narrow_kernel<CIN, COUT, K, S, 1>), dim3(grid.x, grid.y, 1), dim3(kBlock), 0, s, in,
+                       wt, out, H, W, Ho, Wo, tiles_x, sc, sh, mu);
 }
 
 }  // namespace
@@ -145,15 +174,16 @@ void launch2d(const float* in, const float* wt, float* out, int N, int H, int W,
 int launch_conv2d_narrow(const float* in, const float* wt, float* out, int N, int Cin, int Cout, int H, int W,
                          int K, int stride, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                          hipStream_t s) {
-#define MVS_CONV2D_CASE(A, C, KK, SS)                                                   \
+#define MVS_CONV2D_CASE(A, C, KK, SS, MS)                                               \
   if (Cin == A && Cout == C && K == KK && stride == SS) {                               \
-    launch2d<A, C, KK, SS>(in, wt, out, N, H, W, bn_scale, bn_shift, bn_mean, s);       \
+    launch2d<A, C, KK, SS, MS>(in, wt, out, N, H, W, bn_scale, bn_shift, bn_mean, s);   \
     return MVS_OK;                                                                      \
   }
-  // FeatureEncoder (model.py:22-65) and the refinement net (model.py:134-145)
-  MVS_CONV2D_CASE(3, 8, 3, 1) MVS_CONV2D_CASE(8, 8, 3, 1) MVS_CONV2D_CASE(8, 16, 5, 2)
-  MVS_CONV2D_CASE(16, 16, 3, 1) MVS_CONV2D_CASE(16, 32, 5, 2) MVS_CONV2D_CASE(32, 32, 3, 1)
-  MVS_CONV2D_CASE(4, 32, 3, 1) MVS_CONV2D_CASE(32, 1, 3, 1)
+  // FeatureEncoder (model.py:22-65) and the refinement net (model.py:134-145); the last argument
+  // is the largest output-channel split (CO = COUT / split stays a multiple of 8)
+  MVS_CONV2D_CASE(3, 8, 3, 1, 1) MVS_CONV2D_CASE(8, 8, 3, 1, 1) MVS_CONV2D_CASE(8, 16, 5, 2, 2)
+  MVS_CONV2D_CASE(16, 16, 3, 1, 2) MVS_CONV2D_CASE(16, 32, 5, 2, 4) MVS_CONV2D_CASE(32, 32, 3, 1, 4)
+  MVS_CONV2D_CASE(4, 32, 3, 1, 4) MVS_CONV2D_CASE(32, 1, 3, 1, 1)
 #undef MVS_CONV2D_CASE
   return MVS_ERR_INVALID_ARGUMENT;
 }

@@ -485,6 +485,28 @@ def test_narrow_conv3d_matches_torch(shape, wino):
     assert err <= 4 * err_t + 1e-6 * scale, (err, err_t)   # no worse than MIOpen's own fp32 sums
 
 
+@pytest.mark.parametrize("shape", [(32, 32, 3, 1, 4, 128, 160), (16, 32, 5, 2, 2, 70, 90), (8, 16, 5, 2, 1, 33, 67),
+                                   (4, 32, 3, 1, 2, 24, 50)])
+def test_conv2d_channel_split_is_bit_identical(shape, monkeypatch):
+    """The output-channel split of small conv2d grids (csrc/conv2d_narrow.hip launch2d: COUT over 2
+    or 4 workgroups per tile) leaves every channel's sum unchanged: splits 1, 2, 4 bit-identical."""
+    from mvs_amd.ops import conv2d
+    cin, cout, k, st, n, h, w = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(n, cin, h, w, generator=g).to(DEV)
+    wt = (torch.randn(cout, cin, k, k, generator=g) * 0.2).to(DEV)
+    p = [(torch.rand(cout, generator=g) + 0.5).to(DEV), torch.randn(cout, generator=g).to(DEV),
+         torch.randn(cout, generator=g).to(DEV)]
+    outs = []
+    for sp in ("1", "2", "4"):
+        monkeypatch.setenv("MVS_CONV2D_SPLIT", sp)
+        with torch.no_grad():
+            outs.append(conv2d(x, wt, st, *p).cpu())
+    monkeypatch.delenv("MVS_CONV2D_SPLIT")
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+
+
 @pytest.mark.parametrize("shape", [(3, 8, 3, 1, 2, 37, 70), (8, 8, 3, 1, 1, 64, 96), (8, 16, 5, 2, 2, 33, 67),
                                    (16, 16, 3, 1, 1, 20, 31), (16, 32, 5, 2, 1, 40, 64),
                                    (32, 32, 3, 1, 2, 16, 40), (4, 32, 3, 1, 1, 24, 50), (32, 1, 3, 1, 2, 17, 33)])
