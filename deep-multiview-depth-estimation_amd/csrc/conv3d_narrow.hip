@@ -33,12 +33,13 @@ constexpr int kTX = 32, kTY = 8, kDT = 4;
 // (g0 - g1 + g2) / 2, g2; formed in float64 on the host, ops.py), accumulated per position; the
 // outputs are A^T m (m0 + m1 + m2, m1 - m2 - m3) at the end.  Per input channel 288 packed FMAs +
 // 36 packed adds instead of 432 packed FMAs.  Weights wu[c][ky][kx][4][co].
-template <int COUT, int C4, bool WZ = false>
+template <int COUT, int C4, bool WZ = false, int DT = kDT>
 __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
     const float* __restrict__ in, const float* __restrict__ wt, float* __restrict__ out, int Cin,
     int D, int H, int W, int tiles_x, int tiles_y, int dgroups, int n_batch, const float* __restrict__ bn_scale,
     const float* __restrict__ bn_shift, const float* __restrict__ bn_mean) {
-  constexpr int kPX = kTX + 2, kPY = kTY + 2, kPD = kDT + 2;
+  static_assert(!WZ || DT == 4, "depth Winograd: two windows of 2");
+  constexpr int kPX = kTX + 2, kPY = kTY + 2, kPD = DT + 2;
   constexpr int kPlane = kPX * kPY;
   constexpr int kStage = kPD * kPlane;                      // floats per input channel
   constexpr int kPer = (kStage + kBlock - 1) / kBlock;      // staging elements per thread
@@ -54,7 +55,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   t /= tiles_x;
   const int ty0 = (t % tiles_y) * kTY;
   t /= tiles_y;
-  const int d0 = (t % dgroups) * kDT;
+  const int d0 = (t % dgroups) * DT;
   const int b = t / dgroups;
   const size_t plane = (size_t)H * W;
   const size_t vol = (size_t)D * plane;
@@ -105,10 +106,10 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   fetch(0);
 
   const int lx = (int)threadIdx.x % kTX, ly = (int)threadIdx.x / kTX;
-  f2v acc2[kDT][NP > 0 ? NP : 1];
-  float acc1[kDT];
+  f2v acc2[DT][NP > 0 ? NP : 1];
+  float acc1[DT];
 #pragma unroll
-  for (int d = 0; d < kDT; ++d) {
+  for (int d = 0; d < DT; ++d) {
     acc1[d] = 0.0f;
 #pragma unroll
     for (int q = 0; q < (NP > 0 ? NP : 1); ++q) acc2[d][q] = f2v{0.0f, 0.0f};
@@ -186,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
 #pragma unroll
             for (int k = 0; k < 9; ++k) wp[k] = wg[k * 4];
 #pragma unroll
-            for (int d = 0; d < kDT; ++d)   // output depth d reads plane d + kd through kernel depth kd
+            for (int d = 0; d < DT; ++d)   // output depth d reads plane d + kd through kernel depth kd
 #pragma unroll
               for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
 #pragma unroll
           for (int k = 0; k < 9; ++k) w9[k] = wg[k];
 #pragma unroll
-          for (int d = 0; d < kDT; ++d)
+          for (int d = 0; d < DT; ++d)
 #pragma unroll
             for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   if (gx >= W || gy >= H) return;
   float* ob = out + (size_t)b * COUT * vol + (size_t)gy * W + gx;
 #pragma unroll
-  for (int d = 0; d < kDT; ++d) {
+  for (int d = 0; d < DT; ++d) {
     if (d0 + d >= D) break;
 #pragma unroll
     for (int co = 0; co < COUT; ++co) {
@@ -236,13 +237,21 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   }
 }
 
+// COUT = 1 (conv_out): kOutDT output depths per thread -- the (DT + 2)-plane halo is re-read
+// (DT + 2) / DT times (cfg 2: 4 -> 1.5x, 8 -> 1.25x of the 503 MB input)
+#ifndef MVS_CONV_OUT_DT
+#define MVS_CONV_OUT_DT 8
+#endif
+constexpr int kOutDT = MVS_CONV_OUT_DT;
+
 template <int COUT, int C4, bool WZ = false>
 void launch_narrow(const float* in, const float* weight, float* out, int B, int Cin, int D, int H, int W,
                    const float* bn_scale, const float* bn_shift, const float* bn_mean, hipStream_t s) {
-  const int tiles_x = (W + kTX - 1) / kTX, tiles_y = (H + kTY - 1) / kTY, dgroups = (D + kDT - 1) / kDT;
+  constexpr int DT = COUT == 1 ? kOutDT : kDT;
+  const int tiles_x = (W + kTX - 1) / kTX, tiles_y = (H + kTY - 1) / kTY, dgroups = (D + DT - 1) / DT;
   const dim3 grid = xcd_grid(B * dgroups * tiles_y * tiles_x);
-  hipLaunchKernelGGL((conv3d_k3_narrow_kernel<COUT, C4, WZ>), grid, dim3(kBlock), 0, s, in, weight, out, Cin, D, H,
-                     W, tiles_x, tiles_y, dgroups, B, bn_scale, bn_shift, bn_mean);
+  hipLaunchKernelGGL((conv3d_k3_narrow_kernel<COUT, C4, WZ, DT>), grid, dim3(kBlock), 0, s, in, weight, out, Cin, D,
+                     H, W, tiles_x, tiles_y, dgroups, B, bn_scale, bn_shift, bn_mean);
 }
 
 }  // namespace

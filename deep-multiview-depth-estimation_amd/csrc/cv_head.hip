@@ -57,7 +57,10 @@ constexpr int kRing = 6;                                 // 4 planes read + 2 be
 constexpr int kRingB = kRing * kSlotB;                   // 82,944 B
 constexpr int kW1B = 27 * 2 * 64 * 16;                   // conv_1_0 fragments: 55,296 B
 constexpr int kScrB = 2 * 3 * 64 * 16;                   // conv_1_0 partials, double buffered
-constexpr int kZC = 48;                                  // output depths per workgroup
+#ifndef MVS_HEAD_ZC
+#define MVS_HEAD_ZC 48
+#endif
+constexpr int kZC = MVS_HEAD_ZC;                         // output depths per workgroup (even)
 constexpr int kThreads = 512;
 constexpr int kPlaneItems = kHV * kC4;                   // 864 (voxel, quad) items per plane
 constexpr int kBatchItems = 2 * kPlaneItems;             // two planes per step
