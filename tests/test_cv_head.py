@@ -54,12 +54,12 @@ def test_bound_cost_volume_travels_with_its_bound():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,V,D,h,w", [(2, 3, 16, 32, 48), (1, 2, 20, 24, 40), (1, 3, 100, 36, 44),
-                                       (2, 3, 48, 28, 64), (1, 2, 20, 26, 32), (1, 3, 16, 30, 40)])
+                                       (2, 3, 48, 28, 64), (1, 2, 20, 25, 32), (1, 3, 16, 29, 41)])
 def test_head_is_bit_equal_to_the_split_path(B, V, D, h, w):
     """y0, y1 and the stored box are bit-equal to cost_volume_c4_split -> conv3d_k3_split /
     conv_s2_split; geometries with one and several 48-plane chunks (a partial last one at D = 100),
-    V = 2 and 3, widths / heights not multiples of the 16 x 4 tile; both, one (26 x 32: x only, 24 x 40:
-    y only) and neither (30 x 40) of w % 16 == 0, h % 4 == 0 (the edge tile column / row that owns only
+    V = 2 and 3, widths / heights not multiples of the 16 x 4 tile; both, one (25 x 32: x only, 24 x 40:
+    y only) and neither (29 x 41) of w % 16 == 0, h % 4 == 0 (the edge tile column / row that owns only
     the last stride-2 window)."""
     from cameras import camera_batch, depth_range
     from mvs_amd import ops
