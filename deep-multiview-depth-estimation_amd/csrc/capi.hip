@@ -586,6 +586,28 @@ int mvs_softmax_depth_fwd(const float* x, int batch, int d_count, int h, int w, 
   return lc.status();
 }
 
+int mvs_refine_input_fwd(const float* initial_depth, const float* d_min, const float* d_int, int batch, int h,
+                         int w, int d_num, float d_scale, const float* ref_img, float* out, void* stream) {
+  if (!initial_depth || !d_min || !d_int || !ref_img || !out || batch <= 0 || h <= 0 || w <= 0 || d_num <= 0)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if ((uint64_t)h * (uint64_t)w >= (1ull << 32) || (uint64_t)batch * h * w >= (1ull << 37)) return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
+  mvs::launch_refine_input(initial_depth, d_min, d_int, d_num, d_scale, ref_img, batch, (uint32_t)((uint64_t)h * w),
+                           out, (hipStream_t)stream);
+  return lc.status();
+}
+
+int mvs_refine_output_fwd(const float* conv, const float* refine_in, const float* d_min, const float* d_int,
+                          int batch, int h, int w, int d_num, float d_scale, float* out, void* stream) {
+  if (!conv || !refine_in || !d_min || !d_int || !out || batch <= 0 || h <= 0 || w <= 0 || d_num <= 0)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if ((uint64_t)h * (uint64_t)w >= (1ull << 32) || (uint64_t)batch * h * w >= (1ull << 37)) return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
+  mvs::launch_refine_output(conv, refine_in, d_min, d_int, d_num, d_scale, batch, (uint32_t)((uint64_t)h * w), out,
+                            (hipStream_t)stream);
+  return lc.status();
+}
+
 static bool channel_layout_ok(int layout, int channels, const void* a, const void* b, const void* c) {
   if (layout & ~MVS_LAYOUT_CHANNELS_LAST) return false;
   if (!(layout & MVS_LAYOUT_CHANNELS_LAST)) return true;

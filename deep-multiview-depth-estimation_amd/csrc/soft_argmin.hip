@@ -133,4 +133,60 @@ void launch_softmax_depth(const float* x, int B, int D, uint32_t hw, float* y, h
   hipLaunchKernelGGL(softmax_depth_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, x, B, D, hw, y);
 }
 
+namespace {
+
+// model.py:189-205 around the refinement net, one kernel on each side (was 9 elementwise launches of
+// ~5 us each): d_span = (d_int * D) * D_SCALE, the normalised depth (ini - d_min) / d_span concatenated
+// with the down-sampled reference image, and refined = ((conv + norm) * d_span) + d_min -- every
+// operation a separately rounded fp32 op in the reference's order (fp contraction off in the kernels:
+// the default would fuse a * b + c into an fma; the division is the correctly rounded one), so the
+// results equal the torch sequence bit for bit.
+__global__ __launch_bounds__(kBlock) void refine_input_kernel(const float* __restrict__ ini,
+                                                              const float* __restrict__ d_min,
+                                                              const float* __restrict__ d_int, float dnum,
+                                                              float scale, const float* __restrict__ img,
+                                                              int B, uint32_t hw, float* __restrict__ out) {
+#pragma clang fp contract(off)   // separately rounded ops: no a * b + c fused into an fma
+  const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= (size_t)B * hw) return;
+  const size_t b = e / hw, p = e - b * hw;
+  const float span = (d_int[b] * dnum) * scale;
+  float* o = out + b * 4 * hw + p;
+  o[0] = (ini[e] - d_min[b]) / span;
+  const float* im = img + b * 3 * hw + p;
+  o[hw] = im[0];
+  o[2 * (size_t)hw] = im[hw];
+  o[3 * (size_t)hw] = im[2 * (size_t)hw];
+}
+
+__global__ __launch_bounds__(kBlock) void refine_output_kernel(const float* __restrict__ conv,
+                                                               const float* __restrict__ inp,
+                                                               const float* __restrict__ d_min,
+                                                               const float* __restrict__ d_int, float dnum,
+                                                               float scale, int B, uint32_t hw,
+                                                               float* __restrict__ out) {
+#pragma clang fp contract(off)   // separately rounded ops: no a * b + c fused into an fma
+  const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= (size_t)B * hw) return;
+  const size_t b = e / hw, p = e - b * hw;
+  const float span = (d_int[b] * dnum) * scale;
+  out[e] = ((conv[e] + inp[b * 4 * hw + p]) * span) + d_min[b];
+}
+
+}  // namespace
+
+void launch_refine_input(const float* ini, const float* d_min, const float* d_int, int d_num, float d_scale,
+                         const float* img, int B, uint32_t hw, float* out, hipStream_t s) {
+  const size_t n = (size_t)B * hw;
+  hipLaunchKernelGGL(refine_input_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ini, d_min,
+                     d_int, (float)d_num, d_scale, img, B, hw, out);
+}
+
+void launch_refine_output(const float* conv, const float* inp, const float* d_min, const float* d_int, int d_num,
+                          float d_scale, int B, uint32_t hw, float* out, hipStream_t s) {
+  const size_t n = (size_t)B * hw;
+  hipLaunchKernelGGL(refine_output_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, conv,
+                     inp, d_min, d_int, (float)d_num, d_scale, B, hw, out);
+}
+
 }  // namespace mvs

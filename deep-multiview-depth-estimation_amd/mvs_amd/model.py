@@ -799,11 +799,21 @@ class MVSNet(nn.Module):
         """model.py:189-205: normalise, concat the downsampled reference image, refine, rescale."""
         c = self.cfg
         device = initial_depth_map.device
-        d_trans = d_min.to(device)
-        d_span = d_int.to(device).mul(c.d_num).mul(c.d_scale)
-        norm_depth = torch.div(torch.subtract(initial_depth_map, d_trans), d_span)
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
             ref_img = F.interpolate(_select_images(nn_input, ref_views), (c.feat_h, c.feat_w), mode="bilinear")
+        if (_hip_inference(initial_depth_map) and initial_depth_map.dim() == 4 and initial_depth_map.shape[1] == 1
+                and tuple(ref_img.shape) == (initial_depth_map.shape[0], 3) + tuple(initial_depth_map.shape[2:])
+                and all(t.numel() == 1 or tuple(t.shape) == (initial_depth_map.shape[0], 1, 1, 1)
+                        for t in (d_min, d_int))   # per sample [B, 1, 1, 1] (data.py) or one value
+                and os.environ.get("MVS_REFINE_GLUE", "1") != "0"):
+            # the elementwise steps on either side of the refinement net as one HIP launch each
+            # (ops.refine_input / refine_output: 9 launches -> 2, bit-equal to the sequence below)
+            from .ops import refine_input, refine_output
+            x = refine_input(initial_depth_map, d_min, d_int, c.d_num, c.d_scale, ref_img)
+            return refine_output(_run_stack(self.depthmap_refine.model, x), x, d_min, d_int, c.d_num, c.d_scale)
+        d_trans = d_min.to(device)
+        d_span = d_int.to(device).mul(c.d_num).mul(c.d_scale)
+        norm_depth = torch.div(torch.subtract(initial_depth_map, d_trans), d_span)
         refined = self.depthmap_refine(torch.cat((norm_depth, ref_img), dim=1))
         return refined.mul(d_span).add(d_trans)

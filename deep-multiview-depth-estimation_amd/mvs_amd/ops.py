@@ -1069,3 +1069,56 @@ def softmax_depth(x: torch.Tensor) -> torch.Tensor:
     rc = lib.mvs_softmax_depth_fwd(_lib.ptr(x), b, d, h, w, _lib.ptr(y), _lib.stream_handle(x.device))
     _lib.check(rc, "mvs_softmax_depth_fwd")
     return y
+
+
+def _per_sample(t, batch, device):
+    """d_min / d_int as a contiguous fp32 [batch] device tensor (one value per sample, or one for all)."""
+    t = t.to(device=device, dtype=_F32).reshape(-1)
+    if t.numel() == 1:
+        t = t.expand(batch)
+    if t.numel() != batch:
+        raise ValueError("d_min / d_int: one value per sample (%d) or one in all, got %d" % (batch, t.numel()))
+    return t.contiguous()
+
+
+def refine_input(initial_depth: torch.Tensor, d_min: torch.Tensor, d_int: torch.Tensor, d_num: int,
+                 d_scale: float, ref_img: torch.Tensor) -> torch.Tensor:
+    """torch.cat(((initial_depth - d_min) / ((d_int * d_num) * d_scale), ref_img), 1) (model.py:195-199)
+    in one HIP launch (mvs_refine_input_fwd), bit-equal to the torch sequence.  Inference only."""
+    _require_gpu(initial_depth, "initial_depth")
+    lib = _lib.load()
+    b, c, h, w = initial_depth.shape
+    if c != 1 or tuple(ref_img.shape) != (b, 3, h, w):
+        raise ValueError("initial_depth [B, 1, h, w] and ref_img [B, 3, h, w] expected, got %s, %s"
+                         % (tuple(initial_depth.shape), tuple(ref_img.shape)))
+    dev = initial_depth.device
+    ini = initial_depth.to(_F32).contiguous()
+    img = ref_img.to(device=dev, dtype=_F32).contiguous()
+    dm, di = _per_sample(d_min, b, dev), _per_sample(d_int, b, dev)
+    out = torch.empty((b, 4, h, w), device=dev, dtype=_F32)
+    rc = lib.mvs_refine_input_fwd(_lib.ptr(ini), _lib.ptr(dm), _lib.ptr(di), b, h, w, int(d_num), float(d_scale),
+                                  _lib.ptr(img), _lib.ptr(out), _lib.stream_handle(dev))
+    _lib.check(rc, "mvs_refine_input_fwd")
+    return out
+
+
+def refine_output(conv: torch.Tensor, refine_in: torch.Tensor, d_min: torch.Tensor, d_int: torch.Tensor,
+                  d_num: int, d_scale: float) -> torch.Tensor:
+    """((conv + refine_in[:, 0]) * ((d_int * d_num) * d_scale)) + d_min -- the refinement's residual
+    add and the rescale (model.py:150, 204-205) in one HIP launch (mvs_refine_output_fwd), bit-equal to
+    the torch sequence.  Inference only."""
+    _require_gpu(conv, "conv")
+    lib = _lib.load()
+    b, c, h, w = conv.shape
+    if c != 1 or tuple(refine_in.shape) != (b, 4, h, w):
+        raise ValueError("conv [B, 1, h, w] and refine_in [B, 4, h, w] expected, got %s, %s"
+                         % (tuple(conv.shape), tuple(refine_in.shape)))
+    dev = conv.device
+    cv = conv.to(_F32).contiguous()
+    ri = refine_in.to(_F32).contiguous()
+    dm, di = _per_sample(d_min, b, dev), _per_sample(d_int, b, dev)
+    out = torch.empty((b, 1, h, w), device=dev, dtype=_F32)
+    rc = lib.mvs_refine_output_fwd(_lib.ptr(cv), _lib.ptr(ri), _lib.ptr(dm), _lib.ptr(di), b, h, w, int(d_num),
+                                   float(d_scale), _lib.ptr(out), _lib.stream_handle(dev))
+    _lib.check(rc, "mvs_refine_output_fwd")
+    return out

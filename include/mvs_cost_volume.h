@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 10
+#define MVS_ABI_VERSION 11
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -448,6 +448,20 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
  * model.py:97 / :125): y[b][0][d][p] = exp(x - max_d x) / sum_d exp(x - max_d x) per pixel p, in
  * torch's operation order; x, y [batch][1][d_count][h][w] fp32 (y may alias x). */
 int mvs_softmax_depth_fwd(const float* x, int batch, int d_count, int h, int w, float* y, void* stream);
+
+/* The elementwise steps around the refinement net (model.py:189-205, MVSNet.refine), each one launch,
+ * every operation a separately rounded fp32 op in the reference's order (bit-equal to the torch
+ * sequence).  d_span = (d_int * d_num) * d_scale per sample; d_min, d_int DEVICE [batch] fp32.
+ *   mvs_refine_input_fwd:  out [batch][4][h][w] = cat((initial_depth - d_min) / d_span, ref_img) --
+ *                          torch.cat((norm_depth, ref_img), 1), model.py:197-199; initial_depth
+ *                          [batch][1][h][w], ref_img [batch][3][h][w] (the down-sampled reference image).
+ *   mvs_refine_output_fwd: out [batch][1][h][w] = ((conv + refine_in[:, 0]) * d_span) + d_min --
+ *                          the refinement's residual add (model.py:150) and the rescale (model.py:204-205);
+ *                          conv [batch][1][h][w] the refinement net's last conv, refine_in the first's input. */
+int mvs_refine_input_fwd(const float* initial_depth, const float* d_min, const float* d_int, int batch, int h,
+                         int w, int d_num, float d_scale, const float* ref_img, float* out, void* stream);
+int mvs_refine_output_fwd(const float* conv, const float* refine_in, const float* d_min, const float* d_int,
+                          int batch, int h, int w, int d_num, float d_scale, float* out, void* stream);
 
 /* ---- train-mode BatchNorm of the regulariser (model.py:101-121 with every BatchNorm3d in training
  * mode: test.py:53,61 runs `model.train()` under no_grad; CostVolumeReg.forward_live_train) ---- */

@@ -979,3 +979,50 @@ def test_channel_stats_bit_reproducible():
         a = channel_stats(x, cl)
         b = channel_stats(x, cl)
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("distinct", [False, True])
+def test_refine_glue_kernels_match_cpu_fp32(distinct):
+    """ops.refine_input / refine_output (csrc/soft_argmin.hip) equal the torch sequence of
+    model.py:195-205 evaluated in fp32 on the CPU (IEEE division, every op separately rounded) bit for
+    bit, per-sample d_min / d_int included."""
+    from cameras import depth_range
+    from mvs_amd.ops import refine_input, refine_output
+    B, h, w, D, scale = 3, 29, 43, 48, 1.0
+    g = torch.Generator().manual_seed(12)
+    d_min, d_int = depth_range(B, distinct=distinct)
+    ini = d_min + D * d_int * torch.rand(B, 1, h, w, generator=g)
+    img = torch.randn(B, 3, h, w, generator=g)
+    conv = torch.randn(B, 1, h, w, generator=g) * 0.1
+    span = d_int.mul(D).mul(scale)
+    x_ref = torch.cat((torch.div(torch.subtract(ini, d_min), span), img), dim=1)
+    y_ref = (conv + x_ref[:, 0].unsqueeze(1)).mul(span).add(d_min)
+    with torch.no_grad():
+        x = refine_input(ini.to(DEV), d_min.to(DEV), d_int.to(DEV), D, scale, img.to(DEV))
+        y = refine_output(conv.to(DEV), x, d_min.to(DEV), d_int.to(DEV), D, scale)
+    assert torch.equal(x.cpu(), x_ref)
+    assert torch.equal(y.cpu(), y_ref)
+
+
+@pytest.mark.parametrize("distinct", [False, True])
+def test_refine_glue_equals_torch_sequence(distinct, monkeypatch):
+    """MVSNet.refine with the two fused HIP launches equals the torch sequence on the GPU
+    (MVS_REFINE_GLUE=0) bit for bit."""
+    from cameras import depth_range
+    from mvs_amd.config import MVSConfig
+    from mvs_amd.model import MVSNet
+    from weights import deterministic_state_dict
+    B, V, H, W = 2, 3, 96, 128
+    net = MVSNet(MVSConfig(d_num=48, in_h=H, in_w=W))
+    net.load_state_dict(deterministic_state_dict(net.state_dict()))
+    net = net.to(DEV).eval()
+    g = torch.Generator().manual_seed(11)
+    img = torch.randn(B * V, 3, H, W, generator=g).to(DEV)
+    d_min, d_int = depth_range(B, distinct=distinct)
+    ini = (d_min + 48 * d_int * torch.rand(B, 1, H // 4, W // 4, generator=g)).to(DEV)
+    ref_views = torch.arange(0, B * V, V)
+    with torch.no_grad():
+        fused = net.refine(img, ini, d_min.to(DEV), d_int.to(DEV), ref_views)
+        monkeypatch.setenv("MVS_REFINE_GLUE", "0")
+        ref = net.refine(img, ini, d_min.to(DEV), d_int.to(DEV), ref_views)
+    assert torch.equal(fused, ref), (fused - ref).abs().max().item()
