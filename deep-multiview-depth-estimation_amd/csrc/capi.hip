@@ -586,6 +586,15 @@ int mvs_softmax_depth_fwd(const float* x, int batch, int d_count, int h, int w, 
   return lc.status();
 }
 
+int mvs_depth_hypotheses_fwd(const float* d_min, const float* d_int, int batch, int d_num, float d_scale, float* out,
+                             void* stream) {
+  if (!d_min || !d_int || !out || batch <= 0 || d_num <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if ((int64_t)batch * d_num >= (1ll << 31)) return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
+  mvs::launch_depth_hypotheses(d_min, d_int, d_scale, batch, d_num, out, (hipStream_t)stream);
+  return lc.status();
+}
+
 int mvs_refine_input_fwd(const float* initial_depth, const float* d_min, const float* d_int, int batch, int h,
                          int w, int d_num, float d_scale, const float* ref_img, float* out, void* stream) {
   if (!initial_depth || !d_min || !d_int || !ref_img || !out || batch <= 0 || h <= 0 || w <= 0 || d_num <= 0)

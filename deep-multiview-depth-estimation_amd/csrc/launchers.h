@@ -67,6 +67,8 @@ int launch_cost_volume_bwd(const Geometry& g, const float* feat, const float* fw
 
 // soft_argmin.hip (+ the regulariser's softmax over depth, model.py:97)
 void launch_softmax_depth(const float* x, int B, int D, uint32_t hw, float* y, hipStream_t s);
+void launch_depth_hypotheses(const float* d_min, const float* d_int, float d_scale, int B, int D, float* out,
+                             hipStream_t s);
 void launch_refine_input(const float* ini, const float* d_min, const float* d_int, int d_num, float d_scale,
                          const float* img, int B, uint32_t hw, float* out, hipStream_t s);
 void launch_refine_output(const float* conv, const float* inp, const float* d_min, const float* d_int, int d_num,

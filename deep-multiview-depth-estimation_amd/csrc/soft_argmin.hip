@@ -189,4 +189,28 @@ void launch_refine_output(const float* conv, const float* inp, const float* d_mi
                      inp, d_min, d_int, (float)d_num, d_scale, B, hw, out);
 }
 
+namespace {
+
+// homography.py:24-26: d_batch_0[b][k] = d_min[b] + (D_SCALE * d_int[b]) * k in one launch (was 4:
+// arange, two multiplies, the add), each op separately rounded in that order (contraction off), so
+// the planes equal the torch expression bit for bit -- and the sampling matrices' depths
+// (sampling_matrix.h forms the same expression).
+__global__ __launch_bounds__(kBlock) void depth_hypotheses_kernel(const float* __restrict__ d_min,
+                                                                  const float* __restrict__ d_int, float scale,
+                                                                  int B, int D, float* __restrict__ out) {
+#pragma clang fp contract(off)   // separately rounded ops: no a * b + c fused into an fma
+  const int e = (int)(blockIdx.x * kBlock + threadIdx.x);
+  if (e >= B * D) return;
+  const int b = e / D, k = e - b * D;
+  out[e] = d_min[b] + (scale * d_int[b]) * (float)k;
+}
+
+}  // namespace
+
+void launch_depth_hypotheses(const float* d_min, const float* d_int, float d_scale, int B, int D, float* out,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(depth_hypotheses_kernel, dim3((unsigned)((B * D + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                     d_min, d_int, d_scale, B, D, out);
+}
+
 }  // namespace mvs

@@ -20,7 +20,13 @@ from .config import D_NUM, D_SCALE
 
 
 def depth_hypotheses(d_min, d_int, d_num, d_scale=D_SCALE):
-    """homography.py:24-26: d_batch_0 = d_min + D_SCALE * d_int * k, shape [B, D, 1, 1]."""
+    """homography.py:24-26: d_batch_0 = d_min + D_SCALE * d_int * k, shape [B, D, 1, 1].  fp32
+    inference on the GPU with the data loader's [B, 1, 1, 1] shapes: one HIP launch (ops.depth_hypotheses,
+    bit-equal to the expression below)."""
+    if (d_min.is_cuda and d_int.is_cuda and d_min.dtype == torch.float32 and d_int.dtype == torch.float32
+            and not torch.is_grad_enabled() and d_min.dim() == 4 and tuple(d_min.shape[1:]) == (1, 1, 1)
+            and tuple(d_int.shape) == tuple(d_min.shape)):
+        return ops.depth_hypotheses(d_min, d_int, d_num, d_scale)
     d_num_tensor = torch.arange(d_num, device=d_min.device).reshape(1, d_num, 1, 1)
     return d_min + d_scale * d_int * d_num_tensor
 

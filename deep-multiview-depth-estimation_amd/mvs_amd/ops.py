@@ -1122,3 +1122,19 @@ def refine_output(conv: torch.Tensor, refine_in: torch.Tensor, d_min: torch.Tens
                                    float(d_scale), _lib.ptr(out), _lib.stream_handle(dev))
     _lib.check(rc, "mvs_refine_output_fwd")
     return out
+
+
+def depth_hypotheses(d_min: torch.Tensor, d_int: torch.Tensor, d_num: int, d_scale: float) -> torch.Tensor:
+    """homography.py:24-26 d_batch_0 [B, d_num, 1, 1] = d_min + d_scale * d_int * k in one HIP launch
+    (mvs_depth_hypotheses_fwd), bit-equal to the torch expression.  d_min, d_int [B, 1, 1, 1] (or one
+    value for all samples) on the device; inference only."""
+    _require_gpu(d_min, "d_min")
+    lib = _lib.load()
+    b = d_min.shape[0] if d_min.numel() > 1 else d_int.reshape(-1).shape[0]
+    dev = d_min.device
+    dm, di = _per_sample(d_min, b, dev), _per_sample(d_int, b, dev)
+    out = torch.empty((b, int(d_num), 1, 1), device=dev, dtype=_F32)
+    rc = lib.mvs_depth_hypotheses_fwd(_lib.ptr(dm), _lib.ptr(di), b, int(d_num), float(d_scale), _lib.ptr(out),
+                                      _lib.stream_handle(dev))
+    _lib.check(rc, "mvs_depth_hypotheses_fwd")
+    return out

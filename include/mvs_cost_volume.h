@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 11
+#define MVS_ABI_VERSION 12
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -448,6 +448,12 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
  * model.py:97 / :125): y[b][0][d][p] = exp(x - max_d x) / sum_d exp(x - max_d x) per pixel p, in
  * torch's operation order; x, y [batch][1][d_count][h][w] fp32 (y may alias x). */
 int mvs_softmax_depth_fwd(const float* x, int batch, int d_count, int h, int w, float* y, void* stream);
+
+/* The depth planes (homography.py:24-26): out[b][k] = d_min[b] + (d_scale * d_int[b]) * k, k < d_num, each
+ * op separately rounded in that order (the torch expression's result, bit for bit); d_min, d_int
+ * DEVICE [batch] fp32, out DEVICE [batch][d_num]. */
+int mvs_depth_hypotheses_fwd(const float* d_min, const float* d_int, int batch, int d_num, float d_scale, float* out,
+                             void* stream);
 
 /* The elementwise steps around the refinement net (model.py:189-205, MVSNet.refine), each one launch,
  * every operation a separately rounded fp32 op in the reference's order (bit-equal to the torch

@@ -1026,3 +1026,19 @@ def test_refine_glue_equals_torch_sequence(distinct, monkeypatch):
         monkeypatch.setenv("MVS_REFINE_GLUE", "0")
         ref = net.refine(img, ini, d_min.to(DEV), d_int.to(DEV), ref_views)
     assert torch.equal(fused, ref), (fused - ref).abs().max().item()
+
+
+@pytest.mark.parametrize("D,scale", [(48, 1.0), (192, 2.5), (256, 0.8)])
+def test_depth_hypotheses_kernel_equals_torch_expression(D, scale):
+    """ops.depth_hypotheses (csrc/soft_argmin.hip) equals homography.py:24-26's expression
+    d_min + d_scale * d_int * arange(D) on the CPU and on the GPU, bit for bit."""
+    from cameras import depth_range
+    from mvs_amd.ops import depth_hypotheses
+    d_min, d_int = depth_range(3, distinct=True)
+    ref = d_min + scale * d_int * torch.arange(D).reshape(1, D, 1, 1)
+    gpu_expr = (d_min.to(DEV) + scale * d_int.to(DEV) * torch.arange(D, device=DEV).reshape(1, D, 1, 1)).cpu()
+    with torch.no_grad():
+        got = depth_hypotheses(d_min.to(DEV), d_int.to(DEV), D, scale).cpu()
+    assert got.shape == ref.shape
+    assert torch.equal(got, ref)
+    assert torch.equal(got, gpu_expr)
