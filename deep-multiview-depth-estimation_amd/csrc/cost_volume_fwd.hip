@@ -238,7 +238,10 @@ __global__ __launch_bounds__(kBlock) void absmax_reduce_kernel(const uint32_t* _
   }
 }
 
-constexpr int kPackPartials = 1024;
+// pack workgroups with the bound words requested (one partial maximum each): enough for one element per
+// thread at cfg 2 (7,898 workgroups); 1,024 made every thread walk 8 grid-stride steps, each waiting
+// on its strided loads (the head prologue 28 us)
+constexpr int kPackPartials = 8192;
 constexpr int kTileW = 32;                // pixels per tile row: every cost-volume store is a 128-B row
 constexpr int kTileH = kBlock / kTileW;   // 8
 
