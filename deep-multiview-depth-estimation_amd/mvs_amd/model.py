@@ -361,8 +361,9 @@ class CostVolumeReg(nn.Module):
                            org(C3), size(C3), pad, *bn_eval(self.BN_2))
         y2 = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, org(B), size(B), org(C2),
                            size(C2), pad, *bn_eval(self.BN_1), out_ncdhw=True)
-        main.wait_stream(side)
-        y0.record_stream(main)
+        if side != main:   # (a stream waiting on itself is an event + barrier packet: a 6 us bubble)
+            main.wait_stream(side)
+            y0.record_stream(main)
         if os.environ.get("MVS_DECONV_OUT", "0") == "1":
             # opt-in: deconv_1_0 + BN_0 + ReLU + y0 and conv_out in one kernel, the 8-channel volume
             # kept on chip (csrc/deconv_out.hip; bit-identical to the two calls below, but slower at
