@@ -21,9 +21,11 @@ constexpr int kBlock = 256;
 constexpr uint32_t kInvalidTap = 0xFFFFFFFFu;
 
 // ------------------------------------------------------------------------------------------
-// sampling coordinates.  Every rounding step is explicit (__f*_rn) so that every call site -- every
-// view, every kernel -- produces bit-identical coordinates for identical inputs, whatever the
-// compiler's contraction choices in the surrounding code.
+// sampling coordinates, one inline definition for every call site -- every view, every kernel -- so
+// identical inputs give identical coordinates (the head / split-path bit-equality tests).  Note: in
+// HIP the __f*_rn helpers are plain operators, so hipcc's default contraction may fuse a multiply and
+// the following add into one fma (gfx950 ISA of cost_volume_fwd.hip: (u + 1) * (w / 2) - 0.5 as
+// v_fma_f32 ..., -0.5); the parity against the reference is pinned by its fixtures.
 // ------------------------------------------------------------------------------------------
 __device__ inline float norm_coord(uint32_t x, int size) {
   return __fmul_rn(__fsub_rn(__fdiv_rn((float)x, (float)(size - 1)), 0.5f), 2.0f);
