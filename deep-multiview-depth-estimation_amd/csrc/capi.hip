@@ -314,7 +314,8 @@ int mvs_cost_volume_head_fwd(const float* feat, const float* K, const float* R, 
     if (scv_lo[d] < 0 || scv_hi[d] > n[d] || scv_lo[d] > scv_hi[d]) return MVS_ERR_INVALID_ARGUMENT;
     ovox *= (uint64_t)y1_size[d];
   }
-  if (128ull * (uint64_t)d_count * (uint64_t)h * (uint64_t)w > 0xFFFFFFF0ull ||
+  if (128ull * (uint64_t)(scv_hi[0] - scv_lo[0]) * (uint64_t)(scv_hi[1] - scv_lo[1]) *
+          (uint64_t)(scv_hi[2] - scv_lo[2]) > 0xFFFFFFF0ull ||
       (uint64_t)batch_size * ovox * 16ull >= (1ull << 40))
     return MVS_ERR_TOO_LARGE;
   const mvs::LaunchCheck lc;
@@ -510,24 +511,6 @@ int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch,
   return lc.status();
 }
 
-int mvs_deconv_out_fwd(const float* x, const float* x2, int batch, int c_in, int rd, int rh, int rw, int x0d,
-                       int x0h, int x0w, const float* weight_taps, int d, int h, int w, int pd, int ph, int pw,
-                       const float* bn_scale, const float* bn_shift, const float* bn_mean, const float* residual,
-                       const float* conv_out_weight, float* out, void* stream) {
-  if (!x || !weight_taps || !conv_out_weight || !out || batch <= 0 || c_in <= 0 || c_in > 64)
-    return MVS_ERR_INVALID_ARGUMENT;
-  if (rd <= 0 || rh <= 0 || rw <= 0 || d <= 0 || h <= 0 || w <= 0) return MVS_ERR_INVALID_ARGUMENT;
-  if (x0d < 0 || x0h < 0 || x0w < 0 || pd < 0 || ph < 0 || pw < 0) return MVS_ERR_INVALID_ARGUMENT;
-  if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
-    return MVS_ERR_INVALID_ARGUMENT;
-  const mvs::LaunchCheck lc;
-  const int st = mvs::launch_deconv_out(x, x2, batch, c_in, rd, rh, rw, x0d, x0h, x0w, weight_taps, d, h, w, pd, ph,
-                                        pw, bn_scale, bn_shift, bn_mean, residual, conv_out_weight, out,
-                                        (hipStream_t)stream);
-  if (st != MVS_OK) return st;
-  return lc.status();
-}
-
 int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, const float* weight, float* y,
                           int batch, int c_in, int c_out, const int* dims, const int* out_origin,
                           const int* out_size, const int* in_origin, const int* in_size,
@@ -543,6 +526,8 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
     return MVS_ERR_INVALID_ARGUMENT;
   if ((flags & MVS_CONV_IN_C4) && (mode != MVS_CONV_S2 || c_in % 4)) return MVS_ERR_INVALID_ARGUMENT;
   if (mode != MVS_CONV_S2 && (!in_origin || !in_size)) return MVS_ERR_INVALID_ARGUMENT;
+  if ((in_origin != nullptr) != (in_size != nullptr)) return MVS_ERR_INVALID_ARGUMENT;
+  const bool boxed = in_origin != nullptr;   // S2: x holds the box [in_origin, + in_size) of the volume
   if (mode != MVS_CONV_S1 && !pad) return MVS_ERR_INVALID_ARGUMENT;
   if (((uintptr_t)x | (uintptr_t)x2 | (uintptr_t)weight) & 15u) return MVS_ERR_INVALID_ARGUMENT;   // 16-byte loads
   if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
@@ -551,17 +536,16 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
   for (int k = 0; k < 3; ++k) {
     if (dims[k] <= 0 || out_size[k] <= 0 || out_origin[k] < 0 || out_origin[k] + out_size[k] > dims[k])
       return MVS_ERR_INVALID_ARGUMENT;
-    if (mode != MVS_CONV_S2 &&
-        (in_size[k] <= 0 || in_origin[k] < 0 || in_origin[k] + in_size[k] > dims[k]))
+    if (boxed && (in_size[k] <= 0 || in_origin[k] < 0 || in_origin[k] + in_size[k] > dims[k]))
       return MVS_ERR_INVALID_ARGUMENT;
     ovox *= (uint64_t)out_size[k];
-    ivox *= (uint64_t)(mode == MVS_CONV_S2 ? dims[k] : in_size[k]);
+    ivox *= (uint64_t)(boxed ? in_size[k] : dims[k]);
     nvox *= (uint64_t)dims[k];
   }
   // 32-bit row indices; per sample, 32-bit buffer descriptors over the input (S2: the 16 channel planes
   // or 4 channel quads of one 16-channel block, 64 B per voxel; S1 / T2: the region tensor)
   uint64_t svox = 1;
-  for (int k = 0; k < 3; ++k) svox *= (uint64_t)(mode == MVS_CONV_S2 ? dims[k] : in_size[k]);
+  for (int k = 0; k < 3; ++k) svox *= (uint64_t)(boxed ? in_size[k] : dims[k]);
   const uint64_t desc_bytes = mode == MVS_CONV_S2 ? svox * 64u : svox * (uint64_t)c_in * 4u;
   if (ovox >= (1ull << 31) || desc_bytes >= 0xFFFFFFC0ull || ivox * (uint64_t)c_in >= (1ull << 62) ||
       nvox >= (1ull << 62))

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #include "../../include/mvs_cost_volume.h"
 
@@ -21,28 +22,81 @@ constexpr int kBlock = 256;
 constexpr uint32_t kInvalidTap = 0xFFFFFFFFu;
 
 // ------------------------------------------------------------------------------------------
-// sampling coordinates, one inline definition for every call site -- every view, every kernel -- so
-// identical inputs give identical coordinates (the head / split-path bit-equality tests).  Note: in
-// HIP the __f*_rn helpers are plain operators, so hipcc's default contraction may fuse a multiply and
-// the following add into one fma (gfx950 ISA of cost_volume_fwd.hip: (u + 1) * (w / 2) - 0.5 as
-// v_fma_f32 ..., -0.5); the parity against the reference is pinned by its fixtures.
+// sampling coordinates, one inline definition for every call site -- every view, every kernel.
+// Every rounding step is the reference's torch CPU one, pinned bit for bit against torch in
+// tests/test_oracle.py::test_sampling_law_is_torch_cpu_bitwise (contraction is off inside these
+// helpers, and every fused step is an explicit fma, so the result never depends on what the
+// compiler chooses to fuse):
+//   * kornia transform_points -> torch.bmm (MKL sgemm, k-ordered fma accumulation):
+//       u = fma(yn, G1, xn * G0) + G2
+//   * kornia convert_points_from_homogeneous: u * (1 / (s + 1e-8)) where |s| > 1e-8
+//   * grid_sample(align_corners=False) unnormalise, ATen GridSamplerKernel.cpp (vectorised, fma):
+//       ix = fma(u + 1, w / 2, -0.5)
 // ------------------------------------------------------------------------------------------
 __device__ inline float norm_coord(uint32_t x, int size) {
-  return __fmul_rn(__fsub_rn(__fdiv_rn((float)x, (float)(size - 1)), 0.5f), 2.0f);
+#pragma clang fp contract(off)
+  return ((float)x / (float)(size - 1) - 0.5f) * 2.0f;   // kornia create_meshgrid (normalised)
 }
 
 __device__ inline void sample_coord(const float* __restrict__ G, float xn, float yn, int h, int w,
                                     float& ix, float& iy) {
-  float u = __fmaf_rn(G[1], yn, __fmaf_rn(G[0], xn, G[2]));
-  float v = __fmaf_rn(G[4], yn, __fmaf_rn(G[3], xn, G[5]));
-  const float s = __fmaf_rn(G[7], yn, __fmaf_rn(G[6], xn, G[8]));
+#pragma clang fp contract(off)
+  float u = __builtin_fmaf(yn, G[1], xn * G[0]) + G[2];
+  float v = __builtin_fmaf(yn, G[4], xn * G[3]) + G[5];
+  const float s = __builtin_fmaf(yn, G[7], xn * G[6]) + G[8];
   // selects, not a branch: the division runs on every lane and |s| <= 1e-8 keeps (u, v)
   const bool div = fabsf(s) > 1e-8f;
-  const float sc = __fdiv_rn(1.0f, __fadd_rn(s, 1e-8f));
-  u = div ? __fmul_rn(u, sc) : u;
-  v = div ? __fmul_rn(v, sc) : v;
-  ix = __fsub_rn(__fmul_rn(__fadd_rn(u, 1.0f), 0.5f * (float)w), 0.5f);
-  iy = __fsub_rn(__fmul_rn(__fadd_rn(v, 1.0f), 0.5f * (float)h), 0.5f);
+  const float sc = 1.0f / (s + 1e-8f);
+  u = div ? u * sc : u;
+  v = div ? v * sc : v;
+  ix = __builtin_fmaf(u + 1.0f, 0.5f * (float)w, -0.5f);
+  iy = __builtin_fmaf(v + 1.0f, 0.5f * (float)h, -0.5f);
+}
+
+// grid_sample's bilinear sum as torch CPU forms it: nw * t0, then fma over ne, sw, se (the
+// vectorised kernel's fused multiply-adds; zero taps add exactly nothing)
+__device__ inline float bilerp_sum(float t0, float t1, float t2, float t3, const float (&wt)[4]) {
+#pragma clang fp contract(off)
+  return __builtin_fmaf(t3, wt[3], __builtin_fmaf(t2, wt[2], __builtin_fmaf(t1, wt[1], t0 * wt[0])));
+}
+
+// ------------------------------------------------------------------------------------------
+// costvolume.py:12-14 as torch CPU rounds it (pinned in tests/test_oracle.py): the view sum in view
+// order, mean = sum / V and cv = (sum of (x - mean) * (x - mean) in view order) / V, every product
+// and sum rounded on its own and both divisions correctly rounded.  x / V is formed as
+// q = x * r, q + fma(x - q V, r) (r = RN(1 / V), the remainder exact by fma): the correctly rounded
+// quotient for every fp32 x and V = 2..16, checked exhaustively (tests/test_exact_division.py);
+// one multiply and two fmas instead of the IEEE division sequence.
+// ------------------------------------------------------------------------------------------
+struct ViewDiv {
+  float v, r;   // V and RN(1 / V)
+};
+
+__host__ __device__ inline ViewDiv view_div(int V) { return ViewDiv{(float)V, 1.0f / (float)V}; }
+
+__device__ inline float div_views(float x, ViewDiv d) {
+#pragma clang fp contract(off)
+  const float q = x * d.r;
+  return __builtin_fmaf(__builtin_fmaf(-q, d.v, x), d.r, q);
+}
+
+// the variance of one element over V <= MAXV views x[0 .. V) (scalar form of packed.h variance_law4)
+template <int MAXV>
+__device__ inline float variance_law(const float (&x)[MAXV], int V, ViewDiv vd) {
+#pragma clang fp contract(off)
+  float sum = x[0];
+#pragma unroll
+  for (int v = 1; v < MAXV; ++v)
+    if (v < V) sum += x[v];
+  const float mean = div_views(sum, vd);
+  float acc = 0.0f;
+#pragma unroll
+  for (int v = 0; v < MAXV; ++v)
+    if (v < V) {
+      const float dlt = x[v] - mean;
+      acc = v == 0 ? dlt * dlt : acc + dlt * dlt;
+    }
+  return div_views(acc, vd);
 }
 
 // Compact tap state: integer corner (x0, y0) packed as ((y0 + 2) << 16) | (x0 + 2) plus the two
@@ -107,7 +161,7 @@ __device__ inline void make_taps(const float* __restrict__ G, float xn, float yn
 __device__ inline float gather(const float* __restrict__ plane, const Taps& tp) {
   const char* pb = reinterpret_cast<const char*>(plane);
   auto ld = [&](int t) { return *reinterpret_cast<const float*>(pb + tp.off[t]); };
-  return ld(0) * tp.wt[0] + ld(1) * tp.wt[1] + ld(2) * tp.wt[2] + ld(3) * tp.wt[3];
+  return bilerp_sum(ld(0), ld(1), ld(2), ld(3), tp.wt);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -149,7 +203,7 @@ __device__ inline float gather_buf(Rsrc rs, uint32_t soff, const Taps& tp) {
   const float b = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, tp.off[1], soff, 0));
   const float c = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, tp.off[2], soff, 0));
   const float d = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, tp.off[3], soff, 0));
-  return a * tp.wt[0] + b * tp.wt[1] + c * tp.wt[2] + d * tp.wt[3];
+  return bilerp_sum(a, b, c, d, tp.wt);
 }
 
 __device__ inline void store_buf(Rsrc rs, uint32_t voff, float v) {
@@ -211,12 +265,16 @@ struct Geometry {
 // Launch status of ONE entry point.  HIP's last-error slot is per thread and sticky.  An error left
 // there before the call (a torch kernel, another library) would otherwise mask this call's own:
 // comparing the slot before and after cannot tell a new failure with the same code from the old one.
-// So the slot is CLEARED at entry (the earlier error belonged to an earlier call, which had its chance
-// to read it; it is kept in prior() for diagnostics) and any error in it after the launches is this
-// call's own: consumed, and reported as MVS_ERR_HIP.  (Construct at entry, status() after the launches.)
+// So the slot is CLEARED at entry and any error in it after the launches is this call's own:
+// consumed, and reported as MVS_ERR_HIP.  The earlier error is not dropped silently: it is reported
+// on stderr (once per entry) and kept in prior().  (Construct at entry, status() after the launches.)
 class LaunchCheck {
  public:
-  LaunchCheck() : prior_(hipGetLastError()) {}
+  LaunchCheck() : prior_(hipGetLastError()) {
+    if (prior_ != hipSuccess)
+      fprintf(stderr, "mvs: a HIP error was pending before this call (cleared, not ours): %s\n",
+              hipGetErrorString(prior_));
+  }
   int status() const { return hipGetLastError() == hipSuccess ? MVS_OK : MVS_ERR_HIP; }
   hipError_t prior() const { return prior_; }
 

@@ -45,8 +45,8 @@ struct Geo {
   int n[3];     // volume dims (D, H, W)
   int o0[3];    // output region origin
   int on[3];    // output region size
-  int i0[3];    // input region origin (S1, T2)
-  int in[3];    // input region size (S1, T2)
+  int i0[3];    // input region origin (S1, T2; S2: the box of the volume the input tensor holds)
+  int in[3];    // input region size (S1, T2; S2: the box size, = n when the whole volume is given)
   int pad[3];   // P (S2, T2)
   int out_cf;   // 1: output region tensor channels-first y[b][co][z][y][x] (else channels-last)
   int in_c4;    // S2: the volume is channel-quad x[b][C/4][D][H][W][4], fp32 (1), bf16 (2) or the split
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
   // parity: t = par, par + 2)
   int lim[3];
 #pragma unroll
-  for (int d = 0; d < 3; ++d) lim[d] = MODE == kS2 ? g.n[d] : g.in[d];
+  for (int d = 0; d < 3; ++d) lim[d] = g.in[d];
   int lin[RB];            // linear index of the base voxel (may be negative; masked)
   unsigned vm[RB][3];     // per dim: bit t = tap t's input exists
 #pragma unroll
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
       if constexpr (MODE == kS1) bs[d] = o[d] - 1 - g.i0[d];
-      else if constexpr (MODE == kS2) bs[d] = 2 * o[d] - g.pad[d];
+      else if constexpr (MODE == kS2) bs[d] = 2 * o[d] - g.pad[d] - g.i0[d];   // taps off the box: off the volume
       else bs[d] = ((o[d] + g.pad[d] - par[d]) >> 1) - g.i0[d];
       unsigned mk = 0;
 #pragma unroll
@@ -155,8 +155,8 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
   // buffer descriptors (workgroup-uniform bases; out-of-range offsets read 0): S2 the sample's
   // volume (channel-quad: quads cb*4 .. cb*4+3 per channel block; NCDHW: 16 channel planes per
   // block), S1 / T2 the sample's region tensor (and addend)
-  const size_t nvol = (size_t)g.n[0] * g.n[1] * g.n[2];
   const size_t rvol = (size_t)g.in[0] * g.in[1] * g.in[2];
+  const size_t nvol = rvol;   // S2: voxels of the (boxed) volume per channel plane / quad plane
   const int sy = lim[2], sz = lim[1] * lim[2];
   // ---- K loop: taps by rows (tz, ty); per row and 16-channel block the A values of its (up to)
   // three x taps and every row block and the matching weights are loaded together, then fed to

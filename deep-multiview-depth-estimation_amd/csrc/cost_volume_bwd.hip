@@ -234,6 +234,7 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
   const f4v x0 = {r4.x, r4.y, r4.z, r4.w};
   const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
   const f4v two_inv_v = inv_v + inv_v;
+  const ViewDiv vd = view_div(V);   // the forward's mean (packed.h variance_law4)
   const int soff = (int)((uint32_t)ch * pg.plane * 16u);
   const int row_bytes = pg.pitch * 16;
   // grad_cv of channel 4 ch + j, plane k0 + pl at this pixel: byte j * cst_bytes + (pl * hw + pix) * 4
@@ -397,7 +398,7 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_kernel(
         xs[s] = bilerp(tp[s], wx[s], wy[s]);
         sum += xs[s];
       }
-      const f4v nmean = -(sum * inv_v);
+      const f4v nmean = -div_views4(sum, vd);
       const f4v k2 = two_inv_v * g;
       if (s0 == 0) racc += k2 * (x0 + nmean);
 #pragma unroll
@@ -555,6 +556,7 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_generic_kernel(
   for (int v = 0; v < V; ++v) make_taps(sampling + ((size_t)(it.b * V + v) * Dc + it.kk) * 9, xn, yn, h, w, tp[v]);
   const float* fb = feat + (size_t)it.b * V * C * hw;
   const float inv_v = 1.0f / (float)V;
+  const ViewDiv vd = view_div(V);
   for (int c = 0; c < C; ++c) {
     const float g = grad_cv[(((size_t)it.b * C + c) * Dc + it.kk) * hw + p];
     float val[MVS_MAX_VIEWS];
@@ -563,7 +565,7 @@ __global__ __launch_bounds__(kBlock) void cost_volume_bwd_generic_kernel(
       val[v] = gather(fb + ((size_t)v * C + c) * hw, tp[v]);
       sum += val[v];
     }
-    const float nmean = -(sum * inv_v);
+    const float nmean = -div_views(sum, vd);   // the forward's mean (common.h variance_law)
     const float k2 = (inv_v + inv_v) * g;
     for (int v = 0; v < V; ++v) {
       const float coef = k2 * (val[v] + nmean);

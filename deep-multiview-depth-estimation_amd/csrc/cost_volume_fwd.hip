@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kBlock) void cost_volume_kernel(
 #pragma unroll
   for (int v = 0; v < MAXV; ++v)
     if (v < V) rs[v] = make_rsrc(fb + (size_t)v * C * hw, (uint32_t)C * plane_bytes);
-  const float inv_v = 1.0f / (float)V;
+  const ViewDiv vd = view_div(V);
   const uint32_t pbyte = p * 4u;
 
   for (int c0 = 0; c0 < C; c0 += CU) {
@@ -74,43 +74,13 @@ __global__ __launch_bounds__(kBlock) void cost_volume_kernel(
 #pragma unroll
     for (int cu = 0; cu < CU; ++cu) {
       if (c0 + cu < C) {
-        // costvolume.py:12-14 -- mean = sum/V, cv = sum (x - mean)^2 / V (two-pass)
-        float sum = val[cu][0];
-#pragma unroll
-        for (int v = 1; v < MAXV; ++v)
-          if (v < V) sum += val[cu][v];
-        const float mean = sum * inv_v;
-        float acc = 0.0f;
-#pragma unroll
-        for (int v = 0; v < MAXV; ++v)
-          if (v < V) {
-            const float dlt = val[cu][v] - mean;
-            acc += dlt * dlt;
-          }
-        if (active) store_buf(make_rsrc(ob + (size_t)(c0 + cu) * ostride, plane_bytes), pbyte, acc * inv_v);
+        if (active)
+          store_buf(make_rsrc(ob + (size_t)(c0 + cu) * ostride, plane_bytes), pbyte, variance_law<MAXV>(val[cu], V, vd));
       }
     }
   }
 }
 
-// costvolume.py:12-14: mean = sum / V, cv = sum (x - mean)^2 / V (two-pass), 4 channels at once;
-// every intermediate rounded as written (no contraction of the mean into the differences).
-template <int NS>
-__device__ inline f4v variance4(const f4v& x0, const f4v (&xs)[NS], const f4v& inv_v) {
-#pragma clang fp contract(off)
-  f4v sum = x0;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) sum += xs[s];
-  const f4v nmean = -(sum * inv_v);   // x + (-mean) == x - mean exactly; keeps v_pk_add_f32
-  f4v d = x0 + nmean;
-  f4v acc = d * d;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    d = xs[s] + nmean;
-    acc = __builtin_elementwise_fma(d, d, acc);
-  }
-  return acc * inv_v;
-}
 
 // Prologue of the fused launch: ONE kernel, three independent jobs by workgroup range (they used
 // to be three dependent launches; cfg 4's 32-plane shard is launch-bound):
@@ -479,7 +449,7 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
     layout();
   }
 
-  const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
+  const ViewDiv vd = view_div(V);
   const uint32_t pix = (uint32_t)(active ? py : 0) * (uint32_t)w + (uint32_t)(active ? px : 0);
   const float4* rbase = refs + (size_t)b * c4 * hw + pix;
   // store byte offset of (plane 0, this pixel) inside a (channel, group) descriptor
@@ -503,7 +473,7 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
     }
   };
   auto emit = [&](int pl, const Rsrc (&rs)[4], const f4v& x0, const f4v (&xs)[NS]) {
-    const f4v acc = variance4<NS>(x0, xs, inv_v);
+    const f4v acc = variance_law4<NS>(x0, xs, vd);
     if constexpr (ES == kQuad) {
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc),
                                              rs[0], (int)(soff0 + (uint32_t)pl * hw * (uint32_t)kQuad), 0, kStoreAux);

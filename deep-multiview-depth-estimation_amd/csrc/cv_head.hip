@@ -90,7 +90,7 @@ struct HeadArgs {
   const float *bn1_sc, *bn1_sh, *bn1_mu;   // BN_1 (16), all or none
   float* y0;                  // [B][8][D][H][W]
   float* y1;                  // [B][on0][on1][on2][16]
-  void* scv;                  // split cost volume [B][8][D][H][W] x 16 B (box written), or null
+  void* scv;                  // split cost volume on the box only: [B][8][r1 - r0 ...] x 16 B, or null
   int V, D, H, W;
   int w_exp0, w_exp1;
   int tiles_x, tiles_y, zchunks, total;
@@ -108,24 +108,6 @@ constexpr int kStampWG = 512, kStampN = 128;
 
 __device__ inline float ror8(float v) {   // value of lane (l ^ 8) inside each 16-lane row
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
-}
-
-// costvolume.py:12-14 -- as cost_volume_fwd.hip::variance4 (same operation order, no contraction)
-template <int NS>
-__device__ inline f4v head_variance4(const f4v& x0, const f4v (&xs)[NS], const f4v& inv_v) {
-#pragma clang fp contract(off)
-  f4v sum = x0;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) sum += xs[s];
-  const f4v nmean = -(sum * inv_v);
-  f4v d = x0 + nmean;
-  f4v acc = d * d;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    d = xs[s] + nmean;
-    acc = __builtin_elementwise_fma(d, d, acc);
-  }
-  return acc * inv_v;
 }
 
 template <int V>
@@ -251,9 +233,13 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       }
     }
   };
-  const f4v inv_v = {1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V, 1.0f / (float)V};
-  const Rsrc rscv = make_rsrc(a.scv ? static_cast<char*>(a.scv) + (size_t)b * kC4 * D * HW * 16 : nullptr,
-                              a.scv ? (uint32_t)min((uint64_t)kC4 * D * HW * 16ull, 0xFFFFFFF0ull) : 0u);
+  const ViewDiv vd = view_div(V);
+  // the box [r0, r1) of sample b's split volume: [8 quads][bz][by][bx] x 16 B
+  const int bz = a.r1[0] - a.r0[0], by = a.r1[1] - a.r0[1], bxw = a.r1[2] - a.r0[2];
+  const uint32_t bhw = (uint32_t)by * (uint32_t)bxw;
+  const uint64_t box_bytes = (uint64_t)kC4 * (uint64_t)bz * bhw * 16ull;
+  const Rsrc rscv = make_rsrc(a.scv ? static_cast<char*>(a.scv) + (size_t)b * box_bytes : nullptr,
+                              a.scv ? (uint32_t)box_bytes : 0u);
   // variance of batch j's two planes -> ring slots.  Software-pipelined so the gathers of several
   // items are in flight together: item u + kAhead's sampling state (LDS) and 4 taps x NS views are
   // issued before item u is reduced (each wave keeps up to (kAhead + 1) x 4 x NS 16-byte gathers in
@@ -357,7 +343,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       f4v xs[NS];
 #pragma unroll
       for (int s = 0; s < NS; ++s) xs[s] = bilerp(tp[rr][s], fx[rr][s], fy[rr][s]);
-      const f4v acc = head_variance4<NS>(ref[u], xs, inv_v);
+      const f4v acc = variance_law4<NS>(ref[u], xs, vd);   // costvolume.py:12-14 (packed.h)
       uint2 hi, lo;
       split4(acc, ex, hi, lo);
       if (!valid) hi = lo = make_uint2(0u, 0u);
@@ -484,9 +470,11 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       const uint2 h = *reinterpret_cast<const uint2*>(base + off);
       const uint2 l = *reinterpret_cast<const uint2*>(base + kPartB + off);
       if (gx < W && gy < H && gx >= a.r0[2] && gx < a.r1[2] && gy >= a.r0[1] && gy < a.r1[1])
-        __builtin_amdgcn_raw_buffer_store_b128(v4u{h.x, h.y, l.x, l.y}, rscv,
-                                               (int)((((uint32_t)q * D + p) * (uint32_t)HW + (uint32_t)(gy * W + gx)) * 16u),
-                                               0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v4u{h.x, h.y, l.x, l.y}, rscv,
+            (int)((((uint32_t)q * (uint32_t)bz + (uint32_t)(p - a.r0[0])) * bhw +
+                   (uint32_t)((gy - a.r0[1]) * bxw + (gx - a.r0[2]))) * 16u),
+            0, 0);
     }
   };
   // wave 3: the completed window of depth start s from the partials in scratch buffer sb

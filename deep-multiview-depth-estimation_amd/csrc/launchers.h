@@ -114,13 +114,6 @@ void launch_deconv3d_k3s2(const float* x, const float* x2, int layout, int B, in
                           int W, int pd, int ph, int pw, const float* bn_scale, const float* bn_shift,
                           const float* bn_mean, const float* residual, float* y, hipStream_t s);
 
-// deconv_out.hip: deconv_1_0 (NCDHW region input + x2, tap-major weights, BN + ReLU + residual) and
-// conv_out (8 -> 1) in one kernel, the 8-channel volume kept on chip; out[B][1][D][H][W]
-int launch_deconv_out(const float* x, const float* x2, int B, int Cin, int rd, int rh, int rw, int x0d, int x0h,
-                      int x0w, const float* weight_taps, int D, int H, int W, int pd, int ph, int pw,
-                      const float* bn_scale, const float* bn_shift, const float* bn_mean, const float* residual,
-                      const float* conv_out_weight, float* out, hipStream_t s);
-
 // conv3d_region.hip: region convolutions of the regulariser on the fp32 MFMA (mode 0 = stride 1,
 // 1 = stride 2 from the full NCDHW volume, 2 = transposed stride 2), channels-last region tensors,
 // optional fused eval BN + ReLU, output channels-last or (out_cf) channels-first; in_c4 (S2): the

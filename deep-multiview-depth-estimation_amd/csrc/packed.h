@@ -48,10 +48,11 @@ __device__ inline void load_taps(Rsrc rs, uint32_t voff, int soff, int row_bytes
   t[3] = ld4(rs, voff + 16u, soff + row_bytes);
 }
 
-// Bilinear sample of 4 channels: acc = 0, then fma(tap_t, weight_t, acc) over nw, ne, sw, se --
-// the order of every other gather in this library (zero taps add exactly nothing).  Packed fp32
-// FMAs (v_pk_fma_f32), elementwise identical to scalar fmaf.
+// Bilinear sample of 4 channels: nw * t0, then fma(tap_t, weight_t, acc) over ne, sw, se -- torch CPU
+// grid_sample's sum (common.h bilerp_sum; zero taps add exactly nothing).  Packed fp32 FMAs
+// (v_pk_fma_f32), elementwise identical to scalar fmaf.
 __device__ inline f4v bilerp(const f4v (&t)[4], float wx, float wy) {
+#pragma clang fp contract(off)
   // weights {nw, ne} = (1-wy) * {1-wx, wx}, {sw, se} = wy * {1-wx, wx}: tap_weights() in pairs
   const f2v e = {1.0f - wx, wx};
   const f2v w01 = f2v{1.0f - wy, 1.0f - wy} * e;
@@ -64,6 +65,34 @@ __device__ inline f4v bilerp(const f4v (&t)[4], float wx, float wy) {
   lo = __builtin_elementwise_fma(t[3].xy, w23.yy, lo);
   hi = __builtin_elementwise_fma(t[3].zw, w23.yy, hi);
   return f4v{lo.x, lo.y, hi.x, hi.y};
+}
+
+// x / V for 4 channels (div_views, packed: v_pk_mul_f32 + 2 v_pk_fma_f32 per channel pair)
+__device__ inline f4v div_views4(const f4v& x, ViewDiv d) {
+#pragma clang fp contract(off)
+  const f4v r = {d.r, d.r, d.r, d.r};
+  const f4v q = x * r;
+  return __builtin_elementwise_fma(__builtin_elementwise_fma(-q, f4v{d.v, d.v, d.v, d.v}, x), r, q);
+}
+
+// costvolume.py:12-14 for 4 channels of one voxel, in the reference's torch CPU roundings (common.h:
+// view_div): mean = ((x0 + x1) + ...) / V, cv = ((d0 d0 + d1 d1) + ...) / V with d = x - mean.
+// x + (-mean) == x - mean exactly (keeps v_pk_add_f32).  The one variance of every forward kernel.
+template <int NS>
+__device__ inline f4v variance_law4(const f4v& x0, const f4v (&xs)[NS], ViewDiv vd) {
+#pragma clang fp contract(off)
+  f4v sum = x0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) sum += xs[s];
+  const f4v nmean = -div_views4(sum, vd);
+  f4v d = x0 + nmean;
+  f4v acc = d * d;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    d = xs[s] + nmean;
+    acc += d * d;
+  }
+  return div_views4(acc, vd);
 }
 
 // workspace layout of mvs_cost_volume_fwd (and read back by mvs_cost_volume_bwd):

@@ -59,6 +59,7 @@ __device__ inline Mat3 load_mat(const float* p) {
 // function, so identical inputs give bit-identical matrices.
 __device__ inline void sampling_matrix(const Cams& cm, int B, int V, int h, int w, int i, int kk,
                                        float* __restrict__ o) {
+#pragma clang fp contract(off)   // the fp32 depth below rounds each op as torch does (no fma)
   const float* K = cm.K;
   const float* R = cm.R;
   const float* T = cm.T;

@@ -48,20 +48,15 @@ __global__ __launch_bounds__(kBlock) void warp_kernel(const float* __restrict__ 
 __global__ __launch_bounds__(kBlock) void variance_kernel(const float* __restrict__ warped,
                                                           int B, int V, size_t M,
                                                           float* __restrict__ cv) {
-  const float inv_v = 1.0f / (float)V;
+  const ViewDiv vd = view_div(V);
   const size_t n = (size_t)B * M;
   for (size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (size_t)gridDim.x * kBlock) {
     const size_t b = e / M, m = e - b * M;
     const float* x = warped + b * V * M + m;
-    float sum = x[0];
-    for (int v = 1; v < V; ++v) sum += x[(size_t)v * M];
-    const float mean = sum * inv_v;
-    float acc = 0.0f;
-    for (int v = 0; v < V; ++v) {
-      const float dlt = x[(size_t)v * M] - mean;
-      acc += dlt * dlt;
-    }
-    cv[e] = acc * inv_v;
+    float val[MVS_MAX_VIEWS];
+#pragma unroll
+    for (int v = 0; v < MVS_MAX_VIEWS; ++v) val[v] = v < V ? x[(size_t)v * M] : 0.0f;
+    cv[e] = variance_law<MVS_MAX_VIEWS>(val, V, vd);
   }
 }
 

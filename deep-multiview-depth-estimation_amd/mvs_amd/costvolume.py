@@ -52,7 +52,7 @@ class DeferredCostVolume:
             self.feature_maps, self.K, self.R, self.T, self.d_min, self.d_int, self.batch_size, self.n_views,
             0, self.d_num, self.d_scale, w0, *bn0, w1, *bn1, list(pad), list(y1_origin), list(y1_size),
             list(scv_lo), list(scv_hi))
-        return y0, y1, ops.BoundCostVolume(scv, absmax) if scv.dim() == 6 else None
+        return y0, y1, ops.BoundCostVolume(scv, absmax, scv_lo, self.shape[2:]) if scv.dim() == 6 else None
 
     def materialize(self):
         cv, _ = ops.cost_volume(self.feature_maps, self.K, self.R, self.T, self.d_min, self.d_int,

@@ -215,7 +215,8 @@ class CostVolumeReg(nn.Module):
         y0, y1, box = dcv.head(self.conv_0_0.weight, _bn_eval(self.BN_0), self.conv_1_0.weight,
                                _bn_eval(self.BN_1), self.pad, [a for a, _ in h1], [b - a + 1 for a, b in h1],
                                lo, hi)
-        return self._forward_live_hip(box.data, n, B, C2, C3, True, box.absmax, head=(y0, y1))
+        return self._forward_live_hip(box.data, n, B, C2, C3, True, box.absmax, head=(y0, y1),
+                                      cv_box=box.box_region())
 
     def live_train_ok(self, n):
         """forward_live_train applies: every BN in train mode with running statistics (test.py:61's
@@ -297,7 +298,7 @@ class CostVolumeReg(nn.Module):
         z = act(self.BN_0, _tconv_region(y2 + y1, B, self.deconv_1_0.weight, full, self.pad)) + y0
         return self.Norm(self.conv_out(z))
 
-    def _forward_live_hip(self, cv, n, B, C2, C3, c4=False, bound=None, head=None):
+    def _forward_live_hip(self, cv, n, B, C2, C3, c4=False, bound=None, head=None, cv_box=(None, None)):
         """forward_live on the HIP kernels: conv_0_0 (csrc/conv3d_narrow.hip), every region conv
         and transposed conv on the fp32 MFMA with channels-last region tensors and the eval BN +
         ReLU fused (csrc/conv3d_region.hip), deconv_1_0 + BN_0 + ReLU + `+ y0` and the `y2 + y1`
@@ -305,9 +306,9 @@ class CostVolumeReg(nn.Module):
         the channel-quad volume, read by conv_0_0 and the three stride-2 convs with 16-byte loads;
         ``bound``: its bound words (the split-fp16 kernels' scale).  ``head``: (y0, y1) from the fused
         head kernel (forward_live_head) -- conv_0_0's and conv_1_0's outputs; cv is then the split
-        volume on conv_2_0's input box only."""
+        volume on conv_2_0's input box only, ``cv_box`` (origin, size) that box."""
         from .ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_k3_split, conv3d_region, conv_s2_split,
-                          deconv3d_k3s2, deconv_out, region_weight, softmax_depth)
+                          deconv3d_k3s2, region_weight, softmax_depth)
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad = list(n), list(self.pad)
@@ -349,8 +350,8 @@ class CostVolumeReg(nn.Module):
                 # conv_1_0 reads the whole volume: LDS-staged split-fp16 kernel (csrc/conv3d_s2_split.hip)
                 ya = conv_s2_split(cv, bound, conv_a.weight, dims, org(halo), size(halo), pad, *bn_eval(bn))
             else:
-                ya = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(halo), size(halo), None,
-                                   None, pad, *bn_eval(bn), in_c4=c4, absmax=bound if split_cv else None)
+                ya = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(halo), size(halo), cv_box[0],
+                                   cv_box[1], pad, *bn_eval(bn), in_c4=c4, absmax=bound if split_cv else None)
             # level 1's output only feeds deconv_1_0's input sum: channels-first for its loads
             return conv3d_region(ya, None, region_weight(conv_b), CONV_S1, dims, org(reg), size(reg),
                                  org(halo), size(halo), None, *bn_eval(bn), out_ncdhw=reg is B)
@@ -364,13 +365,6 @@ class CostVolumeReg(nn.Module):
         if side != main:   # (a stream waiting on itself is an event + barrier packet: a 6 us bubble)
             main.wait_stream(side)
             y0.record_stream(main)
-        if os.environ.get("MVS_DECONV_OUT", "0") == "1":
-            # opt-in: deconv_1_0 + BN_0 + ReLU + y0 and conv_out in one kernel, the 8-channel volume
-            # kept on chip (csrc/deconv_out.hip; bit-identical to the two calls below, but slower at
-            # cfg 2: 1.9 ms against 0.72 -- its per-(c_in, tap row) scalar weight loads are latency-
-            # bound at the one or two workgroups per CU its LDS ring allows)
-            return softmax_depth(deconv_out(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0,
-                                            self.conv_out.weight, x2=y1))
         z = deconv3d_k3s2(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0, x2=y1)
         return softmax_depth(conv3d_k3(z, self.conv_out.weight))
 

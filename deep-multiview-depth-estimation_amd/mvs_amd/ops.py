@@ -260,15 +260,27 @@ class BoundCostVolume:
     channel-quad volume [B, C/4, D, h, w, 4] (cost_volume_c4_absmax) or the split volume (int32,
     cost_volume_c4_split), ``absmax`` its int32[8] bound words (every element <= max|feat|^2; the split
     scale).  The two travel as ONE object, so no copy, view or re-layout of the tensor can separate the
-    volume from its scale (CostVolumeReg.forward raises on a bare split tensor)."""
-    __slots__ = ("data", "absmax")
+    volume from its scale (CostVolumeReg.forward raises on a bare split tensor).
 
-    def __init__(self, data: torch.Tensor, absmax: torch.Tensor):
+    ``box_origin`` (3 ints) marks a PARTIAL volume: ``data`` then holds only the box
+    [box_origin, box_origin + data.shape[2:5]) of a volume of extent ``dims`` -- what the fused head
+    stores (conv_2_0 / conv_3_0's input box); such a volume is read only by the box-aware region conv
+    (box_region()), and quads() / to_ncdhw() refuse it."""
+    __slots__ = ("data", "absmax", "box_origin", "dims")
+
+    def __init__(self, data: torch.Tensor, absmax: torch.Tensor, box_origin=None, dims=None):
         if data.dim() != 6 or data.dtype not in (_F32, torch.int32):
             raise ValueError("channel-quad cost volume [B, C/4, D, h, w, 4] fp32 or int32 expected")
         if absmax.numel() != 8 or absmax.dtype != torch.int32 or absmax.device != data.device:
             raise ValueError("absmax: int32[8] on the volume's device expected")
-        self.data, self.absmax = data, absmax
+        if (box_origin is None) != (dims is None):
+            raise ValueError("a partial volume needs both its box origin and the full dims")
+        if box_origin is not None:
+            box_origin, dims = [int(v) for v in box_origin], [int(v) for v in dims]
+            if len(box_origin) != 3 or len(dims) != 3 or any(
+                    o < 0 or o + s > d for o, s, d in zip(box_origin, data.shape[2:5], dims)):
+                raise ValueError("box %s + %s outside the volume %s" % (box_origin, list(data.shape[2:5]), dims))
+        self.data, self.absmax, self.box_origin, self.dims = data, absmax, box_origin, dims
 
     shape = property(lambda self: self.data.shape)
     dtype = property(lambda self: self.data.dtype)
@@ -279,11 +291,20 @@ class BoundCostVolume:
     def dim(self):
         return self.data.dim()
 
+    partial = property(lambda self: self.box_origin is not None)
+
     def clone(self):
-        return BoundCostVolume(self.data.clone(), self.absmax.clone())
+        return BoundCostVolume(self.data.clone(), self.absmax.clone(), self.box_origin, self.dims)
+
+    def box_region(self):
+        """(origin, size) of the voxels ``data`` holds: the box, or the whole volume."""
+        size = [int(v) for v in self.data.shape[2:5]]
+        return (list(self.box_origin) if self.partial else [0, 0, 0]), size
 
     def quads(self):
         """fp32 channel-quad values (the split volume re-formed to 2^-22 relative)."""
+        if self.partial:
+            raise ValueError("a partial (boxed) cost volume has no values outside its box")
         return unsplit_cost_volume(self.data, self.absmax) if self.split else self.data
 
     def to_ncdhw(self):
@@ -305,8 +326,8 @@ def cost_volume_head(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: to
     §8 f3): warp + variance (homography.py:6-92, costvolume.py:3-16) fused with conv_0_0 + BN_0 + ReLU
     (model.py:101) and conv_1_0 + BN_1 + ReLU (model.py:103) on the split-fp16 matrix cores.  Returns
     (y0 [B, 8, d_count, h, w], y1 channels-last [B, *y1_size, 16], scv, absmax): scv is the split cost
-    volume [B, 8, d_count, h, w, 4] int32 written ONLY on the box [scv_lo, scv_hi) (what conv_2_0 /
-    conv_3_0 read), absmax its bound words.  Bit-identical to cost_volume_c4_split -> conv3d_k3_split /
+    volume on the box [scv_lo, scv_hi) only (what conv_2_0 / conv_3_0 read), int32
+    [B, 8, *(scv_hi - scv_lo), 4]; absmax its bound words.  Bit-identical to cost_volume_c4_split -> conv3d_k3_split /
     conv_s2_split.  C = 32, 2 <= n_views <= 3, d_count even, pad odd; inference only."""
     _require_gpu(feat, "feature_maps")
     lib = _lib.load()
@@ -330,7 +351,8 @@ def cost_volume_head(feat: torch.Tensor, K: torch.Tensor, R: torch.Tensor, T: to
     y0 = torch.empty((batch_size, 8, d_count, h, w), device=dev, dtype=_F32)
     y1 = torch.empty([batch_size] + [int(v) for v in y1_size] + [16], device=dev, dtype=_F32)
     boxed = all(int(hi_) > int(lo_) for lo_, hi_ in zip(scv_lo, scv_hi))
-    scv = torch.empty((batch_size, 8, d_count, h, w, 4) if boxed else (0,), device=dev, dtype=torch.int32)
+    box = [int(hi_) - int(lo_) for lo_, hi_ in zip(scv_lo, scv_hi)]
+    scv = torch.empty([batch_size, 8] + box + [4] if boxed else [0], device=dev, dtype=torch.int32)
     absmax = torch.empty((8,), device=dev, dtype=torch.int32)
     ws = torch.empty((_ws_floats(batch_size, n_views, c, h, w, d_count),), device=dev, dtype=_F32)
     evs = (None, None)
@@ -351,8 +373,9 @@ def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scal
       bn0_mean, w1, bn1_scale, bn1_shift, bn1_mean, pad, y1_origin, y1_size, scv_lo, scv_hi):
     n, c, h, w = feat.shape
     boxed = all(int(hi_) > int(lo_) for lo_, hi_ in zip(scv_lo, scv_hi))
+    box = [int(hi_) - int(lo_) for lo_, hi_ in zip(scv_lo, scv_hi)]
     return (feat.new_empty((batch_size, 8, d_count, h, w)), feat.new_empty([batch_size] + list(y1_size) + [16]),
-            feat.new_empty((batch_size, 8, d_count, h, w, 4) if boxed else (0,), dtype=torch.int32),
+            feat.new_empty([batch_size, 8] + box + [4] if boxed else [0], dtype=torch.int32),
             feat.new_empty((8,), dtype=torch.int32))
 
 
@@ -858,52 +881,6 @@ def _(x, origin, weight, out_dims, pad, bn_scale, bn_shift, bn_mean, residual, x
     return x.new_empty((x.shape[0], 8) + tuple(out_dims))
 
 
-@torch.library.custom_op("mvs::deconv_out", mutates_args=())
-def deconv_out(x: torch.Tensor, origin: list[int], weight: torch.Tensor, out_dims: list[int], pad: list[int],
-               bn_scale: Optional[torch.Tensor], bn_shift: Optional[torch.Tensor], bn_mean: Optional[torch.Tensor],
-               residual: Optional[torch.Tensor], conv_out_weight: torch.Tensor,
-               x2: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """deconv3d_k3s2 (NCDHW region input x (+ x2), BN + ReLU + residual epilogue) followed by conv_out
-    (Conv3d(8, 1, 3, padding 1), conv_out_weight [1, 8, 3, 3, 3]) in one kernel (csrc/deconv_out.hip):
-    [B, 1, D, H, W], bit-identical to conv3d_k3(deconv3d_k3s2(...), conv_out_weight), the 8-channel
-    volume between them never written.  Inference only."""
-    _require_gpu(x, "x")
-    lib = _lib.load()
-    x = x.to(_F32).contiguous()
-    b, cin, rd, rh, rw = x.shape
-    if x2 is not None:
-        x2 = x2.to(_F32).contiguous()
-        if x2.shape != x.shape:
-            raise ValueError("x2 must have x's shape")
-    if tuple(weight.shape) != (cin, 8, 3, 3, 3):
-        raise ValueError("weight [c_in, 8, 3, 3, 3] expected, got %s" % (tuple(weight.shape),))
-    if tuple(conv_out_weight.shape) != (1, 8, 3, 3, 3):
-        raise ValueError("conv_out_weight [1, 8, 3, 3, 3] expected, got %s" % (tuple(conv_out_weight.shape),))
-    w = derived("deconv_taps", (weight,),
-                lambda wt: wt.to(device=x.device, dtype=_F32).reshape(cin, 8, 27).transpose(1, 2).contiguous(),
-                x.device)
-    wo = conv_out_weight.to(device=x.device, dtype=_F32).contiguous()
-    d, h, wd = out_dims
-    f = lambda t: None if t is None else t.to(device=x.device, dtype=_F32).contiguous()
-    sc, sh, mu, res = f(bn_scale), f(bn_shift), f(bn_mean), f(residual)
-    if (sc is None) != (sh is None) or (sc is None) != (mu is None):
-        raise ValueError("bn_scale, bn_shift and bn_mean go together")
-    if res is not None and tuple(res.shape) != (b, 8, d, h, wd):
-        raise ValueError("residual must be [B, 8, D, H, W]")
-    y = torch.empty((b, 1, d, h, wd), device=x.device, dtype=_F32)
-    pt = lambda t: None if t is None else _lib.ptr(t)
-    st = lib.mvs_deconv_out_fwd(_lib.ptr(x), pt(x2), b, cin, rd, rh, rw, *origin, _lib.ptr(w), d, h, wd, *pad,
-                                pt(sc), pt(sh), pt(mu), pt(res), _lib.ptr(wo), _lib.ptr(y),
-                                _lib.stream_handle(x.device))
-    _lib.check(st, "mvs_deconv_out_fwd")
-    return y
-
-
-@deconv_out.register_fake
-def _(x, origin, weight, out_dims, pad, bn_scale, bn_shift, bn_mean, residual, conv_out_weight, x2=None):
-    return x.new_empty((x.shape[0], 1) + tuple(out_dims))
-
-
 # ----------------------------------------------------------------------------------------------
 # mvs::conv3d_region -- the regulariser's region convolutions on the fp32 MFMA (model.py:101-121)
 # ----------------------------------------------------------------------------------------------
@@ -967,7 +944,8 @@ def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Ten
                   bn_mean: Optional[torch.Tensor] = None, out_ncdhw: bool = False,
                   in_c4: bool = False, absmax: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Region convolution (mvs_conv3d_region_fwd): mode CONV_S2 reads the full NCDHW volume x
-    (in_c4: the channel-quad [B, C/4, D, H, W, 4] of cost_volume_c4, or bf16 of cost_volume_c4_bf16),
+    (in_c4: the channel-quad [B, C/4, D, H, W, 4] of cost_volume_c4, or bf16 of cost_volume_c4_bf16;
+    with in_origin / in_size, x holds only that box of the volume: the fused head's stored box),
     CONV_S1 / CONV_T2 a channels-last region tensor x (+ x2) on in_origin + [0, in_size); returns the
     channels-last region tensor [B, *out_size, c_out] ([B, c_out, *out_size] with out_ncdhw), eval
     BN + ReLU fused when bn_* are given.  ``weight`` is region_weight(module).  Inference only."""

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 12
+#define MVS_ABI_VERSION 13
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -348,8 +348,9 @@ int mvs_conv3d_s2_split_weights(const float* weight, unsigned short* frag, int* 
  *     into scv (the input box of the regulariser's conv_2_0 / conv_3_0; scv NULL: nothing stored);
  *   feat_absmax: 8 bound words (DEVICE), written as mvs_cost_volume_fwd_c4_absmax does;
  *   y0: [batch][8][d_count][h][w] fp32 = relu(BN_0(conv_0_0(cv))); y1: channels-last region
- *     [batch][y1_size...][16] fp32 = relu(BN_1(conv_1_0(cv))); scv: [batch][8][d_count][h][w] x 16 B
- *     (full-size allocation, 16-byte aligned; only the box is written).
+ *     [batch][y1_size...][16] fp32 = relu(BN_1(conv_1_0(cv))); scv: the box only,
+ *     [batch][8][hi0 - lo0][hi1 - lo1][hi2 - lo2] x 16 B, 16-byte aligned (read back by
+ *     mvs_conv3d_region_fwd with in_origin = scv_lo, in_size = scv_hi - scv_lo).
  * 128 * d_count * h * w <= 2^32 - 16.  Events (either may be NULL) are recorded around the fused kernel. */
 int mvs_cost_volume_head_fwd(const float* feat, const float* K, const float* R, const float* T,
                              const float* d_min, const float* d_int, int batch_size, int n_views,
@@ -397,20 +398,6 @@ int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch,
                           const float* bn_shift, const float* bn_mean, const float* residual, float* y,
                           void* stream);
 
-/* Regulariser layers deconv_1_0 + BN_0 + ReLU + `+ y0` and conv_out in ONE launch (model.py:121-125,
- * eval-mode inference): mvs_deconv3d_k3s2_fwd's NCDHW form (x[batch][c_in][rd][rh][rw] region input on
- * [x0, x0 + r) per dim, x2 nullable and added on load, weight_taps[c_in][27][8] tap-major as with
- * MVS_DECONV_WEIGHT_TAPS, padding (pd, ph, pw), BN pointers all or none, residual nullable) followed by
- * nn.Conv3d(8, 1, 3, padding=1, bias=False) with conv_out_weight[1][8][3][3][3], into
- * out[batch][1][d][h][w] fp32.  The 8-channel volume between the two layers is never written: the
- * kernel forms it per tile in LDS.  Bit-identical to mvs_deconv3d_k3s2_fwd followed by
- * mvs_conv3d_k3_fwd (same products, same order).  c_in <= 64; batch*c_in*rd*rh*rw*4 < 2^31 and
- * batch*8*d*h*w*4 < 2^32 - 16 (MVS_ERR_TOO_LARGE).  Replaces the two calls at model.py:121 and :125. */
-int mvs_deconv_out_fwd(const float* x, const float* x2, int batch, int c_in, int rd, int rh, int rw, int x0d,
-                       int x0h, int x0w, const float* weight_taps, int d, int h, int w, int pd, int ph, int pw,
-                       const float* bn_scale, const float* bn_shift, const float* bn_mean, const float* residual,
-                       const float* conv_out_weight, float* out, void* stream);
-
 /* mvs_conv3d_region_fwd modes */
 #define MVS_CONV_S1 0   /* Conv3d 3x3x3, stride 1, padding 1: region -> region                     */
 #define MVS_CONV_S2 1   /* Conv3d 3x3x3, stride 2, padding pad: full NCDHW volume -> region         */
@@ -427,7 +414,9 @@ int mvs_deconv_out_fwd(const float* x, const float* x2, int batch, int c_in, int
  * y[batch][out_size[0]][out_size[1]][out_size[2]][c_out] holding voxels out_origin + [0, out_size)
  * (flags = MVS_CONV_OUT_NCDHW: channels-first y[batch][c_out][out_size...]).
  * Input: MVS_CONV_S2 the full cost volume x[batch][c_in][D][H][W] (reads 2 o - pad + t, zero outside
- * the volume); MVS_CONV_S1 / MVS_CONV_T2 a channels-last region tensor
+ * the volume) -- or, with in_origin / in_size given, only the box in_origin + [0, in_size) of it,
+ * x[batch][c_in][in_size...] (the caller guarantees the box holds every in-volume voxel the outputs
+ * read: voxels off the box read zero); MVS_CONV_S1 / MVS_CONV_T2 a channels-last region tensor
  * x[batch][in_size...][c_in] on in_origin + [0, in_size) (S1: o + t - 1; T2: i = (o + pad - t) / 2 for
  * t of o + pad's parity; voxels outside the volume or the input region read zero), plus x2 (same
  * geometry, nullable) added on load.  Weights transposed to weight[27][c_out][c_in] (tap =

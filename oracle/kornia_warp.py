@@ -88,6 +88,18 @@ def warp_perspective(src: torch.Tensor, M: torch.Tensor, dsize, mode: str = "bil
     h_out, w_out = dsize
     dst_norm_T_src_norm = normalize_homography(M, (H, W), (h_out, w_out))
     src_norm_T_dst_norm = torch.inverse(dst_norm_T_src_norm)
+    return warp_normalized(src, src_norm_T_dst_norm, dsize, mode, padding_mode, align_corners)
+
+
+def warp_normalized(src: torch.Tensor, G: torch.Tensor, dsize, mode: str = "bilinear",
+                    padding_mode: str = "zeros", align_corners: bool = True) -> torch.Tensor:
+    """The second half of ``warp_perspective``: sample ``src`` through a GIVEN normalised sampling
+    matrix ``G = src_norm_T_dst_norm`` (B x 3 x 3, src's dtype) -- kornia's meshgrid,
+    ``transform_points`` and ``grid_sample`` exactly as above.  Lets a test hand the oracle the
+    matrices the HIP kernels formed (fp64 algebra, stored fp32), isolating the sampling arithmetic
+    from the reference's fp32 homography composition."""
+    B = src.shape[0]
+    h_out, w_out = dsize
     grid = create_meshgrid(h_out, w_out, device=src.device, dtype=src.dtype).repeat(B, 1, 1, 1)
-    grid = transform_points(src_norm_T_dst_norm[:, None, None], grid)
+    grid = transform_points(G[:, None, None], grid)
     return F.grid_sample(src, grid, mode=mode, padding_mode=padding_mode, align_corners=align_corners)

@@ -32,7 +32,7 @@ import torch
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from kornia_warp import warp_perspective  # noqa: E402
+from kornia_warp import warp_normalized, warp_perspective  # noqa: E402
 
 D_SCALE = 25      # scripts/config.py:6
 N_DEPTH_EST = 5   # scripts/config.py:9
@@ -72,23 +72,50 @@ def plane_homographies(K, R, T, d_batch, ref_idx, img_idx, d_num):
     return torch.matmul(left, torch.matmul(plane, right))
 
 
+def sampling_matrices64(K_batch, R_batch, T_batch, d_min, d_int, batch_size, n_views, d_num, h, w,
+                        d_scale=D_SCALE):
+    """The per-(image, plane) normalised sampling matrix ``G = inv(N H N^-1)`` that kornia's
+    ``warp_perspective`` forms (homography.py:40-75 for H, kornia 0.6.3 ``normalize_homography`` +
+    ``inverse``), composed and inverted in FLOAT64 instead of the reference's fp32 -- the planes
+    themselves are the reference's fp32 ``d_batch`` (homography.py:24-26).  Returns float64
+    [N, D, 3, 3].  Used by ``homography_warping(..., hom64=True)`` to separate the reference's fp32
+    homography rounding from the rest of its arithmetic (tests/golden/make_cfg5_oracle.py)."""
+    d_batch = torch.tile(depth_planes(d_min, d_int, d_num, d_scale), (n_views, 1, 1, 1))
+    _, ref_idx, img_idx = view_indices(batch_size, n_views)
+    H = plane_homographies(K_batch.double(), R_batch.double(), T_batch.double(), d_batch.double(),
+                           ref_idx, img_idx, d_num)
+    n_src = torch.tensor([[2.0 / (w - 1), 0.0, -1.0], [0.0, 2.0 / (h - 1), -1.0], [0.0, 0.0, 1.0]],
+                         dtype=torch.float64)
+    return torch.inverse(n_src @ (H @ torch.inverse(n_src)))
+
+
 def homography_warping(K_batch, R_batch, T_batch, d_min, d_int, feature_maps, batch_size,
-                       n_views, d_num, d_scale=D_SCALE, concat_growth=True):
+                       n_views, d_num, d_scale=D_SCALE, concat_growth=True, hom64=False):
     """homography.py:6-92 restated.  Returns (warped [N,C,D,h,w], d_batch_0 [B,D,1,1], ref_idx_0).
 
     ``concat_growth=True`` keeps the reference's O(D^2) ``torch.cat`` accumulation (:83-90) -- the
-    timed CPU baseline; ``False`` stacks the same per-plane results (same values, test speed)."""
+    timed CPU baseline; ``False`` stacks the same per-plane results (same values, test speed).
+    ``hom64=True`` (NOT the reference: a diagnostic variant) samples through the float64-composed
+    sampling matrices rounded once to fp32 (``sampling_matrices64``), everything after them -- the
+    meshgrid, ``transform_points``, ``grid_sample`` -- the reference's fp32 ops unchanged."""
     d_batch_0 = depth_planes(d_min, d_int, d_num, d_scale)
     d_batch = torch.tile(d_batch_0, (n_views, 1, 1, 1))
     ref_idx_0, ref_idx, img_idx = view_indices(batch_size, n_views)
-    H = plane_homographies(K_batch.float(), R_batch.float(), T_batch.float(), d_batch,
-                           ref_idx, img_idx, d_num)
     hw = tuple(feature_maps.shape[-2:])
+    if hom64:
+        G = sampling_matrices64(K_batch, R_batch, T_batch, d_min, d_int, batch_size, n_views, d_num,
+                                hw[0], hw[1], d_scale).float()
+    else:
+        H = plane_homographies(K_batch.float(), R_batch.float(), T_batch.float(), d_batch,
+                               ref_idx, img_idx, d_num)
     src = feature_maps[img_idx]
     planes = []
     warped = None
     for k in range(d_num):
-        cur = warp_perspective(src, H[:, k], hw, align_corners=False).unsqueeze(2)
+        if hom64:
+            cur = warp_normalized(src, G[:, k], hw, align_corners=False).unsqueeze(2)
+        else:
+            cur = warp_perspective(src, H[:, k], hw, align_corners=False).unsqueeze(2)
         if concat_growth:
             warped = cur if warped is None else torch.cat((warped, cur), 2)
         else:
@@ -115,13 +142,14 @@ def extract_depth_map(prob_volume, d_batch, n_est=N_DEPTH_EST):
 
 
 def mvsnet_forward(model, nn_input, K_batch, R_batch, T_batch, d_min, d_int, batch_size, n_views,
-                   d_num, feat_hw, d_scale=D_SCALE, concat_growth=False):
+                   d_num, feat_hw, d_scale=D_SCALE, concat_growth=False, hom64=False):
     """model.py:168-207 on the CPU with the oracle hot path.  ``model`` supplies the three nn
-    sub-modules (feature_encoder, cost_volume_reg, depthmap_refine) -- plain torch layers."""
+    sub-modules (feature_encoder, cost_volume_reg, depthmap_refine) -- plain torch layers.
+    ``hom64``: see ``homography_warping`` (diagnostic variant, not the reference)."""
     feats = model.feature_encoder(nn_input)
     warped, d_batch, ref_views = homography_warping(K_batch, R_batch, T_batch, d_min, d_int, feats,
                                                     batch_size, n_views, d_num, d_scale,
-                                                    concat_growth=concat_growth)
+                                                    concat_growth=concat_growth, hom64=hom64)
     cv = assemble_cost_volume(warped, n_views)
     reg = model.cost_volume_reg
     # the reference's op sequence (model.py:100-126) over the whole volume: the build's

@@ -18,6 +18,13 @@ D=256, eval BN) on the test's weights and seed-2001 images, and commits
 The variance is formed in depth chunks of assemble_cost_volume's own expression (elementwise per
 voxel, so bit-identical to the one-shot call) to keep the peak near 25 GB; ~15 min on 8 cores.
 Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_cfg5_oracle.py
+
+``--hom64`` (VERDICT r4 "next" 1a) writes cfg5_oracle_h64.npz instead: the same forward with the
+per-(image, plane) sampling matrices composed and inverted in FLOAT64 and rounded once to fp32
+(mvs_oracle.homography_warping(hom64=True)), every later op the reference's fp32 one.  It tests the
+stated cause of the cfg-5 residue -- the reference's fp32 homography (homography.py:40-75 + kornia's
+normalize / inverse) at 4.8x cfg 2's pixel coordinates -- and also records how far the two oracles
+are from each other (the reference's own homography rounding, in depth).
 """
 import os
 import sys
@@ -32,7 +39,8 @@ for sub in ("deep-multiview-depth-estimation_amd", "oracle", os.path.join("tests
     if os.path.join(REPO, sub) not in sys.path:
         sys.path.insert(0, os.path.join(REPO, sub))
 
-OUT = os.path.join(HERE, "cfg5_oracle.npz")
+HOM64 = "--hom64" in sys.argv[1:]
+OUT = os.path.join(HERE, "cfg5_oracle_h64.npz" if HOM64 else "cfg5_oracle.npz")
 GEOM = (1, 3, 256, 1184, 1600)   # B, V, D, image H, W
 N_SAMPLES = 4096
 
@@ -61,7 +69,7 @@ def sample_voxels(D, h, w, n=N_SAMPLES, seed=5):
 
 def main():
     import mvs_oracle
-    from make_cfg2_selfnoise import SIG_P, kept_with_p, kept_planes
+    from make_cfg2_selfnoise import SIG_P, kept_with_p, kept_planes, significant_flips
     B, V, D, H, W = GEOM
     h, w = H // 4, W // 4
     torch.set_num_threads(os.cpu_count() or 8)
@@ -70,7 +78,7 @@ def main():
     with torch.no_grad():
         feats = net.feature_encoder(img)
         warped, d_batch, _ = mvs_oracle.homography_warping(K, R, T, d_min, d_int, feats, B, V, D,
-                                                           concat_growth=False)
+                                                           concat_growth=False, hom64=HOM64)
         print("warp %.0f s" % (time.time() - t0), flush=True)
         x = warped.reshape(B, V, 32, D, h, w)
         cv = torch.empty((B, 32, D, h, w))
@@ -88,8 +96,21 @@ def main():
     keep, p = kept_with_p(P)
     tie = (kept_planes(P, stable=False) != keep).any(0)
     pz, py, px = sample_voxels(D, h, w)
+    extra = {}
+    if HOM64:   # the fp32-homography oracle (the reference) against this one, on the same pixels
+        ref = np.load(os.path.join(HERE, "cfg5_oracle.npz"))
+        d64, d32 = ini[0, 0].numpy().astype(np.float64), ref["ini"].astype(np.float64)
+        flip = significant_flips(ref["keep"], ref["sig"].astype(np.float32), keep, (p >= SIG_P).astype(np.float32))
+        flip |= ref["tie"] | tie
+        rel = np.abs(d32 - d64) / np.abs(d64)
+        extra = dict(ref_vs_h64_flip_frac=np.float64(flip.mean()),
+                     ref_vs_h64_within_1e4_unflipped=np.float64((rel[~flip] <= 1e-4).mean()),
+                     ref_vs_h64_max_rel_unflipped=np.float64(rel[~flip].max()))
+        print("fp32-homography oracle vs this: flips %.4f %%, unflipped within 1e-4 %.5f, max rel %.3g" % (
+            100 * extra["ref_vs_h64_flip_frac"], extra["ref_vs_h64_within_1e4_unflipped"],
+            extra["ref_vs_h64_max_rel_unflipped"]))
     np.savez_compressed(OUT, ini=ini[0, 0].numpy().astype(np.float32), keep=keep, sig=p >= SIG_P, tie=tie,
-                        pz=pz, py=py, px=px, pv=P[pz, py, px].astype(np.float32))
+                        pz=pz, py=py, px=px, pv=P[pz, py, px].astype(np.float32), **extra)
     print("tie pixels %.4f %%; wrote %s (%d bytes), %.0f s" % (100 * tie.mean(), OUT, os.path.getsize(OUT),
                                                           time.time() - t0))
 

@@ -52,6 +52,23 @@ def test_bound_cost_volume_travels_with_its_bound():
         BoundCostVolume(q, torch.zeros(4, dtype=torch.int32))
 
 
+def test_partial_cost_volume_refuses_whole_volume_views():
+    """CPU: a boxed (partial) volume -- what the fused head stores -- keeps its box through clone()
+    and raises instead of returning values it does not hold (no silent uninitialised data)."""
+    from mvs_amd.ops import BoundCostVolume
+    q = torch.zeros(1, 8, 3, 4, 5, 4, dtype=torch.int32)
+    b = BoundCostVolume(q, torch.zeros(8, dtype=torch.int32), [1, 2, 3], [8, 8, 8])
+    assert b.partial and b.box_region() == ([1, 2, 3], [3, 4, 5])
+    assert b.clone().box_region() == b.box_region()
+    for f in (b.quads, b.to_ncdhw):
+        with pytest.raises(ValueError, match="partial"):
+            f()
+    with pytest.raises(ValueError, match="outside"):
+        BoundCostVolume(q, torch.zeros(8, dtype=torch.int32), [6, 0, 0], [8, 8, 8])
+    with pytest.raises(ValueError):
+        BoundCostVolume(q, torch.zeros(8, dtype=torch.int32), [0, 0, 0], None)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,V,D,h,w", [(2, 3, 16, 32, 48), (1, 2, 20, 24, 40), (1, 3, 100, 36, 44),
                                        (2, 3, 48, 28, 64), (1, 2, 20, 25, 32), (1, 3, 16, 29, 41)])
@@ -91,7 +108,8 @@ def test_head_is_bit_equal_to_the_split_path(B, V, D, h, w):
     assert torch.equal(y0, y0_ref), (y0 - y0_ref).abs().max().item()
     assert torch.equal(y1, y1_ref), (y1 - y1_ref).abs().max().item()
     sl = (slice(None), slice(None)) + tuple(slice(a, b) for a, b in zip(lo, hi))
-    assert torch.equal(box[sl], scv[sl])
+    assert list(box.shape) == [B, 8] + [b - a for a, b in zip(lo, hi)] + [4]   # only the box is allocated
+    assert torch.equal(box, scv[sl])
     # without BN epilogues (raw convolution values) as well
     with torch.no_grad():
         y0n, y1n, _, _ = ops.cost_volume_head(feat, K, R, T, d_min, d_int, B, V, 0, D, 25.0, w0, None, None, None,

@@ -735,42 +735,6 @@ def test_region_deconv_channels_last_with_addend():
     assert torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("n", [(13, 10, 17), (14, 11, 22), (48, 32, 40), (20, 37, 70), (96, 64, 80)])
-def test_deconv_out_equals_deconv_then_conv_out(n):
-    """mvs::deconv_out (csrc/deconv_out.hip: deconv_1_0 + BN_0 + ReLU + y0 and conv_out in one kernel,
-    the 8-channel volume kept on chip) is BIT-EQUAL to mvs::deconv3d_k3s2 followed by mvs::conv3d_k3
-    (model.py:121-125 as the two-kernel path runs it): pad classes odd and even per dim (n mod 4),
-    widths / heights / depths not multiples of the 32 x 16 x 32 tile, with and without the BN
-    epilogue, residual and addend."""
-    from mvs_amd.config import pad_outpad
-    from mvs_amd.model import _tconv_input_region
-    from mvs_amd.ops import conv3d_k3, deconv3d_k3s2, deconv_out
-    pad, _ = pad_outpad(*n)
-    reg = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
-    org = [lo for lo, _ in reg]
-    g = torch.Generator().manual_seed(sum(n))
-    r = [hi - lo + 1 for lo, hi in reg]
-    a, b = torch.randn(2, 16, *r, generator=g).to(DEV), torch.randn(2, 16, *r, generator=g).to(DEV)
-    wt = (torch.randn(16, 8, 3, 3, 3, generator=g) * 0.1).to(DEV)
-    wo = (torch.randn(1, 8, 3, 3, 3, generator=g) * 0.1).to(DEV)
-    sc, sh, mu = (t.to(DEV) for t in _bn_params(8, g))
-    y0 = torch.randn(2, 8, *n, generator=g).to(DEV)
-    with torch.no_grad():
-        ref = conv3d_k3(deconv3d_k3s2(a, org, wt, list(n), list(pad), sc, sh, mu, y0, x2=b), wo)
-        got = deconv_out(a, org, wt, list(n), list(pad), sc, sh, mu, y0, wo, x2=b)
-        assert got.shape == ref.shape == (2, 1) + tuple(n)
-        assert torch.equal(got, ref), (got - ref).abs().max().item()
-        ref = conv3d_k3(deconv3d_k3s2(a, org, wt, list(n), list(pad), None, None, None, None), wo)
-        got = deconv_out(a, org, wt, list(n), list(pad), None, None, None, None, wo)
-        assert torch.equal(got, ref), (got - ref).abs().max().item()
-
-
-def _to_c4(x):
-    """[B, C, D, H, W] -> channel-quad [B, C/4, D, H, W, 4]."""
-    b, c = x.shape[:2]
-    return x.reshape((b, c // 4, 4) + tuple(x.shape[2:])).permute(0, 1, 3, 4, 5, 2).contiguous()
-
-
 @pytest.mark.parametrize("nv,shape", [(3, (2, 32, 24, 64, 80)), (2, (1, 8, 7, 37, 53)), (5, (1, 16, 9, 20, 36)),
                                       (8, (1, 4, 3, 16, 16))])
 def test_channel_quad_cost_volume_is_the_same_values(nv, shape):
@@ -1042,3 +1006,38 @@ def test_depth_hypotheses_kernel_equals_torch_expression(D, scale):
     assert got.shape == ref.shape
     assert torch.equal(got, ref)
     assert torch.equal(got, gpu_expr)
+
+
+@pytest.mark.parametrize("geom", [(2, 3, 8, 128, 160), (1, 5, 4, 64, 80), (1, 3, 4, 296, 400), (1, 9, 2, 32, 40)])
+def test_cost_volume_bit_exact_vs_oracle_given_matrices(geom):
+    """The HIP warp + variance equals the reference's torch CPU arithmetic BIT FOR BIT once both sample
+    through the same matrices: the oracle's kornia meshgrid -> transform_points (torch.bmm) ->
+    grid_sample -> costvolume.py expression (oracle/kornia_warp.py::warp_normalized,
+    mvs_oracle.assemble_cost_volume), fed the sampling matrices the HIP prologue formed (fp64
+    algebra, stored fp32: the op's workspace).  The one remaining difference from the reference is
+    those matrices (fp32 composition there; tests/golden/make_cfg5_oracle.py --hom64 measures it).
+    V = 3 and 5 run the staged kernel (and the warp-only kernel), V = 9 the generic one; the
+    channel-quad / split / fused-head paths are bit-equal to this output (test_cv_head.py and the
+    channel-quad tests)."""
+    import kornia_warp
+    import mvs_oracle
+    from cameras import camera_batch, depth_range
+    from mvs_amd import ops
+    B, V, D, h, w = geom
+    K, R, T = camera_batch(B, V, h, w)
+    d_min, d_int = depth_range(B)
+    feat = torch.randn(B * V, 32, h, w, generator=torch.Generator().manual_seed(sum(geom)))
+    cv, ws = ops.cost_volume(feat.to(DEV), K, R, T, d_min, d_int, B, V, 0, D, 25.0)
+    warped_gpu = ops.homography_warp(feat.to(DEV), K, R, T, d_min, d_int, B, V, 0, D, 25.0)
+    torch.cuda.synchronize()
+    G = ws[:B * V * D * 9].view(B * V, D, 3, 3).cpu()
+    # the matrices: fp64 algebra rounded once -- equal to the oracle's float64 composition rounded to
+    # fp32 up to the last bit of an fp64 reordering
+    G64 = mvs_oracle.sampling_matrices64(K, R, T, d_min, d_int, B, V, D, h, w)
+    assert ((G.double() - G64).abs() <= 2 * torch.finfo(torch.float32).eps * G64.abs() + 1e-30).all()
+    with torch.no_grad():
+        warped = torch.stack([kornia_warp.warp_normalized(feat, G[:, k], (h, w), align_corners=False)
+                              for k in range(D)], 2)
+        cv_ref = mvs_oracle.assemble_cost_volume(warped, V)
+    assert torch.equal(warped_gpu.cpu(), warped), (warped_gpu.cpu() != warped).float().mean()
+    assert torch.equal(cv.cpu(), cv_ref), (cv.cpu() != cv_ref).float().mean()

@@ -1,0 +1,190 @@
+"""CPU: the fp32 law of the HIP sampling and variance helpers, pinned bit for bit against the
+reference's own torch CPU ops (the oracle's kornia 0.6.3 restatement + torch.bmm + F.grid_sample,
+and costvolume.py's expression).
+
+``deep-multiview-depth-estimation_amd/csrc/common.h`` (sample_coord, bilerp_sum, div_views,
+variance_law) and ``packed.h`` (bilerp, variance_law4) write every rounding step explicitly
+(contraction off, fused steps as explicit fmas).  The functions below restate those exact steps in
+numpy with a correctly rounded fp32 fma; each test asserts that the restatement equals what torch
+computes on the CPU -- the reference's numerics -- on every element.  The GPU side of the same
+identity (HIP cost volume == the oracle's warp through the HIP kernels' own sampling matrices,
+torch.equal) is tests/test_gpu_parity.py::test_cost_volume_bit_exact_vs_oracle_given_matrices.
+
+What this does not cover: the sampling matrices themselves (the HIP prologue composes and inverts
+them in fp64, the reference in fp32 -- DESIGN.md §4, tests/golden/make_cfg5_oracle.py --hom64).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import kornia_warp
+import mvs_oracle
+from cameras import camera_batch, depth_range
+
+f32 = np.float32
+
+
+def fma32(a, b, c):
+    """Correctly rounded fp32 fma(a, b, c), elementwise.  a*b is exact in float64 and TwoSum makes
+    hi + lo == a*b + c exactly; rounding hi to fp32 differs from rounding the exact value only when hi
+    is exactly an fp32 midpoint and lo != 0 -- then lo's sign picks the neighbour."""
+    a, b, c = (np.asarray(x, np.float32).astype(np.float64) for x in np.broadcast_arrays(a, b, c))
+    p = a * b
+    hi = p + c
+    bb = hi - p
+    lo = (p - (hi - bb)) + (c - bb)
+    r = hi.astype(np.float32)
+    r64 = r.astype(np.float64)
+    other = np.nextafter(r, np.where(hi > r64, np.float32(np.inf), np.float32(-np.inf)).astype(np.float32))
+    mid = (r64 != hi) & (hi == (r64 + other.astype(np.float64)) / 2)
+    r = np.where(mid & (lo > 0), np.maximum(r, other), r)
+    r = np.where(mid & (lo < 0), np.minimum(r, other), r)
+    return r.astype(np.float32)
+
+
+def test_fma32_is_a_correctly_rounded_fma():
+    # midpoint cases: 1 + 2^-24 is the midpoint of 1 and 1 + 2^-23; a tiny product decides
+    one = f32(1.0)
+    # 1 + 2^-24 is the midpoint of 1 and 1 + 2^-23: fma(x, y, 1) just above, just below and on it
+    x = f32(2.0 ** -12)
+    assert fma32(x, f32(2.0 ** -12 + 2.0 ** -35), one) == f32(1.0 + 2.0 ** -23)   # above the midpoint
+    assert fma32(x, f32(2.0 ** -12 - 2.0 ** -36), one) == one                      # below it
+    assert fma32(x, x, one) == one                                                 # exact tie -> even
+    rng = np.random.default_rng(0)
+    a, b, c = (rng.standard_normal(100000).astype(np.float32) for _ in range(3))
+    from fractions import Fraction
+    for i in range(0, 100000, 9973):
+        exact = Fraction(float(a[i])) * Fraction(float(b[i])) + Fraction(float(c[i]))
+        r = fma32(a[i:i + 1], b[i:i + 1], c[i:i + 1])[0]
+        cands = [np.nextafter(r, f32(-np.inf)), r, np.nextafter(r, f32(np.inf))]
+        errs = [abs(Fraction(float(v)) - exact) for v in cands]
+        assert errs[1] <= min(errs), i
+
+
+def norm_coord(n):
+    """kornia create_meshgrid: (x / (n - 1) - 0.5) * 2 (common.h norm_coord)."""
+    x = np.arange(n, dtype=np.float32)
+    return ((x / f32(n - 1)) - f32(0.5)) * f32(2)
+
+
+def sample_coord(G, xn, yn, h, w):
+    """common.h sample_coord: u = fma(yn, G1, xn*G0) + G2 (torch.bmm on MKL), dehomogenise as kornia,
+    unnormalise as ATen's vectorised grid_sample: ix = fma(u + 1, w/2, -0.5)."""
+    def row(r):
+        return fma32(yn, G[3 * r + 1], xn * G[3 * r]) + G[3 * r + 2]
+    u, v, s = row(0), row(1), row(2)
+    div = np.abs(s) > f32(1e-8)
+    sc = f32(1) / (s + f32(1e-8))
+    u = np.where(div, u * sc, u).astype(np.float32)
+    v = np.where(div, v * sc, v).astype(np.float32)
+    ix = fma32(u + f32(1), f32(0.5) * f32(w), f32(-0.5))
+    iy = fma32(v + f32(1), f32(0.5) * f32(h), f32(-0.5))
+    return ix, iy
+
+
+def sample_law(img, ix, iy):
+    """common.h tap_weights + bilerp_sum: nw = (1-wy)(1-wx) ..., t0*nw then fma over ne, sw, se;
+    taps outside the image read 0 (the HIP kernels' zero padding)."""
+    c, h, w = img.shape
+    fx, fy = np.floor(ix), np.floor(iy)
+    wx, wy = (ix - fx).astype(np.float32), (iy - fy).astype(np.float32)
+    ex, ny = f32(1) - wx, f32(1) - wy
+    wt = [ny * ex, ny * wx, wy * ex, wy * wx]
+
+    def tap(dx, dy):
+        xx, yy = fx + dx, fy + dy
+        ok = (xx >= 0) & (xx < w) & (yy >= 0) & (yy < h)
+        xi = np.where(ok, xx, 0).astype(np.int64)
+        yi = np.where(ok, yy, 0).astype(np.int64)
+        return np.where(ok[None], img[:, yi, xi], f32(0)).astype(np.float32)
+    t = [tap(0, 0), tap(1, 0), tap(0, 1), tap(1, 1)]
+    return fma32(t[3], wt[3], fma32(t[2], wt[2], fma32(t[1], wt[1], t[0] * wt[0])))
+
+
+def _matrices(B, V, D, h, w):
+    """The oracle's fp32 G (kornia normalize_homography + inverse of the reference's fp32 H) and the
+    float64-composed G rounded to fp32 (what the HIP prologue stores) at the cfg cameras."""
+    K, R, T = camera_batch(B, V, h, w)
+    d_min, d_int = depth_range(B)
+    d_batch = torch.tile(mvs_oracle.depth_planes(d_min, d_int, D), (V, 1, 1, 1))
+    _, ref_idx, img_idx = mvs_oracle.view_indices(B, V)
+    H = mvs_oracle.plane_homographies(K.float(), R.float(), T.float(), d_batch, ref_idx, img_idx, D)
+    G32 = torch.stack([torch.inverse(kornia_warp.normalize_homography(H[:, k], (h, w), (h, w)))
+                       for k in range(D)], 1)
+    G64 = mvs_oracle.sampling_matrices64(K, R, T, d_min, d_int, B, V, D, h, w).float()
+    return G32, G64
+
+
+@pytest.mark.parametrize("geom", [(1, 3, 6, 128, 160), (1, 3, 4, 296, 400), (1, 5, 3, 37, 53)])
+def test_sampling_law_is_torch_cpu_bitwise(geom):
+    """The oracle's warp (kornia meshgrid -> transform_points (torch.bmm) -> grid_sample) equals the
+    HIP law restated above on every element, for both kinds of sampling matrix."""
+    B, V, D, h, w = geom
+    torch.manual_seed(7)
+    feat = torch.randn(B * V, 8, h, w)
+    xn, yn = norm_coord(w)[None, :], norm_coord(h)[:, None]
+    for G in _matrices(B, V, D, h, w):
+        for k in range(D):
+            for i in range(B * V):
+                g = G[i, k].numpy().astype(np.float32).ravel()
+                want = kornia_warp.warp_normalized(feat[i:i + 1], G[i:i + 1, k], (h, w),
+                                                   align_corners=False)[0].numpy()
+                ix, iy = sample_coord(g, xn, yn, h, w)
+                got = sample_law(feat[i].numpy(), ix, iy)
+                assert np.array_equal(got, want), (geom, k, i, np.mean(got != want))
+
+
+def test_contracted_or_reordered_laws_are_not_torch():
+    """The same check fails for the point transform the HIP helpers used before round 5
+    (fma(G1, yn, fma(G0, xn, G2))): the test can tell the laws apart."""
+    B, V, D, h, w = 1, 3, 2, 128, 160
+    G = _matrices(B, V, D, h, w)[1]
+    feat = torch.randn(B * V, 8, h, w, generator=torch.Generator().manual_seed(3))
+    xn, yn = norm_coord(w)[None, :], norm_coord(h)[:, None]
+    g = G[1, 1].numpy().astype(np.float32).ravel()
+    want = kornia_warp.warp_normalized(feat[1:2], G[1:2, 1], (h, w), align_corners=False)[0].numpy()
+    u = fma32(yn, g[1], fma32(xn, g[0], g[2]))
+    v = fma32(yn, g[4], fma32(xn, g[3], g[5]))
+    s = fma32(yn, g[7], fma32(xn, g[6], g[8]))
+    sc = f32(1) / (s + f32(1e-8))
+    ix = fma32(u * sc + f32(1), f32(w / 2), f32(-0.5))
+    iy = fma32(v * sc + f32(1), f32(h / 2), f32(-0.5))
+    assert not np.array_equal(sample_law(feat[1].numpy(), ix, iy), want)
+
+
+def variance_law(x):
+    """common.h variance_law / packed.h variance_law4 over axis 0: view sum in order, mean = sum / V,
+    cv = (sum of (x - mean)^2 in order) / V, every op rounded on its own, divisions correctly rounded."""
+    V = x.shape[0]
+    s = x[0]
+    for v in range(1, V):
+        s = s + x[v]
+    mean = (s.astype(np.float64) / V).astype(np.float32)
+    acc = (x[0] - mean) * (x[0] - mean)
+    for v in range(1, V):
+        d = x[v] - mean
+        acc = acc + d * d
+    return (acc.astype(np.float64) / V).astype(np.float32)
+
+
+@pytest.mark.parametrize("V", [2, 3, 5, 9, 16])
+def test_variance_law_is_costvolume_py_bitwise(V):
+    """Per sample the reduced tensor's inner size C*D*h*w is a multiple of 32 here, as in every real
+    cost volume (C = 32): torch's vectorised reduction then sums the views in order for every
+    element.  (Only a scalar tail of < 32 elements, which no C = 32 volume has, uses four
+    interleaved accumulators for V >= 5.)"""
+    torch.manual_seed(V)
+    warped = torch.randn(2 * V, 4, 3, 16, 16) * torch.rand(2 * V, 4, 1, 1, 1) * 10
+    cv = mvs_oracle.assemble_cost_volume(warped, V).numpy()
+    x = warped.numpy().reshape(2, V, 4, 3, 16, 16).transpose(1, 0, 2, 3, 4, 5)
+    assert np.array_equal(variance_law(x), cv)
+    # the multiply-by-reciprocal / fused form the kernels used before round 5 differs (V = 3, 5, 9)
+    if V in (3, 5, 9):
+        r = f32(1.0 / V)
+        s = x.sum(0, dtype=np.float32)
+        mean = s * r
+        acc = np.zeros_like(mean)
+        for v in range(V):
+            acc = fma32(x[v] - mean, x[v] - mean, acc)
+        assert not np.array_equal(acc * r, cv)

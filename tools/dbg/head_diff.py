@@ -59,7 +59,7 @@ for (B, V, D, h, w) in CFGS:
     if bad1.any():
         print("  y1 z", bad1.any(4).any(3).any(2)[0].nonzero().flatten().tolist()[:60])
     sl = (slice(None), slice(None)) + tuple(slice(a, b) for a, b in zip(lo, hi))
-    bb = (box[sl] != scv[sl]).any(-1)
+    bb = (box != scv[sl]).any(-1)
     print("  box bad", int(bb.sum()), "of", bb.numel())
     if bb.any():
         idx = bb.nonzero()[:8].tolist()

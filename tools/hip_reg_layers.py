@@ -114,7 +114,7 @@ def main():
         sl = (slice(None), slice(None)) + tuple(slice(a0, b1) for a0, b1 in zip(lo, hi))
         print("cv_head vs split path: y0 equal %s (max|d| %.3g), y1 equal %s (max|d| %.3g), box equal %s" % (
             torch.equal(y0h, y0s), (y0h - y0s).abs().max().item(), torch.equal(y1h, y1s),
-            (y1h - y1s).abs().max().item(), torch.equal(box.data[sl], cvs[sl])), flush=True)
+            (y1h - y1s).abs().max().item(), torch.equal(box.data, cvs[sl])), flush=True)
         if a.only:   # one layer or a comma-separated list ("step": the whole eval step)
             for name in a.only.split(","):
                 timed(name, (lambda: net(img, K, R, T, d_min, d_int, B, V)) if name == "step" else layers[name],
