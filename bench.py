@@ -17,11 +17,12 @@ mvs_amd/depth_shards.py) to the rank that owns the sample, which runs the regula
 
 Also reported (one JSON line, rank 0):
   roofline      the step's dominant kernel, the fused head (cv_head_kernel: the cost volume formed on
-                chip and consumed by conv_0_0 + conv_1_0): executed f16 MFMA flops per
-                launch / its average launch time (HIP events on the launch stream inside the timed
-                steps) vs the 2.5 PF dense f16 peak; beside it the fp32 convolution flops it computes
-                and its algorithmic HBM bytes (no cost volume round trip: features in, y0 / y1 / the
-                conv_2_0 box out); traffic = PMC HBM bytes from profiles/ when measured
+                chip and consumed by conv_0_0 + conv_1_0): the ALGORITHMIC fp32
+                convolution flops per launch / its average launch time (HIP events on the launch stream
+                inside the timed steps) vs the dense fp32 matrix peak; beside it the executed f16 MFMA
+                flops (split operands) vs the f16 peak and its algorithmic HBM bytes (no cost volume
+                round trip: features in, y0 / y1 / the conv_2_0 box out); traffic = PMC HBM bytes per
+                launch from profiles/head_traffic_<cfg>.json (rocprofv3 --pmc, FETCH_SIZE x2 + WRITE_SIZE)
   warp_kernel   the standalone fused warp + variance kernel (cost_volume_staged_kernel, channel-quad
                 split store): algorithmic bytes (features read once + cost volume written once) /
                 launch time vs 8 TB/s -- the metric's "warp-kernel HBM GB/s"; traffic = PMC bytes
@@ -76,9 +77,6 @@ def _heartbeat():
               flush=True)
 
 
-threading.Thread(target=_heartbeat, daemon=True).start()
-
-
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -126,6 +124,58 @@ def max_over_ranks(x, world, device):
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t.item()
+
+
+DSHARD_PHASES = ("encoder", "shard_kernel", "exchange", "owner_compute", "gather")
+
+
+def dshard_step(net, world, rank, inputs, B, V, ops=None, group=None):
+    """BASELINE configs[3]'s step: mvs_amd.depth_shards.DepthShardedMVSNet around ``net`` (this rank's
+    D-slab of the cost volume, the owner-targeted exchange, the owner's regulariser / soft-argmin /
+    refinement, the depth maps gathered to rank 0).  Returns (the wrapper, a no-argument step).
+    ``ops`` swaps the slab producer / soft-argmin (the CPU gloo test passes the oracle's)."""
+    from mvs_amd.depth_shards import DepthShardedMVSNet
+    sharded = DepthShardedMVSNet(net, world, rank, group=group, ops=ops)
+    return sharded, (lambda: sharded(*inputs, B, V))
+
+
+def dshard_phase_ms(sharded, step, steps, device, world):
+    """This rank's time per phase of the D-sharded step (DSHARD_PHASES, DepthShardedMVSNet.phase_hook),
+    averaged over ``steps`` steps: HIP events on the current stream at each phase end on a GPU (a phase
+    is the time between its end and the previous one's), wall clock after a synchronising phase end
+    on the CPU.  All-gathered: returns [[ms per phase] for every rank] on every rank."""
+    cuda = device.type == "cuda"
+    sums = [0.0] * len(DSHARD_PHASES)
+    for _ in range(steps):
+        marks = []
+
+        def mark(name):
+            if cuda:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record()
+                marks.append((name, e))
+            else:
+                marks.append((name, time.perf_counter()))
+        mark("start")
+        sharded.phase_hook = mark
+        try:
+            with torch.no_grad():
+                step()
+        finally:
+            sharded.phase_hook = None
+        if cuda:
+            torch.cuda.synchronize(device)
+        names = [n for n, _ in marks]
+        assert tuple(names[1:]) == DSHARD_PHASES, names
+        for i in range(1, len(marks)):
+            a, b = marks[i - 1][1], marks[i][1]
+            sums[i - 1] += a.elapsed_time(b) if cuda else 1000.0 * (b - a)
+    mine = [v / steps for v in sums]
+    if world == 1:
+        return [mine]
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    return allr
 
 
 def make_inputs(B, V, H, W, seed, device):
@@ -370,7 +420,7 @@ def train_step_bench(B, V, D, H, W, device, steps):
     step()
     torch.cuda.synchronize()
     first = time.perf_counter() - t0
-    n = steps if first < 20.0 else 1     # a very slow first step (solver search) is reported as is
+    n = max(3, steps)   # the first (slow: library initialisation) step is reported on its own
     t0 = time.perf_counter()
     for _ in range(n):
         loss = step()
@@ -513,6 +563,7 @@ def cpu_baseline(V, H, W, D):
 
 
 def main():
+    threading.Thread(target=_heartbeat, daemon=True).start()
     args = parse()
     world, rank, device = init_dist(args)
     V, H, W = args.views, args.height, args.width
@@ -532,13 +583,12 @@ def main():
     if not args.kernel_only:
         log("building model (D=%d, %dx%d)" % (D, H, W))
         net = build_model(D, H, W, device)
-        inputs = make_inputs(B, V, H, W, rank, device)
+        # samples mode: every rank its own batch; dshard: ONE batch, replicated on every rank
+        inputs = make_inputs(B, V, H, W, rank if args.mode == "samples" else 0, device)
         if args.mode == "samples":
             step = lambda: net(*inputs, B, V)
         else:
-            from mvs_amd.depth_shards import DepthShardedMVSNet
-            sharded = DepthShardedMVSNet(net, world, rank)
-            step = lambda: sharded(*inputs, B, V)
+            sharded, step = dshard_step(net, world, rank, inputs, B, V)
         # the main fused kernel's launches inside the timed steps, bracketed by HIP events on its
         # launch stream (ops.KERNEL_EVENT_HOOK -> mvs_cost_volume_fwd_c4's event arguments)
         from mvs_amd import ops as mvs_ops
@@ -568,6 +618,10 @@ def main():
             ev = [p for k, p in step_events if k == kind]
             result.setdefault("step_kernel_ms", {})[kind] = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
         log("timed %d steps: %.2f ms/step" % (args.steps, 1000.0 * dt / args.steps))
+        if args.mode == "dshard":
+            # the same step phase by phase, per rank (not part of the timed region above)
+            result["dshard_phases"] = dshard_phase_ms(sharded, step, max(1, min(args.steps, 5)), device, world)
+            log("dshard phases (ms, this rank): %s" % dict(zip(DSHARD_PHASES, result["dshard_phases"][rank])))
         dt = max_over_ranks(dt, world, device)
         ms_step = 1000.0 * dt / args.steps
         maps = (B * world if args.mode == "samples" else B) * args.steps
@@ -700,25 +754,38 @@ def main():
     if head_ms is not None:
         # the step's dominant kernel: the fused head (cost volume formed on chip + conv_0_0 + conv_1_0)
         hw_ = head_work(B, V, D, h, w)
-        tf = hw_["mfma_flops"] / (head_ms * 1e-3) / 1e12
+        alg_tf = hw_["alg_flops"] / (head_ms * 1e-3) / 1e12
+        exe_tf = hw_["mfma_flops"] / (head_ms * 1e-3) / 1e12
         out["roofline"] = {
-            "bound": "mfma", "achieved": tf, "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s",
-            "frac": tf / MFMA_F16_PEAK_TFS, "traffic": None if head_traffic(tag) is None else head_traffic(tag),
+            "bound": "mfma", "achieved": alg_tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": alg_tf / MFMA_F32_PEAK_TFS, "traffic": head_traffic(tag),
             "kernel": "cv_head_kernel<V=%d>" % V, "kernel_ms": head_ms,
             "timing": "HIP events around each launch inside the %d timed steps" % args.steps,
-            "flops_per_launch": hw_["mfma_flops"],
-            "flops": "executed f16 MFMA flops: conv_0_0 B*D*h*w voxels x 27 taps x 2 v_mfma_f32_16x16x32_f16 "
-                     "per 16 voxels (x_hi, x_lo rows against w_hi|w_lo columns) = 55,296 per voxel; conv_1_0 "
-                     "B*|window region| x 27 taps x 3 per 16 windows (three split products) = 82,944 per window",
-            "alg_fp32_conv_flops_per_launch": hw_["alg_flops"],
-            "alg_fp32_conv_tflops": hw_["alg_flops"] / (head_ms * 1e-3) / 1e12,
-            "alg_fp32_conv_frac_of_f32_mfma_peak": hw_["alg_flops"] / (head_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS,
-            "hbm_alg_bytes_per_launch": hw_["hbm_bytes"],
-            "hbm_GBps": hw_["hbm_bytes"] / (head_ms * 1e-3) / 1e9,
-            "hbm_frac": hw_["hbm_bytes"] / (head_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "flops_per_launch": hw_["alg_flops"],
+            "flops": "ALGORITHMIC fp32 convolution flops of the two layers the head computes: conv_0_0 "
+                     "B*D*h*w voxels x 8 out x 32 in x 27 taps x 2, conv_1_0 B*|window region| x 16 x 32 x 27 x 2; "
+                     "peak = the dense fp32 matrix peak (the path computes fp32 values, dtype f32)",
+            "executed_f16_mfma": {
+                "flops_per_launch": hw_["mfma_flops"], "tflops": exe_tf, "peak": MFMA_F16_PEAK_TFS,
+                "frac": exe_tf / MFMA_F16_PEAK_TFS,
+                "note": "the split-fp16 scheme runs the fp32 convolutions on the f16 matrix cores: conv_0_0 2 "
+                        "v_mfma_f32_16x16x32_f16 per (16 voxels, tap) = 55,296 flops per voxel (hi/lo rows x "
+                        "w_hi|w_lo columns), conv_1_0 3 per (16 windows, tap) = 82,944 per window"},
+            "hbm": {"alg_bytes_per_launch": hw_["hbm_bytes"], "GBps": hw_["hbm_bytes"] / (head_ms * 1e-3) / 1e9,
+                    "peak": HBM_PEAK_GBS, "frac": hw_["hbm_bytes"] / (head_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    "note": "features + reference views in; y0, y1 and the conv_2_0 box out (the cost volume "
+                            "itself never reaches HBM)"},
             "regions": hw_["regions"]}
     else:
         out["roofline"] = dict(out["warp_kernel"])
+    if "dshard_phases" in result:
+        out["dshard_phases"] = {
+            "phases": list(DSHARD_PHASES), "ms_per_rank": result["dshard_phases"],
+            "note": "per rank, mean over up to 5 extra steps after the timed ones (HIP events on the current "
+                    "stream at each phase end): encoder, this rank's D-slab kernel (shard_kernel), the "
+                    "owner-targeted point-to-point exchange (exchange, incl. waiting for the slowest sender), "
+                    "the owner's regulariser + soft-argmin + refinement (owner_compute; 0 on ranks owning no "
+                    "sample), the depth maps to rank 0 (gather)"}
     out["arithmetic"] = ("fp32 throughout, except conv_0_0 and conv_1_0 (model.py:101,103) in samples mode: "
                          "f16 MFMA with split-fp16 operands (hi + lo parts of the fp32 values; conv_0_0 all four "
                          "partial products, conv_1_0 three; fp32 accumulation), the cost volume formed on chip by "

@@ -27,7 +27,8 @@ constexpr uint32_t kInvalidTap = 0xFFFFFFFFu;
 // tests/test_oracle.py::test_sampling_law_is_torch_cpu_bitwise (contraction is off inside these
 // helpers, and every fused step is an explicit fma, so the result never depends on what the
 // compiler chooses to fuse):
-//   * kornia transform_points -> torch.bmm (MKL sgemm, k-ordered fma accumulation):
+//   * kornia transform_points -> torch.bmm ([h, w, 3] x [3, 3] per image; MKL sgemm, k-ordered fma
+//     accumulation, for every w >= 45 -- all real feature widths; torch's own loop for 9 w < 400):
 //       u = fma(yn, G1, xn * G0) + G2
 //   * kornia convert_points_from_homogeneous: u * (1 / (s + 1e-8)) where |s| > 1e-8
 //   * grid_sample(align_corners=False) unnormalise, ATen GridSamplerKernel.cpp (vectorised, fma):

@@ -322,7 +322,9 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     // the whole variance to finish), item u + kAhead's gathers, and only then this item's LDS work.
     auto lds_drain = [&]() {
       __builtin_amdgcn_sched_barrier(0);
+#ifndef MVS_HEAD_NO_LDS_DRAIN   // (mutation build of tests/test_head_isa.py only: the rule's checker must fail)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
       __builtin_amdgcn_sched_barrier(0);
     };
     rdc(0);

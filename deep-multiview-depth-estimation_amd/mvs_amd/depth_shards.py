@@ -186,7 +186,13 @@ class DepthShardedMVSNet(nn.Module):
     rank ``dst`` (the owners' maps gathered there, ``gather_depth_maps``) and ``(None, None)`` on the
     other ranks; with ``gather=False`` it returns ``(samples, initial, refined)`` on every rank: the
     samples this rank owns and their maps (``None`` when it owns none).  ``ops`` supplies the slab
-    producer and the soft-argmin (default: the HIP kernels)."""
+    producer and the soft-argmin (default: the HIP kernels).
+
+    ``phase_hook`` (optional callable, name -> None) is called at the END of each phase of a step,
+    in order: "encoder", "shard_kernel" (this rank's D-slab of the cost volume), "exchange" (the
+    owner-targeted point-to-point exchange), "owner_compute" (regulariser + soft-argmin + refinement
+    of the owned samples; nothing on a rank that owns none), "gather" (the depth maps to ``dst``).
+    bench.py --mode dshard records a HIP event there, per rank."""
 
     def __init__(self, net, world, rank, group=None, ops=None, gather=True, dst=0):
         super().__init__()
@@ -197,6 +203,11 @@ class DepthShardedMVSNet(nn.Module):
         self.ops = ops or _HipOps
         self.gather = gather
         self.dst = dst
+        self.phase_hook = None
+
+    def _phase(self, name):
+        if self.phase_hook is not None:
+            self.phase_hook(name)
 
     def _check_mode(self):
         if torch.is_grad_enabled():
@@ -212,10 +223,13 @@ class DepthShardedMVSNet(nn.Module):
         c = self.net.cfg
         d_begin, d_count = plane_shard(c.d_num, self.world, self.rank)
         feats = self.net.feature_encoder(nn_input)
+        self._phase("encoder")
         slab, d_batch, ref_views = self.ops.cost_volume_slab(
             K_batch, R_batch, T_batch, d_min, d_int, feats, batch_size, n_views, c.d_num, c.d_scale,
             d_begin, d_count)
+        self._phase("shard_kernel")
         cv = exchange_to_owners(slab, self.world, self.rank, self.group)
+        self._phase("exchange")
         mine = owned_samples(batch_size, self.world, self.rank)
         initial = refined = None
         if mine:
@@ -226,8 +240,11 @@ class DepthShardedMVSNet(nn.Module):
             dm = d_min.reshape(-1, 1, 1, 1).expand(batch_size, 1, 1, 1).to(cv.device).index_select(0, idx)
             di = d_int.reshape(-1, 1, 1, 1).expand(batch_size, 1, 1, 1).to(cv.device).index_select(0, idx)
             refined = self.net.refine(nn_input, initial, dm, di, ref_views[mine])
+        self._phase("owner_compute")
         if not self.gather:
             return mine, initial, refined
         h, w = feats.shape[2:]
-        return gather_depth_maps(initial, refined, batch_size, self.world, self.rank, h, w, self.dst, self.group,
-                                 feats.device, feats.dtype)
+        out = gather_depth_maps(initial, refined, batch_size, self.world, self.rank, h, w, self.dst, self.group,
+                                feats.device, feats.dtype)
+        self._phase("gather")
+        return out

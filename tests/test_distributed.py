@@ -201,3 +201,52 @@ def test_depth_sharded_model_world2(B):
     assert all(r[1] for r in res), res
     assert res[0][2] == ([0, 2] if B == 3 else [0]) and res[1][2] == ([1] if B == 3 else [])
     assert all(r[3] == 2 for r in res), res
+
+
+def _bench_dshard_worker(rank, world, port, q):
+    """bench.py's own D-sharded step (bench.dshard_step) and its per-phase timing
+    (bench.dshard_phase_ms), on the CPU with the oracle as the slab producer: the step must return
+    every sample's maps on rank 0 equal to the single-process oracle model's, and the phase record
+    must come back all-gathered, five non-negative phases per rank."""
+    _setup(rank, world, port)
+    try:
+        import sys
+        sys.path.insert(0, REPO)
+        import bench
+        import mvs_oracle
+        from cameras import camera_batch, depth_range
+        from weights import deterministic_state_dict
+        from mvs_amd.config import MVSConfig
+        from mvs_amd.model import MVSNet
+        B, V, D, H, W = 1, 3, 8, 64, 80   # cfg 4's shape at test size: one sample, D split over the ranks
+        net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W), device=torch.device("cpu"))
+        net.load_state_dict(deterministic_state_dict(net.state_dict()))
+        net.eval()
+        net.cost_volume_reg.live_region = False
+        K, R, T = camera_batch(B, V, H // 4, W // 4)
+        d_min, d_int = depth_range(B, d_int=6.0, distinct=True)
+        img = torch.randn(B * V, 3, H, W, generator=torch.Generator().manual_seed(11))
+        inputs = (img, K, R, T, d_min, d_int)
+        sharded, step = bench.dshard_step(net, world, rank, inputs, B, V, ops=_OracleOps)
+        with torch.no_grad():
+            ini, ref = step()
+            ini1, ref1, _ = mvs_oracle.mvsnet_forward(net, img, K, R, T, d_min, d_int, B, V, D, (H // 4, W // 4))
+        phases = bench.dshard_phase_ms(sharded, step, 2, torch.device("cpu"), world)
+        ok = (len(phases) == world and all(len(p) == len(bench.DSHARD_PHASES) for p in phases)
+              and all(v >= 0.0 for p in phases for v in p))
+        if rank == 0:
+            ok = ok and torch.allclose(ini, ini1, rtol=1e-6, atol=0) and torch.allclose(ref, ref1, rtol=1e-5, atol=1e-3)
+            ok = ok and phases[1][bench.DSHARD_PHASES.index("owner_compute")] < phases[0][
+                bench.DSHARD_PHASES.index("owner_compute")]   # rank 1 owns no sample at B = 1
+        else:
+            ok = ok and ini is None and ref is None
+        q.put((rank, ok, phases))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_dshard_step_world2():
+    """The D-sharded step exactly as bench.py --mode dshard builds and times it (gloo, world 2, CPU)."""
+    res = _run(_bench_dshard_worker, 2)
+    assert all(r[1] for r in res), res
+    assert res[0][2] == res[1][2]   # the all-gathered phase table is the same on both ranks

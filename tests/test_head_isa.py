@@ -1,0 +1,126 @@
+"""CPU: the fused head's producer-gather rule, checked on the gfx950 code object that ships.
+
+DESIGN.md §3.7 (hazard 1): a producer wave of ``cv_head_kernel`` must not issue a feature gather
+(``buffer_load_dwordx4``) while one of its own LDS instructions is still outstanding -- under the
+consumer waves' LDS load a ``ds_write`` / ``ds_read`` can still be reading its data or address VGPRs
+when a younger gather's data lands in registers the allocator reused.  The kernel enforces it with an
+explicit ``s_waitcnt lgkmcnt(0)`` (inline asm between ``sched_barrier``s: ``items()`` in
+csrc/cv_head.hip) before each item's gathers.  A compiler or schedule change could move gathers above
+that wait, and a low-rate corruption would then pass the bit-equality tests, so this test reads the
+built library's own ISA:
+
+  * in every basic block of the producer item loop (the blocks that round the variance into fp16
+    hi / lo: ``v_cvt_pk_f16_f32``, split4 -- no other code of the kernel does), each
+    ``buffer_load_dwordx4`` has no ``ds_*`` instruction between it and the last
+    ``s_waitcnt lgkmcnt(0)`` before it, and that wait is inside the same block (a branch target's
+    predecessor is not known from the layout);
+  * the rule is not vacuous: those blocks hold the unrolled items' gathers (4 taps x NS views each)
+    and one wait per item.
+
+The disassembly comes from the in-tree libmvs_cost_volume.so (copied to a temp dir first:
+``llvm-objdump --offloading`` writes the extracted bundles next to its input).
+"""
+import glob
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+LIB = os.path.join(REPO, "deep-multiview-depth-estimation_amd", "mvs_amd", "libmvs_cost_volume.so")
+OBJDUMP = "/opt/rocm/llvm/bin/llvm-objdump"
+
+
+def _disassemble(tmp_path, symbol_substr, so):
+    if not os.path.exists(OBJDUMP):
+        pytest.skip("llvm-objdump not available")
+    if not os.path.exists(so):
+        pytest.skip("library not built")
+    lib = tmp_path / "lib.so"
+    shutil.copy(so, lib)
+    subprocess.run([OBJDUMP, "--offloading", str(lib)], cwd=tmp_path, check=True, capture_output=True)
+    for co in sorted(glob.glob(str(tmp_path / "lib.so.*gfx950*"))):
+        asm = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", "--symbolize-operands", co],
+                             capture_output=True, text=True, check=True).stdout
+        # the function: from its header line to the next function header (local block labels
+        # <L..> are printed between, as "<addr> <Ln>:" lines)
+        lines = asm.splitlines()
+        heads = [i for i, l in enumerate(lines) if re.match(r"^[0-9a-f]+ <_Z.*>:$", l.strip())]
+        for j, i in enumerate(heads):
+            if symbol_substr in lines[i]:
+                end = heads[j + 1] if j + 1 < len(heads) else len(lines)
+                return "\n".join(lines[i + 1:end])
+    raise AssertionError("no gfx950 code object holds %s" % symbol_substr)
+
+
+def _instructions(asm):
+    """[(kind, text)] in layout order: kind 'label' for a basic-block label line, else 'insn'."""
+    out = []
+    for line in asm.splitlines():
+        s = line.split("//")[0].strip()
+        if not s:
+            continue
+        if re.match(r"^[0-9a-f]+ <.*>:$", s):
+            out.append(("label", s))
+        elif not s.endswith(":"):
+            out.append(("insn", s))
+    return out
+
+
+def _check(asm):
+    """(gathers checked, waits seen, violations) of the rule over the producer item blocks."""
+    blocks, cur = [], []
+    for kind, text in _instructions(asm):
+        if kind == "label":
+            blocks.append(cur)
+            cur = []
+        else:
+            cur.append(text)
+    blocks.append(cur)
+    assert len(blocks) >= 20, len(blocks)   # the basic blocks are visible to the scan
+    gathers = drains = 0
+    bad = []
+    for bi, blk in enumerate(blocks):
+        # producer item blocks: the only code that rounds the variance into fp16 hi / lo (split4)
+        if not any(t.startswith("v_cvt_pk_f16_f32") for t in blk):
+            continue
+        state = "block entry"   # the predecessor is not known from the layout
+        for t in blk:
+            op = t.split()[0]
+            if op == "s_waitcnt" and "lgkmcnt(0)" in t:
+                state = "drained"
+                drains += 1
+            elif op.startswith("ds_"):
+                state = "lds outstanding"
+            elif op == "buffer_load_dwordx4":
+                gathers += 1
+                if state != "drained":
+                    bad.append((bi, t, state))
+    return gathers, drains, bad
+
+
+@pytest.mark.parametrize("V", [2, 3])
+def test_no_gather_issued_with_lds_outstanding(tmp_path, V):
+    gathers, drains, bad = _check(_disassemble(tmp_path, "cv_head_kernelILi%d" % V, LIB))
+    assert gathers >= 4 * (V - 1) * 6, gathers   # the producer item loop (unrolled items) is covered
+    assert drains >= 6, drains
+    assert not bad, "gathers issued with LDS work possibly outstanding: %s" % bad[:5]
+
+
+def test_checker_flags_a_build_without_the_wait(tmp_path):
+    """Mutation: csrc/cv_head.hip built alone with -DMVS_HEAD_NO_LDS_DRAIN (the explicit wait compiled
+    out; nothing else changes) must violate the rule -- so the check above can tell."""
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    src = os.path.join(REPO, "deep-multiview-depth-estimation_amd", "csrc", "cv_head.hip")
+    mut = tmp_path / "mutant.so"
+    subprocess.run([hipcc, "-O3", "-std=c++17", "-Wno-pass-failed", "--offload-arch=gfx950", "-fPIC", "-shared",
+                    "-DMVS_HEAD_NO_LDS_DRAIN", "-o", str(mut), src], check=True, capture_output=True)
+    work = tmp_path / "mut"
+    work.mkdir()
+    gathers, _, bad = _check(_disassemble(work, "cv_head_kernelILi3", str(mut)))
+    assert gathers > 0 and bad, "the mutant (no explicit wait) passed the check"

@@ -188,3 +188,26 @@ def test_variance_law_is_costvolume_py_bitwise(V):
         for v in range(V):
             acc = fma32(x[v] - mean, x[v] - mean, acc)
         assert not np.array_equal(acc * r, cv)
+
+
+@pytest.mark.parametrize("w", [37, 40, 53, 160])
+def test_bmm_small_width_branch(w):
+    """Where the law holds: torch.bmm of kornia's transform_points ([h, w, 3] x [3, 3] per image) goes
+    to MKL's sgemm (k-ordered fma: fma(y, G1, x G0) + G2, the HIP law) when 9 w >= 400, and to torch's
+    own loop below that (every product and sum rounded on its own).  Every real feature width (160,
+    400; 32 x 4 ... ) is on the MKL side; this pins both branches so a test at a narrow width knows
+    which law it is comparing with."""
+    h = 16
+    G = _matrices(1, 3, 1, h, w)[1][:, 0]
+    grid = kornia_warp.create_meshgrid(h, w).repeat(3, 1, 1, 1)
+    pts_h = torch.nn.functional.pad(grid.reshape(-1, w, 2), [0, 1], "constant", 1.0)
+    out = torch.bmm(pts_h, torch.repeat_interleave(G, h, 0).permute(0, 2, 1)).numpy()
+    xn, yn = norm_coord(w)[None, :], norm_coord(h)[:, None]
+    g = G.numpy()
+    for i in range(3):
+        for r in range(3):
+            a, b, c = g[i, r]
+            mkl = fma32(yn, b, xn * a) + c
+            loop = ((xn * a) + (yn * b)) + c
+            got = out[i * h:(i + 1) * h, :, r]
+            assert np.array_equal(got, mkl if 9 * w >= 400 else loop), (w, i, r)
