@@ -16,13 +16,13 @@ D-slab, and each sample's slab goes point to point (RCCL send/recv over xGMI,
 mvs_amd/depth_shards.py) to the rank that owns the sample, which runs the regulariser.
 
 Also reported (one JSON line, rank 0):
-  roofline      the step's dominant kernel, the fused head (cv_head_kernel: the cost volume formed on
-                chip and consumed by conv_0_0 + conv_1_0): the ALGORITHMIC fp32
+  roofline      the step's dominant kernel, the split head (cv_head_kernel<2, PRESPLIT>: conv_0_0 +
+                conv_1_0 in one pass over the split cost volume): the ALGORITHMIC fp32
                 convolution flops per launch / its average launch time (HIP events on the launch stream
                 inside the timed steps) vs the dense fp32 matrix peak; beside it the executed f16 MFMA
-                flops (split operands) vs the f16 peak and its algorithmic HBM bytes (no cost volume
-                round trip: features in, y0 / y1 / the conv_2_0 box out); traffic = PMC HBM bytes per
-                launch from profiles/head_traffic_<cfg>.json (rocprofv3 --pmc, FETCH_SIZE x2 + WRITE_SIZE)
+                flops (split operands) vs the f16 peak and its algorithmic HBM bytes (the split volume
+                in, y0 / y1 out); traffic = PMC HBM bytes per launch from
+                profiles/split_head_traffic_<cfg>.json (rocprofv3 --pmc, FETCH_SIZE x2 + WRITE_SIZE)
   warp_kernel   the standalone fused warp + variance kernel (cost_volume_staged_kernel, channel-quad
                 split store): algorithmic bytes (features read once + cost volume written once) /
                 launch time vs 8 TB/s -- the metric's "warp-kernel HBM GB/s"; traffic = PMC bytes
@@ -438,11 +438,13 @@ def train_step_bench(B, V, D, H, W, device, steps):
     return out
 
 
-def head_work(B, V, D, h, w):
-    """Work of one cv_head launch at the eval step's regions (CostVolumeReg.forward_live_head):
-    executed f16 MFMA flops, the fp32 convolution flops they compute (model.py:101,103), and the
-    algorithmic HBM bytes (pixel-major padded features + resampled reference views read once; y0,
-    the conv_1_0 window region and the split cost volume on conv_2_0's input box written once)."""
+def head_work(B, V, D, h, w, kind="split_head"):
+    """Work of one head launch at the eval step's regions: executed f16 MFMA flops, the fp32
+    convolution flops they compute (conv_0_0 + conv_1_0, model.py:101,103), and the algorithmic HBM
+    bytes.  kind "split_head" (the default path, ops.split_head): the split cost volume read once
+    (128 B per voxel: 8 channel quads x hi/lo fp16), y0 and the conv_1_0 window region written once.
+    kind "cv_head" (opt-in fused head): pixel-major padded features + resampled reference views read
+    once; y0, the window region and the split volume on conv_2_0's input box written once."""
     from mvs_amd import model as M
     from mvs_amd.config import pad_outpad
     n = (D, h, w)
@@ -456,15 +458,20 @@ def head_work(B, V, D, h, w):
     vox = D * h * w
     win = int(np.prod([b - a + 1 for a, b in h1]))
     box = int(np.prod([b - a for a, b in zip(lo, hi)]))
+    out_bytes = B * (vox * 8 * 4 + win * 16 * 4)
+    if kind == "split_head":
+        hbm = B * vox * 128 + out_bytes
+    else:
+        hbm = B * V * (h + 2) * (w + 2) * 128 + B * h * w * 128 + out_bytes + B * box * 8 * 16
     return {"mfma_flops": B * (vox * 55296 + win * 82944),
             "alg_flops": B * (vox * 8 * 32 * 27 * 2 + win * 16 * 32 * 27 * 2),
-            "hbm_bytes": B * V * (h + 2) * (w + 2) * 128 + B * h * w * 128 + B * (vox * 8 * 4 + win * 16 * 4 + box * 8 * 16),
+            "hbm_bytes": hbm,
             "regions": {"conv_1_0_windows": list(h1), "scv_box": [lo, hi]}}
 
 
-def head_traffic(tag):
-    """PMC HBM bytes per cv_head launch (profiles/, rocprofv3 --pmc), or None."""
-    path = os.path.join(REPO, "profiles", "head_traffic_%s.json" % tag)
+def head_traffic(tag, kind="split_head"):
+    """PMC HBM bytes per head launch (profiles/, rocprofv3 --pmc), or None."""
+    path = os.path.join(REPO, "profiles", "%s_traffic_%s.json" % ("head" if kind == "cv_head" else kind, tag))
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -698,7 +705,7 @@ def main():
     nc_ms, nc_op_ms, _ = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count)
     nc_ms = max_over_ranks(nc_ms, world, device)
     # warp-kernel duration: its launches inside the timed steps when the step runs it; the isolated
-    # back-to-back launches otherwise (samples mode: the step forms the volume inside the fused head)
+    # back-to-back launches otherwise (e.g. with the opt-in fused head, which forms the volume itself)
     step_k = result.get("step_kernel_ms", {})
     iso_ms = k_ms
     if "cost_volume" in step_k:
@@ -706,7 +713,8 @@ def main():
     gbs = alg / (k_ms * 1e-3) / 1e9
     tag = "b%dv%dd%dh%dw%d" % (B, V, d_count, h, w)
     traffic = load_traffic(tag)
-    head_ms = max_over_ranks(step_k["cv_head"], world, device) if "cv_head" in step_k else None
+    head_kind = next((k for k in ("split_head", "cv_head") if k in step_k), None)
+    head_ms = max_over_ranks(step_k[head_kind], world, device) if head_kind else None
 
     if rank != 0:
         if world > 1:
@@ -752,14 +760,16 @@ def main():
                      "op_GBps": alg / (op_ms * 1e-3) / 1e9},
     }
     if head_ms is not None:
-        # the step's dominant kernel: the fused head (cost volume formed on chip + conv_0_0 + conv_1_0)
-        hw_ = head_work(B, V, D, h, w)
+        # the step's dominant kernel: the split head (conv_0_0 + conv_1_0 in one pass over the split
+        # volume), or with MVS_CV_HEAD=1 the fused head (the volume formed on chip as well)
+        hw_ = head_work(B, V, D, h, w, head_kind)
         alg_tf = hw_["alg_flops"] / (head_ms * 1e-3) / 1e12
         exe_tf = hw_["mfma_flops"] / (head_ms * 1e-3) / 1e12
         out["roofline"] = {
             "bound": "mfma", "achieved": alg_tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
-            "frac": alg_tf / MFMA_F32_PEAK_TFS, "traffic": head_traffic(tag),
-            "kernel": "cv_head_kernel<V=%d>" % V, "kernel_ms": head_ms,
+            "frac": alg_tf / MFMA_F32_PEAK_TFS, "traffic": head_traffic(tag, head_kind),
+            "kernel": "cv_head_kernel<2, PRESPLIT>" if head_kind == "split_head" else "cv_head_kernel<V=%d>" % V,
+            "kernel_ms": head_ms,
             "timing": "HIP events around each launch inside the %d timed steps" % args.steps,
             "flops_per_launch": hw_["alg_flops"],
             "flops": "ALGORITHMIC fp32 convolution flops of the two layers the head computes: conv_0_0 "
@@ -773,8 +783,9 @@ def main():
                         "w_hi|w_lo columns), conv_1_0 3 per (16 windows, tap) = 82,944 per window"},
             "hbm": {"alg_bytes_per_launch": hw_["hbm_bytes"], "GBps": hw_["hbm_bytes"] / (head_ms * 1e-3) / 1e9,
                     "peak": HBM_PEAK_GBS, "frac": hw_["hbm_bytes"] / (head_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                    "note": "features + reference views in; y0, y1 and the conv_2_0 box out (the cost volume "
-                            "itself never reaches HBM)"},
+                    "note": ("the split cost volume in (once); y0 and y1 out" if head_kind == "split_head" else
+                             "features + reference views in; y0, y1 and the conv_2_0 box out (the cost volume "
+                             "itself never reaches HBM)")},
             "regions": hw_["regions"]}
     else:
         out["roofline"] = dict(out["warp_kernel"])
@@ -788,8 +799,8 @@ def main():
                     "sample), the depth maps to rank 0 (gather)"}
     out["arithmetic"] = ("fp32 throughout, except conv_0_0 and conv_1_0 (model.py:101,103) in samples mode: "
                          "f16 MFMA with split-fp16 operands (hi + lo parts of the fp32 values; conv_0_0 all four "
-                         "partial products, conv_1_0 three; fp32 accumulation), the cost volume formed on chip by "
-                         "the fused head kernel as those hi/lo parts; max error 0.3-0.5x that of the exact fp32 "
+                         "partial products, conv_1_0 three; fp32 accumulation), the cost volume stored by the "
+                         "fused warp kernel as those hi/lo parts; max error 0.3-0.5x that of the exact fp32 "
                          "kernels vs float64 (tests/test_split_conv.py, DESIGN.md 3.5); element contract |x - "
                          "(hi + lo) 2^-e| <= 2^-22 |x| + 2^-37 B^2 (B = max|feat|): fp32-level relative error down "
                          "to ~1e-5 of the volume bound, an absolute floor below (test_split_conv_dynamic_range)")

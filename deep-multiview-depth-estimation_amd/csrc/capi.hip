@@ -330,6 +330,51 @@ int mvs_cost_volume_head_fwd(const float* feat, const float* K, const float* R, 
   return lc.status();
 }
 
+int mvs_split_head_fwd(const void* scv, const unsigned* x_absmax, int batch, int d_count, int h, int w,
+                       const void* w0_frag, int w0_exp, const float* bn0_scale, const float* bn0_shift,
+                       const float* bn0_mean, const void* w1_frag, int w1_exp, const float* bn1_scale,
+                       const float* bn1_shift, const float* bn1_mean, const int* pad, const int* y1_origin,
+                       const int* y1_size, float* y0, float* y1, void* stream, void* main_begin_event,
+                       void* main_end_event) {
+  if (!scv || !x_absmax || !y0 || !y1 || !w0_frag || !w1_frag || !pad || !y1_origin || !y1_size)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (batch <= 0 || d_count <= 0 || h <= 0 || w <= 0 || (d_count & 1)) return MVS_ERR_INVALID_ARGUMENT;
+  if ((((uintptr_t)scv) | ((uintptr_t)w0_frag) | ((uintptr_t)w1_frag) | ((uintptr_t)y0)) & 15u ||
+      ((uintptr_t)x_absmax & 3u))
+    return MVS_ERR_INVALID_ARGUMENT;
+  if ((bn0_scale != nullptr) != (bn0_shift != nullptr) || (bn0_scale != nullptr) != (bn0_mean != nullptr) ||
+      (bn1_scale != nullptr) != (bn1_shift != nullptr) || (bn1_scale != nullptr) != (bn1_mean != nullptr))
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (w0_exp < -120 || w0_exp > 120 || w1_exp < -120 || w1_exp > 120) return MVS_ERR_INVALID_ARGUMENT;
+  const int n[3] = {d_count, h, w};
+  uint64_t ovox = 1;
+  for (int d = 0; d < 3; ++d) {
+    if (pad[d] < 1 || !(pad[d] & 1)) return MVS_ERR_INVALID_ARGUMENT;
+    if (y1_size[d] <= 0 || y1_origin[d] < 0 || y1_origin[d] + y1_size[d] > (n[d] + 2 * pad[d] - 3) / 2 + 1)
+      return MVS_ERR_INVALID_ARGUMENT;
+    ovox *= (uint64_t)y1_size[d];
+  }
+  if (128ull * (uint64_t)d_count * (uint64_t)h * (uint64_t)w > 0xFFFFFFF0ull ||
+      (uint64_t)batch * ovox * 16ull >= (1ull << 40))
+    return MVS_ERR_TOO_LARGE;
+  mvs::Geometry g;
+  g.B = batch;
+  g.V = 2;
+  g.C = 32;
+  g.h = h;
+  g.w = w;
+  g.Dc = d_count;
+  g.tiles = 0;
+  g.total = 0;
+  const mvs::LaunchCheck lc;
+  const float* bn0[3] = {bn0_scale, bn0_shift, bn0_mean};
+  const float* bn1[3] = {bn1_scale, bn1_shift, bn1_mean};
+  const int st = mvs::launch_split_head(g, scv, reinterpret_cast<const uint32_t*>(x_absmax), w0_frag, w0_exp, w1_frag,
+                                        w1_exp, bn0, bn1, y0, y1, pad, y1_origin, y1_size, (hipStream_t)stream,
+                                        (hipEvent_t)main_begin_event, (hipEvent_t)main_end_event);
+  return st != MVS_OK ? st : lc.status();
+}
+
 int mvs_conv3d_k3_split_fwd(const void* x, int flags, const void* weight_frag, int weight_exp,
                             const unsigned* x_absmax, float* y, int batch, int d, int h, int w,
                             const float* bn_scale, const float* bn_shift, const float* bn_mean, void* stream) {

@@ -70,13 +70,13 @@ constexpr int kPF = 3;                                   // conv_0_0 A-fragment 
 // the step barrier otherwise; the producers' gathers are the step's critical path: cfg 2 2.28 -> 2.19 ms)
 constexpr bool kCoordsByConsumers = true;
 
-template <int NS>
+template <int NS, bool PRE = false>
 constexpr int coord_bytes() {   // [2 buffers][2 planes][NS views][108 voxels] x {off, wx, wy, -}
-  return 2 * 2 * NS * kHV * 16;
+  return PRE ? 0 : 2 * 2 * NS * kHV * 16;
 }
-template <int NS>
+template <int NS, bool PRE = false>
 constexpr int lds_bytes() {
-  return kRingB + kW1B + coord_bytes<NS>() + kScrB;
+  return kRingB + kW1B + coord_bytes<NS, PRE>() + kScrB;
 }
 
 struct HeadArgs {
@@ -91,6 +91,7 @@ struct HeadArgs {
   float* y0;                  // [B][8][D][H][W]
   float* y1;                  // [B][on0][on1][on2][16]
   void* scv;                  // split cost volume on the box only: [B][8][r1 - r0 ...] x 16 B, or null
+  const void* scv_in;         // PRE: the materialised split cost volume [B][8][D][H][W] x 16 B (split.h)
   int V, D, H, W;
   int w_exp0, w_exp1;
   int tiles_x, tiles_y, zchunks, total;
@@ -110,14 +111,18 @@ __device__ inline float ror8(float v) {   // value of lane (l ^ 8) inside each 1
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
 }
 
-template <int V>
+// PRE (mvs_split_head_fwd): the cost volume is already materialised as the split volume; the producer
+// waves only copy its planes into the ring (one 16-byte load and two 8-byte LDS stores per item) and
+// the consumers run exactly the MFMA code below -- conv_0_0 and conv_1_0 of the split path in ONE pass
+// over the volume, bit-equal to conv3d_split.hip + conv3d_s2_split.hip.
+template <int V, bool PRE = false>
 __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   constexpr int NS = V - 1;
-  __shared__ __attribute__((aligned(16))) char lds[lds_bytes<NS>()];
+  __shared__ __attribute__((aligned(16))) char lds[lds_bytes<NS, PRE>()];
   char* const ring = lds;
   char* const w1l = lds + kRingB;
   char* const coord = lds + kRingB + kW1B;
-  char* const scr = coord + coord_bytes<NS>();
+  char* const scr = coord + coord_bytes<NS, PRE>();
 
   const int wk = xcd_work_id((int)blockIdx.x, (int)gridDim.x);
   if (wk >= a.total) return;   // workgroup-uniform, before any barrier
@@ -172,7 +177,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   const uint32_t pstride = (uint32_t)kC4 * 16u;   // bytes per padded pixel
   Rsrc rsv[NS];
   f4v ref[kItems];
-  if (!consumer) {
+  if (!consumer && !PRE) {
 #pragma unroll
     for (int s = 0; s < NS; ++s)
       rsv[s] = make_rsrc(a.packed + (size_t)(b * V + 1 + s) * pg.plane * kC4, pg.plane * pstride);
@@ -193,7 +198,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   // whether they lie in the image
   float cxn[2] = {0.f, 0.f}, cyn[2] = {0.f, 0.f};
   bool cin[2] = {false, false};
-  if (kCoordsByConsumers == consumer) {
+  if (kCoordsByConsumers == consumer && !PRE) {
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
       const int v = lane + 64 * pass;
@@ -206,6 +211,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   }
   // sampling state of batch j's planes for every (plane, view, halo voxel) -> coordinate buffer tb
   auto coords = [&](int j, int tb) {
+    if constexpr (PRE) return;
     const int pbase = z0 - 1 + 2 * j;
     for (int c = wave & 3; c < 2 * NS; c += 4) {   // wave-uniform (plane, view) combos
       const int pl = c / NS, s = c - pl * NS;
@@ -247,7 +253,10 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   // in range (an out-of-range load returns at once and made hazard 1 of DESIGN.md §3.7 frequent).
   // (Measured and dropped: skipping the items of edge tiles whose 64 lanes lie outside the image --
   // 2.34 against 2.18 ms, the extra branches cost the interior tiles more than the edges save.)
-  constexpr int kAhead = 2;
+#ifndef MVS_HEAD_AHEAD
+#define MVS_HEAD_AHEAD 2
+#endif
+  constexpr int kAhead = MVS_HEAD_AHEAD;
   // per-item constants (the same every batch), packed: LDS offset inside a ring slot (bits 0-12), in
   // the image (13), plane of the batch (15), quad (16-18), halo voxel (19-25)
   uint32_t meta[kItems];
@@ -266,7 +275,47 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     }
   }
   const int zst0 = max(z0, a.r0[0]), zst1 = min(z1, a.r1[0]);   // planes stored to the SCV box
+  // PRE: batch j's two planes copied from the split volume (all items' loads in flight together, then
+  // their LDS stores); invalid items (outside the image or the volume) load the sample's first element
+  // and store zeros -- no out-of-range load
+  const Rsrc rin = make_rsrc(PRE ? static_cast<const char*>(a.scv_in) + (size_t)b * kC4 * D * HW * 16 : nullptr,
+                             PRE ? (uint32_t)min((uint64_t)kC4 * D * HW * 16ull, 0xFFFFFFF0ull) : 0u);
+  auto items_pre = [&](int j) {
+    const int pbase = z0 - 1 + 2 * j;
+    const int sl0 = slot_of(pbase);
+    const int nu = __builtin_amdgcn_readfirstlane(ptid + 256 * (kItems - 1) < kBatchItems ? kItems : kItems - 1);
+    typedef __attribute__((ext_vector_type(4))) unsigned v4u;
+    v4u d[kItems];
+    bool ok[kItems];
+#pragma unroll
+    for (int u = 0; u < kItems; ++u) {
+      if (u == kItems - 1 && nu != kItems) break;   // wave-uniform
+      const uint32_t m = meta[u];
+      const int pl = (m >> 15) & 1, q = (m >> 16) & 7, v = (int)(m >> 19);
+      const int p = pbase + pl;
+      const int yy = v / kHX, xx = v - yy * kHX;
+      ok[u] = (m & (1u << 13)) && (unsigned)p < (unsigned)D;
+      const uint32_t off = ok[u] ? ((((uint32_t)q * (uint32_t)D + (uint32_t)p) * (uint32_t)HW +
+                                     (uint32_t)((y0 - 1 + yy) * W + (x0 - 1 + xx))) * 16u) : 0u;
+      d[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, (int)off, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kItems; ++u) {
+      if (u == kItems - 1 && nu != kItems) break;
+      const uint32_t m = meta[u];
+      const int pl = (m >> 15) & 1;
+      const uint2 hi = ok[u] ? make_uint2(d[u].x, d[u].y) : make_uint2(0u, 0u);
+      const uint2 lo = ok[u] ? make_uint2(d[u].z, d[u].w) : make_uint2(0u, 0u);
+      char* dst = ring + (sl0 + pl) * kSlotB + (m & 0x1FFFu);
+      *reinterpret_cast<uint2*>(dst) = hi;
+      *reinterpret_cast<uint2*>(dst + kPartB) = lo;
+    }
+  };
   auto items = [&](int j, int tb) {
+    if constexpr (PRE) {
+      items_pre(j);
+      return;
+    }
     const int pbase = z0 - 1 + 2 * j;
     const int sl0 = slot_of(pbase);   // even: the batch's second plane is the next slot
     const int nu = __builtin_amdgcn_readfirstlane(ptid + 256 * (kItems - 1) < kBatchItems ? kItems : kItems - 1);
@@ -282,7 +331,11 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         const uint4 ce = *reinterpret_cast<const uint4*>(coord + (((tb * 2 + pl) * NS + s) * kHV + v) * 16);
+#ifdef MVS_HEAD_RDC128   // experiment: all four words used (ce.w == 0), so the read is a ds_read_b128, not b96
+        co[u & 1][s] = ce.x | ce.w;
+#else
         co[u & 1][s] = ce.x;
+#endif
         cx[u & 1][s] = __uint_as_float(ce.y);
         cy[u & 1][s] = __uint_as_float(ce.z);
       }
@@ -302,6 +355,25 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
           tp[rr][s][1] = f4v{f, 1.f, f, f};
           tp[rr][s][2] = f4v{f, f, 2.f, f};
           tp[rr][s][3] = f4v{f, f, f, 3.f};
+        }
+#elif defined(MVS_HEAD_X2)   // experiment: each 16-byte tap as two 8-byte loads
+        {
+          typedef __attribute__((ext_vector_type(2))) unsigned v2u;
+          const uint32_t offs[4] = {o, o + pstride, o + (uint32_t)pg.pitch * pstride, o + (uint32_t)pg.pitch * pstride + pstride};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const v2u a0 = __builtin_amdgcn_raw_buffer_load_b64(rsv[s], (int)offs[t], 0, 0);
+            const v2u a1 = __builtin_amdgcn_raw_buffer_load_b64(rsv[s], (int)(offs[t] + 8u), 0, 0);
+            tp[rr][s][t] = f4v{__uint_as_float(a0.x), __uint_as_float(a0.y), __uint_as_float(a1.x), __uint_as_float(a1.y)};
+          }
+        }
+#elif defined(MVS_HEAD_GLOBAL)   // experiment: taps through global (flat-space) loads instead of buffer loads
+        {
+          const char* gb = reinterpret_cast<const char*>(a.packed) + (size_t)(b * V + 1 + s) * pg.plane * pstride;
+          tp[rr][s][0] = *reinterpret_cast<const f4v*>(gb + o);
+          tp[rr][s][1] = *reinterpret_cast<const f4v*>(gb + o + pstride);
+          tp[rr][s][2] = *reinterpret_cast<const f4v*>(gb + o + (uint32_t)pg.pitch * pstride);
+          tp[rr][s][3] = *reinterpret_cast<const f4v*>(gb + o + (uint32_t)pg.pitch * pstride + pstride);
         }
 #else
         tp[rr][s][0] = ld4(rsv[s], o, 0);
@@ -342,6 +414,14 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       const int p = pbase + pl;
       const bool valid = (m & (1u << 13)) && (unsigned)p < (unsigned)D;
       const int rr = u % (kAhead + 1);
+#ifdef MVS_HEAD_VMWAIT   // experiment: item u's gathers explicitly waited for (item u + 1's may stay in flight), then nops
+      __builtin_amdgcn_sched_barrier(0);
+      if (kAhead > 1 && has(u + 1))
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_nop %1" ::"n"(4 * NS), "n"(MVS_HEAD_VMWAIT) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_nop %0" ::"n"(MVS_HEAD_VMWAIT) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#endif
       f4v xs[NS];
 #pragma unroll
       for (int s = 0; s < NS; ++s) xs[s] = bilerp(tp[rr][s], fx[rr][s], fy[rr][s]);
@@ -355,6 +435,11 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       char* dst = ring + (sl0 + pl) * kSlotB + (m & 0x1FFFu);
       *reinterpret_cast<uint2*>(dst) = hi;
       *reinterpret_cast<uint2*>(dst + kPartB) = lo;
+#ifdef MVS_HEAD_WAIT_AFTER_STORE   // experiment: the item's LDS stores complete before any later VALU
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#endif
       // one item per scheduling region: without it the scheduler hoists every item's loads to the
       // top (all 7 items' gathers live at once: VGPR spills)
       __builtin_amdgcn_sched_barrier(0);
@@ -664,6 +749,51 @@ __global__ __launch_bounds__(256) void head_faces_kernel(float* __restrict__ y1,
   }
 }
 
+// outputs of the conv_1_0 region whose window no tile owns (all-padding windows, head_faces_kernel)
+void launch_head_faces(const Geometry& g, const HeadArgs& a, const float* const* bn1, float* y1, const int* pad,
+                       const int* o0, const int* on, hipStream_t s) {
+  // per dim, per dim, region outputs whose window start 2 o - P lies below -1 (before tile 0) or at /
+  // beyond the last owned start (n_tiles * tile - 1 in x / y, D - 1 + 2 in z)
+  int lo[3], hi[3];
+  const int own_hi[3] = {g.Dc - 1, a.tiles_y * kTY - 1, a.tiles_x * kTX - 1};   // first unowned start
+  for (int d = 0; d < 3; ++d) {
+    lo[d] = 0;
+    while (lo[d] < on[d] && 2 * (o0[d] + lo[d]) - pad[d] < -1) ++lo[d];
+    hi[d] = 0;
+    while (hi[d] < on[d] - lo[d] && 2 * (o0[d] + on[d] - 1 - hi[d]) - pad[d] > own_hi[d] - (d == 0 ? 0 : 1)) ++hi[d];
+  }
+  if (lo[0] + hi[0] + lo[1] + hi[1] + lo[2] + hi[2] > 0) {
+    const long n = (long)g.B * on[0] * on[1] * on[2] * 16;
+    const int blocks = (int)std::min<long>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(head_faces_kernel, dim3(blocks), dim3(256), 0, s, y1, g.B, on[0], on[1], on[2], lo[0], hi[0],
+                       lo[1], hi[1], lo[2], hi[2], bn1[0], bn1[1], bn1[2]);
+  }
+}
+
+// grid and geometry fields shared by both launchers
+int head_grid(const Geometry& g, HeadArgs& a, const int* pad, const int* o0, const int* on, const int* r0,
+              const int* r1) {
+  a.D = g.Dc;
+  a.H = g.h;
+  a.W = g.w;
+  // tiles cover conv_0_0's outputs and every stride-2 window that touches the volume: a tile owns
+  // window starts [x0 - 1, x0 + 15) / [y0 - 1, y0 + 3), the last start is n - 1 (P odd, n even)
+  a.tiles_x = g.w / kTX + 1;
+  a.tiles_y = g.h / kTY + 1;
+  a.zchunks = (g.Dc + kZC - 1) / kZC;
+  const long total = (long)a.tiles_x * a.tiles_y * a.zchunks * g.B;
+  if (total >= (1L << 31) - 8) return MVS_ERR_TOO_LARGE;
+  a.total = (int)total;
+  for (int d = 0; d < 3; ++d) {
+    a.pad[d] = pad[d];
+    a.o0[d] = o0[d];
+    a.on[d] = on[d];
+    a.r0[d] = r0[d];
+    a.r1[d] = r1[d];
+  }
+  return MVS_OK;
+}
+
 }  // namespace
 
 size_t cv_head_lds_bytes(int V) { return V == 2 ? (size_t)lds_bytes<1>() : (size_t)lds_bytes<2>(); }
@@ -692,27 +822,12 @@ int launch_cv_head(const Geometry& g, const float* feat, const Cams& cm, float* 
   a.y0 = y0;
   a.y1 = y1;
   a.scv = scv;
+  a.scv_in = nullptr;
   a.V = g.V;
-  a.D = g.Dc;
-  a.H = g.h;
-  a.W = g.w;
   a.w_exp0 = w_exp0;
   a.w_exp1 = w_exp1;
-  // tiles cover conv_0_0's outputs and every stride-2 window that touches the volume: a tile owns
-  // window starts [x0 - 1, x0 + 15) / [y0 - 1, y0 + 3), the last start is n - 1 (P odd, n even)
-  a.tiles_x = g.w / kTX + 1;
-  a.tiles_y = g.h / kTY + 1;
-  a.zchunks = (g.Dc + kZC - 1) / kZC;
-  const long total = (long)a.tiles_x * a.tiles_y * a.zchunks * g.B;
-  if (total >= (1L << 31) - 8) return MVS_ERR_TOO_LARGE;
-  a.total = (int)total;
-  for (int d = 0; d < 3; ++d) {
-    a.pad[d] = pad[d];
-    a.o0[d] = o0[d];
-    a.on[d] = on[d];
-    a.r0[d] = r0[d];
-    a.r1[d] = r1[d];
-  }
+  const int gst = head_grid(g, a, pad, o0, on, r0, r1);
+  if (gst != MVS_OK) return gst;
 #ifdef MVS_HEAD_STAMP
   static unsigned long long* stamps = nullptr;
   const size_t stamp_bytes = (size_t)kStampWG * 8 * kStampN * sizeof(unsigned long long);
@@ -737,22 +852,38 @@ int launch_cv_head(const Geometry& g, const float* feat, const Cams& cm, float* 
     }
   }
 #endif
-  // faces: per dim, region outputs whose window start 2 o - P lies below -1 (before tile 0) or at /
-  // beyond the last owned start (n_tiles * tile - 1 in x / y, D - 1 + 2 in z)
-  int lo[3], hi[3];
-  const int own_hi[3] = {g.Dc - 1, a.tiles_y * kTY - 1, a.tiles_x * kTX - 1};   // first unowned start
-  for (int d = 0; d < 3; ++d) {
-    lo[d] = 0;
-    while (lo[d] < on[d] && 2 * (o0[d] + lo[d]) - pad[d] < -1) ++lo[d];
-    hi[d] = 0;
-    while (hi[d] < on[d] - lo[d] && 2 * (o0[d] + on[d] - 1 - hi[d]) - pad[d] > own_hi[d] - (d == 0 ? 0 : 1)) ++hi[d];
-  }
-  if (lo[0] + hi[0] + lo[1] + hi[1] + lo[2] + hi[2] > 0) {
-    const long n = (long)g.B * on[0] * on[1] * on[2] * 16;
-    const int blocks = (int)std::min<long>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(head_faces_kernel, dim3(blocks), dim3(256), 0, s, y1, g.B, on[0], on[1], on[2], lo[0], hi[0],
-                       lo[1], hi[1], lo[2], hi[2], bn1[0], bn1[1], bn1[2]);
-  }
+  launch_head_faces(g, a, bn1, y1, pad, o0, on, s);
+  return MVS_OK;
+}
+
+int launch_split_head(const Geometry& g, const void* scv_in, const uint32_t* absmax, const void* w0frag, int w_exp0,
+                      const void* w1frag, int w_exp1, const float* const* bn0, const float* const* bn1, float* y0,
+                      float* y1, const int* pad, const int* o0, const int* on, hipStream_t s, hipEvent_t ev0,
+                      hipEvent_t ev1) {
+  HeadArgs a = {};
+  a.absmax = absmax;
+  a.w0 = reinterpret_cast<const h8v*>(w0frag);
+  a.w1 = reinterpret_cast<const h8v*>(w1frag);
+  a.bn0_sc = bn0[0];
+  a.bn0_sh = bn0[1];
+  a.bn0_mu = bn0[2];
+  a.bn1_sc = bn1[0];
+  a.bn1_sh = bn1[1];
+  a.bn1_mu = bn1[2];
+  a.y0 = y0;
+  a.y1 = y1;
+  a.scv = nullptr;
+  a.scv_in = scv_in;
+  a.V = 2;
+  a.w_exp0 = w_exp0;
+  a.w_exp1 = w_exp1;
+  const int zero[3] = {0, 0, 0};
+  const int gst = head_grid(g, a, pad, o0, on, zero, zero);
+  if (gst != MVS_OK) return gst;
+  if (ev0) (void)hipEventRecord(ev0, s);
+  hipLaunchKernelGGL((cv_head_kernel<2, true>), xcd_grid(a.total), dim3(kThreads), 0, s, a);
+  if (ev1) (void)hipEventRecord(ev1, s);
+  launch_head_faces(g, a, bn1, y1, pad, o0, on, s);
   return MVS_OK;
 }
 

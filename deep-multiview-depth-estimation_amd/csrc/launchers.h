@@ -51,6 +51,11 @@ int launch_cv_head(const Geometry& g, const float* feat, const Cams& cm, float* 
                    const float* const* bn1, float* y0, float* y1, void* scv, const int* pad, const int* o0,
                    const int* on, const int* r0, const int* r1, hipStream_t s, hipEvent_t ev0 = nullptr,
                    hipEvent_t ev1 = nullptr);
+// the same kernel on a materialised split cost volume (conv_0_0 + conv_1_0 in one pass over it)
+int launch_split_head(const Geometry& g, const void* scv_in, const uint32_t* absmax, const void* w0frag, int w_exp0,
+                      const void* w1frag, int w_exp1, const float* const* bn0, const float* const* bn1, float* y0,
+                      float* y1, const int* pad, const int* o0, const int* on, hipStream_t s, hipEvent_t ev0 = nullptr,
+                      hipEvent_t ev1 = nullptr);
 
 // warp_variance.hip
 void launch_warp(const Geometry& g, const float* feat, const float* sampling, float* warped,

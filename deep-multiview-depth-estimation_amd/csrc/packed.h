@@ -81,6 +81,17 @@ __device__ inline f4v div_views4(const f4v& x, ViewDiv d) {
 template <int NS>
 __device__ inline f4v variance_law4(const f4v& x0, const f4v (&xs)[NS], ViewDiv vd) {
 #pragma clang fp contract(off)
+#ifdef MVS_EXP_OLD_VARIANCE   // experiment only: the round-4 arithmetic (reciprocal multiply, fused squares)
+  {
+    const f4v iv = {vd.r, vd.r, vd.r, vd.r};
+    f4v sm = x0;
+    for (int s = 0; s < NS; ++s) sm += xs[s];
+    const f4v nm = -(sm * iv);
+    f4v dd = x0 + nm, ac = dd * dd;
+    for (int s = 0; s < NS; ++s) { dd = xs[s] + nm; ac = __builtin_elementwise_fma(dd, dd, ac); }
+    return ac * iv;
+  }
+#endif
   f4v sum = x0;
 #pragma unroll
   for (int s = 0; s < NS; ++s) sum += xs[s];

@@ -58,6 +58,8 @@ SIGNATURES = {
     "mvs_conv3d_split_weights": (_c_int, [_p, _p, _p]),
     "mvs_conv3d_s2_split_fwd": (_c_int, [_p, _c_int, _p, _c_int, _p, _p, _c_int] + [_p] * 8),
     "mvs_conv3d_s2_split_weights": (_c_int, [_p, _p, _p]),
+    "mvs_split_head_fwd": (_c_int, [_p, _p, _c_int, _c_int, _c_int, _c_int, _p, _c_int, _p, _p, _p,
+                                    _p, _c_int, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "mvs_cost_volume_head_fwd": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int,
                                           _c_int, _c_int, _c_float,
                                           _p, _c_int, _p, _p, _p, _p, _c_int, _p, _p, _p,

@@ -191,9 +191,9 @@ class CostVolumeReg(nn.Module):
     def head_ok(self, dcv):
         """The fused head kernel applies to this deferred cost volume: eval-mode live regions with the
         split-fp16 convolutions, fp32 HIP inference, C = 32, 2-3 views, D even and every stride-2
-        padding odd (the kernel's window ownership), MVS_CV_HEAD not 0."""
+        padding odd (the kernel's window ownership), MVS_CV_HEAD=1 (opt-in)."""
         n = tuple(dcv.shape[2:])
-        return (os.environ.get("MVS_CV_HEAD", "1") != "0" and self.split_f16 and self.live_ok(n)
+        return (os.environ.get("MVS_CV_HEAD", "0") == "1" and self.split_f16 and self.live_ok(n)
                 and _hip_inference(dcv.feature_maps) and dcv.shape[1] == 32 and dcv.n_views in (2, 3)
                 and n[0] % 2 == 0 and all(p % 2 == 1 for p in self.pad))
 
@@ -308,7 +308,7 @@ class CostVolumeReg(nn.Module):
         head kernel (forward_live_head) -- conv_0_0's and conv_1_0's outputs; cv is then the split
         volume on conv_2_0's input box only, ``cv_box`` (origin, size) that box."""
         from .ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_k3_split, conv3d_region, conv_s2_split,
-                          deconv3d_k3s2, region_weight, softmax_depth)
+                          deconv3d_k3s2, region_weight, softmax_depth, split_head)
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad = list(n), list(self.pad)
@@ -330,6 +330,12 @@ class CostVolumeReg(nn.Module):
         # for the same CUs (cfg 2: 5.67 ms serialised against 5.78 ms on a side stream,
         # profiles/r03/r03u_reg_layers.log); the exact-fp32 VALU kernel overlaps the MFMA chain
         side = main if bound is not None else _side_stream(cv.device)
+        if head is None and split_cv and self._split_head_ok(cv, n):
+            # conv_0_0 + BN_0 + ReLU and conv_1_0 + BN_1 + ReLU in one pass over the split volume
+            # (ops.split_head, csrc/cv_head.hip PRESPLIT mode): bit-equal to the two kernels below
+            h1 = _grow(B, n, 1)
+            head = split_head(cv, bound, self.conv_0_0.weight, *bn_eval(self.BN_0), self.conv_1_0.weight,
+                              *bn_eval(self.BN_1), pad, org(h1), size(h1))
         if head is not None:
             y0, y1_head = head
         else:
@@ -367,6 +373,12 @@ class CostVolumeReg(nn.Module):
             y0.record_stream(main)
         z = deconv3d_k3s2(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0, x2=y1)
         return softmax_depth(conv3d_k3(z, self.conv_out.weight))
+
+    def _split_head_ok(self, cv, n):
+        """ops.split_head applies to this split volume: C = 32 (8 channel quads), D even and every
+        stride-2 padding odd (the kernel's window ownership), MVS_SPLIT_HEAD not 0."""
+        return (os.environ.get("MVS_SPLIT_HEAD", "1") != "0" and cv.shape[1] == 8 and n[0] % 2 == 0
+                and all(p % 2 == 1 for p in self.pad))
 
     def forward_live_train(self, cv, bound=None):
         """Train-mode-BatchNorm regulariser (test.py:53,61: `model.train()` under `no_grad`)
@@ -773,10 +785,12 @@ class MVSNet(nn.Module):
         # eval mode with the split-fp16 regulariser: the fused kernel writes the split cost volume
         split = (quads and not bf16 and reg.split_f16
                  and reg.live_ok((c.d_num,) + tuple(feature_maps.shape[2:])) and feature_maps.shape[1] == 32)
-        # ... and where the fused head kernel applies, the volume is not formed here at all: the
-        # regulariser forms it on chip inside conv_0_0 / conv_1_0
+        # ... and with the opt-in fused head kernel (MVS_CV_HEAD=1), the volume is not formed here at
+        # all: the regulariser forms it on chip inside conv_0_0 / conv_1_0.  Opt-in:
+        # its gathering producers corrupt one item sporadically; the default path
+        # materialises the split volume and runs both convolutions in one pass (ops.split_head)
         deferred = split and (c.d_num % 2 == 0 and n_views in (2, 3) and all(p % 2 == 1 for p in reg.pad)
-                              and os.environ.get("MVS_CV_HEAD", "1") != "0")
+                              and os.environ.get("MVS_CV_HEAD", "0") == "1")
         cost_volume, d_batch, ref_views = warp_and_assemble_cost_volume(
             K_batch, R_batch, T_batch, d_min, d_int, feature_maps, batch_size, n_views,
             d_num=c.d_num, d_scale=c.d_scale,

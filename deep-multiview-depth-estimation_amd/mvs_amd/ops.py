@@ -123,8 +123,9 @@ def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scal
 
 # Live timing of the main fused kernel inside a real step (bench.py): when set, a callable returning a
 # KERNEL_EVENT_HOOK(kind) -> (begin, end) pair of torch.cuda.Event for each fused-kernel call (kind
-# "cost_volume": the cost_volume_c4* ops' warp kernel; "cv_head": the fused head kernel); the C ABI
-# records them on the launch stream right around that kernel (the ops' event arguments).
+# "cost_volume": the cost_volume_c4* ops' warp kernel; "split_head": ops.split_head; "cv_head": the
+# opt-in fused head); the C ABI records them on the launch stream right around that kernel (the ops'
+# event arguments).
 KERNEL_EVENT_HOOK = None
 
 
@@ -377,6 +378,52 @@ def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scal
     return (feat.new_empty((batch_size, 8, d_count, h, w)), feat.new_empty([batch_size] + list(y1_size) + [16]),
             feat.new_empty([batch_size, 8] + box + [4] if boxed else [0], dtype=torch.int32),
             feat.new_empty((8,), dtype=torch.int32))
+
+
+@torch.library.custom_op("mvs::split_head", mutates_args=())
+def split_head(scv: torch.Tensor, absmax: torch.Tensor, w0: torch.Tensor, bn0_scale: Optional[torch.Tensor],
+               bn0_shift: Optional[torch.Tensor], bn0_mean: Optional[torch.Tensor], w1: torch.Tensor,
+               bn1_scale: Optional[torch.Tensor], bn1_shift: Optional[torch.Tensor], bn1_mean: Optional[torch.Tensor],
+               pad: list[int], y1_origin: list[int], y1_size: list[int]) -> tuple[torch.Tensor, torch.Tensor]:
+    """conv_0_0 + BN_0 + ReLU (model.py:101) and conv_1_0 + BN_1 + ReLU (model.py:103) of the split cost
+    volume ``scv`` [B, 8, D, h, w, 4] int32 (cost_volume_c4_split) in ONE pass over it
+    (mvs_split_head_fwd).  Returns (y0 [B, 8, D, h, w], y1 channels-last [B, *y1_size, 16]): bit-identical
+    to conv3d_k3_split and conv_s2_split.  D even, pad odd; inference only."""
+    _require_gpu(scv, "scv")
+    lib = _lib.load()
+    if scv.dim() != 6 or scv.dtype != torch.int32 or scv.shape[1] != 8 or scv.shape[5] != 4:
+        raise ValueError("split cost volume [B, 8, D, h, w, 4] int32 expected")
+    if tuple(w0.shape) != (8, 32, 3, 3, 3) or tuple(w1.shape) != (16, 32, 3, 3, 3):
+        raise ValueError("conv_0_0 [8, 32, 3, 3, 3] and conv_1_0 [16, 32, 3, 3, 3] weights expected")
+    scv = scv.contiguous()
+    b, _, d, h, w, _ = scv.shape
+    dev = scv.device
+    f0, e0 = derived("k3split", (w0,), lambda wt: split_weight_fragments(wt, dev), dev)
+    f1, e1 = derived("s2split", (w1,), lambda wt: _s2_split_fragments(wt, dev), dev)
+
+    def bn(ts):
+        ts = [t if t is None else t.to(device=dev, dtype=_F32).contiguous() for t in ts]
+        if any(t is None for t in ts) and not all(t is None for t in ts):
+            raise ValueError("BN scale, shift and mean go together")
+        return ts, [None if t is None else _lib.ptr(t) for t in ts]
+    bn0, bp0 = bn((bn0_scale, bn0_shift, bn0_mean))
+    bn1, bp1 = bn((bn1_scale, bn1_shift, bn1_mean))
+    y0 = torch.empty((b, 8, d, h, w), device=dev, dtype=_F32)
+    y1 = torch.empty([b] + [int(v) for v in y1_size] + [16], device=dev, dtype=_F32)
+    evs = (None, None)
+    if KERNEL_EVENT_HOOK is not None:
+        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK("split_head"))
+    st = lib.mvs_split_head_fwd(_lib.ptr(scv), _lib.ptr(absmax.contiguous()), b, d, h, w, _lib.ptr(f0), int(e0),
+                                *bp0, _lib.ptr(f1), int(e1), *bp1, _ints3(pad), _ints3(y1_origin),
+                                _ints3(y1_size), _lib.ptr(y0), _lib.ptr(y1), _lib.stream_handle(dev), *evs)
+    _lib.check(st, "mvs_split_head_fwd")
+    return y0, y1
+
+
+@split_head.register_fake
+def _(scv, absmax, w0, bn0_scale, bn0_shift, bn0_mean, w1, bn1_scale, bn1_shift, bn1_mean, pad, y1_origin, y1_size):
+    b, _, d, h, w, _ = scv.shape
+    return (scv.new_empty((b, 8, d, h, w), dtype=_F32), scv.new_empty([b] + list(y1_size) + [16], dtype=_F32))
 
 
 @torch.library.custom_op("mvs::cost_volume_c4_bf16", mutates_args=())

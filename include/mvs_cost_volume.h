@@ -292,6 +292,21 @@ int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, 
  *   y[batch][8][d][h][w] fp32; BN pointers as mvs_conv3d_k3_fwd (8 floats each, all or none).
  * 128*d*h*w <= 2^32 - 16 (one sample's volume bytes).  Replaces the Conv3d behind model.py:101's
  * conv_0_0 in eval inference. */
+/* conv_0_0 + BN_0 + ReLU (model.py:101) and conv_1_0 + BN_1 + ReLU (model.py:103) of a MATERIALISED
+ * split cost volume in ONE pass over it (the split volume of mvs_cost_volume_fwd_c4_split: read once
+ * instead of once per layer; csrc/cv_head.hip's MFMA code fed by plain plane loads).
+ * Bit-identical to mvs_conv3d_k3_split_fwd + mvs_conv3d_s2_split_fwd on the same volume.
+ *   scv: [batch][8][d_count][h][w] x 16 B (DEVICE, 16-byte aligned), x_absmax its bound words;
+ *   w0_frag / w0_exp, bn0_*, w1_frag / w1_exp, bn1_*, pad, y1_origin, y1_size, y0, y1: as
+ *   mvs_cost_volume_head_fwd (d_count even, every pad odd).
+ * 128 * d_count * h * w <= 2^32 - 16.  Events (either may be NULL) are recorded around the kernel. */
+int mvs_split_head_fwd(const void* scv, const unsigned* x_absmax, int batch, int d_count, int h, int w,
+                       const void* w0_frag, int w0_exp, const float* bn0_scale, const float* bn0_shift,
+                       const float* bn0_mean, const void* w1_frag, int w1_exp, const float* bn1_scale,
+                       const float* bn1_shift, const float* bn1_mean, const int* pad, const int* y1_origin,
+                       const int* y1_size, float* y0, float* y1, void* stream, void* main_begin_event,
+                       void* main_end_event);
+
 int mvs_conv3d_k3_split_fwd(const void* x, int flags, const void* weight_frag, int weight_exp,
                             const unsigned* x_absmax, float* y, int batch, int d, int h, int w,
                             const float* bn_scale, const float* bn_shift, const float* bn_mean, void* stream);

@@ -60,10 +60,19 @@ def cfg2_inputs():
 
 def kept_planes(P, stable=True):
     """[D,h,w] -> [5,h,w] uint8: the ascending indices of the planes depthmap.py:11-15 keeps (ties in
-    P ranked by ascending plane index when stable; torch.sort exactly as the reference calls it else)."""
+    P ranked by ascending plane index when stable; torch.sort exactly as the reference calls it else).
+
+    The reference keeps plane r when argsort_desc(P)[r] < N_DEPTH_EST (``prob_mask < N``: the mask is
+    indexed by plane, the test by the index found at that RANK) -- i.e. the planes r that equal the
+    ranks of planes 0..4, not the five most probable planes (the permutation-indexed
+    mask; tests/test_oracle.py::test_soft_argmin_golden pins it on the reference's own output).
+    (Before round 5 this helper returned the five most probable planes: a pixel whose real mask
+    changed could count as unflipped.)"""
     t = torch.as_tensor(np.ascontiguousarray(P))
     _, order = torch.sort(t, dim=0, descending=True, stable=stable)
-    return np.sort(order[:N_EST].numpy(), axis=0).astype(np.uint8)
+    mask = (order < N_EST).numpy()
+    # the N_EST planes where the mask holds, in ascending plane order
+    return np.argsort(~mask, axis=0, kind="stable")[:N_EST].astype(np.uint8)
 
 
 SIG_P = 1e-7   # a kept plane below this probability moves depth by < ~1e-7 relative: not a flip

@@ -175,9 +175,9 @@ def _depth_parity(P_gpu, P_ref, d_gpu, d_ref):
 
 def test_cfg2_end_to_end_as_benchmarked():
     """The bench workload exactly as bench.py runs it: B=4, V=3, 640x512, D=192, BN eval mode,
-    no_grad, MVSNet.forward -> the fused head (csrc/cv_head.hip: warp + variance formed on chip, split-
-    fp16 conv_0_0 / conv_1_0) -> forward_live's HIP region convs on the head's outputs and stored box ->
-    HIP softmax / soft-argmin -> refinement.
+    no_grad, MVSNet.forward -> the fused warp + variance kernel (split cost volume) -> the split head
+    (csrc/cv_head.hip PRESPLIT: split-fp16 conv_0_0 + conv_1_0 in one pass) -> forward_live's HIP region
+    convs -> HIP softmax / soft-argmin -> refinement.
 
       * the benchmarked call's OWN probability volume (captured from the regulariser by a forward
         hook) against the CPU oracle forward (oracle/mvs_oracle.py::mvsnet_forward, the reference's
@@ -282,8 +282,8 @@ def test_cfg2_end_to_end_as_benchmarked():
 def test_cfg2_depth_flips_within_reference_self_noise():
     """cfg 2's depth against the float64 law, with the reference's OWN fp32 noise as the yardstick
     (tests/golden/make_cfg2_selfnoise.py: the CPU fp32 oracle and mvs_oracle.mvsnet_forward64 on the
-    same weights / images, committed).  The benchmarked call (MVSNet.forward: fused head, split-fp16
-    conv_0_0 / conv_1_0, HIP soft-argmin) is run on all 4 samples; with its probability volume (the
+    same weights / images, committed).  The benchmarked call (MVSNet.forward: split cost volume, split
+    head -- split-fp16 conv_0_0 / conv_1_0 --, HIP soft-argmin) is run on all 4 samples; with its probability volume (the
     regulariser's output, captured by a forward hook):
 
       * GPU-vs-f64 mask flips (the depthmap.py:11-15 kept-plane sets differ in a plane that carries

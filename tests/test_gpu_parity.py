@@ -1071,4 +1071,7 @@ def test_cost_volume_bit_exact_vs_oracle_given_matrices(geom):
                   cv_gpu_vs_host_torch_max_abs=float(np.abs(cg - cv_ref).max()))
     assert np.array_equal(wg, law), (wg != law).mean()
     assert np.array_equal(cg, cv_law), (cg != cv_law).mean()
-    np.testing.assert_allclose(cg, cv_ref, rtol=1e-5, atol=1e-6)
+    # torch CPU on another host (e.g. an AMD EPYC box: MKL's sgemm kernel, reduction order) rounds some
+    # steps differently: fp32 rounding level relative to the volume's scale (a variance of nearly equal
+    # samples cancels, so elementwise relative differences are not the measure)
+    assert np.abs(cg - cv_ref).max() <= 1e-4 * np.abs(cv_ref).max(), np.abs(cg - cv_ref).max()

@@ -26,6 +26,8 @@ DEV = torch.device("cuda", 0)
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 USE_BN = len(sys.argv) > 2 and sys.argv[2] == "bn"
 CFGS = [(1, 2, 20, 24, 40), (1, 3, 16, 29, 41), (2, 3, 16, 32, 48), (1, 3, 48, 28, 64), (4, 3, 192, 128, 160)]
+if os.environ.get("HEAD_STRESS_CFGS"):   # e.g. "1,2,20,24,40;1,3,16,29,41"
+    CFGS = [tuple(int(v) for v in c.split(",")) for c in os.environ["HEAD_STRESS_CFGS"].split(";")]
 
 
 def where(bad, tag):
@@ -74,21 +76,49 @@ for (B, V, D, h, w) in CFGS:
 
     with torch.no_grad():
         ref = split_path()
+        ref_full = ops.cost_volume_c4_split(feat, K, R, T, d_min, d_int, B, V, 0, D, 25.0)
         torch.cuda.synchronize()
         counts = {}
         shown = 0
-        for name, fn in (("head", head), ("split", split_path)):
+        def split_head():   # the head's consumers fed from the materialised split volume (V = 2 only)
+            scv, am = ref_full
+            y0, y1 = ops.split_head(scv, am, w0, *bn0, w1, *bn1, pad, org, size)
+            return y0, y1, ref[2]
+        kinds = [("head", head), ("split", split_path)] + ([("split_head", split_head)] if V == 2 else [])
+        for name, fn in kinds:
             nbad = 0
             for it in range(N):
                 out = fn()
                 torch.cuda.synchronize()
                 diff = [not torch.equal(a, b) for a, b in zip(out, ref)]
+                if os.environ.get("HEAD_STRESS_BOX_ONLY") and name == "head":   # ablation builds: y0 / y1 not formed
+                    diff[0] = diff[1] = False
                 if any(diff):
                     nbad += 1
-                    if shown < 4:
+                    if shown < int(os.environ.get("HEAD_STRESS_SHOW", "4")):
                         shown += 1
                         print("  %s launch %d differs: y0 %s y1 %s box %s" % (name, it, *diff), flush=True)
                         if diff[0]:
                             where(out[0] != ref[0], "y0")
+                        if diff[2] and os.environ.get("HEAD_STRESS_DETAIL"):
+                            # the box holds the ring's split operands: which (quad, plane, y, x) and what was
+                            # written instead -- zeros (a lost write), or the value of another voxel / plane
+                            bb = (out[2] != ref[2]).any(-1).nonzero()
+                            full_ref = ref_full[0]
+                            for e in bb[:6].tolist():
+                                b_, q, z, y, x = e
+                                got = out[2][b_, q, z, y, x].tolist()
+                                want = ref[2][b_, q, z, y, x].tolist()
+                                zz, yy, xx = z + lo[0], y + lo[1], x + lo[2]
+                                hits = (full_ref[b_, q] == out[2][b_, q, z, y, x]).all(-1).nonzero()[:4].tolist()
+                                # the wrong half-words alone: hi.y / lo.y = channels 4q+2, 4q+3 (fp16 pairs)
+                                wy = out[2][b_, q, z, y, x]
+                                h1 = (full_ref[b_, q][..., 1] == wy[1]).nonzero()[:4].tolist()
+                                l1 = (full_ref[b_, q][..., 3] == wy[3]).nonzero()[:4].tolist()
+                                # low fp16 (channel 4q+2) of hi.y anywhere in the quad plane
+                                lo16 = (full_ref[b_, q][..., 1] & 0xFFFF) == (int(wy[1]) & 0xFFFF)
+                                print("    box (b%d q%d z%d y%d x%d): head %s ref %s; whole entry in ref at %s; hi.y at %s; lo.y at %s;"
+                                      " hi.y low fp16 at %s" % (b_, q, zz, yy, xx, got, want, hits, h1, l1,
+                                                               lo16.nonzero()[:6].tolist()), flush=True)
             counts[name] = nbad
     print("cfg", (B, V, D, h, w), "bn" if USE_BN else "raw", "differing launches of %d:" % N, counts, flush=True)

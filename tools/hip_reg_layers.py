@@ -15,7 +15,7 @@ sys.path.insert(0, REPO)
 import bench  # noqa: E402
 import torch  # noqa: E402
 from mvs_amd import model as M  # noqa: E402
-from mvs_amd.ops import conv_s2_split  # noqa: E402
+from mvs_amd.ops import conv_s2_split, split_head  # noqa: E402
 from mvs_amd.ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_k3_split, conv3d_region,  # noqa: E402
                          deconv3d_k3s2, region_weight, softmax_depth)
 
@@ -115,6 +115,11 @@ def main():
         print("cv_head vs split path: y0 equal %s (max|d| %.3g), y1 equal %s (max|d| %.3g), box equal %s" % (
             torch.equal(y0h, y0s), (y0h - y0s).abs().max().item(), torch.equal(y1h, y1s),
             (y1h - y1s).abs().max().item(), torch.equal(box.data, cvs[sl])), flush=True)
+        layers["split_head"] = lambda: split_head(cvs, bound, reg.conv_0_0.weight, *bn(reg.BN_0), reg.conv_1_0.weight,
+                                                  *bn(reg.BN_1), pad, org(h1), size(h1))
+        y0p, y1p = layers["split_head"]()
+        print("split_head vs split path: y0 equal %s, y1 equal %s" % (torch.equal(y0p, y0s), torch.equal(y1p, y1s)),
+              flush=True)
         if a.only:   # one layer or a comma-separated list ("step": the whole eval step)
             for name in a.only.split(","):
                 timed(name, (lambda: net(img, K, R, T, d_min, d_int, B, V)) if name == "step" else layers[name],
@@ -123,9 +128,12 @@ def main():
         for name, fn in layers.items():
             timed(name, fn, a.reps)
         step = lambda: net(img, K, R, T, d_min, d_int, B, V)
-        timed("eval step (fused head)", step, a.reps)
-        os.environ["MVS_CV_HEAD"] = "0"
-        timed("eval step (split volume)", step, a.reps)
+        timed("eval step (split volume + split head)", step, a.reps)
+        os.environ["MVS_SPLIT_HEAD"] = "0"
+        timed("eval step (split volume, separate conv_0_0 / conv_1_0)", step, a.reps)
+        os.environ.pop("MVS_SPLIT_HEAD")
+        os.environ["MVS_CV_HEAD"] = "1"
+        timed("eval step (opt-in fused gather head)", step, a.reps)
         os.environ.pop("MVS_CV_HEAD")
         reg.split_f16 = False
         timed("eval step (exact fp32 conv_0_0)", step, a.reps)
