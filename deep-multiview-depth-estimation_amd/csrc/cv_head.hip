@@ -275,47 +275,55 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     }
   }
   const int zst0 = max(z0, a.r0[0]), zst1 = min(z1, a.r1[0]);   // planes stored to the SCV box
-  // PRE: batch j's two planes copied from the split volume (all items' loads in flight together, then
-  // their LDS stores); invalid items (outside the image or the volume) load the sample's first element
-  // and store zeros -- no out-of-range load
+  // PRE: batch j's two planes copied from the split volume, software-pipelined across the step
+  // barrier: pre_load(j + 1) is issued right after pre_store(j)'s LDS stores have completed, so its
+  // HBM latency runs under a whole step of MFMAs (issued and stored in the same step, the loads were
+  // the step's critical path); invalid items (outside the image or the volume) load the sample's first
+  // element and store zeros -- no out-of-range load
   const Rsrc rin = make_rsrc(PRE ? static_cast<const char*>(a.scv_in) + (size_t)b * kC4 * D * HW * 16 : nullptr,
                              PRE ? (uint32_t)min((uint64_t)kC4 * D * HW * 16ull, 0xFFFFFFF0ull) : 0u);
-  auto items_pre = [&](int j) {
+  typedef __attribute__((ext_vector_type(4))) unsigned v4u;
+  v4u pd[kItems];
+  uint32_t pok = 0;   // bit u: item u of the batch in registers is valid
+  const int pnu = __builtin_amdgcn_readfirstlane(ptid + 256 * (kItems - 1) < kBatchItems ? kItems : kItems - 1);
+  auto pre_load = [&](int j) {
     const int pbase = z0 - 1 + 2 * j;
-    const int sl0 = slot_of(pbase);
-    const int nu = __builtin_amdgcn_readfirstlane(ptid + 256 * (kItems - 1) < kBatchItems ? kItems : kItems - 1);
-    typedef __attribute__((ext_vector_type(4))) unsigned v4u;
-    v4u d[kItems];
-    bool ok[kItems];
+    pok = 0;
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
-      if (u == kItems - 1 && nu != kItems) break;   // wave-uniform
+      if (u == kItems - 1 && pnu != kItems) break;   // wave-uniform
       const uint32_t m = meta[u];
       const int pl = (m >> 15) & 1, q = (m >> 16) & 7, v = (int)(m >> 19);
       const int p = pbase + pl;
       const int yy = v / kHX, xx = v - yy * kHX;
-      ok[u] = (m & (1u << 13)) && (unsigned)p < (unsigned)D;
-      const uint32_t off = ok[u] ? ((((uint32_t)q * (uint32_t)D + (uint32_t)p) * (uint32_t)HW +
-                                     (uint32_t)((y0 - 1 + yy) * W + (x0 - 1 + xx))) * 16u) : 0u;
-      d[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, (int)off, 0, 0);
+      const bool ok = (m & (1u << 13)) && (unsigned)p < (unsigned)D;
+      pok |= ok ? (1u << u) : 0u;
+      const uint32_t off = ok ? ((((uint32_t)q * (uint32_t)D + (uint32_t)p) * (uint32_t)HW +
+                                  (uint32_t)((y0 - 1 + yy) * W + (x0 - 1 + xx))) * 16u) : 0u;
+      pd[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, (int)off, 0, 0);
     }
+  };
+  auto pre_store = [&](int j) {
+    const int sl0 = slot_of(z0 - 1 + 2 * j);
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
-      if (u == kItems - 1 && nu != kItems) break;
+      if (u == kItems - 1 && pnu != kItems) break;
       const uint32_t m = meta[u];
       const int pl = (m >> 15) & 1;
-      const uint2 hi = ok[u] ? make_uint2(d[u].x, d[u].y) : make_uint2(0u, 0u);
-      const uint2 lo = ok[u] ? make_uint2(d[u].z, d[u].w) : make_uint2(0u, 0u);
+      const bool ok = (pok >> u) & 1u;
+      const uint2 hi = ok ? make_uint2(pd[u].x, pd[u].y) : make_uint2(0u, 0u);
+      const uint2 lo = ok ? make_uint2(pd[u].z, pd[u].w) : make_uint2(0u, 0u);
       char* dst = ring + (sl0 + pl) * kSlotB + (m & 0x1FFFu);
       *reinterpret_cast<uint2*>(dst) = hi;
       *reinterpret_cast<uint2*>(dst + kPartB) = lo;
     }
+    // the stores have read their data registers before the next batch's loads target them
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
   };
   auto items = [&](int j, int tb) {
-    if constexpr (PRE) {
-      items_pre(j);
-      return;
-    }
+    if constexpr (PRE) return;   // (pre_load / pre_store)
     const int pbase = z0 - 1 + 2 * j;
     const int sl0 = slot_of(pbase);   // even: the batch's second plane is the next slot
     const int nu = __builtin_amdgcn_readfirstlane(ptid + 256 * (kItems - 1) < kBatchItems ? kItems : kItems - 1);
@@ -449,6 +457,25 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   // ================================ schedule ================================
   // Both roles pass the same barriers (nsteps + 3): producers fill batches 0, 1 before step 0 and batch
   // k + 2 during step k; the sampling state of a batch is formed at least one barrier before its items.
+  if (!consumer && PRE) {
+    pre_load(0);
+    __syncthreads();
+    pre_store(0);
+    pre_load(1);
+    pre_store(1);
+    if (2 < nbatch) pre_load(2);
+    __syncthreads();
+    __syncthreads();
+    for (int k = 0; k < nsteps; ++k) {
+      if (k + 2 < nbatch) {
+        pre_store(k + 2);
+        if (k + 3 < nbatch) pre_load(k + 3);
+      }
+      __syncthreads();
+    }
+    __syncthreads();
+    return;
+  }
   if (!consumer) {
     stamp();
     if (!kCoordsByConsumers) {
@@ -601,7 +628,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   for (int k = 0; k < nsteps; ++k) {
     const int zs = z0 + 2 * k;
     // ---- conv_0_0 on planes zs - 1 .. zs + 2 (conv3d_split.hip's item order) ----
-#ifdef MVS_HEAD_ABL_C
+#if defined(MVS_HEAD_ABL_C) || defined(MVS_HEAD_NO_C0)   // (timing ablations)
     if (false) {
 #else
     if (row_on) {
@@ -665,7 +692,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     }
     stamp();
     // ---- conv_1_0: window zs - 1 completes (depth tap 2 on plane zs + 1), window zs + 1 starts ----
-#ifdef MVS_HEAD_ABL_C
+#if defined(MVS_HEAD_ABL_C) || defined(MVS_HEAD_NO_MAC1)
     if (false) {
 #else
     if (wave < 3) {

@@ -471,11 +471,13 @@ def test_model_end_to_end_at_cfg3_cfg5(cfg):
         # north_star's 1e-4 on the depth map, against the reference arithmetic given the same matrices
         h64 = res["cfg5_oracle_h64"]
         assert h64["mask_flip_frac"] < 0.02 and h64["within_1e4_frac_unflipped"] >= 0.9995, h64
-        # against the reference itself: no further than the reference's own fp32 homography puts it from
-        # the same fixture (r05: reference 97.81 % of unflipped pixels within 1e-4, max 15.8 %)
+        # against the reference itself: north_star's 1e-4 on every unflipped pixel's depth, and mask flips
+        # no more frequent than the reference's own fp32 homography makes them against the fp64-matrix
+        # fixture (r05 with the reference's permutation-indexed mask: reference vs h64 2.24 % flips, every
+        # unflipped pixel within 1e-4, max 5.9e-5; GPU vs reference 2.23 %, max 5.9e-5)
         rf, own = res["cfg5_oracle"], res["reference_vs_h64"]
-        assert rf["mask_flip_frac"] < 0.02, rf
-        assert rf["within_1e4_frac_unflipped"] >= own["within_1e4_frac_unflipped"] - 3e-3, (rf, own)
+        assert rf["within_1e4_frac_unflipped"] >= 0.9995, rf
+        assert rf["mask_flip_frac"] <= own["mask_flip_frac"] + 2e-3, (rf, own)
     assert torch.isfinite(ini).all() and torch.isfinite(ref).all()
     assert torch.equal(ini_live, ini)
     torch.testing.assert_close(P_live, P_full, rtol=1e-4, atol=1e-9)

@@ -6,7 +6,8 @@
 #   prof   rocprofv3 --kernel-trace --stats of a short bench (the roofline agreement source)
 #   pmc    head counters, one counter group per rocprofv3 pass, on tools/hip_reg_layers.py --only cv_head
 #   stress tools/dbg/head_stress.py: repeatability of the head and the split path (raw and with BN)
-#   trace  rocprofv3 kernel stats of one step kind each: cfg-2 train-mode BN (test.py:61), cfg-3 eval
+#   trace  rocprofv3 kernel stats of one step kind each (TRACES="mode batch views;..."): cfg-2 eval, cfg-2
+#          train-mode BN (test.py:61), cfg-3 eval; per step = over 3 warm-up + 5 timed steps
 # Every GPU step has its own time limit; the script stops at the first failing step.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; TAG=${1:-r5}; shift; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
 STAGES=${*:-tests smoke bench prof pmc}
@@ -61,11 +62,13 @@ if has stress; then
   echo "stress bn rc=$rc"; grep -E "cfg|differs" $OUT/head_stress_bn.log | head -40; [ $rc -ne 0 ] && exit $rc
 fi
 if has trace; then
-  for m in "train 4 3" "eval 8 5"; do set -- $m
+  IFS=';' read -ra TRACES <<< "${TRACES:-eval 4 3;train 4 3;eval 8 5}"
+  for m in "${TRACES[@]}"; do set -- $m
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/tr_$1_v$3" -o run --output-format csv -- \
       python3 tools/step_trace.py --mode $1 --batch $2 --views $3 --steps 5 > $OUT/tr_$1_v$3.log 2>&1
     rc=$?; echo "trace $1 v$3 rc=$rc"; grep "step" $OUT/tr_$1_v$3.log | tail -2; [ $rc -ne 0 ] && exit $rc
-    f=$(ls $OUT/tr_$1_v$3/*/run_kernel_stats.csv $OUT/tr_$1_v$3/run_kernel_stats.csv 2>/dev/null | head -1); head -16 "$f" | cut -c1-150
+    f=$(ls $OUT/tr_$1_v$3/*/run_kernel_stats.csv $OUT/tr_$1_v$3/run_kernel_stats.csv 2>/dev/null | head -1)
+    python3 tools/kstats.py "$f" 8 22
   done
 fi
 exit 0
