@@ -65,7 +65,18 @@ constexpr int kThreads = 512;
 constexpr int kPlaneItems = kHV * kC4;                   // 864 (voxel, quad) items per plane
 constexpr int kBatchItems = 2 * kPlaneItems;             // two planes per step
 constexpr int kItems = (kBatchItems + 255) / 256;        // 7 per producer thread
-constexpr int kPF = 3;                                   // conv_0_0 A-fragment prefetch (items)
+#ifndef MVS_HEAD_KPF
+#define MVS_HEAD_KPF 3
+#endif
+constexpr int kPF = MVS_HEAD_KPF;                        // conv_0_0 A-fragment prefetch (items)
+#ifndef MVS_HEAD_PD
+#define MVS_HEAD_PD 1
+#endif
+constexpr int kPD = MVS_HEAD_PD;                         // PRESPLIT: batches of loads in flight
+#ifndef MVS_HEAD_VFAST
+#define MVS_HEAD_VFAST 1
+#endif
+constexpr bool kPreVoxelFast = MVS_HEAD_VFAST;
 // the sampling state of a batch is formed by the CONSUMER waves after their matrix work (they wait at
 // the step barrier otherwise; the producers' gathers are the step's critical path: cfg 2 2.28 -> 2.19 ms)
 constexpr bool kCoordsByConsumers = true;
@@ -74,9 +85,13 @@ template <int NS, bool PRE = false>
 constexpr int coord_bytes() {   // [2 buffers][2 planes][NS views][108 voxels] x {off, wx, wy, -}
   return PRE ? 0 : 2 * 2 * NS * kHV * 16;
 }
+template <bool PRE>
+constexpr int w1_lds_bytes() {   // PRE: the conv_1_0 product waves hold their fragments in registers
+  return PRE ? 0 : kW1B;
+}
 template <int NS, bool PRE = false>
 constexpr int lds_bytes() {
-  return kRingB + kW1B + coord_bytes<NS, PRE>() + kScrB;
+  return kRingB + w1_lds_bytes<PRE>() + coord_bytes<NS, PRE>() + kScrB;
 }
 
 struct HeadArgs {
@@ -112,16 +127,17 @@ __device__ inline float ror8(float v) {   // value of lane (l ^ 8) inside each 1
 }
 
 // PRE (mvs_split_head_fwd): the cost volume is already materialised as the split volume; the producer
-// waves only copy its planes into the ring (one 16-byte load and two 8-byte LDS stores per item) and
-// the consumers run exactly the MFMA code below -- conv_0_0 and conv_1_0 of the split path in ONE pass
-// over the volume, bit-equal to conv3d_split.hip + conv3d_s2_split.hip.
+// waves copy its planes into the ring (one 16-byte load and two 8-byte LDS stores per item) and, while
+// the next planes' loads are in flight, run conv_1_0 (its three split products with their weight
+// fragments in registers, and the window finish); the consumers run conv_0_0 -- both convolutions
+// of the split path in ONE pass over the volume, bit-equal to conv3d_split.hip + conv3d_s2_split.hip.
 template <int V, bool PRE = false>
 __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   constexpr int NS = V - 1;
   __shared__ __attribute__((aligned(16))) char lds[lds_bytes<NS, PRE>()];
   char* const ring = lds;
   char* const w1l = lds + kRingB;
-  char* const coord = lds + kRingB + kW1B;
+  char* const coord = lds + kRingB + w1_lds_bytes<PRE>();
   char* const scr = coord + coord_bytes<NS, PRE>();
 
   const int wk = xcd_work_id((int)blockIdx.x, (int)gridDim.x);
@@ -158,7 +174,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
 #endif
 
   // conv_1_0 weight fragments -> LDS (every thread)
-  {
+  if constexpr (!PRE) {
     const Rsrc rw = make_rsrc(a.w1, (uint32_t)kW1B);
 #pragma unroll
     for (int j = 0; j < (kW1B / 16 + kThreads - 1) / kThreads; ++j) {
@@ -266,7 +282,10 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       const int e = min(ptid + 256 * u, kBatchItems - 1);
       const int pl = e >= kPlaneItems ? 1 : 0;
       const int r = e - pl * kPlaneItems;
-      const int v = r >> 3, q = r & 7;
+      // PRE (MVS_HEAD_VFAST): voxel fastest, so a wave's 64 loads are runs of one quad plane (rows of
+      // 18 x 16 B) instead of 8 voxels x 8 quad planes 2^22 B apart
+      const bool vfast = PRE && kPreVoxelFast;
+      const int v = vfast ? r % kHV : r >> 3, q = vfast ? r / kHV : r & 7;
       const int yy = v / kHX, xx = v - yy * kHX;
       const int gx = x0 - 1 + xx, gy = y0 - 1 + yy;
       const bool vin = gx >= 0 && gx < W && gy >= 0 && gy < H;
@@ -283,12 +302,12 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   const Rsrc rin = make_rsrc(PRE ? static_cast<const char*>(a.scv_in) + (size_t)b * kC4 * D * HW * 16 : nullptr,
                              PRE ? (uint32_t)min((uint64_t)kC4 * D * HW * 16ull, 0xFFFFFFF0ull) : 0u);
   typedef __attribute__((ext_vector_type(4))) unsigned v4u;
-  v4u pd[kItems];
-  uint32_t pok = 0;   // bit u: item u of the batch in registers is valid
+  v4u pd[kPD][kItems];   // kPD batches in flight (buffer j % kPD)
+  uint32_t pok[kPD];     // bit u: item u of the buffered batch is valid
   const int pnu = __builtin_amdgcn_readfirstlane(ptid + 256 * (kItems - 1) < kBatchItems ? kItems : kItems - 1);
-  auto pre_load = [&](int j) {
+  auto pre_load = [&](int j, int pb) {
     const int pbase = z0 - 1 + 2 * j;
-    pok = 0;
+    pok[pb] = 0;
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
       if (u == kItems - 1 && pnu != kItems) break;   // wave-uniform
@@ -297,22 +316,22 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       const int p = pbase + pl;
       const int yy = v / kHX, xx = v - yy * kHX;
       const bool ok = (m & (1u << 13)) && (unsigned)p < (unsigned)D;
-      pok |= ok ? (1u << u) : 0u;
+      pok[pb] |= ok ? (1u << u) : 0u;
       const uint32_t off = ok ? ((((uint32_t)q * (uint32_t)D + (uint32_t)p) * (uint32_t)HW +
                                   (uint32_t)((y0 - 1 + yy) * W + (x0 - 1 + xx))) * 16u) : 0u;
-      pd[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, (int)off, 0, 0);
+      pd[pb][u] = __builtin_amdgcn_raw_buffer_load_b128(rin, (int)off, 0, 0);
     }
   };
-  auto pre_store = [&](int j) {
+  auto pre_store = [&](int j, int pb) {
     const int sl0 = slot_of(z0 - 1 + 2 * j);
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
       if (u == kItems - 1 && pnu != kItems) break;
       const uint32_t m = meta[u];
       const int pl = (m >> 15) & 1;
-      const bool ok = (pok >> u) & 1u;
-      const uint2 hi = ok ? make_uint2(pd[u].x, pd[u].y) : make_uint2(0u, 0u);
-      const uint2 lo = ok ? make_uint2(pd[u].z, pd[u].w) : make_uint2(0u, 0u);
+      const bool ok = (pok[pb] >> u) & 1u;
+      const uint2 hi = ok ? make_uint2(pd[pb][u].x, pd[pb][u].y) : make_uint2(0u, 0u);
+      const uint2 lo = ok ? make_uint2(pd[pb][u].z, pd[pb][u].w) : make_uint2(0u, 0u);
       char* dst = ring + (sl0 + pl) * kSlotB + (m & 0x1FFFu);
       *reinterpret_cast<uint2*>(dst) = hi;
       *reinterpret_cast<uint2*>(dst + kPartB) = lo;
@@ -454,26 +473,158 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     }
   };
 
+  // ================================ conv_1_0 state ================================
+  // conv_1_0 (model.py:103) runs on the consumer waves, or in PRE on the producer waves, idle while
+  // their loads are in flight; c1w = the wave's index in that role: 0-2 the three split products, 3
+  // finishes each window from their partials (scratch, double buffered)
+  const bool c1role = PRE ? !consumer : consumer;
+  const int c1w = wave & 3;
+  const int i16 = lane & 15, g4 = lane >> 4;
+  float sc1 = 1.0f, sh1 = 0.0f, mu1 = 0.0f;
+  auto load_bn1 = [&]() {
+    if (a.bn1_sc) {
+      sc1 = a.bn1_sc[i16];
+      sh1 = a.bn1_sh[i16];
+      mu1 = a.bn1_mu[i16];
+    }
+    asm volatile("" ::"v"(sc1), "v"(sh1), "v"(mu1));
+  };
+  const int oexp1 = -(ex + a.w_exp1);
+  // PRE: the product wave's 27 (depth tap, tap) fragments of its weight part, in registers
+  // (loaded inside the role's branch: live ranges of the two roles' fragments never overlap)
+  h8v bw1[PRE ? 27 : 1];
+  auto load_bw1 = [&]() {
+    if (c1w < 3) {
+      const Rsrc rw = make_rsrc(a.w1, (uint32_t)kW1B);
+      const int bp = c1w == 1 ? 1 : 0;
+#pragma unroll
+      for (int j = 0; j < (PRE ? 27 : 1); ++j)
+        bw1[j] = __builtin_bit_cast(h8v, __builtin_amdgcn_raw_buffer_load_b128(rw, ((j * 2 + bp) * 64 + lane) * 16, 0, 0));
+    }
+  };
+  // conv_1_0: MFMA row i16 = window (jx, jy); product wave w < 3
+  const int jx = i16 & 7, jy = i16 >> 3;
+  const int apart = c1w == 2 ? kPartB : 0;    // x_lo for product 2
+  const int bpart = c1w == 1 ? 1 : 0;         // w_lo for product 1
+  int acol[3];
+#pragma unroll
+  for (int tx = 0; tx < 3; ++tx) {
+    const int c = 2 * jx + tx;
+    acol[tx] = apart + c * kVoxB + ((g4 ^ ((c >> 1) & 3)) << 4);
+  }
+  f4 cur = {0.f, 0.f, 0.f, 0.f}, nxt = cur;
+  // acc += the 9 (ty, tx) taps of depth tap tz on plane slot sl (product wave's operands), in tap order;
+  // conv3d_s2_split.hip's pipeline: operands read two taps ahead into a register ring, the schedule
+  // pinned (sched_barrier) so no LDS read is re-targeted at registers an in-flight MFMA still reads
+  auto mac1 = [&](f4& acc, int sl, int tz) {
+    const char* base = ring + sl * kSlotB;
+    auto ld = [&](int t, h8v& x, h8v& wv) {
+      const int ty = t / 3, tx = t - 3 * (t / 3);
+      x = *reinterpret_cast<const h8v*>(base + (2 * jy + ty) * kRowB + acol[tx]);
+      if constexpr (PRE) wv = bw1[tz * 9 + t];
+      else wv = *reinterpret_cast<const h8v*>(w1l + (((tz * 9 + t) * 2 + bpart) * 64 + lane) * 16);
+    };
+    h8v xr[3], wr[3];
+    ld(0, xr[0], wr[0]);
+    ld(1, xr[1], wr[1]);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (t + 2 < 9) ld(t + 2, xr[(t + 2) % 3], wr[(t + 2) % 3]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xr[t % 3], wr[t % 3], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // role wave 3: the completed window of depth start s from the partials in scratch buffer sb
+  auto finish1 = [&](int s, int sb) {
+    const f4 aa = *reinterpret_cast<const f4*>(scr + ((sb * 3 + 0) * 64 + lane) * 16);
+    const f4 ab = *reinterpret_cast<const f4*>(scr + ((sb * 3 + 1) * 64 + lane) * 16);
+    const f4 ac = *reinterpret_cast<const f4*>(scr + ((sb * 3 + 2) * 64 + lane) * 16);
+    const int oz = (s + a.pad[0]) >> 1;
+    if (oz < a.o0[0] || oz >= a.o0[0] + a.on[0]) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * g4 + r, wx_ = row & 7, wy_ = row >> 3;
+      const int oy = (y0 - 1 + 2 * wy_ + a.pad[1]) >> 1, ox = (x0 - 1 + 2 * wx_ + a.pad[2]) >> 1;
+      if (oy < a.o0[1] || oy >= a.o0[1] + a.on[1] || ox < a.o0[2] || ox >= a.o0[2] + a.on[2]) continue;
+      float v = ldexpf(aa[r] + (ab[r] + ac[r]), oexp1);
+      if (a.bn1_sc) v = fmaxf((v - mu1) * sc1 + sh1, 0.0f);
+      const size_t vx = (((size_t)(oz - a.o0[0]) * a.on[1] + (oy - a.o0[1])) * a.on[2] + (ox - a.o0[2]));
+      a.y1[(((size_t)b * a.on[0] * a.on[1] * a.on[2]) + vx) * 16 + i16] = v;
+    }
+  };
+
+  // conv_1_0 in step k: window zs - 1 completes (depth tap 2 on plane zs + 1), window zs + 1 starts
+  auto conv1_step = [&](int k) {
+    const int zs = z0 + 2 * k;
+#if defined(MVS_HEAD_ABL_C) || defined(MVS_HEAD_NO_MAC1)
+    if (false) {
+#else
+    if (c1w < 3) {
+#endif
+      if (k == 0) {
+        mac1(cur, slot_of(z0 - 1), 0);
+        mac1(cur, slot_of(z0), 1);
+      }
+      mac1(cur, slot_of(zs + 1), 2);   // completes window zs - 1
+      mac1(nxt, slot_of(zs + 1), 0);   // window zs + 1: depth taps 0, 1
+      mac1(nxt, slot_of(zs + 2), 1);
+      *reinterpret_cast<f4*>(scr + (((k & 1) * 3 + c1w) * 64 + lane) * 16) = cur;
+      cur = nxt;
+      nxt = f4{0.f, 0.f, 0.f, 0.f};
+    } else if (k > 0) {
+      finish1(zs - 3, (k - 1) & 1);   // the window completed in step k - 1
+    }
+  };
+  // the last step's window; the last chunk also owns the window starting at D - 1 (its taps on
+  // planes D, D + 1 are zero: complete after the last step).  Contains the kernel's last barrier.
+  auto conv1_tail = [&]() {
+    const bool tail = z1 == D;
+    if (c1w < 3 && tail) *reinterpret_cast<f4*>(scr + (((nsteps & 1) * 3 + c1w) * 64 + lane) * 16) = cur;
+    if (c1w == 3) finish1(z1 - 3, (nsteps - 1) & 1);
+    __syncthreads();
+    if (c1w == 3 && tail) finish1(z1 - 1, nsteps & 1);
+  };
+
   // ================================ schedule ================================
   // Both roles pass the same barriers (nsteps + 3): producers fill batches 0, 1 before step 0 and batch
   // k + 2 during step k; the sampling state of a batch is formed at least one barrier before its items.
   if (!consumer && PRE) {
-    pre_load(0);
+    // batches 0, 1 before the first step; batch k + 2 stored during step k, its loads issued kPD
+    // steps earlier (buffer (k + 2) % kPD: the step loop unrolled by kPD keeps the index static)
+    stamp();
+    pre_load(0, 0);
+    load_bw1();
+    load_bn1();
+    stamp();
     __syncthreads();
-    pre_store(0);
-    pre_load(1);
-    pre_store(1);
-    if (2 < nbatch) pre_load(2);
+    stamp();
+    pre_store(0, 0);
+    pre_load(1, 0);
+    pre_store(1, 0);
+#pragma unroll
+    for (int r = 0; r < kPD; ++r)
+      if (2 + r < nbatch) pre_load(2 + r, (2 + r) % kPD);
+    stamp();
     __syncthreads();
+    stamp();
+    stamp();
     __syncthreads();
-    for (int k = 0; k < nsteps; ++k) {
-      if (k + 2 < nbatch) {
-        pre_store(k + 2);
-        if (k + 3 < nbatch) pre_load(k + 3);
+    stamp();
+    for (int k0 = 0; k0 < nsteps; k0 += kPD) {
+#pragma unroll
+      for (int r = 0; r < kPD; ++r) {
+        const int k = k0 + r;
+        if (k >= nsteps) break;   // uniform
+        if (k + 2 < nbatch) pre_store(k + 2, (r + 2) % kPD);
+        if (k + 2 + kPD < nbatch) pre_load(k + 2 + kPD, (r + 2) % kPD);
+        stamp();
+        conv1_step(k);
+        stamp();
+        __syncthreads();
+        stamp();
       }
-      __syncthreads();
     }
-    __syncthreads();
+    conv1_tail();
     return;
   }
   if (!consumer) {
@@ -506,9 +657,8 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     return;
   }
   // ================================ consumer state ================================
-  const int i16 = lane & 15, g4 = lane >> 4;
   h8v bw[27];
-  float sc0 = 1.0f, sh0 = 0.0f, mu0 = 0.0f, sc1 = 1.0f, sh1 = 0.0f, mu1 = 0.0f;
+  float sc0 = 1.0f, sh0 = 0.0f, mu0 = 0.0f;
   {
     const Rsrc rwf = make_rsrc(a.w0, 27u * 64u * 16u);
 #pragma unroll
@@ -519,12 +669,8 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       sh0 = a.bn0_sh[lane & 7];
       mu0 = a.bn0_mu[lane & 7];
     }
-    if (a.bn1_sc) {
-      sc1 = a.bn1_sc[i16];
-      sh1 = a.bn1_sh[i16];
-      mu1 = a.bn1_mu[i16];
-    }
-    asm volatile("" ::"v"(sc0), "v"(sh0), "v"(mu0), "v"(sc1), "v"(sh1), "v"(mu1));
+    asm volatile("" ::"v"(sc0), "v"(sh0), "v"(mu0));
+    if constexpr (!PRE) load_bn1();
   }
   const int gy_out = y0 + wave;   // consumer wave's conv_0_0 output row
   const bool row_on = consumer && gy_out < H && x0 < W;
@@ -532,42 +678,11 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
 #pragma unroll
   for (int kx = 0; kx < 3; ++kx)
     aoff[kx] = (wave & 3) * kRowB + (i16 + kx) * kVoxB + ((g4 ^ (((i16 + kx) >> 1) & 3)) << 4);
-  const int oexp0 = -(ex + a.w_exp0), oexp1 = -(ex + a.w_exp1);
+  const int oexp0 = -(ex + a.w_exp0);
   const int gx0 = x0 + 4 * g4;
   const bool store_lane = (lane & 15) < 8;
   const bool vec_store = (W & 3) == 0 && gx0 + 3 < W;
   const size_t DHW = (size_t)D * HW;
-  // conv_1_0: MFMA row i16 = window (jx, jy); product wave w < 3
-  const int jx = i16 & 7, jy = i16 >> 3;
-  const int apart = wave == 2 ? kPartB : 0;    // x_lo for product 2
-  const int bpart = wave == 1 ? 1 : 0;         // w_lo for product 1
-  int acol[3];
-#pragma unroll
-  for (int tx = 0; tx < 3; ++tx) {
-    const int c = 2 * jx + tx;
-    acol[tx] = apart + c * kVoxB + ((g4 ^ ((c >> 1) & 3)) << 4);
-  }
-  f4 cur = {0.f, 0.f, 0.f, 0.f}, nxt = cur;
-  // acc += the 9 (ty, tx) taps of depth tap tz on plane slot sl (product wave's operands), in tap order;
-  // conv3d_s2_split.hip's pipeline: operands read two taps ahead into a register ring, the schedule
-  // pinned (sched_barrier) so no LDS read is re-targeted at registers an in-flight MFMA still reads
-  auto mac1 = [&](f4& acc, int sl, int tz) {
-    const char* base = ring + sl * kSlotB;
-    auto ld = [&](int t, h8v& x, h8v& wv) {
-      const int ty = t / 3, tx = t - 3 * (t / 3);
-      x = *reinterpret_cast<const h8v*>(base + (2 * jy + ty) * kRowB + acol[tx]);
-      wv = *reinterpret_cast<const h8v*>(w1l + (((tz * 9 + t) * 2 + bpart) * 64 + lane) * 16);
-    };
-    h8v xr[3], wr[3];
-    ld(0, xr[0], wr[0]);
-    ld(1, xr[1], wr[1]);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      if (t + 2 < 9) ld(t + 2, xr[(t + 2) % 3], wr[(t + 2) % 3]);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(xr[t % 3], wr[t % 3], acc, 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
   // conv_2_0 / conv_3_0 read the SCV on their input box: the tile-interior voxels of this chunk's
   // planes (every in-volume voxel is interior to exactly one tile and one chunk), copied from plane p's
   // ring slot -- 512 (voxel, quad) items of 16 B, a wave's 64 lanes four 256-B rows of one quad
@@ -591,25 +706,6 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
             0, 0);
     }
   };
-  // wave 3: the completed window of depth start s from the partials in scratch buffer sb
-  auto finish1 = [&](int s, int sb) {
-    const f4 aa = *reinterpret_cast<const f4*>(scr + ((sb * 3 + 0) * 64 + lane) * 16);
-    const f4 ab = *reinterpret_cast<const f4*>(scr + ((sb * 3 + 1) * 64 + lane) * 16);
-    const f4 ac = *reinterpret_cast<const f4*>(scr + ((sb * 3 + 2) * 64 + lane) * 16);
-    const int oz = (s + a.pad[0]) >> 1;
-    if (oz < a.o0[0] || oz >= a.o0[0] + a.on[0]) return;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = 4 * g4 + r, wx_ = row & 7, wy_ = row >> 3;
-      const int oy = (y0 - 1 + 2 * wy_ + a.pad[1]) >> 1, ox = (x0 - 1 + 2 * wx_ + a.pad[2]) >> 1;
-      if (oy < a.o0[1] || oy >= a.o0[1] + a.on[1] || ox < a.o0[2] || ox >= a.o0[2] + a.on[2]) continue;
-      float v = ldexpf(aa[r] + (ab[r] + ac[r]), oexp1);
-      if (a.bn1_sc) v = fmaxf((v - mu1) * sc1 + sh1, 0.0f);
-      const size_t vx = (((size_t)(oz - a.o0[0]) * a.on[1] + (oy - a.o0[1])) * a.on[2] + (ox - a.o0[2]));
-      a.y1[(((size_t)b * a.on[0] * a.on[1] * a.on[2]) + vx) * 16 + i16] = v;
-    }
-  };
-
   stamp();
   if (kCoordsByConsumers) {
     coords(0, 0);
@@ -691,25 +787,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       }
     }
     stamp();
-    // ---- conv_1_0: window zs - 1 completes (depth tap 2 on plane zs + 1), window zs + 1 starts ----
-#if defined(MVS_HEAD_ABL_C) || defined(MVS_HEAD_NO_MAC1)
-    if (false) {
-#else
-    if (wave < 3) {
-#endif
-      if (k == 0) {
-        mac1(cur, slot_of(z0 - 1), 0);
-        mac1(cur, slot_of(z0), 1);
-      }
-      mac1(cur, slot_of(zs + 1), 2);   // completes window zs - 1
-      mac1(nxt, slot_of(zs + 1), 0);   // window zs + 1: depth taps 0, 1
-      mac1(nxt, slot_of(zs + 2), 1);
-      *reinterpret_cast<f4*>(scr + (((k & 1) * 3 + wave) * 64 + lane) * 16) = cur;
-      cur = nxt;
-      nxt = f4{0.f, 0.f, 0.f, 0.f};
-    } else if (k > 0) {
-      finish1(zs - 3, (k - 1) & 1);   // the window completed in step k - 1
-    }
+    if constexpr (!PRE) conv1_step(k);
     if (kCoordsByConsumers && k + 3 < nbatch) coords(k + 3, (k + 3) & 1);
     // batch k + 1's planes (and plane z0 of batch 0) to the box: resident in their slots this step
     if (k == 0) box_store(z0);
@@ -719,13 +797,8 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     __syncthreads();
     stamp();
   }
-  // the last step's window; the last chunk also owns the window starting at D - 1 (its taps on
-  // planes D, D + 1 are zero: complete after the last step)
-  const bool tail = z1 == D;
-  if (wave < 3 && tail) *reinterpret_cast<f4*>(scr + (((nsteps & 1) * 3 + wave) * 64 + lane) * 16) = cur;
-  if (wave == 3) finish1(z1 - 3, (nsteps - 1) & 1);
-  __syncthreads();
-  if (wave == 3 && tail) finish1(z1 - 1, nsteps & 1);
+  if constexpr (PRE) __syncthreads();   // (the producers' conv1_tail barrier)
+  else conv1_tail();
 }
 
 // Outputs of the conv_1_0 region whose depth / row / column window no tile owns: windows entirely in
@@ -907,9 +980,27 @@ int launch_split_head(const Geometry& g, const void* scv_in, const uint32_t* abs
   const int zero[3] = {0, 0, 0};
   const int gst = head_grid(g, a, pad, o0, on, zero, zero);
   if (gst != MVS_OK) return gst;
+#ifdef MVS_HEAD_STAMP
+  static unsigned long long* stamps = nullptr;
+  const size_t stamp_bytes = (size_t)kStampWG * 8 * kStampN * sizeof(unsigned long long);
+  if (!stamps) (void)hipMalloc(&stamps, stamp_bytes);
+  (void)hipMemsetAsync(stamps, 0, stamp_bytes, s);
+  a.stamps = stamps;
+#endif
   if (ev0) (void)hipEventRecord(ev0, s);
   hipLaunchKernelGGL((cv_head_kernel<2, true>), xcd_grid(a.total), dim3(kThreads), 0, s, a);
   if (ev1) (void)hipEventRecord(ev1, s);
+#ifdef MVS_HEAD_STAMP
+  if (const char* path = getenv("MVS_HEAD_STAMPS")) {   // diagnostic build only: synchronous dump
+    std::vector<unsigned long long> h(stamp_bytes / sizeof(unsigned long long));
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h.data(), stamps, stamp_bytes, hipMemcpyDeviceToHost);
+    if (FILE* f = fopen(path, "ab")) {
+      fwrite(h.data(), 1, stamp_bytes, f);
+      fclose(f);
+    }
+  }
+#endif
   launch_head_faces(g, a, bn1, y1, pad, o0, on, s);
   return MVS_OK;
 }
