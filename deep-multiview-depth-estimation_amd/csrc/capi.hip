@@ -334,10 +334,11 @@ int mvs_split_head_fwd(const void* scv, const unsigned* x_absmax, int batch, int
                        const void* w0_frag, int w0_exp, const float* bn0_scale, const float* bn0_shift,
                        const float* bn0_mean, const void* w1_frag, int w1_exp, const float* bn1_scale,
                        const float* bn1_shift, const float* bn1_mean, const int* pad, const int* y1_origin,
-                       const int* y1_size, float* y0, float* y1, void* stream, void* main_begin_event,
-                       void* main_end_event) {
+                       const int* y1_size, float* y0, float* y1, unsigned* y1_bound, void* stream,
+                       void* main_begin_event, void* main_end_event) {
   if (!scv || !x_absmax || !y0 || !y1 || !w0_frag || !w1_frag || !pad || !y1_origin || !y1_size)
     return MVS_ERR_INVALID_ARGUMENT;
+  if ((uintptr_t)y1_bound & 3u) return MVS_ERR_INVALID_ARGUMENT;
   if (batch <= 0 || d_count <= 0 || h <= 0 || w <= 0 || (d_count & 1)) return MVS_ERR_INVALID_ARGUMENT;
   if ((((uintptr_t)scv) | ((uintptr_t)w0_frag) | ((uintptr_t)w1_frag) | ((uintptr_t)y0)) & 15u ||
       ((uintptr_t)x_absmax & 3u))
@@ -370,7 +371,8 @@ int mvs_split_head_fwd(const void* scv, const unsigned* x_absmax, int batch, int
   const float* bn0[3] = {bn0_scale, bn0_shift, bn0_mean};
   const float* bn1[3] = {bn1_scale, bn1_shift, bn1_mean};
   const int st = mvs::launch_split_head(g, scv, reinterpret_cast<const uint32_t*>(x_absmax), w0_frag, w0_exp, w1_frag,
-                                        w1_exp, bn0, bn1, y0, y1, pad, y1_origin, y1_size, (hipStream_t)stream,
+                                        w1_exp, bn0, bn1, y0, y1, pad, y1_origin, y1_size,
+                                        reinterpret_cast<uint32_t*>(y1_bound), (hipStream_t)stream,
                                         (hipEvent_t)main_begin_event, (hipEvent_t)main_end_event);
   return st != MVS_OK ? st : lc.status();
 }
@@ -560,8 +562,9 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
                           int batch, int c_in, int c_out, const int* dims, const int* out_origin,
                           const int* out_size, const int* in_origin, const int* in_size,
                           const int* pad, const float* bn_scale, const float* bn_shift,
-                          const float* bn_mean, const unsigned* x_absmax, void* stream) {
+                          const float* bn_mean, const unsigned* x_absmax, unsigned* y_bound, void* stream) {
   if (!x || !weight || !y || !dims || !out_origin || !out_size || batch <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if ((uintptr_t)y_bound & 3u) return MVS_ERR_INVALID_ARGUMENT;
   if (mode < MVS_CONV_S1 || mode > MVS_CONV_T2 ||
       (flags & ~(MVS_CONV_OUT_NCDHW | MVS_CONV_IN_C4 | MVS_CONV_IN_BF16 | MVS_CONV_IN_SPLIT)))
     return MVS_ERR_INVALID_ARGUMENT;
@@ -601,7 +604,86 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
   const int st = mvs::launch_conv3d_region(mode, (flags & MVS_CONV_OUT_NCDHW) != 0, quads,
                                            x, x2, weight, y, batch, c_in, c_out, dims, out_origin, out_size,
                                            in_origin, in_size, pad, bn_scale, bn_shift, bn_mean,
-                                           (hipStream_t)stream, reinterpret_cast<const uint32_t*>(x_absmax));
+                                           (hipStream_t)stream, reinterpret_cast<const uint32_t*>(x_absmax),
+                                           reinterpret_cast<uint32_t*>(y_bound));
+  if (st != MVS_OK) return st;
+  return lc.status();
+}
+
+int mvs_conv3d_region_split_weights(const float* weight, int c_in, int c_out, unsigned short* frag, int* weight_exp) {
+  if (!weight || !frag || !weight_exp) return MVS_ERR_INVALID_ARGUMENT;
+  if (c_out <= 0 || c_out % 16 || !(c_in == 16 || (c_in > 0 && c_in % 32 == 0))) return MVS_ERR_INVALID_ARGUMENT;
+  const int n = 27 * c_out * c_in;
+  float m = 0.0f;
+  for (int k = 0; k < n; ++k) {
+    if (!std::isfinite(weight[k])) return MVS_ERR_INVALID_ARGUMENT;
+    m = std::max(m, std::fabs(weight[k]));
+  }
+  int e = 0;
+  if (m > 0.0f) (void)std::frexp(m, &e);
+  const int ew = m > 0.0f ? std::min(std::max(14 - e, -120), 120) : 0;
+  // frag[kb][nb][part][lane][j]: lane (c = lane & 15, g = lane >> 4) holds B[k = 8g + j][column c] of the
+  // 16x16x32 MFMA for output channel nb * 16 + c; part 0 = fp16(w 2^ew), 1 = fp16(w 2^ew - part 0).
+  // K block kb: c_in >= 32: tap kb / (c_in / 32), input channel (kb % (c_in / 32)) * 32 + 8g + j;
+  // c_in = 16: tap 2 kb + (g >> 1) (zero past tap 26), input channel 8 (g & 1) + j.  weight [27][c_out][c_in]
+  const int kbs = mvs::conv3d_region_split_kblocks(c_in), nbs = c_out / 16;
+  for (int kb = 0; kb < kbs; ++kb)
+    for (int nb = 0; nb < nbs; ++nb)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int c = lane & 15, gq = lane >> 4, co = nb * 16 + c;
+          int tap, ci;
+          if (c_in == 16) {
+            tap = 2 * kb + (gq >> 1);
+            ci = 8 * (gq & 1) + j;
+          } else {
+            tap = kb / (c_in / 32);
+            ci = (kb % (c_in / 32)) * 32 + 8 * gq + j;
+          }
+          const float v = tap < 27 ? std::ldexp(weight[((size_t)tap * c_out + co) * c_in + ci], ew) : 0.0f;
+          const _Float16 hi = (_Float16)v;
+          const _Float16 lo = (_Float16)(v - (float)hi);
+          uint16_t bh, bl;
+          std::memcpy(&bh, &hi, 2);
+          std::memcpy(&bl, &lo, 2);
+          const size_t base = ((((size_t)kb * nbs + nb) * 2) * 64 + lane) * 8 + j;
+          frag[base] = bh;
+          frag[base + 64 * 8] = bl;
+        }
+  *weight_exp = ew;
+  return MVS_OK;
+}
+
+int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float* x2, const void* weight_frag,
+                                int weight_exp, float* y, int batch, int c_in, int c_out, const int* dims,
+                                const int* out_origin, const int* out_size, const int* in_origin, const int* in_size,
+                                const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                                const unsigned* x_bound, const unsigned* x2_bound, unsigned* y_bound, void* stream) {
+  if (!x || !weight_frag || !y || !dims || !out_origin || !out_size || !in_origin || !in_size || batch <= 0)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if ((mode != MVS_CONV_S1 && mode != MVS_CONV_T2) || (flags & ~MVS_CONV_OUT_NCDHW)) return MVS_ERR_INVALID_ARGUMENT;
+  if (mode == MVS_CONV_T2 && !pad) return MVS_ERR_INVALID_ARGUMENT;
+  if (x2 && x_bound && !x2_bound) return MVS_ERR_INVALID_ARGUMENT;   // a sum needs both bounds
+  if (((uintptr_t)x | (uintptr_t)x2 | (uintptr_t)weight_frag) & 15u ||
+      ((uintptr_t)x_bound | (uintptr_t)x2_bound | (uintptr_t)y_bound) & 3u)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (weight_exp < -120 || weight_exp > 120) return MVS_ERR_INVALID_ARGUMENT;
+  if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
+    return MVS_ERR_INVALID_ARGUMENT;
+  uint64_t ovox = (uint64_t)batch, svox = 1;
+  for (int k = 0; k < 3; ++k) {
+    if (dims[k] <= 0 || out_size[k] <= 0 || out_origin[k] < 0 || out_origin[k] + out_size[k] > dims[k])
+      return MVS_ERR_INVALID_ARGUMENT;
+    if (in_size[k] <= 0 || in_origin[k] < 0 || in_origin[k] + in_size[k] > dims[k]) return MVS_ERR_INVALID_ARGUMENT;
+    ovox *= (uint64_t)out_size[k];
+    svox *= (uint64_t)in_size[k];
+  }
+  if (ovox >= (1ull << 31) || svox * (uint64_t)c_in * 4u >= 0xFFFFFFC0ull) return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
+  const int st = mvs::launch_conv3d_region_split(
+      mode, (flags & MVS_CONV_OUT_NCDHW) != 0, x, x2, weight_frag, weight_exp, y, batch, c_in, c_out, dims, out_origin,
+      out_size, in_origin, in_size, pad, bn_scale, bn_shift, bn_mean, reinterpret_cast<const uint32_t*>(x_bound),
+      reinterpret_cast<const uint32_t*>(x2_bound), reinterpret_cast<uint32_t*>(y_bound), (hipStream_t)stream);
   if (st != MVS_OK) return st;
   return lc.status();
 }

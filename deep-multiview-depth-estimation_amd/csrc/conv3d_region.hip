@@ -52,6 +52,7 @@ struct Geo {
   int in_c4;    // S2: the volume is channel-quad x[b][C/4][D][H][W][4], fp32 (1), bf16 (2) or the split
                 //     cost volume (3, split.h: fp32 re-formed on load as (hi + lo) 2^-e); 0 NCDHW
   const uint32_t* absmax;   // in_c4 = 3: the volume's bound words (its scale)
+  uint32_t* y_bound;        // optional: the output's bound words (split.h), raised in the epilogue
 };
 
 // T2 parity class: per dim, outputs o with (o + P) % 2 == par; first such o in the region and count
@@ -252,6 +253,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
   }
 
   // ---- epilogue: eval BN + ReLU, NDHWC store.  acc[rb][nb][r] = (row (lane>>4)*4 + r, col lane&15)
+  float vmax = 0.0f;
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     const int co = nb * 16 + m;
@@ -269,9 +271,11 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
                   vx = cf[2] + step * jx - g.o0[2];
         float v = acc[rb][nb][r];
         if (bn_scale) v = fmaxf((v - mu) * sc + sh, 0.0f);
+        vmax = fmaxf(vmax, fabsf(v));
         store_out(y, g, b, co, vz, vy, vx, CO, v);
       }
   }
+  if (g.y_bound) bound_update(g.y_bound, vmax);
 }
 
 template <int MODE, int CI, int CO, int RB, int QM = 0>
@@ -294,8 +298,9 @@ void launch_mode(const float* x, const float* x2, const float* w, float* y, cons
 int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const float* x2, const float* w,
                          float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on, const int* i0,
                          const int* in, const int* pad, const float* bn_scale, const float* bn_shift,
-                         const float* bn_mean, hipStream_t s, const uint32_t* absmax) {
+                         const float* bn_mean, hipStream_t s, const uint32_t* absmax, uint32_t* y_bound) {
   Geo g;
+  g.y_bound = y_bound;
   g.out_cf = out_cf ? 1 : 0;
   g.in_c4 = in_c4;
   g.absmax = absmax;

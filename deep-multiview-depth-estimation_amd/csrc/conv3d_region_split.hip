@@ -1,0 +1,281 @@
+// conv3d_region_split.hip -- the regulariser's stride-1 convolutions (conv_k_1, model.py:79-85,
+// forward at model.py:104-113) and stride-2 transposed convolutions (deconv_3_0 / deconv_2_0,
+// model.py:86-88, forward at model.py:117-120) on the f16 matrix cores with split operands, eval BN +
+// ReLU fused.  Same GEMM mapping, region geometry, tap order and epilogue as conv3d_region.hip (whose
+// fp32-MFMA kernel it replaces on the split-fp16 eval path); only the arithmetic differs:
+//
+//   * operands are split as in split.h: an activation v (fp32, channels-last region tensor, or the sum
+//     of two for `y3 + y2`) is scaled by 2^ex and carried as hi = fp16(v 2^ex), lo = fp16(v 2^ex - hi),
+//     the weights likewise with 2^ew (host, mvs_conv3d_region_split_weights);
+//   * one K-32 step is three v_mfma_f32_16x16x32_f16 into the same accumulator: x_hi w_hi, x_hi w_lo,
+//     x_lo w_hi (the dropped x_lo w_lo is below 2^-22 of the product), each product exact in fp32;
+//   * ex comes from the input's BOUND WORDS: kBoundWords partial maxima of |v| that the kernel which
+//     produced the tensor wrote in its epilogue (bound_update, split.h), so max|v| 2^ex < 2^14.
+//
+// gfx950 runs the f16 MFMA at 16x the fp32 one's rate: the three products cost 48 cycles per
+// (16 rows, 16 columns, 32 K) against 256 for the eight fp32 16x16x4 steps, on the same operand bytes
+// (an fp32 K-8 lane slice is 32 B; a split one is 2 x 16 B).
+//
+// K blocking.  CI >= 32: one K-32 block per (tap, 32 input channels), lane (m, g) supplies channels
+// 8g .. 8g + 7 of its row's tap voxel.  CI = 16 (conv_1_1, S1 only): one K-32 block per PAIR of taps
+// (2j, 2j + 1; tap 27 is empty), lanes g = 0, 1 the first tap's 16 channels, g = 2, 3 the second's.
+#include "launchers.h"
+#include "packed.h"
+#include "split.h"
+
+namespace mvs {
+namespace {
+
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+constexpr uint32_t kOob = 0xFFFFFFC0u;   // out-of-range buffer offset (loads return 0); +16 stays out
+constexpr int kS1 = 0, kT2 = 2;
+
+struct GeoS {
+  int n[3];    // volume dims
+  int o0[3];   // output region origin
+  int on[3];   // output region size
+  int i0[3];   // input region origin
+  int in[3];   // input region size
+  int pad[3];  // T2: P
+  int out_cf;  // 1: output channels-first
+};
+
+__device__ inline void class_dim_s(int o0, int on, int p, int par, int& first, int& cnt) {
+  first = o0 + (((o0 + p) & 1) != par ? 1 : 0);
+  cnt = first < o0 + on ? (o0 + on - 1 - first) / 2 + 1 : 0;
+}
+
+template <int MODE, int CI, int CO, int RB>
+__global__ __launch_bounds__(kBlock) void conv3d_region_split_kernel(
+    const float* __restrict__ x, const float* __restrict__ x2, const h8v* __restrict__ wf, int w_exp,
+    float* __restrict__ y, const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
+    const float* __restrict__ bn_mean, GeoS g, const uint32_t* __restrict__ xb, const uint32_t* __restrict__ xb2,
+    uint32_t* __restrict__ yb) {
+  constexpr int NB = CO / 16;
+  constexpr bool PAIR = CI == 16;
+  constexpr int CB = PAIR ? 1 : CI / 32;   // K-32 blocks per tap
+  static_assert(CO % 16 == 0 && (PAIR || CI % 32 == 0), "channel counts");
+  static_assert(!PAIR || MODE == kS1, "tap pairs: stride-1 convolutions only");
+  const int lane = (int)threadIdx.x & 63;
+  const int m = lane & 15, kq = lane >> 4;
+  const int b = (int)blockIdx.z;
+
+  int cf[3], cn[3], par[3] = {0, 0, 0};
+  if constexpr (MODE == kT2) {
+    const int cls = (int)blockIdx.y;
+    par[0] = (cls >> 2) & 1;
+    par[1] = (cls >> 1) & 1;
+    par[2] = cls & 1;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) class_dim_s(g.o0[d], g.on[d], g.pad[d], par[d], cf[d], cn[d]);
+  } else {
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      cf[d] = g.o0[d];
+      cn[d] = g.on[d];
+    }
+  }
+  const int rows = cn[0] * cn[1] * cn[2];
+  const int step = MODE == kT2 ? 2 : 1;
+  constexpr int kRows = 16 * RB;
+  const int bx = xcd_work_id((int)blockIdx.x, (int)gridDim.x);
+  const int row0 = (bx * (kBlock / 64) + ((int)threadIdx.x >> 6)) * kRows;
+  if (row0 >= rows) return;   // wave-uniform; no barriers in this kernel
+
+  // the input's scale: max|x| (+ max|x2|) 2^ex < 2^14
+  float bound = bound_read(xb);
+  if (x2) bound += bound_read(xb2);
+  const int ex = act_split_exponent(bound);
+
+  int lin[RB];
+  unsigned vm[RB][3];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int r = row0 + rb * 16 + m;
+    const bool ok = r < rows;
+    const int rr = ok ? r : 0;
+    const int jx = rr % cn[2], t = rr / cn[2];
+    const int jy = t % cn[1], jz = t / cn[1];
+    const int o[3] = {cf[0] + step * jz, cf[1] + step * jy, cf[2] + step * jx};
+    int bs[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      if constexpr (MODE == kS1) bs[d] = o[d] - 1 - g.i0[d];
+      else bs[d] = ((o[d] + g.pad[d] - par[d]) >> 1) - g.i0[d];
+      unsigned mk = 0;
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt) {
+        const int dl = MODE == kT2 ? -(tt >> 1) : tt;
+        const bool in = ok && bs[d] + dl >= 0 && bs[d] + dl < g.in[d] && !(MODE == kT2 && ((tt & 1) != par[d]));
+        mk |= in ? (1u << tt) : 0u;
+      }
+      vm[rb][d] = mk;
+    }
+    lin[rb] = (bs[0] * g.in[1] + bs[1]) * g.in[2] + bs[2];
+  }
+
+  f4v acc[RB][NB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+
+  const size_t rvol = (size_t)g.in[0] * g.in[1] * g.in[2];
+  const Rsrc rs = make_rsrc(x + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
+  const Rsrc rs2 = make_rsrc(x2 ? x2 + (size_t)b * rvol * CI : x, x2 ? (uint32_t)(rvol * CI * 4) : 0u);
+  const int sy = g.in[2], sz = g.in[1] * g.in[2];
+
+  // 8 channels c0 .. c0 + 7 of input voxel vx (kOob: zeros) as split fp16 parts
+  auto load_split = [&](uint32_t vx, int c0, h8v& hi, h8v& lo) {
+    const uint32_t eo = vx == kOob ? kOob : (vx * (uint32_t)CI + (uint32_t)c0) * 4u;
+    f4v a0 = ld4(rs, eo, 0), a1 = ld4(rs, eo + 16u, 0);
+    if (x2) {
+      a0 += ld4(rs2, eo, 0);
+      a1 += ld4(rs2, eo + 16u, 0);
+    }
+    uint2 h0, l0, h1, l1;
+    split4(a0, ex, h0, l0);
+    split4(a1, ex, h1, l1);
+    hi = __builtin_bit_cast(h8v, make_uint4(h0.x, h0.y, h1.x, h1.y));
+    lo = __builtin_bit_cast(h8v, make_uint4(l0.x, l0.y, l1.x, l1.y));
+  };
+  // one K-32 block: the row blocks' split A fragments, the column blocks' (hi, lo) weight fragments
+  // (wf[kb][nb][part][lane]), then x_hi w_hi, x_hi w_lo, x_lo w_hi per (row block, column block)
+  auto kblock = [&](int kb, const uint32_t (&vx)[RB], int c0) {
+    h8v ahi[RB], alo[RB], bhi[NB], blo[NB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) load_split(vx[rb], c0, ahi[rb], alo[rb]);
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      bhi[nb] = wf[((size_t)(kb * NB + nb) * 2 + 0) * 64 + lane];
+      blo[nb] = wf[((size_t)(kb * NB + nb) * 2 + 1) * 64 + lane];
+    }
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[rb], bhi[nb], acc[rb][nb], 0, 0, 0);
+        acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[rb], blo[nb], acc[rb][nb], 0, 0, 0);
+        acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[rb], bhi[nb], acc[rb][nb], 0, 0, 0);
+      }
+  };
+
+  if constexpr (PAIR) {
+    // tap pairs: this lane's tap 2j + (kq >> 1), channels 8 (kq & 1) .. + 7
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+      const int tap = 2 * j + (kq >> 1);
+      const int tz = tap / 9, ty = (tap / 3) % 3, tx = tap % 3;
+      uint32_t vx[RB];
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        const bool ok = tap < 27 && ((vm[rb][0] >> tz) & (vm[rb][1] >> ty) & (vm[rb][2] >> tx) & 1u) != 0;
+        vx[rb] = ok ? (uint32_t)(lin[rb] + tz * sz + ty * sy + tx) : kOob;
+      }
+      kblock(j, vx, 8 * (kq & 1));
+    }
+  } else {
+#pragma unroll
+    for (int tz = 0; tz < 3; ++tz) {
+      if (MODE == kT2 && ((tz & 1) != par[0])) continue;   // taps of o + P's parity only
+#pragma unroll
+      for (int ty = 0; ty < 3; ++ty) {
+        if (MODE == kT2 && ((ty & 1) != par[1])) continue;
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx) {
+          if (MODE == kT2 && ((tx & 1) != par[2])) continue;
+          const int dz = MODE == kT2 ? -(tz >> 1) : tz, dy = MODE == kT2 ? -(ty >> 1) : ty,
+                    dx = MODE == kT2 ? -(tx >> 1) : tx;
+          uint32_t vx[RB];
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb) {
+            const bool ok = ((vm[rb][0] >> tz) & (vm[rb][1] >> ty) & (vm[rb][2] >> tx) & 1u) != 0;
+            vx[rb] = ok ? (uint32_t)(lin[rb] + dz * sz + dy * sy + dx) : kOob;
+          }
+          const int tap = (tz * 3 + ty) * 3 + tx;
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb) kblock(tap * CB + cb, vx, cb * 32 + 8 * kq);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: unscale, eval BN + ReLU, store; the output's bound words.  acc[rb][nb][r] = (row
+  // (lane >> 4) * 4 + r, column lane & 15)
+  const int oexp = -(ex + w_exp);
+  const size_t orvol = (size_t)g.on[0] * g.on[1] * g.on[2];
+  float vmax = 0.0f;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const int co = nb * 16 + m;
+    const float sc = bn_scale ? bn_scale[co] : 1.0f, sh = bn_scale ? bn_shift[co] : 0.0f,
+                mu = bn_scale ? bn_mean[co] : 0.0f;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + rb * 16 + kq * 4 + r;
+        if (row >= rows) continue;
+        const int jx = row % cn[2], t = row / cn[2];
+        const int jy = t % cn[1], jz = t / cn[1];
+        const int vz = cf[0] + step * jz - g.o0[0], vy = cf[1] + step * jy - g.o0[1],
+                  vxx = cf[2] + step * jx - g.o0[2];
+        float v = ldexpf(acc[rb][nb][r], oexp);
+        if (bn_scale) v = fmaxf((v - mu) * sc + sh, 0.0f);
+        vmax = fmaxf(vmax, fabsf(v));
+        const size_t vox = ((size_t)vz * g.on[1] + vy) * g.on[2] + vxx;
+        if (g.out_cf) y[((size_t)b * CO + co) * orvol + vox] = v;
+        else y[((size_t)b * orvol + vox) * CO + co] = v;
+      }
+  }
+  if (yb) bound_update(yb, vmax);
+}
+
+template <int MODE, int CI, int CO, int RB>
+void launch_split_mode(const float* x, const float* x2, const void* wf, int w_exp, float* y, const float* sc,
+                       const float* sh, const float* mu, int B, const GeoS& g, const uint32_t* xb,
+                       const uint32_t* xb2, uint32_t* yb, hipStream_t s) {
+  const int classes = MODE == kT2 ? 8 : 1;
+  const int rz = MODE == kT2 ? (g.on[0] + 1) / 2 : g.on[0], ry = MODE == kT2 ? (g.on[1] + 1) / 2 : g.on[1],
+            rx = MODE == kT2 ? (g.on[2] + 1) / 2 : g.on[2];
+  const int rows = rz * ry * rx;
+  const int per_block = (kBlock / 64) * 16 * RB;
+  const int blocks = (rows + per_block - 1) / per_block;
+  const dim3 grid((unsigned)((blocks + 7) / 8 * 8), (unsigned)classes, (unsigned)B);
+  hipLaunchKernelGGL((conv3d_region_split_kernel<MODE, CI, CO, RB>), grid, dim3(kBlock), 0, s, x, x2,
+                     reinterpret_cast<const h8v*>(wf), w_exp, y, sc, sh, mu, g, xb, xb2, yb);
+}
+
+}  // namespace
+
+int conv3d_region_split_kblocks(int c_in) { return c_in == 16 ? 14 : 27 * (c_in / 32); }
+
+int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const float* x2, const void* wfrag, int w_exp,
+                               float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on,
+                               const int* i0, const int* in, const int* pad, const float* bn_scale,
+                               const float* bn_shift, const float* bn_mean, const uint32_t* x_bound,
+                               const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s) {
+  GeoS g;
+  g.out_cf = out_cf ? 1 : 0;
+  for (int d = 0; d < 3; ++d) {
+    g.n[d] = n[d];
+    g.o0[d] = o0[d];
+    g.on[d] = on[d];
+    g.i0[d] = i0[d];
+    g.in[d] = in[d];
+    g.pad[d] = pad ? pad[d] : 1;
+  }
+#define MVS_RSPLIT_CASE(MD, A, C)                                                                         \
+  if (mode == MD && CI == A && CO == C) {                                                                 \
+    launch_split_mode<MD, A, C, 2>(x, x2, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound,  \
+                                   x2_bound, y_bound, s);                                                 \
+    return MVS_OK;                                                                                        \
+  }
+  // S1: conv_k_1 (16 / 32 / 64 channels); T2: deconv_3_0 (64 -> 32), deconv_2_0 (32 -> 16)
+  MVS_RSPLIT_CASE(kS1, 16, 16) MVS_RSPLIT_CASE(kS1, 32, 32) MVS_RSPLIT_CASE(kS1, 64, 64)
+  MVS_RSPLIT_CASE(kT2, 64, 32) MVS_RSPLIT_CASE(kT2, 32, 16)
+#undef MVS_RSPLIT_CASE
+  return MVS_ERR_INVALID_ARGUMENT;
+}
+
+}  // namespace mvs

@@ -105,6 +105,7 @@ struct HeadArgs {
   const float *bn1_sc, *bn1_sh, *bn1_mu;   // BN_1 (16), all or none
   float* y0;                  // [B][8][D][H][W]
   float* y1;                  // [B][on0][on1][on2][16]
+  uint32_t* y1_bound;         // optional: y1's bound words (split.h), for the split-fp16 conv_1_1
   void* scv;                  // split cost volume on the box only: [B][8][r1 - r0 ...] x 16 B, or null
   const void* scv_in;         // PRE: the materialised split cost volume [B][8][D][H][W] x 16 B (split.h)
   int V, D, H, W;
@@ -306,6 +307,9 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   uint32_t pok[kPD];     // bit u: item u of the buffered batch is valid
   const int pnu = __builtin_amdgcn_readfirstlane(ptid + 256 * (kItems - 1) < kBatchItems ? kItems : kItems - 1);
   auto pre_load = [&](int j, int pb) {
+#ifdef MVS_HEAD_NO_LOAD   // (timing ablation: the ring is never filled)
+    return;
+#endif
     const int pbase = z0 - 1 + 2 * j;
     pok[pb] = 0;
 #pragma unroll
@@ -323,6 +327,9 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     }
   };
   auto pre_store = [&](int j, int pb) {
+#ifdef MVS_HEAD_NO_LOAD
+    return;
+#endif
     const int sl0 = slot_of(z0 - 1 + 2 * j);
 #pragma unroll
     for (int u = 0; u < kItems; ++u) {
@@ -540,7 +547,8 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     const f4 ab = *reinterpret_cast<const f4*>(scr + ((sb * 3 + 1) * 64 + lane) * 16);
     const f4 ac = *reinterpret_cast<const f4*>(scr + ((sb * 3 + 2) * 64 + lane) * 16);
     const int oz = (s + a.pad[0]) >> 1;
-    if (oz < a.o0[0] || oz >= a.o0[0] + a.on[0]) return;
+    if (oz < a.o0[0] || oz >= a.o0[0] + a.on[0]) return;   // wave-uniform
+    float vmax = 0.0f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = 4 * g4 + r, wx_ = row & 7, wy_ = row >> 3;
@@ -548,9 +556,11 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       if (oy < a.o0[1] || oy >= a.o0[1] + a.on[1] || ox < a.o0[2] || ox >= a.o0[2] + a.on[2]) continue;
       float v = ldexpf(aa[r] + (ab[r] + ac[r]), oexp1);
       if (a.bn1_sc) v = fmaxf((v - mu1) * sc1 + sh1, 0.0f);
+      vmax = fmaxf(vmax, fabsf(v));
       const size_t vx = (((size_t)(oz - a.o0[0]) * a.on[1] + (oy - a.o0[1])) * a.on[2] + (ox - a.o0[2]));
       a.y1[(((size_t)b * a.on[0] * a.on[1] * a.on[2]) + vx) * 16 + i16] = v;
     }
+    if (a.y1_bound) bound_update(a.y1_bound, vmax);
   };
 
   // conv_1_0 in step k: window zs - 1 completes (depth tap 2 on plane zs + 1), window zs + 1 starts
@@ -906,7 +916,7 @@ int launch_cv_head(const Geometry& g, const float* feat, const Cams& cm, float* 
   float* packed = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) +
                                            align256((size_t)g.B * g.V * g.Dc * 9 * sizeof(float)));
   launch_cv_prologue_pm(g, feat, cm, smp, packed, absmax, s);
-  HeadArgs a;
+  HeadArgs a = {};
   a.packed = reinterpret_cast<const float4*>(packed);
   a.refs = a.packed + (size_t)g.B * g.V * kC4 * pad_geom(g.h, g.w).plane;
   a.sampling = smp;
@@ -958,9 +968,10 @@ int launch_cv_head(const Geometry& g, const float* feat, const Cams& cm, float* 
 
 int launch_split_head(const Geometry& g, const void* scv_in, const uint32_t* absmax, const void* w0frag, int w_exp0,
                       const void* w1frag, int w_exp1, const float* const* bn0, const float* const* bn1, float* y0,
-                      float* y1, const int* pad, const int* o0, const int* on, hipStream_t s, hipEvent_t ev0,
-                      hipEvent_t ev1) {
+                      float* y1, const int* pad, const int* o0, const int* on, uint32_t* y1_bound, hipStream_t s,
+                      hipEvent_t ev0, hipEvent_t ev1) {
   HeadArgs a = {};
+  a.y1_bound = y1_bound;
   a.absmax = absmax;
   a.w0 = reinterpret_cast<const h8v*>(w0frag);
   a.w1 = reinterpret_cast<const h8v*>(w1frag);

@@ -54,8 +54,8 @@ int launch_cv_head(const Geometry& g, const float* feat, const Cams& cm, float* 
 // the same kernel on a materialised split cost volume (conv_0_0 + conv_1_0 in one pass over it)
 int launch_split_head(const Geometry& g, const void* scv_in, const uint32_t* absmax, const void* w0frag, int w_exp0,
                       const void* w1frag, int w_exp1, const float* const* bn0, const float* const* bn1, float* y0,
-                      float* y1, const int* pad, const int* o0, const int* on, hipStream_t s, hipEvent_t ev0 = nullptr,
-                      hipEvent_t ev1 = nullptr);
+                      float* y1, const int* pad, const int* o0, const int* on, uint32_t* y1_bound, hipStream_t s,
+                      hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 
 // warp_variance.hip
 void launch_warp(const Geometry& g, const float* feat, const float* sampling, float* warped,
@@ -128,7 +128,14 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
                          float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on, const int* i0,
                          const int* in,
                          const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                         hipStream_t s, const uint32_t* absmax = nullptr);
+                         hipStream_t s, const uint32_t* absmax = nullptr, uint32_t* y_bound = nullptr);
+// the S1 / T2 region convolutions on split-fp16 MFMA (conv3d_region_split.hip); K-32 weight blocks
+int conv3d_region_split_kblocks(int c_in);
+int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const float* x2, const void* wfrag, int w_exp,
+                               float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on,
+                               const int* i0, const int* in, const int* pad, const float* bn_scale,
+                               const float* bn_shift, const float* bn_mean, const uint32_t* x_bound,
+                               const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s);
 
 // channel_ops.hip: train-mode BatchNorm pieces -- per-channel float64 sums into
 // stats[slot][2][C] (64 slots) and y = relu(BN(x)) [+ relu(BN'(r))], channels-last or NCDHW

@@ -49,4 +49,35 @@ __device__ inline f4v unsplit4(const uint4 p, int e) {
              ldexpf(h(p.y, 0) + h(p.w, 0), -e), ldexpf(h(p.y, 1) + h(p.w, 1), -e)};
 }
 
+// Activation bounds of a region tensor ("bound words"): kBoundWords words holding maxima of |v| as fp32
+// bits (non-negative floats order like their bit patterns), raised by the producing kernel's epilogue
+// with one atomic max per wave (word = workgroup index mod kBoundWords, spreading the atomics) into
+// words the caller zeroed; the split-fp16 consumers scale the tensor by 2^act_split_exponent(bound).
+constexpr int kBoundWords = 64;
+
+// the tensor's bound: the max over its words (whole wave; 0 without words)
+__device__ inline float bound_read(const uint32_t* __restrict__ words) {
+  if (!words) return 0.0f;
+  uint32_t v = words[threadIdx.x & 63];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  return __uint_as_float(v);
+}
+
+// e with bound 2^e < 2^14 (fp16 max 65504); 0 for a zero or non-finite bound
+__device__ inline int act_split_exponent(float bound) {
+  if (!(bound > 0.0f) || !(bound <= 3.0e38f)) return 0;
+  int e;
+  (void)frexpf(bound, &e);   // bound < 2^e
+  return min(max(14 - e, -120), 120);
+}
+
+// raise the bound words by this wave's max |v| (m >= 0 per lane; whole wave)
+__device__ inline void bound_update(uint32_t* __restrict__ words, float m) {
+  uint32_t v = __float_as_uint(m);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(words + (blockIdx.x % kBoundWords), v);
+}
+
 }  // namespace mvs

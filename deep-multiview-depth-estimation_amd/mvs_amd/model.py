@@ -307,8 +307,9 @@ class CostVolumeReg(nn.Module):
         ``bound``: its bound words (the split-fp16 kernels' scale).  ``head``: (y0, y1) from the fused
         head kernel (forward_live_head) -- conv_0_0's and conv_1_0's outputs; cv is then the split
         volume on conv_2_0's input box only, ``cv_box`` (origin, size) that box."""
-        from .ops import (CONV_S1, CONV_S2, CONV_T2, conv3d_k3, conv3d_k3_split, conv3d_region, conv_s2_split,
-                          deconv3d_k3s2, region_weight, softmax_depth, split_head)
+        from .ops import (CONV_S1, CONV_S2, CONV_T2, bound_words, conv3d_k3, conv3d_k3_split, conv3d_region,
+                          conv3d_region_split, conv_s2_split, deconv3d_k3s2, region_weight, softmax_depth,
+                          split_head)
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad = list(n), list(self.pad)
@@ -330,12 +331,19 @@ class CostVolumeReg(nn.Module):
         # for the same CUs (cfg 2: 5.67 ms serialised against 5.78 ms on a side stream,
         # profiles/r03/r03u_reg_layers.log); the exact-fp32 VALU kernel overlaps the MFMA chain
         side = main if bound is not None else _side_stream(cv.device)
+        # the split-fp16 eval path also runs the stride-1 and transposed region convolutions on the f16
+        # matrix cores (ops.conv3d_region_split, csrc/conv3d_region_split.hip; MVS_REGION_SPLIT=0: the
+        # fp32-MFMA kernels): every region tensor they read carries bound words, raised by the kernel
+        # that writes it -- rows 0-2 conv_k_0's outputs, 3-5 conv_k_1's, 6 deconv_3_0's (one memset)
+        bw = bound_words(7, cv.device) if split_cv and os.environ.get("MVS_REGION_SPLIT", "1") != "0" else None
+        y1_bounded = False
         if head is None and split_cv and self._split_head_ok(cv, n):
             # conv_0_0 + BN_0 + ReLU and conv_1_0 + BN_1 + ReLU in one pass over the split volume
             # (ops.split_head, csrc/cv_head.hip PRESPLIT mode): bit-equal to the two kernels below
             h1 = _grow(B, n, 1)
             head = split_head(cv, bound, self.conv_0_0.weight, *bn_eval(self.BN_0), self.conv_1_0.weight,
-                              *bn_eval(self.BN_1), pad, org(h1), size(h1))
+                              *bn_eval(self.BN_1), pad, org(h1), size(h1), None if bw is None else bw[0])
+            y1_bounded = bw is not None
         if head is not None:
             y0, y1_head = head
         else:
@@ -348,26 +356,40 @@ class CostVolumeReg(nn.Module):
                     y0 = conv3d_k3(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), in_c4=c4, wino_z=True)
             cv.record_stream(side)
 
-        def level(conv_a, conv_b, bn, reg):
+        def level(k, conv_a, conv_b, bn, reg):
             halo = _grow(reg, n, 1)
+            ab = None if bw is None else bw[k]   # ya's bound words
             if head is not None and reg is B:
-                ya = y1_head   # conv_1_0 + BN_1 + ReLU on halo(B), from the fused head kernel
+                ya = y1_head   # conv_1_0 + BN_1 + ReLU on halo(B), from the head kernel
+                ab = ab if y1_bounded else None
             elif bound is not None and conv_a.weight.shape[0] == 16:
                 # conv_1_0 reads the whole volume: LDS-staged split-fp16 kernel (csrc/conv3d_s2_split.hip)
                 ya = conv_s2_split(cv, bound, conv_a.weight, dims, org(halo), size(halo), pad, *bn_eval(bn))
+                ab = None
             else:
                 ya = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(halo), size(halo), cv_box[0],
-                                   cv_box[1], pad, *bn_eval(bn), in_c4=c4, absmax=bound if split_cv else None)
+                                   cv_box[1], pad, *bn_eval(bn), in_c4=c4, absmax=bound if split_cv else None,
+                                   y_bound=ab)
             # level 1's output only feeds deconv_1_0's input sum: channels-first for its loads
+            if ab is not None:
+                return conv3d_region_split(ya, None, region_weight(conv_b), CONV_S1, dims, org(reg), size(reg),
+                                           org(halo), size(halo), None, ab, None, bw[3 + k], *bn_eval(bn),
+                                           out_ncdhw=reg is B)
             return conv3d_region(ya, None, region_weight(conv_b), CONV_S1, dims, org(reg), size(reg),
                                  org(halo), size(halo), None, *bn_eval(bn), out_ncdhw=reg is B)
-        y1 = level(self.conv_1_0, self.conv_1_1, self.BN_1, B)
-        y2 = level(self.conv_2_0, self.conv_2_1, self.BN_2, C2)
-        y3 = level(self.conv_3_0, self.conv_3_1, self.BN_3, C3)
-        y3 = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, org(C2), size(C2),
-                           org(C3), size(C3), pad, *bn_eval(self.BN_2))
-        y2 = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, org(B), size(B), org(C2),
-                           size(C2), pad, *bn_eval(self.BN_1), out_ncdhw=True)
+        y1 = level(0, self.conv_1_0, self.conv_1_1, self.BN_1, B)
+        y2 = level(1, self.conv_2_0, self.conv_2_1, self.BN_2, C2)
+        y3 = level(2, self.conv_3_0, self.conv_3_1, self.BN_3, C3)
+        if bw is not None:
+            y3 = conv3d_region_split(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, org(C2), size(C2),
+                                     org(C3), size(C3), pad, bw[5], None, bw[6], *bn_eval(self.BN_2))
+            y2 = conv3d_region_split(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, org(B), size(B),
+                                     org(C2), size(C2), pad, bw[6], bw[4], None, *bn_eval(self.BN_1), out_ncdhw=True)
+        else:
+            y3 = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, org(C2), size(C2),
+                               org(C3), size(C3), pad, *bn_eval(self.BN_2))
+            y2 = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, org(B), size(B), org(C2),
+                               size(C2), pad, *bn_eval(self.BN_1), out_ncdhw=True)
         if side != main:   # (a stream waiting on itself is an event + barrier packet: a 6 us bubble)
             main.wait_stream(side)
             y0.record_stream(main)

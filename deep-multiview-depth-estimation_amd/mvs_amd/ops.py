@@ -380,15 +380,19 @@ def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scal
             feat.new_empty((8,), dtype=torch.int32))
 
 
+# (the bound words are raised in place; not declared as a mutation: torch's ADInplaceOrView wrapper
+# indexes every declared mutable argument positionally, which fails for an omitted trailing default)
 @torch.library.custom_op("mvs::split_head", mutates_args=())
 def split_head(scv: torch.Tensor, absmax: torch.Tensor, w0: torch.Tensor, bn0_scale: Optional[torch.Tensor],
                bn0_shift: Optional[torch.Tensor], bn0_mean: Optional[torch.Tensor], w1: torch.Tensor,
                bn1_scale: Optional[torch.Tensor], bn1_shift: Optional[torch.Tensor], bn1_mean: Optional[torch.Tensor],
-               pad: list[int], y1_origin: list[int], y1_size: list[int]) -> tuple[torch.Tensor, torch.Tensor]:
+               pad: list[int], y1_origin: list[int], y1_size: list[int],
+               y1_bound: Optional[torch.Tensor] = None) -> tuple[torch.Tensor, torch.Tensor]:
     """conv_0_0 + BN_0 + ReLU (model.py:101) and conv_1_0 + BN_1 + ReLU (model.py:103) of the split cost
     volume ``scv`` [B, 8, D, h, w, 4] int32 (cost_volume_c4_split) in ONE pass over it
     (mvs_split_head_fwd).  Returns (y0 [B, 8, D, h, w], y1 channels-last [B, *y1_size, 16]): bit-identical
-    to conv3d_k3_split and conv_s2_split.  D even, pad odd; inference only."""
+    to conv3d_k3_split and conv_s2_split.  D even, pad odd; inference only.  ``y1_bound``: int32
+    [MVS_BOUND_WORDS] zeroed words raised to max|y1| (the scale of conv3d_region_split's input)."""
     _require_gpu(scv, "scv")
     lib = _lib.load()
     if scv.dim() != 6 or scv.dtype != torch.int32 or scv.shape[1] != 8 or scv.shape[5] != 4:
@@ -415,13 +419,15 @@ def split_head(scv: torch.Tensor, absmax: torch.Tensor, w0: torch.Tensor, bn0_sc
         evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK("split_head"))
     st = lib.mvs_split_head_fwd(_lib.ptr(scv), _lib.ptr(absmax.contiguous()), b, d, h, w, _lib.ptr(f0), int(e0),
                                 *bp0, _lib.ptr(f1), int(e1), *bp1, _ints3(pad), _ints3(y1_origin),
-                                _ints3(y1_size), _lib.ptr(y0), _lib.ptr(y1), _lib.stream_handle(dev), *evs)
+                                _ints3(y1_size), _lib.ptr(y0), _lib.ptr(y1), _bound_ptr(y1_bound),
+                                _lib.stream_handle(dev), *evs)
     _lib.check(st, "mvs_split_head_fwd")
     return y0, y1
 
 
 @split_head.register_fake
-def _(scv, absmax, w0, bn0_scale, bn0_shift, bn0_mean, w1, bn1_scale, bn1_shift, bn1_mean, pad, y1_origin, y1_size):
+def _(scv, absmax, w0, bn0_scale, bn0_shift, bn0_mean, w1, bn1_scale, bn1_shift, bn1_mean, pad, y1_origin, y1_size,
+      y1_bound=None):
     b, _, d, h, w, _ = scv.shape
     return (scv.new_empty((b, 8, d, h, w), dtype=_F32), scv.new_empty([b] + list(y1_size) + [16], dtype=_F32))
 
@@ -983,19 +989,23 @@ def _ints3(v):
     return (ctypes.c_int * 3)(*[int(a) for a in v])
 
 
+# (the bound words are raised in place; not declared as a mutation: torch's ADInplaceOrView wrapper
+# indexes every declared mutable argument positionally, which fails for an omitted trailing default)
 @torch.library.custom_op("mvs::conv3d_region", mutates_args=())
 def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Tensor, mode: int,
                   dims: list[int], out_origin: list[int], out_size: list[int],
                   in_origin: Optional[list[int]], in_size: Optional[list[int]], pad: Optional[list[int]],
                   bn_scale: Optional[torch.Tensor] = None, bn_shift: Optional[torch.Tensor] = None,
                   bn_mean: Optional[torch.Tensor] = None, out_ncdhw: bool = False,
-                  in_c4: bool = False, absmax: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  in_c4: bool = False, absmax: Optional[torch.Tensor] = None,
+                  y_bound: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Region convolution (mvs_conv3d_region_fwd): mode CONV_S2 reads the full NCDHW volume x
     (in_c4: the channel-quad [B, C/4, D, H, W, 4] of cost_volume_c4, or bf16 of cost_volume_c4_bf16;
     with in_origin / in_size, x holds only that box of the volume: the fused head's stored box),
     CONV_S1 / CONV_T2 a channels-last region tensor x (+ x2) on in_origin + [0, in_size); returns the
     channels-last region tensor [B, *out_size, c_out] ([B, c_out, *out_size] with out_ncdhw), eval
-    BN + ReLU fused when bn_* are given.  ``weight`` is region_weight(module).  Inference only."""
+    BN + ReLU fused when bn_* are given.  ``weight`` is region_weight(module).  ``y_bound``: zeroed
+    bound words (int32 [MVS_BOUND_WORDS]) raised to max|y|.  Inference only."""
     _require_gpu(x, "x")
     lib = _lib.load()
     quad_bf16 = in_c4 and x.dtype == torch.bfloat16
@@ -1022,14 +1032,89 @@ def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Ten
                                    None if pad is None else _ints3(pad),
                                    *[None if t is None else _lib.ptr(t) for t in bn],
                                    _lib.ptr(absmax.contiguous()) if quad_split else None,
-                                   _lib.stream_handle(x.device))
+                                   _bound_ptr(y_bound), _lib.stream_handle(x.device))
     _lib.check(st, "mvs_conv3d_region_fwd")
     return y
 
 
 @conv3d_region.register_fake
 def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, bn_scale=None, bn_shift=None,
-      bn_mean=None, out_ncdhw=False, in_c4=False, absmax=None):
+      bn_mean=None, out_ncdhw=False, in_c4=False, absmax=None, y_bound=None):
+    if out_ncdhw:
+        return x.new_empty((x.shape[0], weight.shape[1]) + tuple(out_size), dtype=_F32)
+    return x.new_empty((x.shape[0],) + tuple(out_size) + (weight.shape[1],), dtype=_F32)
+
+
+BOUND_WORDS = 64   # MVS_BOUND_WORDS
+
+
+def bound_words(n, device):
+    """n zeroed bound-word sets (int32 [n, MVS_BOUND_WORDS]) -- one memset for a forward's tensors."""
+    return torch.zeros((n, BOUND_WORDS), device=device, dtype=torch.int32)
+
+
+def _bound_ptr(t):
+    if t is None:
+        return None
+    if t.dtype != torch.int32 or t.numel() != BOUND_WORDS or not t.is_contiguous():
+        raise ValueError("bound words: a contiguous int32 tensor of %d words" % BOUND_WORDS)
+    return _lib.ptr(t)
+
+
+def region_split_fragments(weight, device):
+    """(split-fp16 MFMA fragments on ``device``, exponent) of a region convolution's weight
+    [27][c_out][c_in] (region_weight's layout), formed on the host by mvs_conv3d_region_split_weights."""
+    lib = _lib.load()
+    w = weight.detach().to(device="cpu", dtype=_F32).contiguous()
+    _, cout, cin = w.shape
+    kb = 14 if cin == 16 else 27 * (cin // 32)
+    frag = torch.empty((kb * (cout // 16) * 2 * 64 * 8,), dtype=torch.int16)
+    e = ctypes.c_int(0)
+    st = lib.mvs_conv3d_region_split_weights(_lib.ptr(w), cin, cout, _lib.ptr(frag), ctypes.byref(e))
+    _lib.check(st, "mvs_conv3d_region_split_weights")
+    return frag.to(device), e.value
+
+
+# (the bound words are raised in place; not declared as a mutation: torch's ADInplaceOrView wrapper
+# indexes every declared mutable argument positionally, which fails for an omitted trailing default)
+@torch.library.custom_op("mvs::conv3d_region_split", mutates_args=())
+def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Tensor, mode: int,
+                        dims: list[int], out_origin: list[int], out_size: list[int], in_origin: list[int],
+                        in_size: list[int], pad: Optional[list[int]], x_bound: Optional[torch.Tensor],
+                        x2_bound: Optional[torch.Tensor], y_bound: Optional[torch.Tensor],
+                        bn_scale: Optional[torch.Tensor] = None, bn_shift: Optional[torch.Tensor] = None,
+                        bn_mean: Optional[torch.Tensor] = None, out_ncdhw: bool = False) -> torch.Tensor:
+    """conv3d_region's CONV_S1 / CONV_T2 convolutions on the f16 matrix cores with split operands
+    (mvs_conv3d_region_split_fwd, csrc/conv3d_region_split.hip): same geometry, layouts and epilogue;
+    the input scaled by its bound words ``x_bound`` (+ ``x2_bound`` for the sum x + x2), ``y_bound``
+    (zeroed words or None) raised to max|y|.  fp32-level error.  Inference only."""
+    _require_gpu(x, "x")
+    lib = _lib.load()
+    x = x.to(_F32).contiguous()
+    if x2 is not None:
+        x2 = x2.to(_F32).contiguous()
+    dev = x.device
+    frag, ew = derived("region_split", (weight,), lambda wt: region_split_fragments(wt, dev), dev)
+    _, cout, cin = weight.shape
+    b = x.shape[0]
+    bn = [t if t is None else t.to(device=dev, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
+    if any(t is None for t in bn) and not all(t is None for t in bn):
+        raise ValueError("bn_scale, bn_shift and bn_mean go together")
+    shape = (b, cout) + tuple(out_size) if out_ncdhw else (b,) + tuple(out_size) + (cout,)
+    y = torch.empty(shape, device=dev, dtype=_F32)
+    st = lib.mvs_conv3d_region_split_fwd(int(mode), _lib.MVS_CONV_OUT_NCDHW if out_ncdhw else 0, _lib.ptr(x),
+                                         None if x2 is None else _lib.ptr(x2), _lib.ptr(frag), int(ew), _lib.ptr(y),
+                                         b, cin, cout, _ints3(dims), _ints3(out_origin), _ints3(out_size),
+                                         _ints3(in_origin), _ints3(in_size), None if pad is None else _ints3(pad),
+                                         *[None if t is None else _lib.ptr(t) for t in bn], _bound_ptr(x_bound),
+                                         _bound_ptr(x2_bound), _bound_ptr(y_bound), _lib.stream_handle(dev))
+    _lib.check(st, "mvs_conv3d_region_split_fwd")
+    return y
+
+
+@conv3d_region_split.register_fake
+def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, x_bound, x2_bound, y_bound,
+      bn_scale=None, bn_shift=None, bn_mean=None, out_ncdhw=False):
     if out_ncdhw:
         return x.new_empty((x.shape[0], weight.shape[1]) + tuple(out_size), dtype=_F32)
     return x.new_empty((x.shape[0],) + tuple(out_size) + (weight.shape[1],), dtype=_F32)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 13
+#define MVS_ABI_VERSION 14
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -298,14 +298,16 @@ int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, 
  * Bit-identical to mvs_conv3d_k3_split_fwd + mvs_conv3d_s2_split_fwd on the same volume.
  *   scv: [batch][8][d_count][h][w] x 16 B (DEVICE, 16-byte aligned), x_absmax its bound words;
  *   w0_frag / w0_exp, bn0_*, w1_frag / w1_exp, bn1_*, pad, y1_origin, y1_size, y0, y1: as
- *   mvs_cost_volume_head_fwd (d_count even, every pad odd).
+ *   mvs_cost_volume_head_fwd (d_count even, every pad odd);
+ *   y1_bound: NULL, or MVS_BOUND_WORDS words (DEVICE, zeroed by the caller) raised to max|y1| (the
+ *   bound words mvs_conv3d_region_split_fwd scales its input by).
  * 128 * d_count * h * w <= 2^32 - 16.  Events (either may be NULL) are recorded around the kernel. */
 int mvs_split_head_fwd(const void* scv, const unsigned* x_absmax, int batch, int d_count, int h, int w,
                        const void* w0_frag, int w0_exp, const float* bn0_scale, const float* bn0_shift,
                        const float* bn0_mean, const void* w1_frag, int w1_exp, const float* bn1_scale,
                        const float* bn1_shift, const float* bn1_mean, const int* pad, const int* y1_origin,
-                       const int* y1_size, float* y0, float* y1, void* stream, void* main_begin_event,
-                       void* main_end_event);
+                       const int* y1_size, float* y0, float* y1, unsigned* y1_bound, void* stream,
+                       void* main_begin_event, void* main_end_event);
 
 int mvs_conv3d_k3_split_fwd(const void* x, int flags, const void* weight_frag, int weight_exp,
                             const unsigned* x_absmax, float* y, int batch, int d, int h, int w,
@@ -440,13 +442,45 @@ int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch,
  * (32, 32), (64, 64), T2 (64, 32), (32, 16); else MVS_ERR_INVALID_ARGUMENT.  dims, origins, sizes and
  * pad are HOST pointers to 3 ints.  flags = MVS_CONV_S2 input MVS_CONV_IN_C4 | MVS_CONV_IN_SPLIT: the split
  * cost volume, re-formed to fp32 on load as (hi + lo) 2^-e (2^-22 of each element), x_absmax its bound
- * words (DEVICE; NULL otherwise).  Eval-mode inference only; products summed in the order (tap,
- * c_in) -- MIOpen sums them in other orders (fp32 rounding-level differences). */
+ * words (DEVICE; NULL otherwise).  y_bound: NULL, or MVS_BOUND_WORDS words (DEVICE, zeroed by the
+ * caller) raised to max|y| (see mvs_conv3d_region_split_fwd).  Eval-mode inference only; products
+ * summed in the order (tap, c_in) -- MIOpen sums them in other orders (fp32 rounding-level differences). */
 int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, const float* weight, float* y,
                           int batch, int c_in, int c_out, const int* dims, const int* out_origin,
                           const int* out_size, const int* in_origin, const int* in_size,
                           const int* pad, const float* bn_scale, const float* bn_shift,
-                          const float* bn_mean, const unsigned* x_absmax, void* stream);
+                          const float* bn_mean, const unsigned* x_absmax, unsigned* y_bound, void* stream);
+
+/* Bound words of a region tensor: MVS_BOUND_WORDS uint32 holding maxima of |v| as fp32 bit patterns
+ * (the tensor's bound is their maximum), raised with atomic maxima by the kernel that writes the tensor
+ * into words the caller zeroed. */
+#define MVS_BOUND_WORDS 64
+
+/* HOST function: the split-fp16 MFMA fragments of a region convolution's weight for
+ * mvs_conv3d_region_split_fwd.  weight [27][c_out][c_in] fp32 HOST (mvs_conv3d_region_fwd's layout),
+ * finite; c_out a multiple of 16, c_in 16 or a multiple of 32; frag HOST, kb * (c_out / 16) * 2 * 64 * 8
+ * uint16 with kb = 14 (c_in 16: K blocks of two taps x 16 channels) or 27 * c_in / 32;
+ * *weight_exp = ew with max|w| 2^ew < 2^14.  frag[kb][nb][part][lane][j]: lane (c = lane & 15,
+ * g = lane >> 4) holds K element 8g + j of output channel 16 nb + c, part 0 = fp16(w 2^ew), part 1 =
+ * fp16(w 2^ew - part 0) (nearest). */
+int mvs_conv3d_region_split_weights(const float* weight, int c_in, int c_out, unsigned short* frag, int* weight_exp);
+
+/* mvs_conv3d_region_fwd's MVS_CONV_S1 and MVS_CONV_T2 convolutions (conv_k_1, model.py:104-113;
+ * deconv_3_0 / deconv_2_0, model.py:117-120) on the f16 matrix cores with split operands
+ * (csrc/conv3d_region_split.hip): the input v (x, or x + x2) is scaled by 2^ex -- max(bound(x) +
+ * bound(x2)) 2^ex < 2^14 from its bound words -- and split into fp16 hi + lo, the weights likewise
+ * (mvs_conv3d_region_split_weights: weight_frag DEVICE, 16-byte aligned, weight_exp); per K-32 block
+ * x_hi w_hi + x_hi w_lo + x_lo w_hi in fp32 accumulation, output unscaled by 2^-(ex + ew): fp32-level
+ * error.  Geometry, layouts, BN epilogue and flags (MVS_CONV_OUT_NCDHW) as
+ * mvs_conv3d_region_fwd; in_origin / in_size required.  x_bound / x2_bound: the inputs' bound words
+ * (DEVICE; NULL = unscaled, only when every |v| < 2^14 is known); y_bound: NULL or the output's bound
+ * words (zeroed by the caller).  Supported (mode, c_in, c_out): S1 (16, 16), (32, 32), (64, 64), T2
+ * (64, 32), (32, 16).  Eval-mode inference only. */
+int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float* x2, const void* weight_frag,
+                                int weight_exp, float* y, int batch, int c_in, int c_out, const int* dims,
+                                const int* out_origin, const int* out_size, const int* in_origin, const int* in_size,
+                                const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                                const unsigned* x_bound, const unsigned* x2_bound, unsigned* y_bound, void* stream);
 
 /* Softmax over the depth planes of the regulariser's output (CostVolumeReg.Norm = nn.Softmax(2),
  * model.py:97 / :125): y[b][0][d][p] = exp(x - max_d x) / sum_d exp(x - max_d x) per pixel p, in

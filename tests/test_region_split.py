@@ -1,0 +1,156 @@
+"""The regulariser's stride-1 and transposed region convolutions on split-fp16 MFMA
+(csrc/conv3d_region_split.hip, ops.conv3d_region_split; model.py:104-120's conv_k_1 / deconv_3_0 /
+deconv_2_0 on the eval path) and the bound words that scale their inputs.
+
+Parity: against torch's convolution of the zero-extended tensors in float64 (CPU) -- the same check
+test_gpu_parity.py::test_region_conv_matches_torch applies to the fp32-MFMA kernel -- with the error
+bounded by the fp32 kernel's own (the split operands carry 22 significant bits; the fp32 accumulation
+order is the fp32 kernel's).  Bound words: the kernel raises them to exactly max|y|.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+DEV = torch.device("cuda", 0)
+
+
+def _bn_params(c, g):
+    return (torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1, torch.randn(c, generator=g) * 0.1)
+
+
+def _bn_relu(y, sc, sh, mu):
+    v = lambda t: t.view(1, -1, 1, 1, 1)
+    return torch.relu((y - v(mu)) * v(sc) + v(sh))
+
+
+def test_split_weight_fragments_host():
+    """CPU: mvs_conv3d_region_split_weights lays out hi / lo parts as documented (K-32 blocks; tap pairs
+    for c_in = 16), the parts sum to w 2^ew to 2^-22, and tap 27 of the last pair is zero."""
+    from mvs_amd.ops import region_split_fragments
+    g = torch.Generator().manual_seed(3)
+    for cin, cout in ((16, 16), (32, 32), (64, 64), (64, 32), (32, 16)):
+        w = torch.randn(27, cout, cin, generator=g) * 0.05
+        frag, ew = region_split_fragments(w, torch.device("cpu"))
+        kb = 14 if cin == 16 else 27 * cin // 32
+        f = frag.view(torch.float16).float().view(kb, cout // 16, 2, 4, 16, 8)   # [kb][nb][part][g][c][j]
+        parts = f[:, :, 0] + f[:, :, 1]                                           # [kb][nb][g][c][j]
+        # rebuild w[tap][co][ci] * 2^ew from the fragments
+        rec = torch.zeros(28 if cin == 16 else 27, cout, cin)
+        for k in range(kb):
+            for gq in range(4):
+                if cin == 16:
+                    tap, ci = 2 * k + (gq >> 1), slice(8 * (gq & 1), 8 * (gq & 1) + 8)
+                else:
+                    tap, c0 = k // (cin // 32), (k % (cin // 32)) * 32 + 8 * gq
+                    ci = slice(c0, c0 + 8)
+                for nb in range(cout // 16):
+                    rec[tap, nb * 16:(nb + 1) * 16, ci] = parts[k, nb, gq]
+        ref = w.double() * 2.0 ** ew
+        assert w.abs().max().item() * 2.0 ** ew < 2.0 ** 14
+        assert (rec[:27].double() - ref).abs().max().item() <= 2.0 ** -21 * ref.abs().max().item()
+        if cin == 16:
+            assert rec[27].abs().max().item() == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,cin,cout,ncdhw,amp", [(0, 16, 16, False, 1.0), (0, 32, 32, False, 1.0),
+                                                    (0, 64, 64, False, 1.0), (2, 64, 32, False, 1.0),
+                                                    (2, 32, 16, False, 1.0), (0, 16, 16, True, 1.0),
+                                                    (2, 32, 16, True, 1.0), (0, 32, 32, False, 3e3),
+                                                    (2, 64, 32, False, 2e-4)])
+def test_region_split_conv_matches_torch(mode, cin, cout, ncdhw, amp):
+    """conv3d_region_split at forward_live's regions (24 x 20 x 26: odd and even dims, both parities
+    of P), channels-last and channels-first, inputs scaled by ``amp`` (the bound words carry the scale):
+    max error <= 1e-5 of the output scale against float64 torch and <= 2x the fp32-MFMA kernel's
+    (conv3d_region on the same inputs) + 1e-6; the output bound words equal max|y| exactly."""
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _grow, _tconv_input_region
+    from mvs_amd.ops import bound_words, conv3d_region, conv3d_region_split, region_weight
+    import torch.nn.functional as F
+    n = (24, 20, 26)
+    pad, outpad = pad_outpad(*n)
+    full = tuple((0, d - 1) for d in n)
+    Bx = _tconv_input_region(full, n, pad)
+    C2 = _tconv_input_region(Bx, n, pad)
+    g = torch.Generator().manual_seed(mode * 100 + cin + cout + int(ncdhw))
+    sc, sh, mu = _bn_params(cout, g)
+    sh = sh * amp
+    mu = mu * amp
+    org = lambda r: [lo for lo, _ in r]
+    size = lambda r: [hi - lo + 1 for lo, hi in r]
+    sl = lambda r: (slice(None), slice(None)) + tuple(slice(lo, hi + 1) for lo, hi in r)
+    cl = lambda t: t.permute(0, 2, 3, 4, 1).contiguous()
+
+    def zero_ext(reg, c):
+        t = torch.zeros(2, c, *n)
+        t[sl(reg)] = torch.relu(torch.randn(2, c, *size(reg), generator=g)) * amp   # post-ReLU activations
+        return t
+
+    if mode == 0:      # S1: conv_k_1 on B from halo(B)
+        out_reg, in_reg = Bx, _grow(Bx, n, 1)
+        x, x2 = zero_ext(in_reg, cin), None
+        wt = torch.randn(cout, cin, 3, 3, 3, generator=g) * 0.1
+        f = lambda xx, ww: F.conv3d(xx, ww, padding=1)
+    else:              # T2: deconv from C2 (+ addend) onto B
+        out_reg, in_reg = Bx, C2
+        x, x2 = zero_ext(in_reg, cin), zero_ext(in_reg, cin)
+        wt = torch.randn(cin, cout, 3, 3, 3, generator=g) * 0.1
+        f = lambda xx, ww: F.conv_transpose3d(xx, ww, stride=2, padding=pad, output_padding=outpad)
+    xin = x + x2 if x2 is not None else x
+    ref64 = _bn_relu(f(xin.double(), wt.double()), sc.double(), sh.double(), mu.double())[sl(out_reg)]
+    conv = torch.nn.ConvTranspose3d(cin, cout, 3) if mode == 2 else torch.nn.Conv3d(cin, cout, 3)
+    conv.weight.data = wt
+    w27 = region_weight(conv).to(DEV)
+    bw = bound_words(3, DEV)
+    xr = cl(x[sl(in_reg)]).to(DEV)
+    x2r = cl(x2[sl(in_reg)]).to(DEV) if x2 is not None else None
+    bw[0, 5] = torch.tensor([xr.abs().max().item()], dtype=torch.float32).view(torch.int32).item()
+    if x2r is not None:
+        bw[1, 0] = torch.tensor([x2r.abs().max().item()], dtype=torch.float32).view(torch.int32).item()
+    bn = (sc.to(DEV), sh.to(DEV), mu.to(DEV))
+    args = (mode, list(n), org(out_reg), size(out_reg), org(in_reg), size(in_reg), list(pad))
+    with torch.no_grad():
+        y = conv3d_region_split(xr, x2r, w27, *args, bw[0], None if x2r is None else bw[1], bw[2], *bn,
+                                out_ncdhw=ncdhw)
+        y32 = conv3d_region(xr, x2r, w27, *args, *bn, out_ncdhw=ncdhw)
+        torch.cuda.synchronize()
+    ymax = y.abs().max().item()
+    got_bound = bw[2].cpu().numpy().view(np.float32).max()
+    assert got_bound == ymax, (got_bound, ymax)
+    y = (y if ncdhw else y.permute(0, 4, 1, 2, 3)).cpu()
+    y32 = (y32 if ncdhw else y32.permute(0, 4, 1, 2, 3)).cpu()
+    assert y.shape == ref64.shape
+    scale = ref64.abs().max().item()
+    err = (y.double() - ref64).abs().max().item()
+    err32 = (y32.double() - ref64).abs().max().item()
+    assert err <= 1e-5 * scale, (err, scale)
+    assert err <= 2 * err32 + 1e-6 * scale, (err, err32, scale)
+
+
+@pytest.mark.gpu
+def test_region_conv_raises_output_bound_words():
+    """The fp32-MFMA region kernel (conv3d_region, the S2 conv_k_0 of the split path) raises its
+    output's bound words to exactly max|y| -- the scale the split-fp16 conv_k_1 reads."""
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _grow, _tconv_input_region
+    from mvs_amd.ops import bound_words, conv3d_region, region_weight
+    n = (24, 20, 26)
+    pad, _ = pad_outpad(*n)
+    Bx = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
+    out_reg = _grow(Bx, n, 1)
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 32, *n, generator=g).to(DEV)
+    conv = torch.nn.Conv3d(32, 32, 3)
+    conv.weight.data = torch.randn(32, 32, 3, 3, 3, generator=g) * 0.1
+    bw = bound_words(1, DEV)
+    with torch.no_grad():
+        y = conv3d_region(x, None, region_weight(conv).to(DEV), 1, list(n), [lo for lo, _ in out_reg],
+                          [hi - lo + 1 for lo, hi in out_reg], None, None, list(pad), y_bound=bw[0])
+        torch.cuda.synchronize()
+    words = bw[0].cpu().numpy().view(np.float32)
+    assert words.max() == y.abs().max().item()
