@@ -754,15 +754,17 @@ int mvs_channel_stats(const float* x, int layout, int batch, int channels, long 
 
 int mvs_bn_relu(const float* x, int layout, int batch, int channels, long long voxels, const float* scale,
                 const float* shift, const float* mean, const float* r, const float* r_scale,
-                const float* r_shift, const float* r_mean, float* y, void* stream) {
+                const float* r_shift, const float* r_mean, float* y, unsigned* y_bound, void* stream) {
   if (!x || !y || !scale || !shift || !mean || batch <= 0 || channels <= 0 || voxels <= 0)
     return MVS_ERR_INVALID_ARGUMENT;
+  if ((uintptr_t)y_bound & 3u) return MVS_ERR_INVALID_ARGUMENT;
   if (r && (!r_scale || !r_shift || !r_mean)) return MVS_ERR_INVALID_ARGUMENT;
   if (!channel_layout_ok(layout, channels, x, r, y)) return MVS_ERR_INVALID_ARGUMENT;
   if ((uint64_t)batch * channels > 65535u && !(layout & MVS_LAYOUT_CHANNELS_LAST)) return MVS_ERR_TOO_LARGE;
   const mvs::LaunchCheck lc;
   mvs::launch_bn_relu(x, (layout & MVS_LAYOUT_CHANNELS_LAST) != 0, batch, channels, (size_t)voxels, scale, shift,
-                      mean, r, r_scale, r_shift, r_mean, y, (hipStream_t)stream);
+                      mean, r, r_scale, r_shift, r_mean, y, reinterpret_cast<uint32_t*>(y_bound),
+                      (hipStream_t)stream);
   return lc.status();
 }
 

@@ -15,6 +15,7 @@
 // statistics -- and the BatchNorm outputs and running statistics built from them -- are bit-identical
 // run to run.
 #include "launchers.h"
+#include "split.h"
 #include "packed.h"
 
 namespace mvs {
@@ -126,9 +127,11 @@ __global__ __launch_bounds__(kBlock) void bn_relu_cl_kernel(const float4* __rest
                                                             const float* __restrict__ sc, const float* __restrict__ sh,
                                                             const float* __restrict__ mu, const float4* __restrict__ r,
                                                             const float* __restrict__ rsc, const float* __restrict__ rsh,
-                                                            const float* __restrict__ rmu, float4* __restrict__ y) {
+                                                            const float* __restrict__ rmu, float4* __restrict__ y,
+                                                            uint32_t* __restrict__ yb) {
   const size_t stride = (size_t)gridDim.x * kBlock;
   const size_t j0 = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  float vmax = 0.0f;   // (outputs are >= 0)
   const int c = 4 * (int)(j0 % (size_t)C4);   // constant per thread (C4 divides the stride)
   float a[4], b[4], m[4], ra[4] = {0, 0, 0, 0}, rb[4] = {0, 0, 0, 0}, rm[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -153,8 +156,10 @@ __global__ __launch_bounds__(kBlock) void bn_relu_cl_kernel(const float4* __rest
       o.z += bn_relu(u.z, ra[2], rb[2], rm[2]);
       o.w += bn_relu(u.w, ra[3], rb[3], rm[3]);
     }
+    vmax = fmaxf(vmax, fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w)));
     y[j] = o;
   }
+  if (yb) bound_update(yb, vmax);
 }
 
 // NCDHW: one (sample, channel) plane per blockIdx.y
@@ -162,8 +167,10 @@ __global__ __launch_bounds__(kBlock) void bn_relu_cf_kernel(const float* __restr
                                                             const float* __restrict__ sc, const float* __restrict__ sh,
                                                             const float* __restrict__ mu, const float* __restrict__ r,
                                                             const float* __restrict__ rsc, const float* __restrict__ rsh,
-                                                            const float* __restrict__ rmu, float* __restrict__ y) {
+                                                            const float* __restrict__ rmu, float* __restrict__ y,
+                                                            uint32_t* __restrict__ yb) {
   const int c = (int)blockIdx.y % C;
+  float vmax = 0.0f;
   const size_t base = (size_t)blockIdx.y * plane;
   const float a = sc[c], b = sh[c], m = mu[c];
   const float ra = r ? rsc[c] : 0.0f, rb = r ? rsh[c] : 0.0f, rm = r ? rmu[c] : 0.0f;
@@ -183,15 +190,18 @@ __global__ __launch_bounds__(kBlock) void bn_relu_cf_kernel(const float* __restr
         o.z += bn_relu(u.z, ra, rb, rm);
         o.w += bn_relu(u.w, ra, rb, rm);
       }
+      vmax = fmaxf(vmax, fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w)));
       y4[j] = o;
     }
   } else {
     for (size_t j = (size_t)blockIdx.x * kBlock + threadIdx.x; j < plane; j += stride) {
       float o = bn_relu(x[base + j], a, b, m);
       if (r) o += bn_relu(r[base + j], ra, rb, rm);
+      vmax = fmaxf(vmax, o);
       y[base + j] = o;
     }
   }
+  if (yb) bound_update(yb, vmax);
 }
 
 unsigned grid_cl(size_t n4) {
@@ -232,15 +242,15 @@ void launch_channel_stats(const float* x, bool channels_last, int B, int C, size
 
 void launch_bn_relu(const float* x, bool channels_last, int B, int C, size_t voxels, const float* sc,
                     const float* sh, const float* mu, const float* r, const float* rsc, const float* rsh,
-                    const float* rmu, float* y, hipStream_t s) {
+                    const float* rmu, float* y, uint32_t* y_bound, hipStream_t s) {
   if (channels_last) {
     const size_t n4 = (size_t)B * voxels * (size_t)C / 4;
     hipLaunchKernelGGL(bn_relu_cl_kernel, dim3(grid_cl(n4)), dim3(kBlock), 0, s, reinterpret_cast<const float4*>(x),
                        n4, C / 4, sc, sh, mu, reinterpret_cast<const float4*>(r), rsc, rsh, rmu,
-                       reinterpret_cast<float4*>(y));
+                       reinterpret_cast<float4*>(y), y_bound);
   } else {
     hipLaunchKernelGGL(bn_relu_cf_kernel, dim3(grid_cf(voxels, (size_t)B * C), (unsigned)(B * C)), dim3(kBlock), 0,
-                       s, x, voxels, C, sc, sh, mu, r, rsc, rsh, rmu, y);
+                       s, x, voxels, C, sc, sh, mu, r, rsc, rsh, rmu, y, y_bound);
   }
 }
 

@@ -145,7 +145,7 @@ void launch_channel_stats(const float* x, bool channels_last, int B, int C, size
                           hipStream_t s);
 void launch_bn_relu(const float* x, bool channels_last, int B, int C, size_t voxels, const float* sc,
                     const float* sh, const float* mu, const float* r, const float* rsc, const float* rsh,
-                    const float* rmu, float* y, hipStream_t s);
+                    const float* rmu, float* y, uint32_t* y_bound, hipStream_t s);
 
 // dtu_input.hip: data.py:206-210 image normalisation (uint8 HWC -> fp32 NCHW), data.py:300-301
 // depth thresholds

@@ -94,7 +94,7 @@ SIGNATURES = {
     "mvs_refine_output_fwd": (_c_int, [_p, _p, _p, _p] + [_c_int] * 4 + [_c_float, _p, _p]),
     "mvs_channel_stats_slots": (ctypes.c_size_t, [_c_int, _c_int, _c_int, ctypes.c_longlong]),
     "mvs_channel_stats": (_c_int, [_p, _c_int, _c_int, _c_int, ctypes.c_longlong, _p, _p]),
-    "mvs_bn_relu": (_c_int, [_p, _c_int, _c_int, _c_int, ctypes.c_longlong] + [_p] * 9),
+    "mvs_bn_relu": (_c_int, [_p, _c_int, _c_int, _c_int, ctypes.c_longlong] + [_p] * 10),
 }
 
 

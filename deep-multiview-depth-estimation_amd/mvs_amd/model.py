@@ -461,9 +461,16 @@ class CostVolumeReg(nn.Module):
         applied in place to the region tensors (channels-last).  The transposed convs run over
         the full output volume (their statistics) and keep the M-region part.  ``cv`` may be the
         channel-quad volume (conv_0_0 and the stride-2 convs read it with 16-byte loads)."""
-        from .ops import (CONV_S1, CONV_S2, CONV_T2, bn_relu_, channel_stats, conv3d_k3, conv3d_k3_split,
-                          conv3d_region, deconv3d_k3s2, region_weight, softmax_depth)
+        from .ops import (CONV_S1, CONV_S2, CONV_T2, bn_relu_, bound_words, channel_stats, conv3d_k3,
+                          conv3d_k3_split, conv3d_region, conv3d_region_split, deconv3d_k3s2, region_weight,
+                          softmax_depth)
         c4 = cv.dim() == 6
+        # with split_f16 the stride-1 and transposed convs run on the split-fp16 matrix cores
+        # (conv3d_region_split): their inputs' bound words are raised by the BN + ReLU passes -- rows 0-2
+        # the conv_k_1 inputs, 4-5 conv_2_1 / conv_3_1's normalised outputs, 6 deconv_3_0's
+        bw = (bound_words(7, cv.device) if self.split_f16 and os.environ.get("MVS_REGION_SPLIT", "1") != "0"
+              else None)
+        bwr = lambda k: None if bw is None else bw[k]
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad, bsz = list(n), list(self.pad), cv.shape[0]
@@ -481,30 +488,44 @@ class CostVolumeReg(nn.Module):
             p0 = _bn_train(self.BN_0, *channel_stats(y0, False), count)
         cv.record_stream(side)
         stage = []
-        for conv_a, bn in ((self.conv_1_0, self.BN_1), (self.conv_2_0, self.BN_2), (self.conv_3_0, self.BN_3)):
+        for k, (conv_a, bn) in enumerate(((self.conv_1_0, self.BN_1), (self.conv_2_0, self.BN_2),
+                                          (self.conv_3_0, self.BN_3))):
             z = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(R2), size(R2), None, None,
                               pad, in_c4=c4)
             p = _bn_train(bn, *channel_stats(z, True), count)
-            stage.append((bn_relu_(z, True, *p), _bn_constant(p)))
+            stage.append((bn_relu_(z, True, *p, y_bound=bwr(k)), _bn_constant(p)))
         lv = []
-        for (y, a), conv_b, bn in zip(stage, (self.conv_1_1, self.conv_2_1, self.conv_3_1),
-                                      (self.BN_1, self.BN_2, self.BN_3)):
+        for k, ((y, a), conv_b, bn) in enumerate(zip(stage, (self.conv_1_1, self.conv_2_1, self.conv_3_1),
+                                                     (self.BN_1, self.BN_2, self.BN_3))):
             # level 1 only feeds deconv_1_0's input sum: channels-first for its loads
             cf = bn is self.BN_1
-            z = conv3d_region(y, None, region_weight(conv_b), CONV_S1, dims, org(R1), size(R1), org(R2),
-                              size(R2), None, out_ncdhw=cf)
+            if bw is not None:
+                z = conv3d_region_split(y, None, region_weight(conv_b), CONV_S1, dims, org(R1), size(R1), org(R2),
+                                        size(R2), None, bw[k], None, None, out_ncdhw=cf)
+            else:
+                z = conv3d_region(y, None, region_weight(conv_b), CONV_S1, dims, org(R1), size(R1), org(R2),
+                                  size(R2), None, out_ncdhw=cf)
             s1, s2 = channel_stats(z, not cf)
             c1, c2 = _border_class_sums(conv_b.weight, a, R1, n, bsz)
             p = _bn_train(bn, s1 + c1, s2 + c2, count)
-            lv.append(bn_relu_((_crop_cf if cf else _crop_cl)(z, R1, M), not cf, *p))
+            lv.append(bn_relu_((_crop_cf if cf else _crop_cl)(z, R1, M), not cf, *p,
+                               y_bound=None if cf else bwr(3 + k)))
         y1, y2, y3 = lv
-        z = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
-                          size(M), pad)
+        if bw is not None:
+            z = conv3d_region_split(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, [0, 0, 0], dims,
+                                    org(M), size(M), pad, bw[5], None, None)
+        else:
+            z = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
+                              size(M), pad)
         p = _bn_train(self.BN_2, *channel_stats(z, True), count)
-        y3 = bn_relu_(_crop_cl(z, full, M), True, *p)
+        y3 = bn_relu_(_crop_cl(z, full, M), True, *p, y_bound=bwr(6))
         del z
-        z = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
-                          size(M), pad, out_ncdhw=True)
+        if bw is not None:
+            z = conv3d_region_split(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, [0, 0, 0], dims,
+                                    org(M), size(M), pad, bw[6], bw[4], None, out_ncdhw=True)
+        else:
+            z = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
+                              size(M), pad, out_ncdhw=True)
         p = _bn_train(self.BN_1, *channel_stats(z, False), count)
         y2 = bn_relu_(_crop_cf(z, full, M), False, *p)
         del z

@@ -1141,9 +1141,10 @@ def channel_stats(x: torch.Tensor, channels_last: bool):
     return s[0], s[1]
 
 
-def bn_relu_(x: torch.Tensor, channels_last: bool, scale, shift, mean, r=None, r_bn=None) -> torch.Tensor:
+def bn_relu_(x: torch.Tensor, channels_last: bool, scale, shift, mean, r=None, r_bn=None, y_bound=None) -> torch.Tensor:
     """In place: x = relu((x - mean) * scale + shift) [+ relu(BN_r(r))], channels on the last dim
-    (channels_last) or dim 1; r_bn = (scale, shift, mean) of r.  x must be contiguous fp32."""
+    (channels_last) or dim 1; r_bn = (scale, shift, mean) of r.  x must be contiguous fp32.
+    ``y_bound``: zeroed bound words raised to max of the result."""
     _require_gpu(x, "x")
     lib = _lib.load()
     if not x.is_contiguous() or x.dtype != _F32:
@@ -1161,7 +1162,7 @@ def bn_relu_(x: torch.Tensor, channels_last: bool, scale, shift, mean, r=None, r
     pt = lambda t: None if t is None else _lib.ptr(t)
     rc = lib.mvs_bn_relu(_lib.ptr(x), _lib.MVS_LAYOUT_CHANNELS_LAST if channels_last else 0, x.shape[0], c, vox,
                          pt(sc), pt(sh), pt(mu), pt(rr), *(pt(t) for t in (rs or (None, None, None))), _lib.ptr(x),
-                         _lib.stream_handle(x.device))
+                         _bound_ptr(y_bound), _lib.stream_handle(x.device))
     _lib.check(rc, "mvs_bn_relu")
     return x
 

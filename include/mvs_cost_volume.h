@@ -525,10 +525,11 @@ int mvs_channel_stats(const float* x, int layout, int batch, int channels, long 
 /* y = max((x - mean) * scale + shift, 0) per channel (BatchNorm3d with the batch statistics:
  * scale = gamma / sqrt(var + eps), shift = beta; then ReLU), and, when r is given,
  * + max((r - r_mean) * r_scale + r_shift, 0) (model.py:121-123: relu(BN_0(deconv_1_0)) + y0).
- * Layouts as mvs_channel_stats; y may alias x. */
+ * Layouts as mvs_channel_stats; y may alias x.  y_bound: NULL or MVS_BOUND_WORDS zeroed words (DEVICE)
+ * raised to max y (the scale a split-fp16 region convolution reads y with). */
 int mvs_bn_relu(const float* x, int layout, int batch, int channels, long long voxels, const float* scale,
                 const float* shift, const float* mean, const float* r, const float* r_scale,
-                const float* r_shift, const float* r_mean, float* y, void* stream);
+                const float* r_shift, const float* r_mean, float* y, unsigned* y_bound, void* stream);
 
 #ifdef __cplusplus
 }

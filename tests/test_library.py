@@ -96,8 +96,8 @@ def test_invalid_arguments_rejected_before_any_launch():
     assert lib.mvs_channel_stats(ctypes.c_void_p(20), 1, 2, 16, 100, fake, null) == -1
     assert lib.mvs_channel_stats(fake, 2, 2, 16, 100, fake, null) == -1
     assert lib.mvs_channel_stats(fake, 0, 2, 16, 0, fake, null) == -1
-    assert lib.mvs_bn_relu(fake, 0, 2, 16, 100, fake, fake, None, None, None, None, None, fake, null) == -1
-    assert lib.mvs_bn_relu(fake, 0, 2, 16, 100, fake, fake, fake, fake, None, fake, fake, fake, null) == -1
+    assert lib.mvs_bn_relu(fake, 0, 2, 16, 100, fake, fake, None, None, None, None, None, fake, None, null) == -1
+    assert lib.mvs_bn_relu(fake, 0, 2, 16, 100, fake, fake, fake, fake, None, fake, fake, fake, None, null) == -1
 
 
 def test_build_is_gfx950_in_tree():
