@@ -659,10 +659,22 @@ int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float
                                 const int* out_origin, const int* out_size, const int* in_origin, const int* in_size,
                                 const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                                 const unsigned* x_bound, const unsigned* x2_bound, unsigned* y_bound, void* stream) {
-  if (!x || !weight_frag || !y || !dims || !out_origin || !out_size || !in_origin || !in_size || batch <= 0)
+  if (!x || !weight_frag || !y || !dims || !out_origin || !out_size || batch <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if (mode < MVS_CONV_S1 || mode > MVS_CONV_T2 || (flags & ~(MVS_CONV_OUT_NCDHW | MVS_CONV_IN_C4 | MVS_CONV_IN_SPLIT)))
     return MVS_ERR_INVALID_ARGUMENT;
-  if ((mode != MVS_CONV_S1 && mode != MVS_CONV_T2) || (flags & ~MVS_CONV_OUT_NCDHW)) return MVS_ERR_INVALID_ARGUMENT;
-  if (mode == MVS_CONV_T2 && !pad) return MVS_ERR_INVALID_ARGUMENT;
+  // S2 reads the split cost volume (its 8 bound words in x_bound), S1 / T2 an fp32 region tensor
+  const bool s2 = mode == MVS_CONV_S2;
+  const int in_flags = MVS_CONV_IN_C4 | MVS_CONV_IN_SPLIT;
+  if (s2 != ((flags & in_flags) == in_flags) || (!s2 && (flags & in_flags))) return MVS_ERR_INVALID_ARGUMENT;
+  if (s2 && (x2 || !x_bound || c_in != 32)) return MVS_ERR_INVALID_ARGUMENT;
+  if ((in_origin != nullptr) != (in_size != nullptr) || (!s2 && !in_origin)) return MVS_ERR_INVALID_ARGUMENT;
+  if (mode != MVS_CONV_S1 && !pad) return MVS_ERR_INVALID_ARGUMENT;
+  int io[3] = {0, 0, 0}, is[3] = {dims[0], dims[1], dims[2]};   // S2 without a box: the whole volume
+  if (in_origin)
+    for (int k = 0; k < 3; ++k) {
+      io[k] = in_origin[k];
+      is[k] = in_size[k];
+    }
   if (x2 && x_bound && !x2_bound) return MVS_ERR_INVALID_ARGUMENT;   // a sum needs both bounds
   if (((uintptr_t)x | (uintptr_t)x2 | (uintptr_t)weight_frag) & 15u ||
       ((uintptr_t)x_bound | (uintptr_t)x2_bound | (uintptr_t)y_bound) & 3u)
@@ -674,15 +686,15 @@ int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float
   for (int k = 0; k < 3; ++k) {
     if (dims[k] <= 0 || out_size[k] <= 0 || out_origin[k] < 0 || out_origin[k] + out_size[k] > dims[k])
       return MVS_ERR_INVALID_ARGUMENT;
-    if (in_size[k] <= 0 || in_origin[k] < 0 || in_origin[k] + in_size[k] > dims[k]) return MVS_ERR_INVALID_ARGUMENT;
+    if (is[k] <= 0 || io[k] < 0 || io[k] + is[k] > dims[k]) return MVS_ERR_INVALID_ARGUMENT;
     ovox *= (uint64_t)out_size[k];
-    svox *= (uint64_t)in_size[k];
+    svox *= (uint64_t)is[k];
   }
   if (ovox >= (1ull << 31) || svox * (uint64_t)c_in * 4u >= 0xFFFFFFC0ull) return MVS_ERR_TOO_LARGE;
   const mvs::LaunchCheck lc;
   const int st = mvs::launch_conv3d_region_split(
       mode, (flags & MVS_CONV_OUT_NCDHW) != 0, x, x2, weight_frag, weight_exp, y, batch, c_in, c_out, dims, out_origin,
-      out_size, in_origin, in_size, pad, bn_scale, bn_shift, bn_mean, reinterpret_cast<const uint32_t*>(x_bound),
+      out_size, io, is, pad, bn_scale, bn_shift, bn_mean, reinterpret_cast<const uint32_t*>(x_bound),
       reinterpret_cast<const uint32_t*>(x2_bound), reinterpret_cast<uint32_t*>(y_bound), (hipStream_t)stream);
   if (st != MVS_OK) return st;
   return lc.status();

@@ -19,6 +19,10 @@
 // K blocking.  CI >= 32: one K-32 block per (tap, 32 input channels), lane (m, g) supplies channels
 // 8g .. 8g + 7 of its row's tap voxel.  CI = 16 (conv_1_1, S1 only): one K-32 block per PAIR of taps
 // (2j, 2j + 1; tap 27 is empty), lanes g = 0, 1 the first tap's 16 channels, g = 2, 3 the second's.
+//
+// S2 (conv_k_0, model.py:78-80 / :103-111): the input is the split cost volume itself (split.h's SCV,
+// or a box of it), already the operands: a lane's 8 channels are the hi / lo halves of quads 2g and
+// 2g + 1 (two 16-byte loads, no conversion), scaled by the volume's bound words (cv_split_exponent).
 #include "launchers.h"
 #include "packed.h"
 #include "split.h"
@@ -28,7 +32,7 @@ namespace {
 
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 constexpr uint32_t kOob = 0xFFFFFFC0u;   // out-of-range buffer offset (loads return 0); +16 stays out
-constexpr int kS1 = 0, kT2 = 2;
+constexpr int kS1 = 0, kS2 = 1, kT2 = 2;
 
 struct GeoS {
   int n[3];    // volume dims
@@ -56,6 +60,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_split_kernel(
   constexpr int CB = PAIR ? 1 : CI / 32;   // K-32 blocks per tap
   static_assert(CO % 16 == 0 && (PAIR || CI % 32 == 0), "channel counts");
   static_assert(!PAIR || MODE == kS1, "tap pairs: stride-1 convolutions only");
+  static_assert(MODE != kS2 || CI == 32, "S2: the 32-channel split cost volume");
   const int lane = (int)threadIdx.x & 63;
   const int m = lane & 15, kq = lane >> 4;
   const int b = (int)blockIdx.z;
@@ -82,10 +87,15 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_split_kernel(
   const int row0 = (bx * (kBlock / 64) + ((int)threadIdx.x >> 6)) * kRows;
   if (row0 >= rows) return;   // wave-uniform; no barriers in this kernel
 
-  // the input's scale: max|x| (+ max|x2|) 2^ex < 2^14
-  float bound = bound_read(xb);
-  if (x2) bound += bound_read(xb2);
-  const int ex = act_split_exponent(bound);
+  // the input's scale: max|x| (+ max|x2|) 2^ex < 2^14; S2: the split volume's own exponent
+  int ex;
+  if constexpr (MODE == kS2) {
+    ex = cv_split_exponent(xb);
+  } else {
+    float bound = bound_read(xb);
+    if (x2) bound += bound_read(xb2);
+    ex = act_split_exponent(bound);
+  }
 
   int lin[RB];
   unsigned vm[RB][3];
@@ -101,6 +111,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_split_kernel(
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
       if constexpr (MODE == kS1) bs[d] = o[d] - 1 - g.i0[d];
+      else if constexpr (MODE == kS2) bs[d] = 2 * o[d] - g.pad[d] - g.i0[d];   // taps off the box: off the volume
       else bs[d] = ((o[d] + g.pad[d] - par[d]) >> 1) - g.i0[d];
       unsigned mk = 0;
 #pragma unroll
@@ -121,12 +132,21 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_split_kernel(
     for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
 
   const size_t rvol = (size_t)g.in[0] * g.in[1] * g.in[2];
+  // S2: the sample's 8 quad planes of 16-byte elements (8 * rvol * 16 B = the same bytes as CI fp32)
   const Rsrc rs = make_rsrc(x + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
   const Rsrc rs2 = make_rsrc(x2 ? x2 + (size_t)b * rvol * CI : x, x2 ? (uint32_t)(rvol * CI * 4) : 0u);
   const int sy = g.in[2], sz = g.in[1] * g.in[2];
 
   // 8 channels c0 .. c0 + 7 of input voxel vx (kOob: zeros) as split fp16 parts
   auto load_split = [&](uint32_t vx, int c0, h8v& hi, h8v& lo) {
+    if constexpr (MODE == kS2) {   // quads c0 / 4, c0 / 4 + 1 of the split volume: {hi x4, lo x4} each
+      const uint32_t q = (uint32_t)c0 >> 2;
+      const uint4 e0 = __builtin_bit_cast(uint4, ld4(rs, vx == kOob ? kOob : ((q * (uint32_t)rvol) + vx) * 16u, 0));
+      const uint4 e1 = __builtin_bit_cast(uint4, ld4(rs, vx == kOob ? kOob : (((q + 1) * (uint32_t)rvol) + vx) * 16u, 0));
+      hi = __builtin_bit_cast(h8v, make_uint4(e0.x, e0.y, e1.x, e1.y));
+      lo = __builtin_bit_cast(h8v, make_uint4(e0.z, e0.w, e1.z, e1.w));
+      return;
+    }
     const uint32_t eo = vx == kOob ? kOob : (vx * (uint32_t)CI + (uint32_t)c0) * 4u;
     f4v a0 = ld4(rs, eo, 0), a1 = ld4(rs, eo + 16u, 0);
     if (x2) {
@@ -271,8 +291,10 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
                                    x2_bound, y_bound, s);                                                 \
     return MVS_OK;                                                                                        \
   }
-  // S1: conv_k_1 (16 / 32 / 64 channels); T2: deconv_3_0 (64 -> 32), deconv_2_0 (32 -> 16)
+  // S1: conv_k_1 (16 / 32 / 64 channels); T2: deconv_3_0 (64 -> 32), deconv_2_0 (32 -> 16); S2: conv_k_0
+  // from the split cost volume (32 -> 16 / 32 / 64)
   MVS_RSPLIT_CASE(kS1, 16, 16) MVS_RSPLIT_CASE(kS1, 32, 32) MVS_RSPLIT_CASE(kS1, 64, 64)
+  MVS_RSPLIT_CASE(kS2, 32, 16) MVS_RSPLIT_CASE(kS2, 32, 32) MVS_RSPLIT_CASE(kS2, 32, 64)
   MVS_RSPLIT_CASE(kT2, 64, 32) MVS_RSPLIT_CASE(kT2, 32, 16)
 #undef MVS_RSPLIT_CASE
   return MVS_ERR_INVALID_ARGUMENT;

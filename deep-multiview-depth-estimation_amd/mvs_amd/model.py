@@ -177,6 +177,9 @@ class CostVolumeReg(nn.Module):
         if cv.dim() == 6:
             if self.live_ok(cv.shape[2:5]) and _hip_cv(cv):
                 return self.forward_live(cv, bound)
+            if (cv.dtype == torch.int32 and bound is not None and self.split_f16 and self.live_train_ok(cv.shape[2:5])
+                    and _hip_cv(cv)):
+                return self.forward_live_train(cv, bound)   # the split-fp16 train-mode path reads it as is
             if cv.dtype == torch.int32:   # the split cost volume: fp32 values back (to 2^-22) for other paths
                 cv = unsplit_cost_volume(cv, bound)
             if self.live_train_ok(cv.shape[2:5]) and _hip_cv(cv):
@@ -366,6 +369,10 @@ class CostVolumeReg(nn.Module):
                 # conv_1_0 reads the whole volume: LDS-staged split-fp16 kernel (csrc/conv3d_s2_split.hip)
                 ya = conv_s2_split(cv, bound, conv_a.weight, dims, org(halo), size(halo), pad, *bn_eval(bn))
                 ab = None
+            elif split_cv and bw is not None:
+                # conv_2_0 / conv_3_0 on the split-fp16 matrix cores, straight from the split volume
+                ya = conv3d_region_split(cv, None, region_weight(conv_a), CONV_S2, dims, org(halo), size(halo),
+                                         cv_box[0], cv_box[1], pad, bound, None, ab, *bn_eval(bn))
             else:
                 ya = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(halo), size(halo), cv_box[0],
                                    cv_box[1], pad, *bn_eval(bn), in_c4=c4, absmax=bound if split_cv else None,
@@ -479,7 +486,8 @@ class CostVolumeReg(nn.Module):
         side = _side_stream(cv.device)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            if bound is not None and c4 and cv.dtype == torch.float32 and self.split_f16 and cv.shape[1] == 8:
+            if bound is not None and c4 and self.split_f16 and cv.shape[1] == 8:
+                # (fp32 channel quads with their bound words, or the split volume itself)
                 # the channel-quad volume with its bound words: conv_0_0 on the split-fp16 matrix cores
                 # (fp32-level error; 4.4 -> ~1 ms at cfg 2), raw output for the batch sums
                 y0 = conv3d_k3_split(cv, bound, self.conv_0_0.weight)
@@ -490,8 +498,12 @@ class CostVolumeReg(nn.Module):
         stage = []
         for k, (conv_a, bn) in enumerate(((self.conv_1_0, self.BN_1), (self.conv_2_0, self.BN_2),
                                           (self.conv_3_0, self.BN_3))):
-            z = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(R2), size(R2), None, None,
-                              pad, in_c4=c4)
+            if cv.dtype == torch.int32:   # the split volume: conv_k_0 on the split-fp16 matrix cores
+                z = conv3d_region_split(cv, None, region_weight(conv_a), CONV_S2, dims, org(R2), size(R2), None,
+                                        None, pad, bound, None, None)
+            else:
+                z = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(R2), size(R2), None, None,
+                                  pad, in_c4=c4)
             p = _bn_train(bn, *channel_stats(z, True), count)
             stage.append((bn_relu_(z, True, *p, y_bound=bwr(k)), _bn_constant(p)))
         lv = []
@@ -826,14 +838,17 @@ class MVSNet(nn.Module):
                  and (reg.live_ok((c.d_num,) + tuple(feature_maps.shape[2:]))
                       or reg.live_train_ok((c.d_num,) + tuple(feature_maps.shape[2:]))))
         # eval mode with the split-fp16 regulariser: the fused kernel writes the split cost volume
-        split = (quads and not bf16 and reg.split_f16
-                 and reg.live_ok((c.d_num,) + tuple(feature_maps.shape[2:])) and feature_maps.shape[1] == 32)
+        # (and in train-mode BN, test.py:61, whose live path reads the split volume the same way)
+        live_n = (c.d_num,) + tuple(feature_maps.shape[2:])
+        split = (quads and not bf16 and reg.split_f16 and (reg.live_ok(live_n) or reg.live_train_ok(live_n))
+                 and feature_maps.shape[1] == 32)
         # ... and with the opt-in fused head kernel (MVS_CV_HEAD=1), the volume is not formed here at
         # all: the regulariser forms it on chip inside conv_0_0 / conv_1_0.  Opt-in:
         # its gathering producers corrupt one item sporadically; the default path
         # materialises the split volume and runs both convolutions in one pass (ops.split_head)
-        deferred = split and (c.d_num % 2 == 0 and n_views in (2, 3) and all(p % 2 == 1 for p in reg.pad)
-                              and os.environ.get("MVS_CV_HEAD", "0") == "1")
+        deferred = split and reg.live_ok(live_n) and (c.d_num % 2 == 0 and n_views in (2, 3)
+                                                      and all(p % 2 == 1 for p in reg.pad)
+                                                      and os.environ.get("MVS_CV_HEAD", "0") == "1")
         cost_volume, d_batch, ref_views = warp_and_assemble_cost_volume(
             K_batch, R_batch, T_batch, d_min, d_int, feature_maps, batch_size, n_views,
             d_num=c.d_num, d_scale=c.d_scale,

@@ -1079,18 +1079,27 @@ def region_split_fragments(weight, device):
 # indexes every declared mutable argument positionally, which fails for an omitted trailing default)
 @torch.library.custom_op("mvs::conv3d_region_split", mutates_args=())
 def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Tensor, mode: int,
-                        dims: list[int], out_origin: list[int], out_size: list[int], in_origin: list[int],
-                        in_size: list[int], pad: Optional[list[int]], x_bound: Optional[torch.Tensor],
+                        dims: list[int], out_origin: list[int], out_size: list[int], in_origin: Optional[list[int]],
+                        in_size: Optional[list[int]], pad: Optional[list[int]], x_bound: Optional[torch.Tensor],
                         x2_bound: Optional[torch.Tensor], y_bound: Optional[torch.Tensor],
                         bn_scale: Optional[torch.Tensor] = None, bn_shift: Optional[torch.Tensor] = None,
                         bn_mean: Optional[torch.Tensor] = None, out_ncdhw: bool = False) -> torch.Tensor:
     """conv3d_region's CONV_S1 / CONV_T2 convolutions on the f16 matrix cores with split operands
     (mvs_conv3d_region_split_fwd, csrc/conv3d_region_split.hip): same geometry, layouts and epilogue;
     the input scaled by its bound words ``x_bound`` (+ ``x2_bound`` for the sum x + x2), ``y_bound``
-    (zeroed words or None) raised to max|y|.  fp32-level error.  Inference only."""
+    (zeroed words or None) raised to max|y|.  CONV_S2: x is the split cost volume (int32 [B, 8, D, H, W,
+    4], or a box of it with in_origin / in_size), x_bound its 8 bound words.  fp32-level error
+    (DESIGN.md §3.8).  Inference only."""
     _require_gpu(x, "x")
     lib = _lib.load()
-    x = x.to(_F32).contiguous()
+    flags = _lib.MVS_CONV_OUT_NCDHW if out_ncdhw else 0
+    if mode == CONV_S2:
+        if x.dtype != torch.int32 or x.dim() != 6 or x_bound is None or x_bound.numel() != 8:
+            raise ValueError("CONV_S2: the split cost volume [B, 8, D, H, W, 4] int32 and its 8 bound words")
+        flags |= _lib.MVS_CONV_IN_C4 | _lib.MVS_CONV_IN_SPLIT
+        x = x.contiguous()
+    else:
+        x = x.to(_F32).contiguous()
     if x2 is not None:
         x2 = x2.to(_F32).contiguous()
     dev = x.device
@@ -1102,11 +1111,14 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
         raise ValueError("bn_scale, bn_shift and bn_mean go together")
     shape = (b, cout) + tuple(out_size) if out_ncdhw else (b,) + tuple(out_size) + (cout,)
     y = torch.empty(shape, device=dev, dtype=_F32)
-    st = lib.mvs_conv3d_region_split_fwd(int(mode), _lib.MVS_CONV_OUT_NCDHW if out_ncdhw else 0, _lib.ptr(x),
+    xb = (_lib.ptr(x_bound.contiguous()) if mode == CONV_S2 else _bound_ptr(x_bound))
+    st = lib.mvs_conv3d_region_split_fwd(int(mode), flags, _lib.ptr(x),
                                          None if x2 is None else _lib.ptr(x2), _lib.ptr(frag), int(ew), _lib.ptr(y),
                                          b, cin, cout, _ints3(dims), _ints3(out_origin), _ints3(out_size),
-                                         _ints3(in_origin), _ints3(in_size), None if pad is None else _ints3(pad),
-                                         *[None if t is None else _lib.ptr(t) for t in bn], _bound_ptr(x_bound),
+                                         None if in_origin is None else _ints3(in_origin),
+                                         None if in_size is None else _ints3(in_size),
+                                         None if pad is None else _ints3(pad),
+                                         *[None if t is None else _lib.ptr(t) for t in bn], xb,
                                          _bound_ptr(x2_bound), _bound_ptr(y_bound), _lib.stream_handle(dev))
     _lib.check(st, "mvs_conv3d_region_split_fwd")
     return y

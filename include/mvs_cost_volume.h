@@ -474,8 +474,11 @@ int mvs_conv3d_region_split_weights(const float* weight, int c_in, int c_out, un
  * error.  Geometry, layouts, BN epilogue and flags (MVS_CONV_OUT_NCDHW) as
  * mvs_conv3d_region_fwd; in_origin / in_size required.  x_bound / x2_bound: the inputs' bound words
  * (DEVICE; NULL = unscaled, only when every |v| < 2^14 is known); y_bound: NULL or the output's bound
- * words (zeroed by the caller).  Supported (mode, c_in, c_out): S1 (16, 16), (32, 32), (64, 64), T2
- * (64, 32), (32, 16).  Eval-mode inference only. */
+ * words (zeroed by the caller).  MVS_CONV_S2 (conv_k_0): flags MVS_CONV_IN_C4 | MVS_CONV_IN_SPLIT, x the
+ * split cost volume (mvs_cost_volume_fwd_c4_split; its fp16 parts are the operands, no conversion) or,
+ * with in_origin / in_size, a box of it, x_bound its 8 bound words, x2 NULL.  Supported (mode, c_in,
+ * c_out): S1 (16, 16), (32, 32), (64, 64), T2 (64, 32), (32, 16), S2 (32, 16 | 32 | 64).  Inference
+ * only (the raw outputs without the BN pointers: train-mode BN's batch statistics). */
 int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float* x2, const void* weight_frag,
                                 int weight_exp, float* y, int batch, int c_in, int c_out, const int* dims,
                                 const int* out_origin, const int* out_size, const int* in_origin, const int* in_size,

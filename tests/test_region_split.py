@@ -154,3 +154,61 @@ def test_region_conv_raises_output_bound_words():
         torch.cuda.synchronize()
     words = bw[0].cpu().numpy().view(np.float32)
     assert words.max() == y.abs().max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cout", [16, 32, 64])
+def test_region_split_s2_reads_the_split_volume(cout):
+    """conv3d_region_split CONV_S2 (conv_k_0) straight from the split cost volume (its fp16 parts are
+    the operands) on forward_live's halo(C2) region: against float64 torch on the volume's fp32 values
+    (unsplit_cost_volume) within 1e-5 of the scale and 2x the fp32-MFMA kernel's error (conv3d_region
+    reading the same split volume), and with a box of the volume (in_origin / in_size) bit-equal to the
+    whole-volume read."""
+    from cameras import camera_batch, depth_range
+    from mvs_amd import ops
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _grow, _tconv_input_region
+    import torch.nn.functional as F
+    B, V, D, h, w = 2, 3, 24, 20, 26
+    n = (D, h, w)
+    pad, _ = pad_outpad(*n)
+    Bx = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
+    C2 = _tconv_input_region(Bx, n, pad)
+    out_reg = _grow(C2, n, 1)
+    org, size = [lo for lo, _ in out_reg], [hi - lo + 1 for lo, hi in out_reg]
+    K, R, T = camera_batch(B, V, h, w)
+    d_min, d_int = depth_range(B, d_int=200.0 / D)
+    g = torch.Generator().manual_seed(cout)
+    feat = torch.randn(B * V, 32, h, w, generator=g).to(DEV)
+    conv = torch.nn.Conv3d(32, cout, 3)
+    conv.weight.data = torch.randn(cout, 32, 3, 3, 3, generator=g) * 0.1
+    sc, sh, mu = _bn_params(cout, g)
+    bn = (sc.to(DEV), sh.to(DEV), mu.to(DEV))
+    w27 = ops.region_weight(conv).to(DEV)
+    with torch.no_grad():
+        scv, am = ops.cost_volume_c4_split(feat, K, R, T, d_min, d_int, B, V, 0, D, 25.0)
+        xv = ops.unsplit_cost_volume(scv, am)                      # [B, 8, D, h, w, 4] fp32 values
+        xv = xv.permute(0, 1, 5, 2, 3, 4).reshape(B, 32, *n).cpu()
+        bw = ops.bound_words(1, DEV)
+        y = ops.conv3d_region_split(scv, None, w27, ops.CONV_S2, list(n), org, size, None, None, list(pad), am, None,
+                                    bw[0], *bn)
+        y32 = ops.conv3d_region(scv, None, w27, ops.CONV_S2, list(n), org, size, None, None, list(pad), *bn,
+                                in_c4=True, absmax=am)
+        # the box of the volume the windows read (what the opt-in fused head stores)
+        lo = [max(2 * a - p, 0) for (a, _), p in zip(out_reg, pad)]
+        hi = [min(2 * b - p + 2, d - 1) + 1 for (_, b), p, d in zip(out_reg, pad, n)]
+        box = scv[:, :, lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]].contiguous()
+        yb = ops.conv3d_region_split(box, None, w27, ops.CONV_S2, list(n), org, size, lo,
+                                     [b - a for a, b in zip(lo, hi)], list(pad), am, None, None, *bn)
+        torch.cuda.synchronize()
+    sl = (slice(None), slice(None)) + tuple(slice(a, b + 1) for a, b in out_reg)
+    ref64 = _bn_relu(F.conv3d(xv.double(), conv.weight.double(), stride=2, padding=pad), sc.double(), sh.double(),
+                     mu.double())[sl]
+    yc, y32c = y.permute(0, 4, 1, 2, 3).cpu(), y32.permute(0, 4, 1, 2, 3).cpu()
+    scale = ref64.abs().max().item()
+    err = (yc.double() - ref64).abs().max().item()
+    err32 = (y32c.double() - ref64).abs().max().item()
+    assert err <= 1e-5 * scale, (err, scale)
+    assert err <= 2 * err32 + 1e-6 * scale, (err, err32)
+    assert bw[0].cpu().numpy().view(np.float32).max() == y.abs().max().item()
+    assert torch.equal(yb, y)
