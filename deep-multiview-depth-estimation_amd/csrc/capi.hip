@@ -660,7 +660,8 @@ int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float
                                 const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                                 const unsigned* x_bound, const unsigned* x2_bound, unsigned* y_bound, void* stream) {
   if (!x || !weight_frag || !y || !dims || !out_origin || !out_size || batch <= 0) return MVS_ERR_INVALID_ARGUMENT;
-  if (mode < MVS_CONV_S1 || mode > MVS_CONV_T2 || (flags & ~(MVS_CONV_OUT_NCDHW | MVS_CONV_IN_C4 | MVS_CONV_IN_SPLIT)))
+  if (mode < MVS_CONV_S1 || mode > MVS_CONV_T2 ||
+      (flags & ~(MVS_CONV_OUT_NCDHW | MVS_CONV_IN_C4 | MVS_CONV_IN_SPLIT | MVS_CONV_PER_LANE)))
     return MVS_ERR_INVALID_ARGUMENT;
   // S2 reads the split cost volume (its 8 bound words in x_bound), S1 / T2 an fp32 region tensor
   const bool s2 = mode == MVS_CONV_S2;
@@ -695,7 +696,8 @@ int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float
   const int st = mvs::launch_conv3d_region_split(
       mode, (flags & MVS_CONV_OUT_NCDHW) != 0, x, x2, weight_frag, weight_exp, y, batch, c_in, c_out, dims, out_origin,
       out_size, io, is, pad, bn_scale, bn_shift, bn_mean, reinterpret_cast<const uint32_t*>(x_bound),
-      reinterpret_cast<const uint32_t*>(x2_bound), reinterpret_cast<uint32_t*>(y_bound), (hipStream_t)stream);
+      reinterpret_cast<const uint32_t*>(x2_bound), reinterpret_cast<uint32_t*>(y_bound), (hipStream_t)stream,
+      (flags & MVS_CONV_PER_LANE) != 0);
   if (st != MVS_OK) return st;
   return lc.status();
 }

@@ -266,6 +266,175 @@ void launch_split_mode(const float* x, const float* x2, const void* wf, int w_ex
                      reinterpret_cast<const h8v*>(wf), w_exp, y, sc, sh, mu, g, xb, xb2, yb);
 }
 
+// ---- stride-1 convolutions with LDS-staged operands (conv_k_1; model.py:104-113) ----
+// The per-lane kernel above fetches every input voxel once per tap through L1 (27x): for the
+// 16-channel conv_1_1 that operand traffic, not the MFMA, sets its time.  Here a workgroup (4 waves)
+// owns a 16 (x) x 4 (y) x TZ (z) block of outputs; its input block, 18 x 6 x (TZ + 2) voxels with
+// all CI channels, is loaded once, split into fp16 hi / lo and stored in LDS (one record per voxel:
+// CI hi then CI lo values, 16-byte chunks XOR-swizzled by voxel so the 16 lanes of an MFMA row group,
+// 16 consecutive voxels, hit 16 distinct bank groups).  Wave w owns column block w % NB (16 output
+// channels) and 8 row blocks (16 x-voxels each, one (z, y) row of the tile): every weight fragment
+// (global / L2) feeds 8 row blocks, every A fragment comes from LDS.  Same products, same K order as
+// the per-lane kernel (taps, then channel blocks; tap pairs for CI = 16): bit-equal outputs.
+template <int CI>
+struct S1Tile {
+  static constexpr int TZ = CI == 16 ? 8 : (CI == 32 ? 4 : 2);
+  static constexpr int PX = 18, PY = 6, PZ = TZ + 2, PV = PX * PY * PZ;
+  static constexpr int REC = CI * 4;     // bytes per voxel record (CI hi + CI lo fp16)
+  static constexpr int NCH = REC / 16;   // 16-byte chunks per record: 4, 8, 16
+  static constexpr int LDS = PV * REC;   // 69,120 / 82,944 / 110,592 B
+};
+
+template <int CI>
+__device__ inline int s1_chunk_off(int v, int c) {
+  using T = S1Tile<CI>;
+  return v * T::REC + ((c ^ ((v / (16 / T::NCH)) % T::NCH)) << 4);
+}
+
+template <int CI, int CO>
+__global__ __launch_bounds__(kBlock) void conv3d_s1_split_lds_kernel(
+    const float* __restrict__ x, const h8v* __restrict__ wf, int w_exp, float* __restrict__ y,
+    const float* __restrict__ bn_scale, const float* __restrict__ bn_shift, const float* __restrict__ bn_mean,
+    GeoS g, int tiles_x, int tiles_y, int tiles_z, const uint32_t* __restrict__ xb, uint32_t* __restrict__ yb) {
+  using T = S1Tile<CI>;
+  constexpr int NB = CO / 16;
+  constexpr int RB = 8;                      // row blocks per wave: 4 y x TZ z rows / (4 / NB) row groups
+  static_assert(T::TZ * NB == RB && CI == CO, "tile shapes");
+  constexpr bool PAIR = CI == 16;
+  constexpr int CB = PAIR ? 1 : CI / 32;
+  constexpr int KB = PAIR ? 14 : 27 * CB;
+  __shared__ __attribute__((aligned(16))) char lds[T::LDS];
+
+  int t = xcd_work_id((int)blockIdx.x, (int)gridDim.x);
+  if (t >= tiles_x * tiles_y * tiles_z) return;   // workgroup-uniform, before the barrier
+  const int tx0 = (t % tiles_x) * 16;
+  t /= tiles_x;
+  const int ty0 = (t % tiles_y) * 4;
+  t /= tiles_y;
+  const int tz0 = t * T::TZ;
+  const int b = (int)blockIdx.y;
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m = lane & 15, kq = lane >> 4;
+  const int ex = act_split_exponent(bound_read(xb));
+
+  // ---- stage the input block: items (voxel, channel quad), quad fastest (coalesced channels-last
+  // loads); voxels outside the input region are zeros (the convolution's zero padding) ----
+  {
+    constexpr int NQ = CI / 4, NIT = T::PV * NQ, PER = (NIT + kBlock - 1) / kBlock;
+    const size_t rvol = (size_t)g.in[0] * g.in[1] * g.in[2];
+    const Rsrc rs = make_rsrc(x + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
+    constexpr int BATCH = 8;
+#pragma unroll
+    for (int k0 = 0; k0 < PER; k0 += BATCH) {
+      f4v v4[BATCH];
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int e = tid + kBlock * (k0 + k);
+        const int q = e % NQ, v = e / NQ;
+        const int px = v % T::PX, py = (v / T::PX) % T::PY, pz = v / (T::PX * T::PY);
+        const int rx = g.o0[2] + tx0 - 1 + px - g.i0[2], ry = g.o0[1] + ty0 - 1 + py - g.i0[1],
+                  rz = g.o0[0] + tz0 - 1 + pz - g.i0[0];
+        const bool ok = k0 + k < PER && e < NIT && rx >= 0 && rx < g.in[2] && ry >= 0 && ry < g.in[1] && rz >= 0 &&
+                        rz < g.in[0];
+        const uint32_t off = ok ? (uint32_t)((((size_t)rz * g.in[1] + ry) * g.in[2] + rx) * CI + 4 * q) * 4u : kOob;
+        v4[k] = ld4(rs, off, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int e = tid + kBlock * (k0 + k);
+        if (k0 + k >= PER || e >= NIT) continue;
+        const int q = e % NQ, v = e / NQ;
+        uint2 hi, lo;
+        split4(v4[k], ex, hi, lo);
+        *reinterpret_cast<uint2*>(lds + s1_chunk_off<CI>(v, q >> 1) + ((q & 1) << 3)) = hi;
+        *reinterpret_cast<uint2*>(lds + s1_chunk_off<CI>(v, CI / 8 + (q >> 1)) + ((q & 1) << 3)) = lo;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- this wave: column block nb, row blocks rg * 8 .. + 7 of the tile's 4 TZ (z, y) rows ----
+  const int nb = wave % NB, rg = wave / NB;
+  f4v acc[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) acc[r] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+  // weight fragments (L2) one K block ahead: kb + 1's loads are in flight under kb's MFMAs
+  auto ldb = [&](int kb, h8v& bhi, h8v& blo) {
+    bhi = wf[((size_t)(kb * NB + nb) * 2 + 0) * 64 + lane];
+    blo = wf[((size_t)(kb * NB + nb) * 2 + 1) * 64 + lane];
+  };
+  auto kstep = [&](int kb, const h8v& bhi, const h8v& blo) {
+    int tap, c0;
+    if constexpr (PAIR) {
+      tap = 2 * kb + (kq >> 1);
+      c0 = kq & 1;
+    } else {
+      tap = kb / CB;
+      c0 = (kb % CB) * 4 + kq;
+    }
+    const int tz = tap / 9, ty = (tap / 3) % 3, tx = tap % 3;
+    const bool tap_ok = !PAIR || tap < 27;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int rbi = rg * RB + r, zz = rbi >> 2, yy = rbi & 3;
+      const int v = ((zz + tz) * T::PY + (yy + ty)) * T::PX + (m + tx);
+      h8v ahi = *reinterpret_cast<const h8v*>(lds + s1_chunk_off<CI>(v, c0));
+      h8v alo = *reinterpret_cast<const h8v*>(lds + s1_chunk_off<CI>(v, CI / 8 + c0));
+      if (!tap_ok) ahi = alo = h8v{0, 0, 0, 0, 0, 0, 0, 0};
+      acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bhi, acc[r], 0, 0, 0);
+      acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, blo, acc[r], 0, 0, 0);
+      acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bhi, acc[r], 0, 0, 0);
+    }
+  };
+  h8v bh0, bl0, bh1, bl1;
+  ldb(0, bh0, bl0);
+#pragma unroll 1
+  for (int kb = 0; kb < KB; kb += 2) {
+    if (kb + 1 < KB) ldb(kb + 1, bh1, bl1);
+    kstep(kb, bh0, bl0);
+    if (kb + 1 < KB) {
+      if (kb + 2 < KB) ldb(kb + 2, bh0, bl0);
+      kstep(kb + 1, bh1, bl1);
+    }
+  }
+
+  // ---- epilogue: acc[r][i] = (x = 4 kq + i, channel nb * 16 + m) of row block r ----
+  const int oexp = -(ex + w_exp);
+  const int co = nb * 16 + m;
+  const float sc = bn_scale ? bn_scale[co] : 1.0f, sh = bn_scale ? bn_shift[co] : 0.0f,
+              mu = bn_scale ? bn_mean[co] : 0.0f;
+  const size_t orvol = (size_t)g.on[0] * g.on[1] * g.on[2];
+  float vmax = 0.0f;
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const int rbi = rg * RB + r, zz = rbi >> 2, yy = rbi & 3;
+    const int vz = tz0 + zz, vy = ty0 + yy;
+    if (vz >= g.on[0] || vy >= g.on[1]) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int vx = tx0 + 4 * kq + i;
+      if (vx >= g.on[2]) continue;
+      float v = ldexpf(acc[r][i], oexp);
+      if (bn_scale) v = fmaxf((v - mu) * sc + sh, 0.0f);
+      vmax = fmaxf(vmax, fabsf(v));
+      const size_t vox = ((size_t)vz * g.on[1] + vy) * g.on[2] + vx;
+      if (g.out_cf) y[((size_t)b * CO + co) * orvol + vox] = v;
+      else y[((size_t)b * orvol + vox) * CO + co] = v;
+    }
+  }
+  if (yb) bound_update(yb, vmax);
+}
+
+template <int CI>
+void launch_s1_lds(const float* x, const void* wf, int w_exp, float* y, const float* sc, const float* sh,
+                   const float* mu, int B, const GeoS& g, const uint32_t* xb, uint32_t* yb, hipStream_t s) {
+  const int tx = (g.on[2] + 15) / 16, ty = (g.on[1] + 3) / 4, tz = (g.on[0] + S1Tile<CI>::TZ - 1) / S1Tile<CI>::TZ;
+  const int per = tx * ty * tz;
+  const dim3 grid((unsigned)((per + 7) / 8 * 8), (unsigned)B);
+  hipLaunchKernelGGL((conv3d_s1_split_lds_kernel<CI, CI>), grid, dim3(kBlock), 0, s, x,
+                     reinterpret_cast<const h8v*>(wf), w_exp, y, sc, sh, mu, g, tx, ty, tz, xb, yb);
+}
+
 }  // namespace
 
 int conv3d_region_split_kblocks(int c_in) { return c_in == 16 ? 14 : 27 * (c_in / 32); }
@@ -274,7 +443,7 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
                                float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on,
                                const int* i0, const int* in, const int* pad, const float* bn_scale,
                                const float* bn_shift, const float* bn_mean, const uint32_t* x_bound,
-                               const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s) {
+                               const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s, bool per_lane) {
   GeoS g;
   g.out_cf = out_cf ? 1 : 0;
   for (int d = 0; d < 3; ++d) {
@@ -285,14 +454,32 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
     g.in[d] = in[d];
     g.pad[d] = pad ? pad[d] : 1;
   }
+// row blocks per wave: 4 for the stride-1 convs (each weight fragment feeds 4 row blocks), 2 for the
+// transposed and stride-2 ones (measured at cfg 2, eval and train mode: S1 64 -> 64 2.70 -> 2.41 ms,
+// T2 32 -> 16 2.02 against 2.36 with 4; 1 row block is slower everywhere)
 #define MVS_RSPLIT_CASE(MD, A, C)                                                                         \
   if (mode == MD && CI == A && CO == C) {                                                                 \
-    launch_split_mode<MD, A, C, 2>(x, x2, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound,  \
-                                   x2_bound, y_bound, s);                                                 \
+    launch_split_mode<MD, A, C, MD == kS1 ? 4 : 2>(x, x2, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, \
+                                                   x_bound, x2_bound, y_bound, s);                        \
     return MVS_OK;                                                                                        \
   }
-  // S1: conv_k_1 (16 / 32 / 64 channels); T2: deconv_3_0 (64 -> 32), deconv_2_0 (32 -> 16); S2: conv_k_0
-  // from the split cost volume (32 -> 16 / 32 / 64)
+  // S1: conv_k_1 (16 / 32 / 64 channels; LDS-staged operands per MVS_S1_LDS); T2: deconv_3_0 (64 -> 32),
+  // deconv_2_0 (32 -> 16); S2: conv_k_0 from the split cost volume (32 -> 16 / 32 / 64)
+// bit 0 / 1 / 2: the LDS-staged kernel for 16 / 32 / 64 channels.  Measured per cfg-2 step (eval /
+// train mode): 16 ch 0.37 -> 0.27 / 0.35 -> 0.26 ms, 32 ch 0.18 -> 0.17 / 0.97 -> 0.93 ms; 64 ch slower
+// (0.11 -> 0.13 / 2.41 -> 2.81 ms: its 110 KB tile allows one workgroup per CU).  An LDS-staged
+// transposed kernel (one 17 x 5 x (TZ + 1) block per parity-class tile) measured no gain (0.31 ->
+// 0.34 ms): a class reads each input voxel through 1-8 taps only.
+#ifndef MVS_S1_LDS
+#define MVS_S1_LDS 3
+#endif
+  const int ci_bit = CI == 16 ? 1 : (CI == 32 ? 2 : (CI == 64 ? 4 : 0));
+  if ((MVS_S1_LDS & ci_bit) && !per_lane && mode == kS1 && CI == CO && !x2) {
+    if (CI == 16) launch_s1_lds<16>(x, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, y_bound, s);
+    else if (CI == 32) launch_s1_lds<32>(x, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, y_bound, s);
+    else launch_s1_lds<64>(x, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, y_bound, s);
+    return MVS_OK;
+  }
   MVS_RSPLIT_CASE(kS1, 16, 16) MVS_RSPLIT_CASE(kS1, 32, 32) MVS_RSPLIT_CASE(kS1, 64, 64)
   MVS_RSPLIT_CASE(kS2, 32, 16) MVS_RSPLIT_CASE(kS2, 32, 32) MVS_RSPLIT_CASE(kS2, 32, 64)
   MVS_RSPLIT_CASE(kT2, 64, 32) MVS_RSPLIT_CASE(kT2, 32, 16)

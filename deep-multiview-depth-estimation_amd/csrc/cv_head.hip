@@ -55,6 +55,16 @@ constexpr int kPartB = kHY * kRowB;                      // 6,912 B
 constexpr int kSlotB = 2 * kPartB;                       // hi + lo: 13,824 B per plane
 constexpr int kRing = 6;                                 // 4 planes read + 2 being written
 constexpr int kRingB = kRing * kSlotB;                   // 82,944 B
+// PRESPLIT: the producers run AHEAD batches ahead of the step they fill for (2 more slots each), so
+// a slow load batch does not stall the consumers at the next barrier
+#ifndef MVS_HEAD_PRE_AHEAD
+#define MVS_HEAD_PRE_AHEAD 1
+#endif
+constexpr int kPreAhead = MVS_HEAD_PRE_AHEAD;
+template <bool PRE>
+constexpr int ring_slots() {
+  return PRE ? kRing + 2 * kPreAhead : kRing;
+}
 constexpr int kW1B = 27 * 2 * 64 * 16;                   // conv_1_0 fragments: 55,296 B
 constexpr int kScrB = 2 * 3 * 64 * 16;                   // conv_1_0 partials, double buffered
 #ifndef MVS_HEAD_ZC
@@ -91,7 +101,7 @@ constexpr int w1_lds_bytes() {   // PRE: the conv_1_0 product waves hold their f
 }
 template <int NS, bool PRE = false>
 constexpr int lds_bytes() {
-  return kRingB + w1_lds_bytes<PRE>() + coord_bytes<NS, PRE>() + kScrB;
+  return ring_slots<PRE>() * kSlotB + w1_lds_bytes<PRE>() + coord_bytes<NS, PRE>() + kScrB;
 }
 
 struct HeadArgs {
@@ -137,8 +147,9 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   constexpr int NS = V - 1;
   __shared__ __attribute__((aligned(16))) char lds[lds_bytes<NS, PRE>()];
   char* const ring = lds;
-  char* const w1l = lds + kRingB;
-  char* const coord = lds + kRingB + w1_lds_bytes<PRE>();
+  constexpr int RS = ring_slots<PRE>();
+  char* const w1l = lds + RS * kSlotB;
+  char* const coord = lds + RS * kSlotB + w1_lds_bytes<PRE>();
   char* const scr = coord + coord_bytes<NS, PRE>();
 
   const int wk = xcd_work_id((int)blockIdx.x, (int)gridDim.x);
@@ -185,7 +196,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     }
   }
   // ring slot of plane p (batch j = (p - z0 + 1) / 2 lives in slots 2j, 2j + 1 mod kRing)
-  auto slot_of = [&](int p) { return (p - z0 + 1) % kRing; };
+  auto slot_of = [&](int p) { return (p - z0 + 1) % RS; };
 
   // ================================ producer state ================================
   const int ptid = tid - 256, pw = wave - 4;
@@ -599,8 +610,10 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
   // Both roles pass the same barriers (nsteps + 3): producers fill batches 0, 1 before step 0 and batch
   // k + 2 during step k; the sampling state of a batch is formed at least one barrier before its items.
   if (!consumer && PRE) {
-    // batches 0, 1 before the first step; batch k + 2 stored during step k, its loads issued kPD
-    // steps earlier (buffer (k + 2) % kPD: the step loop unrolled by kPD keeps the index static)
+    // batches 0 .. 1 + kPreAhead before the first step; batch k + 2 + kPreAhead stored during step k
+    // (its slots were last read in step k - 1), its loads issued kPD steps earlier (buffer j % kPD:
+    // the step loop unrolled by kPD keeps the index static)
+    constexpr int A = kPreAhead;
     stamp();
     pre_load(0, 0);
     load_bw1();
@@ -609,11 +622,15 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     __syncthreads();
     stamp();
     pre_store(0, 0);
-    pre_load(1, 0);
-    pre_store(1, 0);
+#pragma unroll
+    for (int j = 1; j <= 1 + A; ++j) {
+      if (j >= nbatch) break;   // uniform
+      pre_load(j, 0);
+      pre_store(j, 0);
+    }
 #pragma unroll
     for (int r = 0; r < kPD; ++r)
-      if (2 + r < nbatch) pre_load(2 + r, (2 + r) % kPD);
+      if (2 + A + r < nbatch) pre_load(2 + A + r, (2 + A + r) % kPD);
     stamp();
     __syncthreads();
     stamp();
@@ -625,8 +642,8 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       for (int r = 0; r < kPD; ++r) {
         const int k = k0 + r;
         if (k >= nsteps) break;   // uniform
-        if (k + 2 < nbatch) pre_store(k + 2, (r + 2) % kPD);
-        if (k + 2 + kPD < nbatch) pre_load(k + 2 + kPD, (r + 2) % kPD);
+        if (k + 2 + A < nbatch) pre_store(k + 2 + A, (r + 2 + A) % kPD);
+        if (k + 2 + A + kPD < nbatch) pre_load(k + 2 + A + kPD, (r + 2 + A) % kPD);
         stamp();
         conv1_step(k);
         stamp();
@@ -747,7 +764,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       }
       const char* base[4];
 #pragma unroll
-      for (int p = 0; p < 4; ++p) base[p] = ring + ((2 * k + p) % kRing) * kSlotB;
+      for (int p = 0; p < 4; ++p) base[p] = ring + ((2 * k + p) % RS) * kSlotB;
       constexpr int kIt = 9 * 4;
       auto lda = [&](int it, h8v& hi, h8v& lo) {
         const int grp = it / 4, p = it % 4, ky = grp / 3, kx = grp % 3;

@@ -25,6 +25,7 @@ MVS_BWD_DETERMINISTIC = 1
 MVS_LAYOUT_CHANNELS_LAST = 1
 MVS_CONV_S1, MVS_CONV_S2, MVS_CONV_T2 = 0, 1, 2
 MVS_CONV_OUT_NCDHW = 1
+MVS_CONV_PER_LANE = 32
 MVS_CONV_IN_C4 = 2
 MVS_CONV_WINO_Z = 4
 MVS_CONV_IN_BF16 = 8

@@ -1083,7 +1083,8 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
                         in_size: Optional[list[int]], pad: Optional[list[int]], x_bound: Optional[torch.Tensor],
                         x2_bound: Optional[torch.Tensor], y_bound: Optional[torch.Tensor],
                         bn_scale: Optional[torch.Tensor] = None, bn_shift: Optional[torch.Tensor] = None,
-                        bn_mean: Optional[torch.Tensor] = None, out_ncdhw: bool = False) -> torch.Tensor:
+                        bn_mean: Optional[torch.Tensor] = None, out_ncdhw: bool = False,
+                        per_lane: bool = False) -> torch.Tensor:
     """conv3d_region's CONV_S1 / CONV_T2 convolutions on the f16 matrix cores with split operands
     (mvs_conv3d_region_split_fwd, csrc/conv3d_region_split.hip): same geometry, layouts and epilogue;
     the input scaled by its bound words ``x_bound`` (+ ``x2_bound`` for the sum x + x2), ``y_bound``
@@ -1092,7 +1093,7 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
     (DESIGN.md §3.8).  Inference only."""
     _require_gpu(x, "x")
     lib = _lib.load()
-    flags = _lib.MVS_CONV_OUT_NCDHW if out_ncdhw else 0
+    flags = (_lib.MVS_CONV_OUT_NCDHW if out_ncdhw else 0) | (_lib.MVS_CONV_PER_LANE if per_lane else 0)
     if mode == CONV_S2:
         if x.dtype != torch.int32 or x.dim() != 6 or x_bound is None or x_bound.numel() != 8:
             raise ValueError("CONV_S2: the split cost volume [B, 8, D, H, W, 4] int32 and its 8 bound words")
@@ -1126,7 +1127,7 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
 
 @conv3d_region_split.register_fake
 def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, x_bound, x2_bound, y_bound,
-      bn_scale=None, bn_shift=None, bn_mean=None, out_ncdhw=False):
+      bn_scale=None, bn_shift=None, bn_mean=None, out_ncdhw=False, per_lane=False):
     if out_ncdhw:
         return x.new_empty((x.shape[0], weight.shape[1]) + tuple(out_size), dtype=_F32)
     return x.new_empty((x.shape[0],) + tuple(out_size) + (weight.shape[1],), dtype=_F32)

@@ -451,6 +451,10 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
                           const int* pad, const float* bn_scale, const float* bn_shift,
                           const float* bn_mean, const unsigned* x_absmax, unsigned* y_bound, void* stream);
 
+/* flag of mvs_conv3d_region_split_fwd: run the per-lane-operand kernel even where the LDS-staged
+ * stride-1 kernel applies (the two are bit-identical; tests and A/B timing) */
+#define MVS_CONV_PER_LANE 32
+
 /* Bound words of a region tensor: MVS_BOUND_WORDS uint32 holding maxima of |v| as fp32 bit patterns
  * (the tensor's bound is their maximum), raised with atomic maxima by the kernel that writes the tensor
  * into words the caller zeroed. */

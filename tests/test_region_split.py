@@ -212,3 +212,37 @@ def test_region_split_s2_reads_the_split_volume(cout):
     assert err <= 2 * err32 + 1e-6 * scale, (err, err32)
     assert bw[0].cpu().numpy().view(np.float32).max() == y.abs().max().item()
     assert torch.equal(yb, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,ncdhw,shape", [(16, False, (24, 20, 26)), (16, True, (13, 11, 37)), (32, False, (24, 20, 26)),
+                                           (32, False, (9, 7, 17)), (32, True, (11, 5, 50))])
+def test_region_split_s1_lds_equals_per_lane(c, ncdhw, shape):
+    """The LDS-staged stride-1 kernel (the default for the 16- and 32-channel conv_k_1) is bit-identical to the per-lane-operand
+    kernel (MVS_CONV_PER_LANE) -- same products in the same order -- on regions that are not multiples
+    of its 16 x 4 x TZ tile, with and without BN, and raises the same bound words."""
+    from mvs_amd.model import _grow, _tconv_input_region
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.ops import CONV_S1, bound_words, conv3d_region_split, region_weight
+    n = shape
+    pad, _ = pad_outpad(*n)
+    Bx = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
+    out_reg, in_reg = Bx, _grow(Bx, n, 1)
+    org = lambda r: [lo for lo, _ in r]
+    size = lambda r: [hi - lo + 1 for lo, hi in r]
+    g = torch.Generator().manual_seed(c + sum(n))
+    x = (torch.relu(torch.randn(2, *size(in_reg), c, generator=g)) * 3).to(DEV)
+    conv = torch.nn.Conv3d(c, c, 3)
+    conv.weight.data = torch.randn(c, c, 3, 3, 3, generator=g) * 0.1
+    w27 = region_weight(conv).to(DEV)
+    bw = bound_words(3, DEV)
+    bw[0, 7] = torch.tensor([x.abs().max().item()], dtype=torch.float32).view(torch.int32).item()
+    args = (CONV_S1, list(n), org(out_reg), size(out_reg), org(in_reg), size(in_reg), None)
+    for bn in ((None, None, None), tuple(t.to(DEV) for t in _bn_params(c, g))):
+        bw[1:].zero_()
+        with torch.no_grad():
+            a = conv3d_region_split(x, None, w27, *args, bw[0], None, bw[1], *bn, out_ncdhw=ncdhw)
+            b = conv3d_region_split(x, None, w27, *args, bw[0], None, bw[2], *bn, out_ncdhw=ncdhw, per_lane=True)
+            torch.cuda.synchronize()
+        assert torch.equal(a, b), (a - b).abs().max().item()
+        assert bw[1].max().item() == bw[2].max().item()
