@@ -658,7 +658,8 @@ int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float
                                 int weight_exp, float* y, int batch, int c_in, int c_out, const int* dims,
                                 const int* out_origin, const int* out_size, const int* in_origin, const int* in_size,
                                 const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                                const unsigned* x_bound, const unsigned* x2_bound, unsigned* y_bound, void* stream) {
+                                const unsigned* x_bound, const unsigned* x2_bound, unsigned* y_bound,
+                                const float* y_addend, void* stream) {
   if (!x || !weight_frag || !y || !dims || !out_origin || !out_size || batch <= 0) return MVS_ERR_INVALID_ARGUMENT;
   if (mode < MVS_CONV_S1 || mode > MVS_CONV_T2 ||
       (flags & ~(MVS_CONV_OUT_NCDHW | MVS_CONV_IN_C4 | MVS_CONV_IN_SPLIT | MVS_CONV_PER_LANE)))
@@ -697,7 +698,7 @@ int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float
       mode, (flags & MVS_CONV_OUT_NCDHW) != 0, x, x2, weight_frag, weight_exp, y, batch, c_in, c_out, dims, out_origin,
       out_size, io, is, pad, bn_scale, bn_shift, bn_mean, reinterpret_cast<const uint32_t*>(x_bound),
       reinterpret_cast<const uint32_t*>(x2_bound), reinterpret_cast<uint32_t*>(y_bound), (hipStream_t)stream,
-      (flags & MVS_CONV_PER_LANE) != 0);
+      (flags & MVS_CONV_PER_LANE) != 0, y_addend);
   if (st != MVS_OK) return st;
   return lc.status();
 }

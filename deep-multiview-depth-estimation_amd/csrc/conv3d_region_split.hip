@@ -42,6 +42,7 @@ struct GeoS {
   int in[3];   // input region size
   int pad[3];  // T2: P
   int out_cf;  // 1: output channels-first
+  const float* addend;   // nullable: added to the output after BN + ReLU (same layout as y)
 };
 
 __device__ inline void class_dim_s(int o0, int on, int p, int par, int& first, int& cnt) {
@@ -242,10 +243,11 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_split_kernel(
                   vxx = cf[2] + step * jx - g.o0[2];
         float v = ldexpf(acc[rb][nb][r], oexp);
         if (bn_scale) v = fmaxf((v - mu) * sc + sh, 0.0f);
-        vmax = fmaxf(vmax, fabsf(v));
         const size_t vox = ((size_t)vz * g.on[1] + vy) * g.on[2] + vxx;
-        if (g.out_cf) y[((size_t)b * CO + co) * orvol + vox] = v;
-        else y[((size_t)b * orvol + vox) * CO + co] = v;
+        const size_t oi = g.out_cf ? ((size_t)b * CO + co) * orvol + vox : ((size_t)b * orvol + vox) * CO + co;
+        if (g.addend) v += g.addend[oi];
+        vmax = fmaxf(vmax, fabsf(v));
+        y[oi] = v;
       }
   }
   if (yb) bound_update(yb, vmax);
@@ -416,10 +418,11 @@ __global__ __launch_bounds__(kBlock) void conv3d_s1_split_lds_kernel(
       if (vx >= g.on[2]) continue;
       float v = ldexpf(acc[r][i], oexp);
       if (bn_scale) v = fmaxf((v - mu) * sc + sh, 0.0f);
-      vmax = fmaxf(vmax, fabsf(v));
       const size_t vox = ((size_t)vz * g.on[1] + vy) * g.on[2] + vx;
-      if (g.out_cf) y[((size_t)b * CO + co) * orvol + vox] = v;
-      else y[((size_t)b * orvol + vox) * CO + co] = v;
+      const size_t oi = g.out_cf ? ((size_t)b * CO + co) * orvol + vox : ((size_t)b * orvol + vox) * CO + co;
+      if (g.addend) v += g.addend[oi];
+      vmax = fmaxf(vmax, fabsf(v));
+      y[oi] = v;
     }
   }
   if (yb) bound_update(yb, vmax);
@@ -443,9 +446,11 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
                                float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on,
                                const int* i0, const int* in, const int* pad, const float* bn_scale,
                                const float* bn_shift, const float* bn_mean, const uint32_t* x_bound,
-                               const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s, bool per_lane) {
+                               const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s, bool per_lane,
+                               const float* y_addend) {
   GeoS g;
   g.out_cf = out_cf ? 1 : 0;
+  g.addend = y_addend;
   for (int d = 0; d < 3; ++d) {
     g.n[d] = n[d];
     g.o0[d] = o0[d];

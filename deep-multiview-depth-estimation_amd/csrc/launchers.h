@@ -135,7 +135,8 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
                                float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on,
                                const int* i0, const int* in, const int* pad, const float* bn_scale,
                                const float* bn_shift, const float* bn_mean, const uint32_t* x_bound,
-                               const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s, bool per_lane = false);
+                               const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s, bool per_lane = false,
+                               const float* y_addend = nullptr);
 
 // channel_ops.hip: train-mode BatchNorm pieces -- per-channel float64 sums into
 // stats[slot][2][C] (64 slots) and y = relu(BN(x)) [+ relu(BN'(r))], channels-last or NCDHW

@@ -388,10 +388,11 @@ class CostVolumeReg(nn.Module):
         y2 = level(1, self.conv_2_0, self.conv_2_1, self.BN_2, C2)
         y3 = level(2, self.conv_3_0, self.conv_3_1, self.BN_3, C3)
         if bw is not None:
-            y3 = conv3d_region_split(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, org(C2), size(C2),
-                                     org(C3), size(C3), pad, bw[5], None, bw[6], *bn_eval(self.BN_2))
-            y2 = conv3d_region_split(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, org(B), size(B),
-                                     org(C2), size(C2), pad, bw[6], bw[4], None, *bn_eval(self.BN_1), out_ncdhw=True)
+            # deconv_3_0 + BN_2 + ReLU, then `+ y2` (model.py:119) in its epilogue: deconv_2_0 reads one tensor
+            y32 = conv3d_region_split(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, org(C2), size(C2),
+                                      org(C3), size(C3), pad, bw[5], None, bw[6], *bn_eval(self.BN_2), y_addend=y2)
+            y2 = conv3d_region_split(y32, None, region_weight(self.deconv_2_0), CONV_T2, dims, org(B), size(B),
+                                     org(C2), size(C2), pad, bw[6], None, None, *bn_eval(self.BN_1), out_ncdhw=True)
         else:
             y3 = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, org(C2), size(C2),
                                org(C3), size(C3), pad, *bn_eval(self.BN_2))
@@ -530,12 +531,18 @@ class CostVolumeReg(nn.Module):
             z = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
                               size(M), pad)
         p = _bn_train(self.BN_2, *channel_stats(z, True), count)
-        y3 = bn_relu_(_crop_cl(z, full, M), True, *p, y_bound=bwr(6))
-        del z
         if bw is not None:
-            z = conv3d_region_split(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, [0, 0, 0], dims,
-                                    org(M), size(M), pad, bw[6], bw[4], None, out_ncdhw=True)
+            # relu(BN_2(deconv_3_0)) + y2 (model.py:119) formed in the BN pass: y2 >= 0 (a ReLU output), so
+            # relu((y2 - 0) * 1 + 0) is y2 exactly; deconv_2_0 then reads one tensor
+            c2 = y2.shape[-1]
+            one, zero = torch.ones(c2, device=y2.device), torch.zeros(c2, device=y2.device)
+            y3 = bn_relu_(_crop_cl(z, full, M), True, *p, r=y2, r_bn=(one, zero, zero), y_bound=bw[6])
+            del z
+            z = conv3d_region_split(y3, None, region_weight(self.deconv_2_0), CONV_T2, dims, [0, 0, 0], dims,
+                                    org(M), size(M), pad, bw[6], None, None, out_ncdhw=True)
         else:
+            y3 = bn_relu_(_crop_cl(z, full, M), True, *p)
+            del z
             z = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
                               size(M), pad, out_ncdhw=True)
         p = _bn_train(self.BN_1, *channel_stats(z, False), count)

@@ -1084,11 +1084,12 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
                         x2_bound: Optional[torch.Tensor], y_bound: Optional[torch.Tensor],
                         bn_scale: Optional[torch.Tensor] = None, bn_shift: Optional[torch.Tensor] = None,
                         bn_mean: Optional[torch.Tensor] = None, out_ncdhw: bool = False,
-                        per_lane: bool = False) -> torch.Tensor:
+                        per_lane: bool = False, y_addend: Optional[torch.Tensor] = None) -> torch.Tensor:
     """conv3d_region's CONV_S1 / CONV_T2 convolutions on the f16 matrix cores with split operands
     (mvs_conv3d_region_split_fwd, csrc/conv3d_region_split.hip): same geometry, layouts and epilogue;
     the input scaled by its bound words ``x_bound`` (+ ``x2_bound`` for the sum x + x2), ``y_bound``
-    (zeroed words or None) raised to max|y|.  CONV_S2: x is the split cost volume (int32 [B, 8, D, H, W,
+    (zeroed words or None) raised to max|y|.  ``y_addend``: added to the output after BN + ReLU (same
+    shape and layout as y).  CONV_S2: x is the split cost volume (int32 [B, 8, D, H, W,
     4], or a box of it with in_origin / in_size), x_bound its 8 bound words.  fp32-level error
     (DESIGN.md §3.8).  Inference only."""
     _require_gpu(x, "x")
@@ -1113,6 +1114,11 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
     shape = (b, cout) + tuple(out_size) if out_ncdhw else (b,) + tuple(out_size) + (cout,)
     y = torch.empty(shape, device=dev, dtype=_F32)
     xb = (_lib.ptr(x_bound.contiguous()) if mode == CONV_S2 else _bound_ptr(x_bound))
+    ya = None
+    if y_addend is not None:
+        if tuple(y_addend.shape) != tuple(y.shape) or y_addend.dtype != _F32 or not y_addend.is_contiguous():
+            raise ValueError("y_addend: a contiguous fp32 tensor of the output's shape")
+        ya = _lib.ptr(y_addend)
     st = lib.mvs_conv3d_region_split_fwd(int(mode), flags, _lib.ptr(x),
                                          None if x2 is None else _lib.ptr(x2), _lib.ptr(frag), int(ew), _lib.ptr(y),
                                          b, cin, cout, _ints3(dims), _ints3(out_origin), _ints3(out_size),
@@ -1120,14 +1126,14 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
                                          None if in_size is None else _ints3(in_size),
                                          None if pad is None else _ints3(pad),
                                          *[None if t is None else _lib.ptr(t) for t in bn], xb,
-                                         _bound_ptr(x2_bound), _bound_ptr(y_bound), _lib.stream_handle(dev))
+                                         _bound_ptr(x2_bound), _bound_ptr(y_bound), ya, _lib.stream_handle(dev))
     _lib.check(st, "mvs_conv3d_region_split_fwd")
     return y
 
 
 @conv3d_region_split.register_fake
 def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, x_bound, x2_bound, y_bound,
-      bn_scale=None, bn_shift=None, bn_mean=None, out_ncdhw=False, per_lane=False):
+      bn_scale=None, bn_shift=None, bn_mean=None, out_ncdhw=False, per_lane=False, y_addend=None):
     if out_ncdhw:
         return x.new_empty((x.shape[0], weight.shape[1]) + tuple(out_size), dtype=_F32)
     return x.new_empty((x.shape[0],) + tuple(out_size) + (weight.shape[1],), dtype=_F32)

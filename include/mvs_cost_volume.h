@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 14
+#define MVS_ABI_VERSION 15
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -482,12 +482,15 @@ int mvs_conv3d_region_split_weights(const float* weight, int c_in, int c_out, un
  * split cost volume (mvs_cost_volume_fwd_c4_split; its fp16 parts are the operands, no conversion) or,
  * with in_origin / in_size, a box of it, x_bound its 8 bound words, x2 NULL.  Supported (mode, c_in,
  * c_out): S1 (16, 16), (32, 32), (64, 64), T2 (64, 32), (32, 16), S2 (32, 16 | 32 | 64).  Inference
- * only (the raw outputs without the BN pointers: train-mode BN's batch statistics). */
+ * only (the raw outputs without the BN pointers: train-mode BN's batch statistics).  y_addend: NULL, or a
+ * tensor of y's shape and layout added after BN + ReLU (deconv_3_0's output + y2, model.py:119, formed
+ * once instead of on every load of deconv_2_0); the bound words then bound the sum. */
 int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float* x2, const void* weight_frag,
                                 int weight_exp, float* y, int batch, int c_in, int c_out, const int* dims,
                                 const int* out_origin, const int* out_size, const int* in_origin, const int* in_size,
                                 const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                                const unsigned* x_bound, const unsigned* x2_bound, unsigned* y_bound, void* stream);
+                                const unsigned* x_bound, const unsigned* x2_bound, unsigned* y_bound,
+                                const float* y_addend, void* stream);
 
 /* Softmax over the depth planes of the regulariser's output (CostVolumeReg.Norm = nn.Softmax(2),
  * model.py:97 / :125): y[b][0][d][p] = exp(x - max_d x) / sum_d exp(x - max_d x) per pixel p, in

@@ -246,3 +246,34 @@ def test_region_split_s1_lds_equals_per_lane(c, ncdhw, shape):
             torch.cuda.synchronize()
         assert torch.equal(a, b), (a - b).abs().max().item()
         assert bw[1].max().item() == bw[2].max().item()
+
+
+@pytest.mark.gpu
+def test_region_split_output_addend():
+    """y_addend (deconv_3_0's `+ y2`, model.py:119, formed in its epilogue) adds after BN + ReLU: bit-equal
+    to the output plus the addend, and the bound words bound the sum."""
+    from mvs_amd.model import _tconv_input_region
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.ops import CONV_T2, bound_words, conv3d_region_split, region_weight
+    n = (24, 20, 26)
+    pad, _ = pad_outpad(*n)
+    Bx = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
+    C2 = _tconv_input_region(Bx, n, pad)
+    org = lambda r: [lo for lo, _ in r]
+    size = lambda r: [hi - lo + 1 for lo, hi in r]
+    g = torch.Generator().manual_seed(21)
+    x = torch.relu(torch.randn(2, *size(C2), 64, generator=g)).to(DEV)
+    conv = torch.nn.ConvTranspose3d(64, 32, 3)
+    conv.weight.data = torch.randn(64, 32, 3, 3, 3, generator=g) * 0.1
+    w27 = region_weight(conv).to(DEV)
+    bn = tuple(t.to(DEV) for t in _bn_params(32, g))
+    bw = bound_words(3, DEV)
+    bw[0, 0] = torch.tensor([x.abs().max().item()], dtype=torch.float32).view(torch.int32).item()
+    add = torch.relu(torch.randn(2, *size(Bx), 32, generator=g)).to(DEV)
+    args = (CONV_T2, list(n), org(Bx), size(Bx), org(C2), size(C2), list(pad))
+    with torch.no_grad():
+        y = conv3d_region_split(x, None, w27, *args, bw[0], None, bw[1], *bn)
+        ys = conv3d_region_split(x, None, w27, *args, bw[0], None, bw[2], *bn, y_addend=add)
+        torch.cuda.synchronize()
+    assert torch.equal(ys, y + add)
+    assert bw[2].cpu().numpy().view(np.float32).max() == ys.abs().max().item()
