@@ -541,7 +541,6 @@ int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch,
                           void* stream) {
   if (!x || !weight || !y || batch <= 0 || c_in <= 0 || c_in > 64 || c_out != 8) return MVS_ERR_INVALID_ARGUMENT;
   if (flags & ~(MVS_LAYOUT_CHANNELS_LAST | MVS_DECONV_WEIGHT_TAPS)) return MVS_ERR_INVALID_ARGUMENT;
-  if ((flags & MVS_LAYOUT_CHANNELS_LAST) && (flags & MVS_DECONV_WEIGHT_TAPS)) return MVS_ERR_INVALID_ARGUMENT;
   if ((flags & MVS_LAYOUT_CHANNELS_LAST) && (c_in % 4 || ((uintptr_t)x & 15u) || ((uintptr_t)x2 & 15u)))
     return MVS_ERR_INVALID_ARGUMENT;   // 16-byte channel-quad loads
   if (rd <= 0 || rh <= 0 || rw <= 0 || d <= 0 || h <= 0 || w <= 0) return MVS_ERR_INVALID_ARGUMENT;
@@ -550,7 +549,8 @@ int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch,
     return MVS_ERR_INVALID_ARGUMENT;
   // the region input is read through 32-bit buffer descriptors over the whole batch
   if ((uint64_t)batch * c_in * rd * rh * rw * 4u >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
-  const int layout = (flags & MVS_LAYOUT_CHANNELS_LAST) ? 1 : ((flags & MVS_DECONV_WEIGHT_TAPS) ? 2 : 0);
+  const int layout = (flags & MVS_LAYOUT_CHANNELS_LAST) ? ((flags & MVS_DECONV_WEIGHT_TAPS) ? 3 : 1)
+                                                        : ((flags & MVS_DECONV_WEIGHT_TAPS) ? 2 : 0);
   const mvs::LaunchCheck lc;
   mvs::launch_deconv3d_k3s2(x, x2, layout, batch, c_in, rd, rh, rw, x0d, x0h,
                             x0w, weight, d, h, w, pd, ph, pw, bn_scale, bn_shift, bn_mean, residual, y,

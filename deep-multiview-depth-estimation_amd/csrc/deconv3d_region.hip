@@ -53,10 +53,10 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
     const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
     const float* __restrict__ mean, const float* __restrict__ residual, float* __restrict__ y,
     int md_n, int mh_n, int mw_n, size_t total, size_t total_in_bytes, size_t out_bytes) {
-  constexpr bool CL = LM == 1;   // channels-last input
-  constexpr bool WT = LM == 2;   // NCDHW input, tap-major weights wt[ci][27][co]: packed FMAs
-  extern __shared__ float4 wl4[];   // CL: [ci][co][7] float4 = W[ci][co][27] padded
-  if constexpr (CL) {
+  constexpr bool CL = LM == 1 || LM == 3;   // channels-last input (LM 3: with tap-major weights)
+  constexpr bool WT = LM == 2 || LM == 3;   // tap-major weights wt[ci][27][co]: packed FMAs, SGPR operands
+  extern __shared__ float4 wl4[];   // LM 1: [ci][co][7] float4 = W[ci][co][27] padded
+  if constexpr (CL && !WT) {
     float* wl = reinterpret_cast<float*>(wl4);
     const int nw = Cin * kCout * kWRow;
     for (int e = (int)threadIdx.x; e < nw; e += kBlock) {
@@ -201,7 +201,8 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
               const float4 t = q[a][c][e];
               v[a][c][e] = j == 0 ? t.x : (j == 1 ? t.y : (j == 2 ? t.z : t.w));
             }
-        channel(c0 + j, v);
+        if constexpr (WT) channel_pk(c0 + j, v);
+        else channel(c0 + j, v);
       }
     }
   } else {
@@ -351,7 +352,11 @@ void launch_cls(dim3 grid, size_t lds, hipStream_t s, const float* x, const floa
   // the epilogue's buffer-store path: even W and the whole output under 2^31 bytes (0 = the general path)
   const size_t ob = total / ((size_t)md_n * mh_n * mw_n) * (size_t)kCout * D * H * W * 4u;
   const size_t out_bytes = (W % 2 == 0 && ob < (1ull << 31)) ? ob : 0;
-  if (lm == 1)
+  if (lm == 3)
+    hipLaunchKernelGGL((deconv3d_k3s2_kernel<CD, CH, CW, 3>), grid, dim3(kBlock), 0, s, x, x2, weight, Cin,
+                       rd, rh, rw, x0d, x0h, x0w, D, H, W, pd >> 1, ph >> 1, pw >> 1, bn_scale, bn_shift,
+                       bn_mean, residual, y, md_n, mh_n, mw_n, total, in_bytes, out_bytes);
+  else if (lm == 1)
     hipLaunchKernelGGL((deconv3d_k3s2_kernel<CD, CH, CW, 1>), grid, dim3(kBlock), lds, s, x, x2, weight, Cin,
                        rd, rh, rw, x0d, x0h, x0w, D, H, W, pd >> 1, ph >> 1, pw >> 1, bn_scale, bn_shift,
                        bn_mean, residual, y, md_n, mh_n, mw_n, total, in_bytes, out_bytes);

@@ -377,22 +377,29 @@ class CostVolumeReg(nn.Module):
                 ya = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(halo), size(halo), cv_box[0],
                                    cv_box[1], pad, *bn_eval(bn), in_c4=c4, absmax=bound if split_cv else None,
                                    y_bound=ab)
-            # level 1's output only feeds deconv_1_0's input sum: channels-first for its loads
+            # -> (output, channels-last?).  Level 1's output only feeds deconv_1_0's input sum: channels-first
+            # for its loads on the fp32 path; the split path keeps it channels-last (deconv_2_0's epilogue
+            # adds it, coalesced)
             if ab is not None:
                 return conv3d_region_split(ya, None, region_weight(conv_b), CONV_S1, dims, org(reg), size(reg),
                                            org(halo), size(halo), None, ab, None, bw[3 + k], *bn_eval(bn),
-                                           out_ncdhw=reg is B)
+                                           out_ncdhw=False), True
             return conv3d_region(ya, None, region_weight(conv_b), CONV_S1, dims, org(reg), size(reg),
-                                 org(halo), size(halo), None, *bn_eval(bn), out_ncdhw=reg is B)
-        y1 = level(0, self.conv_1_0, self.conv_1_1, self.BN_1, B)
-        y2 = level(1, self.conv_2_0, self.conv_2_1, self.BN_2, C2)
-        y3 = level(2, self.conv_3_0, self.conv_3_1, self.BN_3, C3)
+                                 org(halo), size(halo), None, *bn_eval(bn), out_ncdhw=reg is B), reg is not B
+        y1, y1_cl = level(0, self.conv_1_0, self.conv_1_1, self.BN_1, B)
+        y2 = level(1, self.conv_2_0, self.conv_2_1, self.BN_2, C2)[0]
+        y3 = level(2, self.conv_3_0, self.conv_3_1, self.BN_3, C3)[0]
         if bw is not None:
             # deconv_3_0 + BN_2 + ReLU, then `+ y2` (model.py:119) in its epilogue: deconv_2_0 reads one tensor
             y32 = conv3d_region_split(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, org(C2), size(C2),
                                       org(C3), size(C3), pad, bw[5], None, bw[6], *bn_eval(self.BN_2), y_addend=y2)
+            # and, when level 1 ran split (channels-last), deconv_2_0's epilogue forms model.py:121's y2 + y1:
+            # deconv_1_0 reads one channels-last tensor (else deconv_1_0 adds the channels-first y1 on load)
             y2 = conv3d_region_split(y32, None, region_weight(self.deconv_2_0), CONV_T2, dims, org(B), size(B),
-                                     org(C2), size(C2), pad, bw[6], None, None, *bn_eval(self.BN_1), out_ncdhw=True)
+                                     org(C2), size(C2), pad, bw[6], None, None, *bn_eval(self.BN_1),
+                                     out_ncdhw=not y1_cl, y_addend=y1 if y1_cl else None)
+            if y1_cl:
+                y1 = None
         else:
             y3 = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, org(C2), size(C2),
                                org(C3), size(C3), pad, *bn_eval(self.BN_2))
@@ -401,7 +408,8 @@ class CostVolumeReg(nn.Module):
         if side != main:   # (a stream waiting on itself is an event + barrier packet: a 6 us bubble)
             main.wait_stream(side)
             y0.record_stream(main)
-        z = deconv3d_k3s2(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0, x2=y1)
+        z = deconv3d_k3s2(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0, x2=y1,
+                          channels_last=bw is not None and y1_cl)
         return softmax_depth(conv3d_k3(z, self.conv_out.weight))
 
     def _split_head_ok(self, cv, n):
@@ -546,7 +554,14 @@ class CostVolumeReg(nn.Module):
             z = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
                               size(M), pad, out_ncdhw=True)
         p = _bn_train(self.BN_1, *channel_stats(z, False), count)
-        y2 = bn_relu_(_crop_cf(z, full, M), False, *p)
+        if bw is not None:
+            # relu(BN_1(deconv_2_0)) + y1 (model.py:121) formed in the BN pass (y1 >= 0: exact, as above)
+            c1 = y1.shape[1]
+            one, zero = torch.ones(c1, device=y1.device), torch.zeros(c1, device=y1.device)
+            y2 = bn_relu_(_crop_cf(z, full, M), False, *p, r=y1, r_bn=(one, zero, zero))
+            y1 = None
+        else:
+            y2 = bn_relu_(_crop_cf(z, full, M), False, *p)
         del z
         z = deconv3d_k3s2(y2, org(M), self.deconv_1_0.weight, dims, pad, None, None, None, None, x2=y1)
         main.wait_stream(side)

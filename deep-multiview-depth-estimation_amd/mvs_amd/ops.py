@@ -905,14 +905,11 @@ def deconv3d_k3s2(x: torch.Tensor, origin: list[int], weight: torch.Tensor, out_
             raise ValueError("x2 must have x's shape")
     if tuple(weight.shape) != (cin, 8, 3, 3, 3):
         raise ValueError("weight [c_in, 8, 3, 3, 3] expected, got %s" % (tuple(weight.shape),))
-    if channels_last:
-        w = weight.to(device=x.device, dtype=_F32).contiguous()
-        flags = _lib.MVS_LAYOUT_CHANNELS_LAST
-    else:   # tap-major weight[c_in][27][8]: the NCDHW kernel's packed-FMA form
-        w = derived("deconv_taps", (weight,),
-                    lambda wt: wt.to(device=x.device, dtype=_F32).reshape(cin, 8, 27).transpose(1, 2).contiguous(),
-                    x.device)
-        flags = _lib.MVS_DECONV_WEIGHT_TAPS
+    # tap-major weight[c_in][27][8]: the packed-FMA form (either input layout)
+    w = derived("deconv_taps", (weight,),
+                lambda wt: wt.to(device=x.device, dtype=_F32).reshape(cin, 8, 27).transpose(1, 2).contiguous(),
+                x.device)
+    flags = _lib.MVS_DECONV_WEIGHT_TAPS | (_lib.MVS_LAYOUT_CHANNELS_LAST if channels_last else 0)
     d, h, wd = out_dims
     f = lambda t: None if t is None else t.to(device=x.device, dtype=_F32).contiguous()
     sc, sh, mu, res = f(bn_scale), f(bn_shift), f(bn_mean), f(residual)

@@ -394,7 +394,7 @@ int mvs_conv2d_fwd(const float* x, const float* weight, float* y, int n, int c_i
 
 /* layout flag of mvs_deconv3d_k3s2_fwd: the region input is channels-last x[batch][rd][rh][rw][c_in] */
 #define MVS_LAYOUT_CHANNELS_LAST 1
-/* flag of mvs_deconv3d_k3s2_fwd (NCDHW input only): the weight is tap-major weight[c_in][27][8]
+/* flag of mvs_deconv3d_k3s2_fwd (either layout): the weight is tap-major weight[c_in][27][8]
  * (ConvTranspose3d's weight.reshape(c_in, 8, 27).transpose(1, 2)): output-channel pairs adjacent,
  * one 8-byte scalar operand per packed FMA */
 #define MVS_DECONV_WEIGHT_TAPS 2
