@@ -498,7 +498,7 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
 
 int mvs_conv2d_fwd(const float* x, const float* weight, float* y, int n, int c_in, int c_out, int h, int w,
                    int k, int stride, const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                   void* stream) {
+                   unsigned* y_bound, void* stream) {
   if (!x || !weight || !y || n <= 0 || n > 65535 || h <= 0 || w <= 0 || stride <= 0) return MVS_ERR_INVALID_ARGUMENT;
   if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
     return MVS_ERR_INVALID_ARGUMENT;
@@ -506,7 +506,65 @@ int mvs_conv2d_fwd(const float* x, const float* weight, float* y, int n, int c_i
   if ((uint64_t)c_in * (uint64_t)h * (uint64_t)w >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
   const mvs::LaunchCheck lc;
   const int st = mvs::launch_conv2d_narrow(x, weight, y, n, c_in, c_out, h, w, k, stride, bn_scale, bn_shift,
-                                           bn_mean, (hipStream_t)stream);
+                                           bn_mean, y_bound, (hipStream_t)stream);
+  return st != MVS_OK ? st : lc.status();
+}
+
+int mvs_conv2d_split_weights(const float* weight, int c_in, int c_out, int k, unsigned short* frag, int* weight_exp) {
+  if (!weight || !frag || !weight_exp || k <= 0 || k > 7) return MVS_ERR_INVALID_ARGUMENT;
+  if (!(c_in == 8 || c_in == 16 || c_in == 32) || !(c_out == 8 || (c_out > 0 && c_out % 16 == 0)))
+    return MVS_ERR_INVALID_ARGUMENT;
+  const int taps = k * k, n = c_out * c_in * taps;
+  float m = 0.0f;
+  for (int i = 0; i < n; ++i) {
+    if (!std::isfinite(weight[i])) return MVS_ERR_INVALID_ARGUMENT;
+    m = std::max(m, std::fabs(weight[i]));
+  }
+  int e = 0;
+  if (m > 0.0f) (void)std::frexp(m, &e);
+  const int ew = m > 0.0f ? std::min(std::max(14 - e, -120), 120) : 0;
+  const int kbs = mvs::conv2d_split_kblocks(c_in, k), tpb = 32 / c_in, cpt = c_in / 8;
+  const bool narrow = c_out == 8;
+  const int nbs = narrow ? 1 : c_out / 16;
+  auto part = [&](int co, int ci, int t, int p) -> uint16_t {
+    const float v = t < taps ? std::ldexp(weight[((size_t)co * c_in + ci) * taps + t], ew) : 0.0f;
+    const _Float16 hi = (_Float16)v;
+    const _Float16 r = p == 0 ? hi : (_Float16)(v - (float)hi);
+    uint16_t b;
+    std::memcpy(&b, &r, 2);
+    return b;
+  };
+  for (int kb = 0; kb < kbs; ++kb)
+    for (int nb = 0; nb < nbs; ++nb)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int c = lane & 15, g = lane >> 4;
+          const int t = kb * tpb + g / cpt, ci = 8 * (g % cpt) + j;
+          if (narrow) {
+            frag[((size_t)kb * 64 + lane) * 8 + j] = part(c & 7, ci, t, c >> 3);
+          } else {
+            const size_t base = ((((size_t)kb * nbs + nb) * 2) * 64 + lane) * 8 + j;
+            frag[base] = part(nb * 16 + c, ci, t, 0);
+            frag[base + 64 * 8] = part(nb * 16 + c, ci, t, 1);
+          }
+        }
+  *weight_exp = ew;
+  return MVS_OK;
+}
+
+int mvs_conv2d_split_fwd(const float* x, const void* weight_frag, int weight_exp, float* y, int n, int c_in,
+                         int c_out, int h, int w, int k, int stride, const float* bn_scale, const float* bn_shift,
+                         const float* bn_mean, const unsigned* x_bound, unsigned* y_bound, void* stream) {
+  if (!x || !weight_frag || !y || !x_bound || n <= 0 || n > 65535 || h <= 0 || w <= 0 || stride <= 0)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if ((bn_scale != nullptr) != (bn_shift != nullptr) || (bn_scale != nullptr) != (bn_mean != nullptr))
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (reinterpret_cast<uintptr_t>(weight_frag) % 16) return MVS_ERR_INVALID_ARGUMENT;
+  // one image's buffer resource and staging offsets are 32-bit
+  if ((uint64_t)c_in * (uint64_t)h * (uint64_t)w * 4u >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
+  const int st = mvs::launch_conv2d_split(x, weight_frag, weight_exp, y, n, c_in, c_out, h, w, k, stride, bn_scale,
+                                          bn_shift, bn_mean, x_bound, y_bound, (hipStream_t)stream);
   return st != MVS_OK ? st : lc.status();
 }
 

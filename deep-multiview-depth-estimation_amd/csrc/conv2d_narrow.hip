@@ -18,6 +18,7 @@
 #include <cstdlib>
 
 #include "launchers.h"
+#include "split.h"
 
 namespace mvs {
 namespace {
@@ -38,7 +39,7 @@ template <int CIN, int COUT, int K, int S, int SPLIT>
 __global__ __launch_bounds__(kBlock) void conv2d_narrow_kernel(
     const float* __restrict__ in, const float* __restrict__ wt, float* __restrict__ out, int H, int W, int Ho,
     int Wo, int tiles_x, const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
-    const float* __restrict__ bn_mean) {
+    const float* __restrict__ bn_mean, uint32_t* __restrict__ yb) {
   constexpr int P = K / 2;
   constexpr int IH = (k2TY - 1) * S + K, IW = (k2TX - 1) * S + K;
   constexpr int kPlane = IH * IW;
@@ -125,16 +126,20 @@ __global__ __launch_bounds__(kBlock) void conv2d_narrow_kernel(
   }
 
   const int gx = ox0 + lx, gy = oy0 + ly;
-  if (gx >= Wo || gy >= Ho) return;
-  const size_t oplane = (size_t)Ho * Wo;
-  float* ob = out + ((size_t)n * COUT + co0) * oplane + (size_t)gy * Wo + gx;
+  float vmax = 0.0f;   // the output's bound words (split-fp16 consumers: conv2d_split.hip)
+  if (gx < Wo && gy < Ho) {
+    const size_t oplane = (size_t)Ho * Wo;
+    float* ob = out + ((size_t)n * COUT + co0) * oplane + (size_t)gy * Wo + gx;
 #pragma unroll
-  for (int c = 0; c < CO; ++c) {
-    const int co = co0 + c;
-    float v = NP > 0 ? acc2[c / 2][c & 1] : acc1;
-    if (bn_scale) v = fmaxf((v - bn_mean[co]) * bn_scale[co] + bn_shift[co], 0.0f);
-    ob[(size_t)c * oplane] = v;
+    for (int c = 0; c < CO; ++c) {
+      const int co = co0 + c;
+      float v = NP > 0 ? acc2[c / 2][c & 1] : acc1;
+      if (bn_scale) v = fmaxf((v - bn_mean[co]) * bn_scale[co] + bn_shift[co], 0.0f);
+      vmax = fmaxf(vmax, fabsf(v));
+      ob[(size_t)c * oplane] = v;
+    }
   }
+  if (yb) bound_update(yb, vmax);
 }
 
 // output-channel split: a small grid leaves SIMDs idle (the refinement net's 4 x 128 x 160 layers:
@@ -147,7 +152,7 @@ constexpr int kSplitTarget = 960;
 
 template <int CIN, int COUT, int K, int S, int MAXS>
 void launch2d(const float* in, const float* wt, float* out, int N, int H, int W, const float* sc,
-              const float* sh, const float* mu, hipStream_t s) {
+              const float* sh, const float* mu, uint32_t* yb, hipStream_t s) {
   const int Ho = (H + 2 * (K / 2) - K) / S + 1, Wo = (W + 2 * (K / 2) - K) / S + 1;
   const int tiles_x = (Wo + k2TX - 1) / k2TX, tiles_y = (Ho + k2TY - 1) / k2TY;
   const long wgs = (long)tiles_x * tiles_y * N;
@@ -160,23 +165,23 @@ void launch2d(const float* in, const float* wt, float* out, int N, int H, int W,
   const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)N, (unsigned)split);
   if (split >= 4 && MAXS >= 4)
     hipLaunchKernelGGL((conv2d_narrow_kernel<CIN, COUT, K, S, (MAXS >= 4 ? 4 : 1)>), grid, dim3(kBlock), 0, s, in,
-                       wt, out, H, W, Ho, Wo, tiles_x, sc, sh, mu);
+                       wt, out, H, W, Ho, Wo, tiles_x, sc, sh, mu, yb);
   else if (split >= 2 && MAXS >= 2)
     hipLaunchKernelGGL((conv2d_narrow_kernel<CIN, COUT, K, S, (MAXS >= 2 ? 2 : 1)>), dim3(grid.x, grid.y, 2),
-                       dim3(kBlock), 0, s, in, wt, out, H, W, Ho, Wo, tiles_x, sc, sh, mu);
+                       dim3(kBlock), 0, s, in, wt, out, H, W, Ho, Wo, tiles_x, sc, sh, mu, yb);
   else
     hipLaunchKernelGGL((conv2d_narrow_kernel<CIN, COUT, K, S, 1>), dim3(grid.x, grid.y, 1), dim3(kBlock), 0, s, in,
-                       wt, out, H, W, Ho, Wo, tiles_x, sc, sh, mu);
+                       wt, out, H, W, Ho, Wo, tiles_x, sc, sh, mu, yb);
 }
 
 }  // namespace
 
 int launch_conv2d_narrow(const float* in, const float* wt, float* out, int N, int Cin, int Cout, int H, int W,
                          int K, int stride, const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                         hipStream_t s) {
+                         uint32_t* y_bound, hipStream_t s) {
 #define MVS_CONV2D_CASE(A, C, KK, SS, MS)                                               \
   if (Cin == A && Cout == C && K == KK && stride == SS) {                               \
-    launch2d<A, C, KK, SS, MS>(in, wt, out, N, H, W, bn_scale, bn_shift, bn_mean, s);   \
+    launch2d<A, C, KK, SS, MS>(in, wt, out, N, H, W, bn_scale, bn_shift, bn_mean, y_bound, s); \
     return MVS_OK;                                                                      \
   }
   // FeatureEncoder (model.py:22-65) and the refinement net (model.py:134-145); the last argument

@@ -9,7 +9,7 @@
 //     the weights likewise with 2^ew (host, mvs_conv3d_region_split_weights);
 //   * one K-32 step is three v_mfma_f32_16x16x32_f16 into the same accumulator: x_hi w_hi, x_hi w_lo,
 //     x_lo w_hi (the dropped x_lo w_lo is below 2^-22 of the product), each product exact in fp32;
-//   * ex comes from the input's BOUND WORDS: kBoundWords partial maxima of |v| that the kernel which
+//   * ex comes from the input's BOUND WORDS: kBoundSlots partial maxima of |v| that the kernel which
 //     produced the tensor wrote in its epilogue (bound_update, split.h), so max|v| 2^ex < 2^14.
 //
 // gfx950 runs the f16 MFMA at 16x the fp32 one's rate: the three products cost 48 cycles per

@@ -108,7 +108,15 @@ int launch_conv_s2_split(const void* x, bool presplit, const void* wfrag, int w_
 // without an instantiation
 int launch_conv2d_narrow(const float* in, const float* wt, float* out, int N, int Cin, int Cout, int H, int W,
                          int K, int stride, const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                         hipStream_t s);
+                         uint32_t* y_bound, hipStream_t s);
+
+// conv2d_split.hip: the same convolutions (8..32 input channels) on the f16 matrix cores with split
+// operands; x scaled by its bound words, y's bound words raised; weight fragments from
+// mvs_conv2d_split_weights (conv2d_split_kblocks K-32 blocks)
+int conv2d_split_kblocks(int c_in, int k);
+int launch_conv2d_split(const float* x, const void* wfrag, int w_exp, float* y, int N, int Cin, int Cout, int H,
+                        int W, int K, int stride, const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                        const uint32_t* x_bound, uint32_t* y_bound, hipStream_t s);
 
 // deconv3d_region.hip: stride-2 kernel-3 ConvTranspose3d (Cout 8) from a region tensor to the full
 // volume, optional fused BN(eval)+ReLU and residual add

@@ -58,32 +58,47 @@ def _run_stack(seq, x):
     running statistics updated as torch does.  Elsewhere the modules themselves."""
     if not _hip_inference(x):
         return seq(x)
-    from .ops import bn_relu_, channel_stats, conv2d, conv2d_supported
+    from .ops import (CONV2D_SPLIT_SHAPES, bn_relu_, bound_words, channel_stats, conv2d, conv2d_split,
+                      conv2d_supported)
     layers = list(seq)
+    # split-fp16 MFMA convolutions (csrc/conv2d_split.hip) for the 8..32-channel inputs: every layer's
+    # output carries bound words (one zeroed set per layer, one memset) that scale the next layer's input
+    words = bound_words(len(layers), x.device) if os.environ.get("MVS_CONV2D_F16", "1") != "0" else None
 
-    def conv(layer, x, bn=None):   # the HIP direct convolution for the reference's layer shapes
+    def conv(layer, x, xb, yb, bn=None):
+        """(y, whether yb now bounds y): the HIP convolutions for the reference's layer shapes"""
         if isinstance(layer, nn.Conv2d) and conv2d_supported(layer):
-            return conv2d(x, layer.weight, layer.stride[0], *(bn or ()))
+            k = layer.kernel_size[0]
+            if xb is not None and (layer.in_channels, layer.out_channels, k, layer.stride[0]) in CONV2D_SPLIT_SHAPES:
+                return conv2d_split(x, layer.weight, layer.stride[0], xb, yb, *(bn or ())), yb is not None
+            return conv2d(x, layer.weight, layer.stride[0], *(bn or ()), y_bound=yb), yb is not None
         y = layer(x)
-        return y if bn is None else bn_relu_(y.contiguous(), False, *bn)
+        if bn is None:
+            return y, False
+        return bn_relu_(y.contiguous(), False, *bn, y_bound=yb), yb is not None
 
+    xb = None   # x's bound words (None: unknown)
     i = 0
     while i < len(layers):
         layer = layers[i]
+        yb = None if words is None or not isinstance(layer, nn.Conv2d) else words[i]
         if (i + 2 < len(layers) and isinstance(layers[i + 1], nn.BatchNorm2d)
                 and isinstance(layers[i + 2], nn.ReLU)):
             bn = layers[i + 1]
             if bn.running_mean is None or not bn.affine:   # no running statistics: the module
                 return _run_tail(layers[i:], x)
             if bn.training:
-                y = conv(layer, x).contiguous()
-                x = bn_relu_(y, False, *_bn_train(bn, *channel_stats(y, False), y.numel() // y.shape[1]))
+                y = conv(layer, x, xb, None)[0].contiguous()
+                x = bn_relu_(y, False, *_bn_train(bn, *channel_stats(y, False), y.numel() // y.shape[1]),
+                             y_bound=yb)
+                bounded = yb is not None
             else:   # eval BN + ReLU fused into the convolution's epilogue
-                x = conv(layer, x, _bn_eval(bn))
+                x, bounded = conv(layer, x, xb, yb, _bn_eval(bn))
             i += 3
         else:
-            x = conv(layer, x)
+            x, bounded = conv(layer, x, xb, yb)
             i += 1
+        xb = yb if bounded else None
     return x
 
 

@@ -844,12 +844,16 @@ def conv2d_supported(conv):
             and (conv.in_channels, conv.out_channels, k, conv.stride[0]) in CONV2D_SHAPES)
 
 
+# (y_bound is raised in place; not declared as a mutation, as conv3d_region_split's bound words)
 @torch.library.custom_op("mvs::conv2d", mutates_args=())
 def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int, bn_scale: Optional[torch.Tensor] = None,
-           bn_shift: Optional[torch.Tensor] = None, bn_mean: Optional[torch.Tensor] = None) -> torch.Tensor:
+           bn_shift: Optional[torch.Tensor] = None, bn_mean: Optional[torch.Tensor] = None,
+           y_bound: Optional[torch.Tensor] = None) -> torch.Tensor:
     """nn.Conv2d(c_in, c_out, k, stride, padding=k // 2, bias=False) forward, fp32 NCHW, on the HIP
     kernel (csrc/conv2d_narrow.hip); with bn_* given, max((y - mean) * scale + shift, 0) is fused
-    (eval BatchNorm2d + ReLU).  Shapes: CONV2D_SHAPES.  Inference only (no autograd formula)."""
+    (eval BatchNorm2d + ReLU).  ``y_bound``: None or zeroed bound words (bound_words) raised to
+    max|y|, the input scale of a following conv2d_split.  Shapes: CONV2D_SHAPES.  Inference only (no
+    autograd formula)."""
     _require_gpu(x, "x")
     lib = _lib.load()
     if x.dim() != 4 or weight.dim() != 4 or weight.shape[1] != x.shape[1] or weight.shape[2] != weight.shape[3]:
@@ -868,13 +872,74 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int, bn_scale: Optiona
     ho, wo = (h + 2 * (k // 2) - k) // stride + 1, (wd + 2 * (k // 2) - k) // stride + 1
     y = torch.empty((n, cout, ho, wo), device=x.device, dtype=_F32)
     st = lib.mvs_conv2d_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(y), n, cin, cout, h, wd, k, stride, *bp,
-                            _lib.stream_handle(x.device))
+                            _bound_ptr(y_bound), _lib.stream_handle(x.device))
     _lib.check(st, "mvs_conv2d_fwd")
     return y
 
 
 @conv2d.register_fake
-def _(x, weight, stride, bn_scale=None, bn_shift=None, bn_mean=None):
+def _(x, weight, stride, bn_scale=None, bn_shift=None, bn_mean=None, y_bound=None):
+    k = weight.shape[2]
+    return x.new_empty((x.shape[0], weight.shape[0], (x.shape[2] + 2 * (k // 2) - k) // stride + 1,
+                        (x.shape[3] + 2 * (k // 2) - k) // stride + 1))
+
+
+# (c_in, c_out, k, stride) of the split-fp16 MFMA kernel (csrc/conv2d_split.hip): the encoder's layers
+# 2-8 and the refinement net's 32 -> 32
+CONV2D_SPLIT_SHAPES = frozenset({(8, 8, 3, 1), (8, 16, 5, 2), (16, 16, 3, 1), (16, 32, 5, 2), (32, 32, 3, 1)})
+
+
+def conv2d_split_fragments(weight, device):
+    """(split-fp16 MFMA fragments on ``device``, exponent) of an nn.Conv2d weight [c_out][c_in][k][k],
+    formed on the host by mvs_conv2d_split_weights."""
+    lib = _lib.load()
+    w = weight.detach().to(device="cpu", dtype=_F32).contiguous()
+    cout, cin, k, _ = w.shape
+    kb = -(-(k * k) // (32 // cin))
+    parts = 1 if cout == 8 else 2 * (cout // 16)
+    frag = torch.empty((kb * parts * 64 * 8,), dtype=torch.int16)
+    e = ctypes.c_int(0)
+    st = lib.mvs_conv2d_split_weights(_lib.ptr(w), cin, cout, k, _lib.ptr(frag), ctypes.byref(e))
+    _lib.check(st, "mvs_conv2d_split_weights")
+    return frag.to(device), e.value
+
+
+# (y_bound is raised in place; not declared as a mutation, as conv3d_region_split's bound words)
+@torch.library.custom_op("mvs::conv2d_split", mutates_args=())
+def conv2d_split(x: torch.Tensor, weight: torch.Tensor, stride: int, x_bound: torch.Tensor,
+                 y_bound: Optional[torch.Tensor] = None, bn_scale: Optional[torch.Tensor] = None,
+                 bn_shift: Optional[torch.Tensor] = None, bn_mean: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """conv2d on the f16 matrix cores with split operands (mvs_conv2d_split_fwd,
+    csrc/conv2d_split.hip): x scaled by its bound words ``x_bound`` (raised by the conv2d /
+    conv2d_split that produced x), ``y_bound`` (None or zeroed words) raised to max|y|.  Same
+    arguments and epilogue as conv2d otherwise; fp32-level error, not conv2d's bit pattern.  Shapes:
+    CONV2D_SPLIT_SHAPES.  Inference only."""
+    _require_gpu(x, "x")
+    lib = _lib.load()
+    if x.dim() != 4 or weight.dim() != 4 or weight.shape[1] != x.shape[1] or weight.shape[2] != weight.shape[3]:
+        raise ValueError("x [N, C, H, W] and weight [Cout, C, k, k] expected, got %s, %s"
+                         % (tuple(x.shape), tuple(weight.shape)))
+    n, cin, h, wd = x.shape
+    cout, k = weight.shape[0], weight.shape[2]
+    if (cin, cout, k, stride) not in CONV2D_SPLIT_SHAPES:
+        raise ValueError("conv2d_split: unsupported (c_in, c_out, k, stride) %s" % ((cin, cout, k, stride),))
+    x = x.to(_F32).contiguous()
+    dev = x.device
+    frag, ew = derived("conv2d_split", (weight,), lambda wt: conv2d_split_fragments(wt, dev), dev)
+    bn = [t if t is None else t.to(device=dev, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
+    if any(t is None for t in bn) and not all(t is None for t in bn):
+        raise ValueError("bn_scale, bn_shift and bn_mean go together")
+    bp = [None if t is None else _lib.ptr(t) for t in bn]
+    ho, wo = (h + 2 * (k // 2) - k) // stride + 1, (wd + 2 * (k // 2) - k) // stride + 1
+    y = torch.empty((n, cout, ho, wo), device=dev, dtype=_F32)
+    st = lib.mvs_conv2d_split_fwd(_lib.ptr(x), _lib.ptr(frag), ew, _lib.ptr(y), n, cin, cout, h, wd, k, stride,
+                                  *bp, _bound_ptr(x_bound), _bound_ptr(y_bound), _lib.stream_handle(dev))
+    _lib.check(st, "mvs_conv2d_split_fwd")
+    return y
+
+
+@conv2d_split.register_fake
+def _(x, weight, stride, x_bound, y_bound=None, bn_scale=None, bn_shift=None, bn_mean=None):
     k = weight.shape[2]
     return x.new_empty((x.shape[0], weight.shape[0], (x.shape[2] + 2 * (k // 2) - k) // stride + 1,
                         (x.shape[3] + 2 * (k // 2) - k) // stride + 1))
@@ -1042,7 +1107,7 @@ def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, 
     return x.new_empty((x.shape[0],) + tuple(out_size) + (weight.shape[1],), dtype=_F32)
 
 
-BOUND_WORDS = 64   # MVS_BOUND_WORDS
+BOUND_WORDS = 2048   # MVS_BOUND_WORDS (64 slots, one per 128-byte line)
 
 
 def bound_words(n, device):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 15
+#define MVS_ABI_VERSION 16
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -387,10 +387,33 @@ int mvs_cost_volume_head_fwd(const float* feat, const float* K, const float* R, 
  * (4,32,3,1) (32,1,3,1); MVS_ERR_INVALID_ARGUMENT otherwise.  Optional epilogue (all three BN pointers,
  * c_out floats each, or none): y = max((y - bn_mean) * bn_scale + bn_shift, 0), the eval BN + ReLU
  * that follows these convolutions.  Replaces the MIOpen convolution behind torch.nn.Conv2d.forward
- * (and the BatchNorm2d + ReLU after it) in inference; same products, fp32 summation order differs. */
+ * (and the BatchNorm2d + ReLU after it) in inference; same products, fp32 summation order differs.
+ * y_bound: NULL, or MVS_BOUND_WORDS zeroed DEVICE words raised to max|y| (the input scale of a
+ * following mvs_conv2d_split_fwd). */
 int mvs_conv2d_fwd(const float* x, const float* weight, float* y, int n, int c_in, int c_out, int h, int w,
                    int k, int stride, const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                   void* stream);
+                   unsigned* y_bound, void* stream);
+
+/* Split-fp16 weight fragments of an nn.Conv2d weight[c_out][c_in][k][k] (HOST fp32, finite) for
+ * mvs_conv2d_split_fwd: frag (HOST, kb * parts * 64 * 8 uint16, kb = ceil(k^2 / (32 / c_in)) K-32
+ * blocks, parts = 1 for c_out = 8 else 2 c_out / 16) and *weight_exp = ew with max|w| 2^ew < 2^14.
+ * K block kb, lane (c = lane & 15, g = lane >> 4), element j: tap t = kb (32 / c_in) + g / (c_in / 8)
+ * (zero past k^2), input channel 8 (g % (c_in / 8)) + j.  c_out >= 16: frag[kb][nb][part][lane][j] =
+ * part (0: fp16(w 2^ew), 1: fp16(w 2^ew - part 0)) of w[16 nb + c][ci][t]; c_out = 8: frag[kb][lane][j]
+ * = part 0 of w[c][ci][t] for c < 8, part 1 of w[c - 8][ci][t] for c >= 8.  c_in in {8, 16, 32},
+ * c_out 8 or a multiple of 16. */
+int mvs_conv2d_split_weights(const float* weight, int c_in, int c_out, int k, unsigned short* frag, int* weight_exp);
+
+/* mvs_conv2d_fwd's convolutions with 8..32 input channels (FeatureEncoder layers 2-8, the refinement
+ * net's 32 -> 32) on the f16 matrix cores with split operands (csrc/conv2d_split.hip): x scaled by
+ * 2^ex from its bound words x_bound (DEVICE, required: mvs_conv2d_fwd's / this function's y_bound) and
+ * split into fp16 hi + lo, the weights likewise (mvs_conv2d_split_weights: weight_frag DEVICE, 16-byte
+ * aligned); per K-32 block x_hi w_hi + x_hi w_lo + x_lo w_hi in fp32 accumulation: fp32-level error,
+ * not mvs_conv2d_fwd's bit pattern.  Weight in fragments, otherwise arguments as mvs_conv2d_fwd.
+ * Supported (c_in, c_out, k, stride): (8,8,3,1) (8,16,5,2) (16,16,3,1) (16,32,5,2) (32,32,3,1). */
+int mvs_conv2d_split_fwd(const float* x, const void* weight_frag, int weight_exp, float* y, int n, int c_in,
+                         int c_out, int h, int w, int k, int stride, const float* bn_scale, const float* bn_shift,
+                         const float* bn_mean, const unsigned* x_bound, unsigned* y_bound, void* stream);
 
 /* layout flag of mvs_deconv3d_k3s2_fwd: the region input is channels-last x[batch][rd][rh][rw][c_in] */
 #define MVS_LAYOUT_CHANNELS_LAST 1
@@ -455,10 +478,11 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
  * stride-1 kernel applies (the two are bit-identical; tests and A/B timing) */
 #define MVS_CONV_PER_LANE 32
 
-/* Bound words of a region tensor: MVS_BOUND_WORDS uint32 holding maxima of |v| as fp32 bit patterns
- * (the tensor's bound is their maximum), raised with atomic maxima by the kernel that writes the tensor
- * into words the caller zeroed. */
-#define MVS_BOUND_WORDS 64
+/* Bound words of a region tensor: MVS_BOUND_WORDS uint32 (8 KiB) holding maxima of |v| as fp32 bit
+ * patterns (the tensor's bound is their maximum), raised with atomic maxima by the kernel that writes
+ * the tensor into words the caller zeroed (64 slots, one per 128-byte line, so the atomics of different
+ * waves do not serialise on one line; the other words stay zero). */
+#define MVS_BOUND_WORDS 2048
 
 /* HOST function: the split-fp16 MFMA fragments of a region convolution's weight for
  * mvs_conv3d_region_split_fwd.  weight [27][c_out][c_in] fp32 HOST (mvs_conv3d_region_fwd's layout),

@@ -3,7 +3,10 @@ at cfg 2 (B=4, V=3, 512 x 640 images; refinement at 128 x 160, B=4), each layer 
 launches, HIP events), plus a checksum of every output so two library builds can be compared bit for bit
 (MVS_LIB_PATH selects the library).
 
-Usage: python tools/enc_layers.py [--reps N]
+Each layer CONV2D_SPLIT_SHAPES covers is also timed on the split-fp16 MFMA kernel (csrc/conv2d_split.hip)
+with its deviation from the fp32 kernel.
+
+Usage: python tools/enc_layers.py [--reps N]   (MVS_CONV2D_F16=0: the encoder total on the fp32 kernels)
 """
 import argparse
 import hashlib
@@ -28,7 +31,7 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(7)
-    total = 0.0
+    total = split_total = 0.0
     for cin, cout, k, s, n, h, w, calls in LAYERS:
         x = torch.randn(n, cin, h, w, generator=g).to(dev)
         wt = (torch.randn(cout, cin, k, k, generator=g) * 0.2).to(dev)
@@ -50,7 +53,44 @@ def main():
         digest = hashlib.sha1(y.cpu().numpy().tobytes()).hexdigest()[:12]
         print("conv2d %2d->%-2d k%d s%d n%-2d %3dx%-3d  %7.4f ms  %6.1f TF/s  x%d  sha %s"
               % (cin, cout, k, s, n, h, w, ms, fl / ms / 1e9, calls, digest), flush=True)
-    print("per eval step (x calls): %.4f ms" % total, flush=True)
+        if (cin, cout, k, s) in ops.CONV2D_SPLIT_SHAPES:
+            # the split-fp16 MFMA kernel (csrc/conv2d_split.hip) on the same input, its bound words set
+            xb = ops.bound_words(1, dev)[0]
+            xb[0] = x.abs().max().view(torch.int32)
+            fs = lambda: ops.conv2d_split(x, wt, s, xb, None, *bn)
+            ys = fs()
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(a.reps):
+                fs()
+            e1.record()
+            torch.cuda.synchronize()
+            mss = e0.elapsed_time(e1) / a.reps
+            split_total += (ms - mss) * calls
+            by = (x.numel() + ys.numel()) * 4
+            print("  split16 %7.4f ms  %6.0f GB/s  max|split - fp32| / max|y| %.2e"
+                  % (mss, by / mss / 1e6, ((ys - y).abs().max() / y.abs().max()).item()), flush=True)
+            yb = ops.bound_words(1, dev)[0]
+            fb = lambda: ops.conv2d_split(x, wt, s, xb, yb, *bn)
+            fb()
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(a.reps):
+                fb()
+            e1.record()
+            torch.cuda.synchronize()
+            print("  split16 raising y's bound words %7.4f ms" % (e0.elapsed_time(e1) / a.reps), flush=True)
+        yb = ops.bound_words(1, dev)[0]
+        fb = lambda: ops.conv2d(x, wt, s, *bn, y_bound=yb)
+        fb()
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(a.reps):
+            fb()
+        e1.record()
+        torch.cuda.synchronize()
+        print("  fp32 raising y's bound words %7.4f ms" % (e0.elapsed_time(e1) / a.reps), flush=True)
+    print("per eval step (x calls): %.4f ms; split16 saves %.4f ms" % (total, split_total), flush=True)
     dev_ = dev
     B, V, D, H, W = 4, 3, 192, 512, 640
     net = bench.build_model(D, H, W, dev_)
@@ -64,8 +104,9 @@ def main():
             net.feature_encoder(img)
         e1.record()
         torch.cuda.synchronize()
-    print("feature_encoder (B*V=12): %.4f ms  sha %s" % (e0.elapsed_time(e1) / a.reps,
-                                                          hashlib.sha1(f.cpu().numpy().tobytes()).hexdigest()[:12]))
+    print("feature_encoder (B*V=12, MVS_CONV2D_F16=%s): %.4f ms  sha %s"
+          % (os.environ.get("MVS_CONV2D_F16", "1"), e0.elapsed_time(e1) / a.reps,
+             hashlib.sha1(f.cpu().numpy().tobytes()).hexdigest()[:12]))
 
 
 if __name__ == "__main__":
