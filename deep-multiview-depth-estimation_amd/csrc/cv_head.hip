@@ -571,7 +571,7 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       const size_t vx = (((size_t)(oz - a.o0[0]) * a.on[1] + (oy - a.o0[1])) * a.on[2] + (ox - a.o0[2]));
       a.y1[(((size_t)b * a.on[0] * a.on[1] * a.on[2]) + vx) * 16 + i16] = v;
     }
-    if (a.y1_bound) bound_update(a.y1_bound, vmax);
+    if (a.y1_bound) bound_update<false>(a.y1_bound, vmax);   // mid-loop: no read-back
   };
 
   // conv_1_0 in step k: window zs - 1 completes (depth tap 2 on plane zs + 1), window zs + 1 starts

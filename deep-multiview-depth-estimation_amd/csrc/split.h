@@ -76,7 +76,13 @@ __device__ inline int act_split_exponent(float bound) {
   return min(max(14 - e, -120), 120);
 }
 
-// raise the bound words by this wave's max |v| (m >= 0 per lane; whole wave)
+// raise the bound words by this wave's max |v| (m >= 0 per lane; whole wave).  kCheck: read the slot
+// first (the read's round trip holds the wave: for epilogues at a kernel's end; a persistent kernel's
+// mid-loop update, cv_head.hip, sends the atomic unconditionally)
+#ifndef MVS_BOUND_CHECK
+#define MVS_BOUND_CHECK 1
+#endif
+template <bool kCheck = (MVS_BOUND_CHECK != 0)>
 __device__ inline void bound_update(uint32_t* __restrict__ words, float m) {
   uint32_t v = __float_as_uint(m);
 #pragma unroll
@@ -84,7 +90,7 @@ __device__ inline void bound_update(uint32_t* __restrict__ words, float m) {
   if ((threadIdx.x & 63) == 0) {
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     uint32_t* w = words + (wave % kBoundSlots) * kBoundStride;
-    if (v > __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(w, v);
+    if (!kCheck || v > __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(w, v);
   }
 }
 
