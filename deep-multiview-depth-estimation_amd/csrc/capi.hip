@@ -717,8 +717,15 @@ int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float
                                 const int* out_origin, const int* out_size, const int* in_origin, const int* in_size,
                                 const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                                 const unsigned* x_bound, const unsigned* x2_bound, unsigned* y_bound,
-                                const float* y_addend, void* stream) {
+                                const float* y_addend, const int* store_origin, const int* store_size, double* stats,
+                                void* stream) {
   if (!x || !weight_frag || !y || !dims || !out_origin || !out_size || batch <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if ((store_origin != nullptr) != (store_size != nullptr) || ((uintptr_t)stats & 7u)) return MVS_ERR_INVALID_ARGUMENT;
+  if (store_origin)   // the store box lies inside the output region
+    for (int k = 0; k < 3; ++k)
+      if (store_size[k] <= 0 || store_origin[k] < out_origin[k] ||
+          store_origin[k] + store_size[k] > out_origin[k] + out_size[k])
+        return MVS_ERR_INVALID_ARGUMENT;
   if (mode < MVS_CONV_S1 || mode > MVS_CONV_T2 ||
       (flags & ~(MVS_CONV_OUT_NCDHW | MVS_CONV_IN_C4 | MVS_CONV_IN_SPLIT | MVS_CONV_PER_LANE)))
     return MVS_ERR_INVALID_ARGUMENT;
@@ -756,9 +763,18 @@ int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float
       mode, (flags & MVS_CONV_OUT_NCDHW) != 0, x, x2, weight_frag, weight_exp, y, batch, c_in, c_out, dims, out_origin,
       out_size, io, is, pad, bn_scale, bn_shift, bn_mean, reinterpret_cast<const uint32_t*>(x_bound),
       reinterpret_cast<const uint32_t*>(x2_bound), reinterpret_cast<uint32_t*>(y_bound), (hipStream_t)stream,
-      (flags & MVS_CONV_PER_LANE) != 0, y_addend);
+      (flags & MVS_CONV_PER_LANE) != 0, y_addend, store_origin, store_size, stats);
   if (st != MVS_OK) return st;
   return lc.status();
+}
+
+long long mvs_conv3d_region_split_stats_slots(int mode, int flags, int batch, int c_in, int c_out,
+                                              const int* out_size) {
+  if (!out_size || batch <= 0 || mode < MVS_CONV_S1 || mode > MVS_CONV_T2) return MVS_ERR_INVALID_ARGUMENT;
+  for (int k = 0; k < 3; ++k)
+    if (out_size[k] <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  return mvs::conv3d_region_split_slots(mode, batch, c_in, c_out, out_size, (flags & MVS_CONV_PER_LANE) != 0,
+                                        (flags & MVS_CONV_SUM_INPUT) != 0);
 }
 
 
@@ -822,6 +838,22 @@ int mvs_channel_stats(const float* x, int layout, int batch, int channels, long 
   const mvs::LaunchCheck lc;
   mvs::launch_channel_stats(x, (layout & MVS_LAYOUT_CHANNELS_LAST) != 0, batch, channels, (size_t)voxels, stats,
                             (hipStream_t)stream);
+  return lc.status();
+}
+
+int mvs_bn_train_params(const double* sums, int channels, double count, const double* border_u,
+                        const double* border_count, int prev_channels, int classes, const float* prev_params,
+                        const float* weight, const float* bias, float* running_mean, float* running_var,
+                        long long* num_batches_tracked, double momentum, double eps, float* params, void* stream) {
+  if (!sums || !weight || !bias || !params || channels <= 0 || !(count > 0.0) || !(eps >= 0.0))
+    return MVS_ERR_INVALID_ARGUMENT;
+  if ((running_mean != nullptr) != (running_var != nullptr)) return MVS_ERR_INVALID_ARGUMENT;
+  if (border_u && (!border_count || !prev_params || prev_channels <= 0 || classes <= 0))
+    return MVS_ERR_INVALID_ARGUMENT;
+  const mvs::LaunchCheck lc;
+  mvs::launch_bn_train_params(sums, channels, count, border_u, border_count, prev_channels, classes, prev_params,
+                              weight, bias, running_mean, running_var, num_batches_tracked, momentum, eps, params,
+                              (hipStream_t)stream);
   return lc.status();
 }
 

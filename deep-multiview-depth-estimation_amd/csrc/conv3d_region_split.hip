@@ -43,7 +43,42 @@ struct GeoS {
   int pad[3];  // T2: P
   int out_cf;  // 1: output channels-first
   const float* addend;   // nullable: added to the output after BN + ReLU (same layout as y)
+  int sb0[3];  // store box (absolute voxel coordinates, inside the output region): y holds these
+  int sbn[3];  //   voxels only (the whole output region unless a box is given)
+  double* stats;   // nullable: per-workgroup float64 (sum, sum of squares) of every output voxel's
+                   // value, [slot][2][CO] (train-mode BatchNorm's batch sums; slots: split_stats_slots)
 };
+
+// per-workgroup channel sums: the wave's per-lane partial sums s / q (channel nb * 16 + (lane & 15) of
+// column block nb) reduced over the lanes of equal channel, then over the waves in a fixed order, and
+// written to stats[slot] (no atomics: the caller adds the slots in a fixed order -- run-to-run
+// bit-identical, as channel_ops.hip's sums).  Whole workgroup (a barrier).
+template <int CO, int NB, int NW>
+__device__ inline void stats_write(double (&s)[NB], double (&q)[NB], int nb0, int nbs, double* __restrict__ st) {
+  __shared__ double red[NW][2][CO];
+  const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+  for (int w = (int)threadIdx.x; w < NW * 2 * CO; w += (int)blockDim.x) (&red[0][0][0])[w] = 0.0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+      s[j] += __shfl_xor(s[j], o);
+      q[j] += __shfl_xor(q[j], o);
+    }
+    if (lane < 16 && j < nbs) {
+      red[wave][0][(nb0 + j) * 16 + lane] = s[j];
+      red[wave][1][(nb0 + j) * 16 + lane] = q[j];
+    }
+  }
+  __syncthreads();
+  for (int t = (int)threadIdx.x; t < 2 * CO; t += (int)blockDim.x) {
+    double a = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) a += (&red[w][0][0])[t];
+    st[t] = a;
+  }
+}
 
 __device__ inline void class_dim_s(int o0, int on, int p, int par, int& first, int& cnt) {
   first = o0 + (((o0 + p) & 1) != par ? 1 : 0);
@@ -86,7 +121,9 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_split_kernel(
   constexpr int kRows = 16 * RB;
   const int bx = xcd_work_id((int)blockIdx.x, (int)gridDim.x);
   const int row0 = (bx * (kBlock / 64) + ((int)threadIdx.x >> 6)) * kRows;
-  if (row0 >= rows) return;   // wave-uniform; no barriers in this kernel
+  // wave-uniform; no barriers in this kernel unless sums are gathered (then every wave stays, the
+  // ones past the rows on zeros)
+  if (row0 >= rows && !g.stats) return;
 
   // the input's scale: max|x| (+ max|x2|) 2^ex < 2^14; S2: the split volume's own exponent
   int ex;
@@ -224,13 +261,15 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_split_kernel(
   // ---- epilogue: unscale, eval BN + ReLU, store; the output's bound words.  acc[rb][nb][r] = (row
   // (lane >> 4) * 4 + r, column lane & 15)
   const int oexp = -(ex + w_exp);
-  const size_t orvol = (size_t)g.on[0] * g.on[1] * g.on[2];
+  const size_t orvol = (size_t)g.sbn[0] * g.sbn[1] * g.sbn[2];
   float vmax = 0.0f;
+  double ss[NB], sq[NB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     const int co = nb * 16 + m;
     const float sc = bn_scale ? bn_scale[co] : 1.0f, sh = bn_scale ? bn_shift[co] : 0.0f,
                 mu = bn_scale ? bn_mean[co] : 0.0f;
+    ss[nb] = sq[nb] = 0.0;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -239,31 +278,44 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_split_kernel(
         if (row >= rows) continue;
         const int jx = row % cn[2], t = row / cn[2];
         const int jy = t % cn[1], jz = t / cn[1];
-        const int vz = cf[0] + step * jz - g.o0[0], vy = cf[1] + step * jy - g.o0[1],
-                  vxx = cf[2] + step * jx - g.o0[2];
+        const int vz = cf[0] + step * jz - g.sb0[0], vy = cf[1] + step * jy - g.sb0[1],
+                  vxx = cf[2] + step * jx - g.sb0[2];
         float v = ldexpf(acc[rb][nb][r], oexp);
         if (bn_scale) v = fmaxf((v - mu) * sc + sh, 0.0f);
-        const size_t vox = ((size_t)vz * g.on[1] + vy) * g.on[2] + vxx;
+        const bool keep = vz >= 0 && vz < g.sbn[0] && vy >= 0 && vy < g.sbn[1] && vxx >= 0 && vxx < g.sbn[2];
+        const size_t vox = ((size_t)vz * g.sbn[1] + vy) * g.sbn[2] + vxx;
         const size_t oi = g.out_cf ? ((size_t)b * CO + co) * orvol + vox : ((size_t)b * orvol + vox) * CO + co;
-        if (g.addend) v += g.addend[oi];
+        if (g.addend && keep) v += g.addend[oi];
+        ss[nb] += (double)v;
+        sq[nb] += (double)v * (double)v;
+        if (!keep) continue;
         vmax = fmaxf(vmax, fabsf(v));
         y[oi] = v;
       }
   }
   if (yb) bound_update(yb, vmax);
+  if (g.stats) {
+    const size_t slot = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    stats_write<CO, NB, kBlock / 64>(ss, sq, 0, NB, g.stats + slot * 2 * CO);
+  }
+}
+
+// the per-lane kernel's grid: (row chunks of a parity class, rounded to the 8 XCDs) x classes x batch
+inline dim3 split_mode_grid(int mode, int RB, int B, const int* on) {
+  const int classes = mode == kT2 ? 8 : 1;
+  const int rz = mode == kT2 ? (on[0] + 1) / 2 : on[0], ry = mode == kT2 ? (on[1] + 1) / 2 : on[1],
+            rx = mode == kT2 ? (on[2] + 1) / 2 : on[2];
+  const long rows = (long)rz * ry * rx;
+  const long per_block = (kBlock / 64) * 16 * RB;
+  const long blocks = (rows + per_block - 1) / per_block;
+  return dim3((unsigned)((blocks + 7) / 8 * 8), (unsigned)classes, (unsigned)B);
 }
 
 template <int MODE, int CI, int CO, int RB>
 void launch_split_mode(const float* x, const float* x2, const void* wf, int w_exp, float* y, const float* sc,
                        const float* sh, const float* mu, int B, const GeoS& g, const uint32_t* xb,
                        const uint32_t* xb2, uint32_t* yb, hipStream_t s) {
-  const int classes = MODE == kT2 ? 8 : 1;
-  const int rz = MODE == kT2 ? (g.on[0] + 1) / 2 : g.on[0], ry = MODE == kT2 ? (g.on[1] + 1) / 2 : g.on[1],
-            rx = MODE == kT2 ? (g.on[2] + 1) / 2 : g.on[2];
-  const int rows = rz * ry * rx;
-  const int per_block = (kBlock / 64) * 16 * RB;
-  const int blocks = (rows + per_block - 1) / per_block;
-  const dim3 grid((unsigned)((blocks + 7) / 8 * 8), (unsigned)classes, (unsigned)B);
+  const dim3 grid = split_mode_grid(MODE, RB, B, g.on);
   hipLaunchKernelGGL((conv3d_region_split_kernel<MODE, CI, CO, RB>), grid, dim3(kBlock), 0, s, x, x2,
                      reinterpret_cast<const h8v*>(wf), w_exp, y, sc, sh, mu, g, xb, xb2, yb);
 }
@@ -308,7 +360,8 @@ __global__ __launch_bounds__(kBlock) void conv3d_s1_split_lds_kernel(
   __shared__ __attribute__((aligned(16))) char lds[T::LDS];
 
   int t = xcd_work_id((int)blockIdx.x, (int)gridDim.x);
-  if (t >= tiles_x * tiles_y * tiles_z) return;   // workgroup-uniform, before the barrier
+  if (t >= tiles_x * tiles_y * tiles_z) return;   // workgroup-uniform, before the barriers
+  const int t0 = t;
   const int tx0 = (t % tiles_x) * 16;
   t /= tiles_x;
   const int ty0 = (t % tiles_y) * 4;
@@ -405,33 +458,51 @@ __global__ __launch_bounds__(kBlock) void conv3d_s1_split_lds_kernel(
   const int co = nb * 16 + m;
   const float sc = bn_scale ? bn_scale[co] : 1.0f, sh = bn_scale ? bn_shift[co] : 0.0f,
               mu = bn_scale ? bn_mean[co] : 0.0f;
-  const size_t orvol = (size_t)g.on[0] * g.on[1] * g.on[2];
+  const size_t orvol = (size_t)g.sbn[0] * g.sbn[1] * g.sbn[2];
   float vmax = 0.0f;
+  double ss[1] = {0.0}, sq[1] = {0.0};
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
     const int rbi = rg * RB + r, zz = rbi >> 2, yy = rbi & 3;
-    const int vz = tz0 + zz, vy = ty0 + yy;
-    if (vz >= g.on[0] || vy >= g.on[1]) continue;
+    if (tz0 + zz >= g.on[0] || ty0 + yy >= g.on[1]) continue;
+    // store-box-relative coordinates
+    const int vz = g.o0[0] + tz0 + zz - g.sb0[0], vy = g.o0[1] + ty0 + yy - g.sb0[1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int vx = tx0 + 4 * kq + i;
-      if (vx >= g.on[2]) continue;
+      if (tx0 + 4 * kq + i >= g.on[2]) continue;
+      const int vx = g.o0[2] + tx0 + 4 * kq + i - g.sb0[2];
       float v = ldexpf(acc[r][i], oexp);
       if (bn_scale) v = fmaxf((v - mu) * sc + sh, 0.0f);
-      const size_t vox = ((size_t)vz * g.on[1] + vy) * g.on[2] + vx;
+      const bool keep = vz >= 0 && vz < g.sbn[0] && vy >= 0 && vy < g.sbn[1] && vx >= 0 && vx < g.sbn[2];
+      const size_t vox = ((size_t)vz * g.sbn[1] + vy) * g.sbn[2] + vx;
       const size_t oi = g.out_cf ? ((size_t)b * CO + co) * orvol + vox : ((size_t)b * orvol + vox) * CO + co;
-      if (g.addend) v += g.addend[oi];
+      if (g.addend && keep) v += g.addend[oi];
+      ss[0] += (double)v;
+      sq[0] += (double)v * (double)v;
+      if (!keep) continue;
       vmax = fmaxf(vmax, fabsf(v));
       y[oi] = v;
     }
   }
   if (yb) bound_update(yb, vmax);
+  if (g.stats) {
+    const size_t slot = (size_t)b * (tiles_x * tiles_y * tiles_z) + t0;
+    stats_write<CO, 1, kBlock / 64>(ss, sq, nb, 1, g.stats + slot * 2 * CO);
+  }
+}
+
+template <int CI>
+void s1_lds_tiles(const int* on, int& tx, int& ty, int& tz) {
+  tx = (on[2] + 15) / 16;
+  ty = (on[1] + 3) / 4;
+  tz = (on[0] + S1Tile<CI>::TZ - 1) / S1Tile<CI>::TZ;
 }
 
 template <int CI>
 void launch_s1_lds(const float* x, const void* wf, int w_exp, float* y, const float* sc, const float* sh,
                    const float* mu, int B, const GeoS& g, const uint32_t* xb, uint32_t* yb, hipStream_t s) {
-  const int tx = (g.on[2] + 15) / 16, ty = (g.on[1] + 3) / 4, tz = (g.on[0] + S1Tile<CI>::TZ - 1) / S1Tile<CI>::TZ;
+  int tx, ty, tz;
+  s1_lds_tiles<CI>(g.on, tx, ty, tz);
   const int per = tx * ty * tz;
   const dim3 grid((unsigned)((per + 7) / 8 * 8), (unsigned)B);
   hipLaunchKernelGGL((conv3d_s1_split_lds_kernel<CI, CI>), grid, dim3(kBlock), 0, s, x,
@@ -442,34 +513,6 @@ void launch_s1_lds(const float* x, const void* wf, int w_exp, float* y, const fl
 
 int conv3d_region_split_kblocks(int c_in) { return c_in == 16 ? 14 : 27 * (c_in / 32); }
 
-int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const float* x2, const void* wfrag, int w_exp,
-                               float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on,
-                               const int* i0, const int* in, const int* pad, const float* bn_scale,
-                               const float* bn_shift, const float* bn_mean, const uint32_t* x_bound,
-                               const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s, bool per_lane,
-                               const float* y_addend) {
-  GeoS g;
-  g.out_cf = out_cf ? 1 : 0;
-  g.addend = y_addend;
-  for (int d = 0; d < 3; ++d) {
-    g.n[d] = n[d];
-    g.o0[d] = o0[d];
-    g.on[d] = on[d];
-    g.i0[d] = i0[d];
-    g.in[d] = in[d];
-    g.pad[d] = pad ? pad[d] : 1;
-  }
-// row blocks per wave: 4 for the stride-1 convs (each weight fragment feeds 4 row blocks), 2 for the
-// transposed and stride-2 ones (measured at cfg 2, eval and train mode: S1 64 -> 64 2.70 -> 2.41 ms,
-// T2 32 -> 16 2.02 against 2.36 with 4; 1 row block is slower everywhere)
-#define MVS_RSPLIT_CASE(MD, A, C)                                                                         \
-  if (mode == MD && CI == A && CO == C) {                                                                 \
-    launch_split_mode<MD, A, C, MD == kS1 ? 4 : 2>(x, x2, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, \
-                                                   x_bound, x2_bound, y_bound, s);                        \
-    return MVS_OK;                                                                                        \
-  }
-  // S1: conv_k_1 (16 / 32 / 64 channels; LDS-staged operands per MVS_S1_LDS); T2: deconv_3_0 (64 -> 32),
-  // deconv_2_0 (32 -> 16); S2: conv_k_0 from the split cost volume (32 -> 16 / 32 / 64)
 // bit 0 / 1 / 2: the LDS-staged kernel for 16 / 32 / 64 channels.  Measured per cfg-2 step (eval /
 // train mode): 16 ch 0.37 -> 0.27 / 0.35 -> 0.26 ms, 32 ch 0.18 -> 0.17 / 0.97 -> 0.93 ms; 64 ch slower
 // (0.11 -> 0.13 / 2.41 -> 2.81 ms: its 110 KB tile allows one workgroup per CU).  An LDS-staged
@@ -478,8 +521,58 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
 #ifndef MVS_S1_LDS
 #define MVS_S1_LDS 3
 #endif
+static bool split_uses_lds(int mode, int CI, int CO, bool per_lane, bool has_x2) {
   const int ci_bit = CI == 16 ? 1 : (CI == 32 ? 2 : (CI == 64 ? 4 : 0));
-  if ((MVS_S1_LDS & ci_bit) && !per_lane && mode == kS1 && CI == CO && !x2) {
+  return (MVS_S1_LDS & ci_bit) && !per_lane && mode == kS1 && CI == CO && !has_x2;
+}
+
+// row blocks per wave of the per-lane kernel: 4 for the stride-1 convs (each weight fragment feeds 4 row
+// blocks), 2 for the transposed and stride-2 ones (measured at cfg 2, eval and train mode: S1 64 -> 64
+// 2.70 -> 2.41 ms, T2 32 -> 16 2.02 against 2.36 with 4; 1 row block is slower everywhere)
+static int split_rb(int mode) { return mode == kS1 ? 4 : 2; }
+
+long conv3d_region_split_slots(int mode, int B, int CI, int CO, const int* on, bool per_lane, bool has_x2) {
+  if (split_uses_lds(mode, CI, CO, per_lane, has_x2)) {
+    int tx, ty, tz;
+    if (CI == 16) s1_lds_tiles<16>(on, tx, ty, tz);
+    else if (CI == 32) s1_lds_tiles<32>(on, tx, ty, tz);
+    else s1_lds_tiles<64>(on, tx, ty, tz);
+    return (long)B * tx * ty * tz;
+  }
+  const dim3 gr = split_mode_grid(mode, split_rb(mode), B, on);
+  return (long)gr.x * gr.y * gr.z;
+}
+
+int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const float* x2, const void* wfrag, int w_exp,
+                               float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on,
+                               const int* i0, const int* in, const int* pad, const float* bn_scale,
+                               const float* bn_shift, const float* bn_mean, const uint32_t* x_bound,
+                               const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s, bool per_lane,
+                               const float* y_addend, const int* store_origin, const int* store_size,
+                               double* stats) {
+  GeoS g;
+  g.out_cf = out_cf ? 1 : 0;
+  g.addend = y_addend;
+  g.stats = stats;
+  for (int d = 0; d < 3; ++d) {
+    g.n[d] = n[d];
+    g.o0[d] = o0[d];
+    g.on[d] = on[d];
+    g.i0[d] = i0[d];
+    g.in[d] = in[d];
+    g.pad[d] = pad ? pad[d] : 1;
+    g.sb0[d] = store_origin ? store_origin[d] : o0[d];
+    g.sbn[d] = store_origin ? store_size[d] : on[d];
+  }
+#define MVS_RSPLIT_CASE(MD, A, C)                                                                         \
+  if (mode == MD && CI == A && CO == C) {                                                                 \
+    launch_split_mode<MD, A, C, MD == kS1 ? 4 : 2>(x, x2, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, \
+                                                   x_bound, x2_bound, y_bound, s);                        \
+    return MVS_OK;                                                                                        \
+  }
+  // S1: conv_k_1 (16 / 32 / 64 channels; LDS-staged operands per MVS_S1_LDS); T2: deconv_3_0 (64 -> 32),
+  // deconv_2_0 (32 -> 16); S2: conv_k_0 from the split cost volume (32 -> 16 / 32 / 64)
+  if (split_uses_lds(mode, CI, CO, per_lane, x2 != nullptr)) {
     if (CI == 16) launch_s1_lds<16>(x, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, y_bound, s);
     else if (CI == 32) launch_s1_lds<32>(x, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, y_bound, s);
     else launch_s1_lds<64>(x, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, y_bound, s);

@@ -138,13 +138,21 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
                          const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                          hipStream_t s, const uint32_t* absmax = nullptr, uint32_t* y_bound = nullptr);
 // the S1 / T2 region convolutions on split-fp16 MFMA (conv3d_region_split.hip); K-32 weight blocks
+// channel_ops.hip: train-mode BatchNorm parameters (+ running statistics) from the batch sums
+void launch_bn_train_params(const double* sums, int C, double count, const double* bu, const double* bcnt, int Cp,
+                            int ncls, const float* prev, const float* w, const float* bias, float* rmean, float* rvar,
+                            long long* nbt, double momentum, double eps, float* params, hipStream_t s);
+
 int conv3d_region_split_kblocks(int c_in);
 int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const float* x2, const void* wfrag, int w_exp,
                                float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on,
                                const int* i0, const int* in, const int* pad, const float* bn_scale,
                                const float* bn_shift, const float* bn_mean, const uint32_t* x_bound,
                                const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s, bool per_lane = false,
-                               const float* y_addend = nullptr);
+                               const float* y_addend = nullptr, const int* store_origin = nullptr,
+                               const int* store_size = nullptr, double* stats = nullptr);
+// workgroups (= float64 sum slots) of the launch launch_conv3d_region_split makes for these arguments
+long conv3d_region_split_slots(int mode, int B, int CI, int CO, const int* on, bool per_lane, bool has_x2);
 
 // channel_ops.hip: train-mode BatchNorm pieces -- per-channel float64 sums into
 // stats[slot][2][C] (64 slots) and y = relu(BN(x)) [+ relu(BN'(r))], channels-last or NCDHW

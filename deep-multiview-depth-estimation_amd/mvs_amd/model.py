@@ -89,7 +89,7 @@ def _run_stack(seq, x):
                 return _run_tail(layers[i:], x)
             if bn.training:
                 y = conv(layer, x, xb, None)[0].contiguous()
-                x = bn_relu_(y, False, *_bn_train(bn, *channel_stats(y, False), y.numel() // y.shape[1]),
+                x = bn_relu_(y, False, *_bn_train_hip(bn, *channel_stats(y, False), y.numel() // y.shape[1]),
                              y_bound=yb)
                 bounded = yb is not None
             else:   # eval BN + ReLU fused into the convolution's epilogue
@@ -493,7 +493,7 @@ class CostVolumeReg(nn.Module):
         the full output volume (their statistics) and keep the M-region part.  ``cv`` may be the
         channel-quad volume (conv_0_0 and the stride-2 convs read it with 16-byte loads)."""
         from .ops import (CONV_S1, CONV_S2, CONV_T2, bn_relu_, bound_words, channel_stats, conv3d_k3,
-                          conv3d_k3_split, conv3d_region, conv3d_region_split, deconv3d_k3s2, region_weight,
+                          conv3d_k3_split, conv3d_region, conv3d_region_split_sums, deconv3d_k3s2, region_weight,
                           softmax_depth)
         c4 = cv.dim() == 6
         # with split_f16 the stride-1 and transposed convs run on the split-fp16 matrix cores
@@ -517,72 +517,75 @@ class CostVolumeReg(nn.Module):
                 y0 = conv3d_k3_split(cv, bound, self.conv_0_0.weight)
             else:
                 y0 = conv3d_k3(cv, self.conv_0_0.weight, in_c4=c4, wino_z=True)
-            p0 = _bn_train(self.BN_0, *channel_stats(y0, False), count)
+            p0 = _bn_train_hip(self.BN_0, *channel_stats(y0, False), count)
         cv.record_stream(side)
         stage = []
         for k, (conv_a, bn) in enumerate(((self.conv_1_0, self.BN_1), (self.conv_2_0, self.BN_2),
                                           (self.conv_3_0, self.BN_3))):
-            if cv.dtype == torch.int32:   # the split volume: conv_k_0 on the split-fp16 matrix cores
-                z = conv3d_region_split(cv, None, region_weight(conv_a), CONV_S2, dims, org(R2), size(R2), None,
-                                        None, pad, bound, None, None)
+            if cv.dtype == torch.int32:   # the split volume: conv_k_0 on the split-fp16 matrix cores, the
+                # batch sums formed in its epilogue
+                z, s1, s2 = conv3d_region_split_sums(cv, None, region_weight(conv_a), CONV_S2, dims, org(R2),
+                                                     size(R2), None, None, pad, bound)
             else:
                 z = conv3d_region(cv, None, region_weight(conv_a), CONV_S2, dims, org(R2), size(R2), None, None,
                                   pad, in_c4=c4)
-            p = _bn_train(bn, *channel_stats(z, True), count)
-            stage.append((bn_relu_(z, True, *p, y_bound=bwr(k)), _bn_constant(p)))
+                s1, s2 = channel_stats(z, True)
+            p = _bn_train_hip(bn, s1, s2, count)
+            stage.append((bn_relu_(z, True, *p, y_bound=bwr(k)), p))   # p: relu(BN(0)) outside M
         lv = []
-        for k, ((y, a), conv_b, bn) in enumerate(zip(stage, (self.conv_1_1, self.conv_2_1, self.conv_3_1),
+        for k, ((y, pa), conv_b, bn) in enumerate(zip(stage, (self.conv_1_1, self.conv_2_1, self.conv_3_1),
                                                      (self.BN_1, self.BN_2, self.BN_3))):
             # level 1 only feeds deconv_1_0's input sum: channels-first for its loads
             cf = bn is self.BN_1
-            if bw is not None:
-                z = conv3d_region_split(y, None, region_weight(conv_b), CONV_S1, dims, org(R1), size(R1), org(R2),
-                                        size(R2), None, bw[k], None, None, out_ncdhw=cf)
+            if bw is not None:   # sums over R1 in the epilogue, only M stored (the next layers read M)
+                z, s1, s2 = conv3d_region_split_sums(y, None, region_weight(conv_b), CONV_S1, dims, org(R1),
+                                                     size(R1), org(R2), size(R2), None, bw[k], out_ncdhw=cf,
+                                                     store_origin=org(M), store_size=size(M))
             else:
                 z = conv3d_region(y, None, region_weight(conv_b), CONV_S1, dims, org(R1), size(R1), org(R2),
                                   size(R2), None, out_ncdhw=cf)
-            s1, s2 = channel_stats(z, not cf)
-            c1, c2 = _border_class_sums(conv_b.weight, a, R1, n, bsz)
-            p = _bn_train(bn, s1 + c1, s2 + c2, count)
-            lv.append(bn_relu_((_crop_cf if cf else _crop_cl)(z, R1, M), not cf, *p,
-                               y_bound=None if cf else bwr(3 + k)))
+                s1, s2 = channel_stats(z, not cf)
+                z = (_crop_cf if cf else _crop_cl)(z, R1, M)
+            p = _bn_train_hip(bn, s1, s2, count, border=(conv_b.weight, R1, n, bsz, pa))
+            lv.append(bn_relu_(z, not cf, *p, y_bound=None if cf else bwr(3 + k)))
         y1, y2, y3 = lv
         if bw is not None:
-            z = conv3d_region_split(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, [0, 0, 0], dims,
-                                    org(M), size(M), pad, bw[5], None, None)
-        else:
-            z = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
-                              size(M), pad)
-        p = _bn_train(self.BN_2, *channel_stats(z, True), count)
-        if bw is not None:
+            # the transposed convs over the full output (their batch sums, formed in the epilogue), only
+            # M stored: the next layer reads M
+            z, s1, s2 = conv3d_region_split_sums(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims,
+                                                 [0, 0, 0], dims, org(M), size(M), pad, bw[5],
+                                                 store_origin=org(M), store_size=size(M))
+            p = _bn_train_hip(self.BN_2, s1, s2, count)
             # relu(BN_2(deconv_3_0)) + y2 (model.py:119) formed in the BN pass: y2 >= 0 (a ReLU output), so
             # relu((y2 - 0) * 1 + 0) is y2 exactly; deconv_2_0 then reads one tensor
             c2 = y2.shape[-1]
             one, zero = torch.ones(c2, device=y2.device), torch.zeros(c2, device=y2.device)
-            y3 = bn_relu_(_crop_cl(z, full, M), True, *p, r=y2, r_bn=(one, zero, zero), y_bound=bw[6])
-            del z
-            z = conv3d_region_split(y3, None, region_weight(self.deconv_2_0), CONV_T2, dims, [0, 0, 0], dims,
-                                    org(M), size(M), pad, bw[6], None, None, out_ncdhw=True)
+            y3 = bn_relu_(z, True, *p, r=y2, r_bn=(one, zero, zero), y_bound=bw[6])
+            z, s1, s2 = conv3d_region_split_sums(y3, None, region_weight(self.deconv_2_0), CONV_T2, dims,
+                                                 [0, 0, 0], dims, org(M), size(M), pad, bw[6], out_ncdhw=True,
+                                                 store_origin=org(M), store_size=size(M))
+            p = _bn_train_hip(self.BN_1, s1, s2, count)
+            # relu(BN_1(deconv_2_0)) + y1 (model.py:121) formed in the BN pass (y1 >= 0: exact, as above)
+            c1 = y1.shape[1]
+            one, zero = torch.ones(c1, device=y1.device), torch.zeros(c1, device=y1.device)
+            y2 = bn_relu_(z, False, *p, r=y1, r_bn=(one, zero, zero))
+            y1 = None
         else:
+            z = conv3d_region(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
+                              size(M), pad)
+            p = _bn_train_hip(self.BN_2, *channel_stats(z, True), count)
             y3 = bn_relu_(_crop_cl(z, full, M), True, *p)
             del z
             z = conv3d_region(y3, y2, region_weight(self.deconv_2_0), CONV_T2, dims, [0, 0, 0], dims, org(M),
                               size(M), pad, out_ncdhw=True)
-        p = _bn_train(self.BN_1, *channel_stats(z, False), count)
-        if bw is not None:
-            # relu(BN_1(deconv_2_0)) + y1 (model.py:121) formed in the BN pass (y1 >= 0: exact, as above)
-            c1 = y1.shape[1]
-            one, zero = torch.ones(c1, device=y1.device), torch.zeros(c1, device=y1.device)
-            y2 = bn_relu_(_crop_cf(z, full, M), False, *p, r=y1, r_bn=(one, zero, zero))
-            y1 = None
-        else:
+            p = _bn_train_hip(self.BN_1, *channel_stats(z, False), count)
             y2 = bn_relu_(_crop_cf(z, full, M), False, *p)
         del z
         z = deconv3d_k3s2(y2, org(M), self.deconv_1_0.weight, dims, pad, None, None, None, None, x2=y1)
         main.wait_stream(side)
         for t in (y0,) + tuple(p0):
             t.record_stream(main)
-        p = _bn_train(self.BN_0, *channel_stats(z, False), count)
+        p = _bn_train_hip(self.BN_0, *channel_stats(z, False), count)
         z = bn_relu_(z, False, *p, r=y0, r_bn=p0)   # relu(BN_0(deconv_1_0)) + relu(BN_0'(conv_0_0))
         return softmax_depth(conv3d_k3(z, self.conv_out.weight))
 
@@ -705,6 +708,41 @@ def _apply_bn(y, scale, shift, mean):
     return (y - v(mean)) * v(scale) + v(shift)
 
 
+def _bn_train_hip(bn, s1, s2, count, border=None):
+    """_bn_train on the HIP path as ONE launch (ops.bn_train_params), returning the [3, C] parameters
+    (scale, shift, mean); ``border``: None or (weight, region, n, batch, prev) -- conv_k_1's
+    border-class term (_border_class_sums) with the previous BN's parameters ``prev``.  momentum=None
+    (the cumulative average) takes the device-op path."""
+    from .ops import bn_train_params
+    if bn.momentum is None:
+        if border is not None:
+            weight, reg, n, bsz, prev = border
+            c1, c2 = _border_class_sums(weight, _bn_constant(tuple(prev)), reg, n, bsz)
+            s1, s2 = s1 + c1, s2 + c2
+        return torch.stack([t.detach().float() for t in _bn_train(bn, s1, s2, count)])
+    b = None
+    if border is not None:
+        weight, reg, n, bsz, prev = border
+        b = _border_tables_u(weight, reg, n, bsz) + (prev,)
+    return bn_train_params(bn, s1, s2, count, b)
+
+
+def _border_tables_u(weight, reg, n, bsz):
+    """(U [C_out, C_in, K], counts [K]) of _border_class_sums for the K border classes outside reg:
+    U[o][i][k] = the sum of weight[o][i] over class k's in-volume taps (float64), counts = voxels of the
+    class outside reg over the batch -- cached per weight state (ops.derived), so a forward only forms
+    u = U a (mvs_bn_train_params)."""
+    from .ops import derived
+
+    def build(w):
+        masks, cnt, inside = _border_class_tables(tuple(n), tuple(reg), w.device)
+        u = torch.einsum("oiabc,xa,yb,zc->oixyz", w.detach().double(), masks[0], masks[1], masks[2])
+        outer = lambda v: v[0].view(-1, 1, 1) * v[1].view(1, -1, 1) * v[2].view(1, 1, -1)
+        count = bsz * (outer(cnt) - outer(inside))
+        return u.reshape(u.shape[0], u.shape[1], -1).contiguous(), count.reshape(-1).contiguous()
+    return derived(("border_u", tuple(reg), tuple(n), int(bsz)), (weight,), build, weight.device)
+
+
 def _bn_constant(p):
     """relu(BN(0)) per channel: the value of a BN + ReLU output where its input is exactly 0."""
     scale, shift, mean = p
@@ -719,6 +757,29 @@ def _border_classes(d, lo, hi):
     return [(taps, b - a + 1, max(0, min(b, hi) - max(a, lo) + 1)) for a, b, taps in spans]
 
 
+_CLASS_TABLES = {}
+
+
+def _border_class_tables(n, reg, device):
+    """Per dim: (tap masks [classes, 3], class voxel counts, of them inside reg) as float64 device
+    tensors, cached per (volume, region, device): formed once instead of by host-to-device copies in
+    every train-mode forward (pageable copies stall the host's run-ahead)."""
+    key = (n, reg, str(device))
+    hit = _CLASS_TABLES.get(key)
+    if hit is None:
+        masks, cnt, inside = [], [], []
+        for d, (lo, hi) in zip(n, reg):
+            classes = _border_classes(d, lo, hi)
+            masks.append(torch.tensor([[1.0 if k in taps else 0.0 for k in range(3)] for taps, _, _ in classes],
+                                      dtype=torch.float64, device=device))
+            cnt.append(torch.tensor([c for _, c, _ in classes], dtype=torch.float64, device=device))
+            inside.append(torch.tensor([i for _, _, i in classes], dtype=torch.float64, device=device))
+        if len(_CLASS_TABLES) > 64:
+            _CLASS_TABLES.clear()
+        hit = _CLASS_TABLES[key] = (masks, cnt, inside)
+    return hit
+
+
 def _border_class_sums(weight, a, reg, n, bsz):
     """Sums (value, value^2) per output channel of conv3d(field, weight, padding 1) over the
     voxels OUTSIDE reg, where the input field is the per-channel constant a everywhere the
@@ -726,13 +787,7 @@ def _border_class_sums(weight, a, reg, n, bsz):
     voxel's border class: sum_ci a[ci] * sum_(in-volume taps) weight[co, ci, tap].  All classes
     at once (a few device ops, no per-class launches)."""
     w = weight.double()
-    per_dim = [_border_classes(d, lo, hi) for d, (lo, hi) in zip(n, reg)]
-    masks, cnt, inside = [], [], []
-    for classes in per_dim:
-        masks.append(torch.tensor([[1.0 if k in taps else 0.0 for k in range(3)] for taps, _, _ in classes],
-                                  dtype=torch.float64, device=w.device))
-        cnt.append(torch.tensor([c for _, c, _ in classes], dtype=torch.float64, device=w.device))
-        inside.append(torch.tensor([i for _, _, i in classes], dtype=torch.float64, device=w.device))
+    masks, cnt, inside = _border_class_tables(tuple(n), tuple(reg), w.device)
     # the constant field's response summed over each class's in-volume taps
     wa = torch.einsum("oiabc,i->oabc", w, a.double())    # the field's response per tap
     u = torch.einsum("oabc,zc->oabz", wa, masks[2])

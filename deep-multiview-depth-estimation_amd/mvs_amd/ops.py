@@ -1146,14 +1146,18 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
                         x2_bound: Optional[torch.Tensor], y_bound: Optional[torch.Tensor],
                         bn_scale: Optional[torch.Tensor] = None, bn_shift: Optional[torch.Tensor] = None,
                         bn_mean: Optional[torch.Tensor] = None, out_ncdhw: bool = False,
-                        per_lane: bool = False, y_addend: Optional[torch.Tensor] = None) -> torch.Tensor:
+                        per_lane: bool = False, y_addend: Optional[torch.Tensor] = None,
+                        store_origin: Optional[list[int]] = None, store_size: Optional[list[int]] = None,
+                        stats: Optional[torch.Tensor] = None) -> torch.Tensor:
     """conv3d_region's CONV_S1 / CONV_T2 convolutions on the f16 matrix cores with split operands
     (mvs_conv3d_region_split_fwd, csrc/conv3d_region_split.hip): same geometry, layouts and epilogue;
     the input scaled by its bound words ``x_bound`` (+ ``x2_bound`` for the sum x + x2), ``y_bound``
     (zeroed words or None) raised to max|y|.  ``y_addend``: added to the output after BN + ReLU (same
     shape and layout as y).  CONV_S2: x is the split cost volume (int32 [B, 8, D, H, W,
-    4], or a box of it with in_origin / in_size), x_bound its 8 bound words.  fp32-level error
-    (DESIGN.md §3.8).  Inference only."""
+    4], or a box of it with in_origin / in_size), x_bound its 8 bound words.  ``store_origin`` /
+    ``store_size``: y holds only that box of the output region (the rest is computed, not stored);
+    ``stats``: float64 [split_stats_slots, 2, c_out] receiving per-workgroup sums over the whole
+    output region (conv3d_region_split_sums).  fp32-level error.  Inference only."""
     _require_gpu(x, "x")
     lib = _lib.load()
     flags = (_lib.MVS_CONV_OUT_NCDHW if out_ncdhw else 0) | (_lib.MVS_CONV_PER_LANE if per_lane else 0)
@@ -1173,9 +1177,14 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
     bn = [t if t is None else t.to(device=dev, dtype=_F32).contiguous() for t in (bn_scale, bn_shift, bn_mean)]
     if any(t is None for t in bn) and not all(t is None for t in bn):
         raise ValueError("bn_scale, bn_shift and bn_mean go together")
-    shape = (b, cout) + tuple(out_size) if out_ncdhw else (b,) + tuple(out_size) + (cout,)
+    ysz = tuple(out_size if store_size is None else store_size)
+    shape = (b, cout) + ysz if out_ncdhw else (b,) + ysz + (cout,)
     y = torch.empty(shape, device=dev, dtype=_F32)
     xb = (_lib.ptr(x_bound.contiguous()) if mode == CONV_S2 else _bound_ptr(x_bound))
+    if stats is not None:
+        slots = split_stats_slots(mode, b, cin, cout, out_size, per_lane, x2 is not None)
+        if stats.dtype != torch.float64 or stats.numel() != slots * 2 * cout or not stats.is_contiguous():
+            raise ValueError("stats: a contiguous float64 tensor of %d x 2 x %d" % (slots, cout))
     ya = None
     if y_addend is not None:
         if tuple(y_addend.shape) != tuple(y.shape) or y_addend.dtype != _F32 or not y_addend.is_contiguous():
@@ -1188,17 +1197,49 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
                                          None if in_size is None else _ints3(in_size),
                                          None if pad is None else _ints3(pad),
                                          *[None if t is None else _lib.ptr(t) for t in bn], xb,
-                                         _bound_ptr(x2_bound), _bound_ptr(y_bound), ya, _lib.stream_handle(dev))
+                                         _bound_ptr(x2_bound), _bound_ptr(y_bound), ya,
+                                         None if store_origin is None else _ints3(store_origin),
+                                         None if store_size is None else _ints3(store_size),
+                                         None if stats is None else _lib.ptr(stats), _lib.stream_handle(dev))
     _lib.check(st, "mvs_conv3d_region_split_fwd")
     return y
 
 
+def split_stats_slots(mode, batch, c_in, c_out, out_size, per_lane=False, two_inputs=False):
+    """Sum slots (workgroups) of a conv3d_region_split launch (mvs_conv3d_region_split_stats_slots)."""
+    flags = (_lib.MVS_CONV_PER_LANE if per_lane else 0) | (_lib.MVS_CONV_SUM_INPUT if two_inputs else 0)
+    n = _lib.load().mvs_conv3d_region_split_stats_slots(int(mode), flags, int(batch), int(c_in), int(c_out),
+                                                       _ints3(out_size))
+    if n <= 0:
+        raise ValueError("mvs_conv3d_region_split_stats_slots: %d" % n)
+    return int(n)
+
+
+def conv3d_region_split_sums(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, x_bound,
+                             x2_bound=None, y_bound=None, out_ncdhw=False, store_origin=None, store_size=None):
+    """conv3d_region_split without the BN epilogue (train mode's raw output), with the per-channel
+    float64 (sum, sum of squares) over the whole output region formed in the kernel's epilogue:
+    returns (y, s1, s2), y holding the store box (default: the output region).  Replaces
+    channel_stats(y) on the output: no second pass over it, and y may hold only the part the next layer
+    reads."""
+    b, cout, cin = x.shape[0], weight.shape[1], weight.shape[2]
+    slots = split_stats_slots(mode, b, cin, cout, out_size, False, x2 is not None)
+    st = torch.empty((slots, 2, cout), device=x.device, dtype=torch.float64)
+    y = conv3d_region_split(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, x_bound,
+                            x2_bound, y_bound, out_ncdhw=out_ncdhw, store_origin=store_origin,
+                            store_size=store_size, stats=st)
+    s = st.sum(0)
+    return y, s[0], s[1]
+
+
 @conv3d_region_split.register_fake
 def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, x_bound, x2_bound, y_bound,
-      bn_scale=None, bn_shift=None, bn_mean=None, out_ncdhw=False, per_lane=False, y_addend=None):
+      bn_scale=None, bn_shift=None, bn_mean=None, out_ncdhw=False, per_lane=False, y_addend=None,
+      store_origin=None, store_size=None, stats=None):
+    size = tuple(out_size if store_size is None else store_size)
     if out_ncdhw:
-        return x.new_empty((x.shape[0], weight.shape[1]) + tuple(out_size), dtype=_F32)
-    return x.new_empty((x.shape[0],) + tuple(out_size) + (weight.shape[1],), dtype=_F32)
+        return x.new_empty((x.shape[0], weight.shape[1]) + size, dtype=_F32)
+    return x.new_empty((x.shape[0],) + size + (weight.shape[1],), dtype=_F32)
 
 
 # ----------------------------------------------------------------------------------------------
@@ -1220,6 +1261,50 @@ def channel_stats(x: torch.Tensor, channels_last: bool):
     _lib.check(rc, "mvs_channel_stats")
     s = st.sum(0)
     return s[0], s[1]
+
+
+def bn_train_params(bn, s1, s2, count, border=None):
+    """Train-mode BatchNorm parameters [3, C] = (scale, shift, mean) from the float64 batch sums s1, s2
+    over ``count`` elements, updating bn's running statistics and num_batches_tracked (mvs_bn_train_params,
+    csrc/channel_ops.hip: one launch for what model._bn_train does in ~12 device ops).  ``border``: None
+    or (U [C, C_prev, K] float64, counts [K] float64, prev [3, C_prev]) -- conv_k_1's border-class term
+    (model._border_class_sums) with the previous BN's constant relu(BN(0)) formed from its parameters
+    ``prev``.  bn.momentum must be set (None: the cumulative average, model._bn_train)."""
+    lib = _lib.load()
+    if bn.momentum is None:
+        raise ValueError("bn_train_params: momentum=None (cumulative average) is model._bn_train's")
+    c = s1.numel()
+    if (s1.dim() == 1 and s2.dim() == 1 and s1.is_contiguous() and s2.is_contiguous()
+            and s1.dtype == torch.float64 and s2.dtype == torch.float64
+            and s1.untyped_storage().data_ptr() == s2.untyped_storage().data_ptr()
+            and s2.data_ptr() == s1.data_ptr() + 8 * c):
+        sums = torch.as_strided(s1, (2, c), (c, 1))   # the rows of one [2, C] sum tensor
+    else:
+        sums = torch.stack((s1.double(), s2.double()))
+    dev = sums.device
+    f = lambda t: t.detach().to(device=dev, dtype=_F32).contiguous()
+    wt, bias = f(bn.weight), f(bn.bias)
+    params = torch.empty((3, c), device=dev, dtype=_F32)
+    track = bn.running_mean is not None
+    if track and not (bn.running_mean.is_contiguous() and bn.running_mean.dtype == _F32
+                      and bn.running_var.is_contiguous() and bn.running_var.dtype == _F32):
+        raise ValueError("bn_train_params: contiguous fp32 running statistics expected")
+    bu = bc = prev = None
+    cp = ncls = 0
+    if border is not None:
+        bu, bc, prev = border
+        cp, ncls = bu.shape[1], bu.shape[2]
+        if bu.shape[0] != c or bc.numel() != ncls or tuple(prev.shape) != (3, cp):
+            raise ValueError("border: U [C, C_prev, K], counts [K], prev [3, C_prev]")
+        prev = prev.contiguous()
+    nbt = bn.num_batches_tracked if track and bn.num_batches_tracked is not None else None
+    pt = lambda t: None if t is None else _lib.ptr(t)
+    st = lib.mvs_bn_train_params(_lib.ptr(sums.contiguous()), c, float(count), pt(bu), pt(bc), cp, ncls, pt(prev),
+                                 _lib.ptr(wt), _lib.ptr(bias), pt(bn.running_mean if track else None),
+                                 pt(bn.running_var if track else None), pt(nbt), float(bn.momentum), float(bn.eps),
+                                 _lib.ptr(params), _lib.stream_handle(dev))
+    _lib.check(st, "mvs_bn_train_params")
+    return params
 
 
 def bn_relu_(x: torch.Tensor, channels_last: bool, scale, shift, mean, r=None, r_bn=None, y_bound=None) -> torch.Tensor:

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 16
+#define MVS_ABI_VERSION 18
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -508,13 +508,29 @@ int mvs_conv3d_region_split_weights(const float* weight, int c_in, int c_out, un
  * c_out): S1 (16, 16), (32, 32), (64, 64), T2 (64, 32), (32, 16), S2 (32, 16 | 32 | 64).  Inference
  * only (the raw outputs without the BN pointers: train-mode BN's batch statistics).  y_addend: NULL, or a
  * tensor of y's shape and layout added after BN + ReLU (deconv_3_0's output + y2, model.py:119, formed
- * once instead of on every load of deconv_2_0); the bound words then bound the sum. */
+ * once instead of on every load of deconv_2_0); the bound words then bound the sum.
+ * Train-mode BatchNorm (test.py:61): store_origin / store_size (NULL, or a box inside
+ * the output region, absolute voxel coordinates): y holds only that box ([batch][size...][c_out] or
+ * channels-first), the rest of the region is computed but not stored; stats (NULL, or DEVICE float64,
+ * 8-byte aligned, mvs_conv3d_region_split_stats_slots(...) x 2 x c_out): every workgroup writes its
+ * slot stats[slot][0 / 1][c] = sum / sum of squares over the WHOLE output region of the stored value
+ * (after the epilogue); the caller adds the slots in a fixed order (run-to-run bit-identical batch
+ * statistics, as mvs_channel_stats). */
 int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float* x2, const void* weight_frag,
                                 int weight_exp, float* y, int batch, int c_in, int c_out, const int* dims,
                                 const int* out_origin, const int* out_size, const int* in_origin, const int* in_size,
                                 const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                                 const unsigned* x_bound, const unsigned* x2_bound, unsigned* y_bound,
-                                const float* y_addend, void* stream);
+                                const float* y_addend, const int* store_origin, const int* store_size, double* stats,
+                                void* stream);
+
+/* flag of mvs_conv3d_region_split_stats_slots: the call sums two inputs (x2 given) */
+#define MVS_CONV_SUM_INPUT 64
+/* Number of float64 sum slots (workgroups) of the mvs_conv3d_region_split_fwd call with this mode,
+ * flags (MVS_CONV_PER_LANE, MVS_CONV_SUM_INPUT), batch, channels and out_size; < 0 on invalid
+ * arguments.  Host-only: no device work. */
+long long mvs_conv3d_region_split_stats_slots(int mode, int flags, int batch, int c_in, int c_out,
+                                              const int* out_size);
 
 /* Softmax over the depth planes of the regulariser's output (CostVolumeReg.Norm = nn.Softmax(2),
  * model.py:97 / :125): y[b][0][d][p] = exp(x - max_d x) / sum_d exp(x - max_d x) per pixel p, in
@@ -555,6 +571,20 @@ size_t mvs_channel_stats_slots(int layout, int batch, int channels, long long vo
  * x[batch][channels][voxels]). */
 int mvs_channel_stats(const float* x, int layout, int batch, int channels, long long voxels, double* stats,
                       void* stream);
+
+/* Train-mode BatchNorm parameters from the batch sums (replaces torch.nn.functional.batch_norm's
+ * statistics step with training=True, model.py:101-121 under test.py:61): sums (DEVICE float64
+ * [2][channels]: sum, sum of squares over count elements; plus, with border_u, the border term of
+ * CostVolumeReg.forward_live_train: u_k = sum_i border_u[o][i][k] a_i with the previous BN's constant
+ * a_i = relu(-mean_i scale_i + shift_i) from prev_params [3][prev_channels], added as
+ * (sum_k u_k border_count[k], sum_k u_k^2 border_count[k])); mean = s1 / count, var = max(s2 / count -
+ * mean^2, 0) in float64; running_mean / running_var (NULL: not tracked) updated with momentum and the
+ * unbiased variance var count / (count - 1); num_batches_tracked (NULL or int64) += 1; params (DEVICE
+ * fp32 [3][channels]) = (weight / sqrt(var + eps), bias, mean).  One launch, one workgroup. */
+int mvs_bn_train_params(const double* sums, int channels, double count, const double* border_u,
+                        const double* border_count, int prev_channels, int classes, const float* prev_params,
+                        const float* weight, const float* bias, float* running_mean, float* running_var,
+                        long long* num_batches_tracked, double momentum, double eps, float* params, void* stream);
 
 /* y = max((x - mean) * scale + shift, 0) per channel (BatchNorm3d with the batch statistics:
  * scale = gamma / sqrt(var + eps), shift = beta; then ReLU), and, when r is given,

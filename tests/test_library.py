@@ -23,7 +23,7 @@ def _declared():
 def test_header_declares_the_abi():
     names = _declared()
     assert "mvs_cost_volume_fwd" in names and "mvs_cost_volume_bwd" in names
-    assert len(names) == 40, names
+    assert len(names) == 42, names
 
 
 def test_library_exports_every_declared_symbol():
@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from mvs_amd import _lib
     lib = _lib.load()
-    assert lib.mvs_abi_version() == _lib.ABI_VERSION == 16
+    assert lib.mvs_abi_version() == _lib.ABI_VERSION == 18
     assert lib.mvs_status_string(0) == b"ok"
     assert lib.mvs_status_string(-2).startswith(b"n_views")
     assert lib.mvs_sampling_workspace_bytes(12, 192) == 12 * 192 * 9 * 4
@@ -98,6 +98,15 @@ def test_invalid_arguments_rejected_before_any_launch():
     assert lib.mvs_channel_stats(fake, 0, 2, 16, 0, fake, null) == -1
     assert lib.mvs_bn_relu(fake, 0, 2, 16, 100, fake, fake, None, None, None, None, None, fake, None, null) == -1
     assert lib.mvs_bn_relu(fake, 0, 2, 16, 100, fake, fake, fake, fake, None, fake, fake, fake, None, null) == -1
+    # the split region convs' sum slots: host-only arithmetic over the launch geometry
+    size = (ctypes.c_int * 3)(26, 18, 22)
+    s1 = lib.mvs_conv3d_region_split_stats_slots(0, 0, 2, 16, 16, size)                    # LDS kernel tiles
+    assert s1 == 2 * 2 * 5 * 4   # ceil(22 / 16) x ceil(18 / 4) x ceil(26 / 8) tiles x batch 2
+    t2 = lib.mvs_conv3d_region_split_stats_slots(2, 0, 2, 64, 32, size)
+    assert t2 > 0 and t2 % (8 * 2 * 8) == 0   # (row chunks rounded to 8 XCDs) x 8 classes x batch
+    assert lib.mvs_conv3d_region_split_stats_slots(0, _lib.MVS_CONV_PER_LANE, 2, 16, 16, size) != s1
+    assert lib.mvs_conv3d_region_split_stats_slots(3, 0, 2, 16, 16, size) == -1
+    assert lib.mvs_conv3d_region_split_stats_slots(0, 0, 0, 16, 16, size) == -1
 
 
 def test_build_is_gfx950_in_tree():

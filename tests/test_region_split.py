@@ -277,3 +277,64 @@ def test_region_split_output_addend():
         torch.cuda.synchronize()
     assert torch.equal(ys, y + add)
     assert bw[2].cpu().numpy().view(np.float32).max() == ys.abs().max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,cin,cout,ncdhw", [(0, 16, 16, True), (0, 32, 32, False), (0, 64, 64, False),
+                                                 (2, 64, 32, False), (2, 32, 16, True), (1, 32, 16, False),
+                                                 (1, 32, 64, False)])
+def test_region_split_sums_and_store_box(mode, cin, cout, ncdhw):
+    """Train-mode BatchNorm's batch sums formed in the split kernels' epilogues (conv3d_region_split_sums,
+    DESIGN.md §5b): the per-channel float64 sum / sum of squares over the whole output region equal
+    channel_stats of the un-boxed output (1e-12 relative), the stored box is bit-equal to that output's
+    crop, and two launches give bit-identical sums (slot-owned partials, fixed-order total).  S1 on
+    R1 -> stored M (LDS kernel for 16 / 32 channels, per-lane for 64), T2 full volume -> stored M, S2
+    from the split cost volume on R2 (stored whole)."""
+    from cameras import camera_batch, depth_range
+    from mvs_amd import ops
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _grow, _tconv_input_region
+    B, D, h, w = 2, 24, 20, 26
+    n = (D, h, w)
+    pad, _ = pad_outpad(*n)
+    full = tuple((0, d - 1) for d in n)
+    M = _tconv_input_region(full, n, pad)
+    R1, R2 = _grow(M, n, 1), _grow(M, n, 2)
+    org = lambda r: [lo for lo, _ in r]
+    size = lambda r: [hi - lo + 1 for lo, hi in r]
+    g = torch.Generator().manual_seed(mode * 1000 + cin + cout)
+    conv = torch.nn.ConvTranspose3d(cin, cout, 3) if mode == 2 else torch.nn.Conv3d(cin, cout, 3)
+    conv.weight.data = torch.randn(*conv.weight.shape, generator=g) * 0.1
+    w27 = ops.region_weight(conv).to(DEV)
+    bw = ops.bound_words(1, DEV)
+    with torch.no_grad():
+        if mode == 1:   # S2: conv_k_0 from the split cost volume on R2
+            K, R, T = camera_batch(B, 3, h, w)
+            d_min, d_int = depth_range(B, d_int=200.0 / D)
+            feat = torch.randn(B * 3, 32, h, w, generator=g).to(DEV)
+            x, xb = ops.cost_volume_c4_split(feat, K, R, T, d_min, d_int, B, 3, 0, D, 25.0)
+            geo = (ops.CONV_S2, list(n), org(R2), size(R2), None, None, list(pad))
+            box = R2
+        else:
+            in_reg = R2 if mode == 0 else M
+            x = torch.relu(torch.randn(B, *size(in_reg), cin, generator=g)).to(DEV)
+            xb = bw[0]
+            xb[0] = x.abs().max().view(torch.int32)
+            out_reg = R1 if mode == 0 else full
+            geo = (mode, list(n), org(out_reg), size(out_reg), org(in_reg), size(in_reg),
+                   None if mode == 0 else list(pad))
+            box = M
+        out_reg = [(o, o + s - 1) for o, s in zip(geo[2], geo[3])]
+        y_full = ops.conv3d_region_split(x, None, w27, *geo, xb, None, None, out_ncdhw=ncdhw)
+        r1, r2 = ops.channel_stats(y_full, not ncdhw)
+        ys, s1, s2 = ops.conv3d_region_split_sums(x, None, w27, *geo, xb, out_ncdhw=ncdhw, store_origin=org(box),
+                                                  store_size=size(box))
+        _, t1, t2 = ops.conv3d_region_split_sums(x, None, w27, *geo, xb, out_ncdhw=ncdhw, store_origin=org(box),
+                                                 store_size=size(box))
+        torch.cuda.synchronize()
+    crop = [slice(lo - olo, hi - olo + 1) for (olo, _), (lo, hi) in zip(out_reg, box)]
+    want = y_full[:, :, crop[0], crop[1], crop[2]] if ncdhw else y_full[:, crop[0], crop[1], crop[2], :]
+    assert torch.equal(ys, want.contiguous())
+    torch.testing.assert_close(s1, r1, rtol=1e-12, atol=1e-9)
+    torch.testing.assert_close(s2, r2, rtol=1e-12, atol=1e-9)
+    assert torch.equal(s1, t1) and torch.equal(s2, t2)
