@@ -848,7 +848,8 @@ int mvs_bn_train_params(const double* sums, int channels, double count, const do
   if (!sums || !weight || !bias || !params || channels <= 0 || !(count > 0.0) || !(eps >= 0.0))
     return MVS_ERR_INVALID_ARGUMENT;
   if ((running_mean != nullptr) != (running_var != nullptr)) return MVS_ERR_INVALID_ARGUMENT;
-  if (border_u && (!border_count || !prev_params || prev_channels <= 0 || classes <= 0))
+  if (border_u && (!border_count || !prev_params || prev_channels <= 0 || prev_channels > 256 || classes <= 0 ||
+                   (long long)channels * classes > 2048))
     return MVS_ERR_INVALID_ARGUMENT;
   const mvs::LaunchCheck lc;
   mvs::launch_bn_train_params(sums, channels, count, border_u, border_count, prev_channels, classes, prev_params,

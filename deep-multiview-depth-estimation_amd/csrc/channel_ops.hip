@@ -204,30 +204,45 @@ __global__ __launch_bounds__(kBlock) void bn_relu_cf_kernel(const float* __restr
   if (yb) bound_update(yb, vmax);
 }
 
-// Train-mode BatchNorm parameters from the batch sums (mvs_bn_train_params): one thread per channel.
+// Train-mode BatchNorm parameters from the batch sums (mvs_bn_train_params): one workgroup, one thread
+// per channel.
 // Border term (conv_k_1's voxels outside its computed region, CostVolumeReg.forward_live_train): the
 // previous BN's constant a_i = relu(-mean_i scale_i + shift_i), u = sum_i U[o][i][k] a_i per border
 // class k, sums += (sum_k u cnt_k, sum_k u^2 cnt_k).  Then mean = s1 / n, var = max(s2 / n - mean^2, 0)
 // (biased, float64), the running statistics' momentum update (unbiased variance), and
 // params = (weight / sqrt(var + eps), bias, mean) in fp32 -- model.py's _bn_train / _border_class_sums /
 // _bn_constant, as one launch instead of ~20 small device ops.
-__global__ __launch_bounds__(64) void bn_train_params_kernel(
+constexpr int kBnBorderMax = 2048;   // channels x border classes of mvs_bn_train_params
+
+__global__ __launch_bounds__(kBlock) void bn_train_params_kernel(
     const double* __restrict__ sums, int C, double count, const double* __restrict__ bu,
     const double* __restrict__ bcnt, int Cp, int ncls, const float* __restrict__ prev, const float* __restrict__ w,
     const float* __restrict__ bias, float* __restrict__ rmean, float* __restrict__ rvar,
     long long* __restrict__ nbt, double momentum, double eps, float* __restrict__ params) {
+  __shared__ double part[2][kBnBorderMax];
+  __shared__ double a[256];
+  if (bu) {
+    // the previous BN's constant, then u per (channel, class) in parallel; per channel the classes are
+    // added in a fixed order below (bit-identical run to run)
+    for (int i = (int)threadIdx.x; i < Cp; i += (int)blockDim.x)
+      a[i] = (double)fmaxf(-prev[2 * Cp + i] * prev[i] + prev[Cp + i], 0.0f);
+    __syncthreads();
+    for (int e = (int)threadIdx.x; e < C * ncls; e += (int)blockDim.x) {
+      const int o = e / ncls, k = e % ncls;
+      double u = 0.0;
+      for (int i = 0; i < Cp; ++i) u += bu[((size_t)o * Cp + i) * ncls + k] * a[i];
+      part[0][e] = u * bcnt[k];
+      part[1][e] = u * u * bcnt[k];
+    }
+    __syncthreads();
+  }
   for (int o = (int)threadIdx.x; o < C; o += (int)blockDim.x) {
     double s1 = sums[o], s2 = sums[C + o];
     if (bu) {
       double c1 = 0.0, c2 = 0.0;
       for (int k = 0; k < ncls; ++k) {
-        double u = 0.0;
-        for (int i = 0; i < Cp; ++i) {
-          const float a = fmaxf(-prev[2 * Cp + i] * prev[i] + prev[Cp + i], 0.0f);
-          u += bu[((size_t)o * Cp + i) * ncls + k] * (double)a;
-        }
-        c1 += u * bcnt[k];
-        c2 += u * u * bcnt[k];
+        c1 += part[0][o * ncls + k];
+        c2 += part[1][o * ncls + k];
       }
       s1 += c1;
       s2 += c2;
@@ -285,7 +300,7 @@ void launch_channel_stats(const float* x, bool channels_last, int B, int C, size
 void launch_bn_train_params(const double* sums, int C, double count, const double* bu, const double* bcnt, int Cp,
                             int ncls, const float* prev, const float* w, const float* bias, float* rmean, float* rvar,
                             long long* nbt, double momentum, double eps, float* params, hipStream_t s) {
-  hipLaunchKernelGGL(bn_train_params_kernel, dim3(1), dim3(64), 0, s, sums, C, count, bu, bcnt, Cp, ncls, prev, w,
+  hipLaunchKernelGGL(bn_train_params_kernel, dim3(1), dim3(kBlock), 0, s, sums, C, count, bu, bcnt, Cp, ncls, prev, w,
                      bias, rmean, rvar, nbt, momentum, eps, params);
 }
 

@@ -580,7 +580,8 @@ int mvs_channel_stats(const float* x, int layout, int batch, int channels, long 
  * (sum_k u_k border_count[k], sum_k u_k^2 border_count[k])); mean = s1 / count, var = max(s2 / count -
  * mean^2, 0) in float64; running_mean / running_var (NULL: not tracked) updated with momentum and the
  * unbiased variance var count / (count - 1); num_batches_tracked (NULL or int64) += 1; params (DEVICE
- * fp32 [3][channels]) = (weight / sqrt(var + eps), bias, mean).  One launch, one workgroup. */
+ * fp32 [3][channels]) = (weight / sqrt(var + eps), bias, mean).  One launch, one workgroup; with the
+ * border term prev_channels <= 256 and channels x classes <= 2048. */
 int mvs_bn_train_params(const double* sums, int channels, double count, const double* border_u,
                         const double* border_count, int prev_channels, int classes, const float* prev_params,
                         const float* weight, const float* bias, float* running_mean, float* running_var,
