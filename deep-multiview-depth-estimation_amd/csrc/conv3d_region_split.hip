@@ -529,7 +529,16 @@ static bool split_uses_lds(int mode, int CI, int CO, bool per_lane, bool has_x2)
 // row blocks per wave of the per-lane kernel: 4 for the stride-1 convs (each weight fragment feeds 4 row
 // blocks), 2 for the transposed and stride-2 ones (measured at cfg 2, eval and train mode: S1 64 -> 64
 // 2.70 -> 2.41 ms, T2 32 -> 16 2.02 against 2.36 with 4; 1 row block is slower everywhere)
-static int split_rb(int mode) { return mode == kS1 ? 4 : 2; }
+// The stride-1 kernel drops to 2 row blocks when 4 would leave fewer than kS1WideWgs workgroups: eval's
+// deep-level regions are small (conv_3_1 at cfg 2: 3.97 -> 3.87 ms per eval step with 2), train mode's are
+// large (4 measured best: 15.3 against 15.5 ms per train-mode step with 2).  S2 with 1 / 4 row blocks:
+// eval 4.01 / 4.11 ms, train 15.9 / 15.5 ms (tools/gpu_r5_bound_ab.sh r5rb).
+constexpr long kS1WideWgs = 4096;
+static int split_rb(int mode, int B, const int* on) {
+  if (mode != kS1) return 2;
+  const long rows = (long)B * on[0] * on[1] * on[2];
+  return rows >= kS1WideWgs * (kBlock / 64) * 16 * 4 ? 4 : 2;
+}
 
 long conv3d_region_split_slots(int mode, int B, int CI, int CO, const int* on, bool per_lane, bool has_x2) {
   if (split_uses_lds(mode, CI, CO, per_lane, has_x2)) {
@@ -539,7 +548,7 @@ long conv3d_region_split_slots(int mode, int B, int CI, int CO, const int* on, b
     else s1_lds_tiles<64>(on, tx, ty, tz);
     return (long)B * tx * ty * tz;
   }
-  const dim3 gr = split_mode_grid(mode, split_rb(mode), B, on);
+  const dim3 gr = split_mode_grid(mode, split_rb(mode, B, on), B, on);
   return (long)gr.x * gr.y * gr.z;
 }
 
@@ -564,11 +573,15 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
     g.sb0[d] = store_origin ? store_origin[d] : o0[d];
     g.sbn[d] = store_origin ? store_size[d] : on[d];
   }
-#define MVS_RSPLIT_CASE(MD, A, C)                                                                         \
-  if (mode == MD && CI == A && CO == C) {                                                                 \
-    launch_split_mode<MD, A, C, MD == kS1 ? 4 : 2>(x, x2, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, \
-                                                   x_bound, x2_bound, y_bound, s);                        \
-    return MVS_OK;                                                                                        \
+#define MVS_RSPLIT_CASE(MD, A, C)                                                                          \
+  if (mode == MD && CI == A && CO == C) {                                                                  \
+    if (split_rb(mode, B, on) == 4)                                                                        \
+      launch_split_mode<MD, A, C, 4>(x, x2, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound,   \
+                                     x2_bound, y_bound, s);                                                \
+    else                                                                                                   \
+      launch_split_mode<MD, A, C, 2>(x, x2, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound,   \
+                                     x2_bound, y_bound, s);                                                \
+    return MVS_OK;                                                                                         \
   }
   // S1: conv_k_1 (16 / 32 / 64 channels; LDS-staged operands per MVS_S1_LDS); T2: deconv_3_0 (64 -> 32),
   // deconv_2_0 (32 -> 16); S2: conv_k_0 from the split cost volume (32 -> 16 / 32 / 64)
