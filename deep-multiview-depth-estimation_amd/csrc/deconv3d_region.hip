@@ -187,23 +187,11 @@ __global__ __launch_bounds__(kBlock) void deconv3d_k3s2_kernel(
             q[a][c][e] = t;
           }
     };
-#ifdef MVS_DECONV_CL_PF
-    float4 qn[2][2][2];
-    load_q(0, qn);
-#endif
+    // (the next quad's loads issued before this quad's FMAs measured slower: 172 VGPRs, 2 waves per
+    // SIMD; eval step 3.94 -> 4.04 ms)
     for (int c0 = 0; c0 < Cin; c0 += 4) {
       float4 q[2][2][2];
-#ifdef MVS_DECONV_CL_PF
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-          for (int e = 0; e < 2; ++e) q[a][c][e] = qn[a][c][e];
-      if (c0 + 4 < Cin) load_q(c0 + 4, qn);
-#else
       load_q(c0, q);
-#endif
       // one channel of the quad at a time (unrolled, the four channels' weight reads would be
       // hoisted together: 504 VGPRs); the component is picked by selects
 #pragma unroll 1
