@@ -23,6 +23,8 @@
 // S2 (conv_k_0, model.py:78-80 / :103-111): the input is the split cost volume itself (split.h's SCV,
 // or a box of it), already the operands: a lane's 8 channels are the hi / lo halves of quads 2g and
 // 2g + 1 (two 16-byte loads, no conversion), scaled by the volume's bound words (cv_split_exponent).
+#include <cstdlib>
+
 #include "launchers.h"
 #include "packed.h"
 #include "split.h"
@@ -509,6 +511,228 @@ void launch_s1_lds(const float* x, const void* wf, int w_exp, float* y, const fl
                      reinterpret_cast<const h8v*>(wf), w_exp, y, sc, sh, mu, g, tx, ty, tz, xb, yb);
 }
 
+// ---- transposed convolutions over large output regions with LDS-staged operands (train mode's
+// deconv_3_0 / deconv_2_0 over the full volume, model.py:117-120) ----
+// A workgroup owns a TX x 8 x 4 block of outputs of ALL eight parity classes; every output of it reads
+// inputs i = (o + P - t) / 2 from one (TX / 2 + 1) x 5 x 3 input block, which is loaded once, split and
+// stored in LDS as S1Tile's swizzled records (the per-lane kernel re-reads each input voxel through
+// L1 for every (output, tap) pair: 27 times).  The four waves share each class: wave w owns row blocks
+// 2 TXB w .. + 2 TXB - 1 of the class's 8 TXB (16 consecutive class outputs along x each) and all its
+// column blocks; classes run one after another (taps of class (pz, py, px): 2 per dim of parity 0, 1
+// of parity 1 -- 27 over the eight).  Same products and K order as the per-lane kernel (taps, then
+// channel blocks): bit-equal outputs.
+template <int CI, int TXB>
+struct T2Tile {
+  static constexpr int TX = 32 * TXB, TY = 8, TZ = 4;
+  static constexpr int PX = TX / 2 + 1, PY = TY / 2 + 1, PZ = TZ / 2 + 1, PV = PX * PY * PZ;
+  static constexpr int REC = CI * 4, NCH = REC / 16;
+  static constexpr int LDS = PV * REC;
+  __device__ static int chunk_off(int v, int c) { return v * REC + ((c ^ ((v / (16 / NCH)) % NCH)) << 4); }
+};
+
+template <int CI, int CO, int TXB>
+__global__ __launch_bounds__(kBlock) void conv3d_t2_split_lds_kernel(
+    const float* __restrict__ x, const h8v* __restrict__ wf, int w_exp, float* __restrict__ y,
+    const float* __restrict__ bn_scale, const float* __restrict__ bn_shift, const float* __restrict__ bn_mean,
+    GeoS g, int tiles_x, int tiles_y, int tiles_z, const uint32_t* __restrict__ xb, uint32_t* __restrict__ yb) {
+  using T = T2Tile<CI, TXB>;
+  constexpr int NB = CO / 16, CB = CI / 32, RB = 2 * TXB;
+  static_assert(CI % 32 == 0 && CO % 16 == 0, "channel counts");
+  __shared__ __attribute__((aligned(16))) char lds[T::LDS];
+
+  int t = xcd_work_id((int)blockIdx.x, (int)gridDim.x);
+  if (t >= tiles_x * tiles_y * tiles_z) return;   // workgroup-uniform, before the barriers
+  const int t0 = t;
+  // tile origin (absolute output coordinates)
+  const int X0 = g.o0[2] + (t % tiles_x) * T::TX;
+  t /= tiles_x;
+  const int Y0 = g.o0[1] + (t % tiles_y) * T::TY;
+  t /= tiles_y;
+  const int Z0 = g.o0[0] + t * T::TZ;
+  const int b = (int)blockIdx.y;
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m = lane & 15, kq = lane >> 4;
+  const int ex = act_split_exponent(bound_read(xb));
+  // the input block's origin (absolute input coordinates): the smallest (o + P - t) / 2
+  const int ilz = (Z0 + g.pad[0] - 1) >> 1, ily = (Y0 + g.pad[1] - 1) >> 1, ilx = (X0 + g.pad[2] - 1) >> 1;
+
+  // ---- stage the input block: items (voxel, channel quad), quad fastest; outside the input region:
+  // zeros (inputs that reach no output of the region) ----
+  {
+    constexpr int NQ = CI / 4, NIT = T::PV * NQ, PER = (NIT + kBlock - 1) / kBlock, BATCH = 8;
+    const size_t rvol = (size_t)g.in[0] * g.in[1] * g.in[2];
+    const Rsrc rs = make_rsrc(x + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
+#pragma unroll
+    for (int k0 = 0; k0 < PER; k0 += BATCH) {
+      f4v v4[BATCH];
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int e = tid + kBlock * (k0 + k);
+        const int q = e % NQ, v = e / NQ;
+        const int px = v % T::PX, py = (v / T::PX) % T::PY, pz = v / (T::PX * T::PY);
+        const int rx = ilx + px - g.i0[2], ry = ily + py - g.i0[1], rz = ilz + pz - g.i0[0];
+        const bool ok = k0 + k < PER && e < NIT && rx >= 0 && rx < g.in[2] && ry >= 0 && ry < g.in[1] && rz >= 0 &&
+                        rz < g.in[0];
+        const uint32_t off = ok ? (uint32_t)((((size_t)rz * g.in[1] + ry) * g.in[2] + rx) * CI + 4 * q) * 4u : kOob;
+        v4[k] = ld4(rs, off, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int e = tid + kBlock * (k0 + k);
+        if (k0 + k >= PER || e >= NIT) continue;
+        const int q = e % NQ, v = e / NQ;
+        uint2 hi, lo;
+        split4(v4[k], ex, hi, lo);
+        *reinterpret_cast<uint2*>(lds + T::chunk_off(v, q >> 1) + ((q & 1) << 3)) = hi;
+        *reinterpret_cast<uint2*>(lds + T::chunk_off(v, CI / 8 + (q >> 1)) + ((q & 1) << 3)) = lo;
+      }
+    }
+  }
+  __syncthreads();
+
+  const int oexp = -(ex + w_exp);
+  const size_t orvol = (size_t)g.sbn[0] * g.sbn[1] * g.sbn[2];
+  float vmax = 0.0f;
+  double ss[NB], sq[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) ss[nb] = sq[nb] = 0.0;
+  auto ldb = [&](int kb, h8v (&bh)[NB], h8v (&bl)[NB]) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      bh[nb] = wf[((size_t)(kb * NB + nb) * 2 + 0) * 64 + lane];
+      bl[nb] = wf[((size_t)(kb * NB + nb) * 2 + 1) * 64 + lane];
+    }
+  };
+
+#pragma unroll 1
+  for (int cls = 0; cls < 8; ++cls) {
+    const int pz = (cls >> 2) & 1, py = (cls >> 1) & 1, px = cls & 1;
+    // the class's first output per dim inside the tile: (o + P) of parity par
+    const int fz = Z0 + (((Z0 + g.pad[0]) & 1) != pz ? 1 : 0), fy = Y0 + (((Y0 + g.pad[1]) & 1) != py ? 1 : 0),
+              fx = X0 + (((X0 + g.pad[2]) & 1) != px ? 1 : 0);
+    // input block coordinates of (o + P - par) / 2 for the class's first output
+    const int bz = ((fz + g.pad[0] - pz) >> 1) - ilz, by = ((fy + g.pad[1] - py) >> 1) - ily,
+              bx = ((fx + g.pad[2] - px) >> 1) - ilx;
+    const int ntz = 2 - pz, nty = 2 - py, ntx = 2 - px, nk = ntz * nty * ntx * CB;
+    f4v acc[RB][NB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) acc[r][nb] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+    // K block k of the class: taps (tz, ty, tx) with t = par + 2 j, j < nt, then channel blocks
+    auto tap_of = [&](int k, int& tap, int& cb, int& dz, int& dy, int& dx) {
+      cb = k % CB;
+      int j = k / CB;
+      const int jx = j % ntx;
+      j /= ntx;
+      const int jy = j % nty, jz = j / nty;
+      const int tz = pz + 2 * jz, ty = py + 2 * jy, tx = px + 2 * jx;
+      tap = (tz * 3 + ty) * 3 + tx;
+      dz = -jz;   // input offset -(t >> 1)
+      dy = -jy;
+      dx = -jx;
+    };
+    auto kstep = [&](int k, const h8v (&bh)[NB], const h8v (&bl)[NB]) {
+      int tap, cb, dz, dy, dx;
+      tap_of(k, tap, cb, dz, dy, dx);
+      const int c0 = cb * 4 + kq;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int rbi = wave * RB + r;                       // (z_c, y_c, xb) of the class's 8 TXB row blocks
+        const int xbk = rbi % TXB, yc = (rbi / TXB) & 3, zc = rbi / (4 * TXB);
+        const int v = ((bz + zc + dz) * T::PY + (by + yc + dy)) * T::PX + (bx + xbk * 16 + m + dx);
+        const h8v ahi = *reinterpret_cast<const h8v*>(lds + T::chunk_off(v, c0));
+        const h8v alo = *reinterpret_cast<const h8v*>(lds + T::chunk_off(v, CI / 8 + c0));
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          acc[r][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bh[nb], acc[r][nb], 0, 0, 0);
+          acc[r][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi, bl[nb], acc[r][nb], 0, 0, 0);
+          acc[r][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo, bh[nb], acc[r][nb], 0, 0, 0);
+        }
+      }
+    };
+    h8v bh0[NB], bl0[NB], bh1[NB], bl1[NB];
+    {
+      int tap, cb, dz, dy, dx;
+      tap_of(0, tap, cb, dz, dy, dx);
+      ldb(tap * CB + cb, bh0, bl0);
+    }
+#pragma unroll 1
+    for (int k = 0; k < nk; k += 2) {
+      if (k + 1 < nk) {
+        int tap, cb, dz, dy, dx;
+        tap_of(k + 1, tap, cb, dz, dy, dx);
+        ldb(tap * CB + cb, bh1, bl1);
+      }
+      kstep(k, bh0, bl0);
+      if (k + 1 < nk) {
+        if (k + 2 < nk) {
+          int tap, cb, dz, dy, dx;
+          tap_of(k + 2, tap, cb, dz, dy, dx);
+          ldb(tap * CB + cb, bh0, bl0);
+        }
+        kstep(k + 1, bh1, bl1);
+      }
+    }
+    // ---- the class's outputs: acc[r][nb][i] = (class output x index xbk * 16 + 4 kq + i of row r,
+    // channel nb * 16 + m) ----
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int co = nb * 16 + m;
+      const float sc = bn_scale ? bn_scale[co] : 1.0f, sh = bn_scale ? bn_shift[co] : 0.0f,
+                  mu = bn_scale ? bn_mean[co] : 0.0f;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int rbi = wave * RB + r;
+        const int xbk = rbi % TXB, yc = (rbi / TXB) & 3, zc = rbi / (4 * TXB);
+        const int oz = fz + 2 * zc, oy = fy + 2 * yc;
+        if (oz >= min(Z0 + T::TZ, g.o0[0] + g.on[0]) || oy >= min(Y0 + T::TY, g.o0[1] + g.on[1])) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ox = fx + 2 * (xbk * 16 + 4 * kq + i);
+          if (ox >= min(X0 + T::TX, g.o0[2] + g.on[2])) continue;
+          float v = ldexpf(acc[r][nb][i], oexp);
+          if (bn_scale) v = fmaxf((v - mu) * sc + sh, 0.0f);
+          const int vz = oz - g.sb0[0], vy = oy - g.sb0[1], vx = ox - g.sb0[2];
+          const bool keep = vz >= 0 && vz < g.sbn[0] && vy >= 0 && vy < g.sbn[1] && vx >= 0 && vx < g.sbn[2];
+          const size_t vox = ((size_t)vz * g.sbn[1] + vy) * g.sbn[2] + vx;
+          const size_t oi = g.out_cf ? ((size_t)b * CO + co) * orvol + vox : ((size_t)b * orvol + vox) * CO + co;
+          if (g.addend && keep) v += g.addend[oi];
+          ss[nb] += (double)v;
+          sq[nb] += (double)v * (double)v;
+          if (!keep) continue;
+          vmax = fmaxf(vmax, fabsf(v));
+          y[oi] = v;
+        }
+      }
+    }
+  }
+  if (yb) bound_update(yb, vmax);
+  if (g.stats) {
+    const size_t slot = (size_t)b * (tiles_x * tiles_y * tiles_z) + t0;
+    stats_write<CO, NB, kBlock / 64>(ss, sq, 0, NB, g.stats + slot * 2 * CO);
+  }
+}
+
+template <int CI, int TXB>
+void t2_lds_tiles(const int* on, int& tx, int& ty, int& tz) {
+  using T = T2Tile<CI, TXB>;
+  tx = (on[2] + T::TX - 1) / T::TX;
+  ty = (on[1] + T::TY - 1) / T::TY;
+  tz = (on[0] + T::TZ - 1) / T::TZ;
+}
+
+template <int CI, int CO, int TXB>
+void launch_t2_lds(const float* x, const void* wf, int w_exp, float* y, const float* sc, const float* sh,
+                   const float* mu, int B, const GeoS& g, const uint32_t* xb, uint32_t* yb, hipStream_t s) {
+  int tx, ty, tz;
+  t2_lds_tiles<CI, TXB>(g.on, tx, ty, tz);
+  const int per = tx * ty * tz;
+  const dim3 grid((unsigned)((per + 7) / 8 * 8), (unsigned)B);
+  hipLaunchKernelGGL((conv3d_t2_split_lds_kernel<CI, CO, TXB>), grid, dim3(kBlock), 0, s, x,
+                     reinterpret_cast<const h8v*>(wf), w_exp, y, sc, sh, mu, g, tx, ty, tz, xb, yb);
+}
+
 }  // namespace
 
 int conv3d_region_split_kblocks(int c_in) { return c_in == 16 ? 14 : 27 * (c_in / 32); }
@@ -540,7 +764,24 @@ static int split_rb(int mode, int B, const int* on) {
   return rows >= kS1WideWgs * (kBlock / 64) * 16 * 4 ? 4 : 2;
 }
 
+// The LDS-staged transposed kernel for large output regions (train mode's full volumes: T2 64 -> 32
+// 2.41 -> see DESIGN.md §5b); MVS_T2_LDS=0 / 2 forces the per-lane / LDS kernel (A/B and tests)
+constexpr long kT2LdsMinVoxels = 1l << 22;
+static bool split_t2_lds(int mode, int B, int CI, int CO, const int* on, bool per_lane, bool has_x2) {
+  const char* fe = getenv("MVS_T2_LDS");   // read per call: tests switch it
+  const int force = fe ? atoi(fe) : 1;
+  if (mode != kT2 || per_lane || has_x2 || force == 0) return false;
+  if (!((CI == 64 && CO == 32) || (CI == 32 && CO == 16))) return false;
+  return force == 2 || (long)B * on[0] * on[1] * on[2] >= kT2LdsMinVoxels;
+}
+
 long conv3d_region_split_slots(int mode, int B, int CI, int CO, const int* on, bool per_lane, bool has_x2) {
+  if (split_t2_lds(mode, B, CI, CO, on, per_lane, has_x2)) {
+    int tx, ty, tz;
+    if (CI == 64) t2_lds_tiles<64, 1>(on, tx, ty, tz);
+    else t2_lds_tiles<32, 2>(on, tx, ty, tz);
+    return (long)B * tx * ty * tz;
+  }
   if (split_uses_lds(mode, CI, CO, per_lane, has_x2)) {
     int tx, ty, tz;
     if (CI == 16) s1_lds_tiles<16>(on, tx, ty, tz);
@@ -585,6 +826,11 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
   }
   // S1: conv_k_1 (16 / 32 / 64 channels; LDS-staged operands per MVS_S1_LDS); T2: deconv_3_0 (64 -> 32),
   // deconv_2_0 (32 -> 16); S2: conv_k_0 from the split cost volume (32 -> 16 / 32 / 64)
+  if (split_t2_lds(mode, B, CI, CO, on, per_lane, x2 != nullptr)) {
+    if (CI == 64) launch_t2_lds<64, 32, 1>(x, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, y_bound, s);
+    else launch_t2_lds<32, 16, 2>(x, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, y_bound, s);
+    return MVS_OK;
+  }
   if (split_uses_lds(mode, CI, CO, per_lane, x2 != nullptr)) {
     if (CI == 16) launch_s1_lds<16>(x, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, y_bound, s);
     else if (CI == 32) launch_s1_lds<32>(x, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, y_bound, s);

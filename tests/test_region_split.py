@@ -338,3 +338,49 @@ def test_region_split_sums_and_store_box(mode, cin, cout, ncdhw):
     torch.testing.assert_close(s1, r1, rtol=1e-12, atol=1e-9)
     torch.testing.assert_close(s2, r2, rtol=1e-12, atol=1e-9)
     assert torch.equal(s1, t1) and torch.equal(s2, t2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,ncdhw,n", [(64, 32, False, (24, 20, 26)), (32, 16, True, (24, 20, 26)),
+                                              (64, 32, False, (13, 9, 37)), (32, 16, False, (20, 17, 70))])
+def test_region_split_t2_lds_kernel_is_bit_equal(cin, cout, ncdhw, n, monkeypatch):
+    """The LDS-staged transposed kernel (train mode's full-volume deconv_3_0 / deconv_2_0;
+    MVS_T2_LDS=2 forces it) against the per-lane kernel on the full output volume from the middle-half
+    input region: bit-equal outputs (same products, same K order) with BN epilogue and an output
+    addend, bit-equal stored boxes, equal bound words, and the fused sums within 1e-12 (the workgroups,
+    and so the partial sums, are partitioned differently)."""
+    from mvs_amd import ops
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _tconv_input_region
+    pad, _ = pad_outpad(*n)
+    full = tuple((0, d - 1) for d in n)
+    M = _tconv_input_region(full, n, pad)
+    org = lambda r: [lo for lo, _ in r]
+    size = lambda r: [hi - lo + 1 for lo, hi in r]
+    g = torch.Generator().manual_seed(cin + sum(n))
+    conv = torch.nn.ConvTranspose3d(cin, cout, 3)
+    conv.weight.data = torch.randn(*conv.weight.shape, generator=g) * 0.1
+    w27 = ops.region_weight(conv).to(DEV)
+    x = torch.relu(torch.randn(2, *size(M), cin, generator=g)).to(DEV)
+    bw = ops.bound_words(3, DEV)
+    bw[0, 0] = x.abs().max().view(torch.int32)
+    sc, sh, mu = (t.to(DEV) for t in _bn_params(cout, g))
+    geo = (ops.CONV_T2, list(n), [0, 0, 0], list(n), org(M), size(M), list(pad))
+    shape = (2, cout) + tuple(n) if ncdhw else (2,) + tuple(n) + (cout,)
+    add = torch.randn(shape, generator=g).to(DEV)
+    with torch.no_grad():
+        monkeypatch.setenv("MVS_T2_LDS", "2")
+        y = ops.conv3d_region_split(x, None, w27, *geo, bw[0], None, bw[1], sc, sh, mu, out_ncdhw=ncdhw, y_addend=add)
+        ys, s1, s2 = ops.conv3d_region_split_sums(x, None, w27, *geo, bw[0], out_ncdhw=ncdhw, store_origin=org(M),
+                                                  store_size=size(M))
+        monkeypatch.setenv("MVS_T2_LDS", "0")
+        ref = ops.conv3d_region_split(x, None, w27, *geo, bw[0], None, bw[2], sc, sh, mu, out_ncdhw=ncdhw,
+                                      y_addend=add)
+        rs, r1, r2 = ops.conv3d_region_split_sums(x, None, w27, *geo, bw[0], out_ncdhw=ncdhw, store_origin=org(M),
+                                                  store_size=size(M))
+        torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    assert torch.equal(bw[1].max(), bw[2].max())
+    assert torch.equal(ys, rs)
+    torch.testing.assert_close(s1, r1, rtol=1e-12, atol=1e-9)
+    torch.testing.assert_close(s2, r2, rtol=1e-12, atol=1e-9)
