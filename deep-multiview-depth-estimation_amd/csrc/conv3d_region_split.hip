@@ -521,9 +521,15 @@ void launch_s1_lds(const float* x, const void* wf, int w_exp, float* y, const fl
 // column blocks; classes run one after another (taps of class (pz, py, px): 2 per dim of parity 0, 1
 // of parity 1 -- 27 over the eight).  Same products and K order as the per-lane kernel (taps, then
 // channel blocks): bit-equal outputs.
-template <int CI, int TXB>
+// MVS_T2_TYB: class rows along y per tile / 4 (2: a 32 x 16 x 4 tile, 4 row blocks per wave, one
+// workgroup per CU: train-mode step 14.1 -> 15.5 ms; the LDS kernel on eval's small regions: eval step
+// 3.95 -> 4.24 ms, hence kT2LdsMinVoxels)
+#ifndef MVS_T2_TYB
+#define MVS_T2_TYB 1
+#endif
+template <int CI, int TXB, int TYB = MVS_T2_TYB>
 struct T2Tile {
-  static constexpr int TX = 32 * TXB, TY = 8, TZ = 4;
+  static constexpr int TX = 32 * TXB, TY = 8 * TYB, TZ = 4;
   static constexpr int PX = TX / 2 + 1, PY = TY / 2 + 1, PZ = TZ / 2 + 1, PV = PX * PY * PZ;
   static constexpr int REC = CI * 4, NCH = REC / 16;
   static constexpr int LDS = PV * REC;
@@ -536,7 +542,8 @@ __global__ __launch_bounds__(kBlock) void conv3d_t2_split_lds_kernel(
     const float* __restrict__ bn_scale, const float* __restrict__ bn_shift, const float* __restrict__ bn_mean,
     GeoS g, int tiles_x, int tiles_y, int tiles_z, const uint32_t* __restrict__ xb, uint32_t* __restrict__ yb) {
   using T = T2Tile<CI, TXB>;
-  constexpr int NB = CO / 16, CB = CI / 32, RB = 2 * TXB;
+  constexpr int NB = CO / 16, CB = CI / 32, RB = 2 * TXB * MVS_T2_TYB;
+  constexpr int NYC = 4 * MVS_T2_TYB;   // class rows along y
   static_assert(CI % 32 == 0 && CO % 16 == 0, "channel counts");
   __shared__ __attribute__((aligned(16))) char lds[T::LDS];
 
@@ -638,8 +645,8 @@ __global__ __launch_bounds__(kBlock) void conv3d_t2_split_lds_kernel(
       const int c0 = cb * 4 + kq;
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
-        const int rbi = wave * RB + r;                       // (z_c, y_c, xb) of the class's 8 TXB row blocks
-        const int xbk = rbi % TXB, yc = (rbi / TXB) & 3, zc = rbi / (4 * TXB);
+        const int rbi = wave * RB + r;                       // (z_c, y_c, xb) of the class's row blocks
+        const int xbk = rbi % TXB, yc = (rbi / TXB) % NYC, zc = rbi / (NYC * TXB);
         const int v = ((bz + zc + dz) * T::PY + (by + yc + dy)) * T::PX + (bx + xbk * 16 + m + dx);
         const h8v ahi = *reinterpret_cast<const h8v*>(lds + T::chunk_off(v, c0));
         const h8v alo = *reinterpret_cast<const h8v*>(lds + T::chunk_off(v, CI / 8 + c0));
@@ -684,7 +691,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_t2_split_lds_kernel(
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
         const int rbi = wave * RB + r;
-        const int xbk = rbi % TXB, yc = (rbi / TXB) & 3, zc = rbi / (4 * TXB);
+        const int xbk = rbi % TXB, yc = (rbi / TXB) % NYC, zc = rbi / (NYC * TXB);
         const int oz = fz + 2 * zc, oy = fy + 2 * yc;
         if (oz >= min(Z0 + T::TZ, g.o0[0] + g.on[0]) || oy >= min(Y0 + T::TY, g.o0[1] + g.on[1])) continue;
 #pragma unroll
@@ -765,7 +772,8 @@ static int split_rb(int mode, int B, const int* on) {
 }
 
 // The LDS-staged transposed kernel for large output regions (train mode's full volumes: T2 64 -> 32
-// 2.41 -> see DESIGN.md §5b); MVS_T2_LDS=0 / 2 forces the per-lane / LDS kernel (A/B and tests)
+// 2.41 -> 1.45 ms, 32 -> 16 1.10 -> 0.73 ms); MVS_T2_LDS=0 / 2 forces the per-lane / LDS kernel (A/B
+// and tests)
 constexpr long kT2LdsMinVoxels = 1l << 22;
 static bool split_t2_lds(int mode, int B, int CI, int CO, const int* on, bool per_lane, bool has_x2) {
   const char* fe = getenv("MVS_T2_LDS");   // read per call: tests switch it
