@@ -49,7 +49,14 @@ struct GeoS {
   int sbn[3];  //   voxels only (the whole output region unless a box is given)
   double* stats;   // nullable: per-workgroup float64 (sum, sum of squares) of every output voxel's
                    // value, [slot][2][CO] (train-mode BatchNorm's batch sums; slots: split_stats_slots)
+  float* ym[2];    // S2 with CO = 112 (kS2Multi): conv_1_0 / conv_2_0 / conv_3_0 at once -- y holds
+                   // channels 0-15, ym[0] 16-47, ym[1] 48-111, each its own channels-last tensor
 };
+
+// train mode's three stride-2 convolutions read the same split cost volume over the same region R2
+// (CostVolumeReg.forward_live_train): one launch with their 16 + 32 + 64 output channels loads each
+// A fragment once for all seven column blocks (three launches loaded it three times)
+constexpr int kS2Multi = 112;
 
 // per-workgroup channel sums: the wave's per-lane partial sums s / q (channel nb * 16 + (lane & 15) of
 // column block nb) reduced over the lanes of equal channel, then over the waves in a fixed order, and
@@ -286,13 +293,21 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_split_kernel(
         if (bn_scale) v = fmaxf((v - mu) * sc + sh, 0.0f);
         const bool keep = vz >= 0 && vz < g.sbn[0] && vy >= 0 && vy < g.sbn[1] && vxx >= 0 && vxx < g.sbn[2];
         const size_t vox = ((size_t)vz * g.sbn[1] + vy) * g.sbn[2] + vxx;
-        const size_t oi = g.out_cf ? ((size_t)b * CO + co) * orvol + vox : ((size_t)b * orvol + vox) * CO + co;
+        size_t oi;
+        float* dst = y;
+        if constexpr (MODE == kS2 && CO == kS2Multi) {   // (nb 0 | 1-2 | 3-6): 16 / 32 / 64 channels
+          const int ck = nb == 0 ? 16 : (nb < 3 ? 32 : 64), c0 = nb == 0 ? 0 : (nb < 3 ? 16 : 48);
+          dst = nb == 0 ? y : (nb < 3 ? g.ym[0] : g.ym[1]);
+          oi = ((size_t)b * orvol + vox) * ck + (co - c0);
+        } else {
+          oi = g.out_cf ? ((size_t)b * CO + co) * orvol + vox : ((size_t)b * orvol + vox) * CO + co;
+        }
         if (g.addend && keep) v += g.addend[oi];
         ss[nb] += (double)v;
         sq[nb] += (double)v * (double)v;
         if (!keep) continue;
         vmax = fmaxf(vmax, fabsf(v));
-        y[oi] = v;
+        dst[oi] = v;
       }
   }
   if (yb) bound_update(yb, vmax);
@@ -807,8 +822,13 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
                                const float* bn_shift, const float* bn_mean, const uint32_t* x_bound,
                                const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s, bool per_lane,
                                const float* y_addend, const int* store_origin, const int* store_size,
-                               double* stats) {
+                               double* stats, float* y_mid, float* y_high) {
   GeoS g;
+  g.ym[0] = y_mid;
+  g.ym[1] = y_high;
+  if ((CO == kS2Multi) != (y_mid != nullptr) || (y_mid != nullptr) != (y_high != nullptr) ||
+      (CO == kS2Multi && (mode != kS2 || out_cf || y_addend)))
+    return MVS_ERR_INVALID_ARGUMENT;
   g.out_cf = out_cf ? 1 : 0;
   g.addend = y_addend;
   g.stats = stats;
@@ -847,6 +867,7 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
   }
   MVS_RSPLIT_CASE(kS1, 16, 16) MVS_RSPLIT_CASE(kS1, 32, 32) MVS_RSPLIT_CASE(kS1, 64, 64)
   MVS_RSPLIT_CASE(kS2, 32, 16) MVS_RSPLIT_CASE(kS2, 32, 32) MVS_RSPLIT_CASE(kS2, 32, 64)
+  MVS_RSPLIT_CASE(kS2, 32, kS2Multi)
   MVS_RSPLIT_CASE(kT2, 64, 32) MVS_RSPLIT_CASE(kT2, 32, 16)
 #undef MVS_RSPLIT_CASE
   return MVS_ERR_INVALID_ARGUMENT;

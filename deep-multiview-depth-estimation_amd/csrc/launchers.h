@@ -150,7 +150,8 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
                                const float* bn_shift, const float* bn_mean, const uint32_t* x_bound,
                                const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s, bool per_lane = false,
                                const float* y_addend = nullptr, const int* store_origin = nullptr,
-                               const int* store_size = nullptr, double* stats = nullptr);
+                               const int* store_size = nullptr, double* stats = nullptr, float* y_mid = nullptr,
+                               float* y_high = nullptr);
 // workgroups (= float64 sum slots) of the launch launch_conv3d_region_split makes for these arguments
 long conv3d_region_split_slots(int mode, int B, int CI, int CO, const int* on, bool per_lane, bool has_x2);
 

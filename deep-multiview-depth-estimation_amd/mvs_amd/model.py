@@ -493,8 +493,8 @@ class CostVolumeReg(nn.Module):
         the full output volume (their statistics) and keep the M-region part.  ``cv`` may be the
         channel-quad volume (conv_0_0 and the stride-2 convs read it with 16-byte loads)."""
         from .ops import (CONV_S1, CONV_S2, CONV_T2, bn_relu_, bound_words, channel_stats, conv3d_k3,
-                          conv3d_k3_split, conv3d_region, conv3d_region_split_sums, deconv3d_k3s2, region_weight,
-                          softmax_depth)
+                          conv3d_k3_split, conv3d_region, conv3d_region_split_sums, conv_s2_split_multi_sums,
+                          deconv3d_k3s2, region_weight, softmax_depth)
         c4 = cv.dim() == 6
         # with split_f16 the stride-1 and transposed convs run on the split-fp16 matrix cores
         # (conv3d_region_split): their inputs' bound words are raised by the BN + ReLU passes -- rows 0-2
@@ -520,9 +520,18 @@ class CostVolumeReg(nn.Module):
             p0 = _bn_train_hip(self.BN_0, *channel_stats(y0, False), count)
         cv.record_stream(side)
         stage = []
+        zs = None
+        if cv.dtype == torch.int32 and os.environ.get("MVS_S2_MULTI", "1") != "0":
+            # conv_1_0, conv_2_0, conv_3_0 read the same split volume over the same region R2: one launch
+            # (ops.conv_s2_split_multi_sums), the volume's operands loaded once for all three
+            zs = conv_s2_split_multi_sums(cv, [region_weight(c) for c in (self.conv_1_0, self.conv_2_0,
+                                                                          self.conv_3_0)],
+                                          dims, org(R2), size(R2), pad, bound)
         for k, (conv_a, bn) in enumerate(((self.conv_1_0, self.BN_1), (self.conv_2_0, self.BN_2),
                                           (self.conv_3_0, self.BN_3))):
-            if cv.dtype == torch.int32:   # the split volume: conv_k_0 on the split-fp16 matrix cores, the
+            if zs is not None:
+                z, s1, s2 = zs[k]
+            elif cv.dtype == torch.int32:   # the split volume: conv_k_0 on the split-fp16 matrix cores, the
                 # batch sums formed in its epilogue
                 z, s1, s2 = conv3d_region_split_sums(cv, None, region_weight(conv_a), CONV_S2, dims, org(R2),
                                                      size(R2), None, None, pad, bound)

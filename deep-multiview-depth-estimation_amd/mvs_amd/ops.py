@@ -1200,9 +1200,41 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
                                          _bound_ptr(x2_bound), _bound_ptr(y_bound), ya,
                                          None if store_origin is None else _ints3(store_origin),
                                          None if store_size is None else _ints3(store_size),
-                                         None if stats is None else _lib.ptr(stats), _lib.stream_handle(dev))
+                                         None if stats is None else _lib.ptr(stats), None, None,
+                                         _lib.stream_handle(dev))
     _lib.check(st, "mvs_conv3d_region_split_fwd")
     return y
+
+
+def conv_s2_split_multi_sums(cv, weights, dims, out_origin, out_size, pad, bound):
+    """Train mode's conv_1_0, conv_2_0 and conv_3_0 (16 / 32 / 64 channels, model.py:78-80) over ONE
+    region of the split cost volume in one launch (mvs_conv3d_region_split_fwd, c_out = 112: the
+    volume's A fragments are loaded once for all three), without BN, with the per-channel float64 batch
+    sums formed in the epilogue: returns [(y, s1, s2)] per conv, y channels-last on the region.
+    ``weights``: the three region weights [27, c_k, 32] (region_weight)."""
+    _require_gpu(cv, "cv")
+    lib = _lib.load()
+    if cv.dtype != torch.int32 or cv.dim() != 6 or bound is None or bound.numel() != 8:
+        raise ValueError("the split cost volume [B, 8, D, H, W, 4] int32 and its 8 bound words")
+    if [w.shape[1] for w in weights] != [16, 32, 64] or any(w.shape[2] != 32 for w in weights):
+        raise ValueError("weights: region weights of c_out 16, 32, 64 over 32 input channels")
+    cv = cv.contiguous()
+    dev = cv.device
+    frag, ew = derived("region_split_multi", tuple(weights),
+                       lambda *ws: region_split_fragments(torch.cat([w.detach() for w in ws], 1), dev), dev)
+    b = cv.shape[0]
+    ys = [torch.empty((b,) + tuple(out_size) + (c,), device=dev, dtype=_F32) for c in (16, 32, 64)]
+    slots = split_stats_slots(CONV_S2, b, 32, 112, out_size)
+    st = torch.empty((slots, 2, 112), device=dev, dtype=torch.float64)
+    flags = _lib.MVS_CONV_IN_C4 | _lib.MVS_CONV_IN_SPLIT
+    rc = lib.mvs_conv3d_region_split_fwd(CONV_S2, flags, _lib.ptr(cv), None, _lib.ptr(frag), int(ew), _lib.ptr(ys[0]),
+                                         b, 32, 112, _ints3(dims), _ints3(out_origin), _ints3(out_size), None, None,
+                                         _ints3(pad), None, None, None, _lib.ptr(bound.contiguous()), None, None,
+                                         None, None, None, _lib.ptr(st), _lib.ptr(ys[1]), _lib.ptr(ys[2]),
+                                         _lib.stream_handle(dev))
+    _lib.check(rc, "mvs_conv3d_region_split_fwd")
+    s = st.sum(0)
+    return [(ys[k], s[0, lo:hi], s[1, lo:hi]) for k, (lo, hi) in enumerate(((0, 16), (16, 48), (48, 112)))]
 
 
 def split_stats_slots(mode, batch, c_in, c_out, out_size, per_lane=False, two_inputs=False):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 18
+#define MVS_ABI_VERSION 19
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -505,7 +505,7 @@ int mvs_conv3d_region_split_weights(const float* weight, int c_in, int c_out, un
  * words (zeroed by the caller).  MVS_CONV_S2 (conv_k_0): flags MVS_CONV_IN_C4 | MVS_CONV_IN_SPLIT, x the
  * split cost volume (mvs_cost_volume_fwd_c4_split; its fp16 parts are the operands, no conversion) or,
  * with in_origin / in_size, a box of it, x_bound its 8 bound words, x2 NULL.  Supported (mode, c_in,
- * c_out): S1 (16, 16), (32, 32), (64, 64), T2 (64, 32), (32, 16), S2 (32, 16 | 32 | 64).  Inference
+ * c_out): S1 (16, 16), (32, 32), (64, 64), T2 (64, 32), (32, 16), S2 (32, 16 | 32 | 64 | 112).  Inference
  * only (the raw outputs without the BN pointers: train-mode BN's batch statistics).  y_addend: NULL, or a
  * tensor of y's shape and layout added after BN + ReLU (deconv_3_0's output + y2, model.py:119, formed
  * once instead of on every load of deconv_2_0); the bound words then bound the sum.
@@ -515,14 +515,17 @@ int mvs_conv3d_region_split_weights(const float* weight, int c_in, int c_out, un
  * 8-byte aligned, mvs_conv3d_region_split_stats_slots(...) x 2 x c_out): every workgroup writes its
  * slot stats[slot][0 / 1][c] = sum / sum of squares over the WHOLE output region of the stored value
  * (after the epilogue); the caller adds the slots in a fixed order (run-to-run bit-identical batch
- * statistics, as mvs_channel_stats). */
+ * statistics, as mvs_channel_stats).  MVS_CONV_S2 with c_out = 112 (train mode's conv_1_0, conv_2_0
+ * and conv_3_0 over one region, weights concatenated along c_out): y receives channels 0-15, y_mid
+ * 16-47 and y_high 48-111, each its own channels-last tensor (one launch reads the volume once for all
+ * three; no addend, no MVS_CONV_OUT_NCDHW); NULL otherwise. */
 int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float* x2, const void* weight_frag,
                                 int weight_exp, float* y, int batch, int c_in, int c_out, const int* dims,
                                 const int* out_origin, const int* out_size, const int* in_origin, const int* in_size,
                                 const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                                 const unsigned* x_bound, const unsigned* x2_bound, unsigned* y_bound,
                                 const float* y_addend, const int* store_origin, const int* store_size, double* stats,
-                                void* stream);
+                                float* y_mid, float* y_high, void* stream);
 
 /* flag of mvs_conv3d_region_split_stats_slots: the call sums two inputs (x2 given) */
 #define MVS_CONV_SUM_INPUT 64

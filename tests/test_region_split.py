@@ -384,3 +384,39 @@ def test_region_split_t2_lds_kernel_is_bit_equal(cin, cout, ncdhw, n, monkeypatc
     assert torch.equal(ys, rs)
     torch.testing.assert_close(s1, r1, rtol=1e-12, atol=1e-9)
     torch.testing.assert_close(s2, r2, rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_region_split_s2_multi_equals_three_launches():
+    """Train mode's conv_1_0 / conv_2_0 / conv_3_0 in one launch (ops.conv_s2_split_multi_sums, c_out
+    16 + 32 + 64 over the same region of the split cost volume) against three conv3d_region_split_sums
+    launches: the same outputs (one weight exponent for the three weights: the products are the same up
+    to a power of two) and the same batch sums."""
+    from cameras import camera_batch, depth_range
+    from mvs_amd import ops
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _grow, _tconv_input_region
+    B, D, h, w = 2, 24, 20, 26
+    n = (D, h, w)
+    pad, _ = pad_outpad(*n)
+    M = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
+    R2 = _grow(M, n, 2)
+    org, size = [lo for lo, _ in R2], [hi - lo + 1 for lo, hi in R2]
+    g = torch.Generator().manual_seed(17)
+    K, R, T = camera_batch(B, 3, h, w)
+    d_min, d_int = depth_range(B, d_int=200.0 / D)
+    feat = torch.randn(B * 3, 32, h, w, generator=g).to(DEV)
+    ws = []
+    for c, scale in ((16, 0.1), (32, 0.03), (64, 0.2)):   # different magnitudes: one shared exponent
+        conv = torch.nn.Conv3d(32, c, 3)
+        conv.weight.data = torch.randn(c, 32, 3, 3, 3, generator=g) * scale
+        ws.append(ops.region_weight(conv).to(DEV))
+    with torch.no_grad():
+        scv, am = ops.cost_volume_c4_split(feat, K, R, T, d_min, d_int, B, 3, 0, D, 25.0)
+        multi = ops.conv_s2_split_multi_sums(scv, ws, list(n), org, size, list(pad), am)
+        for (y, s1, s2), wk in zip(multi, ws):
+            ry, r1, r2 = ops.conv3d_region_split_sums(scv, None, wk, ops.CONV_S2, list(n), org, size, None, None,
+                                                      list(pad), am)
+            torch.testing.assert_close(y, ry, rtol=1e-6, atol=1e-6 * ry.abs().max().item())
+            torch.testing.assert_close(s1, r1, rtol=1e-9, atol=1e-6)
+            torch.testing.assert_close(s2, r2, rtol=1e-9, atol=1e-6)
