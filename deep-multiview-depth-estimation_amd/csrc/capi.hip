@@ -718,7 +718,7 @@ int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float
                                 const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                                 const unsigned* x_bound, const unsigned* x2_bound, unsigned* y_bound,
                                 const float* y_addend, const int* store_origin, const int* store_size, double* stats,
-                                float* y_mid, float* y_high, void* stream) {
+                                float* y_mid, float* y_high, const float* in_bn, void* stream) {
   if (!x || !weight_frag || !y || !dims || !out_origin || !out_size || batch <= 0) return MVS_ERR_INVALID_ARGUMENT;
   if ((store_origin != nullptr) != (store_size != nullptr) || ((uintptr_t)stats & 7u)) return MVS_ERR_INVALID_ARGUMENT;
   if (store_origin)   // the store box lies inside the output region
@@ -763,7 +763,7 @@ int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float
       mode, (flags & MVS_CONV_OUT_NCDHW) != 0, x, x2, weight_frag, weight_exp, y, batch, c_in, c_out, dims, out_origin,
       out_size, io, is, pad, bn_scale, bn_shift, bn_mean, reinterpret_cast<const uint32_t*>(x_bound),
       reinterpret_cast<const uint32_t*>(x2_bound), reinterpret_cast<uint32_t*>(y_bound), (hipStream_t)stream,
-      (flags & MVS_CONV_PER_LANE) != 0, y_addend, store_origin, store_size, stats, y_mid, y_high);
+      (flags & MVS_CONV_PER_LANE) != 0, y_addend, store_origin, store_size, stats, y_mid, y_high, in_bn);
   if (st != MVS_OK) return st;
   return lc.status();
 }
@@ -774,7 +774,7 @@ long long mvs_conv3d_region_split_stats_slots(int mode, int flags, int batch, in
   for (int k = 0; k < 3; ++k)
     if (out_size[k] <= 0) return MVS_ERR_INVALID_ARGUMENT;
   return mvs::conv3d_region_split_slots(mode, batch, c_in, c_out, out_size, (flags & MVS_CONV_PER_LANE) != 0,
-                                        (flags & MVS_CONV_SUM_INPUT) != 0);
+                                        (flags & MVS_CONV_SUM_INPUT) != 0, (flags & MVS_CONV_IN_BN) != 0);
 }
 
 

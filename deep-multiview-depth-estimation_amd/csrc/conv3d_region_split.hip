@@ -49,6 +49,9 @@ struct GeoS {
   int sbn[3];  //   voxels only (the whole output region unless a box is given)
   double* stats;   // nullable: per-workgroup float64 (sum, sum of squares) of every output voxel's
                    // value, [slot][2][CO] (train-mode BatchNorm's batch sums; slots: split_stats_slots)
+  const float* in_bn;   // nullable (LDS transposed kernel): the input is relu(BN_a(x)) [+ relu(BN_b(x2))],
+                        // in_bn = [6][CI]: scale_a, shift_a, mean_a, scale_b, shift_b, mean_b (train
+                        // mode's BN + ReLU passes folded into the staging)
   float* ym[2];    // S2 with CO = 112 (kS2Multi): conv_1_0 / conv_2_0 / conv_3_0 at once -- y holds
                    // channels 0-15, ym[0] 16-47, ym[1] 48-111, each its own channels-last tensor
 };
@@ -553,9 +556,10 @@ struct T2Tile {
 
 template <int CI, int CO, int TXB>
 __global__ __launch_bounds__(kBlock) void conv3d_t2_split_lds_kernel(
-    const float* __restrict__ x, const h8v* __restrict__ wf, int w_exp, float* __restrict__ y,
-    const float* __restrict__ bn_scale, const float* __restrict__ bn_shift, const float* __restrict__ bn_mean,
-    GeoS g, int tiles_x, int tiles_y, int tiles_z, const uint32_t* __restrict__ xb, uint32_t* __restrict__ yb) {
+    const float* __restrict__ x, const float* __restrict__ x2, const h8v* __restrict__ wf, int w_exp,
+    float* __restrict__ y, const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
+    const float* __restrict__ bn_mean, GeoS g, int tiles_x, int tiles_y, int tiles_z, const uint32_t* __restrict__ xb,
+    const uint32_t* __restrict__ xb2, uint32_t* __restrict__ yb) {
   using T = T2Tile<CI, TXB>;
   constexpr int NB = CO / 16, CB = CI / 32, RB = 2 * TXB * MVS_T2_TYB;
   constexpr int NYC = 4 * MVS_T2_TYB;   // class rows along y
@@ -574,7 +578,22 @@ __global__ __launch_bounds__(kBlock) void conv3d_t2_split_lds_kernel(
   const int b = (int)blockIdx.y;
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m = lane & 15, kq = lane >> 4;
-  const int ex = act_split_exponent(bound_read(xb));
+  // the input's scale: with the folded BN + ReLU a bound of relu(BN(v)) over |v| <= bound(x) per channel
+  // (the larger of the two ends), over the channels; + the same for x2
+  float bound = bound_read(xb), bound2 = x2 ? bound_read(xb2) : 0.0f;
+  if (g.in_bn) {
+    auto bn_bound = [&](float bx, int o) {
+      float r = 0.0f;
+      for (int c = 0; c < CI; ++c) {
+        const float sc = g.in_bn[o * CI + c], sh = g.in_bn[(o + 1) * CI + c], mu = g.in_bn[(o + 2) * CI + c];
+        r = fmaxf(r, fmaxf((bx - mu) * sc, (-bx - mu) * sc) + sh);
+      }
+      return r;
+    };
+    bound = bn_bound(bound, 0);
+    if (x2) bound2 = bn_bound(bound2, 3);
+  }
+  const int ex = act_split_exponent(bound + bound2);
   // the input block's origin (absolute input coordinates): the smallest (o + P - t) / 2
   const int ilz = (Z0 + g.pad[0] - 1) >> 1, ily = (Y0 + g.pad[1] - 1) >> 1, ilx = (X0 + g.pad[2] - 1) >> 1;
 
@@ -584,9 +603,20 @@ __global__ __launch_bounds__(kBlock) void conv3d_t2_split_lds_kernel(
     constexpr int NQ = CI / 4, NIT = T::PV * NQ, PER = (NIT + kBlock - 1) / kBlock, BATCH = 8;
     const size_t rvol = (size_t)g.in[0] * g.in[1] * g.in[2];
     const Rsrc rs = make_rsrc(x + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
+    const Rsrc rs2 = make_rsrc(x2 ? x2 + (size_t)b * rvol * CI : x, x2 ? (uint32_t)(rvol * CI * 4) : 0u);
+    // relu(BN(v)) per channel of quad q (in-region voxels only: the rest stays the zero it reads as)
+    auto bn4 = [&](f4v v, int q, int o) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = 4 * q + j;
+        v[j] = fmaxf((v[j] - g.in_bn[(o + 2) * CI + c]) * g.in_bn[o * CI + c] + g.in_bn[(o + 1) * CI + c], 0.0f);
+      }
+      return v;
+    };
 #pragma unroll
     for (int k0 = 0; k0 < PER; k0 += BATCH) {
-      f4v v4[BATCH];
+      f4v v4[BATCH], w4[BATCH];
+      bool okk[BATCH];
 #pragma unroll
       for (int k = 0; k < BATCH; ++k) {
         const int e = tid + kBlock * (k0 + k);
@@ -596,15 +626,20 @@ __global__ __launch_bounds__(kBlock) void conv3d_t2_split_lds_kernel(
         const bool ok = k0 + k < PER && e < NIT && rx >= 0 && rx < g.in[2] && ry >= 0 && ry < g.in[1] && rz >= 0 &&
                         rz < g.in[0];
         const uint32_t off = ok ? (uint32_t)((((size_t)rz * g.in[1] + ry) * g.in[2] + rx) * CI + 4 * q) * 4u : kOob;
+        okk[k] = ok;
         v4[k] = ld4(rs, off, 0);
+        if (x2) w4[k] = ld4(rs2, off, 0);
       }
 #pragma unroll
       for (int k = 0; k < BATCH; ++k) {
         const int e = tid + kBlock * (k0 + k);
         if (k0 + k >= PER || e >= NIT) continue;
         const int q = e % NQ, v = e / NQ;
+        f4v a = v4[k];
+        if (g.in_bn && okk[k]) a = bn4(a, q, 0);
+        if (x2) a += (g.in_bn && okk[k]) ? bn4(w4[k], q, 3) : w4[k];
         uint2 hi, lo;
-        split4(v4[k], ex, hi, lo);
+        split4(a, ex, hi, lo);
         *reinterpret_cast<uint2*>(lds + T::chunk_off(v, q >> 1) + ((q & 1) << 3)) = hi;
         *reinterpret_cast<uint2*>(lds + T::chunk_off(v, CI / 8 + (q >> 1)) + ((q & 1) << 3)) = lo;
       }
@@ -745,14 +780,15 @@ void t2_lds_tiles(const int* on, int& tx, int& ty, int& tz) {
 }
 
 template <int CI, int CO, int TXB>
-void launch_t2_lds(const float* x, const void* wf, int w_exp, float* y, const float* sc, const float* sh,
-                   const float* mu, int B, const GeoS& g, const uint32_t* xb, uint32_t* yb, hipStream_t s) {
+void launch_t2_lds(const float* x, const float* x2, const void* wf, int w_exp, float* y, const float* sc,
+                   const float* sh, const float* mu, int B, const GeoS& g, const uint32_t* xb, const uint32_t* xb2,
+                   uint32_t* yb, hipStream_t s) {
   int tx, ty, tz;
   t2_lds_tiles<CI, TXB>(g.on, tx, ty, tz);
   const int per = tx * ty * tz;
   const dim3 grid((unsigned)((per + 7) / 8 * 8), (unsigned)B);
-  hipLaunchKernelGGL((conv3d_t2_split_lds_kernel<CI, CO, TXB>), grid, dim3(kBlock), 0, s, x,
-                     reinterpret_cast<const h8v*>(wf), w_exp, y, sc, sh, mu, g, tx, ty, tz, xb, yb);
+  hipLaunchKernelGGL((conv3d_t2_split_lds_kernel<CI, CO, TXB>), grid, dim3(kBlock), 0, s, x, x2,
+                     reinterpret_cast<const h8v*>(wf), w_exp, y, sc, sh, mu, g, tx, ty, tz, xb, xb2, yb);
 }
 
 }  // namespace
@@ -780,7 +816,13 @@ static bool split_uses_lds(int mode, int CI, int CO, bool per_lane, bool has_x2)
 // large (4 measured best: 15.3 against 15.5 ms per train-mode step with 2).  S2 with 1 / 4 row blocks:
 // eval 4.01 / 4.11 ms, train 15.9 / 15.5 ms (tools/gpu_r5_bound_ab.sh r5rb).
 constexpr long kS1WideWgs = 4096;
-static int split_rb(int mode, int B, const int* on) {
+// row blocks of the 3-in-1 S2 (kS2Multi): 4 measured slower (300 registers, one wave per SIMD: train-mode
+// step 12.9 -> 13.1 ms)
+#ifndef MVS_S2M_RB
+#define MVS_S2M_RB 2
+#endif
+static int split_rb(int mode, int B, const int* on, int CO) {
+  if (mode == kS2 && CO == kS2Multi) return MVS_S2M_RB;
   if (mode != kS1) return 2;
   const long rows = (long)B * on[0] * on[1] * on[2];
   return rows >= kS1WideWgs * (kBlock / 64) * 16 * 4 ? 4 : 2;
@@ -790,16 +832,19 @@ static int split_rb(int mode, int B, const int* on) {
 // 2.41 -> 1.45 ms, 32 -> 16 1.10 -> 0.73 ms); MVS_T2_LDS=0 / 2 forces the per-lane / LDS kernel (A/B
 // and tests)
 constexpr long kT2LdsMinVoxels = 1l << 22;
-static bool split_t2_lds(int mode, int B, int CI, int CO, const int* on, bool per_lane, bool has_x2) {
+static bool split_t2_lds(int mode, int B, int CI, int CO, const int* on, bool per_lane, bool has_x2,
+                         bool in_bn = false) {
+  if (mode != kT2 || !((CI == 64 && CO == 32) || (CI == 32 && CO == 16))) return false;
+  if (in_bn) return true;   // the folded input BN + ReLU: this kernel only
   const char* fe = getenv("MVS_T2_LDS");   // read per call: tests switch it
   const int force = fe ? atoi(fe) : 1;
-  if (mode != kT2 || per_lane || has_x2 || force == 0) return false;
-  if (!((CI == 64 && CO == 32) || (CI == 32 && CO == 16))) return false;
+  if (per_lane || force == 0) return false;
   return force == 2 || (long)B * on[0] * on[1] * on[2] >= kT2LdsMinVoxels;
 }
 
-long conv3d_region_split_slots(int mode, int B, int CI, int CO, const int* on, bool per_lane, bool has_x2) {
-  if (split_t2_lds(mode, B, CI, CO, on, per_lane, has_x2)) {
+long conv3d_region_split_slots(int mode, int B, int CI, int CO, const int* on, bool per_lane, bool has_x2,
+                               bool in_bn) {
+  if (split_t2_lds(mode, B, CI, CO, on, per_lane, has_x2, in_bn)) {
     int tx, ty, tz;
     if (CI == 64) t2_lds_tiles<64, 1>(on, tx, ty, tz);
     else t2_lds_tiles<32, 2>(on, tx, ty, tz);
@@ -812,7 +857,7 @@ long conv3d_region_split_slots(int mode, int B, int CI, int CO, const int* on, b
     else s1_lds_tiles<64>(on, tx, ty, tz);
     return (long)B * tx * ty * tz;
   }
-  const dim3 gr = split_mode_grid(mode, split_rb(mode, B, on), B, on);
+  const dim3 gr = split_mode_grid(mode, split_rb(mode, B, on, CO), B, on);
   return (long)gr.x * gr.y * gr.z;
 }
 
@@ -822,8 +867,9 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
                                const float* bn_shift, const float* bn_mean, const uint32_t* x_bound,
                                const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s, bool per_lane,
                                const float* y_addend, const int* store_origin, const int* store_size,
-                               double* stats, float* y_mid, float* y_high) {
+                               double* stats, float* y_mid, float* y_high, const float* in_bn) {
   GeoS g;
+  g.in_bn = in_bn;
   g.ym[0] = y_mid;
   g.ym[1] = y_high;
   if ((CO == kS2Multi) != (y_mid != nullptr) || (y_mid != nullptr) != (y_high != nullptr) ||
@@ -844,7 +890,7 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
   }
 #define MVS_RSPLIT_CASE(MD, A, C)                                                                          \
   if (mode == MD && CI == A && CO == C) {                                                                  \
-    if (split_rb(mode, B, on) == 4)                                                                        \
+    if (split_rb(mode, B, on, CO) == 4)                                                                    \
       launch_split_mode<MD, A, C, 4>(x, x2, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound,   \
                                      x2_bound, y_bound, s);                                                \
     else                                                                                                   \
@@ -854,9 +900,12 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
   }
   // S1: conv_k_1 (16 / 32 / 64 channels; LDS-staged operands per MVS_S1_LDS); T2: deconv_3_0 (64 -> 32),
   // deconv_2_0 (32 -> 16); S2: conv_k_0 from the split cost volume (32 -> 16 / 32 / 64)
-  if (split_t2_lds(mode, B, CI, CO, on, per_lane, x2 != nullptr)) {
-    if (CI == 64) launch_t2_lds<64, 32, 1>(x, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, y_bound, s);
-    else launch_t2_lds<32, 16, 2>(x, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, y_bound, s);
+  if (in_bn && !split_t2_lds(mode, B, CI, CO, on, per_lane, x2 != nullptr, true)) return MVS_ERR_INVALID_ARGUMENT;
+  if (split_t2_lds(mode, B, CI, CO, on, per_lane, x2 != nullptr, in_bn != nullptr)) {
+    if (CI == 64)
+      launch_t2_lds<64, 32, 1>(x, x2, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, x2_bound, y_bound, s);
+    else
+      launch_t2_lds<32, 16, 2>(x, x2, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, x2_bound, y_bound, s);
     return MVS_OK;
   }
   if (split_uses_lds(mode, CI, CO, per_lane, x2 != nullptr)) {

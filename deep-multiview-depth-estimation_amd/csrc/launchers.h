@@ -151,9 +151,10 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
                                const uint32_t* x2_bound, uint32_t* y_bound, hipStream_t s, bool per_lane = false,
                                const float* y_addend = nullptr, const int* store_origin = nullptr,
                                const int* store_size = nullptr, double* stats = nullptr, float* y_mid = nullptr,
-                               float* y_high = nullptr);
+                               float* y_high = nullptr, const float* in_bn = nullptr);
 // workgroups (= float64 sum slots) of the launch launch_conv3d_region_split makes for these arguments
-long conv3d_region_split_slots(int mode, int B, int CI, int CO, const int* on, bool per_lane, bool has_x2);
+long conv3d_region_split_slots(int mode, int B, int CI, int CO, const int* on, bool per_lane, bool has_x2,
+                               bool in_bn = false);
 
 // channel_ops.hip: train-mode BatchNorm pieces -- per-channel float64 sums into
 // stats[slot][2][C] (64 slots) and y = relu(BN(x)) [+ relu(BN'(r))], channels-last or NCDHW

@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmvs_cost_volume.so"
 # MVS_LIB_PATH: load another build of the same ABI (A/B kernel experiments, tools/gpu_*_ab.sh)
 LIB_PATH = os.environ.get("MVS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 MVS_OK = 0
 MVS_BWD_DETERMINISTIC = 1
@@ -27,6 +27,7 @@ MVS_CONV_S1, MVS_CONV_S2, MVS_CONV_T2 = 0, 1, 2
 MVS_CONV_OUT_NCDHW = 1
 MVS_CONV_PER_LANE = 32
 MVS_CONV_SUM_INPUT = 64
+MVS_CONV_IN_BN = 128
 MVS_CONV_IN_C4 = 2
 MVS_CONV_WINO_Z = 4
 MVS_CONV_IN_BF16 = 8
@@ -91,7 +92,7 @@ SIGNATURES = {
     "mvs_conv3d_region_fwd": (_c_int, [_c_int, _c_int, _p, _p, _p, _p, _c_int, _c_int, _c_int] + [_p] * 12),
     "mvs_conv3d_region_split_weights": (_c_int, [_p, _c_int, _c_int, _p, _p]),
     "mvs_conv3d_region_split_fwd": (_c_int, [_c_int, _c_int, _p, _p, _p, _c_int, _p, _c_int, _c_int, _c_int]
-                                    + [_p] * 19),
+                                    + [_p] * 20),
     "mvs_conv3d_region_split_stats_slots": (ctypes.c_longlong, [_c_int] * 5 + [_p]),
     "mvs_softmax_depth_fwd": (_c_int, [_p, _c_int, _c_int, _c_int, _c_int, _p, _p]),
     "mvs_depth_hypotheses_fwd": (_c_int, [_p, _p, _c_int, _c_int, _c_float, _p, _p]),

@@ -498,7 +498,8 @@ class CostVolumeReg(nn.Module):
         c4 = cv.dim() == 6
         # with split_f16 the stride-1 and transposed convs run on the split-fp16 matrix cores
         # (conv3d_region_split): their inputs' bound words are raised by the BN + ReLU passes -- rows 0-2
-        # the conv_k_1 inputs, 4-5 conv_2_1 / conv_3_1's normalised outputs, 6 deconv_3_0's
+        # the conv_k_1 inputs, 4-5 conv_2_1 / conv_3_1's outputs, 6 deconv_3_0's (raw when the transposed
+        # convs fold the BN + ReLU into their staging: `fold`)
         bw = (bound_words(7, cv.device) if self.split_f16 and os.environ.get("MVS_REGION_SPLIT", "1") != "0"
               else None)
         bwr = lambda k: None if bw is None else bw[k]
@@ -542,6 +543,9 @@ class CostVolumeReg(nn.Module):
             p = _bn_train_hip(bn, s1, s2, count)
             stage.append((bn_relu_(z, True, *p, y_bound=bwr(k)), p))   # p: relu(BN(0)) outside M
         lv = []
+        # conv_2_1 / conv_3_1's BN + ReLU (and deconv_3_0's, with the + y2 sum) applied in the transposed
+        # convs' LDS staging instead of a pass over each tensor (ops.conv3d_region_split_sums x_bn / x2_bn)
+        fold = bw is not None and os.environ.get("MVS_T2_FOLD", "1") != "0"
         for k, ((y, pa), conv_b, bn) in enumerate(zip(stage, (self.conv_1_1, self.conv_2_1, self.conv_3_1),
                                                      (self.BN_1, self.BN_2, self.BN_3))):
             # level 1 only feeds deconv_1_0's input sum: channels-first for its loads
@@ -549,16 +553,36 @@ class CostVolumeReg(nn.Module):
             if bw is not None:   # sums over R1 in the epilogue, only M stored (the next layers read M)
                 z, s1, s2 = conv3d_region_split_sums(y, None, region_weight(conv_b), CONV_S1, dims, org(R1),
                                                      size(R1), org(R2), size(R2), None, bw[k], out_ncdhw=cf,
-                                                     store_origin=org(M), store_size=size(M))
+                                                     store_origin=org(M), store_size=size(M),
+                                                     y_bound=bw[3 + k] if fold and not cf else None)
             else:
                 z = conv3d_region(y, None, region_weight(conv_b), CONV_S1, dims, org(R1), size(R1), org(R2),
                                   size(R2), None, out_ncdhw=cf)
                 s1, s2 = channel_stats(z, not cf)
                 z = (_crop_cf if cf else _crop_cl)(z, R1, M)
             p = _bn_train_hip(bn, s1, s2, count, border=(conv_b.weight, R1, n, bsz, pa))
-            lv.append(bn_relu_(z, not cf, *p, y_bound=None if cf else bwr(3 + k)))
+            if fold and not cf:
+                lv.append((z, p))   # raw, with its BN: normalised in the transposed conv's staging
+            else:
+                lv.append(bn_relu_(z, not cf, *p, y_bound=None if cf else bwr(3 + k)))
         y1, y2, y3 = lv
-        if bw is not None:
+        if fold:
+            (z3, p3), (z2, p2) = y3, y2
+            z, s1, s2 = conv3d_region_split_sums(z3, None, region_weight(self.deconv_3_0), CONV_T2, dims, [0, 0, 0],
+                                                 dims, org(M), size(M), pad, bw[5], y_bound=bw[6],
+                                                 store_origin=org(M), store_size=size(M), x_bn=p3)
+            p = _bn_train_hip(self.BN_2, s1, s2, count)
+            # deconv_2_0 reads relu(BN_2(deconv_3_0)) + relu(BN_2(conv_2_1)) (model.py:119-120), both formed
+            # in its staging from the raw tensors
+            z, s1, s2 = conv3d_region_split_sums(z, z2, region_weight(self.deconv_2_0), CONV_T2, dims, [0, 0, 0],
+                                                 dims, org(M), size(M), pad, bw[6], x2_bound=bw[4], out_ncdhw=True,
+                                                 store_origin=org(M), store_size=size(M), x_bn=p, x2_bn=p2)
+            p = _bn_train_hip(self.BN_1, s1, s2, count)
+            c1 = y1.shape[1]
+            one, zero = torch.ones(c1, device=y1.device), torch.zeros(c1, device=y1.device)
+            y2 = bn_relu_(z, False, *p, r=y1, r_bn=(one, zero, zero))
+            y1 = z3 = z2 = None
+        elif bw is not None:
             # the transposed convs over the full output (their batch sums, formed in the epilogue), only
             # M stored: the next layer reads M
             z, s1, s2 = conv3d_region_split_sums(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims,

@@ -1148,7 +1148,7 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
                         bn_mean: Optional[torch.Tensor] = None, out_ncdhw: bool = False,
                         per_lane: bool = False, y_addend: Optional[torch.Tensor] = None,
                         store_origin: Optional[list[int]] = None, store_size: Optional[list[int]] = None,
-                        stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+                        stats: Optional[torch.Tensor] = None, in_bn: Optional[torch.Tensor] = None) -> torch.Tensor:
     """conv3d_region's CONV_S1 / CONV_T2 convolutions on the f16 matrix cores with split operands
     (mvs_conv3d_region_split_fwd, csrc/conv3d_region_split.hip): same geometry, layouts and epilogue;
     the input scaled by its bound words ``x_bound`` (+ ``x2_bound`` for the sum x + x2), ``y_bound``
@@ -1157,7 +1157,9 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
     4], or a box of it with in_origin / in_size), x_bound its 8 bound words.  ``store_origin`` /
     ``store_size``: y holds only that box of the output region (the rest is computed, not stored);
     ``stats``: float64 [split_stats_slots, 2, c_out] receiving per-workgroup sums over the whole
-    output region (conv3d_region_split_sums).  fp32-level error.  Inference only."""
+    output region (conv3d_region_split_sums).  ``in_bn`` (CONV_T2, 64 -> 32 / 32 -> 16): fp32 [6, c_in]
+    = (scale, shift, mean) of x then x2 -- the input is relu(BN(x)) [+ relu(BN(x2))], the bound words
+    bound the raw tensors.  fp32-level error.  Inference only."""
     _require_gpu(x, "x")
     lib = _lib.load()
     flags = (_lib.MVS_CONV_OUT_NCDHW if out_ncdhw else 0) | (_lib.MVS_CONV_PER_LANE if per_lane else 0)
@@ -1182,7 +1184,7 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
     y = torch.empty(shape, device=dev, dtype=_F32)
     xb = (_lib.ptr(x_bound.contiguous()) if mode == CONV_S2 else _bound_ptr(x_bound))
     if stats is not None:
-        slots = split_stats_slots(mode, b, cin, cout, out_size, per_lane, x2 is not None)
+        slots = split_stats_slots(mode, b, cin, cout, out_size, per_lane, x2 is not None, in_bn is not None)
         if stats.dtype != torch.float64 or stats.numel() != slots * 2 * cout or not stats.is_contiguous():
             raise ValueError("stats: a contiguous float64 tensor of %d x 2 x %d" % (slots, cout))
     ya = None
@@ -1201,6 +1203,7 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
                                          None if store_origin is None else _ints3(store_origin),
                                          None if store_size is None else _ints3(store_size),
                                          None if stats is None else _lib.ptr(stats), None, None,
+                                         None if in_bn is None else _lib.ptr(in_bn.contiguous()),
                                          _lib.stream_handle(dev))
     _lib.check(st, "mvs_conv3d_region_split_fwd")
     return y
@@ -1230,16 +1233,17 @@ def conv_s2_split_multi_sums(cv, weights, dims, out_origin, out_size, pad, bound
     rc = lib.mvs_conv3d_region_split_fwd(CONV_S2, flags, _lib.ptr(cv), None, _lib.ptr(frag), int(ew), _lib.ptr(ys[0]),
                                          b, 32, 112, _ints3(dims), _ints3(out_origin), _ints3(out_size), None, None,
                                          _ints3(pad), None, None, None, _lib.ptr(bound.contiguous()), None, None,
-                                         None, None, None, _lib.ptr(st), _lib.ptr(ys[1]), _lib.ptr(ys[2]),
+                                         None, None, None, _lib.ptr(st), _lib.ptr(ys[1]), _lib.ptr(ys[2]), None,
                                          _lib.stream_handle(dev))
     _lib.check(rc, "mvs_conv3d_region_split_fwd")
     s = st.sum(0)
     return [(ys[k], s[0, lo:hi], s[1, lo:hi]) for k, (lo, hi) in enumerate(((0, 16), (16, 48), (48, 112)))]
 
 
-def split_stats_slots(mode, batch, c_in, c_out, out_size, per_lane=False, two_inputs=False):
+def split_stats_slots(mode, batch, c_in, c_out, out_size, per_lane=False, two_inputs=False, in_bn=False):
     """Sum slots (workgroups) of a conv3d_region_split launch (mvs_conv3d_region_split_stats_slots)."""
-    flags = (_lib.MVS_CONV_PER_LANE if per_lane else 0) | (_lib.MVS_CONV_SUM_INPUT if two_inputs else 0)
+    flags = ((_lib.MVS_CONV_PER_LANE if per_lane else 0) | (_lib.MVS_CONV_SUM_INPUT if two_inputs else 0)
+             | (_lib.MVS_CONV_IN_BN if in_bn else 0))
     n = _lib.load().mvs_conv3d_region_split_stats_slots(int(mode), flags, int(batch), int(c_in), int(c_out),
                                                        _ints3(out_size))
     if n <= 0:
@@ -1248,18 +1252,27 @@ def split_stats_slots(mode, batch, c_in, c_out, out_size, per_lane=False, two_in
 
 
 def conv3d_region_split_sums(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, x_bound,
-                             x2_bound=None, y_bound=None, out_ncdhw=False, store_origin=None, store_size=None):
+                             x2_bound=None, y_bound=None, out_ncdhw=False, store_origin=None, store_size=None,
+                             x_bn=None, x2_bn=None):
     """conv3d_region_split without the BN epilogue (train mode's raw output), with the per-channel
     float64 (sum, sum of squares) over the whole output region formed in the kernel's epilogue:
     returns (y, s1, s2), y holding the store box (default: the output region).  Replaces
     channel_stats(y) on the output: no second pass over it, and y may hold only the part the next layer
-    reads."""
+    reads.  ``x_bn`` / ``x2_bn``: (scale, shift, mean) -- the input is relu(BN(x)) [+
+    relu(BN(x2))] (CONV_T2's LDS kernel: the BN + ReLU passes folded into its staging)."""
     b, cout, cin = x.shape[0], weight.shape[1], weight.shape[2]
-    slots = split_stats_slots(mode, b, cin, cout, out_size, False, x2 is not None)
+    in_bn = None
+    if x2 is not None and (x_bn is None) != (x2_bn is None):
+        raise ValueError("x_bn and x2_bn go together when x2 is given")
+    if x_bn is not None:
+        ones, zeros = torch.ones(cin, device=x.device), torch.zeros(cin, device=x.device)
+        rows = list(x_bn) + (list(x2_bn) if x2_bn is not None else [ones, zeros, zeros])
+        in_bn = torch.stack([t.detach().to(device=x.device, dtype=_F32).reshape(cin) for t in rows])
+    slots = split_stats_slots(mode, b, cin, cout, out_size, False, x2 is not None, in_bn is not None)
     st = torch.empty((slots, 2, cout), device=x.device, dtype=torch.float64)
     y = conv3d_region_split(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, x_bound,
                             x2_bound, y_bound, out_ncdhw=out_ncdhw, store_origin=store_origin,
-                            store_size=store_size, stats=st)
+                            store_size=store_size, stats=st, in_bn=in_bn)
     s = st.sum(0)
     return y, s[0], s[1]
 
@@ -1267,7 +1280,7 @@ def conv3d_region_split_sums(x, x2, weight, mode, dims, out_origin, out_size, in
 @conv3d_region_split.register_fake
 def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, x_bound, x2_bound, y_bound,
       bn_scale=None, bn_shift=None, bn_mean=None, out_ncdhw=False, per_lane=False, y_addend=None,
-      store_origin=None, store_size=None, stats=None):
+      store_origin=None, store_size=None, stats=None, in_bn=None):
     size = tuple(out_size if store_size is None else store_size)
     if out_ncdhw:
         return x.new_empty((x.shape[0], weight.shape[1]) + size, dtype=_F32)

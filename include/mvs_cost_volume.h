@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 19
+#define MVS_ABI_VERSION 20
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -518,19 +518,23 @@ int mvs_conv3d_region_split_weights(const float* weight, int c_in, int c_out, un
  * statistics, as mvs_channel_stats).  MVS_CONV_S2 with c_out = 112 (train mode's conv_1_0, conv_2_0
  * and conv_3_0 over one region, weights concatenated along c_out): y receives channels 0-15, y_mid
  * 16-47 and y_high 48-111, each its own channels-last tensor (one launch reads the volume once for all
- * three; no addend, no MVS_CONV_OUT_NCDHW); NULL otherwise. */
+ * three; no addend, no MVS_CONV_OUT_NCDHW); NULL otherwise.  in_bn: NULL, or (MVS_CONV_T2 with (c_in,
+ * c_out) = (64, 32) or (32, 16): the LDS-staged kernel) DEVICE fp32 [6][c_in] = (scale, shift, mean)
+ * of x then of x2: the input is relu((x - mean) scale + shift) [+ the same of x2] -- train mode's BN +
+ * ReLU passes folded into the staging; x_bound / x2_bound then bound the raw x / x2. */
 int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float* x2, const void* weight_frag,
                                 int weight_exp, float* y, int batch, int c_in, int c_out, const int* dims,
                                 const int* out_origin, const int* out_size, const int* in_origin, const int* in_size,
                                 const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                                 const unsigned* x_bound, const unsigned* x2_bound, unsigned* y_bound,
                                 const float* y_addend, const int* store_origin, const int* store_size, double* stats,
-                                float* y_mid, float* y_high, void* stream);
+                                float* y_mid, float* y_high, const float* in_bn, void* stream);
 
-/* flag of mvs_conv3d_region_split_stats_slots: the call sums two inputs (x2 given) */
+/* flags of mvs_conv3d_region_split_stats_slots: the call sums two inputs (x2 given); it passes in_bn */
 #define MVS_CONV_SUM_INPUT 64
+#define MVS_CONV_IN_BN 128
 /* Number of float64 sum slots (workgroups) of the mvs_conv3d_region_split_fwd call with this mode,
- * flags (MVS_CONV_PER_LANE, MVS_CONV_SUM_INPUT), batch, channels and out_size; < 0 on invalid
+ * flags (MVS_CONV_PER_LANE, MVS_CONV_SUM_INPUT, MVS_CONV_IN_BN), batch, channels and out_size; < 0 on invalid
  * arguments.  Host-only: no device work. */
 long long mvs_conv3d_region_split_stats_slots(int mode, int flags, int batch, int c_in, int c_out,
                                               const int* out_size);

@@ -420,3 +420,45 @@ def test_region_split_s2_multi_equals_three_launches():
             torch.testing.assert_close(y, ry, rtol=1e-6, atol=1e-6 * ry.abs().max().item())
             torch.testing.assert_close(s1, r1, rtol=1e-9, atol=1e-6)
             torch.testing.assert_close(s2, r2, rtol=1e-9, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,two", [(64, 32, False), (32, 16, True)])
+def test_region_split_t2_folded_input_bn(cin, cout, two, monkeypatch):
+    """Train mode's BN + ReLU folded into the LDS transposed kernel's staging (x_bn / x2_bn): equal to
+    the same kernel on the explicitly normalised (and summed) input within fp32-level error -- the input
+    scale then comes from a bound of relu(BN(.)) over the raw tensors' bound words, a few bits coarser than
+    the normalised tensor's own -- with the same batch sums."""
+    from mvs_amd import ops
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _tconv_input_region
+    n = (24, 20, 26)
+    pad, _ = pad_outpad(*n)
+    full = tuple((0, d - 1) for d in n)
+    M = _tconv_input_region(full, n, pad)
+    org = lambda r: [lo for lo, _ in r]
+    size = lambda r: [hi - lo + 1 for lo, hi in r]
+    g = torch.Generator().manual_seed(cin * 3 + int(two))
+    conv = torch.nn.ConvTranspose3d(cin, cout, 3)
+    conv.weight.data = torch.randn(*conv.weight.shape, generator=g) * 0.1
+    w27 = ops.region_weight(conv).to(DEV)
+    raw = [torch.randn(2, *size(M), cin, generator=g).to(DEV) for _ in range(2 if two else 1)]
+    bns = [tuple(t.to(DEV) for t in _bn_params(cin, g)) for _ in raw]
+    bw = ops.bound_words(4, DEV)
+    for k, r in enumerate(raw):
+        bw[k, 0] = r.abs().max().view(torch.int32)
+    norm = sum(torch.relu((r - p[2]) * p[0] + p[1]) for r, p in zip(raw, bns))
+    bw[2, 0] = norm.abs().max().view(torch.int32)
+    geo = (ops.CONV_T2, list(n), [0, 0, 0], list(n), org(M), size(M), list(pad))
+    with torch.no_grad():
+        monkeypatch.setenv("MVS_T2_LDS", "2")
+        ref, r1, r2 = ops.conv3d_region_split_sums(norm.contiguous(), None, w27, *geo, bw[2], store_origin=org(M),
+                                                   store_size=size(M))
+        got, s1, s2 = ops.conv3d_region_split_sums(raw[0], raw[1] if two else None, w27, *geo, bw[0],
+                                                   x2_bound=bw[1] if two else None, store_origin=org(M),
+                                                   store_size=size(M), x_bn=bns[0], x2_bn=bns[1] if two else None)
+        torch.cuda.synchronize()
+    scale = ref.abs().max().item()
+    assert (got - ref).abs().max().item() <= 2e-6 * scale
+    torch.testing.assert_close(s1, r1, rtol=1e-5, atol=1e-5 * scale)
+    torch.testing.assert_close(s2, r2, rtol=1e-5, atol=1e-5 * scale * scale)
