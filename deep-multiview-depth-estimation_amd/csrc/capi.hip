@@ -720,7 +720,8 @@ int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float
                                 const float* y_addend, const int* store_origin, const int* store_size, double* stats,
                                 float* y_mid, float* y_high, const float* in_bn, void* stream) {
   if (!x || !weight_frag || !y || !dims || !out_origin || !out_size || batch <= 0) return MVS_ERR_INVALID_ARGUMENT;
-  if ((store_origin != nullptr) != (store_size != nullptr) || ((uintptr_t)stats & 7u)) return MVS_ERR_INVALID_ARGUMENT;
+  if ((store_origin != nullptr) != (store_size != nullptr) || ((uintptr_t)stats & 7u) || ((uintptr_t)in_bn & 15u))
+    return MVS_ERR_INVALID_ARGUMENT;
   if (store_origin)   // the store box lies inside the output region
     for (int k = 0; k < 3; ++k)
       if (store_size[k] <= 0 || store_origin[k] < out_origin[k] ||

@@ -582,12 +582,15 @@ __global__ __launch_bounds__(kBlock) void conv3d_t2_split_lds_kernel(
   // (the larger of the two ends), over the channels; + the same for x2
   float bound = bound_read(xb), bound2 = x2 ? bound_read(xb2) : 0.0f;
   if (g.in_bn) {
-    auto bn_bound = [&](float bx, int o) {
+    static_assert(CI <= 64, "one channel per lane");
+    auto bn_bound = [&](float bx, int o) {   // lane c: channel c, then the wave's max (whole wave)
       float r = 0.0f;
-      for (int c = 0; c < CI; ++c) {
-        const float sc = g.in_bn[o * CI + c], sh = g.in_bn[(o + 1) * CI + c], mu = g.in_bn[(o + 2) * CI + c];
-        r = fmaxf(r, fmaxf((bx - mu) * sc, (-bx - mu) * sc) + sh);
+      if (lane < CI) {
+        const float sc = g.in_bn[o * CI + lane], sh = g.in_bn[(o + 1) * CI + lane], mu = g.in_bn[(o + 2) * CI + lane];
+        r = fmaxf(fmaxf((bx - mu) * sc, (-bx - mu) * sc) + sh, 0.0f);
       }
+#pragma unroll
+      for (int k = 32; k > 0; k >>= 1) r = fmaxf(r, __shfl_xor(r, k));
       return r;
     };
     bound = bn_bound(bound, 0);
@@ -604,13 +607,24 @@ __global__ __launch_bounds__(kBlock) void conv3d_t2_split_lds_kernel(
     const size_t rvol = (size_t)g.in[0] * g.in[1] * g.in[2];
     const Rsrc rs = make_rsrc(x + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
     const Rsrc rs2 = make_rsrc(x2 ? x2 + (size_t)b * rvol * CI : x, x2 ? (uint32_t)(rvol * CI * 4) : 0u);
-    // relu(BN(v)) per channel of quad q (in-region voxels only: the rest stays the zero it reads as)
-    auto bn4 = [&](f4v v, int q, int o) {
+    // relu(BN(v)) per channel of the thread's quad (in-region voxels only: the rest stays the zero it
+    // reads as).  kBlock is a multiple of NQ, so a thread's quad q = tid % NQ is the same for all its
+    // items: its 4 channels' parameters are loaded once
+    static_assert(kBlock % NQ == 0, "one quad per thread");
+    f4v bsc[2], bsh[2], bmu[2];
+    if (g.in_bn) {
+      const int c = 4 * (tid % NQ);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = 4 * q + j;
-        v[j] = fmaxf((v[j] - g.in_bn[(o + 2) * CI + c]) * g.in_bn[o * CI + c] + g.in_bn[(o + 1) * CI + c], 0.0f);
+      for (int o = 0; o < 2; ++o) {
+        bsc[o] = *reinterpret_cast<const f4v*>(g.in_bn + (3 * o) * CI + c);
+        bsh[o] = *reinterpret_cast<const f4v*>(g.in_bn + (3 * o + 1) * CI + c);
+        bmu[o] = *reinterpret_cast<const f4v*>(g.in_bn + (3 * o + 2) * CI + c);
       }
+    }
+    auto bn4 = [&](f4v v, int, int o) {
+      const int k = o / 3;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = fmaxf((v[j] - bmu[k][j]) * bsc[k][j] + bsh[k][j], 0.0f);
       return v;
     };
 #pragma unroll

@@ -519,7 +519,7 @@ int mvs_conv3d_region_split_weights(const float* weight, int c_in, int c_out, un
  * and conv_3_0 over one region, weights concatenated along c_out): y receives channels 0-15, y_mid
  * 16-47 and y_high 48-111, each its own channels-last tensor (one launch reads the volume once for all
  * three; no addend, no MVS_CONV_OUT_NCDHW); NULL otherwise.  in_bn: NULL, or (MVS_CONV_T2 with (c_in,
- * c_out) = (64, 32) or (32, 16): the LDS-staged kernel) DEVICE fp32 [6][c_in] = (scale, shift, mean)
+ * c_out) = (64, 32) or (32, 16): the LDS-staged kernel) DEVICE fp32 [6][c_in], 16-byte aligned = (scale, shift, mean)
  * of x then of x2: the input is relu((x - mean) scale + shift) [+ the same of x2] -- train mode's BN +
  * ReLU passes folded into the staging; x_bound / x2_bound then bound the raw x / x2. */
 int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float* x2, const void* weight_frag,
