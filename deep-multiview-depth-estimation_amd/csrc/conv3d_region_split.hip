@@ -60,6 +60,14 @@ struct GeoS {
 // (CostVolumeReg.forward_live_train): one launch with their 16 + 32 + 64 output channels loads each
 // A fragment once for all seven column blocks (three launches loaded it three times)
 constexpr int kS2Multi = 112;
+#ifndef MVS_S2M_BLDS
+#define MVS_S2M_BLDS 1
+#endif
+// S1 64 -> 64 with the K block's weights in LDS: with 4 row blocks 274 registers, one wave per SIMD:
+// train-mode step 12.3 -> 13.4 ms (off by default)
+#ifndef MVS_S1_BLDS
+#define MVS_S1_BLDS 0
+#endif
 
 // per-workgroup channel sums: the wave's per-lane partial sums s / q (channel nb * 16 + (lane & 15) of
 // column block nb) reduced over the lanes of equal channel, then over the waves in a fixed order, and
@@ -135,7 +143,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_split_kernel(
   const int row0 = (bx * (kBlock / 64) + ((int)threadIdx.x >> 6)) * kRows;
   // wave-uniform; no barriers in this kernel unless sums are gathered (then every wave stays, the
   // ones past the rows on zeros)
-  if (row0 >= rows && !g.stats) return;
+  if (row0 >= rows && !g.stats && !(MODE == kS2 && CO == kS2Multi) && !(MODE == kS1 && CI == 64 && MVS_S1_BLDS)) return;
 
   // the input's scale: max|x| (+ max|x2|) 2^ex < 2^14; S2: the split volume's own exponent
   int ex;
@@ -211,14 +219,48 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_split_kernel(
   };
   // one K-32 block: the row blocks' split A fragments, the column blocks' (hi, lo) weight fragments
   // (wf[kb][nb][part][lane]), then x_hi w_hi, x_hi w_lo, x_lo w_hi per (row block, column block)
+  // BL (the 3-in-1 S2: seven column blocks, 14 KB of weight fragments per K block, 378 KB in all):
+  // each K block's fragments are fetched once per workgroup into an LDS double buffer (one barrier per
+  // K block; the next block's global loads in flight under this block's MFMAs) instead of by every wave
+  // from L2.  Every wave runs the same K sequence (taps, then channel blocks).
+  constexpr bool BL = (MODE == kS2 && CO == kS2Multi && MVS_S2M_BLDS) || (MODE == kS1 && CI == 64 && MVS_S1_BLDS);
+  constexpr int BFR = NB * 2 * 64;                        // h8v per K block
+  constexpr int BPER = (BFR + kBlock - 1) / kBlock;
+  __shared__ h8v blds[BL ? 2 : 1][BL ? BFR : 1];
+  h8v bpre[BPER];
+  auto bfetch = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < BPER; ++i) {
+      const int e = (int)threadIdx.x + i * kBlock;
+      if (e < BFR) bpre[i] = wf[(size_t)kb * BFR + e];
+    }
+  };
+  auto bstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < BPER; ++i) {
+      const int e = (int)threadIdx.x + i * kBlock;
+      if (e < BFR) blds[buf][e] = bpre[i];
+    }
+  };
+  if constexpr (BL) {
+    bfetch(0);
+    bstore(0);
+    __syncthreads();
+    bfetch(1);
+  }
   auto kblock = [&](int kb, const uint32_t (&vx)[RB], int c0) {
     h8v ahi[RB], alo[RB], bhi[NB], blo[NB];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) load_split(vx[rb], c0, ahi[rb], alo[rb]);
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
-      bhi[nb] = wf[((size_t)(kb * NB + nb) * 2 + 0) * 64 + lane];
-      blo[nb] = wf[((size_t)(kb * NB + nb) * 2 + 1) * 64 + lane];
+      if constexpr (BL) {
+        bhi[nb] = blds[kb & 1][(nb * 2 + 0) * 64 + lane];
+        blo[nb] = blds[kb & 1][(nb * 2 + 1) * 64 + lane];
+      } else {
+        bhi[nb] = wf[((size_t)(kb * NB + nb) * 2 + 0) * 64 + lane];
+        blo[nb] = wf[((size_t)(kb * NB + nb) * 2 + 1) * 64 + lane];
+      }
     }
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
@@ -228,6 +270,12 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_split_kernel(
         acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[rb], blo[nb], acc[rb][nb], 0, 0, 0);
         acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[rb], bhi[nb], acc[rb][nb], 0, 0, 0);
       }
+    if constexpr (BL) {
+      constexpr int NK = 27 * CB;   // one K block per (tap, 32 channels)
+      if (kb + 1 < NK) bstore((kb + 1) & 1);
+      __syncthreads();
+      if (kb + 2 < NK) bfetch(kb + 2);
+    }
   };
 
   if constexpr (PAIR) {
@@ -829,7 +877,10 @@ static bool split_uses_lds(int mode, int CI, int CO, bool per_lane, bool has_x2)
 // deep-level regions are small (conv_3_1 at cfg 2: 3.97 -> 3.87 ms per eval step with 2), train mode's are
 // large (4 measured best: 15.3 against 15.5 ms per train-mode step with 2).  S2 with 1 / 4 row blocks:
 // eval 4.01 / 4.11 ms, train 15.9 / 15.5 ms (tools/gpu_r5_bound_ab.sh r5rb).
-constexpr long kS1WideWgs = 4096;
+#ifndef MVS_S1_WIDE_WGS
+#define MVS_S1_WIDE_WGS 4096
+#endif
+constexpr long kS1WideWgs = MVS_S1_WIDE_WGS;
 // row blocks of the 3-in-1 S2 (kS2Multi): 4 measured slower (300 registers, one wave per SIMD: train-mode
 // step 12.9 -> 13.1 ms)
 #ifndef MVS_S2M_RB
