@@ -63,10 +63,10 @@ constexpr int kS2Multi = 112;
 #ifndef MVS_S2M_BLDS
 #define MVS_S2M_BLDS 1
 #endif
-// S1 64 -> 64 with the K block's weights in LDS: with 4 row blocks 274 registers, one wave per SIMD:
-// train-mode step 12.3 -> 13.4 ms (off by default)
+// S1 64 -> 64 with the K block's weights in LDS, 2 row blocks per wave (3 waves per SIMD): train-mode
+// step 12.3 -> 12.1 ms (with 4 row blocks 274 registers, one wave per SIMD: 13.4 ms)
 #ifndef MVS_S1_BLDS
-#define MVS_S1_BLDS 0
+#define MVS_S1_BLDS 1
 #endif
 
 // per-workgroup channel sums: the wave's per-lane partial sums s / q (channel nb * 16 + (lane & 15) of
@@ -873,14 +873,12 @@ static bool split_uses_lds(int mode, int CI, int CO, bool per_lane, bool has_x2)
 // row blocks per wave of the per-lane kernel: 4 for the stride-1 convs (each weight fragment feeds 4 row
 // blocks), 2 for the transposed and stride-2 ones (measured at cfg 2, eval and train mode: S1 64 -> 64
 // 2.70 -> 2.41 ms, T2 32 -> 16 2.02 against 2.36 with 4; 1 row block is slower everywhere)
-// The stride-1 kernel drops to 2 row blocks when 4 would leave fewer than kS1WideWgs workgroups: eval's
-// deep-level regions are small (conv_3_1 at cfg 2: 3.97 -> 3.87 ms per eval step with 2), train mode's are
-// large (4 measured best: 15.3 against 15.5 ms per train-mode step with 2).  S2 with 1 / 4 row blocks:
-// eval 4.01 / 4.11 ms, train 15.9 / 15.5 ms (tools/gpu_r5_bound_ab.sh r5rb).
-#ifndef MVS_S1_WIDE_WGS
-#define MVS_S1_WIDE_WGS 4096
-#endif
-constexpr long kS1WideWgs = MVS_S1_WIDE_WGS;
+// The stride-1 kernel without LDS weights drops to 2 row blocks when 4 would leave fewer than kS1WideWgs
+// workgroups: eval's deep-level regions are small (conv_3_1 at cfg 2: 3.97 -> 3.87 ms per eval step with
+// 2), train mode's are large (4 measured best there: 15.3 against 15.5 ms per train-mode step).  With its
+// weights in LDS (64 channels, MVS_S1_BLDS) it always takes 2.  S2 with 1 / 4 row blocks: eval 4.01 /
+// 4.11 ms, train 15.9 / 15.5 ms (tools/gpu_r5_bound_ab.sh r5rb).
+constexpr long kS1WideWgs = 4096;
 // row blocks of the 3-in-1 S2 (kS2Multi): 4 measured slower (300 registers, one wave per SIMD: train-mode
 // step 12.9 -> 13.1 ms)
 #ifndef MVS_S2M_RB
@@ -888,6 +886,7 @@ constexpr long kS1WideWgs = MVS_S1_WIDE_WGS;
 #endif
 static int split_rb(int mode, int B, const int* on, int CO) {
   if (mode == kS2 && CO == kS2Multi) return MVS_S2M_RB;
+  if (mode == kS1 && CO == 64 && MVS_S1_BLDS) return 2;
   if (mode != kS1) return 2;
   const long rows = (long)B * on[0] * on[1] * on[2];
   return rows >= kS1WideWgs * (kBlock / 64) * 16 * 4 ? 4 : 2;
