@@ -587,6 +587,8 @@ void launch_s1_lds(const float* x, const void* wf, int w_exp, float* y, const fl
 // column blocks; classes run one after another (taps of class (pz, py, px): 2 per dim of parity 0, 1
 // of parity 1 -- 27 over the eight).  Same products and K order as the per-lane kernel (taps, then
 // channel blocks): bit-equal outputs.
+// (the K block's weight fragments staged in LDS once per workgroup, as the 3-in-1 S2 does: train-mode
+// step 12.0 -> 12.4 ms -- a barrier per K block of a class with 1-8 taps; dropped)
 // MVS_T2_TYB: class rows along y per tile / 4 (2: a 32 x 16 x 4 tile, 4 row blocks per wave, one
 // workgroup per CU: train-mode step 14.1 -> 15.5 ms; the LDS kernel on eval's small regions: eval step
 // 3.95 -> 4.24 ms, hence kT2LdsMinVoxels)
