@@ -438,7 +438,20 @@ __global__ __launch_bounds__(kBlock) void conv3d_s1_split_lds_kernel(
   const int b = (int)blockIdx.y;
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m = lane & 15, kq = lane >> 4;
-  const int ex = act_split_exponent(bound_read(xb));
+  // the input's scale; with the folded BN + ReLU (g.in_bn: train mode's conv_k_0 outputs) a bound of
+  // relu(BN(v)) over |v| <= bound(x), one channel per lane
+  float bound = bound_read(xb);
+  if (g.in_bn) {
+    float r = 0.0f;
+    if (lane < CI) {
+      const float sc = g.in_bn[lane], sh = g.in_bn[CI + lane], mu = g.in_bn[2 * CI + lane];
+      r = fmaxf(fmaxf((bound - mu) * sc, (-bound - mu) * sc) + sh, 0.0f);
+    }
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) r = fmaxf(r, __shfl_xor(r, k));
+    bound = r;
+  }
+  const int ex = act_split_exponent(bound);
 
   // ---- stage the input block: items (voxel, channel quad), quad fastest (coalesced channels-last
   // loads); voxels outside the input region are zeros (the convolution's zero padding) ----
@@ -447,9 +460,19 @@ __global__ __launch_bounds__(kBlock) void conv3d_s1_split_lds_kernel(
     const size_t rvol = (size_t)g.in[0] * g.in[1] * g.in[2];
     const Rsrc rs = make_rsrc(x + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
     constexpr int BATCH = 8;
+    // folded BN: the thread's quad q = tid % NQ is the same for all its items (kBlock % NQ == 0)
+    static_assert(kBlock % NQ == 0, "one quad per thread");
+    f4v bsc, bsh, bmu;
+    if (g.in_bn) {
+      const int c = 4 * (tid % NQ);
+      bsc = *reinterpret_cast<const f4v*>(g.in_bn + c);
+      bsh = *reinterpret_cast<const f4v*>(g.in_bn + CI + c);
+      bmu = *reinterpret_cast<const f4v*>(g.in_bn + 2 * CI + c);
+    }
 #pragma unroll
     for (int k0 = 0; k0 < PER; k0 += BATCH) {
       f4v v4[BATCH];
+      bool okk[BATCH];
 #pragma unroll
       for (int k = 0; k < BATCH; ++k) {
         const int e = tid + kBlock * (k0 + k);
@@ -461,6 +484,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_s1_split_lds_kernel(
                         rz < g.in[0];
         const uint32_t off = ok ? (uint32_t)((((size_t)rz * g.in[1] + ry) * g.in[2] + rx) * CI + 4 * q) * 4u : kOob;
         v4[k] = ld4(rs, off, 0);
+        okk[k] = ok;
       }
 #pragma unroll
       for (int k = 0; k < BATCH; ++k) {
@@ -468,7 +492,12 @@ __global__ __launch_bounds__(kBlock) void conv3d_s1_split_lds_kernel(
         if (k0 + k >= PER || e >= NIT) continue;
         const int q = e % NQ, v = e / NQ;
         uint2 hi, lo;
-        split4(v4[k], ex, hi, lo);
+        f4v a = v4[k];
+        if (g.in_bn && okk[k]) {   // in-region voxels only: the zero padding stays zero
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) a[jj] = fmaxf((a[jj] - bmu[jj]) * bsc[jj] + bsh[jj], 0.0f);
+        }
+        split4(a, ex, hi, lo);
         *reinterpret_cast<uint2*>(lds + s1_chunk_off<CI>(v, q >> 1) + ((q & 1) << 3)) = hi;
         *reinterpret_cast<uint2*>(lds + s1_chunk_off<CI>(v, CI / 8 + (q >> 1)) + ((q & 1) << 3)) = lo;
       }
@@ -966,7 +995,9 @@ int launch_conv3d_region_split(int mode, bool out_cf, const float* x, const floa
   }
   // S1: conv_k_1 (16 / 32 / 64 channels; LDS-staged operands per MVS_S1_LDS); T2: deconv_3_0 (64 -> 32),
   // deconv_2_0 (32 -> 16); S2: conv_k_0 from the split cost volume (32 -> 16 / 32 / 64)
-  if (in_bn && !split_t2_lds(mode, B, CI, CO, on, per_lane, x2 != nullptr, true)) return MVS_ERR_INVALID_ARGUMENT;
+  if (in_bn && !split_t2_lds(mode, B, CI, CO, on, per_lane, x2 != nullptr, true) &&
+      !(split_uses_lds(mode, CI, CO, per_lane, x2 != nullptr) && CI <= 64))
+    return MVS_ERR_INVALID_ARGUMENT;   // the folded input BN: the LDS-staged kernels only
   if (split_t2_lds(mode, B, CI, CO, on, per_lane, x2 != nullptr, in_bn != nullptr)) {
     if (CI == 64)
       launch_t2_lds<64, 32, 1>(x, x2, wfrag, w_exp, y, bn_scale, bn_shift, bn_mean, B, g, x_bound, x2_bound, y_bound, s);

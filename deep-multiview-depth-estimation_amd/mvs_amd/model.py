@@ -527,7 +527,7 @@ class CostVolumeReg(nn.Module):
             # (ops.conv_s2_split_multi_sums), the volume's operands loaded once for all three
             zs = conv_s2_split_multi_sums(cv, [region_weight(c) for c in (self.conv_1_0, self.conv_2_0,
                                                                           self.conv_3_0)],
-                                          dims, org(R2), size(R2), pad, bound)
+                                          dims, org(R2), size(R2), pad, bound, y_bound=bwr(0))
         for k, (conv_a, bn) in enumerate(((self.conv_1_0, self.BN_1), (self.conv_2_0, self.BN_2),
                                           (self.conv_3_0, self.BN_3))):
             if zs is not None:
@@ -541,7 +541,13 @@ class CostVolumeReg(nn.Module):
                                   pad, in_c4=c4)
                 s1, s2 = channel_stats(z, True)
             p = _bn_train_hip(bn, s1, s2, count)
-            stage.append((bn_relu_(z, True, *p, y_bound=bwr(k)), p))   # p: relu(BN(0)) outside M
+            if zs is not None and bw is not None and k < 2:
+                # conv_1_1 / conv_2_1's LDS kernels apply relu(BN(.)) in their staging: z stays raw, its
+                # bound the three outputs' (row 0)
+                stage.append(((z, p), p))
+            else:
+                stage.append((bn_relu_(z, True, *p, y_bound=bwr(k if zs is None or bw is None else 2)), p))
+            # (p: relu(BN(0)) outside M)
         lv = []
         # conv_2_1 / conv_3_1's BN + ReLU (and deconv_3_0's, with the + y2 sum) applied in the transposed
         # convs' LDS staging instead of a pass over each tensor (ops.conv3d_region_split_sums x_bn / x2_bn)
@@ -551,10 +557,14 @@ class CostVolumeReg(nn.Module):
             # level 1 only feeds deconv_1_0's input sum: channels-first for its loads
             cf = bn is self.BN_1
             if bw is not None:   # sums over R1 in the epilogue, only M stored (the next layers read M)
-                z, s1, s2 = conv3d_region_split_sums(y, None, region_weight(conv_b), CONV_S1, dims, org(R1),
-                                                     size(R1), org(R2), size(R2), None, bw[k], out_ncdhw=cf,
+                if isinstance(y, tuple):   # (raw conv_k_0 output, its BN): folded into the staging
+                    xin, xbn, xbw = y[0], y[1], bw[0]
+                else:
+                    xin, xbn, xbw = y, None, bw[k if zs is None else 2]
+                z, s1, s2 = conv3d_region_split_sums(xin, None, region_weight(conv_b), CONV_S1, dims, org(R1),
+                                                     size(R1), org(R2), size(R2), None, xbw, out_ncdhw=cf,
                                                      store_origin=org(M), store_size=size(M),
-                                                     y_bound=bw[3 + k] if fold and not cf else None)
+                                                     y_bound=bw[3 + k] if fold and not cf else None, x_bn=xbn)
             else:
                 z = conv3d_region(y, None, region_weight(conv_b), CONV_S1, dims, org(R1), size(R1), org(R2),
                                   size(R2), None, out_ncdhw=cf)

@@ -1159,7 +1159,8 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
     ``stats``: float64 [split_stats_slots, 2, c_out] receiving per-workgroup sums over the whole
     output region (conv3d_region_split_sums).  ``in_bn`` (CONV_T2, 64 -> 32 / 32 -> 16): fp32 [6, c_in]
     = (scale, shift, mean) of x then x2 -- the input is relu(BN(x)) [+ relu(BN(x2))], the bound words
-    bound the raw tensors.  fp32-level error.  Inference only."""
+    bound the raw tensors; also CONV_S1 16 -> 16 / 32 -> 32 (its LDS kernel), x only.  fp32-level error
+    (DESIGN.md §3.8).  Inference only."""
     _require_gpu(x, "x")
     lib = _lib.load()
     flags = (_lib.MVS_CONV_OUT_NCDHW if out_ncdhw else 0) | (_lib.MVS_CONV_PER_LANE if per_lane else 0)
@@ -1209,12 +1210,13 @@ def conv3d_region_split(x: torch.Tensor, x2: Optional[torch.Tensor], weight: tor
     return y
 
 
-def conv_s2_split_multi_sums(cv, weights, dims, out_origin, out_size, pad, bound):
+def conv_s2_split_multi_sums(cv, weights, dims, out_origin, out_size, pad, bound, y_bound=None):
     """Train mode's conv_1_0, conv_2_0 and conv_3_0 (16 / 32 / 64 channels, model.py:78-80) over ONE
     region of the split cost volume in one launch (mvs_conv3d_region_split_fwd, c_out = 112: the
     volume's A fragments are loaded once for all three), without BN, with the per-channel float64 batch
     sums formed in the epilogue: returns [(y, s1, s2)] per conv, y channels-last on the region.
-    ``weights``: the three region weights [27, c_k, 32] (region_weight)."""
+    ``weights``: the three region weights [27, c_k, 32] (region_weight); ``y_bound``: None or zeroed
+    bound words raised to the max |y| over the three outputs."""
     _require_gpu(cv, "cv")
     lib = _lib.load()
     if cv.dtype != torch.int32 or cv.dim() != 6 or bound is None or bound.numel() != 8:
@@ -1232,8 +1234,9 @@ def conv_s2_split_multi_sums(cv, weights, dims, out_origin, out_size, pad, bound
     flags = _lib.MVS_CONV_IN_C4 | _lib.MVS_CONV_IN_SPLIT
     rc = lib.mvs_conv3d_region_split_fwd(CONV_S2, flags, _lib.ptr(cv), None, _lib.ptr(frag), int(ew), _lib.ptr(ys[0]),
                                          b, 32, 112, _ints3(dims), _ints3(out_origin), _ints3(out_size), None, None,
-                                         _ints3(pad), None, None, None, _lib.ptr(bound.contiguous()), None, None,
-                                         None, None, None, _lib.ptr(st), _lib.ptr(ys[1]), _lib.ptr(ys[2]), None,
+                                         _ints3(pad), None, None, None, _lib.ptr(bound.contiguous()), None,
+                                         _bound_ptr(y_bound), None, None, None, _lib.ptr(st), _lib.ptr(ys[1]),
+                                         _lib.ptr(ys[2]), None,
                                          _lib.stream_handle(dev))
     _lib.check(rc, "mvs_conv3d_region_split_fwd")
     s = st.sum(0)

@@ -521,7 +521,8 @@ int mvs_conv3d_region_split_weights(const float* weight, int c_in, int c_out, un
  * three; no addend, no MVS_CONV_OUT_NCDHW); NULL otherwise.  in_bn: NULL, or (MVS_CONV_T2 with (c_in,
  * c_out) = (64, 32) or (32, 16): the LDS-staged kernel) DEVICE fp32 [6][c_in], 16-byte aligned = (scale, shift, mean)
  * of x then of x2: the input is relu((x - mean) scale + shift) [+ the same of x2] -- train mode's BN +
- * ReLU passes folded into the staging; x_bound / x2_bound then bound the raw x / x2. */
+ * ReLU passes folded into the staging; x_bound / x2_bound then bound the raw x / x2.  Also MVS_CONV_S1 with
+ * c_in = c_out = 16 or 32 (its LDS-staged kernel), x only. */
 int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float* x2, const void* weight_frag,
                                 int weight_exp, float* y, int batch, int c_in, int c_out, const int* dims,
                                 const int* out_origin, const int* out_size, const int* in_origin, const int* in_size,

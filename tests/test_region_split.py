@@ -462,3 +462,41 @@ def test_region_split_t2_folded_input_bn(cin, cout, two, monkeypatch):
     assert (got - ref).abs().max().item() <= 2e-6 * scale
     torch.testing.assert_close(s1, r1, rtol=1e-5, atol=1e-5 * scale)
     torch.testing.assert_close(s2, r2, rtol=1e-5, atol=1e-5 * scale * scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", [16, 32])
+def test_region_split_s1_folded_input_bn(c):
+    """Train mode's conv_k_0 BN + ReLU folded into conv_k_1's LDS staging (x_bn on CONV_S1 16 / 32
+    channels): equal to the same kernel on the explicitly normalised input within fp32-level error, the
+    zero padding outside the volume left zero (not relu(BN(0))), and the same batch sums."""
+    from mvs_amd import ops
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _grow, _tconv_input_region
+    n = (24, 20, 26)
+    pad, _ = pad_outpad(*n)
+    M = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
+    R1, R2 = _grow(M, n, 1), _grow(M, n, 2)
+    org = lambda r: [lo for lo, _ in r]
+    size = lambda r: [hi - lo + 1 for lo, hi in r]
+    g = torch.Generator().manual_seed(c + 5)
+    conv = torch.nn.Conv3d(c, c, 3)
+    conv.weight.data = torch.randn(c, c, 3, 3, 3, generator=g) * 0.1
+    w27 = ops.region_weight(conv).to(DEV)
+    raw = torch.randn(2, *size(R2), c, generator=g).to(DEV)
+    p = tuple(t.to(DEV) for t in _bn_params(c, g))
+    norm = torch.relu((raw - p[2]) * p[0] + p[1]).contiguous()
+    bw = ops.bound_words(2, DEV)
+    bw[0, 0] = raw.abs().max().view(torch.int32)
+    bw[1, 0] = norm.abs().max().view(torch.int32)
+    geo = (ops.CONV_S1, list(n), org(R1), size(R1), org(R2), size(R2), None)
+    with torch.no_grad():
+        ref, r1, r2 = ops.conv3d_region_split_sums(norm, None, w27, *geo, bw[1], store_origin=org(M),
+                                                   store_size=size(M))
+        got, s1, s2 = ops.conv3d_region_split_sums(raw, None, w27, *geo, bw[0], store_origin=org(M),
+                                                   store_size=size(M), x_bn=p)
+        torch.cuda.synchronize()
+    scale = ref.abs().max().item()
+    assert (got - ref).abs().max().item() <= 2e-6 * scale
+    torch.testing.assert_close(s1, r1, rtol=1e-5, atol=1e-5 * scale)
+    torch.testing.assert_close(s2, r2, rtol=1e-5, atol=1e-5 * scale * scale)
