@@ -570,7 +570,9 @@ int mvs_conv2d_split_fwd(const float* x, const void* weight_frag, int weight_exp
 
 int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, int batch, int c_in,
                       int c_out, int d, int h, int w, const float* bn_scale, const float* bn_shift,
-                      const float* bn_mean, void* stream) {
+                      const float* bn_mean, const float* x2, const float* in_bn, void* stream) {
+  if (in_bn && (c_out != 1 || flags || !x2 || bn_scale)) return MVS_ERR_INVALID_ARGUMENT;
+  if (!in_bn && x2) return MVS_ERR_INVALID_ARGUMENT;
   if (!x || !weight || !y || batch <= 0 || c_in <= 0 || d <= 0 || h <= 0 || w <= 0)
     return MVS_ERR_INVALID_ARGUMENT;
   if (c_out != 1 && c_out != 8) return MVS_ERR_INVALID_ARGUMENT;
@@ -588,7 +590,7 @@ int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, 
   mvs::launch_conv3d_k3_narrow(x, quads, (flags & MVS_CONV_WINO_Z) != 0, weight, y, batch,
                                c_in, c_out, d, h, w,
                                bn_scale, bn_shift, bn_mean,
-                               (hipStream_t)stream);
+                               (hipStream_t)stream, x2, in_bn);
   return lc.status();
 }
 

@@ -33,11 +33,17 @@ constexpr int kTX = 32, kTY = 8, kDT = 4;
 // (g0 - g1 + g2) / 2, g2; formed in float64 on the host, ops.py), accumulated per position; the
 // outputs are A^T m (m0 + m1 + m2, m1 - m2 - m3) at the end.  Per input channel 288 packed FMAs +
 // 36 packed adds instead of 432 packed FMAs.  Weights wu[c][ky][kx][4][co].
-template <int COUT, int C4, bool WZ = false, int DT = kDT>
+// FOLD (COUT = 1, NCDHW: train mode's conv_out, CostVolumeReg.forward_live_train): the staged input is
+// relu(BN_a(in)) + relu(BN_b(in2)) per channel, ibn = [6][Cin] (scale, shift, mean of in, then of in2)
+// -- model.py:121-123's `relu(BN_0(deconv_1_0)) + y0` formed on load instead of by a pass over the
+// full volume; the zero padding stays zero
+template <int COUT, int C4, bool WZ = false, int DT = kDT, bool FOLD = false>
 __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
     const float* __restrict__ in, const float* __restrict__ wt, float* __restrict__ out, int Cin,
     int D, int H, int W, int tiles_x, int tiles_y, int dgroups, int n_batch, const float* __restrict__ bn_scale,
-    const float* __restrict__ bn_shift, const float* __restrict__ bn_mean) {
+    const float* __restrict__ bn_shift, const float* __restrict__ bn_mean, const float* __restrict__ in2,
+    const float* __restrict__ ibn) {
+  static_assert(!FOLD || (COUT == 1 && C4 == 0), "folded input BN: conv_out on NCDHW");
   static_assert(!WZ || DT == 4, "depth Winograd: two windows of 2");
   constexpr int kPX = kTX + 2, kPY = kTY + 2, kPD = DT + 2;
   constexpr int kPlane = kPX * kPY;
@@ -76,6 +82,8 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   }
   // one pass = one input channel (NCDHW) or one channel quad (C4: 16-byte loads, 4 LDS planes)
   float pre[kPer][NQ];
+  float pre2[FOLD ? kPer : 1];
+  const float* ib2 = FOLD ? in2 + (size_t)b * Cin * vol : nullptr;
   auto fetch = [&](int q) {
     if constexpr (C4 == 2) {   // bf16 quad: the high halves of 4 fp32 words
       const uint2* src = ib16 + (size_t)q * vol;
@@ -101,6 +109,11 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
       const float* src = ib + (size_t)q * vol;
 #pragma unroll
       for (int j = 0; j < kPer; ++j) pre[j][0] = gok[j] ? src[goff[j]] : 0.0f;
+      if constexpr (FOLD) {
+        const float* src2 = ib2 + (size_t)q * vol;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) pre2[j] = gok[j] ? src2[goff[j]] : 0.0f;
+      }
     }
   };
   fetch(0);
@@ -128,6 +141,13 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   const int passes = C4 ? Cin / 4 : Cin;
   for (int q = 0; q < passes; ++q) {
     __syncthreads();   // the previous pass's reads are done
+    if constexpr (FOLD) {   // channel q's two BatchNorms (workgroup-uniform)
+      const float sa = ibn[q], ha = ibn[Cin + q], ma = ibn[2 * Cin + q];
+      const float sb = ibn[3 * Cin + q], hb = ibn[4 * Cin + q], mb = ibn[5 * Cin + q];
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if (gok[j]) pre[j][0] = fmaxf((pre[j][0] - ma) * sa + ha, 0.0f) + fmaxf((pre2[j] - mb) * sb + hb, 0.0f);
+    }
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int e = (int)threadIdx.x + j * kBlock;
@@ -244,21 +264,26 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
 #endif
 constexpr int kOutDT = MVS_CONV_OUT_DT;
 
-template <int COUT, int C4, bool WZ = false>
+template <int COUT, int C4, bool WZ = false, bool FOLD = false>
 void launch_narrow(const float* in, const float* weight, float* out, int B, int Cin, int D, int H, int W,
-                   const float* bn_scale, const float* bn_shift, const float* bn_mean, hipStream_t s) {
+                   const float* bn_scale, const float* bn_shift, const float* bn_mean, hipStream_t s,
+                   const float* in2 = nullptr, const float* ibn = nullptr) {
   constexpr int DT = COUT == 1 ? kOutDT : kDT;
   const int tiles_x = (W + kTX - 1) / kTX, tiles_y = (H + kTY - 1) / kTY, dgroups = (D + DT - 1) / DT;
   const dim3 grid = xcd_grid(B * dgroups * tiles_y * tiles_x);
-  hipLaunchKernelGGL((conv3d_k3_narrow_kernel<COUT, C4, WZ, DT>), grid, dim3(kBlock), 0, s, in, weight, out, Cin, D,
-                     H, W, tiles_x, tiles_y, dgroups, B, bn_scale, bn_shift, bn_mean);
+  hipLaunchKernelGGL((conv3d_k3_narrow_kernel<COUT, C4, WZ, DT, FOLD>), grid, dim3(kBlock), 0, s, in, weight, out,
+                     Cin, D, H, W, tiles_x, tiles_y, dgroups, B, bn_scale, bn_shift, bn_mean, in2, ibn);
 }
 
 }  // namespace
 
 void launch_conv3d_k3_narrow(const float* in, int in_c4, bool wino_z, const float* weight, float* out, int B,
                              int Cin, int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
-                             const float* bn_mean, hipStream_t s) {
+                             const float* bn_mean, hipStream_t s, const float* in2, const float* ibn) {
+  if (ibn) {   // conv_out with the folded BN + ReLU and the second input (capi checks the shape)
+    launch_narrow<1, 0, false, true>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s, in2, ibn);
+    return;
+  }
 #define MVS_NARROW(CO, Q, WZ) launch_narrow<CO, Q, WZ>(in, weight, out, B, Cin, D, H, W, bn_scale, bn_shift, bn_mean, s)
   if (wino_z) {
     if (in_c4 == 2) MVS_NARROW(8, 2, true);

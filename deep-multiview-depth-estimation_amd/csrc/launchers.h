@@ -87,7 +87,8 @@ void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, u
 // wino_z (Cout = 8): Winograd F(2,3) along depth, weight = the transformed wu[Cin][3][3][4][8]
 void launch_conv3d_k3_narrow(const float* in, int in_c4, bool wino_z, const float* weight, float* out, int B,
                              int Cin, int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
-                             const float* bn_mean, hipStream_t s);
+                             const float* bn_mean, hipStream_t s, const float* in2 = nullptr,
+                             const float* ibn = nullptr);
 
 // conv3d_split.hip: conv_0_0 (32 -> 8, 3x3x3, padding 1) on the f16 MFMA with split-fp16 operands;
 // x channel-quad fp32 [B][8][D][H][W][4], wfrag [27][64][8] fp16 fragments (mvs_conv3d_split_weights),

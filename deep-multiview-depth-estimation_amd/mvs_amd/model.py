@@ -629,6 +629,10 @@ class CostVolumeReg(nn.Module):
         for t in (y0,) + tuple(p0):
             t.record_stream(main)
         p = _bn_train_hip(self.BN_0, *channel_stats(z, False), count)
+        if os.environ.get("MVS_OUT_FOLD", "1") != "0":
+            # relu(BN_0(deconv_1_0)) + relu(BN_0'(conv_0_0)) formed in conv_out's staging (one pass over the
+            # full volume fewer)
+            return softmax_depth(conv3d_k3(z, self.conv_out.weight, x2=y0, in_bn=torch.cat((p, p0))))
         z = bn_relu_(z, False, *p, r=y0, r_bn=p0)   # relu(BN_0(deconv_1_0)) + relu(BN_0'(conv_0_0))
         return softmax_depth(conv3d_k3(z, self.conv_out.weight))
 

@@ -657,14 +657,16 @@ torch.library.register_autograd("mvs::extract_depth_map", _sam_backward, setup_c
 @torch.library.custom_op("mvs::conv3d_k3", mutates_args=())
 def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Tensor] = None,
               bn_shift: Optional[torch.Tensor] = None, bn_mean: Optional[torch.Tensor] = None,
-              in_c4: bool = False, wino_z: bool = False) -> torch.Tensor:
+              in_c4: bool = False, wino_z: bool = False, x2: Optional[torch.Tensor] = None,
+              in_bn: Optional[torch.Tensor] = None) -> torch.Tensor:
     """nn.Conv3d(c_in, c_out, 3, stride=1, padding=1, bias=False) forward, c_out in {1, 8}, fp32
     NCDHW, on the HIP kernel (csrc/conv3d_narrow.hip); with bn_* given, max((y - mean) * scale +
     shift, 0) is fused (eval BN + ReLU).  ``in_c4``: x is the channel-quad [B, Cin/4, D, H, W, 4]
     of cost_volume_c4 (fp32) or cost_volume_c4_bf16 (bf16: widened on load, fp32 arithmetic).
     ``wino_z`` (c_out = 8): Winograd F(2,3) along depth (MVS_CONV_WINO_Z; the
-    transformed weights are formed in float64 here).  Inference only (no autograd formula):
-    CostVolumeReg uses it on the eval-mode, no-grad path."""
+    transformed weights are formed in float64 here).  ``x2`` + ``in_bn`` (c_out 1, NCDHW): the input is
+    relu(BN_a(x)) + relu(BN_b(x2)) per channel, in_bn fp32 [6, c_in] (train mode's conv_out input,
+    formed on load).  Inference only (no autograd formula): CostVolumeReg uses it on the no-grad path."""
     _require_gpu(x, "x")
     lib = _lib.load()
     if in_c4:
@@ -696,8 +698,16 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Te
     y = torch.empty((b, cout, d, h, wd), device=x.device, dtype=_F32)
     flags = ((_lib.MVS_CONV_IN_C4 if in_c4 else 0) | (_lib.MVS_CONV_WINO_Z if wino_z else 0)
              | (_lib.MVS_CONV_IN_BF16 if quad_bf16 else 0))
+    if (x2 is None) != (in_bn is None):
+        raise ValueError("x2 and in_bn go together")
+    if x2 is not None:
+        if x2.shape != x.shape or in_bn.shape != (6, cin):
+            raise ValueError("x2 of x's shape and in_bn [6, c_in] expected")
+        x2 = x2.to(_F32).contiguous()
+        in_bn = in_bn.to(device=x.device, dtype=_F32).contiguous()
     st = lib.mvs_conv3d_k3_fwd(_lib.ptr(x), flags, _lib.ptr(w), _lib.ptr(y),
-                               b, cin, cout, d, h, wd, *bp, _lib.stream_handle(x.device))
+                               b, cin, cout, d, h, wd, *bp, None if x2 is None else _lib.ptr(x2),
+                               None if in_bn is None else _lib.ptr(in_bn), _lib.stream_handle(x.device))
     _lib.check(st, "mvs_conv3d_k3_fwd")
     return y
 
@@ -823,7 +833,7 @@ def _wino_z_weight(wt):
 
 
 @conv3d_k3.register_fake
-def _(x, weight, bn_scale=None, bn_shift=None, bn_mean=None, in_c4=False, wino_z=False):
+def _(x, weight, bn_scale=None, bn_shift=None, bn_mean=None, in_c4=False, wino_z=False, x2=None, in_bn=None):
     return x.new_empty((x.shape[0], weight.shape[0]) + tuple(x.shape[2:5]))
 
 

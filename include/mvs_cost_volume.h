@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 20
+#define MVS_ABI_VERSION 21
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -274,10 +274,14 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
  * (all three BN pointers, c_out floats each, or none): y = max((y - bn_mean) * bn_scale + bn_shift,
  * 0), the eval BN + ReLU that follows conv_0_0 (model.py:101; bn_scale = gamma / sqrt(var + eps),
  * bn_shift = beta).  Replaces the MIOpen convolution behind torch.nn.Conv3d.forward for these two
- * layers in eval-mode inference; same products per output, fp32 summation order differs. */
+ * layers in eval-mode inference; same products per output, fp32 summation order differs.
+ * x2, in_bn (both or neither; c_out 1, flags 0, no BN epilogue): train mode's conv_out input
+ * relu((x - m_a) s_a + h_a) + relu((x2 - m_b) s_b + h_b) per channel formed on load (model.py:121-123,
+ * `relu(BN_0(deconv_1_0)) + y0` with y0 the raw conv_0_0 output), in_bn DEVICE fp32 [6][c_in] = (s_a,
+ * h_a, m_a, s_b, h_b, m_b); the zero padding stays zero. */
 int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, int batch, int c_in,
                       int c_out, int d, int h, int w, const float* bn_scale, const float* bn_shift,
-                      const float* bn_mean, void* stream);
+                      const float* bn_mean, const float* x2, const float* in_bn, void* stream);
 
 /* conv_0_0 (model.py:77, 101: nn.Conv3d(32, 8, 3, padding=1, bias=False) + optional eval BN_0 + ReLU)
  * on the f16 matrix cores with split operands (csrc/conv3d_split.hip): every fp32 operand is scaled by

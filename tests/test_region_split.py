@@ -500,3 +500,22 @@ def test_region_split_s1_folded_input_bn(c):
     assert (got - ref).abs().max().item() <= 2e-6 * scale
     torch.testing.assert_close(s1, r1, rtol=1e-5, atol=1e-5 * scale)
     torch.testing.assert_close(s2, r2, rtol=1e-5, atol=1e-5 * scale * scale)
+
+
+@pytest.mark.gpu
+def test_conv_out_folded_input_bn():
+    """Train mode's conv_out input relu(BN_0(deconv_1_0)) + relu(BN_0'(conv_0_0)) formed in conv_out's
+    staging (conv3d_k3 x2 / in_bn) against the bn_relu_ pass followed by conv3d_k3 (model.py:121-123):
+    equal within fp32 rounding, including the volume border (the zero padding stays zero)."""
+    from mvs_amd import ops
+    g = torch.Generator().manual_seed(21)
+    shape = (2, 8, 13, 18, 37)
+    z = torch.randn(shape, generator=g).to(DEV)
+    y0 = torch.randn(shape, generator=g).to(DEV)
+    pa = [t.to(DEV) for t in _bn_params(8, g)]
+    pb = [t.to(DEV) for t in _bn_params(8, g)]
+    w = (torch.randn(1, 8, 3, 3, 3, generator=g) * 0.2).to(DEV)
+    with torch.no_grad():
+        ref = ops.conv3d_k3(ops.bn_relu_(z.clone(), False, *pa, r=y0, r_bn=pb), w)
+        got = ops.conv3d_k3(z, w, x2=y0, in_bn=torch.stack(pa + pb))
+    torch.testing.assert_close(got, ref, rtol=1e-6, atol=1e-6 * ref.abs().max().item())
