@@ -335,9 +335,9 @@ class CostVolumeReg(nn.Module):
         bn_eval = _bn_eval
 
         # conv_0_0 (VALU-bound) runs on a side stream, concurrently with the region chain (MFMA /
-        # memory-latency-bound) that does not need it until deconv_1_0.  (Levels 2-3 on a third
-        # stream beside level 1 measured no gain: 6.21-6.25 against 6.18-6.22 ms per cfg-2 step,
-        # tools/hip_reg_layers.py, profiles/r03e_reg_layers.log)
+        # memory-latency-bound) that does not need it until deconv_1_0.  (Round 3's fp32 kernels measured
+        # no gain from levels 2-3 beside level 1: 6.21-6.25 against 6.18-6.22 ms per cfg-2 step,
+        # profiles/r03e_reg_layers.log; the split-fp16 path below does gain: l1_side)
         main = torch.cuda.current_stream(cv.device)
         # the split cost volume (int32, csrc/split.h) always goes to the split-fp16 kernels; an fp32
         # channel-quad volume does when split_f16 is on and it carries bound words
@@ -401,9 +401,21 @@ class CostVolumeReg(nn.Module):
                                            out_ncdhw=False), True
             return conv3d_region(ya, None, region_weight(conv_b), CONV_S1, dims, org(reg), size(reg),
                                  org(halo), size(halo), None, *bn_eval(bn), out_ncdhw=reg is B), reg is not B
-        y1, y1_cl = level(0, self.conv_1_0, self.conv_1_1, self.BN_1, B)
+        l1_side = bw is not None and head is not None and os.environ.get("MVS_L1_SIDE", "1") != "0"
+        if l1_side:
+            # level 1's conv_1_1 (LDS-bound) on a side stream beside levels 2-3 (L2-bound per-lane convs):
+            # cfg-2 eval step 3.89-4.00 -> 3.80-3.93 ms (same box, tools/gpu_r5_env_ab.sh r5l1)
+            s1 = _side_stream(cv.device, 1)
+            s1.wait_stream(main)
+            with torch.cuda.stream(s1):
+                y1, y1_cl = level(0, self.conv_1_0, self.conv_1_1, self.BN_1, B)
+        else:
+            y1, y1_cl = level(0, self.conv_1_0, self.conv_1_1, self.BN_1, B)
         y2 = level(1, self.conv_2_0, self.conv_2_1, self.BN_2, C2)[0]
         y3 = level(2, self.conv_3_0, self.conv_3_1, self.BN_3, C3)[0]
+        if l1_side:
+            main.wait_stream(s1)
+            y1.record_stream(main)
         if bw is not None:
             # deconv_3_0 + BN_2 + ReLU, then `+ y2` (model.py:119) in its epilogue: deconv_2_0 reads one tensor
             y32 = conv3d_region_split(y3, None, region_weight(self.deconv_3_0), CONV_T2, dims, org(C2), size(C2),
