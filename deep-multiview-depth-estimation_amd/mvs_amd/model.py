@@ -411,8 +411,18 @@ class CostVolumeReg(nn.Module):
                 y1, y1_cl = level(0, self.conv_1_0, self.conv_1_1, self.BN_1, B)
         else:
             y1, y1_cl = level(0, self.conv_1_0, self.conv_1_1, self.BN_1, B)
-        y2 = level(1, self.conv_2_0, self.conv_2_1, self.BN_2, C2)[0]
-        y3 = level(2, self.conv_3_0, self.conv_3_1, self.BN_3, C3)[0]
+        l3_side = l1_side and os.environ.get("MVS_L3_SIDE", "1") != "0"
+        if l3_side:   # level 3 on a second side stream beside level 2 (3.91-3.93 -> 3.84-3.88 ms, r5l3)
+            s3 = _side_stream(cv.device, 2)
+            s3.wait_stream(main)
+            with torch.cuda.stream(s3):
+                y3 = level(2, self.conv_3_0, self.conv_3_1, self.BN_3, C3)[0]
+            y2 = level(1, self.conv_2_0, self.conv_2_1, self.BN_2, C2)[0]
+            main.wait_stream(s3)
+            y3.record_stream(main)
+        else:
+            y2 = level(1, self.conv_2_0, self.conv_2_1, self.BN_2, C2)[0]
+            y3 = level(2, self.conv_3_0, self.conv_3_1, self.BN_3, C3)[0]
         if l1_side:
             main.wait_stream(s1)
             y1.record_stream(main)
