@@ -7,7 +7,8 @@ reference architecture (tests/golden/weights.py formula), fp32, BN eval mode, in
 
 A step = one full MVSNet.forward over one batch (HIP feature encoder -> fused warp+variance HIP
 kernel -> 3-D regulariser on its live regions (HIP MFMA region convs) -> HIP softmax
-and soft-argmin -> HIP refinement).  value = depth maps/s over all ranks.
+and soft-argmin -> HIP refinement), in exact fp32 arithmetic in every layer (MVSConfig(arithmetic=
+"fp32"), the default).  value = depth maps/s over all ranks.
 
 Multi-GPU (torchrun, one process per GPU): --mode samples (default) shards SAMPLES across ranks --
 every rank runs its own batch, no collective in the data path, "scaling": "weak".  --mode dshard
@@ -16,19 +17,20 @@ D-slab, and each sample's slab goes point to point (RCCL send/recv over xGMI,
 mvs_amd/depth_shards.py) to the rank that owns the sample, which runs the regulariser.
 
 Also reported (one JSON line, rank 0):
-  roofline      the step's dominant kernel, the split head (cv_head_kernel<2, PRESPLIT>: conv_0_0 +
-                conv_1_0 in one pass over the split cost volume): the f16 matrix-core
-                flops of its split-fp16 convolutions per launch / its average launch time (HIP events on
-                the launch stream inside the timed steps) vs the dense f16 peak; beside it the fp32
-                convolution flops those compute vs the dense fp32 matrix peak and its algorithmic HBM
-                bytes (the split volume in, y0 / y1 out); traffic = PMC HBM bytes per launch from
-                profiles/split_head_traffic_<cfg>.json (rocprofv3 --pmc, FETCH_SIZE x2 + WRITE_SIZE)
-  warp_kernel   the standalone fused warp + variance kernel (cost_volume_staged_kernel, channel-quad
-                split store): algorithmic bytes (features read once + cost volume written once) /
-                launch time vs 8 TB/s -- the metric's "warp-kernel HBM GB/s"; traffic = PMC bytes
-  cpu_baseline  the oracle (oracle/mvs_oracle.py: the reference's op sequence in torch CPU,
-                per-plane warp loop with torch.cat growth) on ONE sample of the same workload
-  hot_path      cost volumes/s of the fused kernel alone
+  roofline        the fp32 step's dominant kernel, conv_0_0 (conv3d_k3_narrow_kernel<8>, fp32 VALU with a
+                  depth-Winograd transform): its useful convolution flops per launch / its average launch
+                  time (HIP events on its stream inside the timed steps) vs the fp32 peak (157.3 TF, the
+                  f32 VALU and f32-input MFMA rate); traffic = PMC HBM bytes per launch
+                  (profiles/conv0_traffic_<cfg>.json, rocprofv3 --pmc, FETCH_SIZE x2 + WRITE_SIZE)
+  warp_kernel     the fused warp + variance kernel (cost_volume_staged_kernel, fp32 channel-quad store)
+                  inside the timed steps: algorithmic bytes (features read once + cost volume written
+                  once) / launch time vs 8 TB/s -- the metric's "warp-kernel HBM GB/s"; traffic = PMC bytes
+  split_f16_step  the opt-in split-fp16 arithmetic (MVSConfig(arithmetic="split_f16"): f16 matrix cores
+                  with split operands, narrower than fp32) timed the same way, with its split head's
+                  roofline -- never the headline
+  cpu_baseline    the oracle (oracle/mvs_oracle.py: the reference's op sequence in torch CPU,
+                  per-plane warp loop with torch.cat growth) on ONE sample of the same workload
+  hot_path        cost volumes/s of the fused kernel alone
 """
 import argparse
 import ctypes
@@ -126,6 +128,39 @@ def max_over_ranks(x, world, device):
     return t.item()
 
 
+def timed_steps(step, steps, world, device, hooked=False):
+    """``steps`` steps bracketed by a barrier + device synchronisation on both sides: (seconds, {kernel kind:
+    average ms}) -- with ``hooked``, HIP events around the step's own kernels (ops.KERNEL_EVENT_HOOK: the
+    warp kernel "cost_volume", the fp32 "conv_0_0", the split head "split_head"), recorded on the stream
+    each is launched on."""
+    from mvs_amd import ops as mvs_ops
+    events = []
+    stream = torch.cuda.current_stream(device)
+
+    def hook(kind):
+        pair = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        for e in pair:   # materialise the HIP event (torch creates it on first record)
+            e.record(stream)
+        events.append((kind, pair))
+        return pair
+    with torch.no_grad():
+        barrier(world)
+        mvs_ops.KERNEL_EVENT_HOOK = hook if hooked else None
+        try:
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            barrier(world)
+            dt = time.perf_counter() - t0
+        finally:
+            mvs_ops.KERNEL_EVENT_HOOK = None
+    kms = {}
+    for kind in sorted(set(k for k, _ in events)):
+        ev = [p for k, p in events if k == kind]
+        kms[kind] = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    return dt, kms
+
+
 DSHARD_PHASES = ("encoder", "shard_kernel", "exchange", "owner_compute", "gather")
 
 
@@ -187,22 +222,22 @@ def make_inputs(B, V, H, W, seed, device):
     return img, K.to(device), R.to(device), T.to(device), d_min.to(device), d_int.to(device)
 
 
-def build_model(D, H, W, device, cv_dtype="float32"):
+def build_model(D, H, W, device, cv_dtype="float32", arithmetic="fp32"):
     from mvs_amd.config import MVSConfig
     from mvs_amd.model import MVSNet
-    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W, cv_dtype=cv_dtype))
+    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W, cv_dtype=cv_dtype, arithmetic=arithmetic))
     net.load_state_dict(deterministic_state_dict(net.state_dict()))
     return net.to(device).eval()
 
 
-def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=False, quads=False):
+def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=False, quads=False, store="ncdhw"):
     """Fused-kernel timing with HIP events on the launch stream, through the C ABI.
 
     Returns (main_ms, op_ms, alg_bytes): main_ms = average duration of the main fused kernel
     (events recorded by mvs_cost_volume_fwd_timed right around its launch), op_ms = average
     duration of the whole op (sampling matrices + packing + reference resampling + main kernel).
-    quads=True times the split channel-quad variant (mvs_cost_volume_fwd_c4_split, what
-    MVSNet.forward's inference step runs; same bytes).  bf16=True times the opt-in bf16 cost volume
+    store="c4" times the fp32 channel-quad variant (mvs_cost_volume_fwd_c4, what MVSNet.forward's fp32
+    inference step runs), "c4_split" the split channel-quad store of the split-fp16 opt-in (same bytes).  bf16=True times the opt-in bf16 cost volume
     (mvs_cost_volume_fwd_bf16): op-level only (main_ms None), algorithmic bytes with a 2-byte
     cost volume."""
     from mvs_amd import _lib, ops
@@ -240,9 +275,12 @@ def time_kernel(B, V, C, h, w, D, device, iters, d_begin=0, d_count=None, bf16=F
                None if e1 is None else ctypes.c_void_p(e1.cuda_event))
         args = (_lib.ptr(feat), _lib.ptr(K), _lib.ptr(R), _lib.ptr(T), _lib.ptr(d_min), _lib.ptr(d_int),
                 B, V, C, h, w, d_begin, d_count, 25.0, _lib.ptr(ws), _lib.ptr(cv), sp) + evs
-        if quads:   # the split cost volume the eval step writes (16-byte elements, bound words)
+        if store == "c4_split":   # the split cost volume of the split-fp16 opt-in (16-byte elements, bound words)
             st = lib.mvs_cost_volume_fwd_c4_split(*args, _lib.ptr(absmax))
             _lib.check(st, "mvs_cost_volume_fwd_c4_split")
+        elif store == "c4":   # the fp32 channel-quad volume the fp32 eval step writes
+            st = lib.mvs_cost_volume_fwd_c4(*args)
+            _lib.check(st, "mvs_cost_volume_fwd_c4")
         else:
             st = lib.mvs_cost_volume_fwd_timed(*args)
             _lib.check(st, "mvs_cost_volume_fwd_timed")
@@ -312,7 +350,7 @@ def kernel_configs(device, iters):
     out = {}
     for name, (B, V, h, w, D, dc) in KERNEL_CFGS.items():
         quads = dc == D
-        k_ms, op_ms, alg = time_kernel(B, V, 32, h, w, D, device, iters, D - dc, dc, quads=quads)
+        k_ms, op_ms, alg = time_kernel(B, V, 32, h, w, D, device, iters, D - dc, dc, store="c4" if quads else "ncdhw")
         gbs = alg / (k_ms * 1e-3) / 1e9
         out[name] = {"B": B, "V": V, "feature_hw": [h, w], "planes": dc, "kernel_ms": k_ms, "op_ms": op_ms,
                      "alg_bytes": alg, "GBps": gbs, "frac": gbs / HBM_PEAK_GBS,
@@ -469,6 +507,20 @@ def head_work(B, V, D, h, w, kind="split_head"):
             "regions": {"conv_1_0_windows": list(h1), "scv_box": [lo, hi]}}
 
 
+def conv0_flops(B, D, h, w):
+    """Useful fp32 flops of conv_0_0 (model.py:101: Conv3d(32, 8, 3, padding 1) over the whole volume)."""
+    return float(B) * D * h * w * 8 * 32 * 27 * 2
+
+
+def conv0_traffic(tag):
+    """PMC HBM bytes per fp32 conv_0_0 launch (profiles/conv0_traffic_<tag>.json, rocprofv3 --pmc), or None."""
+    path = os.path.join(REPO, "profiles", "conv0_traffic_%s.json" % tag)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
+
+
 def head_traffic(tag, kind="split_head"):
     """PMC HBM bytes per head launch (profiles/, rocprofv3 --pmc), or None."""
     path = os.path.join(REPO, "profiles", "%s_traffic_%s.json" % ("head" if kind == "cv_head" else kind, tag))
@@ -598,32 +650,13 @@ def main():
             sharded, step = dshard_step(net, world, rank, inputs, B, V)
         # the main fused kernel's launches inside the timed steps, bracketed by HIP events on its
         # launch stream (ops.KERNEL_EVENT_HOOK -> mvs_cost_volume_fwd_c4's event arguments)
-        from mvs_amd import ops as mvs_ops
-        step_events = []
-        stream = torch.cuda.current_stream(device)
-
-        def hook(kind):
-            pair = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            for e in pair:   # materialise the HIP event (torch creates it on first record)
-                e.record(stream)
-            step_events.append((kind, pair))
-            return pair
         with torch.no_grad():
             for i in range(args.warmup):
                 step()
                 torch.cuda.synchronize()
                 log("warmup step %d/%d done" % (i + 1, args.warmup))
-            barrier(world)
-            mvs_ops.KERNEL_EVENT_HOOK = hook if args.mode == "samples" else None
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                step()
-            barrier(world)
-            dt = time.perf_counter() - t0
-            mvs_ops.KERNEL_EVENT_HOOK = None
-        for kind in sorted(set(k for k, _ in step_events)):
-            ev = [p for k, p in step_events if k == kind]
-            result.setdefault("step_kernel_ms", {})[kind] = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+        dt, result["step_kernel_ms"] = timed_steps(step, args.steps, world, device,
+                                                   hooked=args.mode == "samples")
         log("timed %d steps: %.2f ms/step" % (args.steps, 1000.0 * dt / args.steps))
         if args.mode == "dshard":
             # the same step phase by phase, per rank (not part of the timed region above)
@@ -631,26 +664,23 @@ def main():
             log("dshard phases (ms, this rank): %s" % dict(zip(DSHARD_PHASES, result["dshard_phases"][rank])))
         dt = max_over_ranks(dt, world, device)
         ms_step = 1000.0 * dt / args.steps
-        maps = (B * world if args.mode == "samples" else B) * args.steps
-        result["value"] = maps / dt
-        # the same step with every product in exact fp32 (conv_0_0 on the fp32 VALU kernel instead
-        # of the split-fp16 MFMA kernel): reported beside value
-        reg = net.cost_volume_reg
-        if reg.split_f16:
-            reg.split_f16 = False
+        maps_per_step = B * world if args.mode == "samples" else B
+        result["value"] = maps_per_step * args.steps / dt
+        if args.mode == "samples":
+            # the opt-in split-fp16 arithmetic (MVSConfig(arithmetic="split_f16"): the f16 matrix cores with
+            # split operands, the split cost volume, the split head; narrower than fp32)
+            # timed the same way: reported beside value, never as value
+            net.set_arithmetic("split_f16")
             with torch.no_grad():
-                step()
-                barrier(world)
-                t0 = time.perf_counter()
-                for _ in range(args.steps):
+                for _ in range(2):
                     step()
-                barrier(world)
-                dte = time.perf_counter() - t0
-            reg.split_f16 = True
-            dte = max_over_ranks(dte, world, device)
-            result["exact_fp32"] = {"ms_per_step": 1000.0 * dte / args.steps,
-                                    "value": (B * world if args.mode == "samples" else B) * args.steps / dte}
-            log("exact-fp32 conv_0_0 step: %.2f ms/step" % result["exact_fp32"]["ms_per_step"])
+                torch.cuda.synchronize()
+            dts, kms = timed_steps(step, args.steps, world, device, hooked=True)
+            net.set_arithmetic("fp32")
+            dts = max_over_ranks(dts, world, device)
+            result["split_f16"] = {"ms_per_step": 1000.0 * dts / args.steps,
+                                   "value": maps_per_step * args.steps / dts, "step_kernel_ms": kms}
+            log("split-fp16 opt-in step: %.2f ms/step" % result["split_f16"]["ms_per_step"])
         # the same step with the regulariser over the WHOLE volume (CostVolumeReg.forward_full,
         # the reference's op sequence) instead of its eval-mode live regions: reported beside
         # value so the gain of the live-region evaluation is visible
@@ -665,30 +695,33 @@ def main():
             barrier(world)
             dtf = time.perf_counter() - t0
         dtf = max_over_ranks(dtf, world, device)
-        result["full"] = {"ms_per_step": 1000.0 * dtf / full_steps,
-                          "value": (B * world if args.mode == "samples" else B) * full_steps / dtf,
+        result["full"] = {"ms_per_step": 1000.0 * dtf / full_steps, "value": maps_per_step * full_steps / dtf,
                           "steps": full_steps}
         log("full-volume regulariser: %.2f ms/step" % result["full"]["ms_per_step"])
+        net.cost_volume_reg.live_region = True
         # test.py:53,61: the reference's test driver runs the model in TRAIN mode under no_grad
         # (BatchNorm normalises with batch statistics over the whole volume, so the eval-mode
-        # live-region shortcut does not apply): timed as its own field
+        # live-region shortcut does not apply): timed as its own field, fp32 and split-fp16
         if args.mode == "samples":
-            net.cost_volume_reg.live_region = True
             net.train()
-            train_steps = max(1, min(args.steps, 10))   # ~12 ms each: 10 steps keep the figure stable
-            with torch.no_grad():
-                for _ in range(2):
-                    step()
-                barrier(world)
-                t0 = time.perf_counter()
-                for _ in range(train_steps):
-                    step()
-                barrier(world)
-                dtt = time.perf_counter() - t0
-            dtt = max_over_ranks(dtt, world, device)
-            result["train_bn"] = {"ms_per_step": 1000.0 * dtt / train_steps,
-                                  "value": B * world * train_steps / dtt, "steps": train_steps}
-            log("train-mode BN step (test.py:61): %.2f ms/step" % result["train_bn"]["ms_per_step"])
+            train_steps = max(1, min(args.steps, 10))   # 10 steps keep the figure stable
+            for arith in ("fp32", "split_f16"):
+                net.set_arithmetic(arith)
+                with torch.no_grad():
+                    for _ in range(2):
+                        step()
+                    barrier(world)
+                    t0 = time.perf_counter()
+                    for _ in range(train_steps):
+                        step()
+                    barrier(world)
+                    dtt = time.perf_counter() - t0
+                dtt = max_over_ranks(dtt, world, device)
+                result["train_bn" if arith == "fp32" else "train_bn_split_f16"] = {
+                    "ms_per_step": 1000.0 * dtt / train_steps, "value": B * world * train_steps / dtt,
+                    "steps": train_steps}
+                log("train-mode BN step (test.py:61), %s: %.2f ms/step" % (arith, 1000.0 * dtt / train_steps))
+            net.set_arithmetic("fp32")
             if not args.no_extra:
                 net.eval()
                 result["bf16"] = bf16_step(net, inputs, B, V, D, H, W, device, world, args.steps)
@@ -697,16 +730,15 @@ def main():
     # fused kernel timing (this rank's share of planes in dshard mode)
     d_count = D if args.mode == "samples" else D // world
     log("timing the fused kernel")
-    # samples mode: the channel-quad store the eval step feeds the regulariser with; dshard mode:
+    # samples mode: the fp32 channel-quad store the eval step feeds the regulariser with; dshard mode:
     # the NCDHW slabs the owner exchange moves
-    quads = args.mode == "samples"
-    k_ms, op_ms, alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count, quads=quads)
+    store = "c4" if args.mode == "samples" else "ncdhw"
+    k_ms, op_ms, alg = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count, store=store)
     k_ms = max_over_ranks(k_ms, world, device)
     op_ms = max_over_ranks(op_ms, world, device)
     nc_ms, nc_op_ms, _ = time_kernel(B, V, C, h, w, D, device, args.kernel_iters, 0, d_count)
     nc_ms = max_over_ranks(nc_ms, world, device)
-    # warp-kernel duration: its launches inside the timed steps when the step runs it; the isolated
-    # back-to-back launches otherwise (e.g. with the opt-in fused head, which forms the volume itself)
+    # warp-kernel duration: its launches inside the timed steps
     step_k = result.get("step_kernel_ms", {})
     iso_ms = k_ms
     if "cost_volume" in step_k:
@@ -714,8 +746,11 @@ def main():
     gbs = alg / (k_ms * 1e-3) / 1e9
     tag = "b%dv%dd%dh%dw%d" % (B, V, d_count, h, w)
     traffic = load_traffic(tag)
-    head_kind = next((k for k in ("split_head", "cv_head") if k in step_k), None)
-    head_ms = max_over_ranks(step_k[head_kind], world, device) if head_kind else None
+    conv0_ms = max_over_ranks(step_k["conv_0_0"], world, device) if "conv_0_0" in step_k else None
+    split = result.get("split_f16")
+    head_ms = split["step_kernel_ms"].get("split_head") if split else None
+    if head_ms is not None:
+        head_ms = max_over_ranks(head_ms, world, device)
 
     if rank != 0:
         if world > 1:
@@ -737,17 +772,23 @@ def main():
                 "weights; BN eval mode, live-region regulariser (train-mode BN as in test.py:61: "
                 "field train_bn)",
         "config": {"workload": "cfg%d: %d-view %dx%d D=%d batch=%d per %s, BN eval, live-region "
-                               "regulariser" % (
+                               "regulariser, fp32 arithmetic" % (
                        2 if args.mode == "samples" else 4, V, W, H, D, B,
                        "GPU" if args.mode == "samples" else "job (D sharded)"),
                    "global_batch": B * (world if args.mode == "samples" else 1),
                    "views": V, "planes": D, "image_hw": [H, W], "feature_hw": [h, w],
                    "parallelism": ("samples%d" % world) if args.mode == "samples" else ("dshard%d" % world)},
+        "arithmetic": ("exact fp32 in every layer of the timed step (MVSConfig(arithmetic='fp32'), the default): "
+                       "fp32 cost volume (the reference's torch-CPU law, bit for bit given the sampling matrices), "
+                       "2-D convolutions on fp32 VALU kernels, conv_0_0 / conv_out on fp32 VALU kernels (conv_0_0 "
+                       "with a depth-Winograd F(2,3) transform), every region convolution on the f32-input matrix "
+                       "cores (v_mfma_f32_16x16x4_f32: each product and sum rounded as an fmaf chain), fp32 "
+                       "softmax / soft-argmin / refinement"),
         "warp_kernel": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": gbs / HBM_PEAK_GBS,
                         "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
                         "kernel": "cost_volume_staged_kernel<V=%d, planes=8, %s>" % (
-                            V, "split-fp16 channel-quad store (16 B per voxel and 4 channels)" if quads
+                            V, "fp32 channel-quad store (16 B per voxel and 4 channels)" if store == "c4"
                             else "NCDHW store"), "kernel_ms": k_ms,
                         "alg_bytes_per_launch": alg,
                         "timing": ("HIP events around each launch inside the %d timed steps" % args.steps
@@ -757,40 +798,59 @@ def main():
                                         "frac": alg / (nc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}},
         "hot_path": {"cost_volumes_per_s": B / (op_ms * 1e-3), "op_ms": op_ms,
                      "op": "mvs_cost_volume_fwd%s: prologue kernel (sampling matrices + channel-quad "
-                           "packing + reference resampling) + cost_volume_staged kernel" % ("_c4" if quads else ""),
+                           "packing + reference resampling) + cost_volume_staged kernel" % (
+                               "_c4" if store == "c4" else ""),
                      "op_GBps": alg / (op_ms * 1e-3) / 1e9},
     }
-    if head_ms is not None:
-        # the step's dominant kernel: the split head (conv_0_0 + conv_1_0 in one pass over the split
-        # volume), or with MVS_CV_HEAD=1 the fused head (the volume formed on chip as well)
-        hw_ = head_work(B, V, D, h, w, head_kind)
-        alg_tf = hw_["alg_flops"] / (head_ms * 1e-3) / 1e12
-        exe_tf = hw_["mfma_flops"] / (head_ms * 1e-3) / 1e12
+    if conv0_ms is not None:
+        # the fp32 step's dominant kernel: conv_0_0 (model.py:101, 32 -> 8 over the whole volume + BN_0 +
+        # ReLU) on the fp32 VALU kernel, concurrent with the region convolutions on the fp32 matrix cores
+        fl = conv0_flops(B, D, h, w)
+        tf = fl / (conv0_ms * 1e-3) / 1e12
         out["roofline"] = {
-            "bound": "mfma", "achieved": exe_tf, "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s",
-            "frac": exe_tf / MFMA_F16_PEAK_TFS, "traffic": head_traffic(tag, head_kind),
-            "kernel": "cv_head_kernel<2, PRESPLIT>" if head_kind == "split_head" else "cv_head_kernel<V=%d>" % V,
-            "kernel_ms": head_ms,
-            "timing": "HIP events around each launch inside the %d timed steps" % args.steps,
-            "flops_per_launch": hw_["mfma_flops"],
-            "flops": "f16 matrix-core flops of the split-fp16 convolutions (the arithmetic the kernel is built "
-                     "on, dense f16 peak): conv_0_0 2 v_mfma_f32_16x16x32_f16 per (16 voxels, tap) = 55,296 flops "
-                     "per voxel (hi/lo rows x w_hi|w_lo columns), conv_1_0 3 per (16 windows, tap) = 82,944 per "
-                     "window",
-            "fp32_equivalent": {
-                "flops_per_launch": hw_["alg_flops"], "tflops": alg_tf, "peak": MFMA_F32_PEAK_TFS,
-                "frac": alg_tf / MFMA_F32_PEAK_TFS,
-                "note": "the fp32 convolution flops the two layers need (conv_0_0 B*D*h*w x 8 x 32 x 27 x 2, "
-                        "conv_1_0 B*|window region| x 16 x 32 x 27 x 2) against the dense fp32 matrix peak: above "
-                        "1 means the split scheme beats any exact-fp32 MFMA kernel's ceiling"},
-            "hbm": {"alg_bytes_per_launch": hw_["hbm_bytes"], "GBps": hw_["hbm_bytes"] / (head_ms * 1e-3) / 1e9,
-                    "peak": HBM_PEAK_GBS, "frac": hw_["hbm_bytes"] / (head_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                    "note": ("the split cost volume in (once); y0 and y1 out" if head_kind == "split_head" else
-                             "features + reference views in; y0, y1 and the conv_2_0 box out (the cost volume "
-                             "itself never reaches HBM)")},
-            "regions": hw_["regions"]}
+            "bound": "mfma", "achieved": tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s", "frac": tf / MFMA_F32_PEAK_TFS,
+            "traffic": conv0_traffic(tag), "kernel": "conv3d_k3_narrow_kernel<8, wino_z> (conv_0_0, fp32 VALU)",
+            "kernel_ms": conv0_ms, "flops_per_launch": fl,
+            "timing": "HIP events around each launch inside the %d timed steps (on its side stream, concurrent "
+                      "with the region convolutions)" % args.steps,
+            "flops": "useful fp32 convolution flops B*D*h*w x 8 x 32 x 27 x 2 (the direct convolution's; the "
+                     "depth-Winograd kernel executes 2/3 of the multiplies) against the fp32 compute peak: 157.3 "
+                     "TF is both the f32 VALU rate and the f32-input MFMA rate (MI355X_MICROARCH.md), so 'mfma' "
+                     "names the fp32 compute roof",
+            "hbm": {"alg_bytes_per_launch": 4.0 * B * D * h * w * (32 + 8),
+                    "GBps": 4.0 * B * D * h * w * 40 / (conv0_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                    "note": "the fp32 cost volume in once, y0 out once"}}
     else:
         out["roofline"] = dict(out["warp_kernel"])
+    if split is not None:
+        # the opt-in split-fp16 arithmetic: never the headline (narrower than fp32)
+        sp = {"ms_per_step": split["ms_per_step"], "value": split["value"], "unit": "depth maps/s",
+              "dtype": "f16x2-split (fp16 hi + lo parts of power-of-two-scaled fp32 operands on the f16 matrix "
+                       "cores, fp32 accumulation; narrower than fp32)",
+              "note": "MVSConfig(arithmetic='split_f16'), opt-in: encoder / refinement / regulariser convolutions "
+                      "on v_mfma_f32_16x16x32_f16 with split operands (22 significant bits per operand, 3-4 partial "
+                      "products), the cost volume stored as its fp16 parts and read once by the split head; element "
+                      "contract |x - (hi + lo) 2^-e| <= 2^-22 |x| + 2^-37 B^2 (an absolute floor below ~1e-5 of a "
+                      "tensor's bound: tests/test_split_conv.py::test_split_conv_dynamic_range, DESIGN.md 3.5)",
+              "step_kernel_ms": split["step_kernel_ms"]}
+        if head_ms is not None:
+            hw_ = head_work(B, V, D, h, w, "split_head")
+            alg_tf = hw_["alg_flops"] / (head_ms * 1e-3) / 1e12
+            exe_tf = hw_["mfma_flops"] / (head_ms * 1e-3) / 1e12
+            sp["roofline"] = {
+                "bound": "mfma", "achieved": exe_tf, "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": exe_tf / MFMA_F16_PEAK_TFS, "traffic": head_traffic(tag, "split_head"),
+                "kernel": "cv_head_kernel<2, PRESPLIT>", "kernel_ms": head_ms,
+                "timing": "HIP events around each launch inside the %d timed split-fp16 steps" % args.steps,
+                "flops_per_launch": hw_["mfma_flops"],
+                "flops": "executed f16 matrix-core flops: conv_0_0 2 v_mfma_f32_16x16x32_f16 per (16 voxels, tap), "
+                         "conv_1_0 3 per (16 windows, tap)",
+                "useful_fp32_conv_flops": {"flops_per_launch": hw_["alg_flops"], "tflops": alg_tf},
+                "hbm": {"alg_bytes_per_launch": hw_["hbm_bytes"], "GBps": hw_["hbm_bytes"] / (head_ms * 1e-3) / 1e9,
+                        "peak": HBM_PEAK_GBS, "frac": hw_["hbm_bytes"] / (head_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "note": "the split cost volume in (once); y0 and y1 out"},
+                "regions": hw_["regions"]}
+        out["split_f16_step"] = sp
     if "dshard_phases" in result:
         out["dshard_phases"] = {
             "phases": list(DSHARD_PHASES), "ms_per_rank": result["dshard_phases"],
@@ -799,17 +859,6 @@ def main():
                     "owner-targeted point-to-point exchange (exchange, incl. waiting for the slowest sender), "
                     "the owner's regulariser + soft-argmin + refinement (owner_compute; 0 on ranks owning no "
                     "sample), the depth maps to rank 0 (gather)"}
-    out["arithmetic"] = ("fp32 throughout, except conv_0_0 and conv_1_0 (model.py:101,103) in samples mode: "
-                         "f16 MFMA with split-fp16 operands (hi + lo parts of the fp32 values; conv_0_0 all four "
-                         "partial products, conv_1_0 three; fp32 accumulation), the cost volume stored by the "
-                         "fused warp kernel as those hi/lo parts; max error 0.3-0.5x that of the exact fp32 "
-                         "kernels vs float64 (tests/test_split_conv.py, DESIGN.md 3.5); element contract |x - "
-                         "(hi + lo) 2^-e| <= 2^-22 |x| + 2^-37 B^2 (B = max|feat|): fp32-level relative error down "
-                         "to ~1e-5 of the volume bound, an absolute floor below (test_split_conv_dynamic_range)")
-    if "exact_fp32" in result:
-        out["exact_fp32_step"] = dict(result["exact_fp32"], unit="depth maps/s", note=(
-            "the same step with every product in exact fp32: the materialised cost volume, conv_0_0 on "
-            "the exact-fp32 kernel and conv_1_0 on the fp32 MFMA region kernel (split_f16 off)"))
     if "full" in result:
         out["full_volume_regulariser"] = dict(result["full"], unit="depth maps/s", note=(
             "same step with CostVolumeReg.forward_full (every voxel of every level, as "
@@ -817,10 +866,13 @@ def main():
             "(eval BN: only the regions whose values reach the output; same sums, fp32 summation "
             "order may differ)"))
     if "train_bn" in result:
-        out["train_bn"] = dict(result["train_bn"], unit="depth maps/s", note=(
+        out["train_bn"] = dict(result["train_bn"], unit="depth maps/s", dtype="f32", note=(
             "test.py:53,61 mode: model.train() under no_grad, BatchNorm batch statistics over the "
             "whole volume and running-statistic updates, exact on live regions "
-            "(CostVolumeReg.forward_live_train, DESIGN.md 5b)"))
+            "(CostVolumeReg.forward_live_train, DESIGN.md 5b); fp32 arithmetic"))
+    if "train_bn_split_f16" in result:
+        out["train_bn_split_f16"] = dict(result["train_bn_split_f16"], unit="depth maps/s", dtype="f16x2-split",
+                                         note="train_bn with MVSConfig(arithmetic='split_f16') (opt-in)")
     # backward of the fused op (train.py:103): informational
     log("timing the backward")
     out["cost_volume_backward"] = time_backward(B, V, C, h, w, d_count, device)

@@ -745,7 +745,9 @@ int mvs_conv3d_region_split_fwd(int mode, int flags, const float* x, const float
       io[k] = in_origin[k];
       is[k] = in_size[k];
     }
-  if (x2 && x_bound && !x2_bound) return MVS_ERR_INVALID_ARGUMENT;   // a sum needs both bounds
+  // every mode scales its input by the bound words (S2: the split volume's; S1 / T2: the region
+  // tensor's, raised by the kernel that wrote it): without them the fp16 hi parts could overflow
+  if (!x_bound || (x2 && !x2_bound)) return MVS_ERR_INVALID_ARGUMENT;   // a sum needs both bounds
   if (((uintptr_t)x | (uintptr_t)x2 | (uintptr_t)weight_frag) & 15u ||
       ((uintptr_t)x_bound | (uintptr_t)x2_bound | (uintptr_t)y_bound) & 3u)
     return MVS_ERR_INVALID_ARGUMENT;

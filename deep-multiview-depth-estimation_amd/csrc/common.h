@@ -66,19 +66,28 @@ __device__ inline float bilerp_sum(float t0, float t1, float t2, float t3, const
 // order, mean = sum / V and cv = (sum of (x - mean) * (x - mean) in view order) / V, every product
 // and sum rounded on its own and both divisions correctly rounded.  x / V is formed as
 // q = x * r, q + fma(x - q V, r) (r = RN(1 / V), the remainder exact by fma): the correctly rounded
-// quotient for every fp32 x and V = 2..16, checked exhaustively (tests/test_exact_division.py);
-// one multiply and two fmas instead of the IEEE division sequence.
+// quotient for every normal fp32 x >= 2^-124 and V = 2..16, and for every x when V is odd or a power of
+// two, checked exhaustively (tests/test_exact_division.py); one multiply and two fmas instead of the IEEE
+// division sequence.  For even V = 2^k m (m odd, k, m > 1: 6, 10, 12, 14) a quotient in the subnormal
+// range can be an exact tie between two subnormals, where the fma's rounding of q + e r (r inexact) falls
+// on the wrong side: lanes with |x| < 2^-120 take the IEEE division then -- a wave-uniform
+// launch flag, so V = 3, 5 (and every odd V) never test for it.
 // ------------------------------------------------------------------------------------------
 struct ViewDiv {
   float v, r;   // V and RN(1 / V)
+  int tie;      // V even and not a power of two: tiny quotients take the IEEE division
 };
 
-__host__ __device__ inline ViewDiv view_div(int V) { return ViewDiv{(float)V, 1.0f / (float)V}; }
+__host__ __device__ inline ViewDiv view_div(int V) {
+  return ViewDiv{(float)V, 1.0f / (float)V, (V % 2 == 0 && (V & (V - 1)) != 0) ? 1 : 0};
+}
 
 __device__ inline float div_views(float x, ViewDiv d) {
 #pragma clang fp contract(off)
   const float q = x * d.r;
-  return __builtin_fmaf(__builtin_fmaf(-q, d.v, x), d.r, q);
+  float y = __builtin_fmaf(__builtin_fmaf(-q, d.v, x), d.r, q);
+  if (d.tie && __builtin_expect(__builtin_fabsf(x) < 0x1p-120f, 0)) y = x / d.v;   // IEEE, correctly rounded
+  return y;
 }
 
 // the variance of one element over V <= MAXV views x[0 .. V) (scalar form of packed.h variance_law4)

@@ -478,13 +478,22 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       if (has(u + kAhead)) issue(u + kAhead);
       if (has(u + kAhead + 1)) rdc(u + kAhead + 1);
       char* dst = ring + (sl0 + pl) * kSlotB + (m & 0x1FFFu);
+      // THE HAZARD: the item's two ds_write_b64 ring stores must not run while
+      // any of this wave's tap gathers (buffer_load_dwordx4) is still in flight, and must complete before
+      // the wave's next VALU work.  With gathers of later items outstanding across the stores, the last
+      // 16-lane group of a ds_write_b64 (lanes 48-63, serviced last) stored wrong data in some launches
+      // (bench geometry: 20 of 20 launches at V = 2 and V = 3); a wait for the stores alone cured V = 2,
+      // not V = 3; both waits: 0 of 20 at every geometry (tools/dbg/stress_r6.sh, gpurun_out r6b / r6c).
+      __builtin_amdgcn_sched_barrier(0);
+#ifndef MVS_HEAD_NO_STORE_FENCE   // (mutation build of tests/test_head_isa.py only: the rule's checker must fail)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      __builtin_amdgcn_sched_barrier(0);
       *reinterpret_cast<uint2*>(dst) = hi;
       *reinterpret_cast<uint2*>(dst + kPartB) = lo;
-#ifdef MVS_HEAD_WAIT_AFTER_STORE   // experiment: the item's LDS stores complete before any later VALU
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-#endif
       // one item per scheduling region: without it the scheduler hoists every item's loads to the
       // top (all 7 items' gathers live at once: VGPR spills)
       __builtin_amdgcn_sched_barrier(0);
@@ -835,8 +844,9 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
 __global__ __launch_bounds__(256) void head_faces_kernel(float* __restrict__ y1, int B, int on0, int on1, int on2,
                                                          int lz, int hz, int ly, int hy, int lx, int hx,
                                                          const float* __restrict__ sc, const float* __restrict__ sh,
-                                                         const float* __restrict__ mu) {
+                                                         const float* __restrict__ mu, uint32_t* __restrict__ y1_bound) {
   const long nzf = lz + hz, nyf = ly + hy, nxf = lx + hx;
+  float vmax = 0.0f;   // the constants this thread wrote raise y1's bound words too
   const long mz = on0 - nzf, my = on1 - nyf;
   const long n0 = nzf * on1 * on2, n1 = mz * nyf * on2, n2 = mz * my * nxf;
   const long per = n0 + n1 + n2;
@@ -873,12 +883,14 @@ __global__ __launch_bounds__(256) void head_faces_kernel(float* __restrict__ y1,
     float v = ldexpf(0.0f + (0.0f + 0.0f), 0);
     if (sc) v = fmaxf((v - mu[co]) * sc[co] + sh[co], 0.0f);
     y1[((((size_t)bb * on0 + oz) * on1 + oy) * on2 + ox) * 16 + co] = v;
+    vmax = fmaxf(vmax, v);
   }
+  if (y1_bound) bound_update<true>(y1_bound, vmax);   // every lane of every wave reaches it
 }
 
 // outputs of the conv_1_0 region whose window no tile owns (all-padding windows, head_faces_kernel)
 void launch_head_faces(const Geometry& g, const HeadArgs& a, const float* const* bn1, float* y1, const int* pad,
-                       const int* o0, const int* on, hipStream_t s) {
+                       const int* o0, const int* on, hipStream_t s, uint32_t* y1_bound = nullptr) {
   // per dim, per dim, region outputs whose window start 2 o - P lies below -1 (before tile 0) or at /
   // beyond the last owned start (n_tiles * tile - 1 in x / y, D - 1 + 2 in z)
   int lo[3], hi[3];
@@ -893,7 +905,7 @@ void launch_head_faces(const Geometry& g, const HeadArgs& a, const float* const*
     const long n = (long)g.B * on[0] * on[1] * on[2] * 16;
     const int blocks = (int)std::min<long>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(head_faces_kernel, dim3(blocks), dim3(256), 0, s, y1, g.B, on[0], on[1], on[2], lo[0], hi[0],
-                       lo[1], hi[1], lo[2], hi[2], bn1[0], bn1[1], bn1[2]);
+                       lo[1], hi[1], lo[2], hi[2], bn1[0], bn1[1], bn1[2], y1_bound);
   }
 }
 
@@ -1029,7 +1041,7 @@ int launch_split_head(const Geometry& g, const void* scv_in, const uint32_t* abs
     }
   }
 #endif
-  launch_head_faces(g, a, bn1, y1, pad, o0, on, s);
+  launch_head_faces(g, a, bn1, y1, pad, o0, on, s, y1_bound);
   return MVS_OK;
 }
 

@@ -72,7 +72,13 @@ __device__ inline f4v div_views4(const f4v& x, ViewDiv d) {
 #pragma clang fp contract(off)
   const f4v r = {d.r, d.r, d.r, d.r};
   const f4v q = x * r;
-  return __builtin_elementwise_fma(__builtin_elementwise_fma(-q, f4v{d.v, d.v, d.v, d.v}, x), r, q);
+  f4v y = __builtin_elementwise_fma(__builtin_elementwise_fma(-q, f4v{d.v, d.v, d.v, d.v}, x), r, q);
+  if (d.tie) {   // launch-uniform: V = 6, 10, 12, 14 only (common.h div_views)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (__builtin_expect(__builtin_fabsf(x[c]) < 0x1p-120f, 0)) y[c] = x[c] / d.v;
+  }
+  return y;
 }
 
 // costvolume.py:12-14 for 4 channels of one voxel, in the reference's torch CPU roundings (common.h:

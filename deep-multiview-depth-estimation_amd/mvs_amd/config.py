@@ -5,6 +5,7 @@ The same names exist here with the same default values, so ``from mvs_amd.config
 is a drop-in; ``MVSConfig`` carries them explicitly for callers that need several geometries
 in one process (the reference cannot: it must be re-imported per geometry).
 """
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -31,6 +32,7 @@ def pad_outpad(d_num, feat_h, feat_w):
 
 PAD, OUTPAD = pad_outpad(D_NUM, FEAT_H, FEAT_W)
 DEVICE = torch.device("cuda:0" if torch.cuda.is_available() else "cpu")  # config.py:24
+ARITHMETICS = ("fp32", "split_f16")
 
 
 @dataclass
@@ -49,8 +51,21 @@ class MVSConfig:
     # regulariser computes in fp32 from the rounded values; the default "float32" is the reference's
     # numerics
     cv_dtype: str = "float32"
+    # the arithmetic of the HIP inference kernels.  "fp32" (default, the reference's model.py:35-59,
+    # 76-89, 134-145 nn.Conv2d / Conv3d / ConvTranspose3d numerics): every product and sum in exact
+    # fp32 -- VALU kernels, fp32-input MFMA (v_mfma_f32_16x16x4_f32, an fmaf chain bit for bit) and
+    # the fp32 cost volume.  "split_f16" (opt-in, narrower than fp32): the encoder / refinement /
+    # regulariser convolutions on the f16 matrix cores with split-fp16 operands (hi + lo fp16 parts
+    # of a power-of-two-scaled fp32 value: 22 significant bits per operand, an absolute floor below
+    # ~1e-5 of a tensor's bound) and the cost volume stored as those parts.
+    # MVS_ARITHMETIC overrides the default for a process.
+    arithmetic: str = field(default=None)
 
     def __post_init__(self):
+        if self.arithmetic is None:
+            self.arithmetic = os.environ.get("MVS_ARITHMETIC", "fp32")
+        if self.arithmetic not in ARITHMETICS:
+            raise ValueError("arithmetic must be one of %s, got %r" % (ARITHMETICS, self.arithmetic))
         if self.feat_h is None:
             self.feat_h = int(self.in_h / self.dim_reduce)
         if self.feat_w is None:

@@ -50,12 +50,14 @@ def _conv_bn_relu_stack(spec, device):
     return nn.Sequential(*layers)
 
 
-def _run_stack(seq, x):
+def _run_stack(seq, x, split_f16=False):
     """A conv -> BatchNorm -> ReLU stack (encoder / refinement).  In fp32 no-grad inference on the
-    GPU the convolutions run on the direct HIP kernel (mvs::conv2d, csrc/conv2d_narrow.hip) with eval
-    BN + ReLU fused into its epilogue; train-mode BN (test.py:61) takes one-pass float64 batch sums
-    of the convolution's output and one in-place BN + ReLU pass (csrc/channel_ops.hip), with the
-    running statistics updated as torch does.  Elsewhere the modules themselves."""
+    GPU the convolutions run on the direct HIP kernel (mvs::conv2d, csrc/conv2d_narrow.hip: exact fp32)
+    with eval BN + ReLU fused into its epilogue; train-mode BN (test.py:61) takes one-pass float64
+    batch sums of the convolution's output and one in-place BN + ReLU pass (csrc/channel_ops.hip),
+    with the running statistics updated as torch does.  Elsewhere the modules themselves.
+    ``split_f16`` (MVSConfig(arithmetic="split_f16"), opt-in): the 8..32-channel layers on the f16
+    matrix cores with split operands (csrc/conv2d_split.hip)."""
     if not _hip_inference(x):
         return seq(x)
     from .ops import (CONV2D_SPLIT_SHAPES, bn_relu_, bound_words, channel_stats, conv2d, conv2d_split,
@@ -63,7 +65,8 @@ def _run_stack(seq, x):
     layers = list(seq)
     # split-fp16 MFMA convolutions (csrc/conv2d_split.hip) for the 8..32-channel inputs: every layer's
     # output carries bound words (one zeroed set per layer, one memset) that scale the next layer's input
-    words = bound_words(len(layers), x.device) if os.environ.get("MVS_CONV2D_F16", "1") != "0" else None
+    words = (bound_words(len(layers), x.device)
+             if split_f16 and os.environ.get("MVS_CONV2D_F16", "1") != "0" else None)
 
     def conv(layer, x, xb, yb, bn=None):
         """(y, whether yb now bounds y): the HIP convolutions for the reference's layer shapes"""
@@ -126,9 +129,10 @@ class FeatureEncoder(nn.Module):
         if (in_ch, base_filt) != (3, 8):
             raise ValueError("the reference encoder is fixed at in_ch=3, base_filt=8")
         self.model = _conv_bn_relu_stack(_ENCODER, device)
+        self.split_f16 = False   # MVSNet.set_arithmetic
 
     def forward(self, x):
-        return _run_stack(self.model, x)
+        return _run_stack(self.model, x, self.split_f16)
 
 
 class CostVolumeReg(nn.Module):
@@ -165,10 +169,10 @@ class CostVolumeReg(nn.Module):
         self.pad, self.outpad = tuple(pad), tuple(outpad)
         # eval-mode live-region evaluation (see forward_live); False = always the full-volume path
         self.live_region = True
-        # conv_0_0 of the HIP eval path on the f16 matrix cores with split-fp16 operands (fp32-level
-        # error, csrc/conv3d_split.hip) when the cost volume carries its bound words; False (or
-        # MVS_SPLIT_F16=0) = the exact-fp32 VALU kernel
-        self.split_f16 = os.environ.get("MVS_SPLIT_F16", "1") != "0"
+        # False (default, MVSConfig(arithmetic="fp32")): every HIP layer in exact fp32 (the depth-Winograd
+        # VALU conv_0_0, fp32-MFMA region convs).  True (arithmetic="split_f16", opt-in, narrower than
+        # fp32): the f16 matrix cores with split-fp16 operands (csrc/split.h) read the split cost volume
+        self.split_f16 = False
 
     def forward(self, cv):
         """cv [B, C, D, H, W] (the reference's input), an ops.BoundCostVolume (the channel-quad layout
@@ -327,7 +331,7 @@ class CostVolumeReg(nn.Module):
         volume on conv_2_0's input box only, ``cv_box`` (origin, size) that box."""
         from .ops import (CONV_S1, CONV_S2, CONV_T2, bound_words, conv3d_k3, conv3d_k3_split, conv3d_region,
                           conv3d_region_split, conv_s2_split, deconv3d_k3s2, region_weight, softmax_depth,
-                          split_head)
+                          split_head, timed_kernel)
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad = list(n), list(self.pad)
@@ -371,7 +375,8 @@ class CostVolumeReg(nn.Module):
                     y0 = conv3d_k3_split(cv, bound, self.conv_0_0.weight, *bn_eval(self.BN_0))
                     bound.record_stream(side)
                 else:
-                    y0 = conv3d_k3(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), in_c4=c4, wino_z=True)
+                    with timed_kernel("conv_0_0"):   # (bench.py's roofline kernel in fp32 arithmetic)
+                        y0 = conv3d_k3(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), in_c4=c4, wino_z=True)
             cv.record_stream(side)
 
         def level(k, conv_a, conv_b, bn, reg):
@@ -970,9 +975,10 @@ class DepthRefinement(nn.Module):
         if (in_ch, base_filt) != (4, 32):
             raise ValueError("the reference refinement net is fixed at in_ch=4, base_filt=32")
         self.model = _conv_bn_relu_stack(_REFINE, device)
+        self.split_f16 = False   # MVSNet.set_arithmetic
 
     def forward(self, depth_and_input):
-        return _run_stack(self.model, depth_and_input) + depth_and_input[:, 0].unsqueeze(1)
+        return _run_stack(self.model, depth_and_input, self.split_f16) + depth_and_input[:, 0].unsqueeze(1)
 
 
 def _select_images(images, idx):
@@ -1004,6 +1010,20 @@ class MVSNet(nn.Module):
         self.parameters = (list(self.feature_encoder.parameters()) +
                            list(self.cost_volume_reg.parameters()) +
                            list(self.depthmap_refine.parameters()))
+        self.set_arithmetic(self.cfg.arithmetic)
+
+    def set_arithmetic(self, arithmetic):
+        """"fp32" (the reference's numerics: every HIP layer in exact fp32) or "split_f16" (opt-in: the
+        encoder, refinement and regulariser convolutions on the f16 matrix cores with split-fp16
+        operands, the cost volume stored as its fp16 hi / lo parts; narrower than fp32)."""
+        from .config import ARITHMETICS
+        if arithmetic not in ARITHMETICS:
+            raise ValueError("arithmetic must be one of %s, got %r" % (ARITHMETICS, arithmetic))
+        self.cfg.arithmetic = arithmetic
+        split = arithmetic == "split_f16"
+        for m in (self.feature_encoder, self.cost_volume_reg, self.depthmap_refine):
+            m.split_f16 = split
+        return self
 
     def forward(self, nn_input, K_batch, R_batch, T_batch, d_min, d_int, batch_size, n_views):
         c = self.cfg
@@ -1059,7 +1079,8 @@ class MVSNet(nn.Module):
             # (ops.refine_input / refine_output: 9 launches -> 2, bit-equal to the sequence below)
             from .ops import refine_input, refine_output
             x = refine_input(initial_depth_map, d_min, d_int, c.d_num, c.d_scale, ref_img)
-            return refine_output(_run_stack(self.depthmap_refine.model, x), x, d_min, d_int, c.d_num, c.d_scale)
+            return refine_output(_run_stack(self.depthmap_refine.model, x, self.depthmap_refine.split_f16), x,
+                                 d_min, d_int, c.d_num, c.d_scale)
         d_trans = d_min.to(device)
         d_span = d_int.to(device).mul(c.d_num).mul(c.d_scale)
         norm_depth = torch.div(torch.subtract(initial_depth_map, d_trans), d_span)

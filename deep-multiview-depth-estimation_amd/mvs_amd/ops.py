@@ -30,6 +30,17 @@ def _require_gpu(t, name):
             "%s must be a GPU (HIP) tensor: the MI355X cost-volume path has no CPU fallback" % name)
 
 
+def _eager_only(op, **side_outputs):
+    """Fake-kernel guard of the ops that raise bound words / write batch sums IN PLACE without declaring
+    the mutation (mutates_args=(): torch's ADInplaceOrView wrapper cannot index an omitted trailing
+    optional): under torch.compile / functionalization such writes could be reordered or dropped, so a
+    trace that passes one fails here instead.  Eager mode (what MVSNet runs) is the only valid mode."""
+    given = [k for k, v in side_outputs.items() if v is not None]
+    if given:
+        raise NotImplementedError("mvs::%s writes %s in place (an undeclared mutation): eager mode only, not "
+                                  "torch.compile / functionalization" % (op, ", ".join(given)))
+
+
 def _cams(K, R, T, d_min, d_int, device, batch_size):
     K = K.to(device=device, dtype=_F32).reshape(-1, 3, 3).contiguous()
     R = R.to(device=device, dtype=_F32).reshape(-1, 3, 3).contiguous()
@@ -127,6 +138,26 @@ def _(feat, K, R, T, d_min, d_int, batch_size, n_views, d_begin, d_count, d_scal
 # opt-in fused head); the C ABI records them on the launch stream right around that kernel (the ops'
 # event arguments).
 KERNEL_EVENT_HOOK = None
+
+
+class timed_kernel:
+    """``with timed_kernel("conv_0_0"):`` -- KERNEL_EVENT_HOOK's event pair recorded on the CURRENT stream
+    right before and after the block (which launches one kernel on that stream, e.g. conv3d_k3); a
+    no-op when no hook is set."""
+
+    def __init__(self, kind):
+        self.kind, self.pair = kind, None
+
+    def __enter__(self):
+        if KERNEL_EVENT_HOOK is not None:
+            self.pair = KERNEL_EVENT_HOOK(self.kind)
+            self.pair[0].record(torch.cuda.current_stream())
+        return self
+
+    def __exit__(self, *exc):
+        if self.pair is not None:
+            self.pair[1].record(torch.cuda.current_stream())
+        return False
 
 
 @torch.library.custom_op("mvs::cost_volume_c4", mutates_args=())
@@ -428,6 +459,7 @@ def split_head(scv: torch.Tensor, absmax: torch.Tensor, w0: torch.Tensor, bn0_sc
 @split_head.register_fake
 def _(scv, absmax, w0, bn0_scale, bn0_shift, bn0_mean, w1, bn1_scale, bn1_shift, bn1_mean, pad, y1_origin, y1_size,
       y1_bound=None):
+    _eager_only("split_head", y1_bound=y1_bound)
     b, _, d, h, w, _ = scv.shape
     return (scv.new_empty((b, 8, d, h, w), dtype=_F32), scv.new_empty([b] + list(y1_size) + [16], dtype=_F32))
 
@@ -889,6 +921,7 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int, bn_scale: Optiona
 
 @conv2d.register_fake
 def _(x, weight, stride, bn_scale=None, bn_shift=None, bn_mean=None, y_bound=None):
+    _eager_only("conv2d", y_bound=y_bound)
     k = weight.shape[2]
     return x.new_empty((x.shape[0], weight.shape[0], (x.shape[2] + 2 * (k // 2) - k) // stride + 1,
                         (x.shape[3] + 2 * (k // 2) - k) // stride + 1))
@@ -950,6 +983,7 @@ def conv2d_split(x: torch.Tensor, weight: torch.Tensor, stride: int, x_bound: to
 
 @conv2d_split.register_fake
 def _(x, weight, stride, x_bound, y_bound=None, bn_scale=None, bn_shift=None, bn_mean=None):
+    _eager_only("conv2d_split", y_bound=y_bound)
     k = weight.shape[2]
     return x.new_empty((x.shape[0], weight.shape[0], (x.shape[2] + 2 * (k // 2) - k) // stride + 1,
                         (x.shape[3] + 2 * (k // 2) - k) // stride + 1))
@@ -1112,6 +1146,7 @@ def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Ten
 @conv3d_region.register_fake
 def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, bn_scale=None, bn_shift=None,
       bn_mean=None, out_ncdhw=False, in_c4=False, absmax=None, y_bound=None):
+    _eager_only("conv3d_region", y_bound=y_bound)
     if out_ncdhw:
         return x.new_empty((x.shape[0], weight.shape[1]) + tuple(out_size), dtype=_F32)
     return x.new_empty((x.shape[0],) + tuple(out_size) + (weight.shape[1],), dtype=_F32)
@@ -1294,6 +1329,7 @@ def conv3d_region_split_sums(x, x2, weight, mode, dims, out_origin, out_size, in
 def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, x_bound, x2_bound, y_bound,
       bn_scale=None, bn_shift=None, bn_mean=None, out_ncdhw=False, per_lane=False, y_addend=None,
       store_origin=None, store_size=None, stats=None, in_bn=None):
+    _eager_only("conv3d_region_split", y_bound=y_bound, stats=stats)
     size = tuple(out_size if store_size is None else store_size)
     if out_ncdhw:
         return x.new_empty((x.shape[0], weight.shape[1]) + size, dtype=_F32)

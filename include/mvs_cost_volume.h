@@ -505,7 +505,8 @@ int mvs_conv3d_region_split_weights(const float* weight, int c_in, int c_out, un
  * x_hi w_hi + x_hi w_lo + x_lo w_hi in fp32 accumulation, output unscaled by 2^-(ex + ew): fp32-level
  * error.  Geometry, layouts, BN epilogue and flags (MVS_CONV_OUT_NCDHW) as
  * mvs_conv3d_region_fwd; in_origin / in_size required.  x_bound / x2_bound: the inputs' bound words
- * (DEVICE; NULL = unscaled, only when every |v| < 2^14 is known); y_bound: NULL or the output's bound
+ * (DEVICE, required: MVS_ERR_INVALID_ARGUMENT when NULL -- unscaled values above 65504 would overflow
+ * the fp16 hi part; x2_bound required with x2); y_bound: NULL or the output's bound
  * words (zeroed by the caller).  MVS_CONV_S2 (conv_k_0): flags MVS_CONV_IN_C4 | MVS_CONV_IN_SPLIT, x the
  * split cost volume (mvs_cost_volume_fwd_c4_split; its fp16 parts are the operands, no conversion) or,
  * with in_origin / in_size, a box of it, x_bound its 8 bound words, x2 NULL.  Supported (mode, c_in,

@@ -82,6 +82,27 @@ def test_fake_kernels_give_shapes():
         assert tuple(d.shape) == (2, 1, 16, 20)
 
 
+def test_fake_kernels_refuse_in_place_side_outputs():
+    """The ops that raise bound words / write batch sums in place (undeclared mutations) are eager-only:
+    their fake kernels -- what torch.compile / functionalization trace -- raise when such an output is
+    passed, and give shapes without one."""
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    from mvs_amd import ops
+    with FakeTensorMode():
+        x = torch.empty(1, 5, 6, 7, 16)
+        w = torch.empty(27, 16, 16)
+        y = ops.conv3d_region_split(x, None, w, ops.CONV_S1, [5, 6, 7], [0, 0, 0], [5, 6, 7], [0, 0, 0],
+                                    [5, 6, 7], None, torch.empty(ops.BOUND_WORDS, dtype=torch.int32), None, None)
+        assert tuple(y.shape) == (1, 5, 6, 7, 16)
+        with pytest.raises(NotImplementedError, match="eager mode only"):
+            ops.conv3d_region_split(x, None, w, ops.CONV_S1, [5, 6, 7], [0, 0, 0], [5, 6, 7], [0, 0, 0],
+                                    [5, 6, 7], None, torch.empty(ops.BOUND_WORDS, dtype=torch.int32), None,
+                                    torch.empty(ops.BOUND_WORDS, dtype=torch.int32))
+        with pytest.raises(NotImplementedError, match="eager mode only"):
+            ops.conv2d(torch.empty(1, 8, 16, 16), torch.empty(8, 8, 3, 3), 1,
+                       y_bound=torch.empty(ops.BOUND_WORDS, dtype=torch.int32))
+
+
 def test_shard_helpers():
     from mvs_amd.depth_shards import plane_shard, owned_samples
     assert [plane_shard(256, 8, r) for r in (0, 7)] == [(0, 32), (224, 32)]

@@ -120,9 +120,9 @@ def test_conv2d_split_matches_torch(shape, bn, amp, hw):
 @pytest.mark.gpu
 @pytest.mark.parametrize("which", ["encoder", "refine"])
 def test_stack_split_path_matches_fp32_path(which, monkeypatch):
-    """FeatureEncoder / DepthRefinement in eval mode: the split-fp16 stack (default) against the fp32
-    direct-kernel stack (MVS_CONV2D_F16=0) and float64 modules: the split path's error is at most 2x
-    the fp32 path's + 1e-6 of the output scale."""
+    """FeatureEncoder / DepthRefinement in eval mode: the split-fp16 stack (split_f16 on: the opt-in
+    arithmetic) against the fp32 direct-kernel stack (the default) and float64 modules: the split path's
+    error is at most 2x the fp32 path's + 1e-6 of the output scale."""
     from mvs_amd.model import DepthRefinement, FeatureEncoder
     torch.manual_seed(0)
     net, shape = (FeatureEncoder(), (3, 3, 96, 136)) if which == "encoder" else (DepthRefinement(), (2, 4, 40, 56))
@@ -137,9 +137,13 @@ def test_stack_split_path_matches_fp32_path(which, monkeypatch):
     with torch.no_grad():
         ref = net.double()(x.double())
         net = net.float().to(DEV)
+        net.split_f16 = True
         y = net(x.to(DEV)).cpu().double()
-        monkeypatch.setenv("MVS_CONV2D_F16", "0")
+        net.split_f16 = False
         y32 = net(x.to(DEV)).cpu().double()
+        monkeypatch.setenv("MVS_CONV2D_F16", "0")   # the kill switch of the split stack
+        net.split_f16 = True
+        assert torch.equal(net(x.to(DEV)).cpu().double(), y32)
     scale = ref.abs().max().item()
     err, err32 = (y - ref).abs().max().item(), (y32 - ref).abs().max().item()
     assert err <= 2 * err32 + 1e-6 * scale, (err, err32, scale)

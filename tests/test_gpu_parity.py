@@ -73,6 +73,26 @@ def test_assemble_cost_volume_matches_golden(nv):
     _close(cv, z["cv"], atol=1e-6, rtol=1e-6, l2=1e-7)
 
 
+@pytest.mark.parametrize("nv", [3, 6, 10, 12, 14])
+def test_assemble_cost_volume_tiny_values_bit_exact(nv):
+    """costvolume.py:12-14 on warped values down in the subnormal range (variances and means whose
+    quotients by V are subnormal, including exact ties between two subnormals): the HIP variance equals
+    torch CPU's (the oracle's assemble_cost_volume, IEEE division) bit for bit for odd V and for the
+    even non-power-of-two V whose ties need div_views' IEEE fallback (common.h)."""
+    import mvs_oracle
+    from mvs_amd import assemble_cost_volume
+    g = torch.Generator().manual_seed(nv)
+    n = 2 * nv * 8 * 4 * 16 * 16
+    k = torch.randint(0, 1 << 23, (n,), generator=g, dtype=torch.int64).to(torch.int32)
+    sub = k.view(torch.float32) * torch.where(torch.rand(n, generator=g) < 0.5, -1.0, 1.0)   # subnormals
+    tiny = torch.randn(n, generator=g) * 1e-20                                                # squares subnormal
+    warped = torch.where(torch.rand(n, generator=g) < 0.5, sub, tiny).reshape(2 * nv, 8, 4, 16, 16)
+    got = assemble_cost_volume(warped.to(DEV), nv).cpu()
+    want = mvs_oracle.assemble_cost_volume(warped, nv)
+    assert (want.abs() < 1.2e-38).any() and (want != 0).any()   # the case is exercised
+    assert torch.equal(got.view(torch.int32), want.view(torch.int32)), int((got != want).sum())
+
+
 def test_fused_no_worse_than_reference_fp32():
     """GPU vs float64 law is within the reference's own fp32 error vs float64."""
     import mvs_oracle
@@ -349,10 +369,11 @@ def _kept_planes(P, n_est):
     return (order < n_est).numpy()
 
 
-@pytest.mark.parametrize("mode", ["eval", "train"])
-def test_mvsnet_end_to_end(mode):
+@pytest.mark.parametrize("mode,arithmetic", [("eval", "fp32"), ("train", "fp32"), ("eval", "split_f16")])
+def test_mvsnet_end_to_end(mode, arithmetic):
     """MVSNet.forward at config 1 (640x512, D=48): BN eval mode and the test.py:61
-    train-mode-under-no_grad mode, against the oracle forward run on this box's CPU (the oracle
+    train-mode-under-no_grad mode, in the default fp32 arithmetic (and eval mode in the opt-in
+    split-fp16 one), against the oracle forward run on this box's CPU (the oracle
     forward is itself pinned to the reference's golden depth maps in test_oracle.py).
 
       * probability volumes agree to 2e-3 relative (the regulariser amplifies the reference's own
@@ -373,7 +394,7 @@ def test_mvsnet_end_to_end(mode):
     from mvs_amd import warp_and_assemble_cost_volume, extract_depth_map
     z = load_golden("cfg1_e2e.npz")
     D = int(z["d_num"])
-    net = MVSNet(MVSConfig(d_num=D), device=torch.device("cpu"))
+    net = MVSNet(MVSConfig(d_num=D, arithmetic=arithmetic), device=torch.device("cpu"))
     net.load_state_dict(deterministic_state_dict(net.state_dict()))
     net.train() if mode == "train" else net.eval()
     img = torch.from_numpy(np.random.default_rng(int(z["img_seed"])).standard_normal(
@@ -393,9 +414,9 @@ def test_mvsnet_end_to_end(mode):
         g_img = img.to(DEV)
         g_ini_full, g_ref = net(g_img, K, R, T, d_min, d_int, 1, 3)
         feats = net.feature_encoder(g_img)
-        # the benchmarked feed: channel-quad volume + bound words (split-fp16 conv_0_0 in eval mode)
+        # the benchmarked feed: the fp32 channel-quad volume, or the split volume in split-fp16 arithmetic
         cv, d_batch, _ = warp_and_assemble_cost_volume(K, R, T, d_min, d_int, feats, 1, 3, d_num=D,
-                                                       channel_quads=True, split=mode == "eval")
+                                                       channel_quads=True, split=arithmetic == "split_f16")
         g_prob = net.cost_volume_reg(cv)
         g_ini = extract_depth_map(g_prob, d_batch)
     if mode == "eval":
@@ -802,9 +823,9 @@ def test_region_conv_s2_channel_quad_input_is_bit_equal(cout):
 def test_mvsnet_channel_quad_feed_equals_ncdhw_feed():
     """MVSNet.forward's HIP inference feed (channel-quad cost volume into the live regulariser)
     against the same network fed the NCDHW volume: identical depth maps with the exact-fp32
-    conv_0_0 (split_f16 off: the layouts carry the same values and sums); with the split-fp16
-    conv_0_0 (the default) the probabilities agree to fp32 level and the depth maps to 1e-4 outside
-    mask flips."""
+    conv_0_0 (split_f16 off, the default fp32 arithmetic: the layouts carry the same values and sums);
+    with the opt-in split-fp16 regulariser the probabilities agree to fp32 level and the depth maps to
+    1e-4 outside mask flips."""
     from cameras import camera_batch, depth_range
     from mvs_amd.config import MVSConfig
     from mvs_amd.model import MVSNet

@@ -1,4 +1,14 @@
-"""CPU: the fused head's producer-gather rule, checked on the gfx950 code object that ships.
+"""CPU: the fused head's producer rules, checked on the gfx950 code object that ships.
+
+Rule 2 (round 6, the cause of the sporadic corruption of DESIGN.md §3.7): a producer's ring stores
+(``ds_write_b64`` of an item's hi / lo parts) run with NONE of the wave's tap gathers in flight -- an
+``s_waitcnt vmcnt(0)`` since the last ``buffer_load_dwordx4`` -- and complete (``s_waitcnt lgkmcnt(0)``)
+before the wave issues another gather.  With gathers of later items outstanding across the stores,
+lanes 48-63 of a store wrote wrong data in some launches (20 of 20 at the bench geometry); with the
+rule, 0 of 20 at every geometry (tools/dbg/stress_r6.sh).  ``test_ring_stores_with_no_gather_in_flight``
+and its mutation test below.
+
+Rule 1 (round 4):
 
 DESIGN.md §3.7 (hazard 1): a producer wave of ``cv_head_kernel`` must not issue a feature gather
 (``buffer_load_dwordx4``) while one of its own LDS instructions is still outstanding -- under the
@@ -124,3 +134,64 @@ def test_checker_flags_a_build_without_the_wait(tmp_path):
     work.mkdir()
     gathers, _, bad = _check(_disassemble(work, "cv_head_kernelILi3", str(mut)))
     assert gathers > 0 and bad, "the mutant (no explicit wait) passed the check"
+
+
+def _check_stores(asm):
+    """(ring stores checked, violations) of rule 2 over the producer item blocks: every ds_write has
+    vmcnt(0) since the block's last gather, and no gather is issued between a ds_write and the next
+    lgkmcnt(0)."""
+    blocks, cur = [], []
+    for kind, text in _instructions(asm):
+        if kind == "label":
+            blocks.append(cur)
+            cur = []
+        else:
+            cur.append(text)
+    blocks.append(cur)
+    stores = 0
+    bad = []
+    for bi, blk in enumerate(blocks):
+        if not any(t.startswith("v_cvt_pk_f16_f32") for t in blk):
+            continue
+        loads = "block entry"   # the predecessor is not known from the layout
+        store_pending = False
+        for t in blk:
+            op = t.split()[0]
+            if op == "s_waitcnt":
+                if "vmcnt(0)" in t:
+                    loads = "drained"
+                if "lgkmcnt(0)" in t:
+                    store_pending = False
+            elif op == "buffer_load_dwordx4":
+                loads = "in flight"
+                if store_pending:
+                    bad.append((bi, t, "gather issued before the ring store completed"))
+            elif op.startswith("ds_write"):
+                stores += 1
+                store_pending = True
+                if loads != "drained":
+                    bad.append((bi, t, "ring store with gathers " + loads))
+    return stores, bad
+
+
+@pytest.mark.parametrize("V", [2, 3])
+def test_ring_stores_with_no_gather_in_flight(tmp_path, V):
+    stores, bad = _check_stores(_disassemble(tmp_path, "cv_head_kernelILi%d" % V, LIB))
+    assert stores >= 2 * 6, stores   # two stores per unrolled item
+    assert not bad, "ring stores that may run beside gathers: %s" % bad[:5]
+
+
+def test_store_checker_flags_a_build_without_the_fence(tmp_path):
+    """Mutation: csrc/cv_head.hip built alone with -DMVS_HEAD_NO_STORE_FENCE (the vmcnt(0) before the ring
+    stores compiled out) must violate rule 2."""
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    src = os.path.join(REPO, "deep-multiview-depth-estimation_amd", "csrc", "cv_head.hip")
+    mut = tmp_path / "mutant.so"
+    subprocess.run([hipcc, "-O3", "-std=c++17", "-Wno-pass-failed", "--offload-arch=gfx950", "-fPIC", "-shared",
+                    "-DMVS_HEAD_NO_STORE_FENCE", "-o", str(mut), src], check=True, capture_output=True)
+    work = tmp_path / "mut"
+    work.mkdir()
+    stores, bad = _check_stores(_disassemble(work, "cv_head_kernelILi3", str(mut)))
+    assert stores > 0 and bad, "the mutant (no fence before the ring stores) passed the check"

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5 GPU driver: bash tools/gpu_r5.sh <tag> [stages...]   stages: tests smoke bench prof pmc (default all)
+# round 6 GPU driver: bash tools/gpu_r6.sh <tag> [stages...]   stages: tests smoke bench prof pmc (default all)
 #   tests  full GPU suite (+ parity records under $OUT/parity)
 #   smoke  __graft_entry__.smoke()
 #   bench  python bench.py (N=1 defaults) -> $OUT/bench.json
@@ -9,7 +9,7 @@
 #   trace  rocprofv3 kernel stats of one step kind each (TRACES="mode batch views;..."): cfg-2 eval, cfg-2
 #          train-mode BN (test.py:61), cfg-3 eval; per step = over 3 warm-up + 5 timed steps
 # Every GPU step has its own time limit; the script stops at the first failing step.
-cd "${GRAFT_REPO_ROOT:-/root/repo}"; TAG=${1:-r5}; shift; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; TAG=${1:-r6}; shift; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
 STAGES=${*:-tests smoke bench prof pmc}
 has() { case " $STAGES " in *" $1 "*) return 0;; esac; return 1; }
 if has tests; then
@@ -62,13 +62,13 @@ if has stress; then
   echo "stress bn rc=$rc"; grep -E "cfg|differs" $OUT/head_stress_bn.log | head -40; [ $rc -ne 0 ] && exit $rc
 fi
 if has trace; then
-  IFS=';' read -ra TRACES <<< "${TRACES:-eval 4 3;train 4 3;eval 8 5}"
-  for m in "${TRACES[@]}"; do set -- $m
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/tr_$1_v$3" -o run --output-format csv -- \
-      python3 tools/step_trace.py --mode $1 --batch $2 --views $3 --steps 5 > $OUT/tr_$1_v$3.log 2>&1
-    rc=$?; echo "trace $1 v$3 rc=$rc"; grep "step" $OUT/tr_$1_v$3.log | tail -2; [ $rc -ne 0 ] && exit $rc
-    f=$(ls $OUT/tr_$1_v$3/*/run_kernel_stats.csv $OUT/tr_$1_v$3/run_kernel_stats.csv 2>/dev/null | head -1)
-    python3 tools/kstats.py "$f" 8 22
+  IFS=';' read -ra TRACES <<< "${TRACES:-eval 4 3 fp32;train 4 3 fp32;eval 8 5 fp32}"
+  for m in "${TRACES[@]}"; do set -- $m; a=${4:-fp32}; t=tr_$1_v$3_$a
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/$t" -o run --output-format csv -- \
+      python3 tools/step_trace.py --mode $1 --batch $2 --views $3 --arithmetic $a --steps 5 > $OUT/$t.log 2>&1
+    rc=$?; echo "trace $t rc=$rc"; grep "step" $OUT/$t.log | tail -2; [ $rc -ne 0 ] && exit $rc
+    f=$(ls $OUT/$t/*/run_kernel_stats.csv $OUT/$t/run_kernel_stats.csv 2>/dev/null | head -1)
+    python3 tools/kstats.py "$f" 8 24
   done
 fi
 exit 0

@@ -21,10 +21,11 @@ def main():
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--planes", type=int, default=192)
     ap.add_argument("--views", type=int, default=3)
+    ap.add_argument("--arithmetic", choices=("fp32", "split_f16"), default="fp32")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, V, D, H, W = a.batch, a.views, a.planes, 512, 640
-    net = bench.build_model(D, H, W, dev)
+    net = bench.build_model(D, H, W, dev, arithmetic=a.arithmetic)
     if a.mode != "eval":
         net.train()
     inputs = bench.make_inputs(B, V, H, W, 0, dev)
