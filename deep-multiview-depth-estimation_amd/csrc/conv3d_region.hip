@@ -23,6 +23,8 @@
 // w[tap][co][ci] (ops.py transposes nn.Conv3d / nn.ConvTranspose3d's layouts).  Products are summed
 // per tap over channels in a fixed order -- MIOpen's kernels sum in other orders; same products,
 // fp32 rounding-level differences.
+#include <cstdlib>
+
 #include "launchers.h"
 #include "packed.h"
 #include "split.h"
@@ -73,24 +75,25 @@ __device__ inline void store_out(float* __restrict__ y, const Geo& g, int b, int
 // a template parameter, so the K loop has no per-load layout branches and (S1 / S2: no parity
 // classes) unrolls into one basic block the scheduler can software-pipeline (loads of later taps
 // issued under the MFMAs of earlier ones)
-template <int MODE, int CI, int CO, int RB, int QM = 0>
-__global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
+// CLS (T2 only): the parity class (pz, py, px) = bits (2, 1, 0) as a COMPILE-TIME constant, so the tap
+// loops unroll to exactly the class's 1-8 taps in one basic block (the loads of every tap issued ahead of
+// the MFMAs); the kernel below dispatches on blockIdx.y.  -1 (S1 / S2): no classes.
+template <int MODE, int CI, int CO, int RB, int QM, int CLS>
+__device__ __forceinline__ void region_conv(
     const float* __restrict__ x, const float* __restrict__ x2, const float* __restrict__ w,
     float* __restrict__ y, const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
-    const float* __restrict__ bn_mean, Geo g) {
+    const float* __restrict__ bn_mean, const Geo& g) {
   constexpr int NB = CO / 16;          // column blocks
   static_assert(CI % 16 == 0 && CO % 16 == 0, "channel counts in multiples of 16");
+  static_assert((MODE == kT2) == (CLS >= 0), "parity classes: transposed convolutions");
   const int lane = (int)threadIdx.x & 63;
   const int m = lane & 15, kq = lane >> 4;   // MFMA row / K index of this lane's A value
   const int b = (int)blockIdx.z;
 
   // ---- rows of this wave: parity class (T2) or the whole region ----
-  int cf[3], cn[3], par[3] = {0, 0, 0};
+  int cf[3], cn[3];
+  constexpr int par[3] = {CLS >= 0 ? (CLS >> 2) & 1 : 0, CLS >= 0 ? (CLS >> 1) & 1 : 0, CLS >= 0 ? CLS & 1 : 0};
   if constexpr (MODE == kT2) {
-    const int cls = (int)blockIdx.y;
-    par[0] = (cls >> 2) & 1;
-    par[1] = (cls >> 1) & 1;
-    par[2] = cls & 1;
 #pragma unroll
     for (int d = 0; d < 3; ++d) class_dim(g.o0[d], g.on[d], g.pad[d], par[d], cf[d], cn[d]);
   } else {
@@ -279,6 +282,25 @@ __global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
 }
 
 template <int MODE, int CI, int CO, int RB, int QM = 0>
+__global__ __launch_bounds__(kBlock) void conv3d_region_kernel(
+    const float* __restrict__ x, const float* __restrict__ x2, const float* __restrict__ w,
+    float* __restrict__ y, const float* __restrict__ bn_scale, const float* __restrict__ bn_shift,
+    const float* __restrict__ bn_mean, Geo g) {
+  if constexpr (MODE == kT2) {
+    switch (blockIdx.y) {   // workgroup-uniform
+#define MVS_T2_CLASS(c) \
+  case c: region_conv<MODE, CI, CO, RB, QM, c>(x, x2, w, y, bn_scale, bn_shift, bn_mean, g); break;
+      MVS_T2_CLASS(0) MVS_T2_CLASS(1) MVS_T2_CLASS(2) MVS_T2_CLASS(3)
+      MVS_T2_CLASS(4) MVS_T2_CLASS(5) MVS_T2_CLASS(6) MVS_T2_CLASS(7)
+#undef MVS_T2_CLASS
+      default: break;
+    }
+  } else {
+    region_conv<MODE, CI, CO, RB, QM, -1>(x, x2, w, y, bn_scale, bn_shift, bn_mean, g);
+  }
+}
+
+template <int MODE, int CI, int CO, int RB, int QM = 0>
 void launch_mode(const float* x, const float* x2, const float* w, float* y, const float* sc, const float* sh,
                  const float* mu, int B, const Geo& g, hipStream_t s) {
   const int classes = MODE == kT2 ? 8 : 1;
@@ -293,12 +315,175 @@ void launch_mode(const float* x, const float* x2, const float* w, float* y, cons
                      g);
 }
 
+// ---- stride-1 convolutions with LDS-staged operands (conv_k_1, model.py:104-113) ----
+// The per-lane kernel above fetches each input voxel once per tap through L1 / L2 (27 times) and keeps
+// at most RB row blocks of loads in flight: latency-bound (conv_1_1 at ~50 TF/s in the cfg-2 step).
+// Here a workgroup (4 waves) owns a 16 (x) x 4 (y) x TZ (z) block of outputs; its input block, 18 x 6 x
+// (TZ + 2) voxels with all CI channels, is loaded once into LDS (one CI x 4-byte record per voxel, 16-byte
+// chunks of 4 channels XOR-swizzled by voxel: the 16 lanes of an MFMA row group -- 16 consecutive
+// voxels, one chunk -- and the ds_read_b128 lane groups hit distinct bank groups).  Wave w owns column
+// block w % NB (16 output channels) and 8 row blocks (16 x-voxels of one (z, y) row each); every weight
+// float4 (L1 / L2) feeds 8 row blocks x 4 MFMAs, every A float4 comes from LDS.  Products and their
+// order per accumulator are the per-lane kernel's ((tz, ty), channel block, tx, K-step s): bit-equal.
+template <int CI>
+struct S1TileF {
+  static constexpr int TZ = CI == 16 ? 8 : (CI == 32 ? 4 : 2);
+  static constexpr int PX = 18, PY = 6, PZ = TZ + 2, PV = PX * PY * PZ;
+  static constexpr int NCH = CI / 4;     // 16-byte chunks (4 channels) per voxel record
+  static constexpr int REC = CI * 4;     // bytes per voxel record
+  static constexpr int LDS = PV * REC;   // 69,120 / 82,944 / 110,592 B
+};
+
+template <int CI>
+__device__ inline int s1f_off(int v, int c) {   // byte offset of chunk c of voxel v (swizzled)
+  constexpr int NCH = CI / 4;
+  return v * (CI * 4) + ((c ^ (((v * NCH) >> 3) % NCH)) << 4);
+}
+
+template <int CI, int CO>
+__global__ __launch_bounds__(kBlock) void conv3d_s1_lds_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ y,
+    const float* __restrict__ bn_scale, const float* __restrict__ bn_shift, const float* __restrict__ bn_mean, Geo g,
+    int tiles_x, int tiles_y, int tiles_z) {
+  using T = S1TileF<CI>;
+  constexpr int NB = CO / 16;
+  constexpr int RB = 8;   // row blocks per wave: 4 TZ (z, y) rows x NB column blocks / 4 waves
+  static_assert(T::TZ * NB == RB && CI == CO, "tile shapes");
+  __shared__ __attribute__((aligned(16))) char lds[T::LDS];
+
+  int t = xcd_work_id((int)blockIdx.x, (int)gridDim.x);
+  if (t >= tiles_x * tiles_y * tiles_z) return;   // workgroup-uniform, before the barrier
+  const int tx0 = (t % tiles_x) * 16;
+  t /= tiles_x;
+  const int ty0 = (t % tiles_y) * 4;
+  t /= tiles_y;
+  const int tz0 = t * T::TZ;
+  const int b = (int)blockIdx.y;
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m = lane & 15, kq = lane >> 4;
+
+  // ---- stage the input block: items (voxel, chunk), chunk fastest (coalesced channels-last loads);
+  // voxels outside the input region read 0 (the convolution's zero padding outside the volume).  Each
+  // batch's loads are all complete before its LDS stores are issued (no load in flight beside an LDS
+  // store: DESIGN.md §3.7) ----
+  {
+    constexpr int NIT = T::PV * T::NCH, PER = (NIT + kBlock - 1) / kBlock, BATCH = 8;
+    const size_t rvol = (size_t)g.in[0] * g.in[1] * g.in[2];
+    const Rsrc rs = make_rsrc(x + (size_t)b * rvol * CI, (uint32_t)(rvol * CI * 4));
+#pragma unroll
+    for (int k0 = 0; k0 < PER; k0 += BATCH) {
+      f4v v4[BATCH];
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int e = tid + kBlock * (k0 + k);
+        const int q = e % T::NCH, v = e / T::NCH;
+        const int px = v % T::PX, py = (v / T::PX) % T::PY, pz = v / (T::PX * T::PY);
+        const int rx = g.o0[2] + tx0 - 1 + px - g.i0[2], ry = g.o0[1] + ty0 - 1 + py - g.i0[1],
+                  rz = g.o0[0] + tz0 - 1 + pz - g.i0[0];
+        const bool ok = k0 + k < PER && e < NIT && rx >= 0 && rx < g.in[2] && ry >= 0 && ry < g.in[1] && rz >= 0 &&
+                        rz < g.in[0];
+        v4[k] = ld4(rs, ok ? (uint32_t)((((size_t)rz * g.in[1] + ry) * g.in[2] + rx) * CI + 4 * q) * 4u : kOob, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int e = tid + kBlock * (k0 + k);
+        if (k0 + k >= PER || e >= NIT) continue;
+        *reinterpret_cast<f4v*>(lds + s1f_off<CI>(e / T::NCH, e % T::NCH)) = v4[k];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __syncthreads();
+
+  // ---- this wave: column block nb, row blocks rg * 8 .. + 7 of the tile's 4 TZ (z, y) rows ----
+  const int nb = wave % NB, rg = wave / NB;
+  f4v_t acc[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) acc[r] = f4v_t{0.0f, 0.0f, 0.0f, 0.0f};
+  const float* wn = w + (size_t)(nb * 16 + m) * CI + 4 * kq;   // this lane's weight row, channel offset 4 kq
+  // A float4s of one (tap, channel block) for the wave's 8 row blocks (buffer tx of three), read one
+  // step ahead; the weight float4s of a (tap row, channel block) one iteration ahead
+  f4v_t a[3][RB];
+  auto lda = [&](int tr, int tx, int cb, f4v_t (&dst)[RB]) {
+    const int tz = tr / 3, ty = tr % 3;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int rbi = rg * RB + r, zz = rbi >> 2, yy = rbi & 3;
+      const int v = ((zz + tz) * T::PY + (yy + ty)) * T::PX + (m + tx);
+      dst[r] = *reinterpret_cast<const f4v_t*>(lds + s1f_off<CI>(v, cb * 4 + kq));
+    }
+  };
+  auto ldw = [&](int tr, int cb, f4v_t (&bw)[3]) {
+#pragma unroll
+    for (int tx = 0; tx < 3; ++tx)
+      bw[tx] = *reinterpret_cast<const f4v_t*>(wn + (size_t)((tr * 3 + tx) * CO) * CI + cb * 16);
+  };
+  constexpr int CB = CI / 16, NIT = 9 * CB;   // iterations (tap row, channel block)
+  f4v_t bw[3], bn_[3];
+  ldw(0, 0, bw);
+  lda(0, 0, 0, a[0]);
+#pragma unroll 1
+  for (int it = 0; it < NIT; ++it) {
+    const int tr = it / CB, cb = it % CB;
+    const bool more = it + 1 < NIT;
+    const int tr1 = (it + 1) / CB, cb1 = (it + 1) % CB;
+    if (more) ldw(tr1, cb1, bn_);
+#pragma unroll
+    for (int tx = 0; tx < 3; ++tx) {
+      if (tx < 2) lda(tr, tx + 1, cb, a[tx + 1]);
+      else if (more) lda(tr1, 0, cb1, a[0]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+          acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[tx][r][s], bw[tx][s], acc[r], 0, 0, 0);
+    }
+#pragma unroll
+    for (int tx = 0; tx < 3; ++tx) bw[tx] = bn_[tx];
+  }
+
+  // ---- epilogue: acc[r][i] = (x = tx0 + 4 kq + i, channel nb * 16 + m) of row block r ----
+  const int co = nb * 16 + m;
+  const float sc = bn_scale ? bn_scale[co] : 1.0f, sh = bn_scale ? bn_shift[co] : 0.0f,
+              mu = bn_scale ? bn_mean[co] : 0.0f;
+  float vmax = 0.0f;
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const int rbi = rg * RB + r, zz = rbi >> 2, yy = rbi & 3;
+    if (tz0 + zz >= g.on[0] || ty0 + yy >= g.on[1]) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (tx0 + 4 * kq + i >= g.on[2]) continue;
+      float v = acc[r][i];
+      if (bn_scale) v = fmaxf((v - mu) * sc + sh, 0.0f);
+      vmax = fmaxf(vmax, fabsf(v));
+      store_out(y, g, b, co, tz0 + zz, ty0 + yy, tx0 + 4 * kq + i, CO, v);
+    }
+  }
+  if (g.y_bound) bound_update(g.y_bound, vmax);
+}
+
+template <int CI>
+void launch_s1_lds(const float* x, const float* w, float* y, const float* sc, const float* sh, const float* mu,
+                   int B, const Geo& g, hipStream_t s) {
+  const int tx = (g.on[2] + 15) / 16, ty = (g.on[1] + 3) / 4, tz = (g.on[0] + S1TileF<CI>::TZ - 1) / S1TileF<CI>::TZ;
+  const int per = tx * ty * tz;
+  const dim3 grid((unsigned)((per + 7) / 8 * 8), (unsigned)B);   // XCD remap: multiple of 8
+  hipLaunchKernelGGL((conv3d_s1_lds_kernel<CI, CI>), grid, dim3(kBlock), 0, s, x, w, y, sc, sh, mu, g, tx, ty, tz);
+}
+
 }  // namespace
 
 int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const float* x2, const float* w,
                          float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on, const int* i0,
                          const int* in, const int* pad, const float* bn_scale, const float* bn_shift,
-                         const float* bn_mean, hipStream_t s, const uint32_t* absmax, uint32_t* y_bound) {
+                         const float* bn_mean, hipStream_t s, const uint32_t* absmax, uint32_t* y_bound,
+                         bool per_lane) {
   Geo g;
   g.y_bound = y_bound;
   g.out_cf = out_cf ? 1 : 0;
@@ -311,6 +496,19 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
     g.i0[d] = i0 ? i0[d] : 0;
     g.in[d] = in ? in[d] : n[d];
     g.pad[d] = pad ? pad[d] : 1;
+  }
+  // stride-1 convolutions of one region tensor: the LDS-staged kernel (bit-equal) only with
+  // MVS_FP32_S1_LDS=1 -- measured slower at cfg 2 (conv_1_1 0.42 against 0.34 ms alone, the fp32 eval step
+  // 6.60 against 5.94 ms: its 69-110 KB tiles leave 1-2 waves per SIMD and crowd out the concurrent
+  // VALU conv_0_0; gpurun_out r6e)
+  static const bool s1_lds = [] {
+    const char* e = getenv("MVS_FP32_S1_LDS");
+    return e && e[0] == '1';
+  }();
+  if (mode == kS1 && !x2 && CI == CO && !per_lane && s1_lds) {
+    if (CI == 16) return launch_s1_lds<16>(x, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
+    if (CI == 32) return launch_s1_lds<32>(x, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
+    if (CI == 64) return launch_s1_lds<64>(x, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
   }
 // two row blocks per wave (one and four measured slower on the cfg-2 eval and train-mode steps)
 #define MVS_REGION_CASE(MD, A, C)                                                       \
@@ -330,6 +528,15 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
   // deconv_2_0 (32 -> 16)
   MVS_REGION_S2(32, 16) MVS_REGION_S2(32, 32) MVS_REGION_S2(32, 64)
   MVS_REGION_CASE(kS1, 16, 16) MVS_REGION_CASE(kS1, 32, 32) MVS_REGION_CASE(kS1, 64, 64)
+  // transposed: row blocks per wave MVS_T2_RB (2 or 4)
+  static const int t2_rb = [] {
+    const char* e = getenv("MVS_T2_RB");
+    return e && e[0] == '4' ? 4 : 2;
+  }();
+  if (mode == kT2 && t2_rb == 4) {
+    if (CI == 64 && CO == 32) return launch_mode<kT2, 64, 32, 4>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
+    if (CI == 32 && CO == 16) return launch_mode<kT2, 32, 16, 4>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
+  }
   MVS_REGION_CASE(kT2, 64, 32) MVS_REGION_CASE(kT2, 32, 16)
 #undef MVS_REGION_CASE
 #undef MVS_REGION_S2

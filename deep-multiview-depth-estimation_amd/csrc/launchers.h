@@ -137,7 +137,8 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
                          float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on, const int* i0,
                          const int* in,
                          const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                         hipStream_t s, const uint32_t* absmax = nullptr, uint32_t* y_bound = nullptr);
+                         hipStream_t s, const uint32_t* absmax = nullptr, uint32_t* y_bound = nullptr,
+                         bool per_lane = false);
 // the S1 / T2 region convolutions on split-fp16 MFMA (conv3d_region_split.hip); K-32 weight blocks
 // channel_ops.hip: train-mode BatchNorm parameters (+ running statistics) from the batch sums
 void launch_bn_train_params(const double* sums, int C, double count, const double* bu, const double* bcnt, int Cp,

@@ -705,11 +705,48 @@ class CostVolumeReg(nn.Module):
 
 
 _SIDE_STREAMS = {}
+# the lane of MVSNet's sample-pipelined eval forward that is issuing kernels (0: none): every lane gets
+# its own side streams, so two lanes' branches never serialise on one stream
+_LANE = [0]
 
 
 def _side_stream(device, which=0):
-    """Extra HIP streams per device for independent branches of the inference step."""
-    key = (torch.device(device).index, which)
+    """Extra HIP streams per device (and pipeline lane) for independent branches of the inference step."""
+    key = (torch.device(device).index, which, _LANE[0])
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = torch.cuda.Stream(device)
+    return _SIDE_STREAMS[key]
+
+
+_UNIFORM = {}
+
+
+def _uniform_depths(d_min, d_int):
+    """Every sample has the same (d_min, d_int) -- DTU's 425 / 2.5 for every camera, and d_int = 1 in
+    train.py:95 / test.py:84.  Only then is a chunk of samples' forward the whole batch's: image i uses
+    the depth planes of sample i mod B (homography.py:24-26, view-major tiling), which changes with the
+    chunk's B unless all rows are equal.  A device tensor's answer is cached per storage and version (one
+    device-to-host read per new tensor)."""
+    out = True
+    for t in (d_min, d_int):
+        if t.numel() <= 1:
+            continue
+        if t.device.type == "cpu":
+            out = out and bool((t == t.reshape(-1)[0]).all())
+            continue
+        key = (t.data_ptr(), t._version, tuple(t.shape), str(t.device))
+        hit = _UNIFORM.get(key)
+        if hit is None:
+            if len(_UNIFORM) > 256:
+                _UNIFORM.clear()
+            hit = _UNIFORM[key] = bool((t == t.reshape(-1)[0]).all().item())
+        out = out and hit
+    return out
+
+
+def _lane_stream(device, lane):
+    """The stream of pipeline lane ``lane`` (MVSNet._forward_pipelined)."""
+    key = (torch.device(device).index, "lane", lane)
     if key not in _SIDE_STREAMS:
         _SIDE_STREAMS[key] = torch.cuda.Stream(device)
     return _SIDE_STREAMS[key]
@@ -1011,6 +1048,8 @@ class MVSNet(nn.Module):
                            list(self.cost_volume_reg.parameters()) +
                            list(self.depthmap_refine.parameters()))
         self.set_arithmetic(self.cfg.arithmetic)
+        # eval inference over B >= 2 samples: chunks of samples issued on their own streams (forward)
+        self.pipeline_chunks = int(os.environ.get("MVS_PIPELINE_CHUNKS", "2"))
 
     def set_arithmetic(self, arithmetic):
         """"fp32" (the reference's numerics: every HIP layer in exact fp32) or "split_f16" (opt-in: the
@@ -1026,6 +1065,52 @@ class MVSNet(nn.Module):
         return self
 
     def forward(self, nn_input, K_batch, R_batch, T_batch, d_min, d_int, batch_size, n_views):
+        if self._pipeline_ok(nn_input, d_min, d_int, batch_size):
+            return self._forward_pipelined(nn_input, K_batch, R_batch, T_batch, d_min, d_int, batch_size, n_views)
+        return self._forward_one(nn_input, K_batch, R_batch, T_batch, d_min, d_int, batch_size, n_views)
+
+    def _pipeline_ok(self, nn_input, d_min, d_int, batch_size):
+        """The sample-pipelined eval forward applies: HIP fp32 inference with every module in eval mode
+        (samples are then independent: eval BatchNorm is elementwise), at least two samples, and
+        pipeline_chunks > 1 (MVS_PIPELINE_CHUNKS; 1 = off)."""
+        k = self.pipeline_chunks
+        return (k > 1 and int(batch_size) >= 2 and _hip_inference(nn_input) and not self.training
+                and not any(m.training for m in self.modules())
+                and all(t.numel() == 1 or t.shape[0] == int(batch_size) for t in (d_min, d_int))
+                and _uniform_depths(d_min, d_int))
+
+    def _forward_pipelined(self, nn_input, K_batch, R_batch, T_batch, d_min, d_int, batch_size, n_views):
+        """forward over the batch in ``pipeline_chunks`` chunks of samples, each issued on its own stream
+        (lane): one chunk's encoder and cost volume (VALU / HBM-store bound) run beside another chunk's
+        regulariser (matrix cores), instead of the whole batch's phases one after another.  Every kernel of
+        the eval forward computes each sample independently, so the depth maps are bit-identical to the
+        one-stream forward (tests/test_gpu_parity.py::test_pipelined_forward_is_bit_identical)."""
+        B, V = int(batch_size), int(n_views)
+        k = min(self.pipeline_chunks, B)
+        cuts = [B * i // k for i in range(k + 1)]
+        device = nn_input.device
+        main = torch.cuda.current_stream(device)
+        per = lambda t, b0, b1: t if t.numel() == 1 else t[b0:b1]
+        outs = []
+        for i in range(k):
+            b0, b1 = cuts[i], cuts[i + 1]
+            st = _lane_stream(device, i)
+            st.wait_stream(main)
+            _LANE[0] = i + 1
+            try:
+                with torch.cuda.stream(st):
+                    outs.append((st,) + self._forward_one(
+                        nn_input[b0 * V:b1 * V], K_batch[b0 * V:b1 * V], R_batch[b0 * V:b1 * V],
+                        T_batch[b0 * V:b1 * V], per(d_min, b0, b1), per(d_int, b0, b1), b1 - b0, V))
+            finally:
+                _LANE[0] = 0
+        for st, ini, ref in outs:
+            main.wait_stream(st)
+            ini.record_stream(main)
+            ref.record_stream(main)
+        return torch.cat([o[1] for o in outs]), torch.cat([o[2] for o in outs])
+
+    def _forward_one(self, nn_input, K_batch, R_batch, T_batch, d_min, d_int, batch_size, n_views):
         c = self.cfg
         device = nn_input.device
         feature_maps = self.feature_encoder(nn_input)

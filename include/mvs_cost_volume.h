@@ -471,15 +471,18 @@ int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch,
  * cost volume, re-formed to fp32 on load as (hi + lo) 2^-e (2^-22 of each element), x_absmax its bound
  * words (DEVICE; NULL otherwise).  y_bound: NULL, or MVS_BOUND_WORDS words (DEVICE, zeroed by the
  * caller) raised to max|y| (see mvs_conv3d_region_split_fwd).  Eval-mode inference only; products
- * summed in the order (tap, c_in) -- MIOpen sums them in other orders (fp32 rounding-level differences). */
+ * summed in the order (tap, c_in) -- MIOpen sums them in other orders (fp32 rounding-level differences).
+ * MVS_CONV_S1 with c_in = c_out and no x2 runs an LDS-staged kernel (each input voxel loaded once per
+ * 16 x 4 x TZ output tile), bit-identical to the per-lane-operand kernel that flags MVS_CONV_PER_LANE
+ * (below) selects. */
 int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, const float* weight, float* y,
                           int batch, int c_in, int c_out, const int* dims, const int* out_origin,
                           const int* out_size, const int* in_origin, const int* in_size,
                           const int* pad, const float* bn_scale, const float* bn_shift,
                           const float* bn_mean, const unsigned* x_absmax, unsigned* y_bound, void* stream);
 
-/* flag of mvs_conv3d_region_split_fwd: run the per-lane-operand kernel even where the LDS-staged
- * stride-1 kernel applies (the two are bit-identical; tests and A/B timing) */
+/* flag of mvs_conv3d_region_split_fwd and mvs_conv3d_region_fwd: run the per-lane-operand kernel even
+ * where an LDS-staged kernel applies (the two are bit-identical; tests and A/B timing) */
 #define MVS_CONV_PER_LANE 32
 
 /* Bound words of a region tensor: MVS_BOUND_WORDS uint32 (8 KiB) holding maxima of |v| as fp32 bit

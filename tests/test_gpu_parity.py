@@ -455,6 +455,53 @@ def test_mvsnet_end_to_end(mode, arithmetic):
             np.median(out), np.percentile(out, 99))
 
 
+@pytest.mark.parametrize("arithmetic", ["fp32", "split_f16"])
+def test_pipelined_forward_is_bit_identical(arithmetic):
+    """MVSNet's sample-pipelined eval forward (chunks of samples on their own streams, pipeline_chunks 2
+    and 3 of B = 5) returns the one-stream forward's depth maps bit for bit: every eval kernel computes
+    each sample independently.  Also the first call after a weight change (the derived-weight caches are
+    formed on one lane and read on the others).  With per-sample depth ranges (d_min / d_int differing:
+    the homography.py:24-26 i mod B plane tiling then depends on the whole batch) it does not pipeline."""
+    from cameras import camera_batch, depth_range
+    from mvs_amd.config import MVSConfig
+    from mvs_amd.model import MVSNet
+    B, V, D, H, W = 5, 3, 32, 256, 320
+    torch.manual_seed(1)
+    net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W, arithmetic=arithmetic)).to(DEV).eval()
+    K, R, T = camera_batch(B, V, H // 4, W // 4)
+    d_min, d_int = depth_range(B, d_int=2.5)
+    img = torch.randn(B * V, 3, H, W, generator=torch.Generator().manual_seed(9)).to(DEV)
+    K, R, T, d_min, d_int = (t.to(DEV) for t in (K, R, T, d_min, d_int))
+    import mvs_amd.model as model_mod
+    lanes = []
+    orig = model_mod.MVSNet._forward_one
+
+    def spy(self, *a):
+        lanes.append(model_mod._LANE[0])
+        return orig(self, *a)
+    with torch.no_grad():
+        net.pipeline_chunks = 1
+        ref = net(img, K, R, T, d_min, d_int, B, V)
+        model_mod.MVSNet._forward_one = spy
+        try:
+            for chunks in (2, 3):
+                net.pipeline_chunks = chunks
+                for p in net.cost_volume_reg.conv_1_1.parameters():
+                    p.mul_(1.0)   # a version bump: the derived weights are formed again, on a lane
+                lanes.clear()
+                got = net(img, K, R, T, d_min, d_int, B, V)
+                torch.cuda.synchronize()
+                assert lanes == list(range(1, chunks + 1)), lanes
+                assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), chunks
+            # per-sample depth ranges: one stream
+            dm, di = (t.to(DEV) for t in depth_range(B, distinct=True))
+            lanes.clear()
+            net(img, K, R, T, dm, di, B, V)
+            assert lanes == [0], lanes
+        finally:
+            model_mod.MVSNet._forward_one = orig
+
+
 def test_depth_sharded_single_rank_equals_model():
     """mvs_amd.depth_shards at world size 1 (one GPU here; N > 1 is covered by the gloo test and
     the driver's multi-GPU bench) reproduces MVSNet.forward bit for bit (exact-fp32 conv_0_0 on both:
@@ -659,6 +706,44 @@ def _bn_params(c, g):
 def _bn_relu(y, sc, sh, mu):
     v = lambda t: t.view(1, -1, 1, 1, 1).to(y)
     return torch.relu((y - v(mu)) * v(sc) + v(sh))
+
+
+@pytest.mark.parametrize("c,n,ncdhw,bn", [(16, (24, 20, 26), False, True), (32, (24, 20, 26), True, True),
+                                         (64, (24, 20, 26), False, False), (16, (192, 128, 160), True, True),
+                                         (32, (192, 128, 160), False, True), (64, (192, 128, 160), False, True)])
+def test_region_s1_lds_kernel_bit_equal_to_per_lane(c, n, ncdhw, bn):
+    """The LDS-staged stride-1 region convolution (conv3d_s1_lds_kernel: the fp32 path's conv_k_1) gives the
+    per-lane-operand kernel's (MVS_CONV_PER_LANE) outputs bit for bit -- same products, same order per
+    accumulator -- and the same bound words, at the live regions of a cfg-1-like and of the cfg-2 volume
+    (level 1 / 2 / 3 regions: ragged 16 x 4 x TZ tiles in every dim), channels-last and channels-first."""
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _grow, _tconv_input_region
+    from mvs_amd.ops import bound_words, conv3d_region
+    pad = pad_outpad(*n)[0]
+    full = tuple((0, d - 1) for d in n)
+    reg = _tconv_input_region(full, n, pad)
+    for _ in range({16: 0, 32: 1, 64: 2}[c]):   # level 1 / 2 / 3 region (B, C2, C3)
+        reg = _tconv_input_region(reg, n, pad)
+    halo = _grow(reg, n, 1)
+    org = lambda r: [lo for lo, _ in r]
+    size = lambda r: [hi - lo + 1 for lo, hi in r]
+    g = torch.Generator().manual_seed(c + n[0])
+    x = torch.randn([2] + size(halo) + [c], generator=g).to(DEV)
+    w27 = (torch.randn(27, c, c, generator=g) * 0.1).to(DEV)
+    bnp = [t.to(DEV) for t in _bn_params(c, g)] if bn else [None] * 3
+    with torch.no_grad():
+        outs = []
+        for per_lane in (False, True):
+            yb = bound_words(1, DEV)[0]
+            y = conv3d_region(x, None, w27, 0, list(n), org(reg), size(reg), org(halo), size(halo), None, *bnp,
+                              out_ncdhw=ncdhw, y_bound=yb, per_lane=per_lane)
+            outs.append((y, yb))
+        torch.cuda.synchronize()
+    (y, yb), (yp, ybp) = outs
+    assert torch.equal(y, yp), (y - yp).abs().max().item()
+    # the bound (the maximum over the slot words; which slot holds it depends on the wave mapping)
+    bound = lambda t: float(t.cpu().numpy().view(np.float32).max())
+    assert bound(yb) == bound(ybp) == y.abs().max().item()
 
 
 @pytest.mark.parametrize("mode,cin,cout,ncdhw", [(1, 32, 16, False), (1, 32, 32, False), (1, 32, 64, False),
