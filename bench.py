@@ -98,24 +98,31 @@ def parse():
     ap.add_argument("--no-train-step", action="store_true",
                     help="skip the train.py step field (autograd through the full-volume regulariser; "
                          "timed by default at N=1)")
+    ap.add_argument("--dist-init", action="store_true",
+                    help="create the RCCL process group even at world size 1 (exercises the nccl code path)")
     ap.add_argument("--conv-search", choices=("on", "off"), default="off",
                     help="torch.backends.cudnn.benchmark (MIOpen find) for the regulariser convs")
     return ap.parse_args()
 
 
 def init_dist(args):
+    """One process per GPU: an RCCL ("nccl") process group when WORLD_SIZE > 1, or with --dist-init at
+    world size 1 (the RCCL code path of --mode dshard on one GPU), created before any other GPU work."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or args.dist_init:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, torch.device("cuda", local)
 
 
 def barrier(world):
-    if world > 1:
+    if world > 1 or (dist.is_available() and dist.is_initialized()):
         dist.barrier()
     torch.cuda.synchronize()
 
@@ -512,9 +519,10 @@ def conv0_flops(B, D, h, w):
     return float(B) * D * h * w * 8 * 32 * 27 * 2
 
 
-def conv0_traffic(tag):
-    """PMC HBM bytes per fp32 conv_0_0 launch (profiles/conv0_traffic_<tag>.json, rocprofv3 --pmc), or None."""
-    path = os.path.join(REPO, "profiles", "conv0_traffic_%s.json" % tag)
+def conv0_traffic(tag, kind="conv0"):
+    """PMC HBM bytes per fp32 conv_0_0 (kind "conv0") or fused fp32 head ("conv_head_fp32") launch
+    (profiles/<kind>_traffic_<tag>.json, rocprofv3 --pmc), or None."""
+    path = os.path.join(REPO, "profiles", "%s_traffic_%s.json" % (kind, tag))
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -747,13 +755,14 @@ def main():
     tag = "b%dv%dd%dh%dw%d" % (B, V, d_count, h, w)
     traffic = load_traffic(tag)
     conv0_ms = max_over_ranks(step_k["conv_0_0"], world, device) if "conv_0_0" in step_k else None
+    head32_ms = max_over_ranks(step_k["conv_head"], world, device) if "conv_head" in step_k else None
     split = result.get("split_f16")
     head_ms = split["step_kernel_ms"].get("split_head") if split else None
     if head_ms is not None:
         head_ms = max_over_ranks(head_ms, world, device)
 
     if rank != 0:
-        if world > 1:
+        if dist.is_initialized():
             dist.destroy_process_group()
         return
     out = {
@@ -802,7 +811,30 @@ def main():
                                "_c4" if store == "c4" else ""),
                      "op_GBps": alg / (op_ms * 1e-3) / 1e9},
     }
-    if conv0_ms is not None:
+    if head32_ms is not None:
+        # the fp32 step's dominant kernel: conv_0_0 (model.py:101, whole volume) + BN_0 + ReLU on the fp32 VALU
+        # and conv_1_0 (model.py:103, 32 -> 16 stride 2 on its live region) + BN_1 + ReLU on the f32-input
+        # matrix cores in ONE kernel over the fp32 channel-quad volume (ops.conv_head_fp32)
+        hw_ = head_work(B, V, D, h, w, "split_head")
+        fl = hw_["alg_flops"]
+        tf = fl / (head32_ms * 1e-3) / 1e12
+        out["roofline"] = {
+            "bound": "mfma", "achieved": tf, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s", "frac": tf / MFMA_F32_PEAK_TFS,
+            "traffic": conv0_traffic(tag, "conv_head_fp32"),
+            "kernel": "conv3d_k3_narrow_kernel<8, wino_z, C1> (conv_0_0 fp32 VALU + conv_1_0 fp32 MFMA)",
+            "kernel_ms": head32_ms, "flops_per_launch": fl,
+            "timing": "HIP events around each launch inside the %d timed steps (on its side stream, concurrent "
+                      "with the region convolutions)" % args.steps,
+            "flops": "useful fp32 convolution flops: conv_0_0 B*D*h*w x 8 x 32 x 27 x 2 + conv_1_0 (its live-region "
+                     "windows) x 16 x 32 x 27 x 2 (the direct convolutions'; the depth-Winograd conv_0_0 executes 2/3 "
+                     "of its multiplies) against the fp32 compute peak: 157.3 TF is both the f32 VALU rate and the "
+                     "f32-input MFMA rate (MI355X_MICROARCH.md), so 'mfma' names the fp32 compute roof (the two "
+                     "pipes co-issue, so the kernel's own ceiling is above it)",
+            "regions": hw_["regions"],
+            "hbm": {"alg_bytes_per_launch": 4.0 * B * D * h * w * (32 + 8),
+                    "GBps": 4.0 * B * D * h * w * 40 / (head32_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                    "note": "the fp32 cost volume in once, y0 out once (y1 is 1/16 of y0's bytes)"}}
+    elif conv0_ms is not None:
         # the fp32 step's dominant kernel: conv_0_0 (model.py:101, 32 -> 8 over the whole volume + BN_0 +
         # ReLU) on the fp32 VALU kernel, concurrent with the region convolutions on the fp32 matrix cores
         fl = conv0_flops(B, D, h, w)
@@ -901,7 +933,7 @@ def main():
     else:
         out["cpu_baseline"] = None
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

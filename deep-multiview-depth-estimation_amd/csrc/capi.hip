@@ -594,6 +594,34 @@ int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, 
   return lc.status();
 }
 
+int mvs_conv_head_fp32_fwd(const float* cv4, int batch, int d, int h, int w, const float* w0_wz,
+                           const float* bn0_scale, const float* bn0_shift, const float* bn0_mean, const float* w1,
+                           const float* w1_pass, const float* bn1_scale, const float* bn1_shift,
+                           const float* bn1_mean, const int* pad, const int* y1_origin, const int* y1_size,
+                           float* y0, float* y1, void* stream, void* ev0, void* ev1) {
+  if (!cv4 || !w0_wz || !w1 || !w1_pass || !y0 || !y1 || !pad || !y1_origin || !y1_size || batch <= 0 || d <= 0 ||
+      h <= 0 || w <= 0)
+    return MVS_ERR_INVALID_ARGUMENT;
+  if (((uintptr_t)cv4 | (uintptr_t)w1 | (uintptr_t)w1_pass) & 15u) return MVS_ERR_INVALID_ARGUMENT;
+  if ((bn0_scale != nullptr) != (bn0_shift != nullptr) || (bn0_scale != nullptr) != (bn0_mean != nullptr) ||
+      (bn1_scale != nullptr) != (bn1_shift != nullptr) || (bn1_scale != nullptr) != (bn1_mean != nullptr))
+    return MVS_ERR_INVALID_ARGUMENT;
+  const int n[3] = {d, h, w};
+  uint64_t ovox = (uint64_t)batch;
+  for (int k = 0; k < 3; ++k) {
+    if (pad[k] < 1 || !(pad[k] & 1)) return MVS_ERR_INVALID_ARGUMENT;   // the fused windows need P odd
+    if (y1_size[k] <= 0 || y1_origin[k] < 0 || y1_origin[k] + y1_size[k] > n[k]) return MVS_ERR_INVALID_ARGUMENT;
+    ovox *= (uint64_t)y1_size[k];
+  }
+  if ((uint64_t)d * h * w >= (1ull << 31) || ovox >= (1ull << 31) || (uint64_t)d * h * w * 64u >= 0xFFFFFFC0ull)
+    return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
+  mvs::launch_conv_head_fp32(cv4, batch, d, h, w, w0_wz, bn0_scale, bn0_shift, bn0_mean, w1, w1_pass, bn1_scale,
+                             bn1_shift, bn1_mean, pad, y1_origin, y1_size, y0, y1, (hipStream_t)stream,
+                             (hipEvent_t)ev0, (hipEvent_t)ev1);
+  return lc.status();
+}
+
 int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch, int c_in, int c_out,
                           int rd, int rh, int rw, int x0d, int x0h, int x0w, const float* weight, int d,
                           int h, int w, int pd, int ph, int pw, const float* bn_scale,

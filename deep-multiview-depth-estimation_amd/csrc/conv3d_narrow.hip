@@ -18,6 +18,8 @@
 //   both halves, the two channels' weights as one 64-bit scalar operand), 2 FMAs per lane-
 //   instruction -- the weights arrive pre-transposed as wt[c][kd][ky][kx][co] (ops.py), so each
 //   pair is one s_load_dwordx2.  COUT = 1: scalar weights as the fmas' SGPR operand.
+#include <algorithm>
+
 #include "launchers.h"
 #include "packed.h"
 
@@ -37,14 +39,39 @@ constexpr int kTX = 32, kTY = 8, kDT = 4;
 // relu(BN_a(in)) + relu(BN_b(in2)) per channel, ibn = [6][Cin] (scale, shift, mean of in, then of in2)
 // -- model.py:121-123's `relu(BN_0(deconv_1_0)) + y0` formed on load instead of by a pass over the
 // full volume; the zero padding stays zero
-template <int COUT, int C4, bool WZ = false, int DT = kDT, bool FOLD = false>
-__global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
+// C1 (COUT = 8, C4 = 1, WZ, Cin = 32: the fp32 eval path's conv_0_0; mvs_conv_head_fp32_fwd): conv_1_0
+// (model.py:103: 32 -> 16, stride 2, padding P odd, + BN_1 + ReLU) computed from the SAME staged halo
+// block on the fp32 matrix cores, so the cost volume is read once for both convolutions and the MFMA work
+// co-issues with the VALU work of the other waves on the SIMD.  The tile owns the stride-2 windows whose
+// start (2 o - P) is x0 - 1 + 2 j (j < 16), y0 - 1 + 2 j (j < 4), d0 - 1 + 2 j (j < 2): 8 row blocks of 16
+// windows, two per wave; every window's 27 taps lie in the staged (x0 - 1 .. x0 + 32) x (y0 - 1 .. y0 + 8)
+// x (d0 - 1 .. d0 + 4) block, which holds zeros outside the volume.  Per channel pass (4 channels = the
+// MFMA's K of 4, lane group kq = channel kq), after the wave's conv_0_0 arithmetic: 27 taps x 2 row
+// blocks of v_mfma_f32_16x16x4_f32 with A (window x, channel) and B (channel, output channel, from the
+// pass's weight slice staged beside the input) read from LDS at immediate tap offsets.
+struct Head1 {
+  const float* w1p;            // conv_1_0 weights [Cin / 4][27][16][4] (pass, tap, c_out, channel in pass)
+  const float *sc, *sh, *mu;   // BN_1 (16), all or none
+  float* y1;                   // [B][on0][on1][on2][16] channels-last
+  int o0[3], on[3];            // y1's region (volume output coordinates)
+  int pad[3];                  // P, odd
+};
+
+// C1's waves per SIMD: 3 keeps conv_0_0's occupancy (168 registers; a few spill outside the pass loop)
+#ifndef MVS_HEAD_WAVES
+#define MVS_HEAD_WAVES 3
+#endif
+
+template <int COUT, int C4, bool WZ = false, int DT = kDT, bool FOLD = false, bool C1 = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(C1 ? MVS_HEAD_WAVES : 1)))
+void conv3d_k3_narrow_kernel(
     const float* __restrict__ in, const float* __restrict__ wt, float* __restrict__ out, int Cin,
     int D, int H, int W, int tiles_x, int tiles_y, int dgroups, int n_batch, const float* __restrict__ bn_scale,
     const float* __restrict__ bn_shift, const float* __restrict__ bn_mean, const float* __restrict__ in2,
-    const float* __restrict__ ibn) {
+    const float* __restrict__ ibn, Head1 h1) {
   static_assert(!FOLD || (COUT == 1 && C4 == 0), "folded input BN: conv_out on NCDHW");
   static_assert(!WZ || DT == 4, "depth Winograd: two windows of 2");
+  static_assert(!C1 || (COUT == 8 && C4 == 1 && WZ), "fused conv_1_0: the fp32 conv_0_0 kernel");
   constexpr int kPX = kTX + 2, kPY = kTY + 2, kPD = DT + 2;
   constexpr int kPlane = kPX * kPY;
   constexpr int kStage = kPD * kPlane;                      // floats per input channel
@@ -52,6 +79,7 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
   constexpr int NP = COUT / 2;                              // channel pairs (COUT = 8)
   constexpr int NQ = C4 ? 4 : 1;                            // channels staged per pass
   __shared__ float lds[NQ * kStage];
+  __shared__ __attribute__((aligned(16))) float w1s[C1 ? 27 * 16 * 4 : 4];   // C1: the pass's conv_1_0 weights
   // XCD-contiguous tiles: the halo-sharing neighbours (next x tile, next y row of tiles, next depth
   // group) run on the same XCD's L2 (common.h xcd_work_id)
   const int total = (int)gridDim.x;
@@ -137,6 +165,18 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
 #pragma unroll
         for (int q = 0; q < NP; ++q) accw[a][ps][q] = f2v{0.0f, 0.0f};
   }
+  // C1: this wave's two conv_1_0 row blocks (wy, wz) = (rbi & 3, rbi >> 2), rbi = 2 wave + rb
+  const int c1lane = (int)threadIdx.x & 63, c1wave = (int)threadIdx.x >> 6;
+  const int m16 = c1lane & 15, kq = c1lane >> 4;
+  f4v c1acc[2] = {f4v{0.0f, 0.0f, 0.0f, 0.0f}, f4v{0.0f, 0.0f, 0.0f, 0.0f}};
+  int abase[2] = {0, 0};
+  if constexpr (C1) {
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int rbi = 2 * c1wave + rb, wy = rbi & 3, wzz = rbi >> 2;
+      abase[rb] = kq * kStage + (2 * wzz) * kPlane + (2 * wy) * kPX + 2 * m16;
+    }
+  }
 
   const int passes = C4 ? Cin / 4 : Cin;
   for (int q = 0; q < passes; ++q) {
@@ -154,6 +194,11 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
       if (e < kStage)
 #pragma unroll
         for (int u = 0; u < NQ; ++u) lds[u * kStage + e] = pre[j][u];
+    }
+    if constexpr (C1) {   // the pass's conv_1_0 weight slice, 432 float4 (L2-resident, 55 KB in all)
+      const f4v* src = reinterpret_cast<const f4v*>(h1.w1p) + (size_t)q * 432;
+      f4v* dst = reinterpret_cast<f4v*>(w1s);
+      for (int i = (int)threadIdx.x; i < 432; i += kBlock) dst[i] = src[i];
     }
     __syncthreads();
     if (q + 1 < passes) fetch(q + 1);   // in flight during this pass's arithmetic
@@ -231,6 +276,38 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
         }
       }
     }
+    if constexpr (C1) {
+      // conv_1_0 on this pass's 4 channels: 27 taps x 2 row blocks, operands from LDS at immediate offsets
+#pragma unroll
+      for (int t = 0; t < 27; ++t) {
+        const int tz = t / 9, ty = (t / 3) % 3, tx = t % 3;
+        const float bv = w1s[t * 64 + m16 * 4 + kq];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+          c1acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(lds[abase[rb] + tz * kPlane + ty * kPX + tx], bv,
+                                                           c1acc[rb], 0, 0, 0);
+      }
+    }
+  }
+
+  if constexpr (C1) {
+    // conv_1_0 epilogue: c1acc[rb][r] = window x = 4 kq + r of row block rb, output channel m16
+    const float sc = h1.sc ? h1.sc[m16] : 1.0f, sh = h1.sc ? h1.sh[m16] : 0.0f, mu = h1.sc ? h1.mu[m16] : 0.0f;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int rbi = 2 * c1wave + rb, wy = rbi & 3, wzz = rbi >> 2;
+      const int oz = (d0 - 1 + 2 * wzz + h1.pad[0]) >> 1, oy = (ty0 - 1 + 2 * wy + h1.pad[1]) >> 1;
+      if (oz < h1.o0[0] || oz >= h1.o0[0] + h1.on[0] || oy < h1.o0[1] || oy >= h1.o0[1] + h1.on[1]) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ox = (tx0 - 1 + 2 * (4 * kq + r) + h1.pad[2]) >> 1;
+        if (ox < h1.o0[2] || ox >= h1.o0[2] + h1.on[2]) continue;
+        float v = c1acc[rb][r];
+        if (h1.sc) v = fmaxf((v - mu) * sc + sh, 0.0f);
+        h1.y1[((((size_t)b * h1.on[0] + (oz - h1.o0[0])) * h1.on[1] + (oy - h1.o0[1])) * h1.on[2] + (ox - h1.o0[2])) *
+                  16 + m16] = v;
+      }
+    }
   }
 
   if constexpr (WZ) {   // A^T m: (m0 + m1 + m2, m1 - m2 - m3) per window
@@ -264,15 +341,15 @@ __global__ __launch_bounds__(kBlock) void conv3d_k3_narrow_kernel(
 #endif
 constexpr int kOutDT = MVS_CONV_OUT_DT;
 
-template <int COUT, int C4, bool WZ = false, bool FOLD = false>
+template <int COUT, int C4, bool WZ = false, bool FOLD = false, bool C1 = false>
 void launch_narrow(const float* in, const float* weight, float* out, int B, int Cin, int D, int H, int W,
                    const float* bn_scale, const float* bn_shift, const float* bn_mean, hipStream_t s,
-                   const float* in2 = nullptr, const float* ibn = nullptr) {
+                   const float* in2 = nullptr, const float* ibn = nullptr, const Head1& h1 = Head1{}) {
   constexpr int DT = COUT == 1 ? kOutDT : kDT;
   const int tiles_x = (W + kTX - 1) / kTX, tiles_y = (H + kTY - 1) / kTY, dgroups = (D + DT - 1) / DT;
   const dim3 grid = xcd_grid(B * dgroups * tiles_y * tiles_x);
-  hipLaunchKernelGGL((conv3d_k3_narrow_kernel<COUT, C4, WZ, DT, FOLD>), grid, dim3(kBlock), 0, s, in, weight, out,
-                     Cin, D, H, W, tiles_x, tiles_y, dgroups, B, bn_scale, bn_shift, bn_mean, in2, ibn);
+  hipLaunchKernelGGL((conv3d_k3_narrow_kernel<COUT, C4, WZ, DT, FOLD, C1>), grid, dim3(kBlock), 0, s, in, weight,
+                     out, Cin, D, H, W, tiles_x, tiles_y, dgroups, B, bn_scale, bn_shift, bn_mean, in2, ibn, h1);
 }
 
 }  // namespace
@@ -299,6 +376,68 @@ void launch_conv3d_k3_narrow(const float* in, int in_c4, bool wino_z, const floa
     else MVS_NARROW(1, 0, false);
   }
 #undef MVS_NARROW
+}
+
+// conv_0_0 + BN_0 + ReLU over the whole volume and conv_1_0 + BN_1 + ReLU on its region from the fp32
+// channel-quad cost volume in ONE kernel (C1 above); the region's outputs whose windows no tile owns --
+// windows starting below -1 or past the last tile's (start >= 32 tiles_x - 1 etc.: all-padding windows
+// and, when a dim is a multiple of the tile, the one at n - 1) -- by the per-lane stride-2 region kernel
+// on up to six slabs, stored into y1 in place
+void launch_conv_head_fp32(const float* cv4, int B, int D, int H, int W, const float* w0wz, const float* bn0_sc,
+                           const float* bn0_sh, const float* bn0_mu, const float* w1, const float* w1p,
+                           const float* bn1_sc, const float* bn1_sh, const float* bn1_mu, const int* pad,
+                           const int* o0, const int* on, float* y0, float* y1, hipStream_t s, hipEvent_t ev0,
+                           hipEvent_t ev1) {
+  Head1 h1;
+  h1.w1p = w1p;
+  h1.sc = bn1_sc;
+  h1.sh = bn1_sh;
+  h1.mu = bn1_mu;
+  h1.y1 = y1;
+  for (int d = 0; d < 3; ++d) {
+    h1.o0[d] = o0[d];
+    h1.on[d] = on[d];
+    h1.pad[d] = pad[d];
+  }
+  if (ev0) (void)hipEventRecord(ev0, s);
+  launch_narrow<8, 1, true, false, true>(cv4, w0wz, y0, B, 32, D, H, W, bn0_sc, bn0_sh, bn0_mu, s, nullptr, nullptr,
+                                         h1);
+  if (ev1) (void)hipEventRecord(ev1, s);
+  // owned windows per dim: starts -1 .. n_tiles * tile - 3 -> outputs [(P - 1) / 2, (n_tiles * tile - 3 + P) / 2]
+  const int tile[3] = {kDT, kTY, kTX}, n[3] = {D, H, W};
+  int clo[3], chi[3];   // core box of y1's region (inclusive), computed by the fused kernel
+  for (int d = 0; d < 3; ++d) {
+    const int tiles = (n[d] + tile[d] - 1) / tile[d];
+    clo[d] = std::max(o0[d], (pad[d] - 1) / 2);
+    chi[d] = std::min(o0[d] + on[d] - 1, (tiles * tile[d] - 3 + pad[d]) / 2);
+  }
+  // slabs: dim 0 lo / hi over the whole region, dim 1 within dim 0's core, dim 2 within both cores
+  for (int d = 0; d < 3; ++d)
+    for (int side = 0; side < 2; ++side) {
+      int so[3], sn[3];
+      bool empty = false;
+      for (int e = 0; e < 3; ++e) {
+        if (e < d) {   // inside the earlier dims' core
+          so[e] = clo[e];
+          sn[e] = chi[e] - clo[e] + 1;
+        } else if (e > d) {   // the whole region
+          so[e] = o0[e];
+          sn[e] = on[e];
+        } else if (side == 0) {
+          so[e] = o0[e];
+          sn[e] = clo[e] - o0[e];
+        } else {
+          so[e] = chi[e] + 1;
+          sn[e] = o0[e] + on[e] - 1 - chi[e];
+        }
+        empty = empty || sn[e] <= 0;
+      }
+      if (empty) continue;
+      int st0[3];
+      for (int e = 0; e < 3; ++e) st0[e] = so[e] - o0[e];
+      launch_conv3d_region(1 /*S2*/, false, 1, cv4, nullptr, w1, y1, B, 32, 16, n, so, sn, nullptr, nullptr, pad,
+                           bn1_sc, bn1_sh, bn1_mu, s, nullptr, nullptr, false, st0, on);
+    }
 }
 
 }  // namespace mvs

@@ -55,6 +55,8 @@ struct Geo {
                 //     cost volume (3, split.h: fp32 re-formed on load as (hi + lo) 2^-e); 0 NCDHW
   const uint32_t* absmax;   // in_c4 = 3: the volume's bound words (its scale)
   uint32_t* y_bound;        // optional: the output's bound words (split.h), raised in the epilogue
+  int st0[3];   // the output region's place in the stored tensor: y holds a box of size stn whose
+  int stn[3];   //   voxel st0 is the region's first (default 0 / on: y is the region)
 };
 
 // T2 parity class: per dim, outputs o with (o + P) % 2 == par; first such o in the region and count
@@ -65,8 +67,8 @@ __device__ inline void class_dim(int o0, int on, int p, int par, int& first, int
 
 __device__ inline void store_out(float* __restrict__ y, const Geo& g, int b, int co, int vz, int vy, int vx,
                                  int CO, float v) {
-  const size_t vox = ((size_t)vz * g.on[1] + vy) * g.on[2] + vx;
-  const size_t rvol = (size_t)g.on[0] * g.on[1] * g.on[2];
+  const size_t vox = ((size_t)(vz + g.st0[0]) * g.stn[1] + (vy + g.st0[1])) * g.stn[2] + (vx + g.st0[2]);
+  const size_t rvol = (size_t)g.stn[0] * g.stn[1] * g.stn[2];
   if (g.out_cf) y[((size_t)b * CO + co) * rvol + vox] = v;
   else y[((size_t)b * rvol + vox) * CO + co] = v;
 }
@@ -483,7 +485,7 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
                          float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on, const int* i0,
                          const int* in, const int* pad, const float* bn_scale, const float* bn_shift,
                          const float* bn_mean, hipStream_t s, const uint32_t* absmax, uint32_t* y_bound,
-                         bool per_lane) {
+                         bool per_lane, const int* st0, const int* stn) {
   Geo g;
   g.y_bound = y_bound;
   g.out_cf = out_cf ? 1 : 0;
@@ -496,6 +498,8 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
     g.i0[d] = i0 ? i0[d] : 0;
     g.in[d] = in ? in[d] : n[d];
     g.pad[d] = pad ? pad[d] : 1;
+    g.st0[d] = st0 ? st0[d] : 0;
+    g.stn[d] = stn ? stn[d] : on[d];
   }
   // stride-1 convolutions of one region tensor: the LDS-staged kernel (bit-equal) only with
   // MVS_FP32_S1_LDS=1 -- measured slower at cfg 2 (conv_1_1 0.42 against 0.34 ms alone, the fp32 eval step
@@ -528,6 +532,15 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
   // deconv_2_0 (32 -> 16)
   MVS_REGION_S2(32, 16) MVS_REGION_S2(32, 32) MVS_REGION_S2(32, 64)
   MVS_REGION_CASE(kS1, 16, 16) MVS_REGION_CASE(kS1, 32, 32) MVS_REGION_CASE(kS1, 64, 64)
+  // S2 from the fp32 channel-quad volume: row blocks per wave MVS_S2_RB (2 or 4) -- A/B
+  static const int s2_rb = [] {
+    const char* e = getenv("MVS_S2_RB");
+    return e && e[0] == '4' ? 4 : 2;
+  }();
+  if (mode == kS2 && in_c4 == 1 && CI == 32 && s2_rb == 4) {
+    if (CO == 16) return launch_mode<kS2, 32, 16, 4, 1>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
+    if (CO == 32) return launch_mode<kS2, 32, 32, 4, 1>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
+  }
   // transposed: row blocks per wave MVS_T2_RB (2 or 4)
   static const int t2_rb = [] {
     const char* e = getenv("MVS_T2_RB");

@@ -138,7 +138,14 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
                          const int* in,
                          const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                          hipStream_t s, const uint32_t* absmax = nullptr, uint32_t* y_bound = nullptr,
-                         bool per_lane = false);
+                         bool per_lane = false, const int* st0 = nullptr, const int* stn = nullptr);
+// conv_0_0 (+ BN_0 + ReLU, whole volume) and conv_1_0 (+ BN_1 + ReLU, on its region o0 / on, channels-last)
+// from the fp32 channel-quad cost volume, one fused kernel (conv3d_narrow.hip)
+void launch_conv_head_fp32(const float* cv4, int B, int D, int H, int W, const float* w0wz, const float* bn0_sc,
+                           const float* bn0_sh, const float* bn0_mu, const float* w1, const float* w1p,
+                           const float* bn1_sc, const float* bn1_sh, const float* bn1_mu, const int* pad,
+                           const int* o0, const int* on, float* y0, float* y1, hipStream_t s,
+                           hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // the S1 / T2 region convolutions on split-fp16 MFMA (conv3d_region_split.hip); K-32 weight blocks
 // channel_ops.hip: train-mode BatchNorm parameters (+ running statistics) from the batch sums
 void launch_bn_train_params(const double* sums, int C, double count, const double* bu, const double* bcnt, int Cp,

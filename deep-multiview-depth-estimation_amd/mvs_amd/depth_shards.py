@@ -95,8 +95,15 @@ def exchange_to_owners(slab, world, rank, group=None):
             req.wait()
     for i, b in enumerate(mine):
         stage[b][rank].copy_(slab[b])
-        # [P, C, Dl, h, w] -> [C, P*Dl, h, w]: slab p holds planes [p*Dl, (p+1)*Dl) of every channel
-        out[i].view(c, world, dl, h, w).copy_(stage[b].transpose(0, 1))
+        interleave_slabs(stage[b], out[i])
+    return out
+
+
+def interleave_slabs(stage, out):
+    """The owner's interleave: ``stage`` [P, C, Dl, h, w] (slab p = planes [p Dl, (p + 1) Dl) of every
+    channel, as received) -> ``out`` [C, P Dl, h, w] (NCDHW), one strided device copy."""
+    p, c, dl, h, w = stage.shape
+    out.view(c, p, dl, h, w).copy_(stage.transpose(0, 1))
     return out
 
 

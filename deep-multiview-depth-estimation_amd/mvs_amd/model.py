@@ -330,8 +330,8 @@ class CostVolumeReg(nn.Module):
         head kernel (forward_live_head) -- conv_0_0's and conv_1_0's outputs; cv is then the split
         volume on conv_2_0's input box only, ``cv_box`` (origin, size) that box."""
         from .ops import (CONV_S1, CONV_S2, CONV_T2, bound_words, conv3d_k3, conv3d_k3_split, conv3d_region,
-                          conv3d_region_split, conv_s2_split, deconv3d_k3s2, region_weight, softmax_depth,
-                          split_head, timed_kernel)
+                          conv3d_region_split, conv_head_fp32, conv_s2_split, deconv3d_k3s2, region_weight,
+                          softmax_depth, split_head, timed_kernel)
         org = lambda reg: [lo for lo, _ in reg]
         size = lambda reg: [hi - lo + 1 for lo, hi in reg]
         dims, pad = list(n), list(self.pad)
@@ -366,7 +366,20 @@ class CostVolumeReg(nn.Module):
             head = split_head(cv, bound, self.conv_0_0.weight, *bn_eval(self.BN_0), self.conv_1_0.weight,
                               *bn_eval(self.BN_1), pad, org(h1), size(h1), None if bw is None else bw[0])
             y1_bounded = bw is not None
-        if head is not None:
+        # the exact-fp32 head (ops.conv_head_fp32, csrc/conv3d_narrow.hip C1): conv_1_0 on the fp32 matrix
+        # cores inside conv_0_0's VALU kernel, from the same LDS tiles -- one read of the volume, the MFMA
+        # work co-issued beside the VALU work -- then conv_1_1 behind it on the side stream
+        y1_done = None
+        if head is None and bound is None and self._fp32_head_ok(cv, c4, pad):
+            h1 = _grow(B, n, 1)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                y0, y1a = conv_head_fp32(cv, self.conv_0_0.weight, *bn_eval(self.BN_0), self.conv_1_0.weight,
+                                         *bn_eval(self.BN_1), pad, org(h1), size(h1))
+                y1_done = conv3d_region(y1a, None, region_weight(self.conv_1_1), CONV_S1, dims, org(B), size(B),
+                                        org(h1), size(h1), None, *bn_eval(self.BN_1), out_ncdhw=True)
+            cv.record_stream(side)
+        elif head is not None:
             y0, y1_head = head
         else:
             side.wait_stream(main)
@@ -406,8 +419,12 @@ class CostVolumeReg(nn.Module):
                                            out_ncdhw=False), True
             return conv3d_region(ya, None, region_weight(conv_b), CONV_S1, dims, org(reg), size(reg),
                                  org(halo), size(halo), None, *bn_eval(bn), out_ncdhw=reg is B), reg is not B
+        # (the fp32 path: the region chain on a high-priority stream, or levels 1 and 3 on side streams beside
+        # level 2 as below, measured 5.99-6.93 against 5.86-5.89 ms per cfg-2 step -- not kept, gpurun_out r6g)
         l1_side = bw is not None and head is not None and os.environ.get("MVS_L1_SIDE", "1") != "0"
-        if l1_side:
+        if y1_done is not None:   # (level 1 ran behind the fp32 head on the side stream)
+            y1, y1_cl = y1_done, False
+        elif l1_side:
             # level 1's conv_1_1 (LDS-bound) on a side stream beside levels 2-3 (L2-bound per-lane convs):
             # cfg-2 eval step 3.89-4.00 -> 3.80-3.93 ms (same box, tools/gpu_r5_env_ab.sh r5l1)
             s1 = _side_stream(cv.device, 1)
@@ -450,9 +467,18 @@ class CostVolumeReg(nn.Module):
         if side != main:   # (a stream waiting on itself is an event + barrier packet: a 6 us bubble)
             main.wait_stream(side)
             y0.record_stream(main)
+            if y1_done is not None:
+                y1.record_stream(main)
         z = deconv3d_k3s2(y2, org(B), self.deconv_1_0.weight, dims, pad, *bn_eval(self.BN_0), y0, x2=y1,
                           channels_last=bw is not None and y1_cl)
         return softmax_depth(conv3d_k3(z, self.conv_out.weight))
+
+    def _fp32_head_ok(self, cv, c4, pad):
+        """ops.conv_head_fp32 applies: the fp32 channel-quad volume of 32 channels, conv_1_0 32 -> 16,
+        every stride-2 padding odd (the kernel's window ownership), MVS_FP32_HEAD not 0."""
+        return (os.environ.get("MVS_FP32_HEAD", "1") != "0" and c4 and cv.dtype == torch.float32
+                and cv.dim() == 6 and cv.shape[1] == 8 and tuple(self.conv_1_0.weight.shape[:2]) == (16, 32)
+                and all(p % 2 == 1 for p in pad))
 
     def _split_head_ok(self, cv, n):
         """ops.split_head applies to this split volume: C = 32 (8 channel quads), D even and every
@@ -710,11 +736,11 @@ _SIDE_STREAMS = {}
 _LANE = [0]
 
 
-def _side_stream(device, which=0):
+def _side_stream(device, which=0, priority=0):
     """Extra HIP streams per device (and pipeline lane) for independent branches of the inference step."""
-    key = (torch.device(device).index, which, _LANE[0])
+    key = (torch.device(device).index, which, _LANE[0], priority)
     if key not in _SIDE_STREAMS:
-        _SIDE_STREAMS[key] = torch.cuda.Stream(device)
+        _SIDE_STREAMS[key] = torch.cuda.Stream(device, priority=priority)
     return _SIDE_STREAMS[key]
 
 
@@ -1049,7 +1075,8 @@ class MVSNet(nn.Module):
                            list(self.depthmap_refine.parameters()))
         self.set_arithmetic(self.cfg.arithmetic)
         # eval inference over B >= 2 samples: chunks of samples issued on their own streams (forward)
-        self.pipeline_chunks = int(os.environ.get("MVS_PIPELINE_CHUNKS", "2"))
+        # (measured slower at cfg 2: 6.32 against 5.87 ms per step with 2 chunks, gpurun_out r6f -- off)
+        self.pipeline_chunks = int(os.environ.get("MVS_PIPELINE_CHUNKS", "1"))
 
     def set_arithmetic(self, arithmetic):
         """"fp32" (the reference's numerics: every HIP layer in exact fp32) or "split_f16" (opt-in: the

@@ -744,6 +744,54 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Te
     return y
 
 
+@torch.library.custom_op("mvs::conv_head_fp32", mutates_args=())
+def conv_head_fp32(cv4: torch.Tensor, w0: torch.Tensor, bn0_scale: Optional[torch.Tensor],
+                   bn0_shift: Optional[torch.Tensor], bn0_mean: Optional[torch.Tensor], w1: torch.Tensor,
+                   bn1_scale: Optional[torch.Tensor], bn1_shift: Optional[torch.Tensor],
+                   bn1_mean: Optional[torch.Tensor], pad: list[int], y1_origin: list[int],
+                   y1_size: list[int]) -> tuple[torch.Tensor, torch.Tensor]:
+    """conv_0_0 + BN_0 + ReLU (model.py:101, whole volume) and conv_1_0 + BN_1 + ReLU (model.py:103, on the
+    region y1_origin + [0, y1_size)) of the fp32 channel-quad cost volume ``cv4`` [B, 8, D, H, W, 4]
+    (cost_volume_c4) in ONE pass over it, in exact fp32 (mvs_conv_head_fp32_fwd: conv_0_0 on the VALU with
+    the depth-Winograd transform, conv_1_0 on the fp32 matrix cores from the same LDS tiles).  ``w0`` /
+    ``w1``: the modules' weights [8, 32, 3, 3, 3] / [16, 32, 3, 3, 3].  Returns (y0 [B, 8, D, H, W],
+    y1 [B, *y1_size, 16] channels-last).  Every pad odd (config.py:20 at even dims).  Inference only."""
+    _require_gpu(cv4, "cv4")
+    lib = _lib.load()
+    if cv4.dim() != 6 or cv4.shape[1] != 8 or cv4.shape[5] != 4 or cv4.dtype != _F32:
+        raise ValueError("cv4: the fp32 channel-quad cost volume [B, 8, D, H, W, 4]")
+    if tuple(w0.shape) != (8, 32, 3, 3, 3) or tuple(w1.shape) != (16, 32, 3, 3, 3):
+        raise ValueError("w0 [8, 32, 3, 3, 3] and w1 [16, 32, 3, 3, 3] expected")
+    cv4 = cv4.contiguous()
+    dev = cv4.device
+    b, _, d, h, wd, _ = cv4.shape
+    w0z = derived("k3wz", (w0,), lambda wt: _wino_z_weight(wt).to(device=dev), dev)
+    w1r = derived("head1_region", (w1,), lambda wt: wt.detach().to(device=dev, dtype=_F32).permute(2, 3, 4, 0, 1)
+                  .reshape(27, 16, 32).contiguous(), dev)
+    w1p = derived("head1_pass", (w1,), lambda wt: w1r.view(27, 16, 8, 4).permute(2, 0, 1, 3).contiguous(), dev)
+    bns = []
+    for t in (bn0_scale, bn0_shift, bn0_mean, bn1_scale, bn1_shift, bn1_mean):
+        bns.append(None if t is None else t.to(device=dev, dtype=_F32).contiguous())
+    y0 = torch.empty((b, 8, d, h, wd), device=dev, dtype=_F32)
+    y1 = torch.empty([b] + [int(v) for v in y1_size] + [16], device=dev, dtype=_F32)
+    bp = [None if t is None else _lib.ptr(t) for t in bns]
+    evs = (None, None)
+    if KERNEL_EVENT_HOOK is not None:   # around the fused kernel (bench.py's fp32 roofline kernel)
+        evs = tuple(ctypes.c_void_p(e.cuda_event) for e in KERNEL_EVENT_HOOK("conv_head"))
+    st = lib.mvs_conv_head_fp32_fwd(_lib.ptr(cv4), b, d, h, wd, _lib.ptr(w0z), *bp[:3], _lib.ptr(w1r), _lib.ptr(w1p),
+                                    *bp[3:], _ints3(pad), _ints3(y1_origin), _ints3(y1_size), _lib.ptr(y0), _lib.ptr(y1),
+                                    _lib.stream_handle(dev), *evs)
+    _lib.check(st, "mvs_conv_head_fp32_fwd")
+    return y0, y1
+
+
+@conv_head_fp32.register_fake
+def _(cv4, w0, bn0_scale, bn0_shift, bn0_mean, w1, bn1_scale, bn1_shift, bn1_mean, pad, y1_origin, y1_size):
+    b, _, d, h, w, _ = cv4.shape
+    return (cv4.new_empty((b, 8, d, h, w), dtype=_F32),
+            cv4.new_empty([b] + [int(v) for v in y1_size] + [16], dtype=_F32))
+
+
 @torch.library.custom_op("mvs::conv3d_k3_split", mutates_args=())
 def conv3d_k3_split(x: torch.Tensor, absmax: Optional[torch.Tensor], weight: torch.Tensor,
                     bn_scale: Optional[torch.Tensor] = None, bn_shift: Optional[torch.Tensor] = None,

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 21
+#define MVS_ABI_VERSION 22
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -441,6 +441,25 @@ int mvs_deconv3d_k3s2_fwd(const float* x, const float* x2, int flags, int batch,
                           int h, int w, int pd, int ph, int pw, const float* bn_scale,
                           const float* bn_shift, const float* bn_mean, const float* residual, float* y,
                           void* stream);
+
+/* conv_0_0 and conv_1_0 of CostVolumeReg (model.py:101 and :103, each + its eval BatchNorm + ReLU) in exact
+ * fp32 from the fp32 channel-quad cost volume cv4 [batch][8][d][h][w][4] (mvs_cost_volume_fwd_c4, 16-byte
+ * aligned) in ONE pass over it -- replaces mvs_conv3d_k3_fwd (MVS_CONV_IN_C4 | MVS_CONV_WINO_Z) for
+ * conv_0_0 plus mvs_conv3d_region_fwd (MVS_CONV_S2, MVS_CONV_IN_C4) for conv_1_0 on its region, the
+ * fp32 eval path's two layers that read the whole volume.  conv_0_0 runs on the fp32 VALU (depth-Winograd
+ * F(2,3), w0_wz the transformed weights as mvs_conv3d_k3_fwd takes them) and writes y0 [batch][8][d][h][w];
+ * conv_1_0 (32 -> 16, stride 2, padding pad[3], every pad odd) runs on the fp32 matrix cores from the same
+ * staged tiles and writes y1 [batch][y1_size...][16] channels-last holding outputs y1_origin + [0, y1_size)
+ * (w1 the region weight [27][16][32] of mvs_conv3d_region_fwd, w1_pass the same values as [8][27][16][4]:
+ * channel quad, tap, output channel, channel in quad).  BN pointers: 8 / 16 floats each, all three or none
+ * per layer.  Same values as the two separate kernels up to fp32 summation order (conv_1_0's channels
+ * are summed per quad of the staging, not per 16).  ev0 / ev1: NULL or hipEvent_t recorded on the stream
+ * right before / after the fused kernel (the slab launches for the region's unowned windows follow it). */
+int mvs_conv_head_fp32_fwd(const float* cv4, int batch, int d, int h, int w, const float* w0_wz,
+                           const float* bn0_scale, const float* bn0_shift, const float* bn0_mean, const float* w1,
+                           const float* w1_pass, const float* bn1_scale, const float* bn1_shift,
+                           const float* bn1_mean, const int* pad, const int* y1_origin, const int* y1_size,
+                           float* y0, float* y1, void* stream, void* ev0, void* ev1);
 
 /* mvs_conv3d_region_fwd modes */
 #define MVS_CONV_S1 0   /* Conv3d 3x3x3, stride 1, padding 1: region -> region                     */

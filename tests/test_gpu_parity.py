@@ -502,6 +502,55 @@ def test_pipelined_forward_is_bit_identical(arithmetic):
             model_mod.MVSNet._forward_one = orig
 
 
+def test_rccl_world1_shard_exchange_and_interleave_at_cfg4():
+    """The D-sharded path's RCCL leg on one GPU (BASELINE configs[3], SURVEY.md §8 e): an "nccl" (RCCL)
+    process group of world size 1; the 8 rank slabs of cfg 4 (B = 1, V = 3, 128 x 160, D = 256, 32 planes
+    each: the HIP kernel with d_begin = 32 r) go through RCCL point-to-point (batch_isend_irecv, self as
+    the peer) into the owner's staging buffer [8, C, 32, h, w], and depth_shards.interleave_slabs (the
+    owner-side copy exchange_to_owners runs for P > 1) forms the NCDHW volume: bit-equal to the unsharded
+    D = 256 volume.  Then DepthShardedMVSNet over that group runs end to end at cfg-4 geometry and gives
+    MVSNet.forward's depth maps bit for bit."""
+    import socket
+    import torch.distributed as dist
+    from cameras import camera_batch, depth_range
+    from mvs_amd import ops
+    from mvs_amd.config import MVSConfig
+    from mvs_amd.depth_shards import DepthShardedMVSNet, interleave_slabs
+    from mvs_amd.model import MVSNet
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1, device_id=DEV)
+    try:
+        B, V, C, H, W, D, P = 1, 3, 32, 512, 640, 256, 8
+        h, w = H // 4, W // 4
+        K, R, T = camera_batch(B, V, h, w)
+        d_min, d_int = depth_range(B)
+        feat = torch.randn(B * V, C, h, w, generator=torch.Generator().manual_seed(4)).to(DEV)
+        with torch.no_grad():
+            full, _ = ops.cost_volume(feat, K, R, T, d_min, d_int, B, V, 0, D, 25.0)
+            slabs = [ops.cost_volume(feat, K, R, T, d_min, d_int, B, V, r * (D // P), D // P, 25.0)[0]
+                     for r in range(P)]
+            stage = torch.empty((P, C, D // P, h, w), device=DEV)
+            reqs = dist.batch_isend_irecv([op for r in range(P) for op in (
+                dist.P2POp(dist.isend, slabs[r][0].contiguous(), 0), dist.P2POp(dist.irecv, stage[r], 0))])
+            for req in reqs:
+                req.wait()
+            out = torch.empty((C, D, h, w), device=DEV)
+            interleave_slabs(stage, out)
+            torch.cuda.synchronize()
+        assert torch.equal(out, full[0])
+        # the model end to end through the wrapper (world 1 over the RCCL group)
+        net = MVSNet(MVSConfig(d_num=D, in_h=H, in_w=W)).to(DEV).eval()
+        img = torch.randn(B * V, 3, H, W, generator=torch.Generator().manual_seed(8)).to(DEV)
+        with torch.no_grad():
+            ini_s, ref_s = DepthShardedMVSNet(net, 1, 0, group=dist.group.WORLD)(img, K, R, T, d_min, d_int, B, V)
+            ini, ref = net(img, K, R, T, d_min, d_int, B, V)
+        assert torch.equal(ini_s, ini) and torch.equal(ref_s, ref)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_depth_sharded_single_rank_equals_model():
     """mvs_amd.depth_shards at world size 1 (one GPU here; N > 1 is covered by the gloo test and
     the driver's multi-GPU bench) reproduces MVSNet.forward bit for bit (exact-fp32 conv_0_0 on both:
@@ -878,6 +927,56 @@ def test_narrow_conv3d_channel_quad_input_is_bit_equal(shape):
     with torch.no_grad():
         for p in ([None, None, None], bn):
             assert torch.equal(conv3d_k3(_to_c4(x), wt, *p, in_c4=True), conv3d_k3(x, wt, *p))
+
+
+@pytest.mark.parametrize("bn", [False, True])
+@pytest.mark.parametrize("shape", [(2, 24, 20, 26), (1, 48, 32, 40), (1, 8, 16, 64), (1, 7, 37, 70), (2, 12, 9, 33)])
+def test_fp32_head_matches_conv0_and_float64_conv1(shape, bn):
+    """ops.conv_head_fp32 (csrc/conv3d_narrow.hip C1 + the slab launches): y0 bit-equal to the
+    standalone conv_0_0 kernel (conv3d_k3 in_c4 wino_z: the same VALU arithmetic), y1 = conv_1_0 +
+    BN_1 + ReLU on halo(B) within fp32 accumulation error of a float64 convolution (the 864-term
+    K = 27 taps x 32 channels MFMA sum: |err| <= 1e-5 * sum|x||w| |scale|), and equal to the
+    per-lane stride-2 region kernel to the same tolerance.  Shapes: tile multiples (8, 16, 64: the
+    windows at n - 1 come from the slab launches), odd depth, cfg-5-like odd widths, batch 2."""
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _grow, _tconv_input_region
+    from mvs_amd.ops import CONV_S2, conv3d_k3, conv3d_region, conv_head_fp32, region_weight
+    b, *n = shape
+    n = tuple(n)
+    pad, _ = pad_outpad(*n)
+    pad = [p | 1 for p in pad]   # (odd at the model's even dims; forced odd for the odd test dims)
+    Bx = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
+    h1 = _grow(Bx, n, 1)
+    o0, on = [lo for lo, _ in h1], [hi - lo + 1 for lo, hi in h1]
+    g = torch.Generator().manual_seed(sum(shape) + bn)
+    x = torch.randn(b, 32, *n, generator=g)
+    w0 = torch.randn(8, 32, 3, 3, 3, generator=g) * 0.1
+    w1 = torch.randn(16, 32, 3, 3, 3, generator=g) * 0.1
+    p0 = [t.to(DEV) for t in _bn_params(8, g)] if bn else [None] * 3
+    p1 = _bn_params(16, g) if bn else None
+    p1d = [t.to(DEV) for t in p1] if bn else [None] * 3
+    x4 = _to_c4(x.to(DEV))
+    with torch.no_grad():
+        y0, y1 = conv_head_fp32(x4, w0.to(DEV), *p0, w1.to(DEV), *p1d, pad, o0, on)
+        torch.cuda.synchronize()
+        assert torch.equal(y0, conv3d_k3(x4, w0.to(DEV), *p0, in_c4=True, wino_z=True))
+        conv = torch.nn.Conv3d(32, 16, 3, bias=False)
+        conv.weight.copy_(w1)
+        y1r = conv3d_region(x4, None, region_weight(conv).to(DEV), CONV_S2, list(n), o0, on, None, None, pad, *p1d,
+                            in_c4=True)
+    sl = tuple(slice(lo, lo + k) for lo, k in zip(o0, on))
+    ref = torch.nn.functional.conv3d(x.double(), w1.double(), stride=2, padding=pad)[(slice(None),) * 2 + sl]
+    aref = torch.nn.functional.conv3d(x.double().abs(), w1.double().abs(), stride=2, padding=pad)[(slice(None),) * 2 + sl]
+    if bn:
+        sc, sh, mu = [t.double().view(1, -1, 1, 1, 1) for t in p1]
+        ref = torch.relu((ref - mu) * sc + sh)
+        aref = aref * sc.abs()
+    ref, aref = ref.permute(0, 2, 3, 4, 1), aref.permute(0, 2, 3, 4, 1)
+    tol = 1e-5 * aref + 1e-30
+    for name, y in (("fused", y1), ("region kernel", y1r)):
+        err = (y.double().cpu() - ref).abs()
+        assert bool((err <= tol).all()), "%s: max err %.3g (tol %.3g)" % (name, err.max().item(), tol.max().item())
+    assert bool(((y1 - y1r).abs().double().cpu() <= 2 * tol).all())
 
 
 @pytest.mark.parametrize("cout", [16, 32, 64])

@@ -139,7 +139,7 @@ def main():
         timed("eval step (exact fp32 conv_0_0)", step, a.reps)
         reg.split_f16 = True
         saved = M._side_stream
-        M._side_stream = lambda device, which=0: torch.cuda.current_stream(device)
+        M._side_stream = lambda device, which=0, priority=0: torch.cuda.current_stream(device)
         try:
             timed("eval step (serialised)", step, a.reps)
         finally:
