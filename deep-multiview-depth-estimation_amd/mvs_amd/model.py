@@ -366,9 +366,12 @@ class CostVolumeReg(nn.Module):
             head = split_head(cv, bound, self.conv_0_0.weight, *bn_eval(self.BN_0), self.conv_1_0.weight,
                               *bn_eval(self.BN_1), pad, org(h1), size(h1), None if bw is None else bw[0])
             y1_bounded = bw is not None
-        # the exact-fp32 head (ops.conv_head_fp32, csrc/conv3d_narrow.hip C1): conv_1_0 on the fp32 matrix
-        # cores inside conv_0_0's VALU kernel, from the same LDS tiles -- one read of the volume, the MFMA
-        # work co-issued beside the VALU work -- then conv_1_1 behind it on the side stream
+        # the exact-fp32 head (ops.conv_head_fp32, csrc/conv3d_narrow.hip C1), opt-in (MVS_FP32_HEAD=1):
+        # conv_1_0 on the fp32 matrix cores inside conv_0_0's VALU kernel, from the same LDS tiles, then
+        # conv_1_1 behind it on the side stream.  Measured slower: the fused kernel 3.60 ms against
+        # 1.88 + 1.15 ms for the two kernels alone, the cfg-2 step 6.6-6.7 against 5.8 ms (packed or single
+        # fp32 FMAs, padded channel planes: 3.61-4.10 ms; gpurun_out r6i / r6j) -- the f32 MFMA does not
+        # co-issue beside the packed-f32 VALU stream, it takes the same SIMD cycles
         y1_done = None
         if head is None and bound is None and self._fp32_head_ok(cv, c4, pad):
             h1 = _grow(B, n, 1)
@@ -475,8 +478,8 @@ class CostVolumeReg(nn.Module):
 
     def _fp32_head_ok(self, cv, c4, pad):
         """ops.conv_head_fp32 applies: the fp32 channel-quad volume of 32 channels, conv_1_0 32 -> 16,
-        every stride-2 padding odd (the kernel's window ownership), MVS_FP32_HEAD not 0."""
-        return (os.environ.get("MVS_FP32_HEAD", "1") != "0" and c4 and cv.dtype == torch.float32
+        every stride-2 padding odd (the kernel's window ownership), MVS_FP32_HEAD=1 (opt-in: slower, above)."""
+        return (os.environ.get("MVS_FP32_HEAD", "0") == "1" and c4 and cv.dtype == torch.float32
                 and cv.dim() == 6 and cv.shape[1] == 8 and tuple(self.conv_1_0.weight.shape[:2]) == (16, 32)
                 and all(p % 2 == 1 for p in pad))
 

@@ -577,6 +577,36 @@ def test_depth_sharded_single_rank_equals_model():
     assert torch.equal(ini, ini_g) and torch.equal(ref, ref_g)
 
 
+def test_mvsnet_opt_in_fp32_head_matches_default(monkeypatch):
+    """MVSNet.forward with the opt-in fused fp32 head (MVS_FP32_HEAD=1: ops.conv_head_fp32 then conv_1_1
+    on the side stream) against the default two-kernel path: conv_1_0's 864-term sums round in another
+    order (fp32 accumulation error only), so the depth maps agree to 1e-4 of the depth range."""
+    from weights import deterministic_state_dict
+    from cameras import camera_batch, depth_range
+    from mvs_amd import ops
+    from mvs_amd.config import MVSConfig
+    from mvs_amd.model import MVSNet
+    D = 16
+    net = MVSNet(MVSConfig(d_num=D, in_h=256, in_w=320))
+    net.load_state_dict(deterministic_state_dict(net.state_dict()))
+    net = net.to(DEV).eval()
+    K, R, T = camera_batch(2, 3, 64, 80)
+    d_min, d_int = depth_range(2, d_int=4.0)
+    img = torch.from_numpy(np.random.default_rng(7).standard_normal((6, 3, 256, 320), dtype=np.float32)).to(DEV)
+    calls = []
+    orig = ops.conv_head_fp32
+    monkeypatch.setattr(ops, "conv_head_fp32", lambda *a: calls.append(1) or orig(*a))
+    with torch.no_grad():
+        ini, ref = net(img, K, R, T, d_min, d_int, 2, 3)
+        assert not calls
+        monkeypatch.setenv("MVS_FP32_HEAD", "1")
+        ini_h, ref_h = net(img, K, R, T, d_min, d_int, 2, 3)
+    assert calls
+    span = D * 4.0
+    assert (ini_h - ini).abs().max().item() <= 1e-4 * span
+    assert (ref_h - ref).abs().max().item() <= 1e-4 * span
+
+
 @pytest.mark.parametrize("shape,wino", [((2, 32, 8, 12, 20, 40), False), ((1, 8, 1, 5, 9, 33), False),
                                         ((1, 32, 8, 7, 8, 32), False), ((2, 8, 1, 16, 24, 70), False),
                                         ((2, 32, 8, 12, 20, 40), True), ((1, 32, 8, 7, 8, 32), True),

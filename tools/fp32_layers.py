@@ -97,14 +97,14 @@ def main():
                                                                       channel_quads=True)
         step = lambda: net(img, K, R, T, d_min, d_int, B, V)
         layers["step"] = step
+        yh0, yh1 = layers["conv_head"]()
+        print("conv_head: y0 bit-equal %s, y1 max|d| vs conv_1_0 %.3g" % (
+            torch.equal(yh0, y0), (yh1 - layers["conv_1_0"]()).abs().max().item()), flush=True)
         names = a.only.split(",") if a.only else list(layers)
         for name in names:
             timed(name, layers[name], a.reps)
         if a.only:
             return
-        yh0, yh1 = layers["conv_head"]()
-        print("conv_head: y0 bit-equal %s, y1 max|d| vs conv_1_0 %.3g" % (
-            torch.equal(yh0, y0), (yh1 - layers["conv_1_0"]()).abs().max().item()), flush=True)
         saved = M._side_stream
         M._side_stream = lambda device, which=0, priority=0: torch.cuda.current_stream(device)
         try:
