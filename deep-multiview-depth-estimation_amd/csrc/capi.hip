@@ -594,6 +594,22 @@ int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, 
   return lc.status();
 }
 
+size_t mvs_conv3d_k3_wgrad_workspace_bytes(int batch, int c_in, int d, int h, int w) {
+  if (batch <= 0 || c_in <= 0 || d <= 0 || h <= 0 || w <= 0) return 0;
+  return mvs::conv3d_wgrad_workspace_bytes(batch, c_in, d, h, w);
+}
+
+int mvs_conv3d_k3_wgrad(const float* x, const float* gy, int batch, int c_in, int c_out, int d, int h, int w,
+                        float* dw, void* workspace, void* stream) {
+  if (!x || !gy || !dw || !workspace || batch <= 0 || d <= 0 || h <= 0 || w <= 0) return MVS_ERR_INVALID_ARGUMENT;
+  if (!mvs::conv3d_wgrad_supported(c_in, c_out)) return MVS_ERR_INVALID_ARGUMENT;
+  if ((uint64_t)d * (uint64_t)h * (uint64_t)w >= (1ull << 31)) return MVS_ERR_TOO_LARGE;
+  const mvs::LaunchCheck lc;
+  mvs::launch_conv3d_wgrad(x, gy, batch, c_in, c_out, d, h, w, static_cast<float*>(workspace), dw,
+                           (hipStream_t)stream);
+  return lc.status();
+}
+
 int mvs_conv_head_fp32_fwd(const float* cv4, int batch, int d, int h, int w, const float* w0_wz,
                            const float* bn0_scale, const float* bn0_shift, const float* bn0_mean, const float* w1,
                            const float* w1_pass, const float* bn1_scale, const float* bn1_shift,

@@ -85,6 +85,11 @@ void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, u
 // (optional epilogue: max((v - bn_mean) * bn_scale + bn_shift, 0), all three or none); in_c4: the
 // input is channel-quad in[B][Cin/4][D][H][W][4], fp32 (1) or bf16 (2)
 // wino_z (Cout = 8): Winograd F(2,3) along depth, weight = the transformed wu[Cin][3][3][4][8]
+// csrc/conv3d_wgrad.hip: narrow Conv3d weight gradient (dw [c_out][c_in][27]); part: the workspace
+size_t conv3d_wgrad_workspace_bytes(int B, int c_in, int D, int H, int W);
+bool conv3d_wgrad_supported(int c_in, int c_out);
+void launch_conv3d_wgrad(const float* x, const float* gy, int B, int c_in, int c_out, int D, int H, int W,
+                         float* part, float* dw, hipStream_t s);
 void launch_conv3d_k3_narrow(const float* in, int in_c4, bool wino_z, const float* weight, float* out, int B,
                              int Cin, int Cout, int D, int H, int W, const float* bn_scale, const float* bn_shift,
                              const float* bn_mean, hipStream_t s, const float* in2 = nullptr,

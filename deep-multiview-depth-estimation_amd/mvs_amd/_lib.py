@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmvs_cost_volume.so"
 # MVS_LIB_PATH: load another build of the same ABI (A/B kernel experiments, tools/gpu_*_ab.sh)
 LIB_PATH = os.environ.get("MVS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 MVS_OK = 0
 MVS_BWD_DETERMINISTIC = 1
@@ -86,6 +86,8 @@ SIGNATURES = {
     "mvs_depth_threshold": (_c_int, [_p, ctypes.c_size_t, _c_float, _c_float, _p, _p]),
     "mvs_conv3d_k3_fwd": (_c_int, [_p, _c_int, _p, _p] + [_c_int] * 6 + [_p] * 6),
     "mvs_conv_head_fp32_fwd": (_c_int, [_p] + [_c_int] * 4 + [_p] * 17),
+    "mvs_conv3d_k3_wgrad_workspace_bytes": (ctypes.c_size_t, [_c_int] * 5),
+    "mvs_conv3d_k3_wgrad": (_c_int, [_p, _p] + [_c_int] * 6 + [_p, _p, _p]),
     "mvs_conv2d_fwd": (_c_int, [_p, _p, _p] + [_c_int] * 7 + [_p] * 5),
     "mvs_conv2d_split_weights": (_c_int, [_p, _c_int, _c_int, _c_int, _p, _p]),
     "mvs_conv2d_split_fwd": (_c_int, [_p, _p, _c_int, _p] + [_c_int] * 7 + [_p] * 6),

@@ -208,7 +208,24 @@ class CostVolumeReg(nn.Module):
             return self.forward_live(cv)
         if self.live_train_ok(cv.shape[2:]):
             return self.forward_live_train(cv)
+        if self.live_autograd_ok(cv):
+            return self.forward_live_train(cv)   # (the torch layers: differentiable)
         return self.forward_full(cv)
+
+    def live_autograd_ok(self, cv):
+        """forward_live_train under autograd (train.py:97-104: model.train(), loss.backward()): the
+        live-region evaluation is the same function of the volume and the parameters as forward_full
+        (structural zeros and per-class constants are exact identities, not approximations), so its
+        autograd gradient is forward_full's -- with the region layers on their live regions only (cfg 2:
+        the stride-2 convs and the deeper levels on 1/8 .. 1/512 of the volume).  On a HIP device in fp32,
+        train-mode BN with running statistics, the module's padding derived from the volume extent;
+        MVS_TRAIN_LIVE=0 keeps forward_full."""
+        bns = (self.BN_0, self.BN_1, self.BN_2, self.BN_3)
+        return (self.live_region and torch.is_grad_enabled() and cv.is_cuda and cv.dtype == torch.float32
+                and cv.dim() == 5 and not torch.is_autocast_enabled()
+                and os.environ.get("MVS_TRAIN_LIVE", "1") != "0" and self._live_geometry_ok(tuple(cv.shape[2:]))
+                and all(bn.training and bn.track_running_stats and bn.running_mean is not None and bn.affine
+                        for bn in bns))
 
     def head_ok(self, dcv):
         """The fused head kernel applies to this deferred cost volume: eval-mode live regions with the
@@ -805,6 +822,9 @@ def _narrow_conv(conv, x):
         from .ops import conv3d_k3
         return conv3d_k3(x, conv.weight)
     if x.is_cuda and torch.is_grad_enabled():
+        from . import narrow_train
+        if narrow_train.applies(conv, x):   # HIP forward, input gradient and weight gradient
+            return narrow_train.conv3d(conv, x)
         return _train_conv(conv, x)
     return conv(x)
 
@@ -859,8 +879,8 @@ def _bn_train(bn, s1, s2, count):
         m = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
         bn.running_mean.mul_(1.0 - m).add_(mean.to(bn.running_mean), alpha=m)
         bn.running_var.mul_(1.0 - m).add_((var * (count / max(count - 1, 1))).to(bn.running_var), alpha=m)
-    scale = bn.weight / torch.sqrt(var.float() + bn.eps)
-    return scale, bn.bias, mean.float()
+    scale = bn.weight / torch.sqrt(var.to(bn.weight.dtype) + bn.eps)
+    return scale, bn.bias, mean.to(bn.weight.dtype)
 
 
 def _apply_bn(y, scale, shift, mean):
@@ -985,6 +1005,22 @@ def _crop_pad(x, x_reg, want, n):
     return F.pad(y, flat) if any(flat) else y
 
 
+def _region_conv3d(x, weight, stride, padding):
+    """F.conv3d of the live-region helpers; under autograd on a HIP device in fp32 the per-tap GEMMs
+    (tap_gemm.conv3d: MIOpen's backward solvers for these shapes are naive)."""
+    if x.is_cuda and torch.is_grad_enabled() and x.dtype == torch.float32 and not torch.is_autocast_enabled():
+        from . import tap_gemm
+        return tap_gemm.conv3d(x, weight, stride, padding)
+    return F.conv3d(x, weight, stride=stride, padding=padding)
+
+
+def _region_conv_transpose3d(x, weight, stride):
+    if x.is_cuda and torch.is_grad_enabled() and x.dtype == torch.float32 and not torch.is_autocast_enabled():
+        from . import tap_gemm
+        return tap_gemm.conv_transpose3d(x, weight, stride)
+    return F.conv_transpose3d(x, weight, stride=stride)
+
+
 def _conv_s2_region(x, weight, out_reg, pad):
     """conv3d(x, weight, stride 2, padding pad) on the output box out_reg (x: full volume).
 
@@ -1005,7 +1041,7 @@ def _conv_s2_region(x, weight, out_reg, pad):
         sl.append(slice(ca, cb + 1))
         pads.append(ps)
         offs.append((ps - lp) // 2)
-    y = F.conv3d(x[:, :, sl[0], sl[1], sl[2]], weight, stride=2, padding=tuple(pads))
+    y = _region_conv3d(x[:, :, sl[0], sl[1], sl[2]], weight, 2, tuple(pads))
     cnt = [hi - lo + 1 for lo, hi in out_reg]
     assert all(o + c <= m for o, c, m in zip(offs, cnt, y.shape[2:]))
     return y[:, :, offs[0]:offs[0] + cnt[0], offs[1]:offs[1] + cnt[1], offs[2]:offs[2] + cnt[2]]
@@ -1014,13 +1050,13 @@ def _conv_s2_region(x, weight, out_reg, pad):
 def _conv_s1_region(x, x_reg, weight, out_reg, n):
     """conv3d(., weight, stride 1, padding 1) on out_reg, from the region tensor x on x_reg."""
     want = tuple((lo - 1, hi + 1) for lo, hi in out_reg)
-    return F.conv3d(_crop_pad(x, x_reg, want, n), weight)
+    return _region_conv3d(_crop_pad(x, x_reg, want, n), weight, 1, 0)
 
 
 def _tconv_region(x, x_reg, weight, out_reg, pad):
     """conv_transpose3d(., weight, stride 2, padding pad) on out_reg, from the region tensor x on
     x_reg (which must hold every input that reaches out_reg: _tconv_input_region)."""
-    y = F.conv_transpose3d(x, weight, stride=2)   # output q <-> volume index 2 * xlo + q - P
+    y = _region_conv_transpose3d(x, weight, 2)   # output q <-> volume index 2 * xlo + q - P
     sl, pads = [], []
     for (xlo, _), (lo, hi), p, m in zip(x_reg, out_reg, pad, y.shape[2:]):
         o0 = 2 * xlo - p

@@ -744,6 +744,32 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bn_scale: Optional[torch.Te
     return y
 
 
+WGRAD_SHAPES = ((32, 8), (16, 8), (8, 8), (8, 1))   # (c_in, c_out) of mvs_conv3d_k3_wgrad
+
+
+def conv3d_k3_wgrad(x: torch.Tensor, gy: torch.Tensor) -> torch.Tensor:
+    """Weight gradient of nn.Conv3d(c_in, c_out, 3, padding=1, bias=False) (model.py:101 conv_0_0,
+    model.py:124 conv_out) from its input x [B, c_in, D, H, W] and output gradient gy [B, c_out, D, H, W]
+    (fp32 NCDHW): dw [c_out, c_in, 3, 3, 3] on the f32 matrix cores (mvs_conv3d_k3_wgrad, deterministic).
+    (c_in, c_out) in WGRAD_SHAPES."""
+    _require_gpu(x, "x")
+    lib = _lib.load()
+    if x.dim() != 5 or gy.dim() != 5 or x.shape[0] != gy.shape[0] or x.shape[2:] != gy.shape[2:]:
+        raise ValueError("x [B, c_in, D, H, W] and gy [B, c_out, D, H, W] expected")
+    b, cin, d, h, w = x.shape
+    cout = gy.shape[1]
+    if (cin, cout) not in WGRAD_SHAPES:
+        raise ValueError("(c_in, c_out) = (%d, %d) not in %s" % (cin, cout, WGRAD_SHAPES))
+    x = x.to(_F32).contiguous()
+    gy = gy.to(_F32).contiguous()
+    ws = torch.empty(lib.mvs_conv3d_k3_wgrad_workspace_bytes(b, cin, d, h, w) // 4, device=x.device, dtype=_F32)
+    dw = torch.empty((cout, cin, 3, 3, 3), device=x.device, dtype=_F32)
+    st = lib.mvs_conv3d_k3_wgrad(_lib.ptr(x), _lib.ptr(gy), b, cin, cout, d, h, w, _lib.ptr(dw), _lib.ptr(ws),
+                                 _lib.stream_handle(x.device))
+    _lib.check(st, "mvs_conv3d_k3_wgrad")
+    return dw
+
+
 @torch.library.custom_op("mvs::conv_head_fp32", mutates_args=())
 def conv_head_fp32(cv4: torch.Tensor, w0: torch.Tensor, bn0_scale: Optional[torch.Tensor],
                    bn0_shift: Optional[torch.Tensor], bn0_mean: Optional[torch.Tensor], w1: torch.Tensor,

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 22
+#define MVS_ABI_VERSION 23
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -282,6 +282,20 @@ int mvs_depth_threshold(const float* depth, size_t n, float lo, float hi, float*
 int mvs_conv3d_k3_fwd(const float* x, int flags, const float* weight, float* y, int batch, int c_in,
                       int c_out, int d, int h, int w, const float* bn_scale, const float* bn_shift,
                       const float* bn_mean, const float* x2, const float* in_bn, void* stream);
+
+/* Weight gradient of a narrow full-volume Conv3d(c_in, c_out, 3, padding=1, bias=False) under autograd
+ * (train.py:103's loss.backward through model.py:101 conv_0_0 and model.py:124 conv_out; csrc/conv3d_wgrad.hip):
+ *   dw[c_out][c_in][3][3][3] (nn.Conv3d's weight layout) = sum over the batch and the voxels of
+ *   gy[b][co][v] * x[b][ci][v + tap - 1] (zero padding), fp32 products and sums on the f32-input matrix
+ *   cores, reduced in a fixed order (bit-reproducible).
+ *   x[batch][c_in][d][h][w], gy[batch][c_out][d][h][w] fp32 NCDHW; (c_in, c_out) in {(32, 8), (16, 8),
+ *   (8, 8), (8, 1)}, else MVS_ERR_INVALID_ARGUMENT; d*h*w < 2^31.
+ *   workspace: DEVICE, mvs_conv3d_k3_wgrad_workspace_bytes(batch, c_in, d, h, w) bytes (the
+ *   workgroups' partial blocks).  Replaces the weight half of torch's Conv3d backward (MIOpen's naive
+ *   solver for these shapes; per-tap GEMMs in mvs_amd/tap_gemm.py). */
+size_t mvs_conv3d_k3_wgrad_workspace_bytes(int batch, int c_in, int d, int h, int w);
+int mvs_conv3d_k3_wgrad(const float* x, const float* gy, int batch, int c_in, int c_out, int d, int h, int w,
+                        float* dw, void* workspace, void* stream);
 
 /* conv_0_0 (model.py:77, 101: nn.Conv3d(32, 8, 3, padding=1, bias=False) + optional eval BN_0 + ReLU)
  * on the f16 matrix cores with split operands (csrc/conv3d_split.hip): every fp32 operand is scaled by

@@ -1,0 +1,61 @@
+"""GPU: the narrow full-volume convolutions under autograd (mvs_amd/narrow_train.py: conv_0_0
+Conv3d(32, 8) and conv_out Conv3d(8, 1), model.py:101,124, in train.py:103's loss.backward) against
+float64 torch autograd: output, input gradient and weight gradient within fp32 accumulation error
+(|err| <= 1e-5 x the same sum over absolute values), the weight gradient bit-reproducible."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+DEV = torch.device("cuda", 0) if torch.cuda.is_available() else None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,shape", [(32, 8, (2, 8, 12, 40)), (8, 1, (1, 7, 37, 53)), (32, 8, (1, 5, 9, 33)),
+                                            (16, 8, (2, 4, 8, 32)), (8, 8, (1, 9, 17, 70)), (8, 1, (3, 1, 1, 1))])
+def test_narrow_conv_autograd_matches_float64(cin, cout, shape):
+    from mvs_amd import narrow_train
+    b, d, h, w = shape
+    g = torch.Generator().manual_seed(cin * 100 + sum(shape))
+    x = torch.randn(b, cin, d, h, w, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, 3, generator=g) * 0.1
+    gy = torch.randn(b, cout, d, h, w, generator=g)
+    conv = torch.nn.Conv3d(cin, cout, 3, padding=1, bias=False).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(wt)
+    xg = x.to(DEV).requires_grad_(True)
+    assert narrow_train.applies(conv, xg)
+    y = narrow_train.conv3d(conv, xg)
+    (y * gy.to(DEV)).sum().backward()
+    x64, w64 = x.double().requires_grad_(True), wt.double().requires_grad_(True)
+    y64 = F.conv3d(x64, w64, padding=1)
+    (y64 * gy.double()).sum().backward()
+    xa, wa = x.double().abs().requires_grad_(True), wt.double().abs().requires_grad_(True)
+    ya = F.conv3d(xa, wa, padding=1)
+    (ya * gy.double().abs()).sum().backward()
+    for name, got, ref, bound in (("y", y.detach(), y64.detach(), ya.detach()), ("gx", xg.grad, x64.grad, xa.grad),
+                                  ("gw", conv.weight.grad, w64.grad, wa.grad)):
+        err = (got.double().cpu() - ref).abs()
+        assert bool((err <= 1e-5 * bound + 1e-30).all()), "%s: max err %.3g" % (name, err.max().item())
+    from mvs_amd.ops import conv3d_k3_wgrad
+    a = conv3d_k3_wgrad(xg.detach(), gy.to(DEV))
+    assert torch.equal(a, conv3d_k3_wgrad(xg.detach(), gy.to(DEV)))
+    assert torch.equal(a, conv.weight.grad)
+
+
+@pytest.mark.gpu
+def test_narrow_conv_autograd_at_cfg2_conv0_shape():
+    """conv_0_0's weight gradient at the cfg-2 volume (B=4, 32 x 192 x 128 x 160): against a float64
+    reference of 6 of its 6,912 entries (per-tap dot products of the whole volume), within 1e-5 of the
+    absolute sums."""
+    from mvs_amd.ops import conv3d_k3_wgrad
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(4, 32, 192, 128, 160, device=DEV, generator=g)
+    gy = torch.randn(4, 8, 192, 128, 160, device=DEV, generator=g)
+    dw = conv3d_k3_wgrad(x, gy)
+    xp = F.pad(x, (1, 1, 1, 1, 1, 1))
+    for co, ci, t in ((0, 0, 0), (7, 31, 26), (3, 17, 13), (5, 2, 4), (1, 30, 22), (6, 9, 8)):
+        kz, ky, kx = t // 9, (t // 3) % 3, t % 3
+        xs = xp[:, ci, kz:kz + 192, ky:ky + 128, kx:kx + 160]
+        ref = (gy[:, co].double() * xs.double()).sum().item()
+        bound = (gy[:, co].double().abs() * xs.double().abs()).sum().item()
+        assert abs(dw[co, ci, kz, ky, kx].item() - ref) <= 1e-5 * bound, (co, ci, t)

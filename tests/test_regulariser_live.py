@@ -75,6 +75,43 @@ def test_train_mode_bn_with_grad_uses_full_volume():
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("shape", [(8, 12, 16), (7, 9, 11), (5, 6, 6), (2, 3, 4), (3, 1, 5), (13, 10, 17)])
+def test_train_mode_live_autograd_equals_full_volume(shape):
+    """train.py:97-104 (model.train(), loss.backward()) through forward_live_train: the same function
+    of the volume and the parameters as forward_full, so in float64 the outputs, the gradients w.r.t.
+    the volume, every conv weight and every BN affine parameter, and the running statistics agree to
+    rounding (CostVolumeReg.live_autograd_ok routes HIP fp32 training through it)."""
+    D, h, w = shape
+    ms = [_reg(D, h, w, seed=5).double().train() for _ in range(2)]
+    cv = torch.rand(2, 32, D, h, w, generator=torch.Generator().manual_seed(D + 31 * w), dtype=torch.float64)
+    g = torch.rand(2, 1, D, h, w, generator=torch.Generator().manual_seed(h), dtype=torch.float64)
+    outs, xgrads = [], []
+    for m, fn in zip(ms, (lambda m, x: m.forward_full(x), lambda m, x: m.forward_live_train(x))):
+        x = cv.clone().requires_grad_(True)
+        y = fn(m, x)
+        (y * g).sum().backward()
+        outs.append(y.detach())
+        xgrads.append(x.grad)
+    torch.testing.assert_close(outs[1], outs[0], rtol=1e-10, atol=1e-13)
+    torch.testing.assert_close(xgrads[1], xgrads[0], rtol=1e-9, atol=1e-13)
+    p_full, p_live = dict(ms[0].named_parameters()), dict(ms[1].named_parameters())
+    for k, v in p_full.items():
+        assert p_live[k].grad is not None, k
+        scale = v.grad.abs().max().item() + 1e-30
+        assert (p_live[k].grad - v.grad).abs().max().item() <= 1e-9 * scale, k
+    s1, s2 = _bn_state(ms[1]), _bn_state(ms[0])
+    for k in s2:
+        torch.testing.assert_close(s1[k], s2[k], rtol=1e-10, atol=1e-12, msg=k)
+
+
+def test_live_autograd_route_conditions():
+    """live_autograd_ok: only on a HIP device in fp32 with grad enabled and train-mode BN (a CPU volume
+    keeps forward_full, test_train_mode_bn_with_grad_uses_full_volume); MVS_TRAIN_LIVE=0 refuses."""
+    m = _reg(8, 12, 16).train()
+    cv = torch.rand(1, 32, 8, 12, 16)
+    assert not m.live_autograd_ok(cv)
+
+
 def test_live_region_disabled_flag():
     m = _reg(8, 12, 16).eval()
     m.live_region = False
