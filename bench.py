@@ -474,10 +474,13 @@ def train_step_bench(B, V, D, H, W, device, steps):
     out = {"B": B, "V": V, "planes": D, "image_hw": [H, W], "ms_per_step": 1000.0 * dt,
            "depth_maps_per_s": B / dt, "steps": n, "first_step_ms": 1000.0 * first,
            "loss": float(loss.item()), "peak_mem_GB": torch.cuda.max_memory_allocated(device) / 1e9,
-           "note": "forward (autograd, train-mode BN, full-volume regulariser as per-tap rocBLAS GEMMs, "
-                   "mvs_amd/tap_gemm.py) + loss.py masked MAE + backward (HIP mvs::cost_volume_backward, "
-                   "tap_gemm per-tap rocBLAS GEMM conv backward) + "
-                   "Adam.step"}
+           "note": "forward (autograd, train-mode BN) + loss.py masked MAE + backward + Adam.step.  Regulariser "
+                   "on its live regions under autograd (CostVolumeReg.live_autograd_ok: the same function as the "
+                   "full-volume op sequence, float64 gradients equal, tests/test_regulariser_live.py): conv_0_0 "
+                   "/ conv_out forward, input and weight gradients on HIP kernels (mvs_amd/narrow_train.py, "
+                   "csrc/conv3d_wgrad.hip), the region convolutions as per-tap rocBLAS GEMMs on dense boxes "
+                   "(mvs_amd/tap_gemm.py; the three stride-2 convs as one); cost volume backward on "
+                   "mvs::cost_volume_backward"}
     del net, opt
     torch.cuda.empty_cache()
     return out

@@ -537,8 +537,12 @@ class CostVolumeReg(nn.Module):
         y0 = _narrow_conv(self.conv_0_0, cv)
         y0 = act(y0, _bn_train(self.BN_0, *_sums(y0), count))
         stage = []
-        for conv_a, bn in ((self.conv_1_0, self.BN_1), (self.conv_2_0, self.BN_2), (self.conv_3_0, self.BN_3)):
-            z = _conv_s2_region(cv, conv_a.weight, R2, self.pad)    # exactly 0 outside M
+        convs_a = ((self.conv_1_0, self.BN_1), (self.conv_2_0, self.BN_2), (self.conv_3_0, self.BN_3))
+        # the three stride-2 convs read the same volume over the same region R2: ONE convolution with their
+        # output channels stacked (under autograd one input layout pass, one input gradient)
+        zs = _conv_s2_region(cv, torch.cat([c.weight for c, _ in convs_a], 0), R2, self.pad)   # 0 outside M
+        zs = zs.split([c.weight.shape[0] for c, _ in convs_a], 1)
+        for z, (conv_a, bn) in zip(zs, convs_a):
             p = _bn_train(bn, *_sums(z), count)
             stage.append((act(z, p), _bn_constant(p)))              # relu(BN(0)) outside M
         lv = []
@@ -550,10 +554,11 @@ class CostVolumeReg(nn.Module):
             p = _bn_train(bn, s1 + c1, s2 + c2, count)
             lv.append(_crop_pad(act(z, p), R1, M, n))
         y1, y2, y3 = lv
+        # (the full outputs for the statistics; BN + ReLU on M only, the next layer's input)
         z = _tconv_region(y3, M, self.deconv_3_0.weight, full, self.pad)
-        y3 = _crop_pad(act(z, _bn_train(self.BN_2, *_sums(z), count)), full, M, n)
+        y3 = act(_crop_pad(z, full, M, n), _bn_train(self.BN_2, *_sums(z), count))
         z = _tconv_region(y3 + y2, M, self.deconv_2_0.weight, full, self.pad)
-        y2 = _crop_pad(act(z, _bn_train(self.BN_1, *_sums(z), count)), full, M, n)
+        y2 = act(_crop_pad(z, full, M, n), _bn_train(self.BN_1, *_sums(z), count))
         z = _tconv_region(y2 + y1, M, self.deconv_1_0.weight, full, self.pad)
         z = act(z, _bn_train(self.BN_0, *_sums(z), count)) + y0
         return self.Norm(_narrow_conv(self.conv_out, z))
@@ -839,9 +844,35 @@ def _train_conv(m, x):
 
 
 # ---- train-mode BatchNorm from sums (CostVolumeReg.forward_live_train) ----------------------
+class _SumsFn(torch.autograd.Function):
+    """(sum y, sum y^2) per channel in float64, with the backward as ONE fp32 pass
+    g1 + 2 y g2 (autograd of the plain expression broadcasts the float64 gradients over the volume:
+    float64 temporaries of twice its size, cfg 2 8 ms per 32-channel pass)."""
+
+    @staticmethod
+    def forward(ctx, y, cdim):
+        red = [d for d in range(y.dim()) if d != cdim]
+        ctx.save_for_backward(y)
+        ctx.cdim = cdim
+        return y.sum(red, dtype=torch.float64), (y * y).sum(red, dtype=torch.float64)
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        (y,) = ctx.saved_tensors
+        shape = [1] * y.dim()
+        shape[ctx.cdim] = -1
+        c = y.shape[ctx.cdim]
+        g1 = (torch.zeros(c, dtype=y.dtype, device=y.device) if g1 is None else g1.to(y.dtype)).view(shape)
+        g2 = (torch.zeros(c, dtype=y.dtype, device=y.device) if g2 is None else g2.to(y.dtype)).view(shape)
+        return torch.addcmul(g1, y, 2.0 * g2), None
+
+
 def _sums(y, cdim=1):
     """Per-channel sum and sum of squares of y (channels on dim cdim) in float64."""
-    red = [d for d in range(y.dim()) if d != cdim % y.dim()]
+    cdim = cdim % y.dim()
+    if torch.is_grad_enabled() and y.requires_grad:
+        return _SumsFn.apply(y, cdim)
+    red = [d for d in range(y.dim()) if d != cdim]
     return y.sum(red, dtype=torch.float64), (y * y).sum(red, dtype=torch.float64)
 
 
@@ -1005,20 +1036,17 @@ def _crop_pad(x, x_reg, want, n):
     return F.pad(y, flat) if any(flat) else y
 
 
+def _taps(x):
+    """The live-region helpers' convolutions go through the per-tap GEMMs (tap_gemm: MIOpen's backward
+    solvers for these shapes are naive): under autograd on a HIP device in fp32."""
+    return x.is_cuda and torch.is_grad_enabled() and x.dtype == torch.float32 and not torch.is_autocast_enabled()
+
+
 def _region_conv3d(x, weight, stride, padding):
-    """F.conv3d of the live-region helpers; under autograd on a HIP device in fp32 the per-tap GEMMs
-    (tap_gemm.conv3d: MIOpen's backward solvers for these shapes are naive)."""
-    if x.is_cuda and torch.is_grad_enabled() and x.dtype == torch.float32 and not torch.is_autocast_enabled():
+    if _taps(x):
         from . import tap_gemm
         return tap_gemm.conv3d(x, weight, stride, padding)
     return F.conv3d(x, weight, stride=stride, padding=padding)
-
-
-def _region_conv_transpose3d(x, weight, stride):
-    if x.is_cuda and torch.is_grad_enabled() and x.dtype == torch.float32 and not torch.is_autocast_enabled():
-        from . import tap_gemm
-        return tap_gemm.conv_transpose3d(x, weight, stride)
-    return F.conv_transpose3d(x, weight, stride=stride)
 
 
 def _conv_s2_region(x, weight, out_reg, pad):
@@ -1030,6 +1058,20 @@ def _conv_s2_region(x, weight, out_reg, pad):
     p of the left overhang's parity (so the stride-2 grid stays aligned), and the wanted outputs
     are sliced out: every kept output reads exactly its own window."""
     n = tuple(x.shape[2:])
+    if _taps(x):
+        # the box itself as a dense tensor: output j - lo reads inputs 2 (j - lo) - pad_lo + t of the crop
+        # starting at max(2 lo - P, 0) (tap_gemm.conv3d_box)
+        from . import tap_gemm
+        sl, pl = [], []
+        for (lo, hi), p, d in zip(out_reg, pad, n):
+            a, b = 2 * lo - p, 2 * hi - p + 2
+            ca, cb = max(a, 0), min(b, d - 1)
+            assert ca <= cb, "output box reads no input"
+            sl.append(slice(ca, cb + 1))
+            pl.append(ca - a)
+        if any(s_.start != 0 or s_.stop != d for s_, d in zip(sl, n)):   # (a whole-extent slice: no copy
+            x = x[:, :, sl[0], sl[1], sl[2]]                             # back in the backward)
+        return tap_gemm.conv3d_box(x, weight, 2, tuple(pl), tuple(hi - lo + 1 for lo, hi in out_reg))
     sl, pads, offs = [], [], []
     for (lo, hi), p, d in zip(out_reg, pad, n):
         a, b = 2 * lo - p, 2 * hi - p + 2
@@ -1056,7 +1098,15 @@ def _conv_s1_region(x, x_reg, weight, out_reg, n):
 def _tconv_region(x, x_reg, weight, out_reg, pad):
     """conv_transpose3d(., weight, stride 2, padding pad) on out_reg, from the region tensor x on
     x_reg (which must hold every input that reaches out_reg: _tconv_input_region)."""
-    y = _region_conv_transpose3d(x, weight, 2)   # output q <-> volume index 2 * xlo + q - P
+    if _taps(x):
+        # the box as a dense tensor (tap_gemm.conv_transpose3d_box: outputs past the inputs' reach are 0)
+        from . import tap_gemm
+        crop = []
+        for (xlo, _), (lo, hi), p in zip(x_reg, out_reg, pad):
+            assert lo - (2 * xlo - p) >= 0, "transposed-conv input region starts after the output box"
+            crop.append(lo - (2 * xlo - p))
+        return tap_gemm.conv_transpose3d_box(x, weight, 2, tuple(crop), tuple(hi - lo + 1 for lo, hi in out_reg))
+    y = F.conv_transpose3d(x, weight, stride=2)   # output q <-> volume index 2 * xlo + q - P
     sl, pads = [], []
     for (xlo, _), (lo, hi), p, m in zip(x_reg, out_reg, pad, y.shape[2:]):
         o0 = 2 * xlo - p

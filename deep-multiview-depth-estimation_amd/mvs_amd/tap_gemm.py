@@ -164,8 +164,8 @@ class _Geom:
 _KSPLIT = 256   # row chunks of the weight-gradient GEMMs
 
 
-def _cl(x):   # [N, C, D, H, W] -> channels-last contiguous [N, D, H, W, C]
-    return x.permute(0, 2, 3, 4, 1).contiguous()
+def _cl(x):   # [N, C, D, H, W] -> channels-last view [N, D, H, W, C] (to_par / to_grid copy it once)
+    return x.permute(0, 2, 3, 4, 1)
 
 
 def _cf(x):   # channels-last [N, D, H, W, C] -> [N, C, D, H, W] view in channels_last_3d strides
@@ -175,10 +175,11 @@ def _cf(x):   # channels-last [N, D, H, W, C] -> [N, C, D, H, W] view in channel
 
 class _Conv3dTaps(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, padding):
+    def forward(ctx, x, w, stride, padding, out_size=None):
         s, p, k = _t3(stride), _t3(padding), tuple(w.shape[2:])
         n = tuple(x.shape[2:])
-        out_n = tuple((d + 2 * pp - kk) // ss + 1 for d, pp, kk, ss in zip(n, p, k, s))
+        out_n = (tuple((d + 2 * pp - kk) // ss + 1 for d, pp, kk, ss in zip(n, p, k, s)) if out_size is None
+                 else tuple(out_size))
         g = _Geom(n, out_n, k, s, p)
         N = x.shape[0]
         ctx.save_for_backward(x, w)
@@ -186,6 +187,7 @@ class _Conv3dTaps(torch.autograd.Function):
         if g.empty:
             return x.new_zeros((N, w.shape[0]) + out_n)
         P = g.to_par(_cl(x))
+        ctx.par = P   # the weight gradient's operand: kept instead of formed again from x
         Y = g.forward(P, lambda t: w[(slice(None), slice(None)) + t].t())
         return _cf(g.from_grid(Y, N))
 
@@ -197,29 +199,32 @@ class _Conv3dTaps(torch.autograd.Function):
         gx = gw = None
         if g.empty:
             return (torch.zeros_like(x) if ctx.needs_input_grad[0] else None,
-                    torch.zeros_like(w) if ctx.needs_input_grad[1] else None, None, None)
+                    torch.zeros_like(w) if ctx.needs_input_grad[1] else None, None, None, None)
         G = g.to_grid(_cl(gy))
         if ctx.needs_input_grad[0]:
             gP = g.scatter(G, lambda t: w[(slice(None), slice(None)) + t], x.shape[1])
             gx = _cf(g.from_par(gP, N))
         if ctx.needs_input_grad[1]:
-            P = g.to_par(_cl(x))
+            P = getattr(ctx, "par", None)
+            P = g.to_par(_cl(x)) if P is None else P
             gw = torch.zeros_like(w)
 
             def put(t, v):
                 gw[(slice(None), slice(None)) + t] = v
             g.weight_grad(G, P, put)
-        return gx, gw, None, None
+        ctx.par = None
+        return gx, gw, None, None, None
 
 
 class _ConvTranspose3dTaps(torch.autograd.Function):
     """conv_transpose3d(x) = d/dx of the conv3d g (input extent = this output's, output extent = n)."""
 
     @staticmethod
-    def forward(ctx, x, w, stride, padding, output_padding):
+    def forward(ctx, x, w, stride, padding, output_padding, out_size=None):
         s, p, op, k = _t3(stride), _t3(padding), _t3(output_padding), tuple(w.shape[2:])
         n = tuple(x.shape[2:])
-        out_n = tuple((d - 1) * ss - 2 * pp + kk + oo for d, ss, pp, kk, oo in zip(n, s, p, k, op))
+        out_n = (tuple((d - 1) * ss - 2 * pp + kk + oo for d, ss, pp, kk, oo in zip(n, s, p, k, op))
+                 if out_size is None else tuple(out_size))
         g = _Geom(out_n, n, k, s, p)
         N = x.shape[0]
         ctx.save_for_backward(x, w)
@@ -238,7 +243,7 @@ class _ConvTranspose3dTaps(torch.autograd.Function):
         gx = gw = None
         if g.empty:
             return (torch.zeros_like(x) if ctx.needs_input_grad[0] else None,
-                    torch.zeros_like(w) if ctx.needs_input_grad[1] else None, None, None, None)
+                    torch.zeros_like(w) if ctx.needs_input_grad[1] else None, None, None, None, None)
         P = g.to_par(_cl(gy))
         if ctx.needs_input_grad[0]:
             Y = g.forward(P, lambda t: w[(slice(None), slice(None)) + t].t())
@@ -250,7 +255,7 @@ class _ConvTranspose3dTaps(torch.autograd.Function):
             def put(t, v):
                 gw[(slice(None), slice(None)) + t] = v
             g.weight_grad(G, P, put)
-        return gx, gw, None, None, None
+        return gx, gw, None, None, None, None
 
 
 def conv3d(x, weight, stride=1, padding=0):
@@ -261,6 +266,19 @@ def conv3d(x, weight, stride=1, padding=0):
 def conv_transpose3d(x, weight, stride=1, padding=0, output_padding=0):
     """F.conv_transpose3d (groups 1, dilation 1, no bias) through per-tap GEMMs, differentiable."""
     return _ConvTranspose3dTaps.apply(x, weight, stride, padding, output_padding)
+
+
+def conv3d_box(x, weight, stride, pad_lo, out_size):
+    """Outputs [0, out_size) of a conv3d whose output u reads inputs u * stride - pad_lo + t (pad_lo >= 0:
+    zeros before the input; past its end likewise): a box of a padded convolution's output computed as
+    a dense tensor (no slice of a larger output)."""
+    return _Conv3dTaps.apply(x, weight, stride, pad_lo, out_size)
+
+
+def conv_transpose3d_box(x, weight, stride, crop_lo, out_size):
+    """Outputs [crop_lo, crop_lo + out_size) of the unpadded conv_transpose3d(x, weight, stride) (input i
+    reaches outputs i * stride + t), as a dense tensor; outputs past the last input's reach are 0."""
+    return _ConvTranspose3dTaps.apply(x, weight, stride, crop_lo, 0, out_size)
 
 
 def conv_module(m, x):

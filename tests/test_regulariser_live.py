@@ -75,12 +75,18 @@ def test_train_mode_bn_with_grad_uses_full_volume():
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("taps", [False, True])
 @pytest.mark.parametrize("shape", [(8, 12, 16), (7, 9, 11), (5, 6, 6), (2, 3, 4), (3, 1, 5), (13, 10, 17)])
-def test_train_mode_live_autograd_equals_full_volume(shape):
+def test_train_mode_live_autograd_equals_full_volume(shape, taps, monkeypatch):
     """train.py:97-104 (model.train(), loss.backward()) through forward_live_train: the same function
     of the volume and the parameters as forward_full, so in float64 the outputs, the gradients w.r.t.
     the volume, every conv weight and every BN affine parameter, and the running statistics agree to
-    rounding (CostVolumeReg.live_autograd_ok routes HIP fp32 training through it)."""
+    rounding (CostVolumeReg.live_autograd_ok routes HIP fp32 training through it).  ``taps``: the
+    region convolutions through the HIP path's per-tap GEMM boxes (tap_gemm.conv3d_box /
+    conv_transpose3d_box), here in float64 on the CPU."""
+    if taps:
+        from mvs_amd import model as model_mod
+        monkeypatch.setattr(model_mod, "_taps", lambda x: torch.is_grad_enabled())
     D, h, w = shape
     ms = [_reg(D, h, w, seed=5).double().train() for _ in range(2)]
     cv = torch.rand(2, 32, D, h, w, generator=torch.Generator().manual_seed(D + 31 * w), dtype=torch.float64)

@@ -58,3 +58,52 @@ def test_conv_module_dispatch():
     torch.testing.assert_close(tap_gemm.conv_module(c, x), c(x), rtol=1e-12, atol=1e-12)
     z = torch.randn(1, 2, 4, 5, 6, dtype=torch.float64)
     torch.testing.assert_close(tap_gemm.conv_module(t, z), t(z), rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("n,pad_lo,out", [((9, 7, 11), (2, 0, 3), (5, 4, 6)), ((6, 5, 8), (1, 1, 1), (4, 3, 5)),
+                                          ((7, 7, 7), (0, 2, 1), (2, 6, 4))])
+def test_conv3d_box_matches_sliced_padded_conv(n, pad_lo, out):
+    """tap_gemm.conv3d_box: a box of a padded stride-2 convolution's output as a dense tensor, values
+    and gradients against F.conv3d on an explicitly padded input, sliced (float64)."""
+    from mvs_amd import tap_gemm
+    g = torch.Generator().manual_seed(sum(n))
+    x = torch.randn((2, 3) + n, generator=g, dtype=torch.float64)
+    w = torch.randn(4, 3, 3, 3, 3, generator=g, dtype=torch.float64)
+    gy = torch.randn((2, 4) + out, generator=g, dtype=torch.float64)
+    xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    ya = tap_gemm.conv3d_box(xa, wa, 2, pad_lo, out)
+    (ya * gy).sum().backward()
+    xb, wb = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    # explicit padding: pad_lo before, enough after for every output's window
+    after = [max(0, 2 * (o - 1) + 3 - pl - d) for o, pl, d in zip(out, pad_lo, n)]
+    xp = torch.nn.functional.pad(xb, (pad_lo[2], after[2], pad_lo[1], after[1], pad_lo[0], after[0]))
+    yb = torch.nn.functional.conv3d(xp, wb, stride=2)[:, :, :out[0], :out[1], :out[2]]
+    (yb * gy).sum().backward()
+    torch.testing.assert_close(ya, yb)
+    torch.testing.assert_close(xa.grad, xb.grad)
+    torch.testing.assert_close(wa.grad, wb.grad)
+
+
+@pytest.mark.parametrize("n,crop,out", [((4, 3, 5), (1, 0, 2), (7, 6, 9)), ((3, 4, 4), (0, 1, 1), (8, 7, 9)),
+                                        ((5, 2, 3), (2, 1, 0), (6, 5, 8))])
+def test_conv_transpose3d_box_matches_sliced(n, crop, out):
+    """tap_gemm.conv_transpose3d_box: outputs [crop, crop + out) of the unpadded stride-2 transposed conv
+    (zeros past its extent), values and gradients against F.conv_transpose3d, sliced / zero padded."""
+    from mvs_amd import tap_gemm
+    g = torch.Generator().manual_seed(sum(n) + 7)
+    x = torch.randn((2, 4) + n, generator=g, dtype=torch.float64)
+    w = torch.randn(4, 3, 3, 3, 3, generator=g, dtype=torch.float64)
+    gy = torch.randn((2, 3) + out, generator=g, dtype=torch.float64)
+    xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    ya = tap_gemm.conv_transpose3d_box(xa, wa, 2, crop, out)
+    (ya * gy).sum().backward()
+    xb, wb = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    full = torch.nn.functional.conv_transpose3d(xb, wb, stride=2)
+    full = torch.nn.functional.pad(full, (0, max(0, crop[2] + out[2] - full.shape[4]), 0,
+                                          max(0, crop[1] + out[1] - full.shape[3]), 0,
+                                          max(0, crop[0] + out[0] - full.shape[2])))
+    yb = full[:, :, crop[0]:crop[0] + out[0], crop[1]:crop[1] + out[1], crop[2]:crop[2] + out[2]]
+    (yb * gy).sum().backward()
+    torch.testing.assert_close(ya, yb)
+    torch.testing.assert_close(xa.grad, xb.grad)
+    torch.testing.assert_close(wa.grad, wb.grad)

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--full", action="store_true")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--prof", action="store_true")
+    ap.add_argument("--ops", action="store_true", help="with --prof: aten ops grouped by input shape")
     a = ap.parse_args()
     if a.full:
         os.environ["MVS_TRAIN_LIVE"] = "0"
@@ -39,10 +40,15 @@ def main():
             opt.step()
         step()
         torch.cuda.synchronize()
-        with profile(activities=[ProfilerActivity.CUDA]) as p:
+        acts = [ProfilerActivity.CUDA] + ([ProfilerActivity.CPU] if a.ops else [])
+        with profile(activities=acts, record_shapes=a.ops) as p:
             step()
             torch.cuda.synchronize()
         print(p.key_averages().table(sort_by="cuda_time_total", row_limit=30, max_name_column_width=70), flush=True)
+        if a.ops:
+            print(p.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=45,
+                                                                  max_name_column_width=40,
+                                                                  max_shapes_column_width=110), flush=True)
 
 
 if __name__ == "__main__":
