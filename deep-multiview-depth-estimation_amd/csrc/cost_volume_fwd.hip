@@ -21,6 +21,8 @@
 //   * a plane group whose union footprint does not fit the 40 KB LDS budget is processed plane by
 //     plane; a plane that still does not fit samples straight from the packed global features.
 // Workgroup ids are remapped so each XCD walks consecutive (tile, plane group) items.
+#include <cstdlib>
+
 #include "launchers.h"
 #include "split.h"
 #include "packed.h"
@@ -166,9 +168,15 @@ __global__ __launch_bounds__(kBlock) void prologue_kernel(const float* __restric
   const int bc = blk / pblocks;   // b * c4 + ch
   const uint32_t p = (uint32_t)(blk - bc * pblocks) * kBlock + threadIdx.x;
   const int ch = bc % c4, b = bc / c4;
+  // the reference image's matrix once per workgroup (fp64, ~1k instructions: per thread it set the
+  // prologue's duration -- cfg 2 34 us, cfg 3 63 us)
+  __shared__ float Gs[9];
+  if (threadIdx.x == 0) sampling_matrix(cm, B, V, h, w, b * V, 0, Gs);
+  __syncthreads();   // (before the pixel-range exit: every thread of the workgroup reaches it)
   if (p >= hw) return;
   float G[9];
-  sampling_matrix(cm, B, V, h, w, b * V, 0, G);
+#pragma unroll
+  for (int e = 0; e < 9; ++e) G[e] = Gs[e];
   const int y = (int)(p / (uint32_t)w), x = (int)(p % (uint32_t)w);
   uint32_t pos;
   float wx, wy;
@@ -338,7 +346,7 @@ template <int V, int KPG, int ES /* output layout: 4 fp32, 2 bf16, 16 / 8 / kQua
 __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_kernel(
     const float4* __restrict__ packed, const float4* __restrict__ refs,
     const float* __restrict__ sampling, void* __restrict__ cv, int C, int h, int w, int Dc, int pg_n,
-    int tiles_x, int tiles_y, int groups, int total, const uint32_t* __restrict__ absmax) {
+    int tiles_x, int tiles_y, int groups, int total, const uint32_t* __restrict__ absmax, int csplit) {
   constexpr int NS = V - 1;
   constexpr int SLOTS = staged_slots<V>();
   __shared__ f4v lds[SLOTS];
@@ -349,8 +357,11 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   // workgroups per CU.
   int* scratch = reinterpret_cast<int*>(&lds[SLOTS - (4 * 4 * NS + 3) / 4]);
 
-  const int wk = xcd_work_id(blockIdx.x, total);
-  if (wk >= total) return;   // workgroup-uniform
+  const int wk0 = xcd_work_id(blockIdx.x, total);
+  if (wk0 >= total) return;   // workgroup-uniform
+  // csplit > 1 (small plane shards): the channel chunks split over csplit workgroups per (tile, group)
+  const int cpart = wk0 % csplit;
+  const int wk = wk0 / csplit;
   const int g = wk % groups;
   const int t = wk / groups;
   const int tile = t % (tiles_x * tiles_y);
@@ -363,6 +374,7 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
   const int npl = min(pg_n, Dc - k0);
   const uint32_t hw = (uint32_t)h * (uint32_t)w;
   const int c4 = (C + 3) / 4;
+  const int ch_lo = (int)(((long)c4 * cpart) / csplit), ch_hi = (int)(((long)c4 * (cpart + 1)) / csplit);
   const PadGeom pg = pad_geom(h, w);
   const float xn = norm_coord(active ? px : 0, w);
   const float yn = norm_coord(active ? py : 0, h);
@@ -502,7 +514,7 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
 #pragma unroll
     for (int s = 0; s < NS; ++s)
       rs[s] = make_rsrc(packed + (size_t)(b * V + 1 + s) * c4 * pg.plane, (uint32_t)c4 * pg.plane * 16u);
-    for (int ch = 0; ch < c4; ++ch) {
+    for (int ch = ch_lo; ch < ch_hi; ++ch) {
       const float4 r4 = rbase[(size_t)ch * hw];
       const f4v x0 = {r4.x, r4.y, r4.z, r4.w};
       const int soff = (int)((uint32_t)ch * pg.plane * 16u);
@@ -591,7 +603,7 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
     for (int j = 0; j < kPrefetch; ++j)
       pre[j] = pbase[psrc[j] + (uint32_t)ch * pg.plane];
   };
-  prefetch(0);
+  prefetch(ch_lo);
 
   // Staging of chunk ch from the prefetch registers (and the pieces beyond them) into LDS.  It runs
   // right after the previous chunk's stores, and consumes only loads issued BEFORE those stores:
@@ -631,12 +643,12 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
       for (int u = 0; u < 4; ++u) lds[slot[u]] = f4v{v[u].x, v[u].y, v[u].z, v[u].w};
     }
   };
-  stage(0);
+  stage(ch_lo);
 
-  for (int ch = 0; ch < c4; ++ch) {
+  for (int ch = ch_lo; ch < ch_hi; ++ch) {
     __syncthreads();   // chunk ch is in LDS
     const f4v xr = x0;
-    if (ch + 1 < c4) prefetch(ch + 1);   // in flight during this chunk's stores
+    if (ch + 1 < ch_hi) prefetch(ch + 1);   // in flight during this chunk's stores
     Rsrc ors[4];
     chunk_rsrc(ch, ors);
 #pragma unroll
@@ -658,7 +670,7 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
       }
       emit(pl, ors, xr, xs);
     }
-    if (ch + 1 < c4) {
+    if (ch + 1 < ch_hi) {
       __syncthreads();   // every wave is done reading chunk ch
       stage(ch + 1);
     }
@@ -671,15 +683,16 @@ __global__ __launch_bounds__(kBlock) MVS_STAGED_ATTR void cost_volume_staged_ker
 template <int V, int KPG, int ES>
 void launch_staged(int pg, dim3 grid, hipStream_t s, const float4* packed, const float4* refs,
                    const float* smp, void* cv, const Geometry& g, int tiles_x, int tiles_y, int groups,
-                   int total, const uint32_t* absmax) {
+                   int total, const uint32_t* absmax, int csplit) {
   if constexpr (KPG > 1) {
     if (pg < KPG) {
-      launch_staged<V, KPG / 2, ES>(pg, grid, s, packed, refs, smp, cv, g, tiles_x, tiles_y, groups, total, absmax);
+      launch_staged<V, KPG / 2, ES>(pg, grid, s, packed, refs, smp, cv, g, tiles_x, tiles_y, groups, total, absmax,
+                                    csplit);
       return;
     }
   }
   hipLaunchKernelGGL((cost_volume_staged_kernel<V, KPG, ES>), grid, dim3(kBlock), 0, s, packed, refs, smp, cv,
-                     g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total, absmax);
+                     g.C, g.h, g.w, g.Dc, pg, tiles_x, tiles_y, groups, total, absmax, csplit);
 }
 
 template <int V, int ES>
@@ -709,12 +722,21 @@ void launch_gather(const Geometry& g, const float* feat, const Cams& cm, float* 
   // (cfg 4, 32-plane shards: 0.128 ms with the 8-plane template at pg = 1, 0.044 ms at pg = 2)
   constexpr long kMinWorkgroups = 1024;
   int pg = group_planes<V>();
-  while (pg > 1 && (long)g.B * tiles_x * tiles_y * ((g.Dc + pg - 1) / pg) < kMinWorkgroups) pg >>= 1;
+  // small shards: the channel chunks split over 2 workgroups per (tile, plane group) (MVS_CV_CSPLIT, 1..8),
+  // then the plane group halved until the grid has the workgroups -- cfg 4's 32-plane shard: 4-plane
+  // groups, 2 chunk halves, 43 us against 47 us for 2-plane groups (4: 51, 8: 57 us; gpurun_out r6s)
+  static const int csplit_env = [] {
+    const char* e = getenv("MVS_CV_CSPLIT");
+    const int v = e ? atoi(e) : 2;
+    return v < 1 ? 1 : (v > 8 ? 8 : v);
+  }();
+  const int csplit = (long)g.B * tiles_x * tiles_y * ((g.Dc + pg - 1) / pg) < kMinWorkgroups ? csplit_env : 1;
+  while (pg > 1 && (long)g.B * tiles_x * tiles_y * ((g.Dc + pg - 1) / pg) * csplit < kMinWorkgroups) pg >>= 1;
   const int groups = (g.Dc + pg - 1) / pg;
-  const int total = g.B * tiles_x * tiles_y * groups;
+  const int total = g.B * tiles_x * tiles_y * groups * csplit;
   if (ev0) (void)hipEventRecord(ev0, s);
   launch_staged<V, group_planes<V>(), ES>(pg, xcd_grid(total), s, packed, refs, smp, cv, g, tiles_x, tiles_y,
-                                         groups, total, absmax);
+                                         groups, total, absmax, csplit);
   if (ev1) (void)hipEventRecord(ev1, s);
 }
 

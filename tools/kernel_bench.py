@@ -27,7 +27,8 @@ def main():
         C = int(os.environ.get("MVS_BENCH_C", "32"))   # channel-count sweeps (set-up vs per-chunk cost)
         bf16 = os.environ.get("MVS_BENCH_BF16") == "1"
         quads = os.environ.get("MVS_BENCH_C4") == "1"   # channel-quad store (inference feed)
-        ms, op_ms, alg = bench.time_kernel(B, V, C, h, w, D, dev, 20, 0, dc, bf16=bf16, quads=quads)
+        store = "c4" if quads and not bf16 else "ncdhw"   # (fp32 channel quads: the inference step's store)
+        ms, op_ms, alg = bench.time_kernel(B, V, C, h, w, D, dev, 20, 0, dc, bf16=bf16, quads=quads, store=store)
         ms = op_ms if ms is None else ms
         gbs = alg / (ms * 1e-3) / 1e9
         print(json.dumps({"cfg": name, "C": C, "B": B, "V": V, "hw": [h, w], "D": dc, "ms": round(ms, 4),
