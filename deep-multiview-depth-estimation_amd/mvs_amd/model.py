@@ -58,6 +58,14 @@ def _run_stack(seq, x, split_f16=False):
     with the running statistics updated as torch does.  Elsewhere the modules themselves.
     ``split_f16`` (MVSConfig(arithmetic="split_f16"), opt-in): the 8..32-channel layers on the f16
     matrix cores with split operands (csrc/conv2d_split.hip)."""
+    if _taps(x) and os.environ.get("MVS_TRAIN_CONV2D", "taps") == "taps":
+        # under autograd on a HIP device (train.py:97-104): the convolutions as per-tap rocBLAS GEMMs
+        # (tap_gemm.conv2d), not MIOpen's (its first training step compiles its kernels: ~40 s at cfg 2)
+        from . import tap_gemm
+        for layer in seq:
+            x = (tap_gemm.conv2d(x, layer.weight, layer.stride, layer.padding)
+                 if isinstance(layer, nn.Conv2d) and tap_gemm.conv2d_applies(layer) else layer(x))
+        return x
     if not _hip_inference(x):
         return seq(x)
     from .ops import (CONV2D_SPLIT_SHAPES, bn_relu_, bound_words, channel_stats, conv2d, conv2d_split,

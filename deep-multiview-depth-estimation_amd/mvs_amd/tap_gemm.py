@@ -281,6 +281,20 @@ def conv_transpose3d_box(x, weight, stride, crop_lo, out_size):
     return _ConvTranspose3dTaps.apply(x, weight, stride, crop_lo, 0, out_size)
 
 
+def conv2d(x, weight, stride=1, padding=0):
+    """F.conv2d (groups 1, dilation 1, no bias) through the per-tap GEMMs: the conv3d of depth 1."""
+    s, p = (stride, stride) if isinstance(stride, int) else tuple(stride), \
+        (padding, padding) if isinstance(padding, int) else tuple(padding)
+    y = _Conv3dTaps.apply(x.unsqueeze(2), weight.unsqueeze(2), (1,) + tuple(s), (0,) + tuple(p))
+    return y.squeeze(2).contiguous()   # NCHW: the BatchNorm2d after it takes MIOpen's NCHW kernels
+
+
+def conv2d_applies(m):
+    """An nn.Conv2d the per-tap GEMMs run: no bias, groups 1, dilation 1, numeric padding."""
+    return (m.bias is None and m.groups == 1 and tuple(m.dilation) == (1, 1)
+            and not isinstance(m.padding, str))
+
+
 def conv_module(m, x):
     """nn.Conv3d / nn.ConvTranspose3d module ``m`` applied through the tap GEMMs."""
     if m.bias is not None or m.groups != 1 or _t3(m.dilation) != (1, 1, 1):

@@ -107,3 +107,23 @@ def test_conv_transpose3d_box_matches_sliced(n, crop, out):
     torch.testing.assert_close(ya, yb)
     torch.testing.assert_close(xa.grad, xb.grad)
     torch.testing.assert_close(wa.grad, wb.grad)
+
+
+@pytest.mark.parametrize("cin,cout,k,s,hw", [(3, 8, 3, 1, (13, 17)), (8, 16, 5, 2, (20, 25)), (16, 32, 3, 1, (9, 7)),
+                                             (32, 32, 3, 2, (11, 14))])
+def test_conv2d_taps_matches_torch(cin, cout, k, s, hw):
+    """tap_gemm.conv2d (the encoder / refinement Conv2d under autograd on a HIP device): values and
+    gradients against F.conv2d in float64, the reference's kernel / stride / padding k // 2."""
+    g = torch.Generator().manual_seed(cin + k)
+    x = torch.randn((2, cin) + hw, generator=g, dtype=torch.float64)
+    w = torch.randn(cout, cin, k, k, generator=g, dtype=torch.float64)
+    xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    ya = tap_gemm.conv2d(xa, wa, s, k // 2)
+    gy = torch.randn(ya.shape, generator=g, dtype=torch.float64)
+    (ya * gy).sum().backward()
+    xb, wb = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    yb = F.conv2d(xb, wb, stride=s, padding=k // 2)
+    (yb * gy).sum().backward()
+    torch.testing.assert_close(ya, yb)
+    torch.testing.assert_close(xa.grad, xb.grad)
+    torch.testing.assert_close(wa.grad, wb.grad)
