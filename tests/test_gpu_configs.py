@@ -174,12 +174,13 @@ def _depth_parity(P_gpu, P_ref, d_gpu, d_ref):
 
 
 def _flip_quantiles(rel, flip):
-    """Relative depth error on the mask-flipped pixels: p50 / p99 / max and their count (0s when none)."""
+    """Relative depth error on the mask-flipped pixels: p50 / p99 / max, their count (0s when none) and
+    the largest ones in descending order ("top", at most 256: the order statistics the criterion uses)."""
     r = rel[flip]
     if r.size == 0:
-        return {"n": 0, "p50": 0.0, "p99": 0.0, "max": 0.0}
+        return {"n": 0, "p50": 0.0, "p99": 0.0, "max": 0.0, "top": []}
     return {"n": int(r.size), "p50": float(np.quantile(r, 0.5)), "p99": float(np.quantile(r, 0.99)),
-            "max": float(r.max())}
+            "max": float(r.max()), "top": [float(v) for v in np.sort(r)[::-1][:256]]}
 
 
 def _reference_flip_quantiles_cfg2(with_rel=False):
@@ -210,16 +211,22 @@ def _tail_fracs(rel):
 def _flips_within_reference(gq, rq, g_rel, r_rel, what):
     """Every pixel of the map under the reference's own noise, against one yardstick
     (the float64 law at cfg 2, the fp64-matrix fixture at cfg 5):
-      * the flipped pixels: the GPU's relative depth error on its flips no larger than the reference's own
-        on ITS flips at the top of the distribution (p99 and max);
+      * the flipped pixels, by order statistics: the GPU's k-th largest flipped-pixel error no larger than
+        the reference's own k-th largest on ITS flips, for every k up to the GPU's flip count (which
+        includes max and, for the GPU's own count, its p99) -- and no more GPU flips than the reference's
+        beyond that;
       * the whole map: for every threshold t of TAIL_T (1e-4 ... 5e-2) the share of pixels off by more
         than t no larger for the GPU than for the reference -- flipped and unflipped pixels alike.
-    The flipped pixels' median is recorded, not asserted: the GPU flips 4-40x fewer pixels than the
-    reference (39 against 159 at cfg 2, 66 against 2,648 at cfg 5, r6d), and a flip's error is the depth
-    jump of swapping two near-tied planes -- a property of the network's probabilities (GPU 0.52 % /
-    0.61 %, reference 0.49 % / 0.55 % at the median), which the whole-map criterion bounds instead."""
-    for k in ("p99", "max"):
-        assert gq[k] <= rq[k], (what, k, gq, rq)
+    Quantiles of the two flip sets are recorded, not compared: the GPU flips 4-40x fewer pixels than the
+    reference (39 against 159 at cfg 2, 66 against 2,648 at cfg 5, r6d), so a p99 of 66 values is their
+    second largest, against the 27th largest of 2,648 (r6w: 0.083 against 0.077 at cfg 5 while the GPU's
+    largest, 0.084, is half the reference's 0.158).  A flip's error is the depth jump of swapping two
+    near-tied planes -- a property of the network's probabilities (GPU 0.52 % / 0.61 %, reference 0.49 % /
+    0.55 % at the median)."""
+    g_top, r_top = gq.get("top", []), rq.get("top", [])
+    assert len(g_top) <= len(r_top) or gq["n"] <= rq["n"], (what, "more flips than the reference", gq["n"], rq["n"])
+    for k, v in enumerate(g_top[:len(r_top)]):
+        assert v <= r_top[k], (what, "k-th largest flipped-pixel error", k, v, r_top[k], gq["n"], rq["n"])
     gt, rt = _tail_fracs(g_rel), _tail_fracs(r_rel)
     assert all(a <= b for a, b in zip(gt, rt)), (what, "tail shares", dict(zip(TAIL_T, gt)), dict(zip(TAIL_T, rt)))
 

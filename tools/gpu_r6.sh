@@ -1,5 +1,6 @@
 #!/bin/bash
-# round 6 GPU driver: bash tools/gpu_r6.sh <tag> [stages...]   stages: tests smoke bench prof pmc (default all)
+# round 6 GPU driver: bash tools/gpu_r6.sh <tag> [stages...]   stages: tests smoke bench prof cfgprof evalprof pmc
+#   (default: tests smoke bench prof pmc)
 #   tests  full GPU suite (+ parity records under $OUT/parity)
 #   smoke  __graft_entry__.smoke()
 #   bench  python bench.py (N=1 defaults) -> $OUT/bench.json
@@ -41,6 +42,18 @@ if has prof; then
     python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra --no-train-step > $OUT/prof_bench.json 2> $OUT/prof_bench.err
   rc=$?; echo "prof rc=$rc"; [ $rc -ne 0 ] && exit $rc
   f=$(ls $OUT/prof/*/run_kernel_stats.csv $OUT/prof/run_kernel_stats.csv 2>/dev/null | head -1); head -14 "$f" | cut -c1-160
+fi
+if has cfgprof; then   # per-config warp-kernel stats (bench kernel_configs legs: cfg 3/5 channel quads, cfg 4 NCDHW)
+  for c in 2 3 4 5; do
+    q=1; [ $c = 4 ] && q=0
+    MVS_BENCH_C4=$q timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/cfg$c" \
+      -o cfg$c -- python3 tools/kernel_bench.py $c > $OUT/cfg$c.log 2>&1; rc=$?
+    echo "cfgprof $c rc=$rc"; grep '^{' $OUT/cfg$c.log; [ $rc -ne 0 ] && exit $rc
+  done
+fi
+if has evalprof; then   # the value leg alone: fp32 cfg-2 eval steps (tools/eval_steps.py)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/eval" -o eval -- \
+    python3 tools/eval_steps.py --steps 10 > $OUT/evalprof.log 2>&1; rc=$?; echo "evalprof rc=$rc"; [ $rc -ne 0 ] && exit $rc
 fi
 if has pmc; then
   i=0
