@@ -670,8 +670,10 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
   if (!x || !weight || !y || !dims || !out_origin || !out_size || batch <= 0) return MVS_ERR_INVALID_ARGUMENT;
   if ((uintptr_t)y_bound & 3u) return MVS_ERR_INVALID_ARGUMENT;
   if (mode < MVS_CONV_S1 || mode > MVS_CONV_T2 ||
-      (flags & ~(MVS_CONV_OUT_NCDHW | MVS_CONV_IN_C4 | MVS_CONV_IN_BF16 | MVS_CONV_IN_SPLIT | MVS_CONV_PER_LANE)))
+      (flags & ~(MVS_CONV_OUT_NCDHW | MVS_CONV_IN_C4 | MVS_CONV_IN_BF16 | MVS_CONV_IN_SPLIT | MVS_CONV_PER_LANE |
+                 MVS_CONV_S2_LDS)))
     return MVS_ERR_INVALID_ARGUMENT;
+  if ((flags & MVS_CONV_S2_LDS) && (flags & MVS_CONV_PER_LANE)) return MVS_ERR_INVALID_ARGUMENT;
   if ((flags & MVS_CONV_IN_BF16) && !(flags & MVS_CONV_IN_C4)) return MVS_ERR_INVALID_ARGUMENT;
   if ((flags & MVS_CONV_IN_SPLIT) && (!(flags & MVS_CONV_IN_C4) || (flags & MVS_CONV_IN_BF16) || !x_absmax ||
                                       ((uintptr_t)x_absmax & 3u)))
@@ -709,7 +711,8 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
                                            x, x2, weight, y, batch, c_in, c_out, dims, out_origin, out_size,
                                            in_origin, in_size, pad, bn_scale, bn_shift, bn_mean,
                                            (hipStream_t)stream, reinterpret_cast<const uint32_t*>(x_absmax),
-                                           reinterpret_cast<uint32_t*>(y_bound), (flags & MVS_CONV_PER_LANE) != 0);
+                                           reinterpret_cast<uint32_t*>(y_bound), (flags & MVS_CONV_PER_LANE) != 0,
+                                           nullptr, nullptr, (flags & MVS_CONV_S2_LDS) != 0);
   if (st != MVS_OK) return st;
   return lc.status();
 }

@@ -485,7 +485,7 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
                          float* y, int B, int CI, int CO, const int* n, const int* o0, const int* on, const int* i0,
                          const int* in, const int* pad, const float* bn_scale, const float* bn_shift,
                          const float* bn_mean, hipStream_t s, const uint32_t* absmax, uint32_t* y_bound,
-                         bool per_lane, const int* st0, const int* stn) {
+                         bool per_lane, const int* st0, const int* stn, bool s2_lds) {
   Geo g;
   g.y_bound = y_bound;
   g.out_cf = out_cf ? 1 : 0;
@@ -514,6 +514,23 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
     if (CI == 32) return launch_s1_lds<32>(x, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
     if (CI == 64) return launch_s1_lds<64>(x, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
   }
+  // conv_1_0 (S2 32 -> 16) from the whole fp32 volume: the LDS-staged kernel with MVS_S2_LDS=1 (opt-in,
+  // slower in the step: conv3d_s2_lds.hip)
+  if (mode == kS2 && CI == 32 && CO == 16 && (in_c4 == 0 || in_c4 == 1) && !x2 && !absmax && !y_bound &&
+      !per_lane && !st0 && !stn && !i0 && !in && !out_cf && pad && (s2_lds || conv_s2_lds_enabled()) &&
+      (uint64_t)n[0] * (uint64_t)n[1] * (uint64_t)n[2] * 128u < 0xFFFFFFF0ull) {   // (32-bit byte offsets)
+    launch_conv_s2_lds(x, in_c4, w, y, B, n, o0, on, pad, bn_scale, bn_shift, bn_mean, s);
+    return MVS_OK;
+  }
+  // S2 from the fp32 channel-quad volume: row blocks per wave MVS_S2_RB (2 or 4) -- A/B
+  static const int s2_rb = [] {
+    const char* e = getenv("MVS_S2_RB");
+    return e && e[0] == '4' ? 4 : 2;
+  }();
+  if (mode == kS2 && in_c4 == 1 && CI == 32 && s2_rb == 4) {
+    if (CO == 16) return launch_mode<kS2, 32, 16, 4, 1>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
+    if (CO == 32) return launch_mode<kS2, 32, 32, 4, 1>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
+  }
 // two row blocks per wave (one and four measured slower on the cfg-2 eval and train-mode steps)
 #define MVS_REGION_CASE(MD, A, C)                                                       \
   if (mode == MD && CI == A && CO == C) {                                               \
@@ -532,15 +549,6 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
   // deconv_2_0 (32 -> 16)
   MVS_REGION_S2(32, 16) MVS_REGION_S2(32, 32) MVS_REGION_S2(32, 64)
   MVS_REGION_CASE(kS1, 16, 16) MVS_REGION_CASE(kS1, 32, 32) MVS_REGION_CASE(kS1, 64, 64)
-  // S2 from the fp32 channel-quad volume: row blocks per wave MVS_S2_RB (2 or 4) -- A/B
-  static const int s2_rb = [] {
-    const char* e = getenv("MVS_S2_RB");
-    return e && e[0] == '4' ? 4 : 2;
-  }();
-  if (mode == kS2 && in_c4 == 1 && CI == 32 && s2_rb == 4) {
-    if (CO == 16) return launch_mode<kS2, 32, 16, 4, 1>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
-    if (CO == 32) return launch_mode<kS2, 32, 32, 4, 1>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
-  }
   // transposed: row blocks per wave MVS_T2_RB (2 or 4)
   static const int t2_rb = [] {
     const char* e = getenv("MVS_T2_RB");

@@ -85,6 +85,11 @@ void launch_soft_argmin(const float* prob, const float* d_batch, int B, int D, u
 // (optional epilogue: max((v - bn_mean) * bn_scale + bn_shift, 0), all three or none); in_c4: the
 // input is channel-quad in[B][Cin/4][D][H][W][4], fp32 (1) or bf16 (2)
 // wino_z (Cout = 8): Winograd F(2,3) along depth, weight = the transformed wu[Cin][3][3][4][8]
+// csrc/conv3d_s2_lds.hip: conv_1_0 (S2 32 -> 16) from the whole fp32 volume (channel quads or NCDHW), LDS-staged
+bool conv_s2_lds_enabled();
+void launch_conv_s2_lds(const float* x, int in_c4, const float* w27, float* y, int B, const int* n, const int* o0,
+                        const int* on, const int* pad, const float* bn_scale, const float* bn_shift,
+                        const float* bn_mean, hipStream_t s);
 // csrc/conv3d_wgrad.hip: narrow Conv3d weight gradient (dw [c_out][c_in][27]); part: the workspace
 size_t conv3d_wgrad_workspace_bytes(int B, int c_in, int D, int H, int W);
 bool conv3d_wgrad_supported(int c_in, int c_out);
@@ -143,7 +148,8 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
                          const int* in,
                          const int* pad, const float* bn_scale, const float* bn_shift, const float* bn_mean,
                          hipStream_t s, const uint32_t* absmax = nullptr, uint32_t* y_bound = nullptr,
-                         bool per_lane = false, const int* st0 = nullptr, const int* stn = nullptr);
+                         bool per_lane = false, const int* st0 = nullptr, const int* stn = nullptr,
+                         bool s2_lds = false);
 // conv_0_0 (+ BN_0 + ReLU, whole volume) and conv_1_0 (+ BN_1 + ReLU, on its region o0 / on, channels-last)
 // from the fp32 channel-quad cost volume, one fused kernel (conv3d_narrow.hip)
 void launch_conv_head_fp32(const float* cv4, int B, int D, int H, int W, const float* w0wz, const float* bn0_sc,

@@ -15,7 +15,7 @@ SOURCES = [os.path.join(CSRC, f) for f in ("capi.hip", "plane_sampling.hip", "co
                                            "conv3d_region.hip", "channel_ops.hip", "conv2d_narrow.hip",
                                            "conv3d_split.hip", "conv3d_s2_split.hip", "cv_head.hip",
                                            "conv3d_region_split.hip", "conv2d_split.hip",
-                                           "conv3d_wgrad.hip")]
+                                           "conv3d_wgrad.hip", "conv3d_s2_lds.hip")]
 HEADERS = [os.path.join(REPO_ROOT, "include", "mvs_cost_volume.h"),
            os.path.join(CSRC, "common.h"), os.path.join(CSRC, "launchers.h"),
            os.path.join(CSRC, "packed.h"), os.path.join(CSRC, "sampling_matrix.h"),

@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmvs_cost_volume.so"
 # MVS_LIB_PATH: load another build of the same ABI (A/B kernel experiments, tools/gpu_*_ab.sh)
 LIB_PATH = os.environ.get("MVS_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 MVS_OK = 0
 MVS_BWD_DETERMINISTIC = 1
@@ -26,6 +26,7 @@ MVS_LAYOUT_CHANNELS_LAST = 1
 MVS_CONV_S1, MVS_CONV_S2, MVS_CONV_T2 = 0, 1, 2
 MVS_CONV_OUT_NCDHW = 1
 MVS_CONV_PER_LANE = 32
+MVS_CONV_S2_LDS = 256
 MVS_CONV_SUM_INPUT = 64
 MVS_CONV_IN_BN = 128
 MVS_CONV_IN_C4 = 2

@@ -1187,7 +1187,8 @@ def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Ten
                   bn_scale: Optional[torch.Tensor] = None, bn_shift: Optional[torch.Tensor] = None,
                   bn_mean: Optional[torch.Tensor] = None, out_ncdhw: bool = False,
                   in_c4: bool = False, absmax: Optional[torch.Tensor] = None,
-                  y_bound: Optional[torch.Tensor] = None, per_lane: bool = False) -> torch.Tensor:
+                  y_bound: Optional[torch.Tensor] = None, per_lane: bool = False,
+                  s2_lds: bool = False) -> torch.Tensor:
     """Region convolution (mvs_conv3d_region_fwd): mode CONV_S2 reads the full NCDHW volume x
     (in_c4: the channel-quad [B, C/4, D, H, W, 4] of cost_volume_c4, or bf16 of cost_volume_c4_bf16;
     with in_origin / in_size, x holds only that box of the volume: the fused head's stored box),
@@ -1195,7 +1196,8 @@ def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Ten
     channels-last region tensor [B, *out_size, c_out] ([B, c_out, *out_size] with out_ncdhw), eval
     BN + ReLU fused when bn_* are given.  ``weight`` is region_weight(module).  ``y_bound``: zeroed
     bound words (int32 [MVS_BOUND_WORDS]) raised to max|y|.  ``per_lane``: the per-lane-operand kernel
-    even where an LDS-staged one applies (bit-identical; tests, A/B).  Inference only."""
+    even where an LDS-staged one applies (bit-identical; tests, A/B).  ``s2_lds``: conv_1_0's shape on the
+    LDS-staged stride-2 kernel (MVS_CONV_S2_LDS; opt-in).  Inference only."""
     _require_gpu(x, "x")
     lib = _lib.load()
     quad_bf16 = in_c4 and x.dtype == torch.bfloat16
@@ -1215,7 +1217,7 @@ def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Ten
     y = torch.empty(shape, device=x.device, dtype=_F32)
     flags = ((_lib.MVS_CONV_OUT_NCDHW if out_ncdhw else 0) | (_lib.MVS_CONV_IN_C4 if in_c4 else 0)
              | (_lib.MVS_CONV_IN_BF16 if quad_bf16 else 0) | (_lib.MVS_CONV_IN_SPLIT if quad_split else 0)
-             | (_lib.MVS_CONV_PER_LANE if per_lane else 0))
+             | (_lib.MVS_CONV_PER_LANE if per_lane else 0) | (_lib.MVS_CONV_S2_LDS if s2_lds else 0))
     st = lib.mvs_conv3d_region_fwd(int(mode), flags, _lib.ptr(x), None if x2 is None else _lib.ptr(x2), _lib.ptr(w),
                                    _lib.ptr(y), b, cin, cout, _ints3(dims), _ints3(out_origin), _ints3(out_size),
                                    None if in_origin is None else _ints3(in_origin),
@@ -1230,7 +1232,7 @@ def conv3d_region(x: torch.Tensor, x2: Optional[torch.Tensor], weight: torch.Ten
 
 @conv3d_region.register_fake
 def _(x, x2, weight, mode, dims, out_origin, out_size, in_origin, in_size, pad, bn_scale=None, bn_shift=None,
-      bn_mean=None, out_ncdhw=False, in_c4=False, absmax=None, y_bound=None, per_lane=False):
+      bn_mean=None, out_ncdhw=False, in_c4=False, absmax=None, y_bound=None, per_lane=False, s2_lds=False):
     _eager_only("conv3d_region", y_bound=y_bound)
     if out_ncdhw:
         return x.new_empty((x.shape[0], weight.shape[1]) + tuple(out_size), dtype=_F32)

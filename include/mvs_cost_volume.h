@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MVS_ABI_VERSION 23
+#define MVS_ABI_VERSION 24
 
 #define MVS_OK 0
 #define MVS_ERR_INVALID_ARGUMENT (-1)  /* null pointer, non-positive or unsupported size   */
@@ -517,6 +517,10 @@ int mvs_conv3d_region_fwd(int mode, int flags, const float* x, const float* x2, 
 /* flag of mvs_conv3d_region_split_fwd and mvs_conv3d_region_fwd: run the per-lane-operand kernel even
  * where an LDS-staged kernel applies (the two are bit-identical; tests and A/B timing) */
 #define MVS_CONV_PER_LANE 32
+/* flag of mvs_conv3d_region_fwd: conv_1_0's shape (MVS_CONV_S2, c_in 32, c_out 16, the whole fp32 volume,
+ * channel quads or NCDHW, channels-last output, no store box) on the LDS-staged kernel (csrc/conv3d_s2_lds.hip;
+ * the default only with the environment variable MVS_S2_LDS=1: slower inside the eval step) */
+#define MVS_CONV_S2_LDS 256
 
 /* Bound words of a region tensor: MVS_BOUND_WORDS uint32 (8 KiB) holding maxima of |v| as fp32 bit
  * patterns (the tensor's bound is their maximum), raised with atomic maxima by the kernel that writes

@@ -1011,6 +1011,55 @@ def test_fp32_head_matches_conv0_and_float64_conv1(shape, bn):
     assert bool(((y1 - y1r).abs().double().cpu() <= 2 * tol).all())
 
 
+@pytest.mark.parametrize("c4", [True, False])
+@pytest.mark.parametrize("bn", [False, True])
+@pytest.mark.parametrize("shape", [(2, 24, 20, 26), (1, 48, 32, 40), (1, 7, 37, 70), (2, 13, 9, 33)])
+def test_region_s2_lds_kernel_matches_per_lane_and_float64(shape, bn, c4):
+    """conv_1_0 (S2 32 -> 16) on halo(B) through the LDS-staged kernel (csrc/conv3d_s2_lds.hip, opt-in:
+    MVS_CONV_S2_LDS) against the per-lane region kernel (MVS_CONV_PER_LANE) and a float64
+    convolution: both within fp32 accumulation error (|err| <= 1e-5 sum|x||w| |scale| + the BN epilogue's
+    rounding), and repeatable launch to launch.  Odd extents, batch 2, channel-quad and NCDHW inputs."""
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _grow, _tconv_input_region
+    from mvs_amd.ops import CONV_S2, conv3d_region, region_weight
+    b, *n = shape
+    n = tuple(n)
+    pad, _ = pad_outpad(*n)
+    Bx = _tconv_input_region(tuple((0, d - 1) for d in n), n, pad)
+    h1 = _grow(Bx, n, 1)
+    o0, on = [lo for lo, _ in h1], [hi - lo + 1 for lo, hi in h1]
+    g = torch.Generator().manual_seed(sum(shape) + 3 * bn + c4)
+    x = torch.randn(b, 32, *n, generator=g)
+    conv = torch.nn.Conv3d(32, 16, 3, bias=False)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(16, 32, 3, 3, 3, generator=g) * 0.1)
+    p1 = _bn_params(16, g) if bn else None
+    p1d = [t.to(DEV) for t in p1] if bn else [None] * 3
+    xin = _to_c4(x.to(DEV)) if c4 else x.to(DEV)
+    w27 = region_weight(conv).detach().to(DEV)
+    args = (list(n), o0, on, None, None, list(pad), *p1d)
+    with torch.no_grad():
+        y = conv3d_region(xin, None, w27, CONV_S2, *args, in_c4=c4, s2_lds=True)
+        y2 = conv3d_region(xin, None, w27, CONV_S2, *args, in_c4=c4, s2_lds=True)
+        yp = conv3d_region(xin, None, w27, CONV_S2, *args, in_c4=c4, per_lane=True)
+    assert torch.equal(y, y2)
+    sl = tuple(slice(lo, lo + k) for lo, k in zip(o0, on))
+    ref = torch.nn.functional.conv3d(x.double(), conv.weight.detach().double(), stride=2, padding=pad)
+    aref = torch.nn.functional.conv3d(x.double().abs(), conv.weight.detach().double().abs(), stride=2, padding=pad)
+    ref, aref = ref[(slice(None),) * 2 + sl], aref[(slice(None),) * 2 + sl]
+    bnmag = 0.0
+    if bn:
+        sc, sh, mu = [t.double().view(1, -1, 1, 1, 1) for t in p1]
+        ref = torch.relu((ref - mu) * sc + sh)
+        aref = aref * sc.abs()
+        bnmag = ((mu * sc).abs() + sh.abs()).permute(0, 2, 3, 4, 1)
+    ref, aref = ref.permute(0, 2, 3, 4, 1), aref.permute(0, 2, 3, 4, 1)
+    tol = 1e-5 * aref + 1e-6 * bnmag + 1e-30
+    for name, got in (("lds", y), ("per-lane", yp)):
+        err = (got.double().cpu() - ref).abs()
+        assert bool((err <= tol).all()), "%s: max err %.3g" % (name, err.max().item())
+
+
 @pytest.mark.parametrize("cout", [16, 32, 64])
 def test_region_conv_s2_channel_quad_input_is_bit_equal(cout):
     """conv3d_region (CONV_S2) reading the channel-quad cost volume equals the NCDHW read bit for

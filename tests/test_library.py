@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from mvs_amd import _lib
     lib = _lib.load()
-    assert lib.mvs_abi_version() == _lib.ABI_VERSION == 23
+    assert lib.mvs_abi_version() == _lib.ABI_VERSION == 24
     assert lib.mvs_status_string(0) == b"ok"
     assert lib.mvs_status_string(-2).startswith(b"n_views")
     assert lib.mvs_sampling_workspace_bytes(12, 192) == 12 * 192 * 9 * 4
