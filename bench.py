@@ -522,6 +522,31 @@ def conv0_flops(B, D, h, w):
     return float(B) * D * h * w * 8 * 32 * 27 * 2
 
 
+def time_conv0_isolated(B, D, h, w, device, iters=10):
+    """conv_0_0's kernel alone (the fp32 eval step's roofline kernel: conv3d_k3, channel-quad input, depth
+    Winograd, BN_0 + ReLU), back-to-back launches on one stream, HIP events: ms per launch -- beside its
+    in-step duration, which the concurrent region chain stretches (they share the CUs)."""
+    from mvs_amd.ops import conv3d_k3
+    g = torch.Generator(device="cpu").manual_seed(11)
+    cv4 = torch.rand((B, 8, D, h, w, 4), generator=g).to(device)
+    wt = (torch.randn(8, 32, 3, 3, 3, generator=g) * 0.05).to(device)
+    bn = [torch.ones(8, device=device), torch.zeros(8, device=device), torch.zeros(8, device=device)]
+    with torch.no_grad():
+        for _ in range(2):
+            conv3d_k3(cv4, wt, *bn, in_c4=True, wino_z=True)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            conv3d_k3(cv4, wt, *bn, in_c4=True, wino_z=True)
+        e1.record()
+        torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    del cv4
+    torch.cuda.empty_cache()
+    return ms
+
+
 def conv0_traffic(tag, kind="conv0"):
     """PMC HBM bytes per fp32 conv_0_0 (kind "conv0") or fused fp32 head ("conv_head_fp32") launch
     (profiles/<kind>_traffic_<tag>.json, rocprofv3 --pmc), or None."""
@@ -758,6 +783,7 @@ def main():
     tag = "b%dv%dd%dh%dw%d" % (B, V, d_count, h, w)
     traffic = load_traffic(tag)
     conv0_ms = max_over_ranks(step_k["conv_0_0"], world, device) if "conv_0_0" in step_k else None
+    conv0_iso_ms = max_over_ranks(time_conv0_isolated(B, D, h, w, device), world, device) if conv0_ms else None
     head32_ms = max_over_ranks(step_k["conv_head"], world, device) if "conv_head" in step_k else None
     split = result.get("split_f16")
     head_ms = split["step_kernel_ms"].get("split_head") if split else None
@@ -854,7 +880,11 @@ def main():
                      "names the fp32 compute roof",
             "hbm": {"alg_bytes_per_launch": 4.0 * B * D * h * w * (32 + 8),
                     "GBps": 4.0 * B * D * h * w * 40 / (conv0_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                    "note": "the fp32 cost volume in once, y0 out once"}}
+                    "note": "the fp32 cost volume in once, y0 out once"},
+            "isolated_kernel_ms": conv0_iso_ms,
+            "isolated_frac": fl / (conv0_iso_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS,
+            "isolated_note": "the same kernel alone (back-to-back launches, bench.time_conv0_isolated): in the step it "
+                             "runs beside the region convolutions on a side stream and shares the CUs with them"}
     else:
         out["roofline"] = dict(out["warp_kernel"])
     if split is not None:
