@@ -92,12 +92,17 @@ class _Geom:
                 P[(pa, slice(None)) + sl[1]] = xc[(slice(None),) + sl[0]]
         return P.view(self.npar, -1, C)
 
-    def from_par(self, P, N):
+    def from_par(self, P, N, channels_first=False):
         """[npar, N * J^3, C] -> channels-last input-shaped [N, n..., C] (each input voxel lies in one
-        parity grid)."""
+        parity grid); ``channels_first``: written straight into a contiguous [N, C, n...] tensor instead
+        (returned as its channels-last view): the input gradient of an NCDHW input in its own layout, one
+        pass, no conversion later."""
         C = P.shape[-1]
         P = P.view((self.npar, N) + tuple(self.J) + (C,))
-        x = P.new_zeros((N,) + tuple(self.n) + (C,))
+        if channels_first:
+            x = P.new_zeros((N, C) + tuple(self.n)).permute(0, 2, 3, 4, 1)
+        else:
+            x = P.new_zeros((N,) + tuple(self.n) + (C,))
         for pa, a in self._parities():
             sl = self._par_slices(a)
             if sl is not None:
@@ -203,7 +208,9 @@ class _Conv3dTaps(torch.autograd.Function):
         G = g.to_grid(_cl(gy))
         if ctx.needs_input_grad[0]:
             gP = g.scatter(G, lambda t: w[(slice(None), slice(None)) + t], x.shape[1])
-            gx = _cf(g.from_par(gP, N))
+            # an NCDHW input (the cost volume) gets its gradient NCDHW: it meets the other readers'
+            # gradients (conv_0_0's) and the cost volume's backward in that layout
+            gx = _cf(g.from_par(gP, N, channels_first=x.is_contiguous()))
         if ctx.needs_input_grad[1]:
             P = getattr(ctx, "par", None)
             P = g.to_par(_cl(x)) if P is None else P
