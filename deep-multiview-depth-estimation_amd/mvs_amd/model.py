@@ -62,9 +62,15 @@ def _run_stack(seq, x, split_f16=False):
         # under autograd on a HIP device (train.py:97-104): the convolutions as per-tap rocBLAS GEMMs
         # (tap_gemm.conv2d), not MIOpen's (its first training step compiles its kernels: ~40 s at cfg 2)
         from . import tap_gemm
+        from .ops import conv2d_supported
+        hip_fwd = os.environ.get("MVS_TRAIN_CONV2D_FWD", "hip") == "hip"
         for layer in seq:
-            x = (tap_gemm.conv2d(x, layer.weight, layer.stride, layer.padding)
-                 if isinstance(layer, nn.Conv2d) and tap_gemm.conv2d_applies(layer) else layer(x))
+            if isinstance(layer, nn.Conv2d) and hip_fwd and conv2d_supported(layer) and x.dim() == 4:
+                x = tap_gemm.conv2d_hip_fwd(x, layer)   # the HIP forward kernel, per-tap-GEMM backward
+            elif isinstance(layer, nn.Conv2d) and tap_gemm.conv2d_applies(layer):
+                x = tap_gemm.conv2d(x, layer.weight, layer.stride, layer.padding)
+            else:
+                x = layer(x)
         return x
     if not _hip_inference(x):
         return seq(x)

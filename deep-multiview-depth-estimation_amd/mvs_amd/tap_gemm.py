@@ -288,12 +288,54 @@ def conv_transpose3d_box(x, weight, stride, crop_lo, out_size):
     return _ConvTranspose3dTaps.apply(x, weight, stride, crop_lo, 0, out_size)
 
 
+class _Conv2dHipTaps(torch.autograd.Function):
+    """Conv2d with the HIP forward (ops.conv2d: csrc/conv2d_narrow.hip, exact fp32) and the per-tap-GEMM
+    backward of the depth-1 conv3d (the parity grid of x formed in the backward)."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, padding):
+        from . import ops
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.padding = stride, padding
+        return ops.conv2d(x.contiguous(), w, stride[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        x3, w3 = x.unsqueeze(2), w.unsqueeze(2)
+        s, p, k = (1,) + tuple(ctx.stride), (0,) + tuple(ctx.padding), tuple(w3.shape[2:])
+        n = tuple(x3.shape[2:])
+        out_n = tuple((d + 2 * pp - kk) // ss + 1 for d, pp, kk, ss in zip(n, p, k, s))
+        g = _Geom(n, out_n, k, s, p)
+        N = x.shape[0]
+        G = g.to_grid(_cl(gy.unsqueeze(2)))
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gP = g.scatter(G, lambda t: w3[(slice(None), slice(None)) + t], x.shape[1])
+            gx = _cf(g.from_par(gP, N, channels_first=True)).squeeze(2)
+        if ctx.needs_input_grad[1]:
+            P = g.to_par(_cl(x3))
+            gw3 = torch.zeros_like(w3)
+
+            def put(t, v):
+                gw3[(slice(None), slice(None)) + t] = v
+            g.weight_grad(G, P, put)
+            gw = gw3.squeeze(2)
+        return gx, gw, None, None
+
+
 def conv2d(x, weight, stride=1, padding=0):
     """F.conv2d (groups 1, dilation 1, no bias) through the per-tap GEMMs: the conv3d of depth 1."""
     s, p = (stride, stride) if isinstance(stride, int) else tuple(stride), \
         (padding, padding) if isinstance(padding, int) else tuple(padding)
     y = _Conv3dTaps.apply(x.unsqueeze(2), weight.unsqueeze(2), (1,) + tuple(s), (0,) + tuple(p))
     return y.squeeze(2).contiguous()   # NCHW: the BatchNorm2d after it takes MIOpen's NCHW kernels
+
+
+def conv2d_hip_fwd(x, m):
+    """conv2d with the HIP forward kernel and the per-tap-GEMM backward, for a reference layer shape
+    (ops.conv2d_supported) on a HIP fp32 NCHW input."""
+    return _Conv2dHipTaps.apply(x, m.weight, tuple(m.stride), tuple(m.padding))
 
 
 def conv2d_applies(m):

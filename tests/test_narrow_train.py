@@ -59,3 +59,35 @@ def test_narrow_conv_autograd_at_cfg2_conv0_shape():
         ref = (gy[:, co].double() * xs.double()).sum().item()
         bound = (gy[:, co].double().abs() * xs.double().abs()).sum().item()
         assert abs(dw[co, ci, kz, ky, kx].item() - ref) <= 1e-5 * bound, (co, ci, t)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,k,s,hw", [(3, 8, 3, 1, (37, 53)), (8, 16, 5, 2, (40, 50)), (16, 32, 5, 2, (20, 26)),
+                                             (32, 32, 3, 1, (19, 23))])
+def test_encoder_conv2d_hip_forward_taps_backward(cin, cout, k, s, hw):
+    """The encoder's Conv2d under autograd (tap_gemm.conv2d_hip_fwd: the HIP forward kernel, per-tap-GEMM
+    backward) against float64 autograd: output and both gradients within 1e-5 of the absolute sums."""
+    from mvs_amd import tap_gemm
+    from mvs_amd.ops import conv2d_supported
+    g = torch.Generator().manual_seed(cin * 7 + k)
+    conv = torch.nn.Conv2d(cin, cout, k, stride=s, padding=k // 2, bias=False).to(DEV)
+    if not conv2d_supported(conv):
+        pytest.skip("not a reference layer shape")
+    x = torch.randn((2, cin) + hw, generator=g)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(cout, cin, k, k, generator=g) * 0.1)
+    xg = x.to(DEV).requires_grad_(True)
+    y = tap_gemm.conv2d_hip_fwd(xg, conv)
+    gy = torch.randn(y.shape, generator=g)
+    (y * gy.to(DEV)).sum().backward()
+    w = conv.weight.detach().cpu().double()
+    x64, w64 = x.double().requires_grad_(True), w.clone().requires_grad_(True)
+    (F.conv2d(x64, w64, stride=s, padding=k // 2) * gy.double()).sum().backward()
+    xa, wa = x.double().abs().requires_grad_(True), w.abs().requires_grad_(True)
+    ya = F.conv2d(xa, wa, stride=s, padding=k // 2)
+    (ya * gy.double().abs()).sum().backward()
+    y64 = F.conv2d(x.double(), w, stride=s, padding=k // 2)
+    for name, got, ref, bound in (("y", y.detach(), y64, ya.detach()), ("gx", xg.grad, x64.grad, xa.grad),
+                                  ("gw", conv.weight.grad, w64.grad, wa.grad)):
+        err = (got.double().cpu() - ref).abs()
+        assert bool((err <= 1e-5 * bound + 1e-30).all()), "%s: max err %.3g" % (name, err.max().item())
