@@ -554,7 +554,8 @@ class CostVolumeReg(nn.Module):
         convs_a = ((self.conv_1_0, self.BN_1), (self.conv_2_0, self.BN_2), (self.conv_3_0, self.BN_3))
         # the three stride-2 convs read the same volume over the same region R2: ONE convolution with their
         # output channels stacked (under autograd one input layout pass, one input gradient)
-        zs = _conv_s2_region(cv, torch.cat([c.weight for c, _ in convs_a], 0), R2, self.pad)   # 0 outside M
+        zs = _conv_s2_region(cv, torch.cat([c.weight for c, _ in convs_a], 0), R2, self.pad,
+                             splits=tuple(c.weight.shape[0] for c, _ in convs_a))   # 0 outside M
         zs = zs.split([c.weight.shape[0] for c, _ in convs_a], 1)
         for z, (conv_a, bn) in zip(zs, convs_a):
             p = _bn_train(bn, *_sums(z), count)
@@ -569,9 +570,9 @@ class CostVolumeReg(nn.Module):
             lv.append(_crop_pad(act(z, p), R1, M, n))
         y1, y2, y3 = lv
         # (the full outputs for the statistics; BN + ReLU on M only, the next layer's input)
-        z = _tconv_region(y3, M, self.deconv_3_0.weight, full, self.pad)
+        z = _tconv_region(y3, M, self.deconv_3_0.weight, full, self.pad, n)
         y3 = act(_crop_pad(z, full, M, n), _bn_train(self.BN_2, *_sums(z), count))
-        z = _tconv_region(y3 + y2, M, self.deconv_2_0.weight, full, self.pad)
+        z = _tconv_region(y3 + y2, M, self.deconv_2_0.weight, full, self.pad, n)
         y2 = act(_crop_pad(z, full, M, n), _bn_train(self.BN_1, *_sums(z), count))
         z = _tconv_region(y2 + y1, M, self.deconv_1_0.weight, full, self.pad)
         z = act(z, _bn_train(self.BN_0, *_sums(z), count)) + y0
@@ -1063,7 +1064,7 @@ def _region_conv3d(x, weight, stride, padding):
     return F.conv3d(x, weight, stride=stride, padding=padding)
 
 
-def _conv_s2_region(x, weight, out_reg, pad):
+def _conv_s2_region(x, weight, out_reg, pad, splits=None):
     """conv3d(x, weight, stride 2, padding pad) on the output box out_reg (x: full volume).
 
     Output j reads inputs 2j - P .. 2j - P + 2.  The input box of out_reg usually leaves the volume
@@ -1083,8 +1084,13 @@ def _conv_s2_region(x, weight, out_reg, pad):
             assert ca <= cb, "output box reads no input"
             sl.append(slice(ca, cb + 1))
             pl.append(ca - a)
-        if any(s_.start != 0 or s_.stop != d for s_, d in zip(sl, n)):   # (a whole-extent slice: no copy
-            x = x[:, :, sl[0], sl[1], sl[2]]                             # back in the backward)
+        whole = all(s_.start == 0 and s_.stop == d for s_, d in zip(sl, n))
+        from . import region_train
+        if (whole and splits is not None and region_train.enabled(x, "s2") and x.shape[1] == 32
+                and tuple(splits) in (region_train.S2_SPLITS, (16,), (32,), (64,))):
+            return region_train.s2_box(x, weight, out_reg, pad, tuple(pl), tuple(splits))   # HIP forward
+        if not whole:   # (a whole-extent slice: no copy back in the backward)
+            x = x[:, :, sl[0], sl[1], sl[2]]
         return tap_gemm.conv3d_box(x, weight, 2, tuple(pl), tuple(hi - lo + 1 for lo, hi in out_reg))
     sl, pads, offs = [], [], []
     for (lo, hi), p, d in zip(out_reg, pad, n):
@@ -1106,10 +1112,15 @@ def _conv_s2_region(x, weight, out_reg, pad):
 def _conv_s1_region(x, x_reg, weight, out_reg, n):
     """conv3d(., weight, stride 1, padding 1) on out_reg, from the region tensor x on x_reg."""
     want = tuple((lo - 1, hi + 1) for lo, hi in out_reg)
-    return _region_conv3d(_crop_pad(x, x_reg, want, n), weight, 1, 0)
+    xin = _crop_pad(x, x_reg, want, n)
+    from . import region_train
+    if (_taps(x) and region_train.enabled(x, "s1") and weight.shape[0] == weight.shape[1]
+            and weight.shape[0] in region_train.S1_CHANNELS):
+        return region_train.s1_valid(xin, weight)   # HIP forward, per-tap-GEMM backward
+    return _region_conv3d(xin, weight, 1, 0)
 
 
-def _tconv_region(x, x_reg, weight, out_reg, pad):
+def _tconv_region(x, x_reg, weight, out_reg, pad, dims=None):
     """conv_transpose3d(., weight, stride 2, padding pad) on out_reg, from the region tensor x on
     x_reg (which must hold every input that reaches out_reg: _tconv_input_region)."""
     if _taps(x):
@@ -1119,6 +1130,10 @@ def _tconv_region(x, x_reg, weight, out_reg, pad):
         for (xlo, _), (lo, hi), p in zip(x_reg, out_reg, pad):
             assert lo - (2 * xlo - p) >= 0, "transposed-conv input region starts after the output box"
             crop.append(lo - (2 * xlo - p))
+        from . import region_train
+        if (dims is not None and region_train.enabled(x, "t2")
+                and (weight.shape[0], weight.shape[1]) in region_train.T2_SHAPES):
+            return region_train.t2_box(x, weight, x_reg, out_reg, pad, dims, tuple(crop))   # HIP forward
         return tap_gemm.conv_transpose3d_box(x, weight, 2, tuple(crop), tuple(hi - lo + 1 for lo, hi in out_reg))
     y = F.conv_transpose3d(x, weight, stride=2)   # output q <-> volume index 2 * xlo + q - P
     sl, pads = [], []

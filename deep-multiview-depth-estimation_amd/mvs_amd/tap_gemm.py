@@ -265,6 +265,54 @@ class _ConvTranspose3dTaps(torch.autograd.Function):
         return gx, gw, None, None, None, None
 
 
+def conv3d_backward(x, w, stride, padding, out_size, gy, need_x=True, need_w=True):
+    """(gx, gw) of conv3d_box / conv3d (output u reads inputs u * stride - padding + t, out_size outputs)
+    from its input x and output gradient gy: the per-tap-GEMM backward of _Conv3dTaps, for a forward
+    computed elsewhere (the HIP region kernels)."""
+    s, p, k = _t3(stride), _t3(padding), tuple(w.shape[2:])
+    g = _Geom(tuple(x.shape[2:]), tuple(out_size), k, s, p)
+    N = x.shape[0]
+    if g.empty:
+        return (torch.zeros_like(x) if need_x else None), (torch.zeros_like(w) if need_w else None)
+    G = g.to_grid(_cl(gy))
+    gx = gw = None
+    if need_x:
+        gP = g.scatter(G, lambda t: w[(slice(None), slice(None)) + t], x.shape[1])
+        gx = _cf(g.from_par(gP, N, channels_first=x.is_contiguous()))
+    if need_w:
+        P = g.to_par(_cl(x))
+        gw = torch.zeros_like(w)
+
+        def put(t, v):
+            gw[(slice(None), slice(None)) + t] = v
+        g.weight_grad(G, P, put)
+    return gx, gw
+
+
+def conv_transpose3d_backward(x, w, stride, crop_lo, out_size, gy, need_x=True, need_w=True):
+    """(gx, gw) of conv_transpose3d_box (outputs [crop_lo, crop_lo + out_size) of the unpadded transposed
+    conv) from its input x and output gradient gy: _ConvTranspose3dTaps's backward for a forward computed
+    elsewhere."""
+    s, p, k = _t3(stride), _t3(crop_lo), tuple(w.shape[2:])
+    g = _Geom(tuple(out_size), tuple(x.shape[2:]), k, s, p)
+    N = x.shape[0]
+    if g.empty:
+        return (torch.zeros_like(x) if need_x else None), (torch.zeros_like(w) if need_w else None)
+    P = g.to_par(_cl(gy))
+    gx = gw = None
+    if need_x:
+        Y = g.forward(P, lambda t: w[(slice(None), slice(None)) + t].t())
+        gx = _cf(g.from_grid(Y, N))
+    if need_w:
+        G = g.to_grid(_cl(x))
+        gw = torch.zeros_like(w)
+
+        def put(t, v):
+            gw[(slice(None), slice(None)) + t] = v
+        g.weight_grad(G, P, put)
+    return gx, gw
+
+
 def conv3d(x, weight, stride=1, padding=0):
     """F.conv3d (groups 1, dilation 1, no bias) through per-tap GEMMs, differentiable."""
     return _Conv3dTaps.apply(x, weight, stride, padding)

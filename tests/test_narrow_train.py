@@ -91,3 +91,58 @@ def test_encoder_conv2d_hip_forward_taps_backward(cin, cout, k, s, hw):
                                   ("gw", conv.weight.grad, w64.grad, wa.grad)):
         err = (got.double().cpu() - ref).abs()
         assert bool((err <= 1e-5 * bound + 1e-30).all()), "%s: max err %.3g" % (name, err.max().item())
+
+
+@pytest.mark.gpu
+def test_region_convs_hip_forward_match_tap_gemms():
+    """mvs_amd/region_train.py (training's region convolutions: HIP region-kernel forward, per-tap-GEMM
+    backward) against tap_gemm's box convolutions on the same inputs at the live geometry of a
+    (24, 20, 26) volume: outputs within fp32 accumulation error, input and weight gradients bit-equal
+    (the same backward on the same saved operands)."""
+    from mvs_amd import region_train, tap_gemm
+    from mvs_amd.config import pad_outpad
+    from mvs_amd.model import _crop_pad, _grow, _tconv_input_region
+    n = (24, 20, 26)
+    pad, _ = pad_outpad(*n)
+    full = tuple((0, d - 1) for d in n)
+    M = _tconv_input_region(full, n, pad)
+    R1, R2 = _grow(M, n, 1), _grow(M, n, 2)
+    g = torch.Generator().manual_seed(5)
+
+    def check(fn_hip, fn_taps, inputs):
+        outs, grads = [], []
+        gy = None
+        for fn in (fn_hip, fn_taps):
+            xs = [t.detach().clone().to(DEV).requires_grad_(True) for t in inputs]
+            y = fn(*xs)
+            if gy is None:
+                gy = torch.randn(y.shape, generator=g).to(DEV)
+            (y * gy).sum().backward()
+            outs.append(y.detach())
+            grads.append([t.grad for t in xs])
+        scale = outs[1].abs().max().item() + 1e-30
+        assert (outs[0] - outs[1]).abs().max().item() <= 1e-5 * scale
+        for a, b in zip(*grads):
+            assert torch.equal(a, b)
+
+    # stride-2 stacked conv_k_0 over R2 from the whole volume
+    x = torch.randn(2, 32, *n, generator=g)
+    w = torch.randn(112, 32, 3, 3, 3, generator=g) * 0.05
+    pl, size = [], []
+    for (lo, hi), p in zip(R2, pad):
+        pl.append(max(2 * lo - p, 0) - (2 * lo - p))
+        size.append(hi - lo + 1)
+    check(lambda a, b: region_train.s2_box(a, b, R2, pad, tuple(pl), region_train.S2_SPLITS),
+          lambda a, b: tap_gemm.conv3d_box(a, b, 2, tuple(pl), tuple(size)), [x, w])
+    # stride-1 on a padded crop
+    for c in (16, 32, 64):
+        xin = torch.randn(2, c, *[hi - lo + 3 for lo, hi in R1], generator=g)
+        w1 = torch.randn(c, c, 3, 3, 3, generator=g) * 0.05
+        check(region_train.s1_valid, lambda a, b: tap_gemm.conv3d(a, b, 1, 0), [xin, w1])
+    # transposed, M -> the full box
+    for ci, co in region_train.T2_SHAPES:
+        xm = torch.randn(2, ci, *[hi - lo + 1 for lo, hi in M], generator=g)
+        wt = torch.randn(ci, co, 3, 3, 3, generator=g) * 0.05
+        crop = tuple(lo - (2 * xlo - p) for (xlo, _), (lo, _), p in zip(M, full, pad))
+        check(lambda a, b: region_train.t2_box(a, b, M, full, pad, n, crop),
+              lambda a, b: tap_gemm.conv_transpose3d_box(a, b, 2, crop, n), [xm, wt])
