@@ -478,7 +478,9 @@ def train_step_bench(B, V, D, H, W, device, steps):
                    "on its live regions under autograd (CostVolumeReg.live_autograd_ok: the same function as the "
                    "full-volume op sequence, float64 gradients equal, tests/test_regulariser_live.py): conv_0_0 "
                    "/ conv_out forward, input and weight gradients on HIP kernels (mvs_amd/narrow_train.py, "
-                   "csrc/conv3d_wgrad.hip), the region convolutions as per-tap rocBLAS GEMMs on dense boxes "
+                   "csrc/conv3d_wgrad.hip); the stride-1 and transposed region convolutions' forward and the "
+                   "encoder convs' forward on the HIP kernels (mvs_amd/region_train.py, tap_gemm.conv2d_hip_fwd), "
+                   "their backward and the stride-2 convs as per-tap rocBLAS GEMMs on dense boxes "
                    "(mvs_amd/tap_gemm.py; the three stride-2 convs as one); cost volume backward on "
                    "mvs::cost_volume_backward"}
     del net, opt

@@ -549,15 +549,17 @@ int launch_conv3d_region(int mode, bool out_cf, int in_c4, const float* x, const
   // deconv_2_0 (32 -> 16)
   MVS_REGION_S2(32, 16) MVS_REGION_S2(32, 32) MVS_REGION_S2(32, 64)
   MVS_REGION_CASE(kS1, 16, 16) MVS_REGION_CASE(kS1, 32, 32) MVS_REGION_CASE(kS1, 64, 64)
-  // transposed: row blocks per wave MVS_T2_RB (2 or 4)
+  // transposed: four row blocks per wave for deconv_2_0 (32 -> 16: 0.323 -> 0.302 ms at cfg 2), two for
+  // deconv_3_0 (64 -> 32: equal); MVS_T2_RB=2 / =4 forces one for both (A/B).  Per-output accumulation
+  // order does not depend on the row blocks: bit-equal either way
   static const int t2_rb = [] {
     const char* e = getenv("MVS_T2_RB");
-    return e && e[0] == '4' ? 4 : 2;
+    return e && e[0] == '4' ? 4 : e && e[0] == '2' ? 2 : 0;
   }();
-  if (mode == kT2 && t2_rb == 4) {
-    if (CI == 64 && CO == 32) return launch_mode<kT2, 64, 32, 4>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
-    if (CI == 32 && CO == 16) return launch_mode<kT2, 32, 16, 4>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
-  }
+  if (mode == kT2 && CI == 64 && CO == 32 && t2_rb == 4)
+    return launch_mode<kT2, 64, 32, 4>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
+  if (mode == kT2 && CI == 32 && CO == 16 && t2_rb != 2)
+    return launch_mode<kT2, 32, 16, 4>(x, x2, w, y, bn_scale, bn_shift, bn_mean, B, g, s), MVS_OK;
   MVS_REGION_CASE(kT2, 64, 32) MVS_REGION_CASE(kT2, 32, 16)
 #undef MVS_REGION_CASE
 #undef MVS_REGION_S2
