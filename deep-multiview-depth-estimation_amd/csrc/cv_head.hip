@@ -449,6 +449,11 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
     lds_drain();
 #pragma unroll
     for (int u = 0; u < kAhead; ++u) issue(u);
+#ifdef MVS_HEAD_RDC_FIRST
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     rdc(kAhead);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -475,8 +480,14 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       split4(acc, ex, hi, lo);
       if (!valid) hi = lo = make_uint2(0u, 0u);
       lds_drain();
+#ifdef MVS_HEAD_RDC_FIRST   // experiment: item u + kAhead + 1's sampling-state read before (not under) u + kAhead's gathers
+      if (has(u + kAhead + 1)) rdc(u + kAhead + 1);
+      lds_drain();
+      if (has(u + kAhead)) issue(u + kAhead);
+#else
       if (has(u + kAhead)) issue(u + kAhead);
       if (has(u + kAhead + 1)) rdc(u + kAhead + 1);
+#endif
       char* dst = ring + (sl0 + pl) * kSlotB + (m & 0x1FFFu);
       // THE HAZARD: the item's two ds_write_b64 ring stores must not run while
       // any of this wave's tap gathers (buffer_load_dwordx4) is still in flight, and must complete before
