@@ -89,7 +89,11 @@ constexpr int kPD = MVS_HEAD_PD;                         // PRESPLIT: batches of
 constexpr bool kPreVoxelFast = MVS_HEAD_VFAST;
 // the sampling state of a batch is formed by the CONSUMER waves after their matrix work (they wait at
 // the step barrier otherwise; the producers' gathers are the step's critical path: cfg 2 2.28 -> 2.19 ms)
+#ifdef MVS_HEAD_COORDS_BY_PRODUCERS   // experiment (DESIGN.md §3.7 residual): the producers form their own sampling state
+constexpr bool kCoordsByConsumers = false;
+#else
 constexpr bool kCoordsByConsumers = true;
+#endif
 
 template <int NS, bool PRE = false>
 constexpr int coord_bytes() {   // [2 buffers][2 planes][NS views][108 voxels] x {off, wx, wy, -}
@@ -498,6 +502,9 @@ __global__ __launch_bounds__(kThreads) void cv_head_kernel(HeadArgs a) {
       __builtin_amdgcn_sched_barrier(0);
 #ifndef MVS_HEAD_NO_STORE_FENCE   // (mutation build of tests/test_head_isa.py only: the rule's checker must fail)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+#ifdef MVS_HEAD_STORE_NOP   // experiment (DESIGN.md §3.7 residual): wait states between the item's VALU and its ring stores
+      asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
 #endif
       __builtin_amdgcn_sched_barrier(0);
       *reinterpret_cast<uint2*>(dst) = hi;

@@ -2,6 +2,7 @@
 import os
 import shutil
 import subprocess
+import tempfile
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
@@ -20,6 +21,13 @@ HEADERS = [os.path.join(REPO_ROOT, "include", "mvs_cost_volume.h"),
            os.path.join(CSRC, "common.h"), os.path.join(CSRC, "launchers.h"),
            os.path.join(CSRC, "packed.h"), os.path.join(CSRC, "sampling_matrix.h"),
            os.path.join(CSRC, "split.h")]
+# per-source device flags, compiled as a separate object: the fused head (cv_head.hip) without packed
+# fp32 VALU instructions -- with v_pk_{fma,add,mul}_f32 in its gather / variance code, the .z / .w halves of
+# a producer item's variance came out wrong in a schedule-dependent share of launches (0 to 100 % of
+# them across builds that only reorder the producer's instructions); the same builds without packed fp32:
+# 0.  Elementwise identical arithmetic (a packed FMA is two fmaf): the outputs keep
+# their bits.
+SOURCE_FLAGS = {"cv_head.hip": ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]}
 OUTPUT = os.path.join(_HERE, "libmvs_cost_volume.so")
 ARCH = os.environ.get("MVS_OFFLOAD_ARCH", "gfx950")
 
@@ -38,10 +46,24 @@ def build_library(force=False, verbose=False, extra_flags=(), output=None):
         newest = max(os.path.getmtime(p) for p in SOURCES + HEADERS)
         if os.path.getmtime(out) >= newest:
             return out
-    cmd = [hipcc(), "-O3", "-std=c++17", "-Wno-pass-failed", "--offload-arch=%s" % ARCH, "-fPIC", "-shared",
-           "-parallel-jobs=%d" % min(8, os.cpu_count() or 1), "-o", out + ".tmp"] + list(extra_flags) + SOURCES
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd)
+    base = [hipcc(), "-O3", "-std=c++17", "-Wno-pass-failed", "--offload-arch=%s" % ARCH, "-fPIC"]
+    objs, srcs = [], []
+    with tempfile.TemporaryDirectory(prefix="mvs_build_") as tmp:
+        for src in SOURCES:
+            flags = SOURCE_FLAGS.get(os.path.basename(src))
+            if flags is None:
+                srcs.append(src)
+                continue
+            obj = os.path.join(tmp, os.path.basename(src) + ".o")
+            cmd = base + ["-c", "-o", obj] + list(extra_flags) + flags + [src]
+            if verbose:
+                print(" ".join(cmd))
+            subprocess.check_call(cmd)
+            objs.append(obj)
+        cmd = base + ["-shared", "-parallel-jobs=%d" % min(8, os.cpu_count() or 1), "-o", out + ".tmp"] + \
+            list(extra_flags) + srcs + ["-Wl,%s" % o for o in objs]   # (a bare .o would be read as HIP source)
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
     os.replace(out + ".tmp", out)
     return out

@@ -195,3 +195,16 @@ def test_store_checker_flags_a_build_without_the_fence(tmp_path):
     work.mkdir()
     stores, bad = _check_stores(_disassemble(work, "cv_head_kernelILi3", str(mut)))
     assert stores > 0 and bad, "the mutant (no fence before the ring stores) passed the check"
+
+
+@pytest.mark.parametrize("V", [2, 3])
+def test_fused_head_has_no_packed_fp32(tmp_path, V):
+    """Rule 3 (round 6): the fused head ships without packed fp32 VALU instructions
+    (csrc/cv_head.hip built with the packed-fp32-ops target feature off, mvs_amd/_build.py SOURCE_FLAGS).
+    With them, the .z / .w halves of a producer item's variance came out wrong in 0-100 % of launches
+    depending on the build's instruction schedule; without them, 0 -- and the scan is not vacuous: the
+    kernel still holds its item loop's gathers."""
+    asm = _disassemble(tmp_path, "cv_head_kernelILi%dELb0E" % V, LIB)
+    packed = [t for k, t in _instructions(asm) if k == "insn" and re.match(r"v_pk_(fma|add|mul)_f32\b", t)]
+    assert not packed, packed[:4]
+    assert sum(1 for k, t in _instructions(asm) if k == "insn" and t.startswith("buffer_load_dwordx4")) >= 4 * (V - 1) * 6
