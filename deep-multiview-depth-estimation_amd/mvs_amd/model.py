@@ -244,17 +244,11 @@ class CostVolumeReg(nn.Module):
     def head_ok(self, dcv):
         """The fused head kernel applies to this deferred cost volume: eval-mode live regions with the
         split-fp16 convolutions, fp32 HIP inference, C = 32, 2-3 views, D even and every stride-2
-        padding odd (the kernel's window ownership), MVS_CV_HEAD=1 (opt-in, experimental: a residual
-        intermittent ring corruption in ~1-4 % of launches, DESIGN.md §3.7 -- warned once when taken)."""
+        padding odd (the kernel's window ownership), MVS_CV_HEAD=1 (opt-in)."""
         n = tuple(dcv.shape[2:])
-        ok = (os.environ.get("MVS_CV_HEAD", "0") == "1" and self.split_f16 and self.live_ok(n)
-              and _hip_inference(dcv.feature_maps) and dcv.shape[1] == 32 and dcv.n_views in (2, 3)
-              and n[0] % 2 == 0 and all(p % 2 == 1 for p in self.pad))
-        if ok:
-            warnings.warn("MVS_CV_HEAD=1: the fused head is experimental -- a residual intermittent ring "
-                          "corruption changes a few voxels in ~1-4 % of launches (DESIGN.md §3.7)",
-                          RuntimeWarning, stacklevel=2)
-        return ok
+        return (os.environ.get("MVS_CV_HEAD", "0") == "1" and self.split_f16 and self.live_ok(n)
+                and _hip_inference(dcv.feature_maps) and dcv.shape[1] == 32 and dcv.n_views in (2, 3)
+                and n[0] % 2 == 0 and all(p % 2 == 1 for p in self.pad))
 
     def forward_live_head(self, dcv):
         """forward_live with the cost volume consumed where it is formed: one fused

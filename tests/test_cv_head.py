@@ -3,14 +3,13 @@
 Two modes of one kernel, both in the opt-in split-fp16 arithmetic (MVSConfig(arithmetic="split_f16")).
 The split head (ops.split_head, PRESPLIT) reads the materialised split volume and runs conv_0_0 and
 conv_1_0 in one pass over it.  The fused head (MVS_CV_HEAD=1, ops.cost_volume_head) forms the variance on
-chip as well, so the volume is never written.  Its gathering producers still corrupt the ring data of a
-few voxels in a small share of launches: round 6 fenced the ring stores against the wave's in-flight tap
-gathers (tests/test_head_isa.py rule 2), which cut the rate from most launches to ~1-4 % at the bench
-geometry (6 of 150 launches, V = 3; tools/dbg/head_stress.py), but did not remove it, and removing every
-LDS / gather overlap of the producer waves (-DMVS_HEAD_RDC_FIRST) still left 3 + 5 of 500 (DESIGN.md
-§3.7).  The fused head is therefore opt-in only (MVS_CV_HEAD=1, off every default and bench path) and
-its bit-equality tests are non-strict xfails that record the hazard; the split head (PRESPLIT, the
-split-fp16 path's default) is strict and repeatable below.
+chip as well, so the volume is never written.  Its gathering producers corrupted the .z / .w halves of
+a few items' variance in a schedule-dependent share of launches (rounds 4-6; up to every launch in some
+builds): the instructions involved are the packed fp32 VALU ops of the gather / variance code, and the
+head now ships without them (csrc/cv_head.hip built with the packed-fp32-ops feature off,
+tests/test_head_isa.py rule 3) -- 0 of 900 launches differ at the bench geometry and a small one, and a
+build that failed every launch fails none without packed fp32.  Its bit-equality tests
+below are strict again, with a 20-launch repeatability test at the bench geometry.
 
 The fused head forms the variance of homography_warping + assemble_cost_volume (homography.py:6-92,
 costvolume.py:3-16) on chip and applies conv_0_0 + BN_0 + ReLU (model.py:101) and conv_1_0 + BN_1 +
@@ -28,11 +27,6 @@ import pytest
 import torch
 
 DEV = torch.device("cuda", 0)
-# the fused head's residual ring corruption (module docstring): its tests pass in most
-# runs and are kept as non-strict xfails, so a run that hits the hazard is recorded, not hidden
-FUSED_HAZARD = pytest.mark.xfail(strict=False, reason="fused head (opt-in MVS_CV_HEAD=1): residual "
-                                 "intermittent ring corruption, ~1-4 % of launches at the bench geometry "
-                                 "(DESIGN.md §3.7)")
 
 
 def _regions(n, pad):
@@ -87,7 +81,6 @@ def test_partial_cost_volume_refuses_whole_volume_views():
         BoundCostVolume(q, torch.zeros(8, dtype=torch.int32), [0, 0, 0], None)
 
 
-@FUSED_HAZARD
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,V,D,h,w", [(2, 3, 16, 32, 48), (1, 2, 20, 24, 40), (1, 3, 100, 36, 44),
                                        (2, 3, 48, 28, 64), (1, 2, 20, 25, 32), (1, 3, 16, 29, 41)])
@@ -137,7 +130,6 @@ def test_head_is_bit_equal_to_the_split_path(B, V, D, h, w):
         assert torch.equal(y1n, ops.conv_s2_split(scv, absmax, w1, list(n), org, size, pad))
 
 
-@FUSED_HAZARD
 @pytest.mark.gpu
 def test_mvsnet_head_equals_split_volume_path():
     """MVSNet.forward with the opt-in fused head (MVS_CV_HEAD=1) gives the same depth maps, bit for
@@ -246,7 +238,6 @@ def test_split_head_is_bit_equal_and_repeatable(B, D, h, w):
                               (y1 - y1_ref).abs().max().item())
 
 
-@FUSED_HAZARD
 @pytest.mark.gpu
 @pytest.mark.parametrize("V", [2, 3])
 def test_fused_head_repeatable_at_the_bench_geometry(V):
